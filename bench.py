@@ -1,0 +1,149 @@
+#!/usr/bin/env python3
+"""Headline benchmark: PFML hyper-parameter grid search (BASELINE.json metric).
+
+One *step* is the full grid search of the reference's S5 + S6 stages on the S&P 500
+production shapes:
+
+* 2 g x 4 p (64, 128, 256, 512 RFFs) x 101 lambda ridge solves for each of 53 expanding
+  hp-year windows = 42,824 "hp x window solves" (PFML_Search_Coef.py:102-137), computed from
+  the per-month summands r_tilde_t (513) and denom_t (513 x 513) of ~710 PFML months,
+  INCLUDING the expanding window sums (the reference's 0.50 s per (g, year) baseline includes
+  its running sums);
+* the out-of-sample utilities of every (g, year, p, lambda) on its 12 validation months =
+  513,888 quadratic forms (PFML_hp_reals.py:73-102);
+* the expanding-mean cum_obj and the dense rank per month (PFML_hp_reals.py:104-125).
+
+Multi-GPU: hp years are sharded over ranks (strong scaling of the fixed reference grid),
+window-sum shard totals are exchanged with one all-gather, utilities all-gathered at the
+end; the time reported is the max over ranks.
+
+Data: synthetic per-month summands of the production shape (no WRDS/JKP data exists here);
+random SPD denom_t = X_t'X_t / N with X_t ~ N(0,1) of shape 500 x 513 (S&P 500 universe).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+import pfml  # noqa: E402
+from pfml.config import Config  # noqa: E402
+from pfml.models.search import PfmlReals, grid_search, validation_scores  # noqa: E402
+from pfml.ops.gemm import gemm  # noqa: E402
+from pfml.parallel import collectives as coll  # noqa: E402
+from pfml.parallel import dist as pdist  # noqa: E402
+from pfml.utils.dates import mi_from_ym  # noqa: E402
+
+BASELINE_SOLVES_PER_S = 808.0     # reference ridge grid, 8-core Xeon
+METRIC = "PFML hp×window solves/sec (whole node); full grid-search wall-clock, S&P500"
+
+
+def synthetic_reals(cfg: Config, device, n_months: int = 710, n_stocks: int = 500,
+                    seed: int = 0) -> PfmlReals:
+    G = len(cfg.g_vec)
+    P = cfg.p_max + 1
+    last = mi_from_ym(int(cfg.hp_years.max()), 11)
+    months = np.arange(last - n_months + 1, last + 1, dtype=np.int64)
+    denom = torch.empty((G, n_months, P, P), dtype=torch.float64, device=device)
+    r = torch.empty((G, n_months, P), dtype=torch.float64, device=device)
+    gen = torch.Generator(device=device)
+    chunk = 32
+    for g in range(G):
+        gen.manual_seed(seed * 1000 + g)
+        for a in range(0, n_months, chunk):
+            b = min(n_months, a + chunk)
+            X = torch.randn((b - a, n_stocks, P), generator=gen, dtype=torch.float64, device=device)
+            gemm(X, X, trans_a=True, alpha=1.0 / n_stocks, out=denom[g, a:b])
+            del X
+        r[g] = 0.05 * torch.randn((n_months, P), generator=gen, dtype=torch.float64, device=device)
+    return PfmlReals(months=months, r_tilde=r, denom=denom)
+
+
+def one_step(reals: PfmlReals, cfg: Config):
+    res = grid_search(reals, cfg)
+    G = res.obj.shape[1]
+    out = []
+    for g in range(G):
+        out.append(validation_scores(res.obj, g, cfg.run.compat_mode))
+    return res, out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--months", type=int, default=710)
+    ap.add_argument("--device", default="auto")
+    ap.add_argument("--profile", action="store_true")
+    args = ap.parse_args()
+
+    env = pdist.init(args.device)
+    dev = env.device
+    cfg = Config.default()
+    n_solves = (len(cfg.g_vec) * len(cfg.hp_years) * len(cfg.p_vec) * len(cfg.l_vec))
+    n_util = n_solves * 12
+
+    t_setup = time.perf_counter()
+    reals = synthetic_reals(cfg, dev, n_months=args.months)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t_setup = time.perf_counter() - t_setup
+
+    for _ in range(args.warmup):
+        one_step(reals, cfg)
+    pdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res, scores = one_step(reals, cfg)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    pdist.barrier()
+    dt = time.perf_counter() - t0
+    dt = coll.all_reduce_max(dt, device=dev)
+    ms = 1000.0 * dt / max(1, args.steps)
+    value = n_solves / (ms / 1000.0)
+    # sanity: finite outputs
+    finite = bool(torch.isfinite(res.obj).all().item())
+    if env.is_main:
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "solves/s",
+            "n_gpus": env.world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(value / BASELINE_SOLVES_PER_S, 2),
+            "dtype": "fp64",
+            "data": "synthetic (per-month PFML summands of production shape: 710 months, "
+                    "P=513, denom_t = X'X/500 with X~N(0,1); no WRDS/JKP data available)",
+            "config": {
+                "model": "PFML grid search S5+S6: 2 g x 4 p(64..512) x 101 lambda x 53 hp-year "
+                         "expanding windows, P=513 (512 RFF + constant), S&P500 universe",
+                "global_batch": n_solves,
+                "seq_len": args.months,
+                "parallelism": f"dp{env.world_size}",
+                "utilities_per_step": n_util,
+                "device": torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu",
+                "setup_s": round(t_setup, 2),
+                "outputs_finite": finite,
+            },
+        }
+        print(json.dumps(rec), flush=True)
+    pdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

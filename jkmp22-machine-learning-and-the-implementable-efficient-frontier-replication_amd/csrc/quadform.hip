@@ -1,0 +1,129 @@
+// Out-of-sample validation utilities (PFML_hp_reals.py:81-102):
+//
+//     obj[job, l] = r_t^T beta_l - 1/2 beta_l^T D_t beta_l
+//
+// for every (g, year, p) cell, every one of its 12 validation months t and all 101 lambdas.
+// The reference evaluates 513,888 of these quadratic forms one at a time from Python.  Here a
+// job = (cell, month); the kernel computes the GEMM  U = D_t[:n,:n] * B  (B = [beta_l], n x L)
+// on fp64 MFMA and folds the two reductions into the epilogue, so U never leaves registers.
+//
+// Tile: 64 rows of D x 112 lambda columns (L <= 112) per 256-thread workgroup; each wave owns
+// 16 rows x 7 MFMA 16x16 accumulators.  Every workgroup writes a deterministic per-row-tile
+// partial; a second tiny kernel sums the partials in a fixed order (bitwise reproducible, no
+// float atomics).
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 64, BK = 16, NCOL = 112, NTILE = NCOL / 16, PAD = 16;
+
+struct JobDesc {
+  int64_t d_off;     // offset of D_t (P x P, ld ldD)
+  int64_t r_off;     // offset of r_t
+  int64_t b_off;     // offset of beta block [L][ldB]
+  int n;             // p + 1
+  int ptile0;        // first partial slot of this job
+};
+
+__global__ __launch_bounds__(256) void quadform_kernel(
+    const double* __restrict__ D, int64_t ldD, const double* __restrict__ R,
+    const double* __restrict__ Bt, int64_t ldB, const JobDesc* __restrict__ jobs,
+    const int* __restrict__ tile_job, int L, double* __restrict__ partial) {
+  __shared__ double As[BK][BM + PAD];
+  __shared__ double Bs[BK][NCOL + PAD];
+  __shared__ double red[4][NCOL];
+
+  const int tile = blockIdx.x;
+  const int j = tile_job[tile];
+  const JobDesc jd = jobs[j];
+  const int rt = tile - jd.ptile0;           // row tile within the job
+  const int i0 = rt * BM;
+  const int n = jd.n;
+  const double* Dm = D + jd.d_off;
+  const double* r = R + jd.r_off;
+  const double* bt = Bt + jd.b_off;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+
+  double4_t acc[NTILE];
+#pragma unroll
+  for (int q = 0; q < NTILE; ++q) acc[q] = double4_t{0.0, 0.0, 0.0, 0.0};
+
+  for (int k0 = 0; k0 < n; k0 += BK) {
+    // D tile: rows i0..i0+63, cols k0..k0+15 (row-major, contiguous along k) -> As[k][i]
+#pragma unroll
+    for (int q = 0; q < (BM * BK) / 256; ++q) {
+      const int e = t + q * 256, i = e / BK, k = e % BK;
+      const int gi = i0 + i, gk = k0 + k;
+      As[k][i] = (gi < n && gk < n) ? Dm[(int64_t)gi * ldD + gk] : 0.0;
+    }
+    // B tile: B[k][l] = beta_l[k0+k]  (beta stored lambda-major: contiguous along k)
+    for (int e = t; e < NCOL * BK; e += 256) {
+      const int l = e / BK, k = e % BK, gk = k0 + k;
+      Bs[k][l] = (l < L && gk < n) ? bt[(int64_t)l * ldB + gk] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      const double a = As[kk + (lane >> 4)][w * 16 + (lane & 15)];
+#pragma unroll
+      for (int q = 0; q < NTILE; ++q)
+        acc[q] = mfma_f64_16x16x4(a, Bs[kk + (lane >> 4)][q * 16 + (lane & 15)], acc[q]);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: sum over this wave's 16 rows of  beta_l[i] * (r_i - 1/2 U[i][l])
+#pragma unroll
+  for (int q = 0; q < NTILE; ++q) {
+    const int l = q * 16 + (lane & 15);
+    double s = 0.0;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int gi = i0 + w * 16 + PFML_F64_CROW(lane, rr);
+      if (gi < n && l < L) {
+        const double b = bt[(int64_t)l * ldB + gi];
+        s += b * (r[gi] - 0.5 * acc[q][rr]);
+      }
+    }
+    // lanes l, l+16, l+32, l+48 share the column
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    if (lane < 16) red[w][l] = s;
+  }
+  __syncthreads();
+  if (t < NCOL) {
+    const double s = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+    if (t < L) partial[(int64_t)tile * L + t] = s;
+  }
+}
+
+__global__ void quadform_reduce_kernel(const double* __restrict__ partial,
+                                       const JobDesc* __restrict__ jobs, int njobs, int L,
+                                       double* __restrict__ obj) {
+  const int j = blockIdx.x;
+  const int l = threadIdx.x;
+  if (j >= njobs || l >= L) return;
+  const JobDesc jd = jobs[j];
+  const int nt = (jd.n + BM - 1) / BM;
+  double s = 0.0;
+  for (int q = 0; q < nt; ++q) s += partial[(int64_t)(jd.ptile0 + q) * L + l];
+  obj[(int64_t)j * L + l] = s;
+}
+
+}  // namespace
+
+extern "C" int pfml_quadform_job_desc_size() { return (int)sizeof(JobDesc); }
+extern "C" int pfml_quadform_rows_per_tile() { return BM; }
+
+extern "C" hipError_t pfml_quadform(const double* D, int64_t ldD, const double* R,
+                                    const double* Bt, int64_t ldB, const void* jobs, int njobs,
+                                    const int* tile_job, int ntiles, int L, double* partial,
+                                    double* obj, hipStream_t st) {
+  if (njobs <= 0) return hipSuccess;
+  if (L > NCOL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(quadform_kernel, dim3(ntiles), dim3(256), 0, st, D, ldD, R, Bt, ldB,
+                     static_cast<const JobDesc*>(jobs), tile_job, L, partial);
+  hipLaunchKernelGGL(quadform_reduce_kernel, dim3(njobs), dim3(128), 0, st, partial,
+                     static_cast<const JobDesc*>(jobs), njobs, L, obj);
+  return hipGetLastError();
+}

@@ -1,0 +1,249 @@
+"""L5 hyper-parameter search: ridge coefficients (26) and out-of-sample utilities.
+
+Replaces PFML_Search_Coef.py (expanding running sums + 101 ``np.linalg.solve`` per
+(g, year, p), :60-143) and PFML_hp_reals.py (one quadratic form per (g, year, p, lambda,
+month) from Python, :62-130) with one batched device pipeline:
+
+1. window sums   - one segmented-sum pass over the resident [G, T, P, P] / [G, T, P] stacks
+                   (burn-in block + one block per hp year), prefix over blocks (K14);
+2. ridge grid    - one Householder tridiagonalisation per (g, year, p) cell and a
+                   tridiagonal solve per lambda (K15, csrc/ridge.hip);
+3. utilities     - fused D_t B GEMM + dot epilogue per (cell, validation month) (K16);
+4. scores        - expanding mean by (p, l) and dense rank per month (K17), in torch.
+
+Signals are kept in the interleaved order [constant, cos1, sin1, cos2, sin2, ...]
+(config.interleaved_order) so every hyper-parameter p uses the LEADING (p+1) x (p+1) block.
+
+Distributed: hp years are split contiguously over ranks.  Each rank sums only its own
+window blocks; the cross-rank exclusive prefix of the block totals is ONE all-gather of a
+P x P matrix per g per rank and the per-month utilities are all-gathered at
+the end (a few MB).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+import pandas as pd
+import torch
+
+from ..config import Config
+from ..ops.ridge import quadform_utilities, ridge_grid, segment_sums
+from ..parallel import collectives as coll
+from ..parallel.dist import env as dist_env
+from ..utils.dates import mi_from_ym, month_end
+from ..utils.trace import range_push, range_pop
+
+
+@dataclass
+class PfmlReals:
+    """Per-month PFML summands of (25) for every g (internal interleaved feature order)."""
+    months: np.ndarray                 # [T] month indices, sorted ascending
+    r_tilde: torch.Tensor              # [G, T, P]
+    denom: torch.Tensor                # [G, T, P, P]
+    risk: torch.Tensor | None = None   # [G, T, P, P] (kept for artifact parity)
+    tc: torch.Tensor | None = None
+
+    @property
+    def G(self):
+        return self.r_tilde.shape[0]
+
+    @property
+    def P(self):
+        return self.r_tilde.shape[-1]
+
+
+@dataclass
+class SearchPlan:
+    years: np.ndarray                  # hp years
+    seg_start: np.ndarray              # [nY] first month row of year block
+    seg_stop: np.ndarray
+    burn_stop: int                     # months[:burn_stop] are the burn-in block
+    count: np.ndarray                  # [nY] months in the expanding window of year Y
+    val_start: np.ndarray              # [nY] validation month rows [(Y-1)-12, Y-11]
+    val_stop: np.ndarray
+
+
+def make_plan(months: np.ndarray, years: np.ndarray) -> SearchPlan:
+    months = np.asarray(months, dtype=np.int64)
+    y0 = int(years.min())
+    # burn-in: eom < (y0-2)-12-31  (PFML_Search_Coef.py:69-72)
+    burn_stop = int(np.searchsorted(months, mi_from_ym(y0 - 2, 12), side="left"))
+    seg_start = np.searchsorted(months, [mi_from_ym(y - 2, 12) for y in years], side="left")
+    seg_stop = np.searchsorted(months, [mi_from_ym(y - 1, 11) for y in years], side="right")
+    # contiguous blocks: year Y's block begins where the previous block ended
+    seg_start = np.maximum(seg_start, np.r_[burn_stop, seg_stop[:-1]])
+    count = seg_stop.astype(np.int64)   # every month up to (Y-1)-11 is in the window
+    val_start = np.searchsorted(months, [mi_from_ym(y - 1, 12) for y in years], side="left")
+    val_stop = np.searchsorted(months, [mi_from_ym(y, 11) for y in years], side="right")
+    return SearchPlan(np.asarray(years), seg_start.astype(np.int64), seg_stop.astype(np.int64),
+                      burn_stop, count, val_start.astype(np.int64), val_stop.astype(np.int64))
+
+
+@dataclass
+class GridResult:
+    years: np.ndarray
+    p_vec: list
+    l_vec: np.ndarray
+    years_local: np.ndarray            # hp years whose betas live on this rank
+    beta: torch.Tensor                 # [G, nY_local, nP, L, P] (zero beyond p+1)
+    val_months: np.ndarray             # [nVal] month indices of all validation rows
+    val_year: np.ndarray               # [nVal] hp_end of each validation month
+    obj: torch.Tensor                  # [nVal, G, nP, L]  (all ranks, gathered)
+    timings: dict = field(default_factory=dict)
+
+
+def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridResult:
+    env = dist_env()
+    dev = reals.denom.device
+    G, T, P = reals.G, reals.denom.shape[1], reals.P
+    years = cfg.hp_years
+    p_vec = cfg.p_vec
+    nP = len(p_vec)
+    lvec = torch.as_tensor(cfg.l_vec, dtype=torch.float64, device=dev)
+    L = lvec.numel()
+    plan = make_plan(reals.months, years)
+
+    yl = np.asarray(list(coll.contiguous_split(len(years), env.world_size, env.rank)))
+    nYl = len(yl)
+
+    # ---- 1. window sums over this rank's blocks ------------------------------------
+    range_push("search.window_sums")
+    st = [plan.seg_start[i] for i in yl]
+    sp = [plan.seg_stop[i] for i in yl]
+    if nYl and yl[0] == 0:
+        st = [0] + st
+        sp = [plan.burn_stop] + sp
+    nseg = len(st)
+    starts = np.concatenate([np.asarray(st, np.int64) + g * T for g in range(G)]).astype(np.int32)
+    stops = np.concatenate([np.asarray(sp, np.int64) + g * T for g in range(G)]).astype(np.int32)
+    if nseg:
+        SD = segment_sums(reals.denom.reshape(G * T, P, P), starts, stops).view(G, nseg, P, P)
+        Sr = segment_sums(reals.r_tilde.reshape(G * T, P), starts, stops).view(G, nseg, P)
+        SD = torch.cumsum(SD, dim=1)
+        Sr = torch.cumsum(Sr, dim=1)
+        totD, totr = SD[:, -1], Sr[:, -1]
+    else:
+        SD = torch.zeros((G, 0, P, P), dtype=torch.float64, device=dev)
+        Sr = torch.zeros((G, 0, P), dtype=torch.float64, device=dev)
+        totD = torch.zeros((G, P, P), dtype=torch.float64, device=dev)
+        totr = torch.zeros((G, P), dtype=torch.float64, device=dev)
+    if env.is_dist:
+        flat = torch.cat([totD.reshape(G, -1), totr], dim=1)
+        off = coll.exclusive_prefix_sum(flat)
+        SD = SD + off[:, : P * P].view(G, 1, P, P)
+        Sr = Sr + off[:, P * P:].view(G, 1, P)
+    if nseg > nYl:                       # drop the burn-in prefix row
+        SD, Sr = SD[:, 1:], Sr[:, 1:]
+    range_pop()
+
+    # ---- 2. ridge grid ---------------------------------------------------------------
+    range_push("search.ridge")
+    cell_src, cell_n, cell_scale = [], [], []
+    for g in range(G):
+        for yi, y in enumerate(yl):
+            for p in p_vec:
+                cell_src.append(g * nYl + yi)
+                cell_n.append(p + 1)
+                cell_scale.append(1.0 / float(max(int(plan.count[y]), 1)))
+    beta = ridge_grid(SD.reshape(G * nYl, P, P), Sr.reshape(G * nYl, P),
+                      np.asarray(cell_src), np.asarray(cell_n), np.asarray(cell_scale), lvec)
+    beta = beta.view(G, nYl, nP, L, P)
+    range_pop()
+
+    # ---- 3. utilities for every (cell, validation month) ------------------------------
+    range_push("search.utilities")
+    jc, jm, jn = [], [], []
+    val_rows = []
+    for yi, y in enumerate(yl):
+        for m in range(plan.val_start[y], plan.val_stop[y]):
+            val_rows.append((m, y))
+    # job order: [val month][g][p]  -> obj reshapes to [nValLocal, G, nP, L]
+    for (m, y) in val_rows:
+        yi = int(np.nonzero(yl == y)[0][0])
+        for g in range(G):
+            for pi, p in enumerate(p_vec):
+                jc.append((g * nYl + yi) * nP + pi)
+                jm.append(g * T + m)
+                jn.append(p + 1)
+    obj = quadform_utilities(reals.denom.reshape(G * T, P, P), reals.r_tilde.reshape(G * T, P),
+                             beta.reshape(G * nYl * nP, L, P), np.asarray(jc), np.asarray(jm),
+                             np.asarray(jn))
+    obj = obj.view(len(val_rows), G, nP, L)
+    range_pop()
+
+    vm = np.asarray([reals.months[m] for m, _ in val_rows], dtype=np.int64)
+    vy = np.asarray([years[y] for _, y in val_rows], dtype=np.int64)
+    if gather and env.is_dist:
+        range_push("search.gather")
+        obj = coll.all_gather_varlen(obj)
+        vm = coll.all_gather_varlen(torch.as_tensor(vm, device=dev)).cpu().numpy()
+        vy = coll.all_gather_varlen(torch.as_tensor(vy, device=dev)).cpu().numpy()
+        range_pop()
+    return GridResult(years=years, p_vec=p_vec, l_vec=cfg.l_vec, years_local=years[yl],
+                      beta=beta, val_months=vm, val_year=vy, obj=obj)
+
+
+# ---------------------------------------------------------------------------------------
+# Scores (K17): expanding mean by (p, l) over eom_ret, dense rank per eom_ret.
+# ---------------------------------------------------------------------------------------
+def validation_scores(obj: torch.Tensor, frame_g: int, compat: bool):
+    """cum_obj and dense rank for the validation frame of ``frame_g``.
+
+    obj: [nVal, G, nP, L].  In compat mode (quirk Q2, PFML_hp_reals.py:60) the frame of g
+    holds the rows of every g' <= g, interleaved per month in g order (stable sort by
+    (p, l, eom_ret)); otherwise only g's own rows.
+    Returns (obj_seq, cum, rank) each [nVal, k, nP, L] with k = frame_g+1 (compat) or 1.
+    """
+    seq = obj[:, : frame_g + 1] if compat else obj[:, frame_g: frame_g + 1]
+    nV, k, nP, L = seq.shape
+    flat = seq.reshape(nV * k, nP, L)
+    cnt = torch.arange(1, nV * k + 1, dtype=flat.dtype, device=flat.device).view(-1, 1, 1)
+    cum = (torch.cumsum(flat, dim=0) / cnt).view(nV, k, nP, L)
+    # dense rank (descending) within each month over k * nP * L rows
+    vals = cum.reshape(nV, -1)
+    sv, idx = torch.sort(vals, dim=1, descending=True, stable=True)
+    new = torch.ones_like(sv, dtype=torch.int64)
+    new[:, 1:] = (sv[:, 1:] != sv[:, :-1]).to(torch.int64)
+    dense = torch.cumsum(new, dim=1).to(vals.dtype)
+    rank = torch.empty_like(vals)
+    rank.scatter_(1, idx, dense)
+    return seq, cum, rank.view(nV, k, nP, L)
+
+
+def validation_frame(grid: GridResult, cfg: Config) -> pd.DataFrame:
+    """validation.csv (columns eom, eom_ret, obj, l, p, hp_end, cum_obj, rank, g)."""
+    compat = cfg.run.compat_mode
+    G = grid.obj.shape[1]
+    frames = []
+    order = np.argsort(grid.val_months, kind="stable")
+    obj = grid.obj[torch.as_tensor(order, device=grid.obj.device)]
+    vm, vy = grid.val_months[order], grid.val_year[order]
+    eom = month_end(vm)
+    eom_ret = month_end(vm + 1)
+    nP, L = len(grid.p_vec), len(grid.l_vec)
+    for g in range(G):
+        seq, cum, rank = validation_scores(obj, g, compat)
+        nV, k = seq.shape[:2]
+        # rows sorted by (p, l, eom_ret, g') as the reference's stable sort leaves them
+        o = seq.permute(2, 3, 0, 1).reshape(-1).cpu().numpy()
+        c = cum.permute(2, 3, 0, 1).reshape(-1).cpu().numpy()
+        r = rank.permute(2, 3, 0, 1).reshape(-1).cpu().numpy()
+        pp = np.repeat(np.asarray(grid.p_vec), L * nV * k)
+        ll = np.tile(np.repeat(np.arange(L), nV * k), nP)
+        mm = np.tile(np.repeat(np.arange(nV), k), nP * L)
+        frames.append(pd.DataFrame({
+            "eom": eom[mm], "eom_ret": eom_ret[mm], "obj": o, "l": ll, "p": pp,
+            "hp_end": vy[mm], "cum_obj": c, "rank": r, "g": g}))
+    return pd.concat(frames, ignore_index=True)
+
+
+def gather_beta(grid: GridResult) -> tuple[np.ndarray, torch.Tensor]:
+    """All hp years' coefficients on every rank: (years, beta [G, nY, nP, L, P])."""
+    env = dist_env()
+    b = grid.beta.permute(1, 0, 2, 3, 4).contiguous()       # [nYl, G, nP, L, P]
+    yrs = torch.as_tensor(grid.years_local, device=b.device)
+    if env.is_dist:
+        b = coll.all_gather_varlen(b)
+        yrs = coll.all_gather_varlen(yrs)
+    return yrs.cpu().numpy(), b.permute(1, 0, 2, 3, 4).contiguous()

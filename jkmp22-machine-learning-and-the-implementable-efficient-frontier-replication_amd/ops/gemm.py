@@ -1,0 +1,71 @@
+"""fp64 batched GEMM with fused diagonal scalings.
+
+``gemm(A, B)`` computes ``alpha * diag(rs) @ op(A) @ op(B) @ diag(cs) + beta * C`` for 2-D or
+3-D (batched) fp64 tensors.  On a HIP device it runs ``pfml_dgemm`` (csrc/gemm_f64.hip,
+v_mfma_f64_16x16x4_f64); on CPU it is the torch fp64 oracle.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _native as nat
+
+
+def _as3(x):
+    return x.unsqueeze(0) if x.dim() == 2 else x
+
+
+def _bstride(x3, batch):
+    return 0 if (x3.shape[0] == 1 and batch > 1) else x3.stride(0)
+
+
+def gemm(A: torch.Tensor, B: torch.Tensor, *, trans_a: bool = False, trans_b: bool = False,
+         alpha: float = 1.0, beta: float = 0.0, out: torch.Tensor | None = None,
+         row_scale: torch.Tensor | None = None, col_scale: torch.Tensor | None = None
+         ) -> torch.Tensor:
+    squeeze = A.dim() == 2 and B.dim() == 2 and (out is None or out.dim() == 2)
+    A3, B3 = _as3(A), _as3(B)
+    batch = max(A3.shape[0], B3.shape[0])
+    M = A3.shape[2] if trans_a else A3.shape[1]
+    K = A3.shape[1] if trans_a else A3.shape[2]
+    N = B3.shape[1] if trans_b else B3.shape[2]
+    Kb = B3.shape[2] if trans_b else B3.shape[1]
+    if K != Kb:
+        raise ValueError(f"gemm: inner dims {K} vs {Kb}")
+    if out is None:
+        if beta != 0.0:
+            raise ValueError("beta != 0 needs out=")
+        out = torch.empty((batch, M, N), dtype=A.dtype, device=A.device)
+    C3 = _as3(out)
+    rs3 = None if row_scale is None else (row_scale.unsqueeze(0) if row_scale.dim() == 1 else row_scale)
+    cs3 = None if col_scale is None else (col_scale.unsqueeze(0) if col_scale.dim() == 1 else col_scale)
+
+    if nat.is_device(A):
+        if A.dtype != torch.float64:
+            raise TypeError("pfml_dgemm is fp64-only")
+        for x in (A3, B3, C3):
+            if x.stride(-1) != 1:
+                raise ValueError("gemm operands must have unit inner stride")
+        lib = nat.hip_lib()
+        err = lib.pfml_dgemm(
+            int(trans_a), int(trans_b), M, N, K, batch, float(alpha),
+            A3.data_ptr(), A3.stride(1), _bstride(A3, batch),
+            B3.data_ptr(), B3.stride(1), _bstride(B3, batch), float(beta),
+            C3.data_ptr(), C3.stride(1), C3.stride(0),
+            nat.ptr(rs3), 0 if rs3 is None else _bstride(rs3, batch),
+            nat.ptr(cs3), 0 if cs3 is None else _bstride(cs3, batch),
+            nat.stream_of(A))
+        nat.check(err, "pfml_dgemm")
+    else:
+        a = A3.transpose(1, 2) if trans_a else A3
+        b = B3.transpose(1, 2) if trans_b else B3
+        r = torch.matmul(a, b)
+        if rs3 is not None:
+            r = r * rs3.unsqueeze(-1)
+        if cs3 is not None:
+            r = r * cs3.unsqueeze(-2)
+        r = alpha * r
+        if beta != 0.0:
+            r = r + beta * C3
+        C3.copy_(r.expand_as(C3))
+    return out.squeeze(0) if squeeze and out.dim() == 3 else out

@@ -1,0 +1,133 @@
+"""Hyper-parameter grid kernels: window sums (K14), ridge solves (K15), utilities (K16).
+
+Device paths run csrc/segsum.hip, csrc/ridge.hip and csrc/quadform.hip; CPU paths are the
+fp64 oracle in the reference's own formulation (np.linalg.solve per lambda,
+PFML_Search_Coef.py:131-133; r'b - 1/2 b'Db per month, PFML_hp_reals.py:94).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _native as nat
+
+CELL_DTYPE = np.dtype([("src", "<i8"), ("rsrc", "<i8"), ("work", "<i8"), ("out", "<i8"),
+                       ("n", "<i4"), ("_pad", "<i4"), ("scale", "<f8")])
+JOB_DTYPE = np.dtype([("d_off", "<i8"), ("r_off", "<i8"), ("b_off", "<i8"), ("n", "<i4"),
+                      ("ptile0", "<i4")])
+
+
+def segment_sums(X: torch.Tensor, starts, stops) -> torch.Tensor:
+    """out[s] = X[starts[s]:stops[s]].sum(0) for X of shape [T, ...]."""
+    T = X.shape[0]
+    tail = X.shape[1:]
+    starts = np.asarray(starts, dtype=np.int32)
+    stops = np.asarray(stops, dtype=np.int32)
+    S = len(starts)
+    out = torch.empty((S, *tail), dtype=X.dtype, device=X.device)
+    if nat.is_device(X):
+        if X.dtype != torch.float64 or not X.is_contiguous():
+            raise ValueError("segment_sums: contiguous fp64 required")
+        E = X[0].numel() if T > 0 else int(np.prod(tail))
+        st = torch.as_tensor(starts, device=X.device)
+        sp = torch.as_tensor(stops, device=X.device)
+        nat.check(nat.hip_lib().pfml_segsum(X.data_ptr(), E, st.data_ptr(), sp.data_ptr(), S,
+                                            out.data_ptr(), nat.stream_of(X)), "pfml_segsum")
+    else:
+        for s in range(S):
+            out[s] = X[starts[s]:stops[s]].sum(0)
+    return out
+
+
+def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n: np.ndarray,
+               cell_scale: np.ndarray, lvec: torch.Tensor) -> torch.Tensor:
+    """beta[c, l, :n_c] = solve(SD[src_c][:n,:n]*scale_c + l I, Sr[src_c][:n]*scale_c).
+
+    SD: [S, P, P] running sums, Sr: [S, P]; returns [ncells, L, P] (zero beyond n_c).
+    """
+    S, P, _ = SD.shape
+    L = int(lvec.numel())
+    nc = len(cell_src)
+    beta = torch.zeros((nc, L, P), dtype=SD.dtype, device=SD.device)
+    if nc == 0:
+        return beta
+    if nat.is_device(SD):
+        lib = nat.hip_lib()
+        if lib.pfml_ridge_cell_desc_size() != CELL_DTYPE.itemsize:
+            raise RuntimeError("CellDesc layout mismatch between python and libpfml_hip")
+        desc = np.zeros(nc, dtype=CELL_DTYPE)
+        wsz = np.array([lib.pfml_ridge_work_doubles(int(n), L) for n in cell_n], dtype=np.int64)
+        woff = np.concatenate([[0], np.cumsum(wsz)[:-1]])
+        desc["src"] = np.asarray(cell_src, np.int64) * P * P
+        desc["rsrc"] = np.asarray(cell_src, np.int64) * P
+        desc["work"] = woff
+        desc["out"] = np.arange(nc, dtype=np.int64) * L * P
+        desc["n"] = np.asarray(cell_n, np.int32)
+        desc["scale"] = np.asarray(cell_scale, np.float64)
+        # big cells first: they bound the kernel's makespan
+        order = np.argsort(-desc["n"], kind="stable")
+        desc = desc[order]
+        d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(SD.device)
+        work = torch.empty(int(wsz.sum()), dtype=torch.float64, device=SD.device)
+        lv = lvec.to(device=SD.device, dtype=torch.float64).contiguous()
+        SDc, Src = SD.contiguous(), Sr.contiguous()
+        nat.check(lib.pfml_ridge_grid(SDc.data_ptr(), P, Src.data_ptr(), d_desc.data_ptr(), nc,
+                                      lv.data_ptr(), L, work.data_ptr(), beta.data_ptr(), P,
+                                      nat.stream_of(SD)), "pfml_ridge_grid")
+        return beta
+    eye_cache = {}
+    lv = lvec.to(dtype=SD.dtype)
+    for c in range(nc):
+        n, s = int(cell_n[c]), int(cell_src[c])
+        A = SD[s, :n, :n] * float(cell_scale[c])
+        r = Sr[s, :n] * float(cell_scale[c])
+        if n not in eye_cache:
+            eye_cache[n] = torch.eye(n, dtype=SD.dtype)
+        sys_ = A.unsqueeze(0) + lv.view(-1, 1, 1) * eye_cache[n]
+        sol, info = torch.linalg.solve_ex(sys_, r.unsqueeze(0).expand(L, n).unsqueeze(-1))
+        sol = sol.squeeze(-1)
+        sol[info != 0] = float("nan")          # singular system (reference: LinAlgError)
+        beta[c, :, :n] = sol
+    return beta
+
+
+def quadform_utilities(D: torch.Tensor, R: torch.Tensor, beta: torch.Tensor,
+                       job_cell: np.ndarray, job_month: np.ndarray, job_n: np.ndarray
+                       ) -> torch.Tensor:
+    """obj[j, l] = R[m_j,:n]·beta[c_j,l,:n] - 1/2 beta[c_j,l,:n]' D[m_j,:n,:n] beta[c_j,l,:n]."""
+    T, P, _ = D.shape
+    nc, L, Pb = beta.shape
+    nj = len(job_cell)
+    obj = torch.empty((nj, L), dtype=D.dtype, device=D.device)
+    if nj == 0:
+        return obj
+    if nat.is_device(D):
+        lib = nat.hip_lib()
+        if lib.pfml_quadform_job_desc_size() != JOB_DTYPE.itemsize:
+            raise RuntimeError("JobDesc layout mismatch between python and libpfml_hip")
+        rows = lib.pfml_quadform_rows_per_tile()
+        ntile = (np.asarray(job_n) + rows - 1) // rows
+        pt0 = np.concatenate([[0], np.cumsum(ntile)[:-1]]).astype(np.int32)
+        desc = np.zeros(nj, dtype=JOB_DTYPE)
+        desc["d_off"] = np.asarray(job_month, np.int64) * P * P
+        desc["r_off"] = np.asarray(job_month, np.int64) * P
+        desc["b_off"] = np.asarray(job_cell, np.int64) * L * Pb
+        desc["n"] = np.asarray(job_n, np.int32)
+        desc["ptile0"] = pt0
+        tile_job = np.repeat(np.arange(nj, dtype=np.int32), ntile)
+        dev = D.device
+        d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
+        d_tj = torch.from_numpy(tile_job).to(dev)
+        partial = torch.empty((len(tile_job), L), dtype=torch.float64, device=dev)
+        Dc, Rc, Bc = D.contiguous(), R.contiguous(), beta.contiguous()
+        nat.check(lib.pfml_quadform(Dc.data_ptr(), P, Rc.data_ptr(), Bc.data_ptr(), Pb,
+                                    d_desc.data_ptr(), nj, d_tj.data_ptr(), len(tile_job), L,
+                                    partial.data_ptr(), obj.data_ptr(), nat.stream_of(D)),
+                  "pfml_quadform")
+        return obj
+    for j in range(nj):
+        n, m, c = int(job_n[j]), int(job_month[j]), int(job_cell[j])
+        Bm = beta[c, :, :n]                       # [L, n]
+        quad = ((Bm @ D[m, :n, :n]) * Bm).sum(1)
+        obj[j] = Bm @ R[m, :n] - 0.5 * quad
+    return obj

@@ -1,0 +1,102 @@
+"""Collectives used by the sharded stages (RCCL on GPU, gloo on CPU).
+
+Every collective here moves MB-scale messages: shard totals of the expanding
+window sums (one P x P matrix per g per rank), per-cell utilities, chosen coefficients.
+On xGMI these are latency-bound, so the design point is *few* collectives per stage, not
+bucketing.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .dist import env
+
+
+def all_gather_cat(x: torch.Tensor) -> torch.Tensor:
+    """Concatenate equally-shaped tensors of every rank along dim 0 (rank order)."""
+    e = env()
+    if not e.is_dist:
+        return x
+    x = x.contiguous()
+    out = torch.empty((e.world_size * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x)
+    return out
+
+
+def all_gather_varlen(x: torch.Tensor) -> torch.Tensor:
+    """Concatenate tensors whose first dimension differs per rank (rank order)."""
+    e = env()
+    if not e.is_dist:
+        return x
+    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
+    ns = all_gather_cat(n).cpu().numpy()
+    m = int(ns.max())
+    pad = torch.zeros((m, *x.shape[1:]), dtype=x.dtype, device=x.device)
+    if x.shape[0]:
+        pad[: x.shape[0]] = x
+    g = all_gather_cat(pad)
+    parts = [g[r * m: r * m + int(ns[r])] for r in range(e.world_size)]
+    return torch.cat(parts, 0)
+
+
+def exclusive_prefix_sum(total: torch.Tensor) -> torch.Tensor:
+    """Sum of ``total`` over all lower ranks (zeros on rank 0): cross-GPU exclusive scan."""
+    e = env()
+    if not e.is_dist:
+        return torch.zeros_like(total)
+    g = all_gather_cat(total.unsqueeze(0))
+    if e.rank == 0:
+        return torch.zeros_like(total)
+    return g[: e.rank].sum(0)
+
+
+def all_reduce_max(v: float, device=None) -> float:
+    e = env()
+    if not e.is_dist:
+        return float(v)
+    t = torch.tensor([float(v)], dtype=torch.float64, device=device or e.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_reduce_sum_(t: torch.Tensor) -> torch.Tensor:
+    e = env()
+    if e.is_dist:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+
+
+def broadcast_object(obj, src: int = 0):
+    e = env()
+    if not e.is_dist:
+        return obj
+    box = [obj]
+    dist.broadcast_object_list(box, src=src,
+                               device=e.device if e.backend == "nccl" else None)
+    return box[0]
+
+
+def contiguous_split(n: int, world: int, rank: int) -> range:
+    """Balanced contiguous block of range(n) for ``rank`` (first n % world ranks get +1)."""
+    q, r = divmod(n, world)
+    start = rank * q + min(rank, r)
+    return range(start, start + q + (1 if rank < r else 0))
+
+
+def weighted_split(weights, world: int) -> list[range]:
+    """Contiguous split of items with positive weights into ``world`` near-equal-weight blocks."""
+    w = np.asarray(weights, dtype=np.float64)
+    n = len(w)
+    if world <= 1 or n == 0:
+        return [range(0, n)] + [range(n, n)] * (world - 1)
+    cum = np.concatenate([[0.0], np.cumsum(w)])
+    bounds = [0]
+    for r in range(1, world):
+        target = cum[-1] * r / world
+        b = int(np.searchsorted(cum, target))
+        b = min(max(b, bounds[-1]), n)
+        bounds.append(b)
+    bounds.append(n)
+    return [range(bounds[i], bounds[i + 1]) for i in range(world)]

@@ -1,0 +1,129 @@
+"""Numerics of the hand-written gfx950 kernels vs the fp64 torch CPU oracle of the same op."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(*shape, seed=0, dev="cpu"):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g, dtype=torch.float64).to(dev)
+
+
+def test_native_library_loaded(gpu):
+    from pfml.ops import _native as nat
+    lib = nat.hip_lib()
+    assert lib is not None
+    assert any(p.endswith("libpfml_hip.so") for p in nat.loaded_libraries())
+
+
+def test_mfma_f64_layout(gpu):
+    """A = I, asymmetric B: catches a swapped C/D row map (cdna_hip_programming.md §3)."""
+    from pfml.ops.gemm import gemm
+    A = torch.eye(16, dtype=torch.float64)
+    B = torch.arange(16 * 16, dtype=torch.float64).view(16, 16)
+    out = gemm(A.to(gpu), B.to(gpu)).cpu()
+    assert torch.equal(out, B)
+    out2 = gemm(B.to(gpu), A.to(gpu)).cpu()
+    assert torch.equal(out2, B)
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("shape", [(1, 37, 53, 29), (3, 64, 64, 64), (2, 130, 257, 100),
+                                   (1, 513, 513, 513)])
+def test_dgemm_matches_torch(gpu, ta, tb, shape):
+    from pfml.ops.gemm import gemm
+    b, M, N, K = shape
+    A = _rand(b, K, M, seed=1) if ta else _rand(b, M, K, seed=1)
+    B = _rand(b, N, K, seed=2) if tb else _rand(b, K, N, seed=2)
+    rs, cs = _rand(b, M, seed=3), _rand(b, N, seed=4)
+    C0 = _rand(b, M, N, seed=5)
+    ref = gemm(A, B, trans_a=ta, trans_b=tb, alpha=0.7, beta=0.3, out=C0.clone(),
+               row_scale=rs, col_scale=cs)
+    Cd = C0.to(gpu)
+    out = gemm(A.to(gpu), B.to(gpu), trans_a=ta, trans_b=tb, alpha=0.7, beta=0.3, out=Cd,
+               row_scale=rs.to(gpu), col_scale=cs.to(gpu)).cpu()
+    err = (out - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-13, err
+
+
+def test_segment_sums(gpu):
+    from pfml.ops.ridge import segment_sums
+    X = _rand(40, 7, 9, seed=7)
+    st, sp = [0, 5, 5, 20], [5, 5, 20, 40]
+    ref = segment_sums(X, st, sp)
+    out = segment_sums(X.to(gpu), st, sp).cpu()
+    assert torch.allclose(out, ref, rtol=1e-14, atol=1e-13)
+    Y = _rand(11, 6, seed=8)   # even row length -> vector path
+    assert torch.allclose(segment_sums(Y.to(gpu), [0, 3], [3, 11]).cpu(),
+                          segment_sums(Y, [0, 3], [3, 11]), rtol=1e-14, atol=1e-13)
+
+
+def _spd_stack(S, P, n_obs=40, seed=0):
+    X = _rand(S, n_obs, P, seed=seed)
+    return X.transpose(1, 2) @ X
+
+
+@pytest.mark.parametrize("P,ns", [(9, [9, 5, 3]), (65, [65, 33, 17]), (129, [129, 65])])
+def test_ridge_grid_matches_solve(gpu, P, ns):
+    from pfml.ops.ridge import ridge_grid
+    S = 3
+    SD = _spd_stack(S, P, n_obs=max(2 * P, 40), seed=11)
+    Sr = _rand(S, P, seed=12)
+    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
+    src = np.array([s for s in range(S) for _ in ns])
+    nn = np.array([n for _ in range(S) for n in ns])
+    sc = np.array([1.0 / (10 + s) for s in src])
+    ref = ridge_grid(SD, Sr, src, nn, sc, lv)
+    out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
+    rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1).clamp_min(1e-300)).max().item()
+    assert rel < 1e-9, rel
+
+
+def test_ridge_grid_production_size(gpu):
+    from pfml.ops.ridge import ridge_grid
+    P = 513
+    SD = _spd_stack(1, P, n_obs=1200, seed=21)
+    Sr = _rand(1, P, seed=22)
+    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
+    src, nn, sc = np.array([0, 0]), np.array([513, 257]), np.array([1e-3, 1e-3])
+    ref = ridge_grid(SD, Sr, src, nn, sc, lv)
+    out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
+    rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
+    assert rel < 1e-8, rel
+
+
+def test_quadform_utilities(gpu):
+    from pfml.ops.ridge import quadform_utilities
+    T, P, L = 5, 130, 101
+    D = _spd_stack(T, P, n_obs=50, seed=31)
+    R = _rand(T, P, seed=32)
+    beta = _rand(4, L, P, seed=33)
+    jc = np.array([0, 1, 2, 3, 3, 0])
+    jm = np.array([0, 1, 2, 3, 4, 4])
+    jn = np.array([130, 65, 33, 17, 130, 1])
+    ref = quadform_utilities(D, R, beta, jc, jm, jn)
+    out = quadform_utilities(D.to(gpu), R.to(gpu), beta.to(gpu), jc, jm, jn).cpu()
+    rel = ((out - ref).abs() / ref.abs().clamp_min(1e-12)).max().item()
+    assert rel < 1e-11, rel
+
+
+def test_grid_search_gpu_matches_cpu(gpu):
+    from pfml.config import Config
+    from pfml.models.search import PfmlReals, grid_search
+    from pfml.utils.dates import mi_from_ym
+    cfg = Config.default().override(["pf_ml.p_vec=[16,32]", "pf.dates.start_year=2001",
+                                     "pf.dates.end_yr=2005"])
+    G, P = 2, 33
+    months = np.arange(mi_from_ym(1994, 3), mi_from_ym(2005, 11) + 1)
+    T = len(months)
+    X = _rand(G * T, 40, P, seed=41)
+    D = (X.transpose(1, 2) @ X / 40).view(G, T, P, P)
+    r = 0.1 * _rand(G, T, P, seed=42)
+    cpu = grid_search(PfmlReals(months, r, D), cfg)
+    dev = grid_search(PfmlReals(months, r.to(gpu), D.to(gpu)), cfg)
+    rb = ((dev.beta.cpu() - cpu.beta).norm(dim=-1) / cpu.beta.norm(dim=-1)).max().item()
+    assert rb < 1e-9
+    ro = ((dev.obj.cpu() - cpu.obj).abs() / cpu.obj.abs().clamp_min(1e-12)).max().item()
+    assert ro < 1e-8
