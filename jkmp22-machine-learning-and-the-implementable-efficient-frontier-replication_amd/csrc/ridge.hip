@@ -7,13 +7,23 @@
 //
 //     beta_l = Q (T + l I)^-1 Q^T rbar
 //
-// One 1024-thread workgroup owns one (g, year, p) cell; the n x n working copy lives in
-// global memory (L2-resident: 2.1 MB at n = 513) and every Householder step makes ONE fused
-// read+write pass over the trailing matrix that applies the previous step's rank-2 update
-// and, in the same sweep, forms the next step's symmetric mat-vec (the standard sytd2
-// formulation needs two passes).  The tridiagonal systems use Gaussian elimination with
-// partial pivoting (as LAPACK dgtsv) so lambda = 0 on an indefinite/singular-ish Dbar behaves
-// like the reference's pivoted LU rather than failing.
+// One 1024-thread workgroup owns one (g, year, p) cell.
+//
+// Phase A (tridiagonalisation).  The n x n working copy lives in global memory (L2-resident:
+//   2.1 MB at n = 513) in FULL symmetric storage.  Each Householder step makes ONE fused
+//   read+write sweep of the trailing matrix that applies the previous step's rank-2 update
+//   and, in the same sweep, accumulates the next step's symmetric mat-vec (textbook sytd2
+//   needs two sweeps).  The sweep is column-oriented: lane l of a wave owns column i and walks
+//   rows j, so A[j][i] loads are coalesced across lanes and, because A is symmetric, the
+//   mat-vec sum  p_i = sum_j A[j][i] v_j  accumulates inside the lane with no cross-lane
+//   reduction; 8-way unrolled rows keep 8 loads per lane in flight.  The rank-2 update term is
+//   evaluated as (v_j w_i + w_j v_i) with contraction off so A stays bitwise symmetric.
+// Phase B (lambda sweep).  One thread per lambda runs Gaussian elimination with partial
+//   pivoting on T + l I (as LAPACK dgtsv), so l = 0 on a singular-ish Dbar behaves like the
+//   reference's pivoted LU; the back-substitution prefetches its operands 8 rows ahead.
+// Phase C (back-transform).  Y = [y_l] (n x L) is held in REGISTERS (thread = (lambda, row
+//   part), rows strided over parts), reflectors are staged through a 3-deep LDS ring, one
+//   barrier per reflector.
 #include "common.h"
 
 namespace {
@@ -21,6 +31,9 @@ namespace {
 constexpr int NMAX = 1024;      // largest p+1 supported (p_max = 512 -> 513)
 constexpr int NT = 1024;        // threads per workgroup
 constexpr int NW = NT / 64;
+constexpr int YREG = 33;        // rows of Y per lane in the register back-transform (n <= 528)
+constexpr int RMAX = 528;       // reflector row length staged by the back-transform ring
+constexpr int KB = 4;           // reflectors per staging block
 
 struct CellDesc {
   int64_t src;      // offset (doubles) of the running-sum matrix S_D for this cell
@@ -31,19 +44,24 @@ struct CellDesc {
   double scale;     // 1 / T  (the reference divides both sums by n months)
 };
 
+__device__ __forceinline__ double rank2(double a, double vj, double wi, double wj, double vi) {
+#pragma clang fp contract(off)
+  const double s = vj * wi + wj * vi;
+  return a - s;
+}
+
 __global__ __launch_bounds__(NT) void ridge_tridiag_kernel(
     const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
-    const CellDesc* __restrict__ cells, const double* __restrict__ lvec, int L,
-    double* __restrict__ work, double* __restrict__ beta_out, int64_t ldo) {
+    const CellDesc* __restrict__ cells, int L, double* __restrict__ work) {
   __shared__ double v[NMAX], vp[NMAX], wp[NMAX], pk[NMAX], z[NMAX];
   __shared__ double dd[NMAX], ee[NMAX], tau[NMAX];
+  __shared__ double part[NT];                 // sweep partials / back-transform partials
   __shared__ double red[NW * 2];
-  __shared__ double bcast[4];
-  __shared__ double part[8][128];
 
   const CellDesc cd = cells[blockIdx.x];
   const int n = cd.n;
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
   double* A = work + cd.work;                 // n x n, ld n
   double* Y = A + (int64_t)n * n;             // n x L  ([i][l])
   double* Ua = Y + (int64_t)n * L;            // pivoted-LU of T + lI, per lambda, [i][l]
@@ -54,9 +72,10 @@ __global__ __launch_bounds__(NT) void ridge_tridiag_kernel(
   const double sc = cd.scale;
 
   // ---- load scaled copy + rhs ---------------------------------------------------------
-  for (int64_t e = t; e < (int64_t)n * n; e += NT) {
-    const int i = (int)(e / n), j = (int)(e % n);
-    A[e] = S[(int64_t)i * ldS + j] * sc;
+  for (int i = wid; i < n; i += NW) {
+    const double* srow = S + (int64_t)i * ldS;
+    double* arow = A + (int64_t)i * n;
+    for (int j = lane; j < n; j += 64) arow[j] = srow[j] * sc;
   }
   for (int i = t; i < n; i += NT) {
     z[i] = Sr[cd.rsrc + i] * sc;
@@ -66,7 +85,6 @@ __global__ __launch_bounds__(NT) void ridge_tridiag_kernel(
   }
   __syncthreads();
 
-  // block reduction of two values at once
   auto bsum2 = [&](double a, double b, double& ra, double& rb) {
     a = wave_sum(a);
     b = wave_sum(b);
@@ -80,11 +98,12 @@ __global__ __launch_bounds__(NT) void ridge_tridiag_kernel(
     __syncthreads();
   };
 
+  // ================================ Phase A ============================================
   for (int k = 0; k + 2 < n; ++k) {
-    // (1) column k with the previous rank-2 update applied:  c_i, i >= k   (stored into pk)
+    // (1) row k (== column k) with the previous rank-2 update applied: c_i, i >= k
     const double vpk = vp[k], wpk = wp[k];
-    for (int i = k + t; i < n; i += NT)
-      pk[i] = A[(int64_t)i * n + k] - vp[i] * wpk - wp[i] * vpk;
+    const double* rowk = A + (int64_t)k * n;
+    for (int i = k + t; i < n; i += NT) pk[i] = rank2(rowk[i], vpk, wp[i], wpk, vp[i]);
     __syncthreads();
     // (2) Householder vector from x = c[k+1:]
     double x2 = 0.0;
@@ -102,111 +121,283 @@ __global__ __launch_bounds__(NT) void ridge_tridiag_kernel(
       ek = bet;
     }
     if (t == 0) { dd[k] = pk[k]; ee[k] = ek; tau[k] = tk; }
+    double* rowk_w = A + (int64_t)k * n;
     for (int i = k + 1 + t; i < n; i += NT) {
       const double vi = (i == k + 1) ? 1.0 : pk[i] * scal;
       v[i] = vi;
-      A[(int64_t)i * n + k] = vi;              // keep the reflector for the back-transform
+      rowk_w[i] = vi;                           // row k now stores reflector k
     }
     __syncthreads();
-    // (3) fused pass: A22 -= vp wp^T + wp vp^T ; pk_i = sum_j A22_ij v_j   (i, j >= k+1)
-    for (int i = k + 1 + wid; i < n; i += NW) {
-      const double vpi = vp[i], wpi = wp[i];
-      double* row = A + (int64_t)i * n;
-      double acc = 0.0;
-      for (int j = k + 1 + lane; j < n; j += 64) {
-        const double a = row[j] - vpi * wp[j] - wpi * vp[j];
-        row[j] = a;
-        acc += a * v[j];
+    // (3) fused column-oriented sweep over rows/cols r0..n-1
+    const int r0 = k + 1, m = n - r0;
+    const int ncb = (m + 63) >> 6;
+    const int nrg = NW / ncb;
+    {
+      const int cb = wid % ncb, rg = wid / ncb;
+      if (rg < nrg) {
+        const int c = cb * 64 + lane;
+        const int i = r0 + c;
+        const int rows_per = (m + nrg - 1) / nrg;
+        const int j0 = r0 + rg * rows_per;
+        const int j1 = min(n, j0 + rows_per);
+        double acc = 0.0;
+        if (i < n) {
+          const double vpi = vp[i], wpi = wp[i];
+          double* col = A + i;
+          int j = j0;
+          for (; j + 8 <= j1; j += 8) {
+            double a[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a[u] = col[(int64_t)(j + u) * n];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              a[u] = rank2(a[u], vp[j + u], wpi, wp[j + u], vpi);
+              col[(int64_t)(j + u) * n] = a[u];
+              acc += a[u] * v[j + u];
+            }
+          }
+          for (; j < j1; ++j) {
+            double a = rank2(col[(int64_t)j * n], vp[j], wpi, wp[j], vpi);
+            col[(int64_t)j * n] = a;
+            acc += a * v[j];
+          }
+        }
+        part[rg * (ncb * 64) + c] = acc;
       }
-      acc = wave_sum(acc);
-      if (lane == 0) pk[i] = tk * acc;
+    }
+    __syncthreads();
+    for (int c = t; c < m; c += NT) {
+      double s = 0.0;
+      for (int q = 0; q < nrg; ++q) s += part[q * (ncb * 64) + c];
+      pk[r0 + c] = tk * s;
     }
     __syncthreads();
     // (4) w = p - (tau/2)(p.v) v ;  z <- H_k z
     double pv = 0.0, vz = 0.0;
-    for (int i = k + 1 + t; i < n; i += NT) { pv += pk[i] * v[i]; vz += v[i] * z[i]; }
+    for (int i = r0 + t; i < n; i += NT) { pv += pk[i] * v[i]; vz += v[i] * z[i]; }
     double spv, svz;
     bsum2(pv, vz, spv, svz);
     const double half = 0.5 * tk * spv;
-    for (int i = k + 1 + t; i < n; i += NT) {
+    for (int i = r0 + t; i < n; i += NT) {
       wp[i] = pk[i] - half * v[i];
       vp[i] = v[i];
       z[i] -= tk * svz * v[i];
     }
-    if (t == 0) { vp[k] = 0.0; wp[k] = 0.0; }
     __syncthreads();
   }
   // trailing 2 x 2 (or smaller) block
   if (t == 0) {
     if (n >= 2) {
       const int a = n - 2, b = n - 1;
-      const double Aaa = A[(int64_t)a * n + a] - 2.0 * vp[a] * wp[a];
-      const double Aba = A[(int64_t)b * n + a] - vp[b] * wp[a] - wp[b] * vp[a];
-      const double Abb = A[(int64_t)b * n + b] - 2.0 * vp[b] * wp[b];
-      dd[a] = Aaa; ee[a] = Aba; dd[b] = Abb;
+      dd[a] = rank2(A[(int64_t)a * n + a], vp[a], wp[a], wp[a], vp[a]);
+      ee[a] = rank2(A[(int64_t)a * n + b], vp[a], wp[b], wp[a], vp[b]);
+      dd[b] = rank2(A[(int64_t)b * n + b], vp[b], wp[b], wp[b], vp[b]);
     } else {
       dd[0] = A[0];
     }
   }
   __syncthreads();
 
-  // ---- tridiagonal solves: one thread per lambda (GE with partial pivoting) -------------
-  if (t < L) {
-    const int l = t;
-    const double lam = lvec[l];
-    double a = dd[0] + lam, b = (n > 1) ? ee[0] : 0.0, c = 0.0, y = z[0];
-    for (int i = 0; i + 1 < n; ++i) {
-      const double lo = ee[i];
-      const double dn = dd[i + 1] + lam;
-      const double up = (i + 2 < n) ? ee[i + 1] : 0.0;
-      const double zn = z[i + 1];
-      double na, nb, ny;
-      if (fabs(a) >= fabs(lo)) {
-        const double m = (a != 0.0) ? lo / a : 0.0;
-        Ua[(int64_t)i * L + l] = a; Ub[(int64_t)i * L + l] = b; Uc[(int64_t)i * L + l] = c;
-        Uy[(int64_t)i * L + l] = y;
-        na = dn - m * b; nb = up - m * c; ny = zn - m * y;
-      } else {
-        const double m = a / lo;
-        Ua[(int64_t)i * L + l] = lo; Ub[(int64_t)i * L + l] = dn; Uc[(int64_t)i * L + l] = up;
-        Uy[(int64_t)i * L + l] = zn;
-        na = b - m * dn; nb = c - m * up; ny = y - m * zn;
-      }
-      a = na; b = nb; c = 0.0; y = ny;
+  // export the tridiagonal factor and Q^T r for the lambda sweep / back-transform kernels
+  double* dg = Uy + (int64_t)n * L;
+  double* eg = dg + n;
+  double* tg = eg + n;
+  double* zg = tg + n;
+  for (int i = t; i < n; i += NT) { dg[i] = dd[i]; eg[i] = ee[i]; tg[i] = tau[i]; zg[i] = z[i]; }
+}
+
+// Phase B: one thread per (cell, lambda) over the whole GPU.
+__global__ __launch_bounds__(256) void ridge_trisolve_kernel(
+    const CellDesc* __restrict__ cells, int ncells, const double* __restrict__ lvec, int L,
+    double* __restrict__ work) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (int64_t)ncells * L) return;
+  const int cell = (int)(gid / L), l = (int)(gid % L);
+  const CellDesc cd = cells[cell];
+  const int n = cd.n;
+  double* A = work + cd.work;
+  double* Y = A + (int64_t)n * n;
+  double* Ua = Y + (int64_t)n * L;
+  double* Ub = Ua + (int64_t)n * L;
+  double* Uc = Ub + (int64_t)n * L;
+  double* Uy = Uc + (int64_t)n * L;
+  const double* dd = Uy + (int64_t)n * L;
+  const double* ee = dd + n;
+  const double* z = ee + 2 * n;
+  const double lam = lvec[l];
+  double a = dd[0] + lam, b = (n > 1) ? ee[0] : 0.0, c = 0.0, y = z[0];
+  for (int i = 0; i + 1 < n; ++i) {
+    const double lo = ee[i];
+    const double dn = dd[i + 1] + lam;
+    const double up = (i + 2 < n) ? ee[i + 1] : 0.0;
+    const double zn = z[i + 1];
+    const int64_t o = (int64_t)i * L + l;
+    double na, nb, ny;
+    if (fabs(a) >= fabs(lo)) {
+      const double mu = (a != 0.0) ? lo / a : 0.0;
+      Ua[o] = a; Ub[o] = b; Uc[o] = c; Uy[o] = y;
+      na = dn - mu * b; nb = up - mu * c; ny = zn - mu * y;
+    } else {
+      const double mu = a / lo;
+      Ua[o] = lo; Ub[o] = dn; Uc[o] = up; Uy[o] = zn;
+      na = b - mu * dn; nb = c - mu * up; ny = y - mu * zn;
     }
-    double x1 = y / a, x2 = 0.0;
-    Y[(int64_t)(n - 1) * L + l] = x1;
-    for (int i = n - 2; i >= 0; --i) {
-      const double xi = (Uy[(int64_t)i * L + l] - Ub[(int64_t)i * L + l] * x1 -
-                         Uc[(int64_t)i * L + l] * x2) / Ua[(int64_t)i * L + l];
-      Y[(int64_t)i * L + l] = xi;
+    a = na; b = nb; c = 0.0; y = ny;
+  }
+  double x1 = y / a, x2 = 0.0;
+  Y[(int64_t)(n - 1) * L + l] = x1;
+  int i = n - 2;
+  for (; i >= 7; i -= 8) {                  // 8 rows of operands in flight
+    double ua[8], ub[8], uc[8], uy[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t o = (int64_t)(i - u) * L + l;
+      ua[u] = Ua[o]; ub[u] = Ub[o]; uc[u] = Uc[o]; uy[u] = Uy[o];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double xi = (uy[u] - ub[u] * x1 - uc[u] * x2) / ua[u];
+      Y[(int64_t)(i - u) * L + l] = xi;
       x2 = x1;
       x1 = xi;
     }
   }
-  __syncthreads();
-
-  // ---- back-transform  Y <- H_0 H_1 ... H_{n-3} Y --------------------------------------
-  const int lcol = t & 127, prt = t >> 7;   // 8 row-partitions x 128 lambda columns
-  for (int k = n - 3; k >= 0; --k) {
-    for (int i = k + 1 + t; i < n; i += NT) v[i] = A[(int64_t)i * n + k];
-    __syncthreads();
-    double s = 0.0;
-    if (lcol < L)
-      for (int i = k + 1 + prt; i < n; i += 8) s += v[i] * Y[(int64_t)i * L + lcol];
-    part[prt][lcol] = s;
-    __syncthreads();
-    if (lcol < L) {
-      double tot = 0.0;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) tot += part[q][lcol];
-      const double f = tau[k] * tot;
-      for (int i = k + 1 + prt; i < n; i += 8) Y[(int64_t)i * L + lcol] -= f * v[i];
-    }
-    __syncthreads();
+  for (; i >= 0; --i) {
+    const int64_t o = (int64_t)i * L + l;
+    const double xi = (Uy[o] - Ub[o] * x1 - Uc[o] * x2) / Ua[o];
+    Y[o] = xi;
+    x2 = x1;
+    x1 = xi;
   }
-  // ---- write beta_l (lambda-major, ld ldo) ---------------------------------------------
+}
+
+// Phase C: back-transform, one 1024-thread workgroup per cell.
+__global__ __launch_bounds__(NT) void ridge_backtransform_kernel(
+    const CellDesc* __restrict__ cells, int L, double* __restrict__ work,
+    double* __restrict__ beta_out, int64_t ldo) {
+  __shared__ double tau[NMAX];
+  const CellDesc cd = cells[blockIdx.x];
+  const int n = cd.n;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);   // wave-uniform row part
+  double* A = work + cd.work;
+  double* Y = A + (int64_t)n * n;
+  const double* tg = Y + 5LL * n * L + 2 * n;
+  for (int i = t; i < n; i += NT) tau[i] = tg[i];
+  __syncthreads();
+  // ================================ Phase C ============================================
+  // Y <- H_0 H_1 ... H_{n-3} Y ; reflector k is stored in row k (cols k+1..n-1).
+  // Register path: lambdas in chunks of 64 (lane = lambda), wave w owns rows w, w+16, ...
+  // (YREG rows per lane); reflectors staged one step ahead through a 3-deep LDS ring so each
+  // reflector costs exactly one barrier.
   double* out = beta_out + cd.out;
+  if ((n + NW - 1) / NW <= YREG && n <= RMAX) {
+    // reflector ring: 3 blocks of KB rows; block b+1 is written to LDS while block b is in use
+    // and block b+2 is in flight in registers (loads get KB reflectors of time to land).
+    __shared__ double ring[3 * KB][RMAX];
+    __shared__ double pp[2][NW][64];
+    const int npos = n - 2;                        // reflectors k = n-3 .. 0  (pos = n-3-k)
+    const int nblk = (npos + KB - 1) / KB;
+    constexpr int PER = (KB * RMAX + NT - 1) / NT; // staged elements per thread per block
+    auto stage_load = [&](int b, double (&reg)[PER]) {
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int e = t + q * NT;
+        const int r = e / RMAX, c = e % RMAX;
+        const int k = n - 3 - (b * KB + r);
+        reg[q] = (b < nblk && r < KB && k >= 0 && c < n) ? A[(int64_t)k * n + c] : 0.0;
+      }
+    };
+    auto stage_store = [&](int b, const double (&reg)[PER]) {
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int e = t + q * NT;
+        const int r = e / RMAX, c = e % RMAX;
+        if (r < KB) ring[(b % 3) * KB + r][c] = reg[q];
+      }
+    };
+    for (int l0 = 0; l0 < L; l0 += 64) {
+      const int l = l0 + lane;
+      const bool lv = l < L;
+      double y[YREG];
+#pragma unroll
+      for (int q = 0; q < YREG; ++q) {
+        const int i = wid + NW * q;
+        y[q] = (lv && i < n) ? Y[(int64_t)i * L + l] : 0.0;
+      }
+      double rg[PER];
+      stage_load(0, rg);
+      stage_store(0, rg);
+      stage_load(1, rg);
+      stage_store(1, rg);
+      stage_load(2, rg);
+      __syncthreads();
+      for (int pos = 0; pos < npos; ++pos) {
+        const int k = n - 3 - pos;
+        const int b = pos / KB;
+        if (pos % KB == 0 && pos > 0) {      // block b in use: publish b+1, fetch b+2
+          stage_store(b + 1, rg);
+          stage_load(b + 2, rg);
+        }
+        const double* vk = ring[(b % 3) * KB + (pos % KB)];
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll
+        for (int q = 0; q < YREG; q += 4) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = wid + NW * (q + u);
+            if (q + u < YREG && i > k && i < n) {
+              const double pr = vk[i] * y[q + u];
+              if (u == 0) s0 += pr; else if (u == 1) s1 += pr; else if (u == 2) s2 += pr; else s3 += pr;
+            }
+          }
+        }
+        pp[pos & 1][wid][lane] = (s0 + s1) + (s2 + s3);
+        __syncthreads();
+        double tot = 0.0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) tot += pp[pos & 1][q][lane];
+        const double f = tau[k] * tot;
+#pragma unroll
+        for (int q = 0; q < YREG; ++q) {
+          const int i = wid + NW * q;
+          if (i > k && i < n) y[q] -= f * vk[i];
+        }
+      }
+      if (lv) {
+#pragma unroll
+        for (int q = 0; q < YREG; ++q) {
+          const int i = wid + NW * q;
+          if (i < n) out[(int64_t)l * ldo + i] = y[q];
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  // Generic path (n > NW * YREG): Y stays in global memory.
+  {
+    __shared__ double vbuf[NMAX];
+    __shared__ double pr[8][128];
+    const int lcol = t & 127, prt = t >> 7;
+    for (int k = n - 3; k >= 0; --k) {
+      for (int i = k + 1 + t; i < n; i += NT) vbuf[i] = A[(int64_t)k * n + i];
+      __syncthreads();
+      double s = 0.0;
+      if (lcol < L)
+        for (int i = k + 1 + prt; i < n; i += 8) s += vbuf[i] * Y[(int64_t)i * L + lcol];
+      pr[prt][lcol] = s;
+      __syncthreads();
+      if (lcol < L) {
+        double tot = 0.0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) tot += pr[q][lcol];
+        const double f = tau[k] * tot;
+        for (int i = k + 1 + prt; i < n; i += 8) Y[(int64_t)i * L + lcol] -= f * vbuf[i];
+      }
+      __syncthreads();
+    }
+  }
   for (int64_t e = t; e < (int64_t)L * n; e += NT) {
     const int l = (int)(e / n), i = (int)(e % n);
     out[(int64_t)l * ldo + i] = Y[(int64_t)i * L + l];
@@ -216,7 +407,7 @@ __global__ __launch_bounds__(NT) void ridge_tridiag_kernel(
 }  // namespace
 
 extern "C" int64_t pfml_ridge_work_doubles(int n, int L) {
-  return (int64_t)n * n + 5LL * n * L;
+  return (int64_t)n * n + 5LL * n * L + 4LL * n;
 }
 
 extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const double* Sr,
@@ -225,8 +416,14 @@ extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const doubl
                                       hipStream_t st) {
   if (ncells <= 0) return hipSuccess;
   if (L > 128) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ridge_tridiag_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr,
-                     static_cast<const CellDesc*>(cells), lvec, L, work, beta_out, ldo);
+  const CellDesc* cd = static_cast<const CellDesc*>(cells);
+  hipLaunchKernelGGL(ridge_tridiag_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr, cd, L,
+                     work);
+  const int64_t nth = (int64_t)ncells * L;
+  hipLaunchKernelGGL(ridge_trisolve_kernel, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0,
+                     st, cd, ncells, lvec, L, work);
+  hipLaunchKernelGGL(ridge_backtransform_kernel, dim3(ncells), dim3(NT), 0, st, cd, L, work,
+                     beta_out, ldo);
   return hipGetLastError();
 }
 
