@@ -1,0 +1,103 @@
+// Panel-wide signal kernels of the PFML input stage.
+//
+// rff_sincos (K13, PFML_Input_Data.py:159-185,245): given Z = X W (computed by pfml_dgemm on
+// MFMA), writes the interleaved signal row [1, cos z_1, sin z_1, cos z_2, sin z_2, ...] so every
+// hyper-parameter p selects a leading column block.  One sincos per element (sincos shares
+// the range reduction).
+//
+// standardize (K11/K12, :357-391): for each (month batch b, lag theta) tile of N gathered
+// rows x P columns: demean the RFF columns (not the constant), scale every column to unit
+// L2 norm over the N real rows, then divide each row by its stock's volatility.  One
+// workgroup per (b, theta, 64-column strip); rows streamed twice from L2 (sum, then sum of
+// squares of the demeaned values) and written once.
+#include "common.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void rff_sincos_kernel(const double* __restrict__ Z, int64_t R,
+                                                         int half, double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t P = 2 * (int64_t)half + 1;
+  if (e >= R * (int64_t)half) return;
+  const int64_t r = e / half;
+  const int i = (int)(e % half);
+  double s, c;
+  sincos(Z[e], &s, &c);
+  double* o = out + r * P;
+  o[1 + 2 * i] = c;
+  o[2 + 2 * i] = s;
+  if (i == 0) o[0] = 1.0;
+}
+
+// rows: [B*TH, N] panel row indices (pad rows point to an all-zero row), n_real: [B] real
+// rows per batch entry, vol: per panel row.  out: [B*TH, N, P]
+__global__ __launch_bounds__(256) void standardize_kernel(const double* __restrict__ F, int P,
+                                                          const int64_t* __restrict__ rows,
+                                                          const int* __restrict__ n_real, int TH,
+                                                          int N, const double* __restrict__ vol,
+                                                          double* __restrict__ out) {
+  __shared__ double red[4][64];
+  __shared__ double colmean[64], colscale[64];
+  const int bt = blockIdx.y;                  // (b, theta)
+  const int b = bt / TH;
+  const int c0 = blockIdx.x * 64;
+  const int t = threadIdx.x, lane = t & 63, part = t >> 6;   // 4 row partitions
+  const int c = c0 + lane;
+  const int n = n_real[b];
+  const int64_t* rw = rows + (int64_t)bt * N;
+  // pass 1: column sums over real rows
+  double s = 0.0;
+  if (c < P)
+    for (int i = part; i < n; i += 4) s += F[rw[i] * P + c];
+  red[part][lane] = s;
+  __syncthreads();
+  if (part == 0) {
+    const double tot = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    colmean[lane] = (c == 0) ? 0.0 : tot / (double)n;     // constant column is not demeaned
+  }
+  __syncthreads();
+  // pass 2: sum of squares of the demeaned values
+  const double mu = colmean[lane];
+  double q = 0.0;
+  if (c < P)
+    for (int i = part; i < n; i += 4) {
+      const double x = F[rw[i] * P + c] - mu;
+      q += x * x;
+    }
+  red[part][lane] = q;
+  __syncthreads();
+  if (part == 0) {
+    const double tot = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    colscale[lane] = sqrt(1.0 / tot);
+  }
+  __syncthreads();
+  const double sc = colscale[lane];
+  double* o = out + (int64_t)bt * N * P;
+  if (c < P)
+    for (int i = part; i < N; i += 4) {
+      double v = 0.0;
+      if (i < n) v = (F[rw[i] * P + c] - mu) * sc / vol[rw[i]];
+      o[(int64_t)i * P + c] = v;
+    }
+}
+
+}  // namespace
+
+extern "C" hipError_t pfml_rff_sincos(const double* Z, int64_t R, int half, double* out,
+                                      hipStream_t st) {
+  const int64_t tot = R * (int64_t)half;
+  if (tot <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rff_sincos_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, Z,
+                     R, half, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pfml_standardize(const double* F, int P, const int64_t* rows,
+                                       const int* n_real, int B, int TH, int N,
+                                       const double* vol, double* out, hipStream_t st) {
+  if (B <= 0 || N <= 0) return hipSuccess;
+  dim3 grid((P + 63) / 64, B * TH);
+  hipLaunchKernelGGL(standardize_kernel, grid, dim3(256), 0, st, F, P, rows, n_real, TH, N, vol,
+                     out);
+  return hipGetLastError();
+}

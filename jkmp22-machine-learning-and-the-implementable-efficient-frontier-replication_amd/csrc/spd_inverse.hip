@@ -1,0 +1,214 @@
+// Batched in-place inverse of symmetric positive definite matrices by blocked Gauss-Jordan
+// elimination without pivoting (the 10 fixed-point inversions of m_func,
+// General_functions.py:959-960, plus the Denman-Beavers square-root iterations that replace
+// scipy.linalg.sqrtm, :956).
+//
+// For block column k (width NB):
+//     P      = A_kk^-1                          (pivot block, Gauss-Jordan in LDS)
+//     A_kj  <- P A_kj            (j != k)       row panel
+//     A_ij  <- A_ij - A_ik A_kj  (i, j != k)    rank-NB trailing update (fp64 MFMA)
+//     A_ik  <- -A_ik P           (i != k)       column panel
+//     A_kk  <- P
+// SPD pivots are Schur-complement diagonals (positive), so no pivoting is needed; a
+// non-positive or non-finite pivot sets the matrix's status flag and the host falls back to
+// a pivoted LU inverse for that matrix only.
+//
+// Kernels per block step (all batched over matrices): pivot+row panel (one workgroup per
+// matrix and column tile), trailing update with the column panel fused in the same launch
+// (workgroups owning column k's tiles apply -A_ik P instead of the update).
+#include "common.h"
+
+namespace {
+
+constexpr int NB = 32;
+
+// ---- step 1: invert the NB x NB pivot block of every matrix in LDS; write P to a side buffer
+__global__ __launch_bounds__(256) void gj_pivot_kernel(double* __restrict__ A, int n, int64_t lda,
+                                                        int64_t sA, int k0, int nb,
+                                                        double* __restrict__ Pbuf,
+                                                        int* __restrict__ status) {
+  __shared__ double P[NB][NB + 1];
+  const int b = blockIdx.x;
+  double* Ab = A + (int64_t)b * sA;
+  const int t = threadIdx.x;
+  for (int e = t; e < nb * nb; e += 256) {
+    const int i = e / nb, j = e % nb;
+    P[i][j] = Ab[(int64_t)(k0 + i) * lda + k0 + j];
+  }
+  __syncthreads();
+  // unblocked Gauss-Jordan on the nb x nb block (in place)
+  for (int p = 0; p < nb; ++p) {
+    const double piv = P[p][p];
+    __syncthreads();
+    if (!(piv > 0.0) || !isfinite(piv)) {
+      if (t == 0) status[b] = 1;
+    }
+    const double inv = 1.0 / piv;
+    // row p scaled, column p updated; thread handles element (i, j)
+    for (int e = t; e < nb * nb; e += 256) {
+      const int i = e / nb, j = e % nb;
+      if (i != p && j != p) P[i][j] -= P[i][p] * P[p][j] * inv;
+    }
+    __syncthreads();
+    for (int e = t; e < nb; e += 256) {
+      if (e != p) {
+        P[p][e] *= inv;
+        P[e][p] *= -inv;
+      }
+    }
+    if (t == 0) P[p][p] = inv;
+    __syncthreads();
+  }
+  double* Pb = Pbuf + (int64_t)b * NB * NB;
+  for (int e = t; e < nb * nb; e += 256) {
+    const int i = e / nb, j = e % nb;
+    Pb[i * NB + j] = P[i][j];
+  }
+}
+
+// ---- step 2: row panel  R_kj = P A_kj  (written to Rbuf, width n), A_kj keeps old values
+__global__ __launch_bounds__(256) void gj_rowpanel_kernel(const double* __restrict__ A, int n,
+                                                           int64_t lda, int64_t sA, int k0, int nb,
+                                                           const double* __restrict__ Pbuf,
+                                                           double* __restrict__ Rbuf) {
+  __shared__ double P[NB][NB + 1];
+  const int b = blockIdx.y;
+  const double* Ab = A + (int64_t)b * sA;
+  const int t = threadIdx.x;
+  for (int e = t; e < nb * nb; e += 256) P[e / nb][e % nb] = Pbuf[(int64_t)b * NB * NB + (e / nb) * NB + (e % nb)];
+  __syncthreads();
+  const int j = blockIdx.x * 256 + t;
+  if (j >= n) return;
+  double col[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) col[q] = (q < nb) ? Ab[(int64_t)(k0 + q) * lda + j] : 0.0;
+  double* Rb = Rbuf + (int64_t)b * NB * n;
+#pragma unroll 4
+  for (int i = 0; i < nb; ++i) {
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) s += P[i][q] * col[q];
+    Rb[(int64_t)i * n + j] = s;
+  }
+}
+
+// ---- step 3: trailing update + column panel, 64 x 64 tiles on fp64 MFMA.
+// For output tile (I, J):
+//   J not in block k, I not in block k: A_IJ -= A_Ik R_kJ       (A_Ik = OLD column panel)
+//   J not in block k, I in block k   : A_kJ  = R_kJ
+//   J in block k, I not in block k   : A_Ik  = -A_Ik P          (OLD A_Ik)
+//   J in block k, I in block k       : A_kk  = P
+// Tiles that read the old column panel must not race with tiles that overwrite it: the
+// column-panel tiles (J in block k) first stash A_Ik in LDS and every other tile reads the
+// column panel from the snapshot Cbuf taken by gj_snapshot_kernel.
+__global__ __launch_bounds__(256) void gj_snapshot_kernel(const double* __restrict__ A, int n,
+                                                           int64_t lda, int64_t sA, int k0, int nb,
+                                                           double* __restrict__ Cbuf) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double* Ab = A + (int64_t)b * sA + (int64_t)i * lda + k0;
+  double* Cb = Cbuf + (int64_t)b * n * NB + (int64_t)i * NB;
+#pragma unroll
+  for (int q = 0; q < NB; ++q) Cb[q] = (q < nb) ? Ab[q] : 0.0;
+}
+
+__global__ __launch_bounds__(256) void gj_update_kernel(double* __restrict__ A, int n, int64_t lda,
+                                                         int64_t sA, int k0, int nb,
+                                                         const double* __restrict__ Pbuf,
+                                                         const double* __restrict__ Rbuf,
+                                                         const double* __restrict__ Cbuf) {
+  constexpr int BT = 64;
+  __shared__ double Cs[NB][BT + 16];     // column panel tile, k-major: Cs[q][i]
+  __shared__ double Rs[NB][BT + 16];     // row panel tile: Rs[q][j]
+  const int b = blockIdx.y;
+  double* Ab = A + (int64_t)b * sA;
+  const double* Pb = Pbuf + (int64_t)b * NB * NB;
+  const double* Rb = Rbuf + (int64_t)b * NB * n;
+  const double* Cb = Cbuf + (int64_t)b * n * NB;
+  const int tiles = (n + BT - 1) / BT;
+  const int I0 = (blockIdx.x / tiles) * BT, J0 = (blockIdx.x % tiles) * BT;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  // load column panel rows I0.. (old values) and row panel cols J0..
+  for (int e = t; e < BT * NB; e += 256) {
+    const int i = e / NB, q = e % NB;
+    Cs[q][i] = (I0 + i < n && q < nb) ? Cb[(int64_t)(I0 + i) * NB + q] : 0.0;
+  }
+  for (int e = t; e < NB * BT; e += 256) {
+    const int q = e / BT, j = e % BT;
+    Rs[q][j] = (J0 + j < n && q < nb) ? Rb[(int64_t)q * n + J0 + j] : 0.0;
+  }
+  __syncthreads();
+  double4_t acc[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) acc[x][y] = double4_t{0.0, 0.0, 0.0, 0.0};
+  // rank-NB product for the whole tile (columns of block k simply ignore it)
+#pragma unroll
+  for (int q = 0; q < NB; q += 4) {
+    double a[2], bb[2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) a[x] = Cs[q + (lane >> 4)][wm * 32 + x * 16 + (lane & 15)];
+#pragma unroll
+    for (int y = 0; y < 2; ++y) bb[y] = Rs[q + (lane >> 4)][wn * 32 + y * 16 + (lane & 15)];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) acc[x][y] = mfma_f64_16x16x4(a[x], bb[y], acc[x][y]);
+  }
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = I0 + wm * 32 + x * 16 + PFML_F64_CROW(lane, r);
+        const int j = J0 + wn * 32 + y * 16 + (lane & 15);
+        if (i >= n || j >= n) continue;
+        const bool ik = (i >= k0 && i < k0 + nb), jk = (j >= k0 && j < k0 + nb);
+        double* p = Ab + (int64_t)i * lda + j;
+        if (!ik && !jk) {
+          *p -= acc[x][y][r];
+        } else if (ik && !jk) {
+          *p = Rb[(int64_t)(i - k0) * n + j];
+        } else if (!ik && jk) {
+          double s = 0.0;
+          for (int q = 0; q < nb; ++q) s += Cb[(int64_t)i * NB + q] * Pb[q * NB + (j - k0)];
+          *p = -s;
+        } else {
+          *p = Pb[(i - k0) * NB + (j - k0)];
+        }
+      }
+}
+
+}  // namespace
+
+extern "C" int64_t pfml_spd_inverse_work_doubles(int n, int batch) {
+  return (int64_t)batch * (NB * NB + 2LL * NB * n);
+}
+
+// In-place inverse of `batch` SPD matrices (n x n, leading dim lda, batch stride sA).
+// work: pfml_spd_inverse_work_doubles(n, batch) doubles; status: batch ints (set to 1 when a
+// non-positive pivot was met; caller zero-initialises).
+extern "C" hipError_t pfml_spd_inverse(double* A, int n, int64_t lda, int64_t sA, int batch,
+                                       double* work, int* status, hipStream_t st) {
+  if (n <= 0 || batch <= 0) return hipSuccess;
+  double* Pbuf = work;
+  double* Rbuf = Pbuf + (int64_t)batch * NB * NB;
+  double* Cbuf = Rbuf + (int64_t)batch * NB * n;
+  const int tiles = (n + 63) / 64;
+  for (int k0 = 0; k0 < n; k0 += NB) {
+    const int nb = (n - k0 < NB) ? (n - k0) : NB;
+    hipLaunchKernelGGL(gj_pivot_kernel, dim3(batch), dim3(256), 0, st, A, n, lda, sA, k0, nb,
+                       Pbuf, status);
+    hipLaunchKernelGGL(gj_rowpanel_kernel, dim3((n + 255) / 256, batch), dim3(256), 0, st, A, n,
+                       lda, sA, k0, nb, Pbuf, Rbuf);
+    hipLaunchKernelGGL(gj_snapshot_kernel, dim3((n + 255) / 256, batch), dim3(256), 0, st, A, n,
+                       lda, sA, k0, nb, Cbuf);
+    hipLaunchKernelGGL(gj_update_kernel, dim3(tiles * tiles, batch), dim3(256), 0, st, A, n, lda,
+                       sA, k0, nb, Pbuf, Rbuf, Cbuf);
+  }
+  return hipGetLastError();
+}

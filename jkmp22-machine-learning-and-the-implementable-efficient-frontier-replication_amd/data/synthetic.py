@@ -229,7 +229,7 @@ def settings_for_small(cfg, spec: SyntheticSpec):
     s["screens"]["start"] = pd.Timestamp(spec.start)
     s["screens"]["end"] = pd.Timestamp(spec.end)
     s["split"]["test_end"] = pd.Timestamp(spec.end)
-    s["cov_set"]["obs"] = 252
+    s["cov_set"]["obs"] = 400
     s["cov_set"]["hl_cor"] = 126
     s["cov_set"]["hl_var"] = 63
     return cfg

@@ -39,6 +39,10 @@ def _declare_hip(lib):
     lib.pfml_quadform_rows_per_tile.restype = I
     lib.pfml_segsum.argtypes = [P, L, P, P, I, P, P]
     lib.pfml_segsum.restype = I
+    lib.pfml_spd_inverse.argtypes = [P, I, L, L, I, P, P, P]
+    lib.pfml_spd_inverse.restype = I
+    lib.pfml_spd_inverse_work_doubles.argtypes = [I, I]
+    lib.pfml_spd_inverse_work_doubles.restype = L
     for name, argt in _EXTRA_HIP.items():
         fn = getattr(lib, name)
         fn.argtypes = argt[0]

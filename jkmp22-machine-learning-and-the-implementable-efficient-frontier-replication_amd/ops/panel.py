@@ -1,0 +1,62 @@
+"""Panel signal ops: RFF features (K13) and per-month standardisation (K11/K12).
+
+Device paths run csrc/panel.hip (+ pfml_dgemm for X W); CPU paths are the torch fp64 oracle
+of PFML_Input_Data.py:179-185 (cos/sin of X W) and :364-388 (demean, unit L2 norm, 1/vol).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _native as nat
+from .gemm import gemm
+
+nat.register_hip("pfml_rff_sincos", [C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p])
+nat.register_hip("pfml_standardize", [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                                      C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p])
+
+
+def rff_features(X: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
+    """[R, k] x [k, P/2] -> [R, P+1] rows [1, cos z1, sin z1, cos z2, sin z2, ...]."""
+    R, half = X.shape[0], W.shape[1]
+    Z = gemm(X, W)
+    out = torch.empty((R, 2 * half + 1), dtype=X.dtype, device=X.device)
+    if nat.is_device(X):
+        Zc = Z.contiguous()
+        nat.check(nat.hip_lib().pfml_rff_sincos(Zc.data_ptr(), R, half, out.data_ptr(),
+                                                nat.stream_of(X)), "pfml_rff_sincos")
+    else:
+        out[:, 0] = 1.0
+        out[:, 1::2] = torch.cos(Z)
+        out[:, 2::2] = torch.sin(Z)
+    return out
+
+
+def standardize_signals(F: torch.Tensor, idx: torch.Tensor, mask: torch.Tensor,
+                        vol: torch.Tensor) -> torch.Tensor:
+    """Gather + standardise the signal windows.
+
+    F: [R+1, P] panel features (last row all zero, used for padding), idx: [B, TH, N] rows,
+    mask: [B, N] 1 for real stocks (real rows first), vol: [R+1].  Returns [B, TH, N, P]."""
+    B, TH, N = idx.shape
+    P = F.shape[1]
+    if nat.is_device(F):
+        out = torch.empty((B, TH, N, P), dtype=F.dtype, device=F.device)
+        n_real = mask.sum(1).to(torch.int32).contiguous()
+        rows = idx.to(torch.int64).contiguous()
+        nat.check(nat.hip_lib().pfml_standardize(F.data_ptr(), P, rows.data_ptr(),
+                                                 n_real.data_ptr(), B, TH, N, vol.data_ptr(),
+                                                 out.data_ptr(), nat.stream_of(F)),
+                  "pfml_standardize")
+        return out
+    S = F[idx]                                                  # [B, TH, N, P]
+    m = mask.view(B, 1, N, 1)
+    n = mask.sum(1).view(B, 1, 1, 1)
+    mean = (S * m).sum(2, keepdim=True) / n
+    mean[..., 0] = 0.0                                          # constant is not demeaned
+    S = (S - mean) * m
+    norm = torch.sqrt(1.0 / (S * S).sum(2, keepdim=True))
+    S = S * norm
+    v = vol[idx].unsqueeze(-1)
+    return S / v

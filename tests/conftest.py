@@ -34,3 +34,20 @@ def pytest_collection_modifyitems(config, items):
 def gpu():
     import torch
     return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="session")
+def small_data(tmp_path_factory):
+    """Synthetic 50-stock panel taken through L0 -> L2 -> L3 once per session (CPU)."""
+    from pfml.config import Config
+    from pfml.data import synthetic as syn, acquire
+    from pfml.models import prep, risk
+    d = str(tmp_path_factory.mktemp("pfml_small"))
+    spec = syn.small_spec()
+    syn.write_raw(syn.generate(spec), d)
+    cfg = syn.settings_for_small(Config.default().override([f"run.data_dir={d}"]), spec)
+    acquire.get_additional_data(cfg)
+    acquire.sp500_subset(cfg)
+    prep.prepare_data(cfg)
+    risk.estimate_cov(cfg)
+    return cfg

@@ -1,0 +1,172 @@
+"""Stage tests on the synthetic small panel (CPU fp64 path) against independent oracles."""
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from oracle import month_ref
+
+
+def _load(cfg):
+    from pfml.config import get_features
+    from pfml.data import io
+    from pfml.models.risk import BarraCov
+    d = cfg.run.data_dir
+    chars = io.read_processed_chars(d, get_features())
+    barra = BarraCov.load(os.path.join(d, "Barra_Cov.npz"))
+    wealth = pd.read_csv(os.path.join(d, "wealth_processed.csv"), parse_dates=["eom"])
+    rf = io.read_risk_free(d)
+    return chars, barra, wealth, rf
+
+
+def test_prep_outputs_schema(small_data):
+    from pfml.data.io import CSV_COLUMNS
+    d = small_data.run.data_dir
+    w = pd.read_csv(os.path.join(d, "wealth_processed.csv"))
+    assert list(w.columns) == CSV_COLUMNS["wealth_processed.csv"]
+    cl = pd.read_csv(os.path.join(d, "cluster_labels_processed.csv"))
+    assert list(cl.columns) == CSV_COLUMNS["cluster_labels_processed.csv"]
+    assert cl.iloc[-1].tolist() == ["rvol_252d", -1, "low_risk"]
+    chars, *_ = _load(small_data)
+    assert chars["valid"].any()
+    # every valid row has its full 12-month lookback (Prepare_Data.py:412-441)
+    from pfml.utils.dates import month_index
+    c = chars.sort_values(["id", "eom"])
+    mi = month_index(c["eom"])
+    lag = c.groupby("id")["eom"].shift(12)
+    ok = ~lag.isna()
+    diff = mi[ok.to_numpy()] - month_index(lag[ok])
+    assert np.all(diff[c["valid"].to_numpy()[ok.to_numpy()]] == 12)
+    feats = chars[[f for f in chars.columns if f.startswith("ret_12_1")]]
+    assert feats.min().min() >= 0.0 and feats.max().max() <= 1.0
+
+
+def test_wealth_func_matches_definition():
+    from pfml.models.prep import wealth_func
+    rf = pd.DataFrame({"eom": pd.date_range("2000-01-31", periods=5, freq="ME"),
+                       "rf": [0.001, 0.002, 0.001, 0.0, 0.003]})
+    mk = pd.DataFrame({"eom_ret": rf["eom"], "mkt_vw_exc": [0.01, -0.02, 0.03, 0.0, 0.01]})
+    w = wealth_func(100.0, pd.Timestamp("2000-05-31"), mk, rf)
+    tret = (mk["mkt_vw_exc"] + rf["rf"]).to_numpy()
+    # backward cumulative product of (1 - tret), inclusive (quirk Q4)
+    exp = 100.0 * np.cumprod((1 - tret)[::-1])[::-1]
+    assert np.allclose(w["wealth"].to_numpy()[:-1], exp)
+    assert w["eom"].iloc[0] == pd.Timestamp("1999-12-31")
+    assert np.isnan(w["mu_ld1"].iloc[-1]) and w["wealth"].iloc[-1] == 100.0
+
+
+def test_categorize_sic_examples():
+    from pfml.models.prep import categorize_sic
+    got = categorize_sic([150, 3711, 3715, 1311, 2834, 3693, 7372, 4813, 4911, 5311, 6021,
+                          1000, np.nan])
+    assert list(got) == ["NoDur", "Durbl", "Manuf", "Enrgy", "Hlth", "Hlth", "BusEq", "Telcm",
+                         "Utils", "Shops", "Money", "Other", "Other"]
+
+
+def test_barra_covariance_psd(small_data):
+    from pfml.models.risk import create_cov
+    _, barra, *_ = _load(small_data)
+    assert barra.F.shape[1:] == (25, 25)
+    mi = barra.months[len(barra.months) // 2]
+    ids, S = create_cov(barra, mi)
+    assert np.allclose(S, S.T)
+    assert np.linalg.eigvalsh(S).min() > 0
+
+
+def test_weighted_cov_matches_definition():
+    from pfml.models.risk import weighted_cov
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(50, 4))
+    w = rng.uniform(0.1, 1.0, 50)
+    wn = w / w.sum()
+    mu = wn @ X
+    Xc = (X - mu) * np.sqrt(wn)[:, None]
+    ref = Xc.T @ Xc / (1 - (wn ** 2).sum())
+    got = weighted_cov(torch.tensor(X)[None], torch.tensor(w)[None], cor=False)[0].numpy()
+    assert np.allclose(got, ref, rtol=1e-12)
+    sd = np.sqrt(np.diag(ref))
+    cref = ref / np.outer(sd, sd)
+    np.fill_diagonal(cref, 1.0)
+    gotc = weighted_cov(torch.tensor(X)[None], torch.tensor(w)[None], cor=True)[0].numpy()
+    assert np.allclose(gotc, cref, rtol=1e-12)
+
+
+def _oracle_month(cfg, chars, barra, wealth, rf, W, d):
+    """Reference-order computation of one month (standardisation done pandas-style)."""
+    from pfml.config import get_features
+    from pfml.models.pfml_inputs import Panel, vol_scales
+    from pfml.utils.dates import month_index, pfml_date_grids
+    feats = get_features()
+    panel = Panel.from_chars(chars, feats)
+    grids = pfml_date_grids(int(barra.months.min()), 11, cfg.settings["split"]["test_end"],
+                            1971, 10)
+    vol = vol_scales(panel, barra, grids["lb"])
+    rows = panel.valid_rows(d)
+    ids = panel.ids[rows]
+    half = W.shape[1]
+    S_win, gt_win = [], []
+    for th in range(13):
+        rr = panel.rows(d - th, ids)
+        Z = panel.feats[rr] @ W
+        s = np.concatenate([np.cos(Z), np.sin(Z)], 1)
+        s = s - s.mean(0)
+        s = np.concatenate([s, np.ones((len(rr), 1))], 1)        # feat_cons: rff..., constant
+        s = s * np.sqrt(1.0 / (s ** 2).sum(0))
+        s = s / vol[rr][:, None]
+        S_win.append(s)
+        g = (1 + panel.cols["tr_ld0"][rr]) / (1 + panel.cols["mu_ld0"][rr])
+        gt_win.append(np.nan_to_num(g, nan=1.0))
+    bids, X, F, iv = barra.slice(d)
+    pos = np.searchsorted(bids, ids)
+    Sigma = X[pos] @ F @ X[pos].T + np.diag(iv[pos])
+    lam = panel.cols["lambda"][rows]
+    w = wealth.set_index(month_index(wealth["eom"]))["wealth"][d]
+    rfv = rf.set_index(month_index(rf["eom"]))["rf"][d]
+    r = panel.cols["ret_ld1"][rows]
+    out = month_ref(np.stack(S_win), np.stack(gt_win), r, Sigma, lam, w, rfv,
+                    cfg.pf_set["mu"], cfg.pf_set["gamma_rel"])
+    # feat_cons order (rff1_cos..rff_h_cos, rff1_sin.., constant) -> feat_all (constant first)
+    perm = np.r_[2 * half, np.arange(2 * half)]
+    rt, risk, tc, m = out
+    return rt[perm], risk[np.ix_(perm, perm)], tc[np.ix_(perm, perm)]
+
+
+def test_pfml_inputs_match_reference_order_oracle(small_data):
+    from pfml.config import get_features
+    from pfml.models.pfml_inputs import build_inputs, to_reference_order
+    from pfml.utils.dates import pfml_date_grids
+    cfg = small_data
+    chars, barra, wealth, rf = _load(cfg)
+    grids = pfml_date_grids(int(barra.months.min()), 11, cfg.settings["split"]["test_end"],
+                            1971, 10)
+    months = grids["m2"][[0, 7, 40]]
+    out = build_inputs(cfg, chars, barra, wealth, rf, "cpu", months=months, keep_risk_tc=True)
+    Pm = cfg.p_max
+    W = out.rff_w[0]
+    for i, d in enumerate(months):
+        rt, risk, tc = _oracle_month(cfg, chars, barra, wealth, rf, W, int(d))
+        e_rt = to_reference_order(out.reals.r_tilde[0, i], Pm).numpy()
+        e_rk = to_reference_order(out.reals.risk[0, i], Pm, dims=(0, 1)).numpy()
+        e_tc = to_reference_order(out.reals.tc[0, i], Pm, dims=(0, 1)).numpy()
+        assert np.abs(e_rt - rt).max() / np.abs(rt).max() < 1e-7
+        assert np.abs(e_rk - risk).max() / np.abs(risk).max() < 1e-7
+        assert np.abs(e_tc - tc).max() / np.abs(tc).max() < 1e-6
+        # compat (Q1): both g identical
+        assert torch.equal(out.reals.denom[0, i], out.reals.denom[1, i])
+
+
+def test_m_func_matches_sqrtm_reference():
+    from oracle import m_func_ref
+    from pfml.ops.linalg import m_func
+    rng = np.random.default_rng(3)
+    N, K = 40, 6
+    X = rng.normal(size=(N, K))
+    F = np.cov(rng.normal(size=(K, 100))) * 2e-2
+    S = X @ F @ X.T + np.diag(rng.uniform(0.01, 0.03, N) ** 2 * 21)
+    lam = 0.2 / rng.uniform(1e7, 1e9, N)
+    ref = m_func_ref(3e9, 0.007, 0.002, S * 10, 10, lam, 10)
+    got = m_func(torch.tensor(S)[None], torch.tensor(lam)[None], torch.tensor([3e9]),
+                 torch.tensor([0.002]), 0.007, 10, 10)[0].numpy()
+    assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-7
