@@ -66,7 +66,12 @@ def synthetic_reals(cfg: Config, device, n_months: int = 710, n_stocks: int = 50
     return PfmlReals(months=months, r_tilde=r, denom=denom)
 
 
-def one_step(reals: PfmlReals, cfg: Config):
+def one_step(reals: PfmlReals, cfg: Config, engine=None):
+    if engine is not None:
+        # full grid-search wall-clock INCLUDING the S4 input construction of every month
+        from pfml.models.pfml_inputs import build_inputs
+        chars, barra, wealth, rf, dev, months = engine
+        reals = build_inputs(cfg, chars, barra, wealth, rf, dev, months=months).reals
     res = grid_search(reals, cfg)
     G = res.obj.shape[1]
     out = []
@@ -83,6 +88,9 @@ def main():
     ap.add_argument("--months", type=int, default=710)
     ap.add_argument("--device", default="auto")
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--with-inputs", action="store_true",
+                    help="time S4 (PFML input construction for every month) + S5 + S6")
+    ap.add_argument("--stocks", type=int, default=500)
     args = ap.parse_args()
 
     env = pdist.init(args.device)
@@ -92,19 +100,33 @@ def main():
     n_util = n_solves * 12
 
     t_setup = time.perf_counter()
-    reals = synthetic_reals(cfg, dev, n_months=args.months)
+    engine = None
+    if args.with_inputs:
+        from pfml.data.synthetic import engine_inputs
+        from pfml.utils.dates import pfml_date_grids
+        cfg.run.compat_mode = False          # distinct RFF draw per g: no Q1 duplication
+        chars, barra, wealth, rf = engine_inputs(n_stocks=args.stocks)
+        g = pfml_date_grids(int(barra.months.min()), 11, cfg.settings["split"]["test_end"],
+                            1971, 10)
+        months = g["m2"]
+        mine = np.asarray(list(coll.contiguous_split(len(months), env.world_size, env.rank)))
+        engine = (chars, barra, wealth, rf, dev, months[mine])
+        args.months = len(months)
+        reals = None
+    else:
+        reals = synthetic_reals(cfg, dev, n_months=args.months)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t_setup = time.perf_counter() - t_setup
 
     for _ in range(args.warmup):
-        one_step(reals, cfg)
+        one_step(reals, cfg, engine)
     pdist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res, scores = one_step(reals, cfg)
+        res, scores = one_step(reals, cfg, engine)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     pdist.barrier()
@@ -139,6 +161,7 @@ def main():
                 "device": torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu",
                 "setup_s": round(t_setup, 2),
                 "outputs_finite": finite,
+                "includes_s4_inputs": bool(args.with_inputs),
             },
         }
         print(json.dumps(rec), flush=True)

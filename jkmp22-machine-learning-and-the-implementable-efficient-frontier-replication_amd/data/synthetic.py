@@ -237,3 +237,68 @@ def settings_for_small(cfg, spec: SyntheticSpec):
 
 __all__ = ["SyntheticSpec", "generate", "write_raw", "small_spec", "settings_for_small",
            "get_settings"]
+
+
+def engine_inputs(n_stocks: int = 500, start: str = "1962-01-31", end: str = "2023-12-31",
+                  n_factors: int = 25, seed: int = 0, turnover: float = 0.005):
+    """Post-prep inputs of the PFML engine at production shape, built directly in memory:
+    (chars DataFrame with the Factors_processed columns, BarraCov, wealth, risk_free).
+
+    Used by the benchmark and the scaling tests to skip the (one-shot, pandas-bound) L2/L3
+    stages: a rolling universe of ``n_stocks`` names with ``turnover`` monthly replacement,
+    ranked features in (0, 1), Barra loadings ~ N(0,1), F = sample covariance * 21e-4,
+    idiosyncratic variance U(0.01, 0.03)^2 * 21, lambda = 0.2 / U(1e7, 1e9), wealth 1e10.
+    Every name has its full 13-month lookback, so every row after the first 12 months of
+    its life is valid."""
+    from .. import config as _c
+    from ..models.risk import BarraCov
+    rng = np.random.default_rng(seed)
+    feats = _c.get_features()
+    m0, m1 = int(month_index(start)[0]), int(month_index(end)[0])
+    T = m1 - m0 + 1
+    # slot timelines: each slot replaced with probability `turnover` per month
+    ids_grid = np.zeros((T, n_stocks), dtype=np.int64)
+    born = np.zeros((T, n_stocks), dtype=np.int64)
+    cur = np.arange(n_stocks) + 10001
+    b = np.full(n_stocks, -24)
+    nxt = 10001 + n_stocks
+    for t in range(T):
+        rep = rng.random(n_stocks) < turnover
+        k = int(rep.sum())
+        cur = cur.copy(); b = b.copy()
+        cur[rep] = nxt + np.arange(k)
+        b[rep] = t
+        nxt += k
+        ids_grid[t], born[t] = cur, b
+    tt = np.repeat(np.arange(T), n_stocks)
+    ids = ids_grid.ravel()
+    age = tt - born.ravel()
+    R = len(ids)
+    months = month_end(m0 + tt)
+    chars = pd.DataFrame({
+        "id": ids, "eom": months, "size_grp": "large",
+        "me": np.exp(rng.normal(9, 1, R)), "lambda": 0.2 / rng.uniform(1e7, 1e9, R),
+        "ret_ld1": rng.normal(0.006, 0.08, R), "tr_ld0": rng.normal(0.009, 0.08, R),
+        "mu_ld0": np.repeat(rng.normal(0.009, 0.04, T), n_stocks),
+        "valid": age >= 12})
+    chars["tr_ld1"] = chars["ret_ld1"] + 0.003
+    chars["eom_ret"] = chars["eom"] + pd.offsets.MonthEnd(1)
+    F = pd.DataFrame(rng.random((R, len(feats))), columns=feats)
+    chars = pd.concat([chars, F], axis=1)
+    # Barra objects for every month over the valid names
+    Fm = np.stack([np.cov(rng.normal(size=(n_factors, 300))) * 1e-4 * 21 for _ in range(T)])
+    val = chars["valid"].to_numpy()
+    vm = (m0 + tt)[val]
+    vid = ids[val]
+    order = np.lexsort((vid, vm))
+    vm, vid = vm[order], vid[order]
+    cnt = np.bincount(vm - m0, minlength=T)
+    barra = BarraCov(months=np.arange(m0, m1 + 1, dtype=np.int64),
+                     offsets=np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64), ids=vid,
+                     X=rng.normal(size=(len(vid), n_factors)),
+                     ivol=rng.uniform(0.01, 0.03, len(vid)) ** 2 * 21, F=Fm,
+                     factors=[f"f{i}" for i in range(n_factors)])
+    allm = month_end(np.arange(m0 - 1, m1 + 1))
+    wealth = pd.DataFrame({"eom": allm, "wealth": 1e10, "mu_ld1": rng.normal(0.009, 0.04, len(allm))})
+    risk_free = pd.DataFrame({"eom": allm, "rf": 0.003})
+    return chars, barra, wealth, risk_free

@@ -155,7 +155,9 @@ def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         rffs.append(torch.cat([R, torch.zeros((1, P), dtype=R.dtype, device=dev)]))  # pad row
     del Xf
     range_pop()
-    vol = vol_scales(panel, barra, grids["lb"])
+    lbm = grids["lb"]
+    lbm = lbm[(lbm >= months.min() - (lb + 1)) & (lbm <= months.max())]
+    vol = vol_scales(panel, barra, lbm)
     vol_t = torch.as_tensor(np.r_[vol, 1.0], dtype=torch.float64, device=dev)
     gt_all = (1.0 + panel.cols["tr_ld0"]) / (1.0 + panel.cols["mu_ld0"])
     gt_all = np.nan_to_num(gt_all, nan=1.0)

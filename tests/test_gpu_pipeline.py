@@ -1,0 +1,100 @@
+"""Device (HIP) path of the per-month engine and the pipeline vs the fp64 CPU path."""
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g, dtype=torch.float64)
+
+
+@pytest.mark.parametrize("n,b", [(17, 3), (64, 2), (100, 4), (513, 2)])
+def test_spd_inverse(gpu, n, b):
+    from pfml.ops.linalg import spd_inverse
+    X = _rand(b, n + 10, n, seed=n)
+    A = X.transpose(1, 2) @ X / n + 0.1 * torch.eye(n, dtype=torch.float64)
+    inv = spd_inverse(A.to(gpu)).cpu()
+    err = (inv @ A - torch.eye(n, dtype=torch.float64)).abs().max().item()
+    assert err < 1e-10, err
+
+
+def test_spd_inverse_lu_fallback(gpu):
+    """An indefinite matrix trips the pivot check and falls back to pivoted LU."""
+    from pfml.ops.linalg import spd_inverse
+    A = torch.tensor([[0.0, 1.0, 0.0], [1.0, 0.0, 0.0], [0.0, 0.0, 2.0]], dtype=torch.float64)
+    inv = spd_inverse(A.to(gpu)).cpu()
+    assert torch.allclose(inv @ A, torch.eye(3, dtype=torch.float64), atol=1e-14)
+
+
+def test_m_func_gpu_matches_cpu(gpu):
+    from pfml.ops.linalg import m_func
+    rng = np.random.default_rng(0)
+    B, N, K = 3, 80, 10
+    X = rng.normal(size=(B, N, K))
+    F = np.stack([np.cov(rng.normal(size=(K, 200))) * 2e-2 for _ in range(B)])
+    S = np.einsum("bik,bkl,bjl->bij", X, F, X) + np.stack([np.diag(rng.uniform(0.01, 0.03, N) ** 2 * 21) for _ in range(B)])
+    lam = 0.2 / rng.uniform(1e7, 1e9, (B, N))
+    args = (torch.tensor(S), torch.tensor(lam), torch.tensor([1e10, 5e9, 2e10]),
+            torch.tensor([0.003, 0.001, 0.0]), 0.007, 10.0, 10)
+    ref = m_func(*args)
+    got = m_func(*[a.to(gpu) if isinstance(a, torch.Tensor) else a for a in args]).cpu()
+    assert (got - ref).abs().max().item() / ref.abs().max().item() < 1e-10
+
+
+def test_rff_and_standardize(gpu):
+    from pfml.ops.panel import rff_features, standardize_signals
+    X = torch.rand(300, 20, dtype=torch.float64)
+    W = 0.3 * _rand(20, 16, seed=1)
+    F = rff_features(X, W)
+    Fd = rff_features(X.to(gpu), W.to(gpu)).cpu()
+    assert torch.allclose(Fd, F, rtol=1e-12, atol=1e-13)
+    Fz = torch.cat([F, torch.zeros(1, F.shape[1], dtype=torch.float64)])
+    idx = torch.randint(0, 300, (2, 13, 40))
+    idx[1, :, 35:] = 300                              # padding rows
+    mask = torch.ones(2, 40, dtype=torch.float64)
+    mask[1, 35:] = 0
+    vol = torch.rand(301, dtype=torch.float64) + 0.05
+    ref = standardize_signals(Fz, idx, mask, vol)
+    got = standardize_signals(Fz.to(gpu), idx.to(gpu), mask.to(gpu), vol.to(gpu)).cpu()
+    assert torch.allclose(got, ref, rtol=1e-11, atol=1e-12)
+
+
+def test_pfml_inputs_gpu_matches_cpu(gpu, small_data):
+    from pfml.config import get_features
+    from pfml.data import io
+    from pfml.models.pfml_inputs import build_inputs
+    from pfml.models.risk import BarraCov
+    from pfml.utils.dates import pfml_date_grids
+    cfg = small_data
+    d = cfg.run.data_dir
+    chars = io.read_processed_chars(d, get_features())
+    barra = BarraCov.load(os.path.join(d, "Barra_Cov.npz"))
+    wealth = pd.read_csv(os.path.join(d, "wealth_processed.csv"), parse_dates=["eom"])
+    rf = io.read_risk_free(d)
+    g = pfml_date_grids(int(barra.months.min()), 11, cfg.settings["split"]["test_end"], 1971, 10)
+    months = g["m2"][:24]
+    cpu = build_inputs(cfg, chars, barra, wealth, rf, "cpu", months=months)
+    dev = build_inputs(cfg, chars, barra, wealth, rf, gpu, months=months)
+    for a, b in [(dev.reals.r_tilde.cpu(), cpu.reals.r_tilde), (dev.reals.denom.cpu(), cpu.reals.denom)]:
+        assert (a - b).abs().max().item() / b.abs().max().item() < 1e-9
+
+
+def test_full_pipeline_gpu(gpu, small_data, tmp_path):
+    from pfml.data.io import CSV_COLUMNS
+    from pfml.pipeline import Pipeline
+    cfg = small_data.override([f"run.artifact_dir={tmp_path}", "pf.dates.start_year=1999",
+                               "pf.dates.end_yr=2012", "pf.dates.split_years=3"])
+    p = Pipeline(cfg, device="cuda")
+    p.run(["pfml-input", "pfml-search-coef", "pfml-hp-reals", "pfml-aim", "pfml-hps",
+           "pfml-best-hps"])
+    for name in ("validation.csv", "weights.csv", "pf.csv", "pf_summary.csv"):
+        df = pd.read_csv(os.path.join(cfg.run.data_dir, name))
+        assert list(df.columns) == CSV_COLUMNS[name]
+    s = pd.read_csv(os.path.join(cfg.run.data_dir, "pf_summary.csv"))
+    assert np.isfinite(s[["r", "sd", "sr", "obj"]].to_numpy()).all()
