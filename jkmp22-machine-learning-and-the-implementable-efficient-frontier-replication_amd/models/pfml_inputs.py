@@ -66,7 +66,7 @@ class Panel:
         for c in ("ret_ld1", "tr_ld0", "mu_ld0", "tr_ld1", "lambda", "me"):
             if c in chars:
                 cols[c] = chars[c].to_numpy(np.float64)[order]
-        feats = chars[features].to_numpy(np.float64)[order]
+        feats = np.ascontiguousarray(chars[features].to_numpy(np.float64)[order])
         return cls(mi=mi, ids=ids, key=mi * 10_000_000 + ids,
                    valid=chars["valid"].to_numpy(bool)[order], cols=cols, feats=feats)
 

@@ -43,9 +43,19 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, trans_a: bool = False, trans_b: bo
     if nat.is_device(A):
         if A.dtype != torch.float64:
             raise TypeError("pfml_dgemm is fp64-only")
-        for x in (A3, B3, C3):
-            if x.stride(-1) != 1:
-                raise ValueError("gemm operands must have unit inner stride")
+        # a transposed view is consumed as-is by flipping the operand's transpose flag
+        if A3.stride(-1) != 1:
+            if A3.stride(-2) == 1:
+                A3, trans_a = A3.transpose(1, 2), not trans_a
+            else:
+                A3 = A3.contiguous()
+        if B3.stride(-1) != 1:
+            if B3.stride(-2) == 1:
+                B3, trans_b = B3.transpose(1, 2), not trans_b
+            else:
+                B3 = B3.contiguous()
+        if C3.stride(-1) != 1:
+            raise ValueError("gemm output must have unit inner stride")
         lib = nat.hip_lib()
         err = lib.pfml_dgemm(
             int(trans_a), int(trans_b), M, N, K, batch, float(alpha),

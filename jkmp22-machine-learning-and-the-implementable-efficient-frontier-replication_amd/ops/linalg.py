@@ -49,7 +49,13 @@ def spd_inverse(A: torch.Tensor, inplace: bool = False) -> torch.Tensor:
 
 def solve(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
     """Batched general solve A X = B with partial pivoting (np.linalg.solve semantics)."""
-    X, info = torch.linalg.solve_ex(A, B)
+    if nat.is_device(A) and A.dim() == 3 and A.shape[0] > 8:
+        # vendor batched getrf allocates per-batch workspace: bound the batch
+        parts = [torch.linalg.solve_ex(A[i:i + 8], B[i:i + 8]) for i in range(0, A.shape[0], 8)]
+        X = torch.cat([p[0] for p in parts])
+        info = torch.cat([p[1] for p in parts])
+    else:
+        X, info = torch.linalg.solve_ex(A, B)
     if bool((info != 0).any()):
         COUNTERS.add("linalg.singular_solve", int((info != 0).sum()))
     return X
