@@ -1,0 +1,275 @@
+// Batched general solve  A X = B  by blocked Gauss-Jordan elimination with partial pivoting
+// (omega = solve(const, Omega), PFML_Input_Data.py:455-456; np.linalg.solve
+// semantics - const = sum_theta agg_theta is not symmetric).
+//
+// The system is stored augmented, one row per equation: M = [ ... B (m cols) ... A (n cols) ...]
+// with B at column b0 and A at column a0 of each row (leading dimension ldm).  This is exactly
+// the layout the Horner aggregation produces ([Omega | const]), so no copies are made.
+// For each block column k (width NB) of A:
+//   1. pivot search: partial-pivoting LU of the panel A[k0:, k-block] in LDS picks NB pivot rows
+//      (LAPACK-style sequential swap list);
+//   2. the swaps are applied to every live column (A cols >= k0 and all B cols);
+//   3. P = A_kk^-1 (Gauss-Jordan in LDS, pivots non-zero by construction);
+//   4. row panel R = P M_k (live columns), column panel snapshot C = M[:, k-block];
+//   5. all other rows: M_i -= C_i R  (rank-NB update on fp64 MFMA); block rows: M_k = R.
+// Columns of A left of the current block are never touched again (they would hold the
+// identity), so the work is n^3 + 2 n^2 m flops like an LU solve.
+#include "common.h"
+
+namespace {
+
+constexpr int NB = 16;
+constexpr int PMAX = 1024;      // panel rows held in LDS
+
+// live column v (0 .. nlive-1) -> physical column
+__device__ __forceinline__ int live_col(int v, int nA_live, int a_first, int b0) {
+  return v < nA_live ? a_first + v : b0 + (v - nA_live);
+}
+
+__global__ __launch_bounds__(256) void lu_pivot_kernel(const double* __restrict__ M, int n,
+                                                       int64_t ldm, int64_t sM, int a0, int k0,
+                                                       int nb, int* __restrict__ piv,
+                                                       int* __restrict__ status) {
+  __shared__ double Pn[PMAX][NB + 1];
+  __shared__ double rv[4];
+  __shared__ int ri[4];
+  const int b = blockIdx.x;
+  const double* Mb = M + (int64_t)b * sM;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int rows = n - k0;
+  for (int e = t; e < rows * nb; e += 256) {
+    const int i = e / nb, j = e % nb;
+    Pn[i][j] = Mb[(int64_t)(k0 + i) * ldm + a0 + k0 + j];
+  }
+  __syncthreads();
+  for (int j = 0; j < nb; ++j) {
+    // argmax |Pn[i][j]|, i in [j, rows)
+    double best = -1.0;
+    int bi = j;
+    for (int i = j + t; i < rows; i += 256) {
+      const double v = fabs(Pn[i][j]);
+      if (v > best) { best = v; bi = i; }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double ov = __shfl_xor(best, off, 64);
+      const int oi = __shfl_xor(bi, off, 64);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    if (lane == 0) { rv[w] = best; ri[w] = bi; }
+    __syncthreads();
+    if (t == 0) {
+      double bv = rv[0];
+      int bx = ri[0];
+      for (int q = 1; q < 4; ++q)
+        if (rv[q] > bv || (rv[q] == bv && ri[q] < bx)) { bv = rv[q]; bx = ri[q]; }
+      ri[0] = bx;
+      piv[(int64_t)b * NB + j] = k0 + bx;
+      if (!(bv > 0.0) || !isfinite(bv)) status[b] = 1;
+    }
+    __syncthreads();
+    const int p = ri[0];
+    if (p != j && t < nb) {
+      const double tmp = Pn[j][t];
+      Pn[j][t] = Pn[p][t];
+      Pn[p][t] = tmp;
+    }
+    __syncthreads();
+    const double pv = Pn[j][j];
+    for (int i = j + 1 + t; i < rows; i += 256) {
+      const double l = Pn[i][j] / pv;
+      for (int c = j + 1; c < nb; ++c) Pn[i][c] -= l * Pn[j][c];
+    }
+    __syncthreads();
+  }
+}
+
+// apply the NB sequential row swaps of block k0 to every live column (+ block k's own A cols)
+__global__ __launch_bounds__(256) void lu_swap_kernel(double* __restrict__ M, int64_t ldm,
+                                                      int64_t sM, int ncol, int a_first, int nA,
+                                                      int b0, int k0, int nb,
+                                                      const int* __restrict__ piv) {
+  const int b = blockIdx.y;
+  const int v = blockIdx.x * 256 + threadIdx.x;
+  if (v >= ncol) return;
+  const int c = live_col(v, nA, a_first, b0);
+  double* Mb = M + (int64_t)b * sM;
+  const int* pb = piv + (int64_t)b * NB;
+  for (int j = 0; j < nb; ++j) {
+    const int p = pb[j];
+    if (p != k0 + j) {
+      double* x = Mb + (int64_t)(k0 + j) * ldm + c;
+      double* y = Mb + (int64_t)p * ldm + c;
+      const double tmp = *x;
+      *x = *y;
+      *y = tmp;
+    }
+  }
+}
+
+// P = A_kk^-1 by Gauss-Jordan without pivoting (rows already pivoted)
+__global__ __launch_bounds__(256) void lu_blockinv_kernel(const double* __restrict__ M,
+                                                          int64_t ldm, int64_t sM, int a0, int k0,
+                                                          int nb, double* __restrict__ Pbuf) {
+  __shared__ double P[NB][NB + 1];
+  const int b = blockIdx.x;
+  const double* Mb = M + (int64_t)b * sM;
+  const int t = threadIdx.x;
+  for (int e = t; e < nb * nb; e += 256) P[e / nb][e % nb] = Mb[(int64_t)(k0 + e / nb) * ldm + a0 + k0 + e % nb];
+  __syncthreads();
+  for (int p = 0; p < nb; ++p) {
+    const double inv = 1.0 / P[p][p];
+    __syncthreads();
+    for (int e = t; e < nb * nb; e += 256) {
+      const int i = e / nb, j = e % nb;
+      if (i != p && j != p) P[i][j] -= P[i][p] * P[p][j] * inv;
+    }
+    __syncthreads();
+    for (int e = t; e < nb; e += 256)
+      if (e != p) { P[p][e] *= inv; P[e][p] *= -inv; }
+    if (t == 0) P[p][p] = inv;
+    __syncthreads();
+  }
+  for (int e = t; e < NB * NB; e += 256) {
+    const int i = e / NB, j = e % NB;
+    Pbuf[(int64_t)b * NB * NB + e] = (i < nb && j < nb) ? P[i][j] : 0.0;
+  }
+}
+
+// R = P M_k over live columns (excluding block k's own A columns) -> Rbuf [NB][nlive]
+__global__ __launch_bounds__(256) void lu_rowpanel_kernel(const double* __restrict__ M, int64_t ldm,
+                                                          int64_t sM, int nlive, int a_first,
+                                                          int nA, int b0, int k0, int nb,
+                                                          const double* __restrict__ Pbuf,
+                                                          double* __restrict__ Rbuf) {
+  __shared__ double P[NB][NB + 1];
+  const int b = blockIdx.y;
+  const int t = threadIdx.x;
+  for (int e = t; e < NB * NB; e += 256) P[e / NB][e % NB] = Pbuf[(int64_t)b * NB * NB + e];
+  __syncthreads();
+  const int v = blockIdx.x * 256 + t;
+  if (v >= nlive) return;
+  const int c = live_col(v, nA, a_first, b0);
+  const double* Mb = M + (int64_t)b * sM;
+  double col[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) col[q] = (q < nb) ? Mb[(int64_t)(k0 + q) * ldm + c] : 0.0;
+  double* Rb = Rbuf + (int64_t)b * NB * nlive;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < NB; ++q) s += P[i][q] * col[q];
+    if (i < nb) Rb[(int64_t)i * nlive + v] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void lu_snapshot_kernel(const double* __restrict__ M, int n,
+                                                          int64_t ldm, int64_t sM, int a0, int k0,
+                                                          int nb, double* __restrict__ Cbuf) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double* src = M + (int64_t)b * sM + (int64_t)i * ldm + a0 + k0;
+  double* dst = Cbuf + ((int64_t)b * n + i) * NB;
+#pragma unroll
+  for (int q = 0; q < NB; ++q) dst[q] = (q < nb) ? src[q] : 0.0;
+}
+
+// rows outside block k: M_i -= C_i R ; block rows: M_k = R   (live columns only)
+__global__ __launch_bounds__(256) void lu_update_kernel(double* __restrict__ M, int n, int64_t ldm,
+                                                        int64_t sM, int nlive, int a_first, int nA,
+                                                        int b0, int k0, int nb,
+                                                        const double* __restrict__ Rbuf,
+                                                        const double* __restrict__ Cbuf) {
+  constexpr int BT = 64;
+  __shared__ double Cs[NB][BT + 16];
+  __shared__ double Rs[NB][BT + 16];
+  const int b = blockIdx.y;
+  double* Mb = M + (int64_t)b * sM;
+  const double* Rb = Rbuf + (int64_t)b * NB * nlive;
+  const double* Cb = Cbuf + (int64_t)b * n * NB;
+  const int tc = (nlive + BT - 1) / BT;
+  const int I0 = (blockIdx.x / tc) * BT, V0 = (blockIdx.x % tc) * BT;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  for (int e = t; e < BT * NB; e += 256) {
+    const int i = e / NB, q = e % NB;
+    Cs[q][i] = (I0 + i < n) ? Cb[(int64_t)(I0 + i) * NB + q] : 0.0;
+  }
+  for (int e = t; e < NB * BT; e += 256) {
+    const int q = e / BT, j = e % BT;
+    Rs[q][j] = (V0 + j < nlive && q < nb) ? Rb[(int64_t)q * nlive + V0 + j] : 0.0;
+  }
+  __syncthreads();
+  double4_t acc[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y) acc[x][y] = double4_t{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < NB; q += 4) {
+    double a[2], bb[2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) a[x] = Cs[q + (lane >> 4)][wm * 32 + x * 16 + (lane & 15)];
+#pragma unroll
+    for (int y = 0; y < 2; ++y) bb[y] = Rs[q + (lane >> 4)][wn * 32 + y * 16 + (lane & 15)];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) acc[x][y] = mfma_f64_16x16x4(a[x], bb[y], acc[x][y]);
+  }
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = I0 + wm * 32 + x * 16 + PFML_F64_CROW(lane, r);
+        const int v = V0 + wn * 32 + y * 16 + (lane & 15);
+        if (i >= n || v >= nlive) continue;
+        double* p = Mb + (int64_t)i * ldm + live_col(v, nA, a_first, b0);
+        if (i >= k0 && i < k0 + nb) *p = Rb[(int64_t)(i - k0) * nlive + v];
+        else *p -= acc[x][y][r];
+      }
+}
+
+}  // namespace
+
+extern "C" int64_t pfml_lu_solve_work_doubles(int n, int m, int batch) {
+  return (int64_t)batch * (NB * NB + (int64_t)NB * (n + m) + (int64_t)n * NB) + 2LL * batch * NB;
+}
+
+// Solve A X = B in place for `batch` augmented systems (see header); X overwrites B.
+extern "C" hipError_t pfml_lu_solve(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
+                                    int b0, int batch, double* work, int* status,
+                                    hipStream_t st) {
+  if (n <= 0 || batch <= 0) return hipSuccess;
+  if (n > PMAX) return hipErrorInvalidValue;
+  double* Pbuf = work;
+  double* Rbuf = Pbuf + (int64_t)batch * NB * NB;
+  double* Cbuf = Rbuf + (int64_t)batch * NB * (n + m);
+  int* piv = reinterpret_cast<int*>(Cbuf + (int64_t)batch * n * NB);
+  for (int k0 = 0; k0 < n; k0 += NB) {
+    const int nb = (n - k0 < NB) ? (n - k0) : NB;
+    hipLaunchKernelGGL(lu_pivot_kernel, dim3(batch), dim3(256), 0, st, M, n, ldm, sM, a0, k0, nb,
+                       piv, status);
+    const int nswap = (n - k0) + m;           // A cols >= k0 and all B cols
+    hipLaunchKernelGGL(lu_swap_kernel, dim3((nswap + 255) / 256, batch), dim3(256), 0, st, M, ldm,
+                       sM, nswap, a0 + k0, n - k0, b0, k0, nb, piv);
+    hipLaunchKernelGGL(lu_blockinv_kernel, dim3(batch), dim3(256), 0, st, M, ldm, sM, a0, k0, nb,
+                       Pbuf);
+    const int nA = n - (k0 + nb);            // live A columns right of the block
+    const int nlive = nA + m;
+    if (nlive > 0) {
+      hipLaunchKernelGGL(lu_rowpanel_kernel, dim3((nlive + 255) / 256, batch), dim3(256), 0, st, M,
+                         ldm, sM, nlive, a0 + k0 + nb, nA, b0, k0, nb, Pbuf, Rbuf);
+      hipLaunchKernelGGL(lu_snapshot_kernel, dim3((n + 255) / 256, batch), dim3(256), 0, st, M, n,
+                         ldm, sM, a0, k0, nb, Cbuf);
+      const int tiles = ((n + 63) / 64) * ((nlive + 63) / 64);
+      hipLaunchKernelGGL(lu_update_kernel, dim3(tiles, batch), dim3(256), 0, st, M, n, ldm, sM,
+                         nlive, a0 + k0 + nb, nA, b0, k0, nb, Rbuf, Cbuf);
+    }
+  }
+  return hipGetLastError();
+}

@@ -257,10 +257,10 @@ def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
             Un = aug(th + 1)
             gemm(Mg1, Ul, beta=1.0, out=Un)
             Ul = Un
-        omega = la.solve(Tc[:, :, GP:], Tc[:, :, :GP])              # [B, N, GP]
-        omega_l1 = la.solve(Ul[:, :, GP:], Ul[:, :, :GP])
+        # omega = const^-1 Omega, solved in place on the augmented [Omega | const] rows
+        omega = la.solve_augmented(Tc, N, GP, a0=GP, b0=0)          # [B, N, GP]
+        omega_l1 = la.solve_augmented(Ul, N, GP, a0=GP, b0=0)
         omega_chg = omega - Dg[:, 0].unsqueeze(-1) * omega_l1
-        del Tc, Ul
 
         # (25): r_tilde, risk, tc
         rt_ = gemm(omega, r.unsqueeze(-1), trans_a=True).squeeze(-1)        # [B, GP]

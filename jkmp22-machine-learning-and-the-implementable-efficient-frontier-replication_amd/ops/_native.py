@@ -43,6 +43,10 @@ def _declare_hip(lib):
     lib.pfml_spd_inverse.restype = I
     lib.pfml_spd_inverse_work_doubles.argtypes = [I, I]
     lib.pfml_spd_inverse_work_doubles.restype = L
+    lib.pfml_lu_solve.argtypes = [P, I, I, L, L, I, I, I, P, P, P]
+    lib.pfml_lu_solve.restype = I
+    lib.pfml_lu_solve_work_doubles.argtypes = [I, I, I]
+    lib.pfml_lu_solve_work_doubles.restype = L
     for name, argt in _EXTRA_HIP.items():
         fn = getattr(lib, name)
         fn.argtypes = argt[0]

@@ -47,18 +47,44 @@ def spd_inverse(A: torch.Tensor, inplace: bool = False) -> torch.Tensor:
     return X.squeeze(0) if squeeze else X
 
 
+def solve_augmented(M: torch.Tensor, n: int, m: int, a0: int, b0: int) -> torch.Tensor:
+    """In-place solve of augmented systems: rows of M [B, n, W] hold A at columns a0..a0+n and
+    B at b0..b0+m; on return the B columns hold X = A^-1 B (returned as a view)."""
+    if nat.is_device(M):
+        if not M.is_contiguous():
+            raise ValueError("solve_augmented: contiguous storage required")
+        Bt, nn, W = M.shape
+        lib = nat.hip_lib()
+        work = torch.empty(lib.pfml_lu_solve_work_doubles(n, m, Bt), dtype=torch.float64,
+                           device=M.device)
+        status = torch.zeros(Bt, dtype=torch.int32, device=M.device)
+        nat.check(lib.pfml_lu_solve(M.data_ptr(), n, m, W, nn * W, a0, b0, Bt, work.data_ptr(),
+                                    status.data_ptr(), nat.stream_of(M)), "pfml_lu_solve")
+        nbad = int(status.sum().item())
+        if nbad:
+            COUNTERS.add("linalg.singular_solve", nbad)
+    else:
+        X, info = torch.linalg.solve_ex(M[:, :, a0:a0 + n], M[:, :, b0:b0 + m])
+        if bool((info != 0).any()):
+            COUNTERS.add("linalg.singular_solve", int((info != 0).sum()))
+        M[:, :, b0:b0 + m] = X
+    return M[:, :, b0:b0 + m]
+
+
 def solve(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
     """Batched general solve A X = B with partial pivoting (np.linalg.solve semantics)."""
-    if nat.is_device(A) and A.dim() == 3 and A.shape[0] > 8:
-        # vendor batched getrf allocates per-batch workspace: bound the batch
-        parts = [torch.linalg.solve_ex(A[i:i + 8], B[i:i + 8]) for i in range(0, A.shape[0], 8)]
-        X = torch.cat([p[0] for p in parts])
-        info = torch.cat([p[1] for p in parts])
-    else:
-        X, info = torch.linalg.solve_ex(A, B)
-    if bool((info != 0).any()):
-        COUNTERS.add("linalg.singular_solve", int((info != 0).sum()))
-    return X
+    squeeze = A.dim() == 2
+    A3 = A.unsqueeze(0) if squeeze else A
+    B3 = B.unsqueeze(0) if squeeze else B
+    vec = B3.dim() == 2
+    if vec:
+        B3 = B3.unsqueeze(-1)
+    n, m = A3.shape[-1], B3.shape[-1]
+    M = torch.cat([B3, A3], dim=-1).contiguous()
+    X = solve_augmented(M, n, m, a0=m, b0=0).clone()
+    if vec:
+        X = X.squeeze(-1)
+    return X.squeeze(0) if squeeze else X
 
 
 def sqrtm_spd(S: torch.Tensor, max_iter: int = 40, tol: float = 1e-13) -> torch.Tensor:

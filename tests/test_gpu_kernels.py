@@ -127,3 +127,15 @@ def test_grid_search_gpu_matches_cpu(gpu):
     assert rb < 1e-9
     ro = ((dev.obj.cpu() - cpu.obj).abs() / cpu.obj.abs().clamp_min(1e-12)).max().item()
     assert ro < 1e-8
+
+
+@pytest.mark.parametrize("n,m,b", [(17, 5, 2), (100, 37, 3), (513, 1026, 2)])
+def test_lu_solve_augmented(gpu, n, m, b):
+    from pfml.ops.linalg import solve
+    A = _rand(b, n, n, seed=n) + n ** 0.5 * torch.eye(n, dtype=torch.float64)
+    A[:, 0, 0] = 1e-8                      # forces a row interchange in the first panel
+    B = _rand(b, n, m, seed=m)
+    ref = torch.linalg.solve(A, B)
+    got = solve(A.to(gpu), B.to(gpu)).cpu()
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < 1e-10, rel
