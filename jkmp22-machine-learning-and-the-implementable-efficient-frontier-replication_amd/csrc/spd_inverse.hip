@@ -212,3 +212,56 @@ extern "C" hipError_t pfml_spd_inverse(double* A, int n, int64_t lda, int64_t sA
   }
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------
+// Large-block variant: the NBL x NBL pivot block (NBL = 128) is inverted in LDS by one
+// 1024-thread workgroup per matrix; the row panel, the rank-NBL trailing update and the
+// column panel are then plain batched GEMMs on pfml_dgemm (host orchestration in
+// ops/linalg.py), so each block step is one MFMA-bound pass over the matrix instead of the
+// four bandwidth-bound passes of the NB = 32 kernels above.
+namespace {
+constexpr int NBL = 128;
+
+__global__ __launch_bounds__(1024) void spd_blockinv_kernel(const double* __restrict__ A,
+                                                            int64_t lda, int64_t sA, int k0,
+                                                            int nb, double* __restrict__ Pout,
+                                                            int* __restrict__ status) {
+  __shared__ double P[NBL][NBL + 1];
+  const int b = blockIdx.x;
+  const double* Ab = A + (int64_t)b * sA + (int64_t)k0 * lda + k0;
+  const int t = threadIdx.x;
+  for (int e = t; e < nb * nb; e += 1024) P[e / nb][e % nb] = Ab[(int64_t)(e / nb) * lda + e % nb];
+  __syncthreads();
+  for (int p = 0; p < nb; ++p) {
+    const double piv = P[p][p];
+    if (t == 0 && (!(piv > 0.0) || !isfinite(piv))) status[b] = 1;
+    const double inv = 1.0 / piv;
+    __syncthreads();
+    for (int e = t; e < nb * nb; e += 1024) {
+      const int i = e / nb, j = e % nb;
+      if (i != p && j != p) P[i][j] -= P[i][p] * P[p][j] * inv;
+    }
+    __syncthreads();
+    if (t < nb && t != p) {
+      P[p][t] *= inv;
+      P[t][p] *= -inv;
+    }
+    if (t == 0) P[p][p] = inv;
+    __syncthreads();
+  }
+  double* Pb = Pout + (int64_t)b * NBL * NBL;
+  for (int e = t; e < nb * nb; e += 1024) Pb[(e / nb) * NBL + e % nb] = P[e / nb][e % nb];
+}
+}  // namespace
+
+extern "C" int pfml_spd_block_size() { return NBL; }
+
+extern "C" hipError_t pfml_spd_blockinv(const double* A, int64_t lda, int64_t sA, int batch,
+                                        int k0, int nb, double* Pout, int* status,
+                                        hipStream_t st) {
+  if (batch <= 0 || nb <= 0) return hipSuccess;
+  if (nb > NBL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(spd_blockinv_kernel, dim3(batch), dim3(1024), 0, st, A, lda, sA, k0, nb, Pout,
+                     status);
+  return hipGetLastError();
+}

@@ -194,9 +194,7 @@ def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
             sig_rows.append(rows_d[bi])
             sig_ids.append(ids)
         idx_t = torch.as_tensor(idx, device=dev)
-        mask = torch.zeros((B, N), dtype=torch.float64, device=dev)
-        for bi, n in enumerate(ns):
-            mask[bi, :n] = 1.0
+        mask = torch.as_tensor((np.arange(N)[None, :] < ns[:, None]).astype(np.float64), device=dev)
         wv = torch.as_tensor([wmap[int(d)] for d in bm], dtype=torch.float64, device=dev)
         rfv = torch.as_tensor([rfmap[int(d)] for d in bm], dtype=torch.float64, device=dev)
 
@@ -209,11 +207,11 @@ def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
             S_all.append(standardize_signals(rffs[g], idx_t, mask, vol_t))
         # Barra Sigma (padded: identity block), Lambda, returns
         K = barra.X.shape[1]
-        Xl = torch.zeros((B, N, K), dtype=torch.float64, device=dev)
-        Fb = torch.zeros((B, K, K), dtype=torch.float64, device=dev)
-        iv = torch.ones((B, N), dtype=torch.float64, device=dev)
-        lam = torch.empty((B, N), dtype=torch.float64, device=dev)
-        r = torch.zeros((B, N), dtype=torch.float64, device=dev)
+        Xl_h = np.zeros((B, N, K))
+        Fb_h = np.zeros((B, K, K))
+        iv_h = np.ones((B, N))
+        lam_h = np.empty((B, N))
+        r_h = np.zeros((B, N))
         for bi, d in enumerate(bm):
             ids = sig_ids[b0 + bi]
             bids, X, F, ivol = barra.slice(int(d))
@@ -221,13 +219,17 @@ def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
             if np.any(pos >= len(bids)) or np.any(bids[np.minimum(pos, len(bids) - 1)] != ids):
                 raise KeyError(f"month {d}: valid ids missing from the Barra universe")
             n = len(ids)
-            Xl[bi, :n] = torch.as_tensor(X[pos], device=dev)
-            Fb[bi] = torch.as_tensor(F, device=dev)
-            iv[bi, :n] = torch.as_tensor(ivol[pos], device=dev)
-            lam[bi] = gamma / float(wmap[int(d)])
-            lam_d = panel.cols["lambda"][rows_d[bi]] if tc_on else np.full(n, 1e-16)
-            lam[bi, :n] = torch.as_tensor(lam_d, device=dev)
-            r[bi, :n] = torch.as_tensor(panel.cols["ret_ld1"][rows_d[bi]], device=dev)
+            Xl_h[bi, :n] = X[pos]
+            Fb_h[bi] = F
+            iv_h[bi, :n] = ivol[pos]
+            lam_h[bi] = gamma / float(wmap[int(d)])
+            lam_h[bi, :n] = panel.cols["lambda"][rows_d[bi]] if tc_on else 1e-16
+            r_h[bi, :n] = panel.cols["ret_ld1"][rows_d[bi]]
+        Xl = torch.as_tensor(Xl_h, device=dev)
+        Fb = torch.as_tensor(Fb_h, device=dev)
+        iv = torch.as_tensor(iv_h, device=dev)
+        lam = torch.as_tensor(lam_h, device=dev)
+        r = torch.as_tensor(r_h, device=dev)
         XF = gemm(Xl, Fb)
         Sigma = gemm(XF, Xl, trans_b=True)
         Sigma.diagonal(dim1=1, dim2=2).add_(iv)

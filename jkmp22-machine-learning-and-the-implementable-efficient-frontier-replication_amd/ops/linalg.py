@@ -32,11 +32,15 @@ def spd_inverse(A: torch.Tensor, inplace: bool = False) -> torch.Tensor:
         X = X.contiguous() if not X.is_contiguous() else X
         B, n, _ = X.shape
         lib = nat.hip_lib()
-        work = torch.empty(lib.pfml_spd_inverse_work_doubles(n, B), dtype=torch.float64,
-                           device=X.device)
         status = torch.zeros(B, dtype=torch.int32, device=X.device)
-        nat.check(lib.pfml_spd_inverse(X.data_ptr(), n, n, n * n, B, work.data_ptr(),
-                                       status.data_ptr(), nat.stream_of(X)), "pfml_spd_inverse")
+        if n >= _BLOCKED_MIN_N:
+            _spd_inverse_blocked(X, status)
+        else:
+            work = torch.empty(lib.pfml_spd_inverse_work_doubles(n, B), dtype=torch.float64,
+                               device=X.device)
+            nat.check(lib.pfml_spd_inverse(X.data_ptr(), n, n, n * n, B, work.data_ptr(),
+                                           status.data_ptr(), nat.stream_of(X)),
+                      "pfml_spd_inverse")
         bad = torch.nonzero(status).flatten()
         if bad.numel():
             COUNTERS.add("linalg.spd_inverse_lu_fallback", int(bad.numel()))
@@ -45,6 +49,36 @@ def spd_inverse(A: torch.Tensor, inplace: bool = False) -> torch.Tensor:
     else:
         X.copy_(torch.linalg.inv(X))
     return X.squeeze(0) if squeeze else X
+
+
+_BLOCKED_MIN_N = 160
+
+
+def _spd_inverse_blocked(X: torch.Tensor, status: torch.Tensor) -> None:
+    """In-place SPD inverse with 128-wide Gauss-Jordan blocks: pivot block inverted in LDS
+    (csrc/spd_inverse.hip: pfml_spd_blockinv); row panel, rank-128 trailing update and column
+    panel as batched fp64 MFMA GEMMs."""
+    lib = nat.hip_lib()
+    B, n, _ = X.shape
+    NB = lib.pfml_spd_block_size()
+    dev = X.device
+    P = torch.empty((B, NB, NB), dtype=torch.float64, device=dev)
+    Cbuf = torch.empty((B, n, NB), dtype=torch.float64, device=dev)
+    Rbuf = torch.empty((B, NB, n), dtype=torch.float64, device=dev)
+    st = nat.stream_of(X)
+    for k0 in range(0, n, NB):
+        nb = min(NB, n - k0)
+        nat.check(lib.pfml_spd_blockinv(X.data_ptr(), n, n * n, B, k0, nb, P.data_ptr(),
+                                        status.data_ptr(), st), "pfml_spd_blockinv")
+        Pk = P[:, :nb, :nb]
+        R = Rbuf[:, :nb, :]
+        gemm(Pk, X[:, k0:k0 + nb, :], out=R)                     # R = P A_k.
+        C = Cbuf[:, :, :nb]
+        C.copy_(X[:, :, k0:k0 + nb])                             # old column panel
+        gemm(C, R, alpha=-1.0, beta=1.0, out=X)                  # A -= C R   (rank nb)
+        X[:, k0:k0 + nb, :] = R                                  # block rows
+        gemm(C, Pk, alpha=-1.0, out=X[:, :, k0:k0 + nb])         # block columns: -C P
+        X[:, k0:k0 + nb, k0:k0 + nb] = Pk
 
 
 def solve_augmented(M: torch.Tensor, n: int, m: int, a0: int, b0: int) -> torch.Tensor:

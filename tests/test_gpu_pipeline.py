@@ -14,7 +14,7 @@ def _rand(*shape, seed=0):
     return torch.randn(*shape, generator=g, dtype=torch.float64)
 
 
-@pytest.mark.parametrize("n,b", [(17, 3), (64, 2), (100, 4), (513, 2)])
+@pytest.mark.parametrize("n,b", [(17, 3), (64, 2), (100, 4), (200, 3), (513, 2)])
 def test_spd_inverse(gpu, n, b):
     from pfml.ops.linalg import spd_inverse
     X = _rand(b, n + 10, n, seed=n)
