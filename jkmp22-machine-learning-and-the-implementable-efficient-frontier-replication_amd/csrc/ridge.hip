@@ -25,6 +25,7 @@
 //   part), rows strided over parts), reflectors are staged through a 3-deep LDS ring, one
 //   barrier per reflector.
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -203,6 +204,222 @@ __global__ __launch_bounds__(NT) void ridge_tridiag_kernel(
   double* eg = dg + n;
   double* tg = eg + n;
   double* zg = tg + n;
+  for (int i = t; i < n; i += NT) { dg[i] = dd[i]; eg[i] = ee[i]; tg[i] = tau[i]; zg[i] = z[i]; }
+}
+
+// Phase A, blocked variant (LAPACK dlatrd structure, panels of PB reflectors).  Within a panel
+// the sweeps are READ-ONLY against the panel-start matrix A0, corrected on the fly by the
+// panel's reflectors V and update vectors W:
+//     column k   c = A0[:, k] - V W[k, :]' - W V[k, :]'
+//     mat-vec    p = A0 v - V (W' v) - W (V' v)
+// and the trailing matrix gets ONE read+write rank-2PB update per panel, so the bytes moved
+// per reflector drop from 16 m^2 (fused read+write sweep) to ~8 m^2 (1 + 2/PB).  The sweep
+// keeps 16 rows of loads in flight per lane.  V and W are stored interleaved per row
+// (VW[i][0..PB) = V, VW[i][PB..2PB) = W) so correction dots are coalesced.
+constexpr int PB = 16;
+
+__global__ __launch_bounds__(NT) void ridge_tridiag_blocked_kernel(
+    const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
+    const CellDesc* __restrict__ cells, int L, double* __restrict__ work) {
+  __shared__ double v[NMAX], pk[NMAX], z[NMAX];
+  __shared__ double dd[NMAX], ee[NMAX], tau[NMAX];
+  __shared__ double part[NT];
+  __shared__ double red[NW * 2];
+  __shared__ double red32[32][33];
+  __shared__ double xy[2 * PB], vwk[2 * PB];
+
+  const CellDesc cd = cells[blockIdx.x];
+  const int n = cd.n;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  double* A = work + cd.work;
+  double* Y = A + (int64_t)n * n;
+  double* Uy = Y + 4LL * n * L;
+  double* dg = Uy + (int64_t)n * L;
+  double* eg = dg + n;
+  double* tg = eg + n;
+  double* zg = tg + n;
+  double* VW = zg + n;                         // [n][2*PB]
+  const double* S = SD + cd.src;
+  const double sc = cd.scale;
+
+  for (int i = wid; i < n; i += NW) {
+    const double* srow = S + (int64_t)i * ldS;
+    double* arow = A + (int64_t)i * n;
+    for (int j = lane; j < n; j += 64) arow[j] = srow[j] * sc;
+  }
+  for (int i = t; i < n; i += NT) z[i] = Sr[cd.rsrc + i] * sc;
+  __syncthreads();
+
+  auto bsum2 = [&](double a, double b, double& ra, double& rb) {
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (lane == 0) { red[wid] = a; red[NW + wid] = b; }
+    __syncthreads();
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) { sa += red[q]; sb += red[NW + q]; }
+    ra = sa;
+    rb = sb;
+    __syncthreads();
+  };
+
+  const int kend = n - 2;                      // reflectors k = 0 .. n-3
+  for (int k0 = 0; k0 < kend; k0 += PB) {
+    const int nbp = min(PB, kend - k0);
+    for (int j = 0; j < nbp; ++j) {
+      const int k = k0 + j;
+      // (1) column k of the current matrix (row k of symmetric A0, panel-corrected)
+      if (t < 2 * PB) vwk[t] = (t % PB < j) ? VW[(int64_t)k * 2 * PB + t] : 0.0;
+      __syncthreads();
+      const double* rowk = A + (int64_t)k * n;
+      for (int i = k + t; i < n; i += NT) {
+        double c = rowk[i];
+        const double* vw = VW + (int64_t)i * 2 * PB;
+        for (int q = 0; q < j; ++q) c -= vw[q] * vwk[PB + q] + vw[PB + q] * vwk[q];
+        pk[i] = c;
+      }
+      __syncthreads();
+      // (2) Householder vector
+      double x2 = 0.0;
+      for (int i = k + 2 + t; i < n; i += NT) x2 += pk[i] * pk[i];
+      double xnorm2, dummy;
+      bsum2(x2, 0.0, xnorm2, dummy);
+      const double alpha = pk[k + 1];
+      double tk, ek, scal;
+      if (xnorm2 == 0.0) {
+        tk = 0.0; ek = alpha; scal = 0.0;
+      } else {
+        const double bet = -copysign(sqrt(alpha * alpha + xnorm2), alpha);
+        tk = (bet - alpha) / bet;
+        scal = 1.0 / (alpha - bet);
+        ek = bet;
+      }
+      if (t == 0) { dd[k] = pk[k]; ee[k] = ek; tau[k] = tk; }
+      double* rowk_w = A + (int64_t)k * n;
+      for (int i = k + 1 + t; i < n; i += NT) {
+        const double vi = (i == k + 1) ? 1.0 : pk[i] * scal;
+        v[i] = vi;
+        rowk_w[i] = vi;
+        VW[(int64_t)i * 2 * PB + j] = vi;
+      }
+      __syncthreads();
+      // (3) read-only column-oriented sweep  p_i = sum_l A0[l][i] v_l  (l, i >= k+1)
+      //     + correction dots  V'v, W'v  (q < j)
+      const int r0 = k + 1, m = n - r0;
+      const int ncb = (m + 63) >> 6;
+      const int nrg = NW / ncb;
+      {
+        const int cb = wid % ncb, rg = wid / ncb;
+        if (rg < nrg) {
+          const int c = cb * 64 + lane;
+          const int i = r0 + c;
+          const int rows_per = (m + nrg - 1) / nrg;
+          const int j0 = r0 + rg * rows_per;
+          const int j1 = min(n, j0 + rows_per);
+          double acc0 = 0.0, acc1 = 0.0;
+          if (i < n) {
+            const double* col = A + i;
+            int l = j0;
+            for (; l + 16 <= j1; l += 16) {
+              double a[16];
+#pragma unroll
+              for (int u = 0; u < 16; ++u) a[u] = col[(int64_t)(l + u) * n];
+#pragma unroll
+              for (int u = 0; u < 16; u += 2) {
+                acc0 += a[u] * v[l + u];
+                acc1 += a[u + 1] * v[l + u + 1];
+              }
+            }
+            for (; l < j1; ++l) acc0 += col[(int64_t)l * n] * v[l];
+          }
+          part[rg * (ncb * 64) + c] = acc0 + acc1;
+        }
+      }
+      {
+        const int q = t & 31, pr = t >> 5;      // 32 partitions of rows
+        double s = 0.0;
+        if ((q & (PB - 1)) < j)
+          for (int i = r0 + pr; i < n; i += 32) s += VW[(int64_t)i * 2 * PB + q] * v[i];
+        red32[pr][q] = s;
+      }
+      __syncthreads();
+      if (t < 2 * PB) {
+        double s = 0.0;
+#pragma unroll 8
+        for (int pr = 0; pr < 32; ++pr) s += red32[pr][t];
+        xy[t] = s;                               // xy[0..PB) = V'v, xy[PB..2PB) = W'v
+      }
+      __syncthreads();
+      // (4) p = tau (A0 v - V (W'v) - W (V'v)),  w = p - (tau/2)(p.v) v,  z <- H_k z
+      double pv = 0.0, vz = 0.0;
+      for (int c = t; c < m; c += NT) {
+        double s = 0.0;
+        for (int qq = 0; qq < nrg; ++qq) s += part[qq * (ncb * 64) + c];
+        const int i = r0 + c;
+        const double* vw = VW + (int64_t)i * 2 * PB;
+        for (int q = 0; q < j; ++q) s -= vw[q] * xy[PB + q] + vw[PB + q] * xy[q];
+        s *= tk;
+        pk[i] = s;
+        pv += s * v[i];
+        vz += v[i] * z[i];
+      }
+      double spv, svz;
+      bsum2(pv, vz, spv, svz);
+      const double half = 0.5 * tk * spv;
+      for (int i = r0 + t; i < n; i += NT) {
+        VW[(int64_t)i * 2 * PB + PB + j] = pk[i] - half * v[i];
+        z[i] -= tk * svz * v[i];
+      }
+      __syncthreads();
+    }
+    // (5) rank-2*nbp update of the trailing matrix (rows, cols >= k0 + nbp) on fp64 MFMA:
+    //     A_T -= U Z'  with  U = [V | W],  Z = [W | V]  (m x 2PB), one 16 x 16 tile per step
+    //     of a wave; the tile is loaded straight into the accumulator layout.
+    const int r0 = k0 + nbp, m = n - r0;
+    if (m > 0) {
+      const int nt = (m + 15) >> 4;
+      const int g4 = lane >> 4, c16 = lane & 15;
+      for (int tile = wid; tile < nt * nt; tile += NW) {
+        const int i0 = r0 + (tile / nt) * 16, j0 = r0 + (tile % nt) * 16;
+        double4_t acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + PFML_F64_CROW(lane, r), jj = j0 + c16;
+          acc[r] = (i < n && jj < n) ? A[(int64_t)i * n + jj] : 0.0;
+        }
+        const int ia = i0 + c16;                 // A-operand row (U), B-operand col (Z)
+        const int jb = j0 + c16;
+#pragma unroll
+        for (int q0 = 0; q0 < 2 * PB; q0 += 4) {
+          const int q = q0 + g4;                 // k index of this lane
+          const int qq = q & (PB - 1);
+          double ua = 0.0, zb = 0.0;
+          if (qq < nbp) {
+            if (ia < n) ua = -VW[(int64_t)ia * 2 * PB + q];                       // -U[i][q]
+            if (jb < n) zb = VW[(int64_t)jb * 2 * PB + (q < PB ? PB + q : q - PB)];  // Z[j][q]
+          }
+          acc = mfma_f64_16x16x4(ua, zb, acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + PFML_F64_CROW(lane, r), jj = j0 + c16;
+          if (i < n && jj < n) A[(int64_t)i * n + jj] = acc[r];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    if (n >= 2) {
+      dd[n - 2] = A[(int64_t)(n - 2) * n + n - 2];
+      ee[n - 2] = A[(int64_t)(n - 1) * n + n - 2];
+      dd[n - 1] = A[(int64_t)(n - 1) * n + n - 1];
+    } else {
+      dd[0] = A[0];
+    }
+  }
+  __syncthreads();
   for (int i = t; i < n; i += NT) { dg[i] = dd[i]; eg[i] = ee[i]; tg[i] = tau[i]; zg[i] = z[i]; }
 }
 
@@ -407,7 +624,7 @@ __global__ __launch_bounds__(NT) void ridge_backtransform_kernel(
 }  // namespace
 
 extern "C" int64_t pfml_ridge_work_doubles(int n, int L) {
-  return (int64_t)n * n + 5LL * n * L + 4LL * n;
+  return (int64_t)n * n + 5LL * n * L + 4LL * n + 32LL * n;
 }
 
 extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const double* Sr,
@@ -417,8 +634,12 @@ extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const doubl
   if (ncells <= 0) return hipSuccess;
   if (L > 128) return hipErrorInvalidValue;
   const CellDesc* cd = static_cast<const CellDesc*>(cells);
-  hipLaunchKernelGGL(ridge_tridiag_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr, cd, L,
-                     work);
+  if (getenv("PFML_RIDGE_UNBLOCKED"))
+    hipLaunchKernelGGL(ridge_tridiag_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr, cd, L,
+                       work);
+  else
+    hipLaunchKernelGGL(ridge_tridiag_blocked_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr,
+                       cd, L, work);
   const int64_t nth = (int64_t)ncells * L;
   hipLaunchKernelGGL(ridge_trisolve_kernel, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0,
                      st, cd, ncells, lvec, L, work);

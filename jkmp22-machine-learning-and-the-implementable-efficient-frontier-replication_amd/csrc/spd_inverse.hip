@@ -220,9 +220,9 @@ extern "C" hipError_t pfml_spd_inverse(double* A, int n, int64_t lda, int64_t sA
 // ops/linalg.py), so each block step is one MFMA-bound pass over the matrix instead of the
 // four bandwidth-bound passes of the NB = 32 kernels above.
 namespace {
-constexpr int NBL = 128;
+constexpr int NBL = 64;
 
-__global__ __launch_bounds__(1024) void spd_blockinv_kernel(const double* __restrict__ A,
+__global__ __launch_bounds__(256) void spd_blockinv_kernel(const double* __restrict__ A,
                                                             int64_t lda, int64_t sA, int k0,
                                                             int nb, double* __restrict__ Pout,
                                                             int* __restrict__ status) {
@@ -230,14 +230,14 @@ __global__ __launch_bounds__(1024) void spd_blockinv_kernel(const double* __rest
   const int b = blockIdx.x;
   const double* Ab = A + (int64_t)b * sA + (int64_t)k0 * lda + k0;
   const int t = threadIdx.x;
-  for (int e = t; e < nb * nb; e += 1024) P[e / nb][e % nb] = Ab[(int64_t)(e / nb) * lda + e % nb];
+  for (int e = t; e < nb * nb; e += 256) P[e / nb][e % nb] = Ab[(int64_t)(e / nb) * lda + e % nb];
   __syncthreads();
   for (int p = 0; p < nb; ++p) {
     const double piv = P[p][p];
     if (t == 0 && (!(piv > 0.0) || !isfinite(piv))) status[b] = 1;
     const double inv = 1.0 / piv;
     __syncthreads();
-    for (int e = t; e < nb * nb; e += 1024) {
+    for (int e = t; e < nb * nb; e += 256) {
       const int i = e / nb, j = e % nb;
       if (i != p && j != p) P[i][j] -= P[i][p] * P[p][j] * inv;
     }
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(1024) void spd_blockinv_kernel(const double* __rest
     __syncthreads();
   }
   double* Pb = Pout + (int64_t)b * NBL * NBL;
-  for (int e = t; e < nb * nb; e += 1024) Pb[(e / nb) * NBL + e % nb] = P[e / nb][e % nb];
+  for (int e = t; e < nb * nb; e += 256) Pb[(e / nb) * NBL + e % nb] = P[e / nb][e % nb];
 }
 }  // namespace
 
@@ -261,7 +261,7 @@ extern "C" hipError_t pfml_spd_blockinv(const double* A, int64_t lda, int64_t sA
                                         hipStream_t st) {
   if (batch <= 0 || nb <= 0) return hipSuccess;
   if (nb > NBL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(spd_blockinv_kernel, dim3(batch), dim3(1024), 0, st, A, lda, sA, k0, nb, Pout,
+  hipLaunchKernelGGL(spd_blockinv_kernel, dim3(batch), dim3(256), 0, st, A, lda, sA, k0, nb, Pout,
                      status);
   return hipGetLastError();
 }
