@@ -82,8 +82,7 @@ class Pipeline:
             if st not in ALL_STAGES:
                 raise ValueError(f"unknown stage {st!r}; choose from {ALL_STAGES}")
         for st in stages:
-            if self.checkpoint and self.store.is_done(st, self._keys[st]) and \
-                    not self._needs_memory(st, stages):
+            if self.checkpoint and self.store.is_done(st, self._keys[st]):
                 log.info(f"[{st}] up to date (resume)")
                 continue
             t0 = time.time()
@@ -96,10 +95,6 @@ class Pipeline:
                    world_size=self.env.world_size, fallbacks=COUNTERS.as_dict())
             log.info(f"[{st}] done in {time.time() - t0:.2f}s")
         return self.state
-
-    def _needs_memory(self, st: str, stages: list[str]) -> bool:
-        # a skipped in-memory stage must still be reloadable by its successors
-        return False
 
     # ---------------------------------------------------------------------------------
     def _get_additional_data(self):
@@ -144,6 +139,7 @@ class Pipeline:
         months = m2[mine]
         res = pin.build_inputs(self.cfg, st["chars"], st["barra"], st["wealth"],
                                st["risk_free"], self.device, months=months)
+        self._guard_inputs(res, months)
         R = res.reals
         G = R.G
         if self.env.is_dist:
@@ -167,16 +163,57 @@ class Pipeline:
         st["signal_t"], st["signal_ids"], st["signal_months"] = signal_t, ids, m2
         st["rff_w"] = res.rff_w
         if self.checkpoint and self.env.is_main:
-            self.store.save_tensors("pfml-input", "reals",
-                                    {"months": torch.as_tensor(R.months), "r_tilde": R.r_tilde,
-                                     "denom": R.denom})
+            payload = {"months": torch.as_tensor(R.months), "r_tilde": R.r_tilde,
+                       "denom": R.denom, "rff_w": torch.as_tensor(res.rff_w),
+                       "counts": torch.as_tensor([len(x) for x in ids]),
+                       "ids": torch.as_tensor(np.concatenate(ids))}
+            for g in range(G):
+                payload[f"sig{g}"] = torch.cat(signal_t[g])
+            self.store.save_tensors("pfml-input", "reals", payload)
+
+    def _guard_inputs(self, res, months) -> None:
+        """Failure detection: months whose summands are not finite are recomputed
+        (once on the device, then on the fp64 CPU oracle).  ``run.fault_inject =
+        "pfml-input"`` poisons the first month of every shard to exercise this path."""
+        R = res.reals
+        if self.cfg.run.fault_inject.startswith("pfml-input") and len(months):
+            R.denom[:, 0, 0, 0] = float("nan")
+            COUNTERS.add("fault_injected")
+        bad = ~(torch.isfinite(R.denom).flatten(2).all(-1) & torch.isfinite(R.r_tilde).all(-1))
+        bad_t = torch.nonzero(bad.any(0)).flatten().cpu().numpy()
+        if len(bad_t) == 0:
+            return
+        st = self.state
+        log.warning(f"non-finite PFML inputs in {len(bad_t)} month(s): recomputing")
+        COUNTERS.add("pfml_input.recomputed_months", len(bad_t))
+        for dev in (self.device, torch.device("cpu")):
+            redo = pin.build_inputs(self.cfg, st["chars"], st["barra"], st["wealth"],
+                                    st["risk_free"], dev, months=months[bad_t])
+            ok = (torch.isfinite(redo.reals.denom).flatten(2).all(-1).all(0) &
+                  torch.isfinite(redo.reals.r_tilde).all(-1).all(0))
+            if bool(ok.all()):
+                idx = torch.as_tensor(bad_t, device=R.denom.device)
+                R.denom[:, idx] = redo.reals.denom.to(R.denom.device)
+                R.r_tilde[:, idx] = redo.reals.r_tilde.to(R.r_tilde.device)
+                return
+        raise FloatingPointError(f"PFML inputs stay non-finite for months {months[bad_t]}")
 
     def _ensure_reals(self):
         if "reals" not in self.state:
             self._load_common()
             t = self.store.load_tensors("pfml-input", "reals", device=self.device)
-            self.state["reals"] = search.PfmlReals(months=t["months"].numpy(),
-                                                   r_tilde=t["r_tilde"], denom=t["denom"])
+            st = self.state
+            st["reals"] = search.PfmlReals(months=t["months"].numpy(),
+                                           r_tilde=t["r_tilde"], denom=t["denom"])
+            counts = t["counts"].numpy()
+            offs = np.concatenate([[0], np.cumsum(counts)])
+            ids = t["ids"].numpy()
+            G = st["reals"].G
+            st["signal_t"] = [[t[f"sig{g}"][offs[i]:offs[i + 1]] for i in range(len(counts))]
+                              for g in range(G)]
+            st["signal_ids"] = [ids[offs[i]:offs[i + 1]] for i in range(len(counts))]
+            st["signal_months"] = st["reals"].months
+            st["rff_w"] = t["rff_w"].numpy()
 
     def _pfml_search_coef(self):
         self._ensure_reals()
@@ -189,7 +226,7 @@ class Pipeline:
                                      "obj": grid.obj, "val_months": torch.as_tensor(grid.val_months),
                                      "val_year": torch.as_tensor(grid.val_year)})
 
-    def _pfml_hp_reals(self):
+    def _pfml_hp_reals_load(self):
         if "grid" not in self.state:
             t = self.store.load_tensors("pfml-search-coef", "coef", device=self.device)
             self.state["beta_years"], self.state["beta"] = t["years"].numpy(), t["beta"]
@@ -197,6 +234,9 @@ class Pipeline:
                 years=self.cfg.hp_years, p_vec=self.cfg.p_vec, l_vec=self.cfg.l_vec,
                 years_local=t["years"].numpy(), beta=t["beta"], val_months=t["val_months"].numpy(),
                 val_year=t["val_year"].numpy(), obj=t["obj"])
+
+    def _pfml_hp_reals(self):
+        self._pfml_hp_reals_load()
         if self.env.is_main:
             val = search.validation_frame(self.state["grid"], self.cfg)
             io.write_csv(val, self.cfg.run.data_dir, "validation.csv")
@@ -214,21 +254,41 @@ class Pipeline:
         st = self.state
         self._load_common()
         if "signal_t" not in st:
-            raise RuntimeError("pfml-aim needs the in-memory signals of pfml-input "
-                               "(run pfml-input in the same invocation)")
+            self._ensure_reals()
+        if "beta" not in st:
+            self._pfml_hp_reals_load()
         st["aims"] = portfolio.aim_portfolios(self.cfg, self._validation(), st["beta_years"],
                                               st["beta"], st["signal_months"], st["signal_t"],
                                               st["signal_ids"], st["grids"]["oos"])
         if self.checkpoint:
-            rows = []
+            rows, coefs = [], {}
             for g, per in st["aims"].items():
                 for d, a in per.items():
-                    rows.append(a["aim_pf"].assign(g=g, p=a["p"], l=a["l"]))
+                    rows.append(a["aim_pf"].assign(g=g, mi=d, p=a["p"], l=a["l"]))
+                    coefs[f"c{g}_{d}"] = torch.as_tensor(a["coef"])
             pd.concat(rows).to_csv(self.store.path("pfml-aim", "aims.csv"), index=False)
+            self.store.save_tensors("pfml-aim", "coef", coefs)
+
+    def _load_aims(self):
+        if "aims" in self.state:
+            return
+        df = pd.read_csv(self.store.path("pfml-aim", "aims.csv"), parse_dates=["eom"])
+        coefs = self.store.load_tensors("pfml-aim", "coef")
+        aims = {}
+        for (g, d), sub in df.groupby(["g", "mi"], sort=True):
+            aims.setdefault(int(g), {})[int(d)] = {
+                "aim_pf": sub[["id", "eom", "w_aim"]].reset_index(drop=True),
+                "coef": coefs[f"c{g}_{d}"].numpy(), "p": int(sub["p"].iloc[0]),
+                "l": int(sub["l"].iloc[0])}
+        self.state["aims"] = aims
+        if "rff_w" not in self.state:
+            t = self.store.load_tensors("pfml-input", "reals")
+            self.state["rff_w"] = t["rff_w"].numpy()
 
     def _pfml_hps(self):
         if not self.env.is_main:
             return
+        self._load_aims()
         self.state["hps"] = portfolio.hps_bundle(self.state["aims"], self._validation(),
                                                  self.state["rff_w"])
         if self.checkpoint:
@@ -240,6 +300,8 @@ class Pipeline:
         st = self.state
         self._load_common()
         oos = st["grids"]["oos"]
+        if "hps" not in st:
+            self._pfml_hps()
         best, chosen, aims = portfolio.best_hps(st["hps"], oos)
         w = portfolio.pfml_weights(self.cfg, st["chars"], st["barra"], st["wealth"],
                                    st["risk_free"], aims, oos, self.device)

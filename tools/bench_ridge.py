@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Micro-benchmark of the ridge-grid kernels: wall time vs number of concurrent cells.
+
+Distinguishes a per-reflector latency bound (time flat in #cells) from a memory-system bound
+(time grows once the cells' working sets exceed L2 / Infinity Cache)."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from pfml.ops.ridge import ridge_grid  # noqa: E402
+
+
+def run(ncells, n, reps=3):
+    dev = torch.device("cuda", 0)
+    P = 513
+    S = max(1, ncells // 4)
+    X = torch.randn(S, 600, P, dtype=torch.float64, device=dev)
+    SD = X.transpose(1, 2) @ X
+    Sr = torch.randn(S, P, dtype=torch.float64, device=dev)
+    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64,
+                      device=dev)
+    src = np.arange(ncells) % S
+    nn = np.full(ncells, n)
+    sc = np.full(ncells, 1e-3)
+    ridge_grid(SD, Sr, src, nn, sc, lv)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        ridge_grid(SD, Sr, src, nn, sc, lv)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / reps * 1e3
+
+
+if __name__ == "__main__":
+    out = {}
+    for n in (513, 257):
+        for nc in (1, 8, 32, 106, 212):
+            out[f"n{n}_cells{nc}_ms"] = round(run(nc, n), 3)
+            print(n, nc, out[f"n{n}_cells{nc}_ms"], flush=True)
+    print(json.dumps(out))
