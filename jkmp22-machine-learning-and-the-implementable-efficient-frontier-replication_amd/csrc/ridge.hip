@@ -423,6 +423,262 @@ __global__ __launch_bounds__(NT) void ridge_tridiag_blocked_kernel(
   for (int i = t; i < n; i += NT) { dg[i] = dd[i]; eg[i] = ee[i]; tg[i] = tau[i]; zg[i] = z[i]; }
 }
 
+// Phase A, fast path for n <= NV (p_max <= 512): same blocked algorithm with PF = 8
+// reflectors per panel and EVERYTHING except A itself in LDS (V/W panel, vectors), so the
+// only global round trips per reflector are the sweep itself and one row of A0 (prefetched a
+// step ahead inside a panel).  The read-only sweep is software-pipelined: the next 16 rows of
+// the lane's column are in flight while the current 16 are consumed.
+constexpr int NV = 513;       // fast path: n <= 513 keeps every sweep within 8 column blocks
+constexpr int PF = 8;
+constexpr int SW = 16;         // sweep rows per load batch (two batches in flight)
+constexpr int NTF = 512;       // fast path: 8 waves, up to 256 VGPRs per lane
+constexpr int NWF = NTF / 64;
+
+__global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
+    const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
+    const CellDesc* __restrict__ cells, int L, double* __restrict__ work) {
+  __shared__ double VWs[NV][2 * PF + 1];
+  __shared__ double v[NV], pk[NV], z[NV], dd[NV], ee[NV], tau[NV];
+  __shared__ double part[NTF];
+  __shared__ double red[NWF * 2];
+  __shared__ double red32[NTF / 16][2 * PF + 1];
+  __shared__ double xy[2 * PF], vwk[2 * PF];
+
+  const CellDesc cd = cells[blockIdx.x];
+  const int n = cd.n;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  double* A = work + cd.work;
+  double* Y = A + (int64_t)n * n;
+  double* Uy = Y + 4LL * n * L;
+  double* dg = Uy + (int64_t)n * L;
+  double* eg = dg + n;
+  double* tg = eg + n;
+  double* zg = tg + n;
+  const double* S = SD + cd.src;
+  const double sc = cd.scale;
+
+  for (int i = wid; i < n; i += NWF) {
+    const double* srow = S + (int64_t)i * ldS;
+    double* arow = A + (int64_t)i * n;
+    for (int j = lane; j < n; j += 64) arow[j] = srow[j] * sc;
+  }
+  for (int i = t; i < n; i += NTF) z[i] = Sr[cd.rsrc + i] * sc;
+  __syncthreads();
+
+  auto bsum2 = [&](double a, double b, double& ra, double& rb) {
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (lane == 0) { red[wid] = a; red[NWF + wid] = b; }
+    __syncthreads();
+    double sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int q = 0; q < NWF; ++q) { sa += red[q]; sb += red[NWF + q]; }
+    ra = sa;
+    rb = sb;
+    __syncthreads();
+  };
+
+  const int kend = n - 2;
+  for (int k0 = 0; k0 < kend; k0 += PF) {
+    const int nbp = min(PF, kend - k0);
+    constexpr int RP = (NV + NTF - 1) / NTF;     // row elements per thread
+    double rcur[RP];                              // row k0 of A0, i = k0 + t + h*NTF
+#pragma unroll
+    for (int h = 0; h < RP; ++h) {
+      const int i = k0 + t + h * NTF;
+      rcur[h] = (i < n) ? A[(int64_t)k0 * n + i] : 0.0;
+    }
+    for (int j = 0; j < nbp; ++j) {
+      const int k = k0 + j;
+      // prefetch row k+1 of A0 (unchanged inside the panel) for the next step
+      double rnext[RP];
+#pragma unroll
+      for (int h = 0; h < RP; ++h) {
+        const int i = k + 1 + t + h * NTF;
+        rnext[h] = (j + 1 < nbp && i < n) ? A[(int64_t)(k + 1) * n + i] : 0.0;
+      }
+      // (1) column k, panel-corrected
+      if (t < 2 * PF) vwk[t] = (t % PF < j) ? VWs[k][t] : 0.0;
+      __syncthreads();
+#pragma unroll
+      for (int h = 0; h < RP; ++h) {
+        const int i = k + t + h * NTF;
+        if (i < n) {
+          double c = rcur[h];
+          for (int q = 0; q < j; ++q) c -= VWs[i][q] * vwk[PF + q] + VWs[i][PF + q] * vwk[q];
+          pk[i] = c;
+        }
+      }
+      __syncthreads();
+      // (2) Householder vector
+      double x2 = 0.0;
+      for (int i = k + 2 + t; i < n; i += NTF) x2 += pk[i] * pk[i];
+      double xnorm2, dummy;
+      bsum2(x2, 0.0, xnorm2, dummy);
+      const double alpha = pk[k + 1];
+      double tk, ek, scal;
+      if (xnorm2 == 0.0) {
+        tk = 0.0; ek = alpha; scal = 0.0;
+      } else {
+        const double bet = -copysign(sqrt(alpha * alpha + xnorm2), alpha);
+        tk = (bet - alpha) / bet;
+        scal = 1.0 / (alpha - bet);
+        ek = bet;
+      }
+      if (t == 0) { dd[k] = pk[k]; ee[k] = ek; tau[k] = tk; }
+      for (int i = k + 1 + t; i < n; i += NTF) {
+        const double vi = (i == k + 1) ? 1.0 : pk[i] * scal;
+        v[i] = vi;
+        A[(int64_t)k * n + i] = vi;                // reflector k for the back-transform
+        VWs[i][j] = vi;
+      }
+      __syncthreads();
+      // (3) pipelined read-only sweep + correction dots
+      const int r0 = k + 1, m = n - r0;
+      const int ncb = (m + 63) >> 6;
+      const int nrg = NWF / ncb;
+      {
+        const int cb = wid % ncb, rg = wid / ncb;
+        if (rg < nrg) {
+          const int c = cb * 64 + lane;
+          const int i = r0 + c;
+          const int rows_per = (m + nrg - 1) / nrg;
+          const int j0 = r0 + rg * rows_per;
+          const int j1 = min(n, j0 + rows_per);
+          double acc0 = 0.0, acc1 = 0.0;
+          if (i < n) {
+            // raw buffer loads: lane offset i*8 in one VGPR, wave-uniform row offset in an SGPR
+            // (no per-load 64-bit address registers -> deep pipelining fits in 128 VGPRs)
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(A, (short)0, n * n * 8, 0x00020000);
+            const int vo = i * 8;
+            const int rowb = n * 8;
+            const int nb16 = (j1 - j0) >> 3;
+            double a0[SW], a1[SW];
+            if (nb16 > 0) {
+#pragma unroll
+              for (int u = 0; u < SW; ++u)
+                a0[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                    rs, vo, __builtin_amdgcn_readfirstlane((j0 + u) * rowb), 0));
+            }
+            for (int b = 0; b < nb16; b += 2) {
+              const int l0 = j0 + SW * b;
+              if (b + 1 < nb16) {
+#pragma unroll
+                for (int u = 0; u < SW; ++u)
+                  a1[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                      rs, vo, __builtin_amdgcn_readfirstlane((l0 + SW + u) * rowb), 0));
+              }
+#pragma unroll
+              for (int u = 0; u < SW; u += 2) {
+                acc0 += a0[u] * v[l0 + u];
+                acc1 += a0[u + 1] * v[l0 + u + 1];
+              }
+              if (b + 2 < nb16) {
+#pragma unroll
+                for (int u = 0; u < SW; ++u)
+                  a0[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                      rs, vo, __builtin_amdgcn_readfirstlane((l0 + 2 * SW + u) * rowb), 0));
+              }
+              if (b + 1 < nb16) {
+#pragma unroll
+                for (int u = 0; u < SW; u += 2) {
+                  acc0 += a1[u] * v[l0 + SW + u];
+                  acc1 += a1[u + 1] * v[l0 + SW + u + 1];
+                }
+              }
+            }
+            for (int l = j0 + SW * nb16; l < j1; ++l) acc0 += A[(int64_t)l * n + i] * v[l];
+          }
+          part[rg * (ncb * 64) + c] = acc0 + acc1;
+        }
+      }
+      {
+        const int q = t & 15, pr = t >> 4;        // NTF/16 row partitions x 16 (V|W) columns
+        double s = 0.0;
+        if ((q & (PF - 1)) < j)
+          for (int i = r0 + pr; i < n; i += NTF / 16) s += VWs[i][q] * v[i];
+        red32[pr][q] = s;
+      }
+      __syncthreads();
+      if (t < 2 * PF) {
+        double s = 0.0;
+#pragma unroll 8
+        for (int pr = 0; pr < NTF / 16; ++pr) s += red32[pr][t];
+        xy[t] = s;                                 // xy[0..PF) = V'v, xy[PF..) = W'v
+      }
+      __syncthreads();
+      // (4) p, w, z
+      double pv = 0.0, vz = 0.0;
+      for (int c = t; c < m; c += NTF) {
+        double s = 0.0;
+        for (int qq = 0; qq < nrg; ++qq) s += part[qq * (ncb * 64) + c];
+        const int i = r0 + c;
+        for (int q = 0; q < j; ++q) s -= VWs[i][q] * xy[PF + q] + VWs[i][PF + q] * xy[q];
+        s *= tk;
+        pk[i] = s;
+        pv += s * v[i];
+        vz += v[i] * z[i];
+      }
+      double spv, svz;
+      bsum2(pv, vz, spv, svz);
+      const double half = 0.5 * tk * spv;
+      for (int i = r0 + t; i < n; i += NTF) {
+        VWs[i][PF + j] = pk[i] - half * v[i];
+        z[i] -= tk * svz * v[i];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int h = 0; h < RP; ++h) rcur[h] = rnext[h];
+    }
+    // (5) rank-2*nbp trailing update (rows, cols >= k0 + nbp), fp64 MFMA, VW from LDS
+    const int r0 = k0 + nbp, m = n - r0;
+    if (m > 0) {
+      const int nt = (m + 15) >> 4;
+      const int g4 = lane >> 4, c16 = lane & 15;
+      for (int tile = wid; tile < nt * nt; tile += NWF) {
+        const int i0 = r0 + (tile / nt) * 16, j0 = r0 + (tile % nt) * 16;
+        double4_t acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + PFML_F64_CROW(lane, r), jj = j0 + c16;
+          acc[r] = (i < n && jj < n) ? A[(int64_t)i * n + jj] : 0.0;
+        }
+        const int ia = i0 + c16, jb = j0 + c16;
+#pragma unroll
+        for (int q0 = 0; q0 < 2 * PF; q0 += 4) {
+          const int q = q0 + g4;
+          const int qq = q & (PF - 1);
+          double ua = 0.0, zb = 0.0;
+          if (qq < nbp) {
+            if (ia < n) ua = -VWs[ia][q];
+            if (jb < n) zb = VWs[jb][q < PF ? PF + q : q - PF];
+          }
+          acc = mfma_f64_16x16x4(ua, zb, acc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + PFML_F64_CROW(lane, r), jj = j0 + c16;
+          if (i < n && jj < n) A[(int64_t)i * n + jj] = acc[r];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    if (n >= 2) {
+      dd[n - 2] = A[(int64_t)(n - 2) * n + n - 2];
+      ee[n - 2] = A[(int64_t)(n - 1) * n + n - 2];
+      dd[n - 1] = A[(int64_t)(n - 1) * n + n - 1];
+    } else {
+      dd[0] = A[0];
+    }
+  }
+  __syncthreads();
+  for (int i = t; i < n; i += NTF) { dg[i] = dd[i]; eg[i] = ee[i]; tg[i] = tau[i]; zg[i] = z[i]; }
+}
+
 // Phase B: one thread per (cell, lambda) over the whole GPU.
 __global__ __launch_bounds__(256) void ridge_trisolve_kernel(
     const CellDesc* __restrict__ cells, int ncells, const double* __restrict__ lvec, int L,
@@ -628,18 +884,24 @@ extern "C" int64_t pfml_ridge_work_doubles(int n, int L) {
 }
 
 extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const double* Sr,
-                                      const void* cells, int ncells, const double* lvec, int L,
-                                      double* work, double* beta_out, int64_t ldo,
-                                      hipStream_t st) {
+                                      const void* cells, int ncells, int nmax,
+                                      const double* lvec, int L, double* work, double* beta_out,
+                                      int64_t ldo, hipStream_t st) {
   if (ncells <= 0) return hipSuccess;
-  if (L > 128) return hipErrorInvalidValue;
+  if (L > 128 || nmax > NMAX) return hipErrorInvalidValue;
   const CellDesc* cd = static_cast<const CellDesc*>(cells);
-  if (getenv("PFML_RIDGE_UNBLOCKED"))
+  const char* var = getenv("PFML_RIDGE_VARIANT");    // unblocked | blocked | fast (default)
+  const bool force_unblocked = var && var[0] == 'u';
+  const bool force_blocked = var && var[0] == 'b';
+  if (force_unblocked || (getenv("PFML_RIDGE_UNBLOCKED") != nullptr))
     hipLaunchKernelGGL(ridge_tridiag_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr, cd, L,
                        work);
-  else
+  else if (force_blocked || nmax > NV)
     hipLaunchKernelGGL(ridge_tridiag_blocked_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr,
                        cd, L, work);
+  else
+    hipLaunchKernelGGL(ridge_tridiag_fast_kernel, dim3(ncells), dim3(NTF), 0, st, SD, ldS, Sr, cd,
+                       L, work);
   const int64_t nth = (int64_t)ncells * L;
   hipLaunchKernelGGL(ridge_trisolve_kernel, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0,
                      st, cd, ncells, lvec, L, work);

@@ -72,6 +72,7 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
         lv = lvec.to(device=SD.device, dtype=torch.float64).contiguous()
         SDc, Src = SD.contiguous(), Sr.contiguous()
         nat.check(lib.pfml_ridge_grid(SDc.data_ptr(), P, Src.data_ptr(), d_desc.data_ptr(), nc,
+                                      int(np.max(cell_n)),
                                       lv.data_ptr(), L, work.data_ptr(), beta.data_ptr(), P,
                                       nat.stream_of(SD)), "pfml_ridge_grid")
         return beta
