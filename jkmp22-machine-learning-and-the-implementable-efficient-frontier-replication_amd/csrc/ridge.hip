@@ -436,7 +436,17 @@ constexpr int NWF = NTF / 64;
 
 __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
     const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
-    const CellDesc* __restrict__ cells, int L, double* __restrict__ work) {
+    const CellDesc* __restrict__ cells, int L, double* __restrict__ work,
+    long long* __restrict__ tim) {
+  // optional per-phase cycle accounting (tools/bench_ridge.py --timing): thread 0 only
+  long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long tlast = 0;
+#define PFML_TMARK(ph)                                                   \
+  if (tim != nullptr && threadIdx.x == 0) {                              \
+    const long long now = (long long)__builtin_amdgcn_s_memtime();       \
+    tacc[ph] += now - tlast;                                             \
+    tlast = now;                                                         \
+  }
   __shared__ double VWs[NV][2 * PF + 1];
   __shared__ double v[NV], pk[NV], z[NV], dd[NV], ee[NV], tau[NV];
   __shared__ double part[NTF];
@@ -480,6 +490,7 @@ __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
   };
 
   const int kend = n - 2;
+  if (tim != nullptr && threadIdx.x == 0) tlast = (long long)__builtin_amdgcn_s_memtime();
   for (int k0 = 0; k0 < kend; k0 += PF) {
     const int nbp = min(PF, kend - k0);
     constexpr int RP = (NV + NTF - 1) / NTF;     // row elements per thread
@@ -511,6 +522,7 @@ __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
         }
       }
       __syncthreads();
+      PFML_TMARK(0)
       // (2) Householder vector
       double x2 = 0.0;
       for (int i = k + 2 + t; i < n; i += NTF) x2 += pk[i] * pk[i];
@@ -534,6 +546,7 @@ __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
         VWs[i][j] = vi;
       }
       __syncthreads();
+      PFML_TMARK(1)
       // (3) pipelined read-only sweep + correction dots
       const int r0 = k + 1, m = n - r0;
       const int ncb = (m + 63) >> 6;
@@ -548,27 +561,27 @@ __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
           const int j1 = min(n, j0 + rows_per);
           double acc0 = 0.0, acc1 = 0.0;
           if (i < n) {
-            // raw buffer loads: lane offset i*8 in one VGPR, wave-uniform row offset in an SGPR
-            // (no per-load 64-bit address registers -> deep pipelining fits in 128 VGPRs)
-            const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(A, (short)0, n * n * 8, 0x00020000);
-            const int vo = i * 8;
-            const int rowb = n * 8;
+            // wave-uniform row base (SGPR pair) + 32-bit lane offset: the saddr form of
+            // global_load, so the in-flight rows need no per-load 64-bit address registers
+            const unsigned vo = (unsigned)i * 8u;
+            const char* Ab = reinterpret_cast<const char*>(A);
+            auto ldrow = [&](int row) -> double {
+              const char* rb = Ab + (int64_t)__builtin_amdgcn_readfirstlane(row) * n * 8;
+              return *reinterpret_cast<const double*>(rb + vo);
+            };
             const int nb16 = (j1 - j0) >> 3;
             double a0[SW], a1[SW];
             if (nb16 > 0) {
 #pragma unroll
               for (int u = 0; u < SW; ++u)
-                a0[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
-                    rs, vo, __builtin_amdgcn_readfirstlane((j0 + u) * rowb), 0));
+                a0[u] = ldrow(j0 + u);
             }
             for (int b = 0; b < nb16; b += 2) {
               const int l0 = j0 + SW * b;
               if (b + 1 < nb16) {
 #pragma unroll
                 for (int u = 0; u < SW; ++u)
-                  a1[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
-                      rs, vo, __builtin_amdgcn_readfirstlane((l0 + SW + u) * rowb), 0));
+                  a1[u] = ldrow(l0 + SW + u);
               }
 #pragma unroll
               for (int u = 0; u < SW; u += 2) {
@@ -578,8 +591,7 @@ __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
               if (b + 2 < nb16) {
 #pragma unroll
                 for (int u = 0; u < SW; ++u)
-                  a0[u] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
-                      rs, vo, __builtin_amdgcn_readfirstlane((l0 + 2 * SW + u) * rowb), 0));
+                  a0[u] = ldrow(l0 + 2 * SW + u);
               }
               if (b + 1 < nb16) {
 #pragma unroll
@@ -602,6 +614,7 @@ __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
         red32[pr][q] = s;
       }
       __syncthreads();
+      PFML_TMARK(2)
       if (t < 2 * PF) {
         double s = 0.0;
 #pragma unroll 8
@@ -609,6 +622,7 @@ __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
         xy[t] = s;                                 // xy[0..PF) = V'v, xy[PF..) = W'v
       }
       __syncthreads();
+      PFML_TMARK(3)
       // (4) p, w, z
       double pv = 0.0, vz = 0.0;
       for (int c = t; c < m; c += NTF) {
@@ -629,9 +643,11 @@ __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
         z[i] -= tk * svz * v[i];
       }
       __syncthreads();
+      PFML_TMARK(4)
 #pragma unroll
       for (int h = 0; h < RP; ++h) rcur[h] = rnext[h];
     }
+    PFML_TMARK(6)
     // (5) rank-2*nbp trailing update (rows, cols >= k0 + nbp), fp64 MFMA, VW from LDS
     const int r0 = k0 + nbp, m = n - r0;
     if (m > 0) {
@@ -665,6 +681,7 @@ __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
       }
     }
     __syncthreads();
+    PFML_TMARK(5)
   }
   if (t == 0) {
     if (n >= 2) {
@@ -677,6 +694,9 @@ __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
   }
   __syncthreads();
   for (int i = t; i < n; i += NTF) { dg[i] = dd[i]; eg[i] = ee[i]; tg[i] = tau[i]; zg[i] = z[i]; }
+  if (tim != nullptr && threadIdx.x == 0)
+    for (int q = 0; q < 8; ++q) tim[(int64_t)blockIdx.x * 8 + q] = tacc[q];
+#undef PFML_TMARK
 }
 
 // Phase B: one thread per (cell, lambda) over the whole GPU.
@@ -883,6 +903,10 @@ extern "C" int64_t pfml_ridge_work_doubles(int n, int L) {
   return (int64_t)n * n + 5LL * n * L + 4LL * n + 32LL * n;
 }
 
+static long long* g_ridge_timing = nullptr;
+// Debug: per-cell phase cycle counters of the fast tridiagonalisation (8 per cell).
+extern "C" void pfml_ridge_set_timing(long long* buf) { g_ridge_timing = buf; }
+
 extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const double* Sr,
                                       const void* cells, int ncells, int nmax,
                                       const double* lvec, int L, double* work, double* beta_out,
@@ -901,7 +925,7 @@ extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const doubl
                        cd, L, work);
   else
     hipLaunchKernelGGL(ridge_tridiag_fast_kernel, dim3(ncells), dim3(NTF), 0, st, SD, ldS, Sr, cd,
-                       L, work);
+                       L, work, g_ridge_timing);
   const int64_t nth = (int64_t)ncells * L;
   hipLaunchKernelGGL(ridge_trisolve_kernel, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0,
                      st, cd, ncells, lvec, L, work);

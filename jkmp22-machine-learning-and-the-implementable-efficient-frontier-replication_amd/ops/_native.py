@@ -50,6 +50,8 @@ def _declare_hip(lib):
     lib.pfml_spd_blockinv.argtypes = [P, L, L, I, I, I, P, P, P]
     lib.pfml_spd_blockinv.restype = I
     lib.pfml_spd_block_size.restype = I
+    lib.pfml_ridge_set_timing.argtypes = [P]
+    lib.pfml_ridge_set_timing.restype = None
     for name, argt in _EXTRA_HIP.items():
         fn = getattr(lib, name)
         fn.argtypes = argt[0]

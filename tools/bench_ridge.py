@@ -36,7 +36,25 @@ def run(ncells, n, reps=3):
     return (time.perf_counter() - t) / reps * 1e3
 
 
+def timing(n=513, ncells=1):
+    """Per-phase cycle split of the fast tridiagonalisation for one cell."""
+    from pfml.ops import _native as nat
+    dev = torch.device("cuda", 0)
+    buf = torch.zeros(ncells * 8, dtype=torch.int64, device=dev)
+    nat.hip_lib().pfml_ridge_set_timing(buf.data_ptr())
+    run(ncells, n, reps=1)
+    torch.cuda.synchronize()
+    nat.hip_lib().pfml_ridge_set_timing(None)
+    t = buf.view(ncells, 8)[0].cpu().numpy()
+    names = ["col_k", "householder", "sweep", "xy", "p_w_z", "trailing", "panel_end", "-"]
+    tot = max(1, int(t.sum()))
+    return {nm: f"{int(v)} cyc ({100.0 * v / tot:.1f}%)" for nm, v in zip(names, t)}
+
+
 if __name__ == "__main__":
+    if "--timing" in sys.argv:
+        print(json.dumps(timing(), indent=1))
+        sys.exit(0)
     out = {}
     for n in (513, 257):
         for nc in (1, 8, 32, 106, 212):
