@@ -430,7 +430,10 @@ __global__ __launch_bounds__(NT) void ridge_tridiag_blocked_kernel(
 // the lane's column are in flight while the current 16 are consumed.
 constexpr int NV = 513;       // fast path: n <= 513 keeps every sweep within 8 column blocks
 constexpr int PF = 8;
-constexpr int SW = 16;         // sweep rows per load batch (two batches in flight)
+constexpr int SW = 16;         // sweep rows per load batch
+constexpr int NBUF = 4;        // batches in the sweep's load ring (NBUF-1 in flight)
+constexpr int TB = 4;          // trailing-update tiles per wave per pass
+constexpr int VPAD = NBUF * SW;   // zero tail of v read by the last (ring-padded) partition
 constexpr int NTF = 512;       // fast path: 8 waves, up to 256 VGPRs per lane
 constexpr int NWF = NTF / 64;
 
@@ -447,8 +450,8 @@ __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
     tacc[ph] += now - tlast;                                             \
     tlast = now;                                                         \
   }
-  __shared__ double VWs[NV][2 * PF + 1];
-  __shared__ double v[NV], pk[NV], z[NV], dd[NV], ee[NV], tau[NV];
+  __shared__ double VWs[NV + 16][2 * PF + 1];     // rows >= n stay zero
+  __shared__ double v[NV + VPAD], pk[NV], z[NV], dd[NV], ee[NV], tau[NV];
   __shared__ double part[NTF];
   __shared__ double red[NWF * 2];
   __shared__ double red32[NTF / 16][2 * PF + 1];
@@ -474,6 +477,8 @@ __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
     for (int j = lane; j < n; j += 64) arow[j] = srow[j] * sc;
   }
   for (int i = t; i < n; i += NTF) z[i] = Sr[cd.rsrc + i] * sc;
+  for (int i = n + t; i < NV + VPAD; i += NTF) v[i] = 0.0;
+  for (int e = t; e < (NV + 16 - n) * (2 * PF + 1); e += NTF) (&VWs[n][0])[e] = 0.0;
   __syncthreads();
 
   auto bsum2 = [&](double a, double b, double& ra, double& rb) {
@@ -556,52 +561,47 @@ __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
         if (rg < nrg) {
           const int c = cb * 64 + lane;
           const int i = r0 + c;
-          const int rows_per = (m + nrg - 1) / nrg;
+          // row partitions are whole rings (NBUF*SW rows) so no batch straddles two partitions
+          constexpr int RING = NBUF * SW;
+          const int rows_per = ((m + nrg - 1) / nrg + RING - 1) / RING * RING;
           const int j0 = r0 + rg * rows_per;
-          const int j1 = min(n, j0 + rows_per);
+          const int nit = max(0, min(rows_per, n - j0) + RING - 1) / RING;
           double acc0 = 0.0, acc1 = 0.0;
-          if (i < n) {
-            // wave-uniform row base (SGPR pair) + 32-bit lane offset: the saddr form of
-            // global_load, so the in-flight rows need no per-load 64-bit address registers
-            const unsigned vo = (unsigned)i * 8u;
-            const char* Ab = reinterpret_cast<const char*>(A);
-            auto ldrow = [&](int row) -> double {
-              const char* rb = Ab + (int64_t)__builtin_amdgcn_readfirstlane(row) * n * 8;
-              return *reinterpret_cast<const double*>(rb + vo);
-            };
-            const int nb16 = (j1 - j0) >> 3;
-            double a0[SW], a1[SW];
-            if (nb16 > 0) {
+          // raw buffer loads: the lane's column offset lives in ONE VGPR, the wave-uniform row
+          // offset in an SGPR (soffset), so in-flight rows cost only their data registers.
+          // Rows past the partition (ring padding, the ring's last prefetches) are clamped to
+          // its last row, which is cache-hot and finite; their weights come from the zero tail
+          // of v (or are never consumed).  Columns past n only feed part[c >= m], never read.
+          const int vo = i * 8;
+          const int rlim = min(n, j0 + nit * RING) - 1;
+          const __amdgpu_buffer_rsrc_t rs =
+              __builtin_amdgcn_make_buffer_rsrc(A, (short)0, n * n * 8, 0x00020000);
+          auto ldrow = [&](int row) -> double {
+            const int so = __builtin_amdgcn_readfirstlane(min(row, rlim) * n * 8);
+            return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0));
+          };
+          // NBUF-stage ring of SW-row batches with no branches inside the loop body, so the
+          // waitcnt pass keeps (NBUF-1)*SW loads in flight while one batch is consumed.
+          double a[NBUF][SW];
+          if (nit > 0) {
 #pragma unroll
-              for (int u = 0; u < SW; ++u)
-                a0[u] = ldrow(j0 + u);
-            }
-            for (int b = 0; b < nb16; b += 2) {
-              const int l0 = j0 + SW * b;
-              if (b + 1 < nb16) {
+            for (int s = 0; s < NBUF - 1; ++s)
 #pragma unroll
-                for (int u = 0; u < SW; ++u)
-                  a1[u] = ldrow(l0 + SW + u);
-              }
+              for (int u = 0; u < SW; ++u) a[s][u] = ldrow(j0 + s * SW + u);
+          }
+          for (int it = 0; it < nit; ++it) {
+#pragma unroll
+            for (int s = 0; s < NBUF; ++s) {
+              const int l0 = j0 + (it * NBUF + s) * SW;
+              const int lp = l0 + (NBUF - 1) * SW;
+#pragma unroll
+              for (int u = 0; u < SW; ++u) a[(s + NBUF - 1) % NBUF][u] = ldrow(lp + u);
 #pragma unroll
               for (int u = 0; u < SW; u += 2) {
-                acc0 += a0[u] * v[l0 + u];
-                acc1 += a0[u + 1] * v[l0 + u + 1];
-              }
-              if (b + 2 < nb16) {
-#pragma unroll
-                for (int u = 0; u < SW; ++u)
-                  a0[u] = ldrow(l0 + 2 * SW + u);
-              }
-              if (b + 1 < nb16) {
-#pragma unroll
-                for (int u = 0; u < SW; u += 2) {
-                  acc0 += a1[u] * v[l0 + SW + u];
-                  acc1 += a1[u + 1] * v[l0 + SW + u + 1];
-                }
+                acc0 += a[s][u] * v[l0 + u];
+                acc1 += a[s][u + 1] * v[l0 + u + 1];
               }
             }
-            for (int l = j0 + SW * nb16; l < j1; ++l) acc0 += A[(int64_t)l * n + i] * v[l];
           }
           part[rg * (ncb * 64) + c] = acc0 + acc1;
         }
@@ -653,31 +653,43 @@ __global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
     if (m > 0) {
       const int nt = (m + 15) >> 4;
       const int g4 = lane >> 4, c16 = lane & 15;
-      for (int tile = wid; tile < nt * nt; tile += NWF) {
-        const int i0 = r0 + (tile / nt) * 16, j0 = r0 + (tile % nt) * 16;
-        double4_t acc;
+      // TB tiles per wave per pass: all 4*TB loads are issued before the first MFMA so the
+      // pass costs one memory latency, not TB.  (Plain global stores: raw buffer stores here
+      // were not seen by the next panel's loads.)
+      const int ntt = nt * nt;
+      for (int tb = wid * TB; tb < ntt; tb += NWF * TB) {
+        double4_t acc[TB];
+        int off[TB][4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = i0 + PFML_F64_CROW(lane, r), jj = j0 + c16;
-          acc[r] = (i < n && jj < n) ? A[(int64_t)i * n + jj] : 0.0;
-        }
-        const int ia = i0 + c16, jb = j0 + c16;
+        for (int u = 0; u < TB; ++u) {
+          const int tile = min(tb + u, ntt - 1);
+          const bool tv = tb + u < ntt;
+          const int i0 = r0 + (tile / nt) * 16, j0 = r0 + (tile % nt) * 16;
 #pragma unroll
-        for (int q0 = 0; q0 < 2 * PF; q0 += 4) {
-          const int q = q0 + g4;
-          const int qq = q & (PF - 1);
-          double ua = 0.0, zb = 0.0;
-          if (qq < nbp) {
-            if (ia < n) ua = -VWs[ia][q];
-            if (jb < n) zb = VWs[jb][q < PF ? PF + q : q - PF];
+          for (int r = 0; r < 4; ++r) {
+            const int i = i0 + PFML_F64_CROW(lane, r), jj = j0 + c16;
+            off[u][r] = (tv && i < n && jj < n) ? i * n + jj : -1;
+            acc[u][r] = (off[u][r] >= 0) ? A[off[u][r]] : 0.0;
           }
-          acc = mfma_f64_16x16x4(ua, zb, acc);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int i = i0 + PFML_F64_CROW(lane, r), jj = j0 + c16;
-          if (i < n && jj < n) A[(int64_t)i * n + jj] = acc[r];
+        for (int u = 0; u < TB; ++u) {
+          const int tile = min(tb + u, ntt - 1);
+          const int ia = r0 + (tile / nt) * 16 + c16, jb = r0 + (tile % nt) * 16 + c16;
+#pragma unroll
+          for (int q0 = 0; q0 < 2 * PF; q0 += 4) {
+            const int q = q0 + g4;
+            const bool qv = (q & (PF - 1)) < nbp;
+            const double ua = qv ? -VWs[ia][q] : 0.0;
+            const double zb = qv ? VWs[jb][q < PF ? PF + q : q - PF] : 0.0;
+            acc[u] = mfma_f64_16x16x4(ua, zb, acc[u]);
+          }
         }
+#pragma unroll
+        for (int u = 0; u < TB; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (off[u][r] >= 0) A[off[u][r]] = acc[u][r];
       }
     }
     __syncthreads();
