@@ -5,7 +5,8 @@
 // for every (g, year, p) cell, every one of its 12 validation months t and all 101 lambdas.
 // The reference evaluates 513,888 of these quadratic forms one at a time from Python.  Here a
 // job = (cell, month); the kernel computes the GEMM  U = D_t[:n,:n] * B  (B = [beta_l], n x L)
-// on fp64 MFMA and folds the two reductions into the epilogue, so U never leaves registers.
+// on fp64 MFMA (upper block triangle only: D_t is symmetric) and folds the two reductions
+// into the epilogue, so U never leaves registers.
 //
 // Tile: 64 rows of D x 112 lambda columns (L <= 112) per 256-thread workgroup; each wave owns
 // 16 rows x 7 MFMA 16x16 accumulators.  Every workgroup writes a deterministic per-row-tile
@@ -29,8 +30,8 @@ __global__ __launch_bounds__(256) void quadform_kernel(
     const double* __restrict__ D, int64_t ldD, const double* __restrict__ R,
     const double* __restrict__ Bt, int64_t ldB, const JobDesc* __restrict__ jobs,
     const int* __restrict__ tile_job, int L, double* __restrict__ partial) {
-  __shared__ double As[BK][BM + PAD];
-  __shared__ double Bs[BK][NCOL + PAD];
+  __shared__ double As[2][BK][BM + PAD];
+  __shared__ double Bs[2][BK][NCOL + PAD];
   __shared__ double red[4][NCOL];
 
   const int tile = blockIdx.x;
@@ -48,28 +49,56 @@ __global__ __launch_bounds__(256) void quadform_kernel(
 #pragma unroll
   for (int q = 0; q < NTILE; ++q) acc[q] = double4_t{0.0, 0.0, 0.0, 0.0};
 
-  for (int k0 = 0; k0 < n; k0 += BK) {
-    // D tile: rows i0..i0+63, cols k0..k0+15 (row-major, contiguous along k) -> As[k][i]
+  // D_t is symmetric:  b'Db = sum_I b_I'(D_II b_I + 2 sum_{K>I} D_IK b_K).  A row tile I only
+  // walks K >= I, with the diagonal block weighted 1/2, so  acc = U_I / 2  and half the
+  // flops and D bytes of the full product are spent.  K tiles are double-buffered in LDS
+  // through registers (one barrier per K step).
+  constexpr int AQ = (BM * BK) / 256;             // D elements per thread per K step
+  constexpr int BQ = (NCOL * BK + 255) / 256;     // beta elements per thread per K step
+  double ra[AQ], rb[BQ];
+  auto gload = [&](int k0) {
+    const double wdiag = (k0 < i0 + BM) ? 0.5 : 1.0;
 #pragma unroll
-    for (int q = 0; q < (BM * BK) / 256; ++q) {
+    for (int q = 0; q < AQ; ++q) {
       const int e = t + q * 256, i = e / BK, k = e % BK;
       const int gi = i0 + i, gk = k0 + k;
-      As[k][i] = (gi < n && gk < n) ? Dm[(int64_t)gi * ldD + gk] : 0.0;
+      ra[q] = (gi < n && gk < n) ? wdiag * Dm[(int64_t)gi * ldD + gk] : 0.0;
     }
-    // B tile: B[k][l] = beta_l[k0+k]  (beta stored lambda-major: contiguous along k)
-    for (int e = t; e < NCOL * BK; e += 256) {
-      const int l = e / BK, k = e % BK, gk = k0 + k;
-      Bs[k][l] = (l < L && gk < n) ? bt[(int64_t)l * ldB + gk] : 0.0;
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) {
+      const int e = t + q * 256, l = e / BK, k = e % BK, gk = k0 + k;
+      rb[q] = (e < NCOL * BK && l < L && gk < n) ? bt[(int64_t)l * ldB + gk] : 0.0;
     }
-    __syncthreads();
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < AQ; ++q) {
+      const int e = t + q * 256, i = e / BK, k = e % BK;
+      As[buf][k][i] = ra[q];
+    }
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) {
+      const int e = t + q * 256, l = e / BK, k = e % BK;
+      if (e < NCOL * BK) Bs[buf][k][l] = rb[q];
+    }
+  };
+  int buf = 0;
+  gload(i0);
+  sstore(0);
+  __syncthreads();
+  for (int k0 = i0; k0 < n; k0 += BK) {
+    const bool more = k0 + BK < n;
+    if (more) gload(k0 + BK);
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
-      const double a = As[kk + (lane >> 4)][w * 16 + (lane & 15)];
+      const double a = As[buf][kk + (lane >> 4)][w * 16 + (lane & 15)];
 #pragma unroll
       for (int q = 0; q < NTILE; ++q)
-        acc[q] = mfma_f64_16x16x4(a, Bs[kk + (lane >> 4)][q * 16 + (lane & 15)], acc[q]);
+        acc[q] = mfma_f64_16x16x4(a, Bs[buf][kk + (lane >> 4)][q * 16 + (lane & 15)], acc[q]);
     }
+    if (more) sstore(buf ^ 1);
     __syncthreads();
+    buf ^= 1;
   }
 
   // epilogue: sum over this wave's 16 rows of  beta_l[i] * (r_i - 1/2 U[i][l])
@@ -82,7 +111,7 @@ __global__ __launch_bounds__(256) void quadform_kernel(
       const int gi = i0 + w * 16 + PFML_F64_CROW(lane, rr);
       if (gi < n && l < L) {
         const double b = bt[(int64_t)l * ldB + gi];
-        s += b * (r[gi] - 0.5 * acc[q][rr]);
+        s += b * (r[gi] - acc[q][rr]);          // acc = U / 2 (symmetric half)
       }
     }
     // lanes l, l+16, l+32, l+48 share the column

@@ -25,6 +25,7 @@
 //   part), rows strided over parts), reflectors are staged through a 3-deep LDS ring, one
 //   barrier per reflector.
 #include "common.h"
+#include "ridge_desc.h"
 #include <cstdlib>
 
 namespace {
@@ -36,14 +37,7 @@ constexpr int YREG = 33;        // rows of Y per lane in the register back-trans
 constexpr int RMAX = 528;       // reflector row length staged by the back-transform ring
 constexpr int KB = 4;           // reflectors per staging block
 
-struct CellDesc {
-  int64_t src;      // offset (doubles) of the running-sum matrix S_D for this cell
-  int64_t rsrc;     // offset of the running-sum vector S_r
-  int64_t work;     // offset of this cell's workspace
-  int64_t out;      // offset of beta output [L][ldo]
-  int n;            // p + 1
-  double scale;     // 1 / T  (the reference divides both sums by n months)
-};
+typedef RidgeCellDesc CellDesc;
 
 __device__ __forceinline__ double rank2(double a, double vj, double wi, double wj, double vi) {
 #pragma clang fp contract(off)
@@ -911,8 +905,18 @@ __global__ __launch_bounds__(NT) void ridge_backtransform_kernel(
 
 }  // namespace
 
+extern "C" int64_t pfml_ridge_band_work_doubles(int n, int L);
+extern "C" int pfml_ridge_band_nmax();
+extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, const double* Sr,
+                                             const void* cells, int ncells, const double* lvec,
+                                             int L, double* work, double* beta_out, int64_t ldo,
+                                             long long* tim, hipStream_t st);
+
+// Workspace per cell: enough for whichever path the launcher picks (band path: ridge_band.hip).
 extern "C" int64_t pfml_ridge_work_doubles(int n, int L) {
-  return (int64_t)n * n + 5LL * n * L + 4LL * n + 32LL * n;
+  const int64_t tri = (int64_t)n * n + 5LL * n * L + 4LL * n + 32LL * n;
+  const int64_t band = pfml_ridge_band_work_doubles(n, L);
+  return tri > band ? tri : band;
 }
 
 static long long* g_ridge_timing = nullptr;
@@ -926,9 +930,15 @@ extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const doubl
   if (ncells <= 0) return hipSuccess;
   if (L > 128 || nmax > NMAX) return hipErrorInvalidValue;
   const CellDesc* cd = static_cast<const CellDesc*>(cells);
-  const char* var = getenv("PFML_RIDGE_VARIANT");    // unblocked | blocked | fast (default)
+  // PFML_RIDGE_VARIANT: band (default) | tridiag-fast | unblocked | blocked
+  const char* var = getenv("PFML_RIDGE_VARIANT");
   const bool force_unblocked = var && var[0] == 'u';
-  const bool force_blocked = var && var[0] == 'b';
+  const bool force_blocked = var && var[0] == 'b' && var[1] == 'l';
+  const bool force_fast = var && (var[0] == 'f' || var[0] == 't');
+  if (!force_unblocked && !force_blocked && !force_fast && !getenv("PFML_RIDGE_UNBLOCKED") &&
+      nmax <= pfml_ridge_band_nmax())
+    return pfml_ridge_band_launch(SD, ldS, Sr, cells, ncells, lvec, L, work, beta_out, ldo,
+                                  g_ridge_timing, st);
   if (force_unblocked || (getenv("PFML_RIDGE_UNBLOCKED") != nullptr))
     hipLaunchKernelGGL(ridge_tridiag_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr, cd, L,
                        work);

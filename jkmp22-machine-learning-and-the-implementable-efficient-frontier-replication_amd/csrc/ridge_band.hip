@@ -1,0 +1,636 @@
+// Ridge hyper-parameter grid, eq. (26), band path:  beta_l = (Dbar + l I)^-1 rbar  for all l.
+//
+// Reference: PFML_Search_Coef.py:124-137 (np.linalg.solve per lambda).  The tridiagonal path
+// (ridge.hip) factors Dbar = Q T Q^T with one Householder reflector at a time; every reflector
+// needs a full mat-vec over the trailing matrix, i.e. ~n^3/3 doubles streamed per cell through
+// ONE CU, and that stream (not the flops) bounds it.  This path reduces Dbar to BAND form
+// instead (bandwidth BB = 16, the two-sided blocked Householder of the first stage of a
+// two-stage symmetric eigensolver):
+//
+//     Dbar = Q B Q^T,   Q = Q_0 Q_1 ... Q_{np-1},   Q_p = I - V_p T_p V_p^T  (compact WY)
+//
+// per panel p (16 columns) the trailing matrix is read once for X = A22 V T and read+written
+// once for the rank-32 update A22 -= V W^T + W V^T, both on v_mfma_f64_16x16x4 with V, W
+// resident in LDS: 16x fewer passes over the trailing matrix than one pass per reflector.
+// Then every lambda is an independent banded Cholesky solve (B + l I) y = Q^T rbar (one wave
+// per lambda, register window with DPP broadcasts, O(n BB^2)), and beta = Q y is a blocked-WY back-transform
+// (MFMA, Y chunk of 16 lambdas resident in LDS).
+//
+//   kernel 1  ridge_band_reduce_kernel       one 512-thread workgroup per cell
+//   kernel 2  ridge_band_solve_kernel        4 lambdas per wave (16-lane DPP rows)
+//   kernel 3  ridge_band_backtransform_kernel one 256-thread workgroup per (cell, 16 lambdas)
+//
+// A non-positive Cholesky pivot (Dbar + l I not numerically SPD, e.g. l = 0 on a singular
+// Dbar) marks that lambda's beta NaN; ops/ridge.py recomputes exactly those systems with a
+// pivoted LU so the result matches the reference's np.linalg.solve semantics.
+#include "common.h"
+#include "ridge_desc.h"
+#include <cstdlib>
+#include <type_traits>
+
+namespace {
+
+constexpr int BB = 16;              // bandwidth = panel width = MFMA tile
+constexpr int LS = BB + 1;          // LDS row stride (bank spread for column-wise reads)
+constexpr int BMP = 512;            // max panel rows m = n - r0  (n <= BNMAX)
+constexpr int BNMAX = BMP + BB;     // 528 >= p_max + 1
+constexpr int NTR = 512;            // reduce kernel: 8 waves
+constexpr int NWR = NTR / 64;
+constexpr int TBR = 4;              // trailing-update tiles per wave per pass
+constexpr int NTB = 256;            // back-transform kernel: 4 waves
+constexpr int NWB = NTB / 64;
+constexpr int LC = 16;              // lambdas per back-transform workgroup
+
+// Per-cell workspace layout (doubles).
+struct BandWork {
+  double *A, *LB, *z, *T, *Yt, *Lf;
+  __device__ BandWork(double* w, int n, int L) {
+    const int np = (n + BB - 1) / BB;
+    A = w;                                   // n x n working matrix (V_p / R_p stored below)
+    LB = A + (int64_t)n * n;                 // n x LS lower band: LB[r][s] = B[r][r-16+s]
+    z = LB + (int64_t)n * LS;                // Q^T rbar
+    T = z + n;                               // np x 16 x 16 compact-WY T_p
+    Yt = T + (int64_t)np * BB * BB;          // L x n   solutions y_l, then beta_l
+    Lf = Yt + (int64_t)L * n;                // L x n x LS banded Cholesky factors
+  }
+};
+
+// DPP helpers (gfx950: row_newbcast broadcasts one lane of each 16-lane row).
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
+template <int SEL>
+__device__ __forceinline__ double row_bcast(double v) {   // lane SEL of each 16-lane row
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x150 + SEL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x150 + SEL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_mov<0xB1>(v);      // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);      // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);     // row_half_mirror
+  v += dpp_mov<0x140>(v);     // row_mirror
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// kernel 1: band reduction of one cell.
+// ---------------------------------------------------------------------------------------
+template <int NQ>
+__device__ __forceinline__ void band_x_accum(const double* __restrict__ A, int n, int r0, int m,
+                                             int wid, int c16, int g4,
+                                             const double (*__restrict__ Ws)[LS],
+                                             double4_t (&X)[4]) {
+  // X_I += A22[I rows][k] U[k][:]  for the NQ row blocks I = wid + 8q of this wave.  A22 is
+  // read through its symmetry (row r0+k, columns of block I: 128 B contiguous per row).
+  int col[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) col[q] = min((wid + NWR * q) * 16 + c16, m - 1);
+  int k = 0;
+  for (; k + 32 <= m; k += 32) {
+    double a[8][NQ], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double* arow = A + (int64_t)(r0 + k + 4 * u + g4) * n + r0;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) a[u][q] = arow[col[q]];
+      b[u] = Ws[k + 4 * u + g4][c16];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) X[q] = mfma_f64_16x16x4(a[u][q], b[u], X[q]);
+  }
+  for (; k < m; k += 4) {
+    const int kr = min(k + g4, m - 1);             // U rows >= m are zero
+    const double* arow = A + (int64_t)(r0 + kr) * n + r0;
+    const double b = Ws[k + g4][c16];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) X[q] = mfma_f64_16x16x4(arow[col[q]], b, X[q]);
+  }
+}
+
+__global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
+    const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
+    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work,
+    long long* __restrict__ tim) {
+  // optional per-phase cycle accounting (tools/bench_ridge.py --timing): thread 0 only
+  long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long tlast = 0;
+#define BAND_TMARK(ph)                                                   \
+  if (tim != nullptr && threadIdx.x == 0) {                              \
+    const long long now = (long long)__builtin_amdgcn_s_memtime();       \
+    tacc[ph] += now - tlast;                                             \
+    tlast = now;                                                         \
+  }
+  __shared__ double Vs[BMP][LS];       // panel: QR workspace, then V (unit lower trapezoid)
+  __shared__ double Ws[BMP][LS];       // G, then U = V T, then W
+  __shared__ double red[NWR][BB * BB]; // cross-wave partials
+  __shared__ double red2[NWR][BB];
+  __shared__ double Ts[BB][LS];
+  __shared__ double taus[BB];
+
+  const RidgeCellDesc cd = cells[blockIdx.x];
+  const int n = cd.n;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int c16 = lane & 15, g4 = lane >> 4;
+  const int cq = t & 15, rg = t >> 4;            // (row group of 32, column) thread map
+  BandWork bw(work + cd.work, n, L);
+  double* A = bw.A;
+  const double* S = SD + cd.src;
+  const double sc = cd.scale;
+  for (int i = wid; i < n; i += NWR) {
+    const double* srow = S + (int64_t)i * ldS;
+    double* arow = A + (int64_t)i * n;
+    for (int j = lane; j < n; j += 64) arow[j] = srow[j] * sc;
+  }
+  for (int i = t; i < n; i += NTR) bw.z[i] = Sr[cd.rsrc + i] * sc;
+  __syncthreads();
+
+  if (tim != nullptr && threadIdx.x == 0) tlast = (long long)__builtin_amdgcn_s_memtime();
+  for (int k0 = 0; k0 + BB < n; k0 += BB) {
+    const int r0 = k0 + BB, m = n - r0, p = k0 / BB;
+    // ---- P1: panel A[r0:, k0:k0+16] -> Vs (read as rows k0..k0+15 of the symmetric A)
+    for (int e = t; e < BB * BMP; e += NTR) {
+      const int c = e / BMP, i = e % BMP;
+      Vs[i][c] = (i < m) ? A[(int64_t)(k0 + c) * n + r0 + i] : 0.0;
+    }
+    __syncthreads();
+    BAND_TMARK(0)
+    // ---- P2: Householder QR of the m x 16 panel in REGISTERS: thread (rg, cq) holds rows
+    //      i = rg + 32 q (q < 16) of column cq; column j reaches the 16 lanes of a row group by
+    //      a row_newbcast DPP move; one barrier per column (cross-wave sums, ping-pong
+    //      buffers).  The dlarft dots G[:, j-1] = V^T v_{j-1} ride in the same reduction.
+    double* redf = &red[0][0];
+    double a[16], vp[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      a[q] = Vs[rg + 32 * q][cq];
+      vp[q] = 0.0;
+    }
+    static_for<0, BB + 1>([&](auto J) {
+      constexpr int j = decltype(J)::value;      // j == BB: only the last G column
+      const int par = j & 1;
+      double x[16];
+      double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = rg + 32 * q;
+        if constexpr (j < BB) {
+          x[q] = row_bcast<j < BB ? j : 0>(a[q]);
+          s1 += (i > j) ? x[q] * a[q] : 0.0;
+        }
+        if constexpr (j > 0) {
+          const double vex = (i > cq) ? a[q] : ((i == cq && i < m) ? 1.0 : 0.0);
+          s2 += vp[q] * vex;
+        }
+      }
+      s1 += __shfl_xor(s1, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (lane < 16) {
+        redf[par * 256 + wid * 16 + lane] = s1;
+        redf[512 + par * 256 + wid * 16 + lane] = s2;
+      }
+      if constexpr (j < BB) {
+        if (rg == j) redf[1024 + par * 16 + cq] = a[0];     // row j (q = 0)
+      }
+      __syncthreads();
+      if constexpr (j > 0) {
+        if (t < BB) {
+          double g = 0.0;
+#pragma unroll
+          for (int w = 0; w < NWR; ++w) g += redf[512 + par * 256 + w * 16 + t];
+          Ws[t][j - 1] = g;                                 // G[t][j-1]
+        }
+      }
+      if constexpr (j < BB) {
+        double xn2 = 0.0, dc = 0.0;
+#pragma unroll
+        for (int w = 0; w < NWR; ++w) {
+          xn2 += redf[par * 256 + w * 16 + j];
+          dc += redf[par * 256 + w * 16 + cq];
+        }
+        const double alpha = redf[1024 + par * 16 + j];
+        const double vjc = redf[1024 + par * 16 + cq];
+        double tau, beta, scal;
+        if (xn2 == 0.0) {
+          tau = 0.0; beta = alpha; scal = 0.0;
+        } else {
+          beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
+          tau = (beta - alpha) / beta;
+          scal = 1.0 / (alpha - beta);
+        }
+        const double wc = tau * (vjc + scal * dc);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int i = rg + 32 * q;
+          const double v = (i > j) ? x[q] * scal : ((i == j && i < m) ? 1.0 : 0.0);
+          if (cq > j) a[q] -= v * wc;
+          else if (cq == j) a[q] = (i > j) ? v : ((i == j) ? beta : a[q]);
+          vp[q] = v;
+        }
+        if (t == 0) taus[j] = tau;
+      }
+    });
+    // explicit V -> Vs (MFMA operand); V (strictly lower) and R (upper) -> A's panel columns
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = rg + 32 * q;
+      Vs[i][cq] = (i > cq) ? a[q] : ((i == cq && i < m) ? 1.0 : 0.0);
+      if (i < m) A[(int64_t)(r0 + i) * n + k0 + cq] = a[q];
+    }
+    __syncthreads();
+    BAND_TMARK(1)
+    // ---- T (dlarft, forward columnwise): T[j][j] = tau_j,
+    //      T[0:j, j] = -tau_j T[0:j, 0:j] G[0:j, j]   (one wave, lane = row)
+    if (wid == 0) {                              // lane = row: no cross-lane dependency
+      for (int j = 0; j < BB; ++j) {
+        double s = 0.0;
+        if (lane < j)
+          for (int k = lane; k < j; ++k) s += Ts[lane][k] * Ws[k][j];
+        if (lane < BB) Ts[lane][j] = (lane < j) ? -taus[j] * s : (lane == j ? taus[j] : 0.0);
+      }
+    }
+    __syncthreads();
+    if (t < BB * BB) bw.T[(int64_t)p * BB * BB + t] = Ts[t / BB][t % BB];
+    BAND_TMARK(2)
+    // ---- U = V T -> Ws  (MFMA, all 32 row blocks so rows >= m read back as zero)
+#pragma unroll
+    for (int q = 0; q < BMP / 16 / NWR; ++q) {
+      const int i0 = (wid + NWR * q) * 16;
+      double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vs[i0 + c16][4 * r + g4], Ts[4 * r + g4][c16], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Ws[i0 + g4 + 4 * r][c16] = acc[r];
+    }
+    __syncthreads();
+    BAND_TMARK(3)
+    // ---- P3: X = A22 U  (row blocks I = wid + 8q)
+    const int nI = (m + 15) >> 4;
+    const int nq = (nI > wid) ? (nI - wid + NWR - 1) / NWR : 0;
+    double4_t X[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) X[q] = double4_t{0.0, 0.0, 0.0, 0.0};
+    switch (nq) {
+      case 1: band_x_accum<1>(A, n, r0, m, wid, c16, g4, Ws, X); break;
+      case 2: band_x_accum<2>(A, n, r0, m, wid, c16, g4, Ws, X); break;
+      case 3: band_x_accum<3>(A, n, r0, m, wid, c16, g4, Ws, X); break;
+      case 4: band_x_accum<4>(A, n, r0, m, wid, c16, g4, Ws, X); break;
+      default: break;
+    }
+    BAND_TMARK(4)
+    // ---- P4: partial V^T X (MFMA: X's accumulator layout IS the B-operand layout), and
+    //          partial V^T z
+    {
+      double4_t Pp = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (q < nq) {
+          const int i0 = (wid + NWR * q) * 16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Pp = mfma_f64_16x16x4(Vs[i0 + 4 * r + g4][c16], X[q][r], Pp);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wid][(g4 + 4 * r) * BB + c16] = Pp[r];
+      double s = 0.0;
+      for (int i = rg; i < m; i += 32) s += Vs[i][cq] * bw.z[r0 + i];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (lane < 16) red2[wid][lane] = s;
+    }
+    __syncthreads();
+    // z <- Q_p^T z = z - V (T^T (V^T z))
+    {
+      double zv[BB];
+#pragma unroll
+      for (int a = 0; a < BB; ++a) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < NWR; ++w) s += red2[w][a];
+        zv[a] = s;
+      }
+      double zt[BB];
+#pragma unroll
+      for (int c = 0; c < BB; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int a = 0; a <= c; ++a) s += Ts[a][c] * zv[a];
+        zt[c] = s;
+      }
+      for (int i = t; i < m; i += NTR) {
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < BB; ++c) s += Vs[i][c] * zt[c];
+        bw.z[r0 + i] -= s;
+      }
+    }
+    // M = T^T (V^T X) ; W_I = X_I - 1/2 V_I M  -> Ws
+    {
+      double4_t Mm = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double pv = 0.0;
+#pragma unroll
+        for (int w = 0; w < NWR; ++w) pv += red[w][(4 * r + g4) * BB + c16];
+        Mm = mfma_f64_16x16x4(Ts[4 * r + g4][c16], pv, Mm);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (q < nq) {
+          const int i0 = (wid + NWR * q) * 16;
+          double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vs[i0 + c16][4 * r + g4], Mm[r], acc);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = i0 + g4 + 4 * r;
+            Ws[i][c16] = (i < m) ? X[q][r] - 0.5 * acc[r] : 0.0;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    BAND_TMARK(5)
+    // ---- P6: A22 -= V W^T + W V^T on the LOWER block triangle (K = 32 MFMA per 16x16 tile,
+    //      TBR tiles per pass); each off-diagonal tile is also stored transposed, so A stays
+    //      bitwise symmetric at half the MFMA work.
+    {
+      const int ntt = nI * (nI + 1) / 2;
+      for (int tb = wid * TBR; tb < ntt; tb += NWR * TBR) {
+        double4_t acc[TBR];
+        int offn[TBR][4], offt[TBR][4], ia[TBR], jb[TBR];
+#pragma unroll
+        for (int u = 0; u < TBR; ++u) {
+          const int tile = min(tb + u, ntt - 1);
+          const bool tv = tb + u < ntt;
+          int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+          if (I * (I + 1) / 2 > tile) --I;
+          if ((I + 1) * (I + 2) / 2 <= tile) ++I;
+          const int Jt = tile - I * (I + 1) / 2;
+          const int i0 = I * 16, j0 = Jt * 16;
+          ia[u] = i0 + c16;
+          jb[u] = j0 + c16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = i0 + g4 + 4 * r, jj = j0 + c16;
+            const bool ok = tv && i < m && jj < m;
+            offn[u][r] = ok ? (r0 + i) * n + r0 + jj : -1;
+            offt[u][r] = (ok && I != Jt) ? (r0 + jj) * n + r0 + i : -1;
+            acc[u][r] = ok ? A[offn[u][r]] : 0.0;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < TBR; ++u) {
+#pragma unroll
+          for (int s = 0; s < 8; ++s) {
+            const int kk = 4 * (s & 3) + g4;
+            const double av = (s < 4) ? Vs[ia[u]][kk] : Ws[ia[u]][kk];
+            const double bv = (s < 4) ? Ws[jb[u]][kk] : Vs[jb[u]][kk];
+            acc[u] = mfma_f64_16x16x4(-av, bv, acc[u]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < TBR; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (offn[u][r] >= 0) A[offn[u][r]] = acc[u][r];
+            if (offt[u][r] >= 0) A[offt[u][r]] = acc[u][r];
+          }
+      }
+    }
+    __syncthreads();
+    BAND_TMARK(6)
+  }
+  BAND_TMARK(7)
+  if (tim != nullptr && threadIdx.x == 0)
+    for (int q = 0; q < 8; ++q) tim[(int64_t)blockIdx.x * 8 + q] = tacc[q];
+#undef BAND_TMARK
+  // ---- row-major lower band: LB[r][s] = B[r][r-16+s]  (s = 16: diagonal)
+  for (int e = t; e < n * LS; e += NTR) {
+    const int r = e / LS, c = r - BB + e % LS;
+    bw.LB[e] = (c >= 0) ? A[(int64_t)r * n + c] : 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// kernel 2: banded Cholesky solves, 4 lambdas per wave (one 16-lane DPP row each).
+//
+// Lane p of a row holds the band row r (r = p mod 16) of the 16-row window j+1..j+16 (the
+// retiring pivot lane takes row j+16 in the same step), columns j..j+16 in 17 registers
+// (slot k <-> column j+k, shifted one slot per step).  Every cross-lane value is a
+// row_newbcast DPP move (no LDS), so a step is ~60 VALU ops and 4 independent solves share
+// each instruction.  Slots right of a row's diagonal hold garbage that is never read.
+// ---------------------------------------------------------------------------------------
+constexpr int NTS = 256;      // 4 waves x 4 rows = 16 lambdas per workgroup
+
+__global__ __launch_bounds__(NTS) void ridge_band_solve_kernel(
+    const RidgeCellDesc* __restrict__ cells, const double* __restrict__ lvec, int L,
+    double* __restrict__ work, int dbg) {
+  const int nb = (L + 15) / 16;
+  const int cell = blockIdx.x / nb;
+  const RidgeCellDesc cd = cells[cell];
+  const int n = cd.n;
+  const int p = threadIdx.x & 15;
+  const int l = (blockIdx.x % nb) * 16 + (threadIdx.x >> 4);
+  const bool lv = l < L;
+  const int lc = lv ? l : L - 1;                 // padding rows redo the last lambda, no stores
+  BandWork bw(work + cd.work, n, L);
+  const double lam = lvec[lc];
+  double* Lrow = bw.Lf + (int64_t)lc * n * LS;
+  double* yl = bw.Yt + (int64_t)lc * n;
+  const double* LB = bw.LB;                      // row-major band: LB[r][s] = B[r][r-16+s]
+  const double* z = bw.z;
+
+  double w[LS], nx[LS];
+  auto band_row = [&](int r, double (&dst)[LS]) {
+#pragma unroll
+    for (int s = 0; s < LS; ++s)
+      dst[s] = (r < n) ? LB[(int64_t)r * LS + s] + (s == BB ? lam : 0.0) : (s == BB ? 1.0 : 0.0);
+  };
+  // window at j = 0: lane p holds row p, slot k <-> column k
+#pragma unroll
+  for (int k = 0; k < LS; ++k)
+    w[k] = (k <= p && p < n) ? LB[(int64_t)p * LS + BB - p + k] + (k == p ? lam : 0.0)
+                             : (k == p ? 1.0 : 0.0);
+  double zr = (p < n) ? z[p] : 0.0;
+  band_row(p + BB, nx);
+  double znx = (p + BB < n) ? z[p + BB] : 0.0;
+  bool ok = true;
+
+  for (int j0 = 0; j0 < n; j0 += 16) {
+    static_for<0, 16>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      const int j = j0 + u;
+      if (j < n) {
+        const bool pl = (p == u);                // pivot lane: holds row j, takes row j+16
+        const double piv = row_bcast<u>(w[0]);
+        ok = ok && (piv > 0.0);
+        const double inv = 1.0 / sqrt(piv);
+        const double yj = row_bcast<u>(zr) * inv;
+#pragma unroll
+        for (int s = 0; s < LS; ++s) w[s] = pl ? nx[s] : w[s];
+        zr = pl ? znx : zr;
+        const double lval = w[0] * inv;          // l_i, i = (p - u) mod 16, pivot lane: i = 16
+        if (lv && !(dbg & 1)) {
+          const int idx = pl ? BB : ((p - u) & 15);
+          Lrow[(int64_t)j * LS + idx] = lval;
+          if (pl) {
+            Lrow[(int64_t)j * LS] = inv;
+            yl[j] = yj;
+          }
+        }
+        zr -= lval * yj;
+        static_for<1, LS>([&](auto K) {
+          constexpr int k = decltype(K)::value;
+          w[k] -= lval * row_bcast<(u + k) & 15>(lval);
+        });
+#pragma unroll
+        for (int s = 0; s < BB; ++s) w[s] = w[s + 1];
+        if (pl) {
+          band_row(j + 2 * BB, nx);
+          znx = (j + 2 * BB < n) ? z[j + 2 * BB] : 0.0;
+        }
+      }
+    });
+  }
+  // back substitution L^T x = y, x overwrites y.  Lane (j+i) mod 16 holds x_{j+i}.
+  __syncthreads();
+  double xr = 0.0;
+  for (int jt = n - 1; jt >= 0; jt -= 16) {
+    static_for<0, 16>([&](auto V) {
+      constexpr int v = decltype(V)::value;
+      const int j = jt - v;
+      if (j >= 0) {
+        const int u = j & 15;
+        const int i = (p - u) & 15;
+        const double li = (dbg & 1) ? 1e-3 * i : Lrow[(int64_t)j * LS + (i == 0 ? BB : i)];
+        const double inv = (dbg & 1) ? 1.0 : Lrow[(int64_t)j * LS];
+        const double s = row16_sum(li * xr);
+        const double xj = (yl[j] - s) * inv;
+        if (p == u) {
+          xr = xj;
+          if (lv) yl[j] = ok ? xj : __builtin_nan("");
+        }
+      }
+    });
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// kernel 3: beta = Q y, blocked WY, one workgroup per (cell, chunk of 16 lambdas).
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
+    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work,
+    double* __restrict__ beta_out, int64_t ldo) {
+  __shared__ double Ys[BNMAX][LS];
+  __shared__ double red[NWB][BB * BB];
+  const int nch = (L + LC - 1) / LC;
+  const int cell = blockIdx.x / nch, ch = blockIdx.x % nch;
+  const RidgeCellDesc cd = cells[cell];
+  const int n = cd.n;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int c16 = lane & 15, g4 = lane >> 4;
+  BandWork bw(work + cd.work, n, L);
+  const double* A = bw.A;
+  const int l0 = ch * LC;
+  const int lw = min(LC, L - l0);
+  for (int e = t; e < BNMAX * LC; e += NTB) {
+    const int c = e / BNMAX, i = e % BNMAX;
+    Ys[i][c] = (c < lw && i < n) ? bw.Yt[(int64_t)(l0 + c) * n + i] : 0.0;
+  }
+  __syncthreads();
+  const int np = (n - 1) / BB;    // panels: k0 = 16 p with k0 + 16 < n
+  for (int p = np - 1; p >= 0; --p) {
+    const int k0 = p * BB, r0 = k0 + BB, m = n - r0;
+    // V[i][c] of panel p: unit lower trapezoid, strictly-lower part stored in A
+    auto vload = [&](int i, int c) -> double {
+      if (i >= m) return 0.0;
+      return (i > c) ? A[(int64_t)(r0 + i) * n + k0 + c] : (i == c ? 1.0 : 0.0);
+    };
+    // P = V^T Y[r0:]  (K over rows, split across waves in 4-row steps)
+    double4_t Pp = {0.0, 0.0, 0.0, 0.0};
+    for (int k = 4 * wid; k < m; k += 4 * NWB) {
+      const int i = k + g4;
+      Pp = mfma_f64_16x16x4(vload(i, c16), (i < m) ? Ys[r0 + i][c16] : 0.0, Pp);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wid][(g4 + 4 * r) * BB + c16] = Pp[r];
+    __syncthreads();
+    // M = T P
+    const double* Tp = bw.T + (int64_t)p * BB * BB;
+    double4_t Mm = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double pv = 0.0;
+#pragma unroll
+      for (int w = 0; w < NWB; ++w) pv += red[w][(4 * r + g4) * BB + c16];
+      Mm = mfma_f64_16x16x4(Tp[c16 * BB + 4 * r + g4], pv, Mm);
+    }
+    // Y[r0:] -= V M   (row blocks I = wid + 4q)
+    const int nI = (m + 15) >> 4;
+    for (int I = wid; I < nI; I += NWB) {
+      const int i0 = I * 16;
+      double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(vload(i0 + c16, 4 * r + g4), Mm[r], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + g4 + 4 * r;
+        if (i < m) Ys[r0 + i][c16] -= acc[r];
+      }
+    }
+    __syncthreads();
+  }
+  double* out = beta_out + cd.out;
+  for (int e = t; e < lw * n; e += NTB) {
+    const int c = e / n, i = e % n;
+    out[(int64_t)(l0 + c) * ldo + i] = Ys[i][c];
+  }
+}
+
+}  // namespace
+
+extern "C" int64_t pfml_ridge_band_work_doubles(int n, int L) {
+  const int64_t np = (n + BB - 1) / BB;
+  return (int64_t)n * n + (int64_t)n * LS + n + np * BB * BB + (int64_t)L * n +
+         (int64_t)L * n * LS;
+}
+
+extern "C" int pfml_ridge_band_nmax() { return BNMAX; }
+
+extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, const double* Sr,
+                                             const void* cells, int ncells, const double* lvec,
+                                             int L, double* work, double* beta_out, int64_t ldo,
+                                             long long* tim, hipStream_t st) {
+  const RidgeCellDesc* cd = static_cast<const RidgeCellDesc*>(cells);
+  hipLaunchKernelGGL(ridge_band_reduce_kernel, dim3(ncells), dim3(NTR), 0, st, SD, ldS, Sr, cd,
+                     L, work, tim);
+  const char* dbgs = getenv("PFML_BAND_DBG");
+  const int dbg = dbgs ? atoi(dbgs) : 0;
+  if (!(dbg & 2))
+    hipLaunchKernelGGL(ridge_band_solve_kernel, dim3(ncells * ((L + 15) / 16)), dim3(NTS), 0, st,
+                       cd, lvec, L, work, dbg);
+  const int nch = (L + LC - 1) / LC;
+  hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3(ncells * nch), dim3(NTB), 0, st, cd,
+                     L, work, beta_out, ldo);
+  return hipGetLastError();
+}

@@ -75,6 +75,7 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
                                       int(np.max(cell_n)),
                                       lv.data_ptr(), L, work.data_ptr(), beta.data_ptr(), P,
                                       nat.stream_of(SD)), "pfml_ridge_grid")
+        _repair_nonspd(beta, SDc, Src, cell_src, cell_n, cell_scale, lv)
         return beta
     eye_cache = {}
     lv = lvec.to(dtype=SD.dtype)
@@ -90,6 +91,26 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
         sol[info != 0] = float("nan")          # singular system (reference: LinAlgError)
         beta[c, :, :n] = sol
     return beta
+
+
+def _repair_nonspd(beta, SD, Sr, cell_src, cell_n, cell_scale, lv) -> None:
+    """The band path marks a (cell, lambda) whose banded Cholesky met a non-positive pivot
+    (Dbar + l I not numerically SPD) with NaN; re-solve exactly those systems with pivoted LU
+    (np.linalg.solve semantics, PFML_Search_Coef.py:131-133).  One device->host flag read."""
+    bad = torch.isnan(beta).any(dim=-1)
+    if not bool(bad.any()):
+        return
+    for c in torch.nonzero(bad.any(dim=1)).flatten().tolist():
+        ls = torch.nonzero(bad[c]).flatten()
+        n, s = int(cell_n[c]), int(cell_src[c])
+        A = SD[s, :n, :n] * float(cell_scale[c])
+        r = Sr[s, :n] * float(cell_scale[c])
+        eye = torch.eye(n, dtype=A.dtype, device=A.device)
+        sys_ = A.unsqueeze(0) + lv[ls].view(-1, 1, 1) * eye
+        sol, info = torch.linalg.solve_ex(sys_, r.expand(len(ls), n).unsqueeze(-1))
+        sol = sol.squeeze(-1)
+        sol[info != 0] = float("nan")
+        beta[c, ls, :n] = sol
 
 
 def quadform_utilities(D: torch.Tensor, R: torch.Tensor, beta: torch.Tensor,

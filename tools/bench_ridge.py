@@ -37,7 +37,8 @@ def run(ncells, n, reps=3):
 
 
 def timing(n=513, ncells=1):
-    """Per-phase cycle split of the fast tridiagonalisation for one cell."""
+    """Per-phase cycle split of the band reduction (or, with PFML_RIDGE_VARIANT=fast, the
+    fast tridiagonalisation) for one cell."""
     from pfml.ops import _native as nat
     dev = torch.device("cuda", 0)
     buf = torch.zeros(ncells * 8, dtype=torch.int64, device=dev)
@@ -46,7 +47,10 @@ def timing(n=513, ncells=1):
     torch.cuda.synchronize()
     nat.hip_lib().pfml_ridge_set_timing(None)
     t = buf.view(ncells, 8)[0].cpu().numpy()
-    names = ["col_k", "householder", "sweep", "xy", "p_w_z", "trailing", "panel_end", "-"]
+    if os.environ.get("PFML_RIDGE_VARIANT", "band")[:1] in ("f", "t"):
+        names = ["col_k", "householder", "sweep", "xy", "p_w_z", "trailing", "panel_end", "-"]
+    else:
+        names = ["load", "qr", "G_T", "U", "X", "P4_z_W", "trailing", "-"]
     tot = max(1, int(t.sum()))
     return {nm: f"{int(v)} cyc ({100.0 * v / tot:.1f}%)" for nm, v in zip(names, t)}
 
