@@ -28,7 +28,7 @@ import pandas as pd
 import torch
 
 from ..config import Config
-from ..ops.ridge import quadform_utilities, ridge_grid, segment_sums
+from ..ops.ridge import ridge_utilities, segment_sums
 from ..parallel import collectives as coll
 from ..parallel.dist import env as dist_env
 from ..utils.dates import mi_from_ym, month_end
@@ -138,7 +138,7 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
     range_pop()
 
     # ---- 2. ridge grid ---------------------------------------------------------------
-    range_push("search.ridge")
+    range_push("search.ridge_utilities")
     cell_src, cell_n, cell_scale = [], [], []
     for g in range(G):
         for yi, y in enumerate(yl):
@@ -146,13 +146,7 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
                 cell_src.append(g * nYl + yi)
                 cell_n.append(p + 1)
                 cell_scale.append(1.0 / float(max(int(plan.count[y]), 1)))
-    beta = ridge_grid(SD.reshape(G * nYl, P, P), Sr.reshape(G * nYl, P),
-                      np.asarray(cell_src), np.asarray(cell_n), np.asarray(cell_scale), lvec)
-    beta = beta.view(G, nYl, nP, L, P)
-    range_pop()
-
     # ---- 3. utilities for every (cell, validation month) ------------------------------
-    range_push("search.utilities")
     jc, jm, jn = [], [], []
     val_rows = []
     for yi, y in enumerate(yl):
@@ -166,9 +160,14 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
                 jc.append((g * nYl + yi) * nP + pi)
                 jm.append(g * T + m)
                 jn.append(p + 1)
-    obj = quadform_utilities(reals.denom.reshape(G * T, P, P), reals.r_tilde.reshape(G * T, P),
-                             beta.reshape(G * nYl * nP, L, P), np.asarray(jc), np.asarray(jm),
-                             np.asarray(jn))
+    # ridge grid + utilities, big-n cells overlapped with the rest on a second stream
+    beta, obj = ridge_utilities(SD.reshape(G * nYl, P, P), Sr.reshape(G * nYl, P),
+                                np.asarray(cell_src), np.asarray(cell_n),
+                                np.asarray(cell_scale), lvec,
+                                reals.denom.reshape(G * T, P, P),
+                                reals.r_tilde.reshape(G * T, P), np.asarray(jc),
+                                np.asarray(jm), np.asarray(jn))
+    beta = beta.view(G, nYl, nP, L, P)
     obj = obj.view(len(val_rows), G, nP, L)
     range_pop()
 

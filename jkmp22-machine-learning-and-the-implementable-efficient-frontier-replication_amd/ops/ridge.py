@@ -40,10 +40,12 @@ def segment_sums(X: torch.Tensor, starts, stops) -> torch.Tensor:
 
 
 def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n: np.ndarray,
-               cell_scale: np.ndarray, lvec: torch.Tensor) -> torch.Tensor:
+               cell_scale: np.ndarray, lvec: torch.Tensor, repair: bool = True) -> torch.Tensor:
     """beta[c, l, :n_c] = solve(SD[src_c][:n,:n]*scale_c + l I, Sr[src_c][:n]*scale_c).
 
     SD: [S, P, P] running sums, Sr: [S, P]; returns [ncells, L, P] (zero beyond n_c).
+    ``repair=False`` leaves the band path's non-SPD markers (NaN rows) for the caller to
+    repair (``repair_nonspd``), so no device->host sync happens here.
     """
     S, P, _ = SD.shape
     L = int(lvec.numel())
@@ -75,7 +77,8 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
                                       int(np.max(cell_n)),
                                       lv.data_ptr(), L, work.data_ptr(), beta.data_ptr(), P,
                                       nat.stream_of(SD)), "pfml_ridge_grid")
-        _repair_nonspd(beta, SDc, Src, cell_src, cell_n, cell_scale, lv)
+        if repair:
+            repair_nonspd(beta, SDc, Src, cell_src, cell_n, cell_scale, lv)
         return beta
     eye_cache = {}
     lv = lvec.to(dtype=SD.dtype)
@@ -93,14 +96,15 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
     return beta
 
 
-def _repair_nonspd(beta, SD, Sr, cell_src, cell_n, cell_scale, lv) -> None:
+def repair_nonspd(beta, SD, Sr, cell_src, cell_n, cell_scale, lv) -> np.ndarray:
     """The band path marks a (cell, lambda) whose banded Cholesky met a non-positive pivot
     (Dbar + l I not numerically SPD) with NaN; re-solve exactly those systems with pivoted LU
     (np.linalg.solve semantics, PFML_Search_Coef.py:131-133).  One device->host flag read."""
     bad = torch.isnan(beta).any(dim=-1)
     if not bool(bad.any()):
-        return
-    for c in torch.nonzero(bad.any(dim=1)).flatten().tolist():
+        return np.zeros(0, dtype=np.int64)
+    cells = torch.nonzero(bad.any(dim=1)).flatten().tolist()
+    for c in cells:
         ls = torch.nonzero(bad[c]).flatten()
         n, s = int(cell_n[c]), int(cell_src[c])
         A = SD[s, :n, :n] * float(cell_scale[c])
@@ -111,6 +115,62 @@ def _repair_nonspd(beta, SD, Sr, cell_src, cell_n, cell_scale, lv) -> None:
         sol = sol.squeeze(-1)
         sol[info != 0] = float("nan")
         beta[c, ls, :n] = sol
+    return np.asarray(cells, dtype=np.int64)
+
+
+def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_scale,
+                    lvec: torch.Tensor, D: torch.Tensor, R: torch.Tensor, job_cell, job_month,
+                    job_n) -> tuple[torch.Tensor, torch.Tensor]:
+    """(beta, obj) = (ridge_grid(...), quadform_utilities(D, R, beta, jobs)).
+
+    On a device the cells split into the largest-n group and the rest; each group's
+    ridge -> utilities chain is issued on its own HIP stream, the big group first, so the
+    small cells' whole chain runs on the CUs the big cells' one-workgroup-per-cell band
+    reductions leave idle.  Non-SPD repairs (rare) are applied once at the end, and the
+    utilities of repaired cells recomputed.
+    """
+    cell_src, cell_n = np.asarray(cell_src), np.asarray(cell_n)
+    cell_scale = np.asarray(cell_scale)
+    job_cell, job_month, job_n = (np.asarray(job_cell), np.asarray(job_month),
+                                  np.asarray(job_n))
+    if not nat.is_device(SD) or len(np.unique(cell_n)) < 2:
+        beta = ridge_grid(SD, Sr, cell_src, cell_n, cell_scale, lvec)
+        return beta, quadform_utilities(D, R, beta, job_cell, job_month, job_n)
+    S, P, _ = SD.shape
+    L = int(lvec.numel())
+    nc = len(cell_src)
+    beta = torch.zeros((nc, L, P), dtype=SD.dtype, device=SD.device)
+    obj = torch.empty((len(job_cell), L), dtype=SD.dtype, device=SD.device)
+    big = cell_n == cell_n.max()
+    cur = torch.cuda.current_stream(SD.device)
+    side = torch.cuda.Stream(device=SD.device)
+    side.wait_stream(cur)
+    parts = []
+    for grp, stream in ((big, side), (~big, cur)):
+        cells = np.nonzero(grp)[0]
+        remap = np.full(nc, -1, dtype=np.int64)
+        remap[cells] = np.arange(len(cells))
+        jobs = np.nonzero(grp[job_cell])[0]
+        with torch.cuda.stream(stream):
+            b = ridge_grid(SD, Sr, cell_src[cells], cell_n[cells], cell_scale[cells], lvec,
+                           repair=False)
+            o = quadform_utilities(D, R, b, remap[job_cell[jobs]], job_month[jobs],
+                                   job_n[jobs])
+        parts.append((cells, jobs, b, o))
+    cur.wait_stream(side)
+    for t in (SD, Sr, D, R, lvec):
+        t.record_stream(side)
+    for cells, jobs, b, o in parts:
+        ci = torch.as_tensor(cells, device=SD.device)
+        beta.index_copy_(0, ci, b)
+        obj.index_copy_(0, torch.as_tensor(jobs, device=SD.device), o)
+    fixed = repair_nonspd(beta, SD, Sr, cell_src, cell_n, cell_scale,
+                          lvec.to(device=SD.device, dtype=torch.float64))
+    if len(fixed):
+        jobs = np.nonzero(np.isin(job_cell, fixed))[0]
+        obj[torch.as_tensor(jobs, device=SD.device)] = quadform_utilities(
+            D, R, beta, job_cell[jobs], job_month[jobs], job_n[jobs])
+    return beta, obj
 
 
 def quadform_utilities(D: torch.Tensor, R: torch.Tensor, beta: torch.Tensor,
