@@ -37,6 +37,7 @@ import pfml  # noqa: E402
 from pfml.config import Config  # noqa: E402
 from pfml.models.search import PfmlReals, grid_search, validation_scores  # noqa: E402
 from pfml.ops.gemm import gemm  # noqa: E402
+from pfml.ops.ridge import _HostClock  # noqa: E402
 from pfml.parallel import collectives as coll  # noqa: E402
 from pfml.parallel import dist as pdist  # noqa: E402
 from pfml.utils.dates import mi_from_ym  # noqa: E402
@@ -75,8 +76,10 @@ def one_step(reals: PfmlReals, cfg: Config, engine=None):
     res = grid_search(reals, cfg)
     G = res.obj.shape[1]
     out = []
+    th = _HostClock()
     for g in range(G):
         out.append(validation_scores(res.obj, g, cfg.run.compat_mode))
+    th("validation_scores")
     return res, out
 
 

@@ -52,11 +52,13 @@ __global__ __launch_bounds__(256) void quadform_kernel(
   // D_t is symmetric:  b'Db = sum_I b_I'(D_II b_I + 2 sum_{K>I} D_IK b_K).  A row tile I only
   // walks K >= I, with the diagonal block weighted 1/2, so  acc = U_I / 2  and half the
   // flops and D bytes of the full product are spent.  K tiles are double-buffered in LDS
-  // through registers (one barrier per K step).
+  // and prefetched two steps ahead through registers (one barrier per K step).
   constexpr int AQ = (BM * BK) / 256;             // D elements per thread per K step
   constexpr int BQ = (NCOL * BK + 255) / 256;     // beta elements per thread per K step
-  double ra[AQ], rb[BQ];
-  auto gload = [&](int k0) {
+  // two register sets: the global loads of step k+2 are in flight while step k is computed
+  // from LDS and step k+1 is written to the other LDS buffer (prefetch distance 2).
+  double ra0[AQ], rb0[BQ], ra1[AQ], rb1[BQ];
+  auto gload = [&](int k0, double (&ra)[AQ], double (&rb)[BQ]) {
     const double wdiag = (k0 < i0 + BM) ? 0.5 : 1.0;
 #pragma unroll
     for (int q = 0; q < AQ; ++q) {
@@ -70,7 +72,7 @@ __global__ __launch_bounds__(256) void quadform_kernel(
       rb[q] = (e < NCOL * BK && l < L && gk < n) ? bt[(int64_t)l * ldB + gk] : 0.0;
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, const double (&ra)[AQ], const double (&rb)[BQ]) {
 #pragma unroll
     for (int q = 0; q < AQ; ++q) {
       const int e = t + q * 256, i = e / BK, k = e % BK;
@@ -82,13 +84,7 @@ __global__ __launch_bounds__(256) void quadform_kernel(
       if (e < NCOL * BK) Bs[buf][k][l] = rb[q];
     }
   };
-  int buf = 0;
-  gload(i0);
-  sstore(0);
-  __syncthreads();
-  for (int k0 = i0; k0 < n; k0 += BK) {
-    const bool more = k0 + BK < n;
-    if (more) gload(k0 + BK);
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       const double a = As[buf][kk + (lane >> 4)][w * 16 + (lane & 15)];
@@ -96,9 +92,24 @@ __global__ __launch_bounds__(256) void quadform_kernel(
       for (int q = 0; q < NTILE; ++q)
         acc[q] = mfma_f64_16x16x4(a, Bs[buf][kk + (lane >> 4)][q * 16 + (lane & 15)], acc[q]);
     }
-    if (more) sstore(buf ^ 1);
+  };
+  gload(i0, ra0, rb0);
+  sstore(0, ra0, rb0);
+  if (i0 + BK < n) gload(i0 + BK, ra1, rb1);
+  __syncthreads();
+  for (int k0 = i0;;) {
+    if (k0 + 2 * BK < n) gload(k0 + 2 * BK, ra0, rb0);
+    compute(0);
+    if (k0 + BK >= n) break;
+    sstore(1, ra1, rb1);
     __syncthreads();
-    buf ^= 1;
+    k0 += BK;
+    if (k0 + 2 * BK < n) gload(k0 + 2 * BK, ra1, rb1);
+    compute(1);
+    if (k0 + BK >= n) break;
+    sstore(0, ra0, rb0);
+    __syncthreads();
+    k0 += BK;
   }
 
   // epilogue: sum over this wave's 16 rows of  beta_l[i] * (r_i - 1/2 U[i][l])

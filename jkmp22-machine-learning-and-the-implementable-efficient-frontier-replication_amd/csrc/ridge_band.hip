@@ -64,17 +64,31 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+// (row_newbcast reads a valid source lane for every lane, so "old" is never used)
 template <int SEL>
 __device__ __forceinline__ double row_bcast(double v) {   // lane SEL of each 16-lane row
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x150 + SEL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x150 + SEL, 0xF, 0xF, false);
-  return __hiloint2double(hi, lo);
+  // one v_mov_b64_dpp (64-bit DPP supports row_newbcast on gfx90a+/gfx950)
+  const long s = __builtin_bit_cast(long, v);
+  const long r = __builtin_amdgcn_update_dpp(s, s, 0x150 + SEL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, r);
+}
+
+// w += bcast_SEL(src) * m  as ONE v_fmac_f64_dpp (row_newbcast on the DPP source).  The
+// first use after `src` is written must follow a VALU write by 2 wait states: FIRST adds them.
+template <int SEL, bool FIRST>
+__device__ __forceinline__ void fmac_bcast(double& w, double src, double m) {
+  if constexpr (FIRST)
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(w) : "v"(src), "v"(m), "i"(SEL));
+  else
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(w) : "v"(src), "v"(m), "i"(SEL));
 }
 
 template <int CTRL>
 __device__ __forceinline__ double dpp_mov(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
   return __hiloint2double(hi, lo);
 }
 
@@ -443,7 +457,8 @@ constexpr int NTS = 256;      // 4 waves x 4 rows = 16 lambdas per workgroup
 
 __global__ __launch_bounds__(NTS) void ridge_band_solve_kernel(
     const RidgeCellDesc* __restrict__ cells, const double* __restrict__ lvec, int L,
-    double* __restrict__ work, int dbg) {
+    double* __restrict__ work, long long* __restrict__ tim, int ncells) {
+  const long long t_start = (long long)__builtin_amdgcn_s_memtime();
   const int nb = (L + 15) / 16;
   const int cell = blockIdx.x / nb;
   const RidgeCellDesc cd = cells[cell];
@@ -459,7 +474,11 @@ __global__ __launch_bounds__(NTS) void ridge_band_solve_kernel(
   const double* LB = bw.LB;                      // row-major band: LB[r][s] = B[r][r-16+s]
   const double* z = bw.z;
 
-  double w[LS], nx[LS];
+  // w: 32 slots; within a 16-step block at phase u, slot u + k <-> column j + k (k <= 16), so
+  // the window never shifts inside a block (one 16-slot move per block).  Rows >= n are
+  // identity rows (band_row), so every block is a full, branch-free 16 steps.
+  const int npad = (n + 15) & ~15;
+  double w[2 * BB], nx[LS], nx2[LS];
   auto band_row = [&](int r, double (&dst)[LS]) {
 #pragma unroll
     for (int s = 0; s < LS; ++s)
@@ -467,70 +486,88 @@ __global__ __launch_bounds__(NTS) void ridge_band_solve_kernel(
   };
   // window at j = 0: lane p holds row p, slot k <-> column k
 #pragma unroll
-  for (int k = 0; k < LS; ++k)
+  for (int k = 0; k < 2 * BB; ++k)
     w[k] = (k <= p && p < n) ? LB[(int64_t)p * LS + BB - p + k] + (k == p ? lam : 0.0)
                              : (k == p ? 1.0 : 0.0);
   double zr = (p < n) ? z[p] : 0.0;
-  band_row(p + BB, nx);
+  band_row(p + BB, nx);                            // taken by lane p at step p
   double znx = (p + BB < n) ? z[p + BB] : 0.0;
   bool ok = true;
 
-  for (int j0 = 0; j0 < n; j0 += 16) {
+  for (int j0 = 0; j0 < npad; j0 += 16) {
+    // rows entering during the NEXT block, one block of latency to land
+    band_row(j0 + 2 * BB + p, nx2);
+    const double znx2 = (j0 + 2 * BB + p < n) ? z[j0 + 2 * BB + p] : 0.0;
     static_for<0, 16>([&](auto U) {
       constexpr int u = decltype(U)::value;
       const int j = j0 + u;
-      if (j < n) {
-        const bool pl = (p == u);                // pivot lane: holds row j, takes row j+16
-        const double piv = row_bcast<u>(w[0]);
-        ok = ok && (piv > 0.0);
-        const double inv = 1.0 / sqrt(piv);
-        const double yj = row_bcast<u>(zr) * inv;
+      const bool pl = (p == u);                  // pivot lane: holds row j, takes row j+16
+      const double piv = row_bcast<u>(w[u]);
+      ok = ok && (piv > 0.0);
+      const double inv = 1.0 / sqrt(piv);
+      const double yj = row_bcast<u>(zr) * inv;
+      if (pl) {                                  // exec-masked 64-bit moves, no selects
 #pragma unroll
-        for (int s = 0; s < LS; ++s) w[s] = pl ? nx[s] : w[s];
-        zr = pl ? znx : zr;
-        const double lval = w[0] * inv;          // l_i, i = (p - u) mod 16, pivot lane: i = 16
-        if (lv && !(dbg & 1)) {
-          const int idx = pl ? BB : ((p - u) & 15);
-          Lrow[(int64_t)j * LS + idx] = lval;
-          if (pl) {
-            Lrow[(int64_t)j * LS] = inv;
-            yl[j] = yj;
-          }
-        }
-        zr -= lval * yj;
-        static_for<1, LS>([&](auto K) {
-          constexpr int k = decltype(K)::value;
-          w[k] -= lval * row_bcast<(u + k) & 15>(lval);
-        });
-#pragma unroll
-        for (int s = 0; s < BB; ++s) w[s] = w[s + 1];
-        if (pl) {
-          band_row(j + 2 * BB, nx);
-          znx = (j + 2 * BB < n) ? z[j + 2 * BB] : 0.0;
-        }
+        for (int s = 0; s < LS; ++s) w[u + s] = nx[s];
+        zr = znx;
       }
+      const double lval = w[u] * inv;            // l_i, i = (p - u) mod 16, pivot lane: i = 16
+      if (lv && j < n) {                         // uniform branch
+        double* lr = Lrow + (int64_t)j * LS;
+        lr[pl ? BB : ((p - u) & 15)] = lval;
+        lr[0] = inv;                             // same value from all 16 lanes
+        yl[j] = yj;
+      }
+      zr -= lval * yj;
+      const double nl = -lval;
+      static_for<1, LS>([&](auto K) {
+        constexpr int k = decltype(K)::value;
+        fmac_bcast<(u + k) & 15, k == 1>(w[u + k], lval, nl);   // w -= l_k * l_i
+      });
     });
+#pragma unroll
+    for (int s = 0; s < BB; ++s) w[s] = w[s + BB];
+#pragma unroll
+    for (int s = 0; s < LS; ++s) nx[s] = nx2[s];
+    znx = znx2;
   }
-  // back substitution L^T x = y, x overwrites y.  Lane (j+i) mod 16 holds x_{j+i}.
+  // back substitution L^T x = y, x overwrites y.  Lane (j+i) mod 16 holds x_{j+i}.  The
+  // factor columns of a 16-step block are loaded together (one memory latency per block).
   __syncthreads();
+  const long long t_mid = (long long)__builtin_amdgcn_s_memtime();
   double xr = 0.0;
-  for (int jt = n - 1; jt >= 0; jt -= 16) {
+  for (int jt = npad - 1; jt >= 0; jt -= 16) {
+    double pli[16], pinv[16], py[16];
     static_for<0, 16>([&](auto V) {
       constexpr int v = decltype(V)::value;
+      constexpr int u = 15 - v;                  // j & 15 of step j = jt - v
       const int j = jt - v;
-      if (j >= 0) {
-        const int u = j & 15;
-        const int i = (p - u) & 15;
-        const double li = (dbg & 1) ? 1e-3 * i : Lrow[(int64_t)j * LS + (i == 0 ? BB : i)];
-        const double inv = (dbg & 1) ? 1.0 : Lrow[(int64_t)j * LS];
-        const double s = row16_sum(li * xr);
-        const double xj = (yl[j] - s) * inv;
-        if (p == u) {
-          xr = xj;
-          if (lv) yl[j] = ok ? xj : __builtin_nan("");
-        }
-      }
+      const int i = (p - u) & 15;
+      const bool in = j < n;
+      pli[v] = in ? Lrow[(int64_t)j * LS + (i == 0 ? BB : i)] : 0.0;
+      pinv[v] = in ? Lrow[(int64_t)j * LS] : 1.0;
+      py[v] = in ? yl[j] : 0.0;
     });
+    static_for<0, 16>([&](auto V) {
+      constexpr int v = decltype(V)::value;
+      constexpr int u = 15 - v;
+      const double s = row16_sum(pli[v] * xr);
+      const double xj = (py[v] - s) * pinv[v];
+      xr = (p == u) ? xj : xr;
+      py[v] = xj;
+    });
+    if (lv) {
+      static_for<0, 16>([&](auto V) {
+        constexpr int v = decltype(V)::value;
+        const int j = jt - v;
+        if (j < n && p == 15 - v) yl[j] = ok ? py[v] : __builtin_nan("");
+      });
+    }
+  }
+  if (tim != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {   // debug: wave 0 of block 0
+    const long long t_end = (long long)__builtin_amdgcn_s_memtime();
+    tim[(int64_t)ncells * 8 + 0] = t_mid - t_start;
+    tim[(int64_t)ncells * 8 + 1] = t_end - t_mid;
   }
 }
 
@@ -624,11 +661,8 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   const RidgeCellDesc* cd = static_cast<const RidgeCellDesc*>(cells);
   hipLaunchKernelGGL(ridge_band_reduce_kernel, dim3(ncells), dim3(NTR), 0, st, SD, ldS, Sr, cd,
                      L, work, tim);
-  const char* dbgs = getenv("PFML_BAND_DBG");
-  const int dbg = dbgs ? atoi(dbgs) : 0;
-  if (!(dbg & 2))
-    hipLaunchKernelGGL(ridge_band_solve_kernel, dim3(ncells * ((L + 15) / 16)), dim3(NTS), 0, st,
-                       cd, lvec, L, work, dbg);
+  hipLaunchKernelGGL(ridge_band_solve_kernel, dim3(ncells * ((L + 15) / 16)), dim3(NTS), 0, st,
+                     cd, lvec, L, work, tim, ncells);
   const int nch = (L + LC - 1) / LC;
   hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3(ncells * nch), dim3(NTB), 0, st, cd,
                      L, work, beta_out, ldo);

@@ -28,7 +28,7 @@ import pandas as pd
 import torch
 
 from ..config import Config
-from ..ops.ridge import ridge_utilities, segment_sums
+from ..ops.ridge import _HostClock, ridge_utilities, segment_sums
 from ..parallel import collectives as coll
 from ..parallel.dist import env as dist_env
 from ..utils.dates import mi_from_ym, month_end
@@ -94,6 +94,7 @@ class GridResult:
 
 
 def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridResult:
+    th = _HostClock()
     env = dist_env()
     dev = reals.denom.device
     G, T, P = reals.G, reals.denom.shape[1], reals.P
@@ -138,28 +139,30 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
     range_pop()
 
     # ---- 2. ridge grid ---------------------------------------------------------------
+    th("grid_search.window_sums")
     range_push("search.ridge_utilities")
-    cell_src, cell_n, cell_scale = [], [], []
-    for g in range(G):
-        for yi, y in enumerate(yl):
-            for p in p_vec:
-                cell_src.append(g * nYl + yi)
-                cell_n.append(p + 1)
-                cell_scale.append(1.0 / float(max(int(plan.count[y]), 1)))
+    pv = np.asarray(p_vec, dtype=np.int64)
+    gg, yy, pp = np.meshgrid(np.arange(G), np.arange(nYl), np.arange(nP), indexing="ij")
+    cell_src = (gg * nYl + yy).reshape(-1)                 # cell order [g][year][p]
+    cell_n = (pv[pp] + 1).reshape(-1)
+    cnt = np.maximum(np.asarray(plan.count, dtype=np.int64)[yl], 1) if nYl else np.zeros(0)
+    cell_scale = (1.0 / cnt[yy].astype(np.float64)).reshape(-1)
+
     # ---- 3. utilities for every (cell, validation month) ------------------------------
-    jc, jm, jn = [], [], []
-    val_rows = []
-    for yi, y in enumerate(yl):
-        for m in range(plan.val_start[y], plan.val_stop[y]):
-            val_rows.append((m, y))
     # job order: [val month][g][p]  -> obj reshapes to [nValLocal, G, nP, L]
-    for (m, y) in val_rows:
-        yi = int(np.nonzero(yl == y)[0][0])
-        for g in range(G):
-            for pi, p in enumerate(p_vec):
-                jc.append((g * nYl + yi) * nP + pi)
-                jm.append(g * T + m)
-                jn.append(p + 1)
+    vs = np.asarray(plan.val_start, dtype=np.int64)[yl] if nYl else np.zeros(0, np.int64)
+    ve = np.asarray(plan.val_stop, dtype=np.int64)[yl] if nYl else np.zeros(0, np.int64)
+    nv = ve - vs
+    v_yi = np.repeat(np.arange(nYl), nv)                   # local year index per val row
+    v_m = (np.concatenate([np.arange(a, b) for a, b in zip(vs, ve)])
+           if nYl else np.zeros(0, np.int64))
+    val_rows = list(zip(v_m.tolist(), yl[v_yi].tolist()))
+    nVr = len(v_m)
+    vi, g2, p2 = np.meshgrid(np.arange(nVr), np.arange(G), np.arange(nP), indexing="ij")
+    jc = ((g2 * nYl + v_yi[vi]) * nP + p2).reshape(-1)
+    jm = (g2 * T + v_m[vi]).reshape(-1)
+    jn = (pv[p2] + 1).reshape(-1)
+    th("grid_search.plan")
     # ridge grid + utilities, big-n cells overlapped with the rest on a second stream
     beta, obj = ridge_utilities(SD.reshape(G * nYl, P, P), Sr.reshape(G * nYl, P),
                                 np.asarray(cell_src), np.asarray(cell_n),
@@ -171,8 +174,9 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
     obj = obj.view(len(val_rows), G, nP, L)
     range_pop()
 
-    vm = np.asarray([reals.months[m] for m, _ in val_rows], dtype=np.int64)
-    vy = np.asarray([years[y] for _, y in val_rows], dtype=np.int64)
+    th("grid_search.ridge_utilities")
+    vm = np.asarray(reals.months, dtype=np.int64)[v_m]
+    vy = np.asarray(years, dtype=np.int64)[yl[v_yi]] if nYl else np.zeros(0, np.int64)
     if gather and env.is_dist:
         range_push("search.gather")
         obj = coll.all_gather_varlen(obj)

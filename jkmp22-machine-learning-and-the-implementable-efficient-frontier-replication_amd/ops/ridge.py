@@ -39,6 +39,86 @@ def segment_sums(X: torch.Tensor, starts, stops) -> torch.Tensor:
     return out
 
 
+class _HostClock:
+    """PFML_HOST_TIMING=1: print host-side section times (microseconds) to stderr."""
+
+    def __init__(self):
+        import os
+        import time
+        self.on = bool(os.environ.get("PFML_HOST_TIMING"))
+        self.time = time.perf_counter
+        self.t = self.time()
+
+    def __call__(self, what: str) -> None:
+        if self.on:
+            import sys
+            now = self.time()
+            print(f"[host] {what}: {1e6 * (now - self.t):.0f} us", file=sys.stderr)
+            self.t = now
+
+
+def upload(arrays, device) -> list[torch.Tensor]:
+    """Copy several small host arrays to the device with ONE pinned, non-blocking H2D copy
+    (the host never waits for queued kernels).  Returns uint8 device views, one per array."""
+    offs, nbytes = [], 0
+    for a in arrays:
+        offs.append(nbytes)
+        nbytes += (a.nbytes + 255) // 256 * 256
+    host = torch.empty(max(nbytes, 1), dtype=torch.uint8, pin_memory=True)
+    hv = host.numpy()
+    for a, o in zip(arrays, offs):
+        hv[o:o + a.nbytes] = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+    dev = host.to(device, non_blocking=True)
+    return [dev[o:o + a.nbytes] for a, o in zip(arrays, offs)]
+
+
+_WORK_CACHE: dict = {}
+
+
+def _work_doubles(n_arr: np.ndarray, L: int) -> np.ndarray:
+    lib = nat.hip_lib()
+    out = np.empty(len(n_arr), dtype=np.int64)
+    for n in np.unique(n_arr):
+        key = (int(n), L)
+        if key not in _WORK_CACHE:
+            _WORK_CACHE[key] = int(lib.pfml_ridge_work_doubles(int(n), L))
+        out[n_arr == n] = _WORK_CACHE[key]
+    return out
+
+
+def ridge_plan(P: int, L: int, cell_src, cell_n, cell_scale) -> dict:
+    """Host-side descriptors of one ridge-grid launch (CELL_DTYPE, big cells first)."""
+    lib = nat.hip_lib()
+    if lib.pfml_ridge_cell_desc_size() != CELL_DTYPE.itemsize:
+        raise RuntimeError("CellDesc layout mismatch between python and libpfml_hip")
+    nc = len(cell_src)
+    cell_n = np.asarray(cell_n)
+    wsz = _work_doubles(cell_n, L)
+    desc = np.zeros(nc, dtype=CELL_DTYPE)
+    desc["src"] = np.asarray(cell_src, np.int64) * P * P
+    desc["rsrc"] = np.asarray(cell_src, np.int64) * P
+    desc["out"] = np.arange(nc, dtype=np.int64) * L * P
+    desc["n"] = cell_n.astype(np.int32)
+    desc["scale"] = np.asarray(cell_scale, np.float64)
+    # big cells first: they bound the kernel's makespan
+    order = np.argsort(-desc["n"], kind="stable")
+    desc = desc[order]
+    wsz = wsz[order]
+    desc["work"] = np.concatenate([[0], np.cumsum(wsz)[:-1]])
+    return {"desc": desc, "work": int(wsz.sum()), "nmax": int(cell_n.max()), "nc": nc}
+
+
+def ridge_launch(plan: dict, d_desc: torch.Tensor, SD: torch.Tensor, Sr: torch.Tensor,
+                 lv: torch.Tensor, beta: torch.Tensor) -> None:
+    P = SD.shape[-1]
+    L = int(lv.numel())
+    work = torch.empty(plan["work"], dtype=torch.float64, device=SD.device)
+    nat.check(nat.hip_lib().pfml_ridge_grid(SD.data_ptr(), P, Sr.data_ptr(), d_desc.data_ptr(),
+                                            plan["nc"], plan["nmax"], lv.data_ptr(), L,
+                                            work.data_ptr(), beta.data_ptr(), beta.shape[-1],
+                                            nat.stream_of(SD)), "pfml_ridge_grid")
+
+
 def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n: np.ndarray,
                cell_scale: np.ndarray, lvec: torch.Tensor, repair: bool = True) -> torch.Tensor:
     """beta[c, l, :n_c] = solve(SD[src_c][:n,:n]*scale_c + l I, Sr[src_c][:n]*scale_c).
@@ -54,29 +134,11 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
     if nc == 0:
         return beta
     if nat.is_device(SD):
-        lib = nat.hip_lib()
-        if lib.pfml_ridge_cell_desc_size() != CELL_DTYPE.itemsize:
-            raise RuntimeError("CellDesc layout mismatch between python and libpfml_hip")
-        desc = np.zeros(nc, dtype=CELL_DTYPE)
-        wsz = np.array([lib.pfml_ridge_work_doubles(int(n), L) for n in cell_n], dtype=np.int64)
-        woff = np.concatenate([[0], np.cumsum(wsz)[:-1]])
-        desc["src"] = np.asarray(cell_src, np.int64) * P * P
-        desc["rsrc"] = np.asarray(cell_src, np.int64) * P
-        desc["work"] = woff
-        desc["out"] = np.arange(nc, dtype=np.int64) * L * P
-        desc["n"] = np.asarray(cell_n, np.int32)
-        desc["scale"] = np.asarray(cell_scale, np.float64)
-        # big cells first: they bound the kernel's makespan
-        order = np.argsort(-desc["n"], kind="stable")
-        desc = desc[order]
-        d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(SD.device)
-        work = torch.empty(int(wsz.sum()), dtype=torch.float64, device=SD.device)
+        plan = ridge_plan(P, L, cell_src, cell_n, cell_scale)
+        (d_desc,) = upload([plan["desc"]], SD.device)
         lv = lvec.to(device=SD.device, dtype=torch.float64).contiguous()
         SDc, Src = SD.contiguous(), Sr.contiguous()
-        nat.check(lib.pfml_ridge_grid(SDc.data_ptr(), P, Src.data_ptr(), d_desc.data_ptr(), nc,
-                                      int(np.max(cell_n)),
-                                      lv.data_ptr(), L, work.data_ptr(), beta.data_ptr(), P,
-                                      nat.stream_of(SD)), "pfml_ridge_grid")
+        ridge_launch(plan, d_desc, SDc, Src, lv, beta)
         if repair:
             repair_nonspd(beta, SDc, Src, cell_src, cell_n, cell_scale, lv)
         return beta
@@ -118,6 +180,17 @@ def repair_nonspd(beta, SD, Sr, cell_src, cell_n, cell_scale, lv) -> np.ndarray:
     return np.asarray(cells, dtype=np.int64)
 
 
+_SIDE: dict = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    """One cached secondary HIP stream per device (stream creation is not free)."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=dev)
+    return _SIDE[key]
+
+
 def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_scale,
                     lvec: torch.Tensor, D: torch.Tensor, R: torch.Tensor, job_cell, job_month,
                     job_n) -> tuple[torch.Tensor, torch.Tensor]:
@@ -136,41 +209,94 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     if not nat.is_device(SD) or len(np.unique(cell_n)) < 2:
         beta = ridge_grid(SD, Sr, cell_src, cell_n, cell_scale, lvec)
         return beta, quadform_utilities(D, R, beta, job_cell, job_month, job_n)
+    th = _HostClock()
     S, P, _ = SD.shape
     L = int(lvec.numel())
     nc = len(cell_src)
-    beta = torch.zeros((nc, L, P), dtype=SD.dtype, device=SD.device)
-    obj = torch.empty((len(job_cell), L), dtype=SD.dtype, device=SD.device)
+    dev = SD.device
+    beta = torch.zeros((nc, L, P), dtype=SD.dtype, device=dev)
+    obj = torch.empty((len(job_cell), L), dtype=SD.dtype, device=dev)
+    SD, Sr, D, R = SD.contiguous(), Sr.contiguous(), D.contiguous(), R.contiguous()
+    lv = lvec.to(device=dev, dtype=torch.float64).contiguous()
     big = cell_n == cell_n.max()
-    cur = torch.cuda.current_stream(SD.device)
-    side = torch.cuda.Stream(device=SD.device)
-    side.wait_stream(cur)
-    parts = []
-    for grp, stream in ((big, side), (~big, cur)):
+    groups = []
+    for grp in (big, ~big):
         cells = np.nonzero(grp)[0]
         remap = np.full(nc, -1, dtype=np.int64)
         remap[cells] = np.arange(len(cells))
         jobs = np.nonzero(grp[job_cell])[0]
+        rp = ridge_plan(P, L, cell_src[cells], cell_n[cells], cell_scale[cells])
+        qp = quad_plan(P, L, P, remap[job_cell[jobs]], job_month[jobs], job_n[jobs])
+        groups.append((cells, jobs, rp, qp))
+    arrays = []
+    for _, _, rp, qp in groups:
+        arrays += [rp["desc"], qp["desc"], qp["tile_job"]]
+    th("plans")
+    dv = upload(arrays, dev)                     # all descriptors, one async copy
+    th("upload")
+    cur = torch.cuda.current_stream(dev)
+    side = _side_stream(dev)
+    side.wait_stream(cur)
+    outs = []
+    for gi, stream in ((0, side), (1, cur)):     # big cells' factorisations issued first
+        cells, jobs, rp, qp = groups[gi]
         with torch.cuda.stream(stream):
-            b = ridge_grid(SD, Sr, cell_src[cells], cell_n[cells], cell_scale[cells], lvec,
-                           repair=False)
-            o = quadform_utilities(D, R, b, remap[job_cell[jobs]], job_month[jobs],
-                                   job_n[jobs])
-        parts.append((cells, jobs, b, o))
+            b = torch.zeros((len(cells), L, P), dtype=SD.dtype, device=dev)
+            ridge_launch(rp, dv[3 * gi], SD, Sr, lv, b)
+            o = torch.empty((len(jobs), L), dtype=SD.dtype, device=dev)
+            quad_launch(qp, dv[3 * gi + 1], dv[3 * gi + 2], D, R, b, o)
+        outs.append((cells, jobs, b, o))
+    th("launch")
     cur.wait_stream(side)
-    for t in (SD, Sr, D, R, lvec):
+    for t in (SD, Sr, D, R, lv, *dv):
         t.record_stream(side)
-    for cells, jobs, b, o in parts:
-        ci = torch.as_tensor(cells, device=SD.device)
-        beta.index_copy_(0, ci, b)
-        obj.index_copy_(0, torch.as_tensor(jobs, device=SD.device), o)
-    fixed = repair_nonspd(beta, SD, Sr, cell_src, cell_n, cell_scale,
-                          lvec.to(device=SD.device, dtype=torch.float64))
+    for cells, jobs, b, o in outs:
+        b.record_stream(cur)
+        o.record_stream(cur)
+        beta.index_copy_(0, torch.as_tensor(cells, device=dev), b)
+        obj.index_copy_(0, torch.as_tensor(jobs, device=dev), o)
+    th("merge")
+    fixed = repair_nonspd(beta, SD, Sr, cell_src, cell_n, cell_scale, lv)
+    th("repair_check")
     if len(fixed):
         jobs = np.nonzero(np.isin(job_cell, fixed))[0]
         obj[torch.as_tensor(jobs, device=SD.device)] = quadform_utilities(
             D, R, beta, job_cell[jobs], job_month[jobs], job_n[jobs])
     return beta, obj
+
+
+def quad_plan(P: int, L: int, Pb: int, job_cell, job_month, job_n) -> dict:
+    """Host-side descriptors of one utilities launch (JOB_DTYPE + row-tile -> job map)."""
+    lib = nat.hip_lib()
+    if lib.pfml_quadform_job_desc_size() != JOB_DTYPE.itemsize:
+        raise RuntimeError("JobDesc layout mismatch between python and libpfml_hip")
+    rows = lib.pfml_quadform_rows_per_tile()
+    job_n = np.asarray(job_n)
+    nj = len(job_n)
+    ntile = (job_n + rows - 1) // rows
+    pt0 = np.concatenate([[0], np.cumsum(ntile)[:-1]]).astype(np.int32)
+    desc = np.zeros(nj, dtype=JOB_DTYPE)
+    desc["d_off"] = np.asarray(job_month, np.int64) * P * P
+    desc["r_off"] = np.asarray(job_month, np.int64) * P
+    desc["b_off"] = np.asarray(job_cell, np.int64) * L * Pb
+    desc["n"] = job_n.astype(np.int32)
+    desc["ptile0"] = pt0
+    tile_job = np.repeat(np.arange(nj, dtype=np.int32), ntile)
+    return {"desc": desc, "tile_job": tile_job, "nj": nj}
+
+
+def quad_launch(plan: dict, d_desc: torch.Tensor, d_tj: torch.Tensor, D: torch.Tensor,
+                R: torch.Tensor, beta: torch.Tensor, obj: torch.Tensor) -> None:
+    if plan["nj"] == 0:
+        return
+    P = D.shape[-1]
+    L, Pb = beta.shape[1], beta.shape[2]
+    nt = len(plan["tile_job"])
+    partial = torch.empty((nt, L), dtype=torch.float64, device=D.device)
+    nat.check(nat.hip_lib().pfml_quadform(D.data_ptr(), P, R.data_ptr(), beta.data_ptr(), Pb,
+                                          d_desc.data_ptr(), plan["nj"], d_tj.data_ptr(), nt, L,
+                                          partial.data_ptr(), obj.data_ptr(),
+                                          nat.stream_of(D)), "pfml_quadform")
 
 
 def quadform_utilities(D: torch.Tensor, R: torch.Tensor, beta: torch.Tensor,
@@ -184,28 +310,9 @@ def quadform_utilities(D: torch.Tensor, R: torch.Tensor, beta: torch.Tensor,
     if nj == 0:
         return obj
     if nat.is_device(D):
-        lib = nat.hip_lib()
-        if lib.pfml_quadform_job_desc_size() != JOB_DTYPE.itemsize:
-            raise RuntimeError("JobDesc layout mismatch between python and libpfml_hip")
-        rows = lib.pfml_quadform_rows_per_tile()
-        ntile = (np.asarray(job_n) + rows - 1) // rows
-        pt0 = np.concatenate([[0], np.cumsum(ntile)[:-1]]).astype(np.int32)
-        desc = np.zeros(nj, dtype=JOB_DTYPE)
-        desc["d_off"] = np.asarray(job_month, np.int64) * P * P
-        desc["r_off"] = np.asarray(job_month, np.int64) * P
-        desc["b_off"] = np.asarray(job_cell, np.int64) * L * Pb
-        desc["n"] = np.asarray(job_n, np.int32)
-        desc["ptile0"] = pt0
-        tile_job = np.repeat(np.arange(nj, dtype=np.int32), ntile)
-        dev = D.device
-        d_desc = torch.from_numpy(desc.view(np.uint8).copy()).to(dev)
-        d_tj = torch.from_numpy(tile_job).to(dev)
-        partial = torch.empty((len(tile_job), L), dtype=torch.float64, device=dev)
-        Dc, Rc, Bc = D.contiguous(), R.contiguous(), beta.contiguous()
-        nat.check(lib.pfml_quadform(Dc.data_ptr(), P, Rc.data_ptr(), Bc.data_ptr(), Pb,
-                                    d_desc.data_ptr(), nj, d_tj.data_ptr(), len(tile_job), L,
-                                    partial.data_ptr(), obj.data_ptr(), nat.stream_of(D)),
-                  "pfml_quadform")
+        plan = quad_plan(P, L, Pb, job_cell, job_month, job_n)
+        d_desc, d_tj = upload([plan["desc"], plan["tile_job"]], D.device)
+        quad_launch(plan, d_desc, d_tj, D.contiguous(), R.contiguous(), beta.contiguous(), obj)
         return obj
     for j in range(nj):
         n, m, c = int(job_n[j]), int(job_month[j]), int(job_cell[j])

@@ -41,18 +41,22 @@ def timing(n=513, ncells=1):
     fast tridiagonalisation) for one cell."""
     from pfml.ops import _native as nat
     dev = torch.device("cuda", 0)
-    buf = torch.zeros(ncells * 8, dtype=torch.int64, device=dev)
+    buf = torch.zeros(ncells * 8 + 16, dtype=torch.int64, device=dev)
     nat.hip_lib().pfml_ridge_set_timing(buf.data_ptr())
     run(ncells, n, reps=1)
     torch.cuda.synchronize()
     nat.hip_lib().pfml_ridge_set_timing(None)
-    t = buf.view(ncells, 8)[0].cpu().numpy()
+    allb = buf.cpu().numpy()
+    t = allb[:ncells * 8].reshape(ncells, 8)[0]
+    extra = {"solve_fwd_cyc": int(allb[ncells * 8]), "solve_bwd_cyc": int(allb[ncells * 8 + 1])}
     if os.environ.get("PFML_RIDGE_VARIANT", "band")[:1] in ("f", "t"):
         names = ["col_k", "householder", "sweep", "xy", "p_w_z", "trailing", "panel_end", "-"]
     else:
         names = ["load", "qr", "G_T", "U", "X", "P4_z_W", "trailing", "-"]
     tot = max(1, int(t.sum()))
-    return {nm: f"{int(v)} cyc ({100.0 * v / tot:.1f}%)" for nm, v in zip(names, t)}
+    out = {nm: f"{int(v)} cyc ({100.0 * v / tot:.1f}%)" for nm, v in zip(names, t)}
+    out.update(extra)
+    return out
 
 
 if __name__ == "__main__":
