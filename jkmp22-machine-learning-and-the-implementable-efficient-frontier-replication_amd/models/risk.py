@@ -4,13 +4,14 @@ Pipeline, batched instead of per-day / per-month Python loops:
 
 1. cluster ranks (K25): a masked GEMM of the ranked characteristics with a signed membership
    matrix (direction -1 columns enter as 1 - x), then a per-month z-score;
-2. daily cross-sectional OLS (K21): rows sorted by trading day, padded into a [days, n_max, K]
-   batch, X'X and X'y as batched GEMMs, one batched solve, pinv fallback for singular days
-   (:224-229) - instead of a full-array mask scan per day (the reference's ~182 s hot spot);
-3. EWMA factor covariance (K22): every month-end's trailing window gathered into one
-   [months, obs, K] batch; the weighted, unbiased cov.wt / cor.wt of General_functions.py:745-835;
-4. EWMA idiosyncratic vol (K23): native per-stock scan (runtime/panel.cpp, HIP kernel on
-   device panels), then the >= 200-of-252-days filter and the last observation per month;
+2. daily cross-sectional OLS (K21): rows sorted by trading day into CSR day segments, one
+   workgroup per day on the device (csrc/risk.hip: [X|y]'[X|y] on MFMA, pivoted LU, residuals),
+   pinv fallback for exactly singular days (:224-229) - instead of a full-array mask scan per day (the reference's ~182 s hot spot);
+3. EWMA factor covariance (K22): one workgroup per month-end over its trailing window of
+   daily factor returns (csrc/risk.hip): the weighted, unbiased cov.wt / cor.wt of
+   General_functions.py:745-835 and F = sd cor sd * 21 fused;
+4. EWMA idiosyncratic vol (K23): csrc/risk.hip wave-per-stock affine scan on the device
+   (runtime/panel.cpp sequential scan on the CPU path), then the >= 200-of-252-days filter and the last observation per month;
 5. Barra assembly (:453-494): size-group median imputation, F * 21, ivol = res_vol^2 * 21.
 
 Output: ``BarraCov`` - per month-end the sorted ids, loadings X (N x K), factor cov F (K x K,
@@ -129,33 +130,19 @@ def weighted_cov(X: torch.Tensor, w: torch.Tensor, cor: bool) -> torch.Tensor:
 
 
 def daily_ols(X: np.ndarray, y: np.ndarray, day: np.ndarray, device) -> tuple:
-    """Per-day OLS without intercept (Estimate Covariance Matrix.py:193-264), batched.
+    """Per-day OLS without intercept (Estimate Covariance Matrix.py:193-264).
 
-    Rows must be sorted by ``day``.  Returns (unique days, coef [D, K], residuals [R])."""
+    Rows must be sorted by ``day``; each day is a CSR segment (no full-array mask scan per
+    day).  Device: csrc/risk.hip daily_ols_kernel (Z'Z on MFMA + pivoted LU per day, pinv
+    fallback for exactly singular days).  Returns (unique days, coef [D, K], residuals [R],
+    number of pinv fallbacks)."""
+    from ..ops.risk_kernels import daily_ols as _ols
     gs = rt.group_starts(day.astype(np.int64))
-    D = len(gs) - 1
-    cnt = np.diff(gs)
-    nmax = int(cnt.max())
-    K = X.shape[1]
-    pos = np.arange(len(y)) - np.repeat(gs[:-1], cnt)
-    drow = np.repeat(np.arange(D), cnt)
     dev = torch.device(device)
-    Xp = torch.zeros((D, nmax, K), dtype=torch.float64, device=dev)
-    yp = torch.zeros((D, nmax, 1), dtype=torch.float64, device=dev)
-    di, pi = torch.as_tensor(drow, device=dev), torch.as_tensor(pos, device=dev)
-    Xp[di, pi] = torch.as_tensor(X, dtype=torch.float64, device=dev)
-    yp[di, pi, 0] = torch.as_tensor(y, dtype=torch.float64, device=dev)
-    XtX = Xp.transpose(1, 2) @ Xp
-    Xty = Xp.transpose(1, 2) @ yp
-    coef, info = torch.linalg.solve_ex(XtX, Xty)
-    bad = info != 0
-    nbad = int(bad.sum().item())
-    if nbad:
-        COUNTERS.add("risk.ols_pinv_fallback", nbad)
-        coef[bad] = torch.linalg.pinv(XtX[bad], rtol=1e-15) @ Xty[bad]
-    fitted = (Xp @ coef)[di, pi, 0]
-    resid = torch.as_tensor(y, dtype=torch.float64, device=dev) - fitted
-    return day[gs[:-1]], coef.squeeze(-1).cpu().numpy(), resid.cpu().numpy(), nbad
+    Xt = torch.as_tensor(np.ascontiguousarray(X, np.float64), device=dev)
+    yt = torch.as_tensor(np.ascontiguousarray(y, np.float64), device=dev)
+    coef, resid, nbad = _ols(Xt, yt, torch.as_tensor(gs))
+    return day[gs[:-1]], coef.cpu().numpy(), resid.cpu().numpy(), nbad
 
 
 def estimate_cov(cfg: Config, device: str = "cpu", write: bool = True) -> BarraCov:
@@ -212,28 +199,19 @@ def estimate_cov(cfg: Config, device: str = "cpu", write: bool = True) -> BarraC
     calc = np.sort(cm.loc[cm["eom"] >= min_date, "eom"].unique())
     calc_mi = month_index(calc)
     end_idx = np.searchsorted(day_dt, np.asarray(calc, dtype="datetime64[D]"), side="right")
-    B, K = len(calc), len(factor_cols)
     dev = torch.device(device)
+    from ..ops.risk_kernels import ewma_factor_cov, ewma_vol as _ewma_vol
     fr = torch.as_tensor(coef, dtype=torch.float64, device=dev)
-    win = torch.zeros((B, obs, K), dtype=torch.float64, device=dev)
-    wc = torch.zeros((B, obs), dtype=torch.float64, device=dev)
-    wv = torch.zeros((B, obs), dtype=torch.float64, device=dev)
-    for b, e in enumerate(end_idx):
-        t = min(obs, int(e))
-        win[b, obs - t:] = fr[e - t:e]
-        wc[b, obs - t:] = torch.as_tensor(w_cor[-t:], device=dev)
-        wv[b, obs - t:] = torch.as_tensor(w_var[-t:], device=dev)
-    cor = weighted_cov(win, wc, cor=True)
-    var = weighted_cov(win, wv, cor=False)
-    sd = torch.sqrt(torch.diagonal(var, dim1=1, dim2=2))
-    Fm = (sd.unsqueeze(-1) * cor * sd.unsqueeze(-2) * 21.0).cpu().numpy()
+    Fm = ewma_factor_cov(fr, end_idx, obs, w_cor, w_var, scale=21.0).cpu().numpy()
 
     # ---- idiosyncratic EWMA vol (:345-442) -----------------------------------------
     sr = pd.DataFrame({"id": dm["id"].to_numpy(np.int64), "date": dnum, "residual": resid})
     sr = sr.sort_values(["id", "date"], kind="stable").reset_index(drop=True)
     gs = rt.group_starts(sr["id"].to_numpy())
     lam = 0.5 ** (1.0 / cs["hl_stock_var"])
-    sr["res_vol"] = rt.ewma_vol(sr["residual"].to_numpy(), gs, lam, int(cs["initial_var_obs"]))
+    rv = _ewma_vol(torch.as_tensor(sr["residual"].to_numpy(), device=dev), gs, lam,
+                   int(cs["initial_var_obs"]))
+    sr["res_vol"] = rv.cpu().numpy()
     td = pd.Series(days)
     td252 = pd.DataFrame({"date": days, "td_252d": td.shift(252).to_numpy()})
     sr = sr.merge(td252, on="date", how="left")
@@ -261,7 +239,7 @@ def estimate_cov(cfg: Config, device: str = "cpu", write: bool = True) -> BarraC
     barra = BarraCov(months=calc_mi.astype(np.int64), offsets=np.asarray(off, np.int64),
                      ids=np.concatenate(ids_l), X=np.concatenate(X_l), ivol=np.concatenate(iv_l),
                      F=Fm, factors=factor_cols)
-    log.info(f"Barra covariance for {len(calc_mi)} months, K = {K} factors.")
+    log.info(f"Barra covariance for {len(calc_mi)} months, K = {len(factor_cols)} factors.")
     if write:
         barra.save(os.path.join(dd, "Barra_Cov.npz"))
     return barra

@@ -1,0 +1,70 @@
+"""Risk-model kernels (csrc/risk.hip, K21-K23) vs the fp64 CPU oracle of the same op."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_daily_ols_matches_lstsq(gpu):
+    from pfml.ops.risk_kernels import daily_ols
+    rng = np.random.default_rng(0)
+    K = 25
+    sizes = [1, 30, 64, 65, 200, 513, 7]
+    off = np.r_[0, np.cumsum(sizes)]
+    R = off[-1]
+    X = rng.standard_normal((R, K))
+    X[:, :12] = (rng.integers(0, 12, R)[:, None] == np.arange(12)[None, :])   # FF12 dummies
+    y = rng.standard_normal(R) * 0.02
+    coef, resid, nbad = daily_ols(torch.tensor(X, device=gpu), torch.tensor(y, device=gpu),
+                                  torch.tensor(off))
+    coef, resid = coef.cpu().numpy(), resid.cpu().numpy()
+    for d in range(len(sizes)):
+        a, b = off[d], off[d + 1]
+        Xd, yd = X[a:b], y[a:b]
+        try:
+            ref = np.linalg.solve(Xd.T @ Xd, Xd.T @ yd)
+        except np.linalg.LinAlgError:
+            ref = np.linalg.pinv(Xd.T @ Xd) @ (Xd.T @ yd)
+        if b - a >= K and np.linalg.matrix_rank(Xd) == K:
+            assert np.allclose(coef[d], ref, rtol=1e-8, atol=1e-10), d
+            assert np.allclose(resid[a:b], yd - Xd @ ref, atol=1e-10), d
+    # the 1-row day is exactly singular: pinv fallback applied
+    assert nbad >= 1
+    assert np.all(np.isfinite(coef)) and np.all(np.isfinite(resid))
+
+
+def test_ewma_factor_cov_matches_cov_wt(gpu):
+    from pfml.ops.risk_kernels import ewma_factor_cov
+    rng = np.random.default_rng(1)
+    days, K, obs = 700, 25, 300
+    fr = rng.standard_normal((days, K)) * 0.01 + 0.001
+    tr = np.arange(obs, 0, -1, dtype=np.float64)
+    w_cor = (0.5 ** (1 / 90.0)) ** tr
+    w_var = (0.5 ** (1 / 30.0)) ** tr
+    ends = np.array([5, 64, 300, 301, 512, 700])
+    F_cpu, c_cpu, v_cpu = ewma_factor_cov(torch.tensor(fr), ends, obs, w_cor, w_var,
+                                          return_parts=True)
+    F, c, v = ewma_factor_cov(torch.tensor(fr, device=gpu), ends, obs, w_cor, w_var,
+                              return_parts=True)
+    assert torch.allclose(F.cpu(), F_cpu, rtol=1e-11, atol=1e-16)
+    assert torch.allclose(c.cpu(), c_cpu, rtol=1e-11, atol=1e-12)
+    assert torch.allclose(v.cpu(), v_cpu, rtol=1e-11, atol=1e-18)
+
+
+def test_ewma_vol_matches_numba_semantics(gpu):
+    from pfml import runtime as rt
+    from pfml.ops.risk_kernels import ewma_vol
+    rng = np.random.default_rng(2)
+    sizes = [10, 63, 64, 65, 300, 1000, 130]
+    gs = np.r_[0, np.cumsum(sizes)]
+    x = rng.standard_normal(gs[-1]) * 0.02
+    x[rng.random(gs[-1]) < 0.05] = np.nan
+    x[gs[5]:gs[5] + 62] = np.nan          # only one valid obs in the start window -> all NaN
+    x[gs[5] + 10] = 0.01
+    lam = 0.5 ** (1 / 126)
+    ref = rt.ewma_vol(x, gs, lam, 63)
+    out = ewma_vol(torch.tensor(x, device=gpu), gs, lam, 63).cpu().numpy()
+    assert np.array_equal(np.isnan(out), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    assert np.allclose(out[ok], ref[ok], rtol=1e-12, atol=0)
