@@ -908,8 +908,9 @@ __global__ __launch_bounds__(NT) void ridge_backtransform_kernel(
 extern "C" int64_t pfml_ridge_band_work_doubles(int n, int L);
 extern "C" int pfml_ridge_band_nmax();
 extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, const double* Sr,
-                                             const void* cells, int ncells, const double* lvec,
-                                             int L, double* work, double* beta_out, int64_t ldo,
+                                             const void* cells, int ncells, int nmax,
+                                             const double* lvec, int L, double* work,
+                                             double* beta_out, int64_t ldo, int band_mode,
                                              long long* tim, hipStream_t st);
 
 // Workspace per cell: enough for whichever path the launcher picks (band path: ridge_band.hip).
@@ -923,10 +924,11 @@ static long long* g_ridge_timing = nullptr;
 // Debug: per-cell phase cycle counters of the fast tridiagonalisation (8 per cell).
 extern "C" void pfml_ridge_set_timing(long long* buf) { g_ridge_timing = buf; }
 
+// band_mode: 0 = PFML_BAND_MODE / default, 1 = one workgroup per cell, 2 = multi-workgroup
 extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const double* Sr,
                                       const void* cells, int ncells, int nmax,
                                       const double* lvec, int L, double* work, double* beta_out,
-                                      int64_t ldo, hipStream_t st) {
+                                      int64_t ldo, int band_mode, hipStream_t st) {
   if (ncells <= 0) return hipSuccess;
   if (L > 128 || nmax > NMAX) return hipErrorInvalidValue;
   const CellDesc* cd = static_cast<const CellDesc*>(cells);
@@ -937,8 +939,8 @@ extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const doubl
   const bool force_fast = var && (var[0] == 'f' || var[0] == 't');
   if (!force_unblocked && !force_blocked && !force_fast && !getenv("PFML_RIDGE_UNBLOCKED") &&
       nmax <= pfml_ridge_band_nmax())
-    return pfml_ridge_band_launch(SD, ldS, Sr, cells, ncells, lvec, L, work, beta_out, ldo,
-                                  g_ridge_timing, st);
+    return pfml_ridge_band_launch(SD, ldS, Sr, cells, ncells, nmax, lvec, L, work, beta_out,
+                                  ldo, band_mode, g_ridge_timing, st);
   if (force_unblocked || (getenv("PFML_RIDGE_UNBLOCKED") != nullptr))
     hipLaunchKernelGGL(ridge_tridiag_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr, cd, L,
                        work);

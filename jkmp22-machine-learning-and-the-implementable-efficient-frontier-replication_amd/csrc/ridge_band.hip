@@ -16,7 +16,9 @@
 // per lambda, register window with DPP broadcasts, O(n BB^2)), and beta = Q y is a blocked-WY back-transform
 // (MFMA, Y chunk of 16 lambdas resident in LDS).
 //
-//   kernel 1  ridge_band_reduce_kernel       one 512-thread workgroup per cell
+//   kernel 1  band_mk_{panel,x,trail}_kernel three launches per panel, many workgroups per
+//                                            cell (ridge_band_reduce_kernel: one 512-thread
+//                                            workgroup per cell, PFML_BAND_MODE=single)
 //   kernel 2  ridge_band_solve_kernel        4 lambdas per wave (16-lane DPP rows)
 //   kernel 3  ridge_band_backtransform_kernel one 256-thread workgroup per (cell, 16 lambdas)
 //
@@ -37,13 +39,13 @@ constexpr int BNMAX = BMP + BB;     // 528 >= p_max + 1
 constexpr int NTR = 512;            // reduce kernel: 8 waves
 constexpr int NWR = NTR / 64;
 constexpr int TBR = 4;              // trailing-update tiles per wave per pass
-constexpr int NTB = 256;            // back-transform kernel: 4 waves
+constexpr int NTB = 512;            // back-transform kernel: 8 waves
 constexpr int NWB = NTB / 64;
 constexpr int LC = 16;              // lambdas per back-transform workgroup
 
 // Per-cell workspace layout (doubles).
 struct BandWork {
-  double *A, *LB, *z, *T, *Yt, *Lf;
+  double *A, *LB, *z, *T, *Yt, *Lf, *Vg, *Ug, *Xg, *Pg;
   __device__ BandWork(double* w, int n, int L) {
     const int np = (n + BB - 1) / BB;
     A = w;                                   // n x n working matrix (V_p / R_p stored below)
@@ -52,6 +54,10 @@ struct BandWork {
     T = z + n;                               // np x 16 x 16 compact-WY T_p
     Yt = T + (int64_t)np * BB * BB;          // L x n   solutions y_l, then beta_l
     Lf = Yt + (int64_t)L * n;                // L x n x LS banded Cholesky factors
+    Vg = Lf + (int64_t)L * n * LS;           // multi-workgroup path: panel V   (BMP x 16)
+    Ug = Vg + BMP * BB;                      //                        U = V T  (BMP x 16)
+    Xg = Ug + BMP * BB;                      //                        X = A U  (BMP x 16)
+    Pg = Xg + BMP * BB;                      //                        V_I^T X_I partials
   }
 };
 
@@ -137,6 +143,139 @@ __device__ __forceinline__ void band_x_accum(const double* __restrict__ A, int n
   }
 }
 
+// P1 + P2 + T of one panel, by one NTR-thread workgroup: the m x 16 panel below the band
+// (columns r0.. of rows k0..k0+15 of the symmetric A) is QR-factored by Householder in
+// registers; V (unit lower trapezoid) -> Vs, V and R -> A's panel columns, the compact-WY T
+// (dlarft) -> Ts and Tglob.  Ends with a barrier.
+__device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n, int k0, int r0,
+                                                  int m, double (*Vs)[LS], double (*Gs)[LS],
+                                                  double* redf, double (*Ts)[LS], double* taus,
+                                                  double* __restrict__ Tglob) {
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int cq = t & 15, rg = t >> 4;
+  // ---- P1: panel A[r0:, k0:k0+16] -> Vs (read as rows k0..k0+15 of the symmetric A)
+  for (int e = t; e < BB * BMP; e += NTR) {
+    const int c = e / BMP, i = e % BMP;
+    Vs[i][c] = (i < m) ? A[(int64_t)(k0 + c) * n + r0 + i] : 0.0;
+  }
+  __syncthreads();
+  // ---- P2: Householder QR of the m x 16 panel in REGISTERS: thread (rg, cq) holds rows
+  //      i = rg + 32 q (q < 16) of column cq; column j reaches the 16 lanes of a row group by
+  //      a row_newbcast DPP move; one barrier per column (cross-wave sums, ping-pong
+  //      buffers).  The dlarft dots G[:, j-1] = V^T v_{j-1} ride in the same reduction.
+  double a[16], vp[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    a[q] = Vs[rg + 32 * q][cq];
+    vp[q] = 0.0;
+  }
+  static_for<0, BB + 1>([&](auto J) {
+    constexpr int j = decltype(J)::value;      // j == BB: only the last G column
+    const int par = j & 1;
+    double x[16];
+    double s1p[4] = {0.0, 0.0, 0.0, 0.0}, s2p[4] = {0.0, 0.0, 0.0, 0.0};
+    // Only row group q = 0 (rows < 32) meets the diagonal; row groups at or beyond m are
+    // all-zero and skipped (wave-uniform branch).  Four partial sums break the FMA chains.
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      if (q > 0 && 32 * q >= m) continue;
+      const int i = rg + 32 * q;
+      if constexpr (j < BB) {
+        x[q] = row_bcast<j < BB ? j : 0>(a[q]);
+        s1p[q & 3] += (q > 0 || i > j) ? x[q] * a[q] : 0.0;
+      }
+      if constexpr (j > 0) {
+        const double vex = (q > 0 || i > cq) ? a[q] : ((i == cq && i < m) ? 1.0 : 0.0);
+        s2p[q & 3] += vp[q] * vex;
+      }
+    }
+    double s1 = (s1p[0] + s1p[1]) + (s1p[2] + s1p[3]);
+    double s2 = (s2p[0] + s2p[1]) + (s2p[2] + s2p[3]);
+    s1 += __shfl_xor(s1, 16, 64);
+    s1 += __shfl_xor(s1, 32, 64);
+    s2 += __shfl_xor(s2, 16, 64);
+    s2 += __shfl_xor(s2, 32, 64);
+    if (lane < 16) {
+      redf[par * 256 + wid * 16 + lane] = s1;
+      redf[512 + par * 256 + wid * 16 + lane] = s2;
+    }
+    if constexpr (j < BB) {
+      if (rg == j) redf[1024 + par * 16 + cq] = a[0];     // row j (q = 0)
+    }
+    __syncthreads();
+    if constexpr (j > 0) {
+      if (t < BB) {
+        double g = 0.0;
+#pragma unroll
+        for (int w = 0; w < NWR; ++w) g += redf[512 + par * 256 + w * 16 + t];
+        Gs[t][j - 1] = g;                                 // G[t][j-1]
+      }
+    }
+    if constexpr (j < BB) {
+      double xn2 = 0.0, dc = 0.0;
+#pragma unroll
+      for (int w = 0; w < NWR; ++w) {
+        xn2 += redf[par * 256 + w * 16 + j];
+        dc += redf[par * 256 + w * 16 + cq];
+      }
+      const double alpha = redf[1024 + par * 16 + j];
+      const double vjc = redf[1024 + par * 16 + cq];
+      double tau, beta, scal;
+      if (xn2 == 0.0) {
+        tau = 0.0; beta = alpha; scal = 0.0;
+      } else {
+        beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
+        tau = (beta - alpha) / beta;
+        scal = 1.0 / (alpha - beta);
+      }
+      const double wc = tau * (vjc + scal * dc);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        if (q > 0 && 32 * q >= m) continue;
+        const int i = rg + 32 * q;
+        if (q == 0) {
+          const double v = (i > j) ? x[q] * scal : ((i == j && i < m) ? 1.0 : 0.0);
+          if (cq > j) a[q] -= v * wc;
+          else if (cq == j) a[q] = (i > j) ? v : ((i == j) ? beta : a[q]);
+          vp[q] = v;
+        } else {
+          const double v = x[q] * scal;
+          a[q] = (cq > j) ? a[q] - v * wc : ((cq == j) ? v : a[q]);
+          vp[q] = v;
+        }
+      }
+      if (t == 0) taus[j] = tau;
+    }
+  });
+  // explicit V -> Vs (MFMA operand); V (strictly lower) and R (upper) -> A's panel columns
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int i = rg + 32 * q;
+    Vs[i][cq] = (i > cq) ? a[q] : ((i == cq && i < m) ? 1.0 : 0.0);
+    if (i < m) A[(int64_t)(r0 + i) * n + k0 + cq] = a[q];
+  }
+  __syncthreads();
+  // ---- T (dlarft, forward columnwise): T[j][j] = tau_j,
+  //      T[0:j, j] = -tau_j T[0:j, 0:j] G[0:j, j]   (one wave, lane = row)
+  if (wid == 0) {                    // lane = row i: T[i][0:j] stays in registers
+    double trow[BB];
+    static_for<0, BB>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < j; ++k) s += trow[k] * Gs[k][j];   // G[k][j]: LDS broadcast
+      trow[j] = (lane < j) ? -taus[j] * s : (lane == j ? taus[j] : 0.0);
+    });
+    if (lane < BB) {
+#pragma unroll
+      for (int j = 0; j < BB; ++j) Ts[lane][j] = trow[j];
+    }
+  }
+  __syncthreads();
+  if (t < BB * BB) Tglob[t] = Ts[t / BB][t % BB];
+}
+
 __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
     const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
     const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work,
@@ -178,112 +317,8 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
   if (tim != nullptr && threadIdx.x == 0) tlast = (long long)__builtin_amdgcn_s_memtime();
   for (int k0 = 0; k0 + BB < n; k0 += BB) {
     const int r0 = k0 + BB, m = n - r0, p = k0 / BB;
-    // ---- P1: panel A[r0:, k0:k0+16] -> Vs (read as rows k0..k0+15 of the symmetric A)
-    for (int e = t; e < BB * BMP; e += NTR) {
-      const int c = e / BMP, i = e % BMP;
-      Vs[i][c] = (i < m) ? A[(int64_t)(k0 + c) * n + r0 + i] : 0.0;
-    }
-    __syncthreads();
-    BAND_TMARK(0)
-    // ---- P2: Householder QR of the m x 16 panel in REGISTERS: thread (rg, cq) holds rows
-    //      i = rg + 32 q (q < 16) of column cq; column j reaches the 16 lanes of a row group by
-    //      a row_newbcast DPP move; one barrier per column (cross-wave sums, ping-pong
-    //      buffers).  The dlarft dots G[:, j-1] = V^T v_{j-1} ride in the same reduction.
-    double* redf = &red[0][0];
-    double a[16], vp[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      a[q] = Vs[rg + 32 * q][cq];
-      vp[q] = 0.0;
-    }
-    static_for<0, BB + 1>([&](auto J) {
-      constexpr int j = decltype(J)::value;      // j == BB: only the last G column
-      const int par = j & 1;
-      double x[16];
-      double s1 = 0.0, s2 = 0.0;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int i = rg + 32 * q;
-        if constexpr (j < BB) {
-          x[q] = row_bcast<j < BB ? j : 0>(a[q]);
-          s1 += (i > j) ? x[q] * a[q] : 0.0;
-        }
-        if constexpr (j > 0) {
-          const double vex = (i > cq) ? a[q] : ((i == cq && i < m) ? 1.0 : 0.0);
-          s2 += vp[q] * vex;
-        }
-      }
-      s1 += __shfl_xor(s1, 16, 64);
-      s1 += __shfl_xor(s1, 32, 64);
-      s2 += __shfl_xor(s2, 16, 64);
-      s2 += __shfl_xor(s2, 32, 64);
-      if (lane < 16) {
-        redf[par * 256 + wid * 16 + lane] = s1;
-        redf[512 + par * 256 + wid * 16 + lane] = s2;
-      }
-      if constexpr (j < BB) {
-        if (rg == j) redf[1024 + par * 16 + cq] = a[0];     // row j (q = 0)
-      }
-      __syncthreads();
-      if constexpr (j > 0) {
-        if (t < BB) {
-          double g = 0.0;
-#pragma unroll
-          for (int w = 0; w < NWR; ++w) g += redf[512 + par * 256 + w * 16 + t];
-          Ws[t][j - 1] = g;                                 // G[t][j-1]
-        }
-      }
-      if constexpr (j < BB) {
-        double xn2 = 0.0, dc = 0.0;
-#pragma unroll
-        for (int w = 0; w < NWR; ++w) {
-          xn2 += redf[par * 256 + w * 16 + j];
-          dc += redf[par * 256 + w * 16 + cq];
-        }
-        const double alpha = redf[1024 + par * 16 + j];
-        const double vjc = redf[1024 + par * 16 + cq];
-        double tau, beta, scal;
-        if (xn2 == 0.0) {
-          tau = 0.0; beta = alpha; scal = 0.0;
-        } else {
-          beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
-          tau = (beta - alpha) / beta;
-          scal = 1.0 / (alpha - beta);
-        }
-        const double wc = tau * (vjc + scal * dc);
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int i = rg + 32 * q;
-          const double v = (i > j) ? x[q] * scal : ((i == j && i < m) ? 1.0 : 0.0);
-          if (cq > j) a[q] -= v * wc;
-          else if (cq == j) a[q] = (i > j) ? v : ((i == j) ? beta : a[q]);
-          vp[q] = v;
-        }
-        if (t == 0) taus[j] = tau;
-      }
-    });
-    // explicit V -> Vs (MFMA operand); V (strictly lower) and R (upper) -> A's panel columns
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int i = rg + 32 * q;
-      Vs[i][cq] = (i > cq) ? a[q] : ((i == cq && i < m) ? 1.0 : 0.0);
-      if (i < m) A[(int64_t)(r0 + i) * n + k0 + cq] = a[q];
-    }
-    __syncthreads();
+    band_panel_factor(A, n, k0, r0, m, Vs, Ws, &red[0][0], Ts, taus, bw.T + (int64_t)p * BB * BB);
     BAND_TMARK(1)
-    // ---- T (dlarft, forward columnwise): T[j][j] = tau_j,
-    //      T[0:j, j] = -tau_j T[0:j, 0:j] G[0:j, j]   (one wave, lane = row)
-    if (wid == 0) {                              // lane = row: no cross-lane dependency
-      for (int j = 0; j < BB; ++j) {
-        double s = 0.0;
-        if (lane < j)
-          for (int k = lane; k < j; ++k) s += Ts[lane][k] * Ws[k][j];
-        if (lane < BB) Ts[lane][j] = (lane < j) ? -taus[j] * s : (lane == j ? taus[j] : 0.0);
-      }
-    }
-    __syncthreads();
-    if (t < BB * BB) bw.T[(int64_t)p * BB * BB + t] = Ts[t / BB][t % BB];
-    BAND_TMARK(2)
     // ---- U = V T -> Ws  (MFMA, all 32 row blocks so rows >= m read back as zero)
 #pragma unroll
     for (int q = 0; q < BMP / 16 / NWR; ++q) {
@@ -445,6 +480,261 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
+// kernel 1, multi-workgroup form (default): the same band reduction with the two O(m^2)
+// phases of every panel spread over many workgroups per cell, so the reduction of ONE cell
+// is no longer bound by one CU (the single-workgroup kernel takes ~4.4 ms for one n = 513
+// cell however many CUs are idle; with few cells per GPU - the multi-GPU case - that is the
+// whole step).  Per panel p the host issues three launches over all cells:
+//
+//   (mk_init  copies the scaled window sums once)
+//   mk_panel  1 WG / cell      P1 + P2 + T (band_panel_factor), U = V T, z <- Q_p^T z;
+//                              V and U to the cell's global panel buffers
+//   mk_x      m/64 WGs / cell  X = A22 U (16 rows per wave) and the partial V_I^T X_I
+//   mk_trail  one WG per 32x32 lower tile of A22:  M = T^T sum(V_I^T X_I),
+//                              W = X - 1/2 V M for the tile's rows and columns, then
+//                              A22 -= V W^T + W V^T (MFMA), off-diagonal tiles mirrored so A
+//                              stays bitwise symmetric
+//
+// and one mk_extract launch copies the lower band out at the end.  Kernel boundaries are the
+// only inter-workgroup synchronisation.
+// ---------------------------------------------------------------------------------------
+constexpr int MK_XR = 64;              // mk_x rows per workgroup (4 waves x 16)
+constexpr int MK_TS = 32;              // mk_trail tile edge (4 waves x 16 x 16)
+
+constexpr int MK_INIT_WG = 16;         // mk_init workgroups per cell
+
+// A = S * scale, z = r * scale (the working copies of the cell's window sums)
+__global__ __launch_bounds__(256) void band_mk_init_kernel(
+    const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
+    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work) {
+  const int cell = blockIdx.x / MK_INIT_WG, part = blockIdx.x % MK_INIT_WG;
+  const RidgeCellDesc cd = cells[cell];
+  const int n = cd.n;
+  BandWork bw(work + cd.work, n, L);
+  const double* S = SD + cd.src;
+  const double sc = cd.scale;
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int i = part * 4 + wid; i < n; i += 4 * MK_INIT_WG) {
+    const double* srow = S + (int64_t)i * ldS;
+    double* arow = bw.A + (int64_t)i * n;
+    for (int j = lane; j < n; j += 64) arow[j] = srow[j] * sc;
+  }
+  if (part == 0)
+    for (int i = threadIdx.x; i < n; i += 256) bw.z[i] = Sr[cd.rsrc + i] * sc;
+}
+
+__global__ __launch_bounds__(NTR) void band_mk_panel_kernel(
+    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work, int p) {
+  __shared__ double Vs[BMP][LS];
+  __shared__ double Gs[BB][LS];         // dlarft dots G
+  __shared__ double red[NWR][BB * BB];
+  __shared__ double red2[NWR][BB];
+  __shared__ double Ts[BB][LS];
+  __shared__ double taus[BB];
+  const RidgeCellDesc cd = cells[blockIdx.x];
+  const int n = cd.n;
+  const int k0 = p * BB, r0 = k0 + BB, m = n - r0;
+  if (r0 >= n) return;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int c16 = lane & 15, g4 = lane >> 4;
+  const int cq = t & 15, rg = t >> 4;
+  BandWork bw(work + cd.work, n, L);
+  double* A = bw.A;
+  band_panel_factor(A, n, k0, r0, m, Vs, Gs, &red[0][0], Ts, taus, bw.T + (int64_t)p * BB * BB);
+  // U = V T -> Ug, V -> Vg (all BMP rows: rows >= m are zero)
+#pragma unroll
+  for (int q = 0; q < BMP / 16 / NWR; ++q) {
+    const int i0 = (wid + NWR * q) * 16;
+    double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vs[i0 + c16][4 * r + g4], Ts[4 * r + g4][c16], acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bw.Ug[(i0 + g4 + 4 * r) * BB + c16] = acc[r];
+  }
+  for (int e = t; e < BMP * BB; e += NTR) bw.Vg[e] = Vs[e / BB][e % BB];
+  // z <- Q_p^T z = z - V (T^T (V^T z))
+  {
+    double s = 0.0;
+    for (int i = rg; i < m; i += 32) s += Vs[i][cq] * bw.z[r0 + i];
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    if (lane < 16) red2[wid][lane] = s;
+  }
+  __syncthreads();
+  double zv[BB], zt[BB];
+#pragma unroll
+  for (int a = 0; a < BB; ++a) {
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < NWR; ++w) s += red2[w][a];
+    zv[a] = s;
+  }
+#pragma unroll
+  for (int c = 0; c < BB; ++c) {
+    double s = 0.0;
+#pragma unroll
+    for (int a = 0; a <= c; ++a) s += Ts[a][c] * zv[a];
+    zt[c] = s;
+  }
+  for (int i = t; i < m; i += NTR) {
+    double s = 0.0;
+#pragma unroll
+    for (int c = 0; c < BB; ++c) s += Vs[i][c] * zt[c];
+    bw.z[r0 + i] -= s;
+  }
+}
+
+__global__ __launch_bounds__(256) void band_mk_x_kernel(const RidgeCellDesc* __restrict__ cells,
+                                                        int L, double* __restrict__ work, int p,
+                                                        int nxb) {
+  __shared__ double red[4][BB * BB];
+  const int cell = blockIdx.x / nxb, xb = blockIdx.x % nxb;
+  const RidgeCellDesc cd = cells[cell];
+  const int n = cd.n;
+  const int r0 = p * BB + BB, m = n - r0;
+  if (r0 >= n || xb * MK_XR >= m) return;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int c16 = lane & 15, g4 = lane >> 4;
+  BandWork bw(work + cd.work, n, L);
+  const double* __restrict__ A = bw.A;
+  const double* __restrict__ Ug = bw.Ug;
+  const double* __restrict__ Vg = bw.Vg;
+  const int i0 = xb * MK_XR + 16 * wid;          // this wave's 16 rows of X
+  double4_t X = {0.0, 0.0, 0.0, 0.0};
+  double4_t Pp = {0.0, 0.0, 0.0, 0.0};
+  if (i0 < m) {
+    // X[i][:] = sum_k A22[k][i] U[k][:]  (A symmetric: row k, 16 contiguous columns)
+    const int col = r0 + min(i0 + c16, m - 1);
+    const double* Ab = A + (int64_t)r0 * n + col;
+    int k = 0;
+    for (; k + 32 <= m; k += 32) {
+      double a[8], b[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        a[u] = Ab[(int64_t)(k + 4 * u + g4) * n];
+        b[u] = Ug[(k + 4 * u + g4) * BB + c16];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) X = mfma_f64_16x16x4(a[u], b[u], X);
+    }
+    for (; k < m; k += 4) {
+      const int kr = min(k + g4, m - 1);          // U rows >= m are zero
+      X = mfma_f64_16x16x4(Ab[(int64_t)kr * n], Ug[(k + g4) * BB + c16], X);
+    }
+    // rows >= m of X are duplicates of row m-1: zero them; partial V_I^T X_I
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (i0 + g4 + 4 * r >= m) X[r] = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      Pp = mfma_f64_16x16x4(Vg[(i0 + 4 * r + g4) * BB + c16], X[r], Pp);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bw.Xg[(i0 + g4 + 4 * r) * BB + c16] = X[r];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[wid][(g4 + 4 * r) * BB + c16] = Pp[r];
+  __syncthreads();
+  bw.Pg[xb * BB * BB + t] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+}
+
+__global__ __launch_bounds__(256) void band_mk_trail_kernel(const RidgeCellDesc* __restrict__ cells,
+                                                            int L, double* __restrict__ work,
+                                                            int p, int ntile) {
+  __shared__ double Ps[BB][LS];
+  __shared__ double Ms[BB][LS];
+  __shared__ double Vl[2 * MK_TS][LS];
+  __shared__ double Wl[2 * MK_TS][LS];
+  const int cell = blockIdx.x / ntile, tile = blockIdx.x % ntile;
+  int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+  if (I * (I + 1) / 2 > tile) --I;
+  if ((I + 1) * (I + 2) / 2 <= tile) ++I;
+  const int J = tile - I * (I + 1) / 2;           // lower tile (I, J), I >= J
+  const RidgeCellDesc cd = cells[cell];
+  const int n = cd.n;
+  const int r0 = p * BB + BB, m = n - r0;
+  if (r0 >= n || I * MK_TS >= m) return;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int c16 = lane & 15, g4 = lane >> 4;
+  BandWork bw(work + cd.work, n, L);
+  double* __restrict__ A = bw.A;
+  // M = T^T sum_b P_b
+  {
+    const int nxb = (m + MK_XR - 1) / MK_XR;
+    double s = 0.0;
+    for (int b = 0; b < nxb; ++b) s += bw.Pg[b * BB * BB + t];
+    Ps[t / BB][t % BB] = s;
+  }
+  // V rows of the I block (local 0..31) and the J block (local 32..63)
+  for (int e = t; e < 2 * MK_TS * BB; e += 256) {
+    const int lr = e / BB, c = e % BB;
+    const int gi = (lr < MK_TS) ? I * MK_TS + lr : J * MK_TS + lr - MK_TS;
+    Vl[lr][c] = (gi < m) ? bw.Vg[gi * BB + c] : 0.0;
+  }
+  __syncthreads();
+  {
+    const double* Tp = bw.T + (int64_t)p * BB * BB;
+    const int a = t / BB, b = t % BB;
+    double s = 0.0;
+#pragma unroll
+    for (int c = 0; c < BB; ++c) s += Tp[c * BB + a] * Ps[c][b];
+    Ms[a][b] = s;
+  }
+  __syncthreads();
+  // W = X - 1/2 V M for the same 64 rows
+  for (int e = t; e < 2 * MK_TS * BB; e += 256) {
+    const int lr = e / BB, c = e % BB;
+    const int gi = (lr < MK_TS) ? I * MK_TS + lr : J * MK_TS + lr - MK_TS;
+    double s = 0.0;
+#pragma unroll
+    for (int a = 0; a < BB; ++a) s += Vl[lr][a] * Ms[a][c];
+    Wl[lr][c] = (gi < m) ? bw.Xg[gi * BB + c] - 0.5 * s : 0.0;
+  }
+  __syncthreads();
+  // wave -> 16 x 16 sub-tile (si, sj); on a diagonal tile the upper sub-tile is the mirror
+  const int si = wid >> 1, sj = wid & 1;
+  if (I == J && sj > si) return;
+  const int gi0 = I * MK_TS + si * 16, gj0 = J * MK_TS + sj * 16;
+  const bool mirror = (I != J) || (si != sj);
+  double4_t acc;
+  int offn[4], offt[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = gi0 + g4 + 4 * r, j = gj0 + c16;
+    const bool ok = i < m && j < m;
+    offn[r] = ok ? (r0 + i) * n + r0 + j : -1;
+    offt[r] = (ok && mirror) ? (r0 + j) * n + r0 + i : -1;
+    acc[r] = ok ? A[offn[r]] : 0.0;
+  }
+  const int ia = si * 16 + c16, jb = MK_TS + sj * 16 + c16;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    const int kk = 4 * (s & 3) + g4;
+    const double av = (s < 4) ? Vl[ia][kk] : Wl[ia][kk];
+    const double bv = (s < 4) ? Wl[jb][kk] : Vl[jb][kk];
+    acc = mfma_f64_16x16x4(-av, bv, acc);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    if (offn[r] >= 0) A[offn[r]] = acc[r];
+    if (offt[r] >= 0) A[offt[r]] = acc[r];
+  }
+}
+
+__global__ __launch_bounds__(256) void band_mk_extract_kernel(
+    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work) {
+  const RidgeCellDesc cd = cells[blockIdx.x];
+  const int n = cd.n;
+  BandWork bw(work + cd.work, n, L);
+  for (int e = threadIdx.x; e < n * LS; e += 256) {
+    const int r = e / LS, c = r - BB + e % LS;
+    bw.LB[e] = (c >= 0) ? bw.A[(int64_t)r * n + c] : 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // kernel 2: banded Cholesky solves, 4 lambdas per wave (one 16-lane DPP row each).
 //
 // Lane p of a row holds the band row r (r = p mod 16) of the 16-row window j+1..j+16 (the
@@ -578,6 +868,7 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
     const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work,
     double* __restrict__ beta_out, int64_t ldo) {
   __shared__ double Ys[BNMAX][LS];
+  __shared__ double Vb[BMP][LS];       // V_p (unit lower trapezoid), staged once per panel
   __shared__ double red[NWB][BB * BB];
   const int nch = (L + LC - 1) / LC;
   const int cell = blockIdx.x / nch, ch = blockIdx.x % nch;
@@ -594,20 +885,22 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
     const int c = e / BNMAX, i = e % BNMAX;
     Ys[i][c] = (c < lw && i < n) ? bw.Yt[(int64_t)(l0 + c) * n + i] : 0.0;
   }
-  __syncthreads();
   const int np = (n - 1) / BB;    // panels: k0 = 16 p with k0 + 16 < n
   for (int p = np - 1; p >= 0; --p) {
     const int k0 = p * BB, r0 = k0 + BB, m = n - r0;
-    // V[i][c] of panel p: unit lower trapezoid, strictly-lower part stored in A
-    auto vload = [&](int i, int c) -> double {
-      if (i >= m) return 0.0;
-      return (i > c) ? A[(int64_t)(r0 + i) * n + k0 + c] : (i == c ? 1.0 : 0.0);
-    };
-    // P = V^T Y[r0:]  (K over rows, split across waves in 4-row steps)
+    // V_p -> Vb: the strictly-lower part lives in A's panel columns (16 contiguous doubles per
+    // row); every load of the panel is in flight at once (one memory latency per panel)
+    for (int e = t; e < m * BB; e += NTB) {
+      const int i = e / BB, c = e % BB;
+      Vb[i][c] = (i > c) ? A[(int64_t)(r0 + i) * n + k0 + c] : (i == c ? 1.0 : 0.0);
+    }
+    __syncthreads();
+    // P = V^T Y[r0:]  (K over rows, 4-row MFMA steps split across the waves)
     double4_t Pp = {0.0, 0.0, 0.0, 0.0};
     for (int k = 4 * wid; k < m; k += 4 * NWB) {
       const int i = k + g4;
-      Pp = mfma_f64_16x16x4(vload(i, c16), (i < m) ? Ys[r0 + i][c16] : 0.0, Pp);
+      const bool in = i < m;
+      Pp = mfma_f64_16x16x4(in ? Vb[i][c16] : 0.0, in ? Ys[r0 + i][c16] : 0.0, Pp);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[wid][(g4 + 4 * r) * BB + c16] = Pp[r];
@@ -622,13 +915,15 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
       for (int w = 0; w < NWB; ++w) pv += red[w][(4 * r + g4) * BB + c16];
       Mm = mfma_f64_16x16x4(Tp[c16 * BB + 4 * r + g4], pv, Mm);
     }
-    // Y[r0:] -= V M   (row blocks I = wid + 4q)
+    // Y[r0:] -= V M   (row blocks I = wid + NWB q)
     const int nI = (m + 15) >> 4;
     for (int I = wid; I < nI; I += NWB) {
       const int i0 = I * 16;
+      const int ia = min(i0 + c16, m - 1);
+      const double vs = (i0 + c16 < m) ? 1.0 : 0.0;
       double4_t acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(vload(i0 + c16, 4 * r + g4), Mm[r], acc);
+      for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(vs * Vb[ia][4 * r + g4], Mm[r], acc);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = i0 + g4 + 4 * r;
@@ -649,18 +944,42 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
 extern "C" int64_t pfml_ridge_band_work_doubles(int n, int L) {
   const int64_t np = (n + BB - 1) / BB;
   return (int64_t)n * n + (int64_t)n * LS + n + np * BB * BB + (int64_t)L * n +
-         (int64_t)L * n * LS;
+         (int64_t)L * n * LS + 3LL * BMP * BB + (int64_t)(BMP / MK_XR) * BB * BB;
 }
 
 extern "C" int pfml_ridge_band_nmax() { return BNMAX; }
 
 extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, const double* Sr,
-                                             const void* cells, int ncells, const double* lvec,
-                                             int L, double* work, double* beta_out, int64_t ldo,
+                                             const void* cells, int ncells, int nmax,
+                                             const double* lvec, int L, double* work,
+                                             double* beta_out, int64_t ldo, int band_mode,
                                              long long* tim, hipStream_t st) {
   const RidgeCellDesc* cd = static_cast<const RidgeCellDesc*>(cells);
-  hipLaunchKernelGGL(ridge_band_reduce_kernel, dim3(ncells), dim3(NTR), 0, st, SD, ldS, Sr, cd,
-                     L, work, tim);
+  // band_mode 1 (or PFML_BAND_MODE=single, or phase timing): one workgroup per cell for the
+  // whole reduction; 2 / default: the multi-workgroup form, three launches per panel.
+  const char* mode = getenv("PFML_BAND_MODE");
+  const bool single = tim != nullptr || band_mode == 1 ||
+                      (band_mode == 0 && mode && mode[0] == 's');
+  if (single) {
+    hipLaunchKernelGGL(ridge_band_reduce_kernel, dim3(ncells), dim3(NTR), 0, st, SD, ldS, Sr, cd,
+                       L, work, tim);
+  } else {
+    const int npan = (nmax - 1) / BB;
+    hipLaunchKernelGGL(band_mk_init_kernel, dim3(ncells * MK_INIT_WG), dim3(256), 0, st, SD, ldS,
+                       Sr, cd, L, work);
+    for (int p = 0; p < npan; ++p) {
+      const int mmax = nmax - (p + 1) * BB;
+      const int nxb = (mmax + MK_XR - 1) / MK_XR;
+      const int tt = (mmax + MK_TS - 1) / MK_TS;
+      const int ntile = tt * (tt + 1) / 2;
+      hipLaunchKernelGGL(band_mk_panel_kernel, dim3(ncells), dim3(NTR), 0, st, cd, L, work, p);
+      hipLaunchKernelGGL(band_mk_x_kernel, dim3(ncells * nxb), dim3(256), 0, st, cd, L, work, p,
+                         nxb);
+      hipLaunchKernelGGL(band_mk_trail_kernel, dim3(ncells * ntile), dim3(256), 0, st, cd, L,
+                         work, p, ntile);
+    }
+    hipLaunchKernelGGL(band_mk_extract_kernel, dim3(ncells), dim3(256), 0, st, cd, L, work);
+  }
   hipLaunchKernelGGL(ridge_band_solve_kernel, dim3(ncells * ((L + 15) / 16)), dim3(NTS), 0, st,
                      cd, lvec, L, work, tim, ncells);
   const int nch = (L + LC - 1) / LC;

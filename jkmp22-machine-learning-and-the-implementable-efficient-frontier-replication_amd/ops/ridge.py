@@ -109,18 +109,20 @@ def ridge_plan(P: int, L: int, cell_src, cell_n, cell_scale) -> dict:
 
 
 def ridge_launch(plan: dict, d_desc: torch.Tensor, SD: torch.Tensor, Sr: torch.Tensor,
-                 lv: torch.Tensor, beta: torch.Tensor) -> None:
+                 lv: torch.Tensor, beta: torch.Tensor, band_mode: int = 0) -> None:
     P = SD.shape[-1]
     L = int(lv.numel())
     work = torch.empty(plan["work"], dtype=torch.float64, device=SD.device)
     nat.check(nat.hip_lib().pfml_ridge_grid(SD.data_ptr(), P, Sr.data_ptr(), d_desc.data_ptr(),
                                             plan["nc"], plan["nmax"], lv.data_ptr(), L,
                                             work.data_ptr(), beta.data_ptr(), beta.shape[-1],
-                                            nat.stream_of(SD)), "pfml_ridge_grid")
+                                            int(band_mode), nat.stream_of(SD)),
+              "pfml_ridge_grid")
 
 
 def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n: np.ndarray,
-               cell_scale: np.ndarray, lvec: torch.Tensor, repair: bool = True) -> torch.Tensor:
+               cell_scale: np.ndarray, lvec: torch.Tensor, repair: bool = True,
+               band_mode: int = 0) -> torch.Tensor:
     """beta[c, l, :n_c] = solve(SD[src_c][:n,:n]*scale_c + l I, Sr[src_c][:n]*scale_c).
 
     SD: [S, P, P] running sums, Sr: [S, P]; returns [ncells, L, P] (zero beyond n_c).
@@ -138,7 +140,7 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
         (d_desc,) = upload([plan["desc"]], SD.device)
         lv = lvec.to(device=SD.device, dtype=torch.float64).contiguous()
         SDc, Src = SD.contiguous(), Sr.contiguous()
-        ridge_launch(plan, d_desc, SDc, Src, lv, beta)
+        ridge_launch(plan, d_desc, SDc, Src, lv, beta, band_mode)
         if repair:
             repair_nonspd(beta, SDc, Src, cell_src, cell_n, cell_scale, lv)
         return beta
@@ -191,6 +193,35 @@ def _side_stream(dev: torch.device) -> torch.cuda.Stream:
     return _SIDE[key]
 
 
+BAND_SINGLE, BAND_MULTI = 1, 2
+# Above this many largest-n cells per launch the one-workgroup-per-cell reduction (throughput
+# form) beats the multi-workgroup one (latency form); measured on MI355X, tools/bench_band.py.
+BAND_MULTI_MAX_CELLS = 64
+
+
+def band_policy(cell_n: np.ndarray) -> tuple[int, bool]:
+    """(band_mode, two_streams) for one grid launch.
+
+    Few big cells (multi-GPU shards): the multi-workgroup band reduction on one stream.  Many
+    (one GPU holds the whole grid): one workgroup per cell, the big cells on a second stream so
+    the small cells' chain fills the CUs they leave idle.  PFML_BAND_MODE=single|multi and
+    PFML_RIDGE_STREAMS=1|2 override."""
+    import os
+    cell_n = np.asarray(cell_n)
+    nbig = int((cell_n == cell_n.max()).sum()) if len(cell_n) else 0
+    mode = BAND_MULTI if nbig <= BAND_MULTI_MAX_CELLS else BAND_SINGLE
+    env = os.environ.get("PFML_BAND_MODE", "")[:1]
+    if env == "s":
+        mode = BAND_SINGLE
+    elif env == "m":
+        mode = BAND_MULTI
+    two = mode == BAND_SINGLE
+    v = os.environ.get("PFML_RIDGE_STREAMS")
+    if v:
+        two = v.strip() == "2"
+    return mode, two
+
+
 def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_scale,
                     lvec: torch.Tensor, D: torch.Tensor, R: torch.Tensor, job_cell, job_month,
                     job_n) -> tuple[torch.Tensor, torch.Tensor]:
@@ -206,8 +237,9 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     cell_scale = np.asarray(cell_scale)
     job_cell, job_month, job_n = (np.asarray(job_cell), np.asarray(job_month),
                                   np.asarray(job_n))
-    if not nat.is_device(SD) or len(np.unique(cell_n)) < 2:
-        beta = ridge_grid(SD, Sr, cell_src, cell_n, cell_scale, lvec)
+    mode, two = band_policy(cell_n)
+    if not nat.is_device(SD) or len(np.unique(cell_n)) < 2 or not two:
+        beta = ridge_grid(SD, Sr, cell_src, cell_n, cell_scale, lvec, band_mode=mode)
         return beta, quadform_utilities(D, R, beta, job_cell, job_month, job_n)
     th = _HostClock()
     S, P, _ = SD.shape
@@ -242,7 +274,7 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
         cells, jobs, rp, qp = groups[gi]
         with torch.cuda.stream(stream):
             b = torch.zeros((len(cells), L, P), dtype=SD.dtype, device=dev)
-            ridge_launch(rp, dv[3 * gi], SD, Sr, lv, b)
+            ridge_launch(rp, dv[3 * gi], SD, Sr, lv, b, mode)
             o = torch.empty((len(jobs), L), dtype=SD.dtype, device=dev)
             quad_launch(qp, dv[3 * gi + 1], dv[3 * gi + 2], D, R, b, o)
         outs.append((cells, jobs, b, o))

@@ -156,3 +156,22 @@ def test_ridge_variants_agree(gpu, variant, monkeypatch):
     out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
     rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
     assert rel < 1e-8, rel
+
+
+@pytest.mark.parametrize("mode", ["single", "multi"])
+def test_band_reduction_modes(gpu, mode, monkeypatch):
+    """One-workgroup-per-cell and multi-workgroup band reductions both reproduce the LU-solve
+    oracle, with cells of different n (65 .. 513) in one launch."""
+    from pfml.ops.ridge import ridge_grid
+    monkeypatch.setenv("PFML_BAND_MODE", mode)
+    P = 513
+    SD = _spd_stack(3, P, n_obs=700, seed=61)
+    Sr = _rand(3, P, seed=62)
+    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
+    src = np.array([0, 1, 2, 1, 0, 2, 2])
+    nn = np.array([513, 513, 65, 257, 129, 100, 513])
+    sc = np.full(len(src), 1.5e-3)
+    ref = ridge_grid(SD, Sr, src, nn, sc, lv)
+    out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
+    rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
+    assert rel < 1e-8, rel
