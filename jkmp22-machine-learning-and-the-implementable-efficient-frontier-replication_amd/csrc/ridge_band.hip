@@ -45,7 +45,7 @@ constexpr int LC = 16;              // lambdas per back-transform workgroup
 
 // Per-cell workspace layout (doubles).
 struct BandWork {
-  double *A, *LB, *z, *T, *Yt, *Lf, *Vg, *Ug, *Xg, *Pg;
+  double *A, *LB, *z, *T, *Yt, *Lf, *Vg, *Ug, *Xg, *Pg, *Pzg;
   __device__ BandWork(double* w, int n, int L) {
     const int np = (n + BB - 1) / BB;
     A = w;                                   // n x n working matrix (V_p / R_p stored below)
@@ -58,6 +58,7 @@ struct BandWork {
     Ug = Vg + BMP * BB;                      //                        U = V T  (BMP x 16)
     Xg = Ug + BMP * BB;                      //                        X = A U  (BMP x 16)
     Pg = Xg + BMP * BB;                      //                        V_I^T X_I partials
+    Pzg = Pg + (BMP / 64) * BB * BB;         //                        V_I^T z_I partials
   }
 };
 
@@ -106,6 +107,19 @@ __device__ __forceinline__ double row16_sum(double v) {
   return v;
 }
 
+// Sum of v over lanes {l, l^16, l^32, l^48} (the 4 row groups of a wave), with the gfx950
+// VALU lane swaps instead of two ds_bpermute round trips.
+__device__ __forceinline__ double rowgroup_sum(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  v = __hiloint2double((int)h16[0], (int)l16[0]) + __hiloint2double((int)h16[1], (int)l16[1]);
+  const int lo2 = __double2loint(v), hi2 = __double2hiint(v);
+  const auto l32 = __builtin_amdgcn_permlane32_swap(lo2, lo2, false, false);
+  const auto h32 = __builtin_amdgcn_permlane32_swap(hi2, hi2, false, false);
+  return __hiloint2double((int)h32[0], (int)l32[0]) + __hiloint2double((int)h32[1], (int)l32[1]);
+}
+
 // ---------------------------------------------------------------------------------------
 // kernel 1: band reduction of one cell.
 // ---------------------------------------------------------------------------------------
@@ -146,107 +160,88 @@ __device__ __forceinline__ void band_x_accum(const double* __restrict__ A, int n
 // P1 + P2 + T of one panel, by one NTR-thread workgroup: the m x 16 panel below the band
 // (columns r0.. of rows k0..k0+15 of the symmetric A) is QR-factored by Householder in
 // registers; V (unit lower trapezoid) -> Vs, V and R -> A's panel columns, the compact-WY T
-// (dlarft) -> Ts and Tglob.  Ends with a barrier.
+// (dlarft) -> Ts and Tglob.  Ends with a barrier.  `redf` needs 2 x 256 + 32 doubles.
 __device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n, int k0, int r0,
                                                   int m, double (*Vs)[LS], double (*Gs)[LS],
                                                   double* redf, double (*Ts)[LS], double* taus,
-                                                  double* __restrict__ Tglob) {
+                                                  double* __restrict__ Tglob,
+                                                  long long* tk = nullptr) {
   const int t = threadIdx.x, lane = t & 63;
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
   const int cq = t & 15, rg = t >> 4;
-  // ---- P1: panel A[r0:, k0:k0+16] -> Vs (read as rows k0..k0+15 of the symmetric A)
-  for (int e = t; e < BB * BMP; e += NTR) {
-    const int c = e / BMP, i = e % BMP;
-    Vs[i][c] = (i < m) ? A[(int64_t)(k0 + c) * n + r0 + i] : 0.0;
-  }
-  __syncthreads();
-  // ---- P2: Householder QR of the m x 16 panel in REGISTERS: thread (rg, cq) holds rows
-  //      i = rg + 32 q (q < 16) of column cq; column j reaches the 16 lanes of a row group by
-  //      a row_newbcast DPP move; one barrier per column (cross-wave sums, ping-pong
-  //      buffers).  The dlarft dots G[:, j-1] = V^T v_{j-1} ride in the same reduction.
-  double a[16], vp[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    a[q] = Vs[rg + 32 * q][cq];
-    vp[q] = 0.0;
-  }
-  static_for<0, BB + 1>([&](auto J) {
-    constexpr int j = decltype(J)::value;      // j == BB: only the last G column
-    const int par = j & 1;
-    double x[16];
-    double s1p[4] = {0.0, 0.0, 0.0, 0.0}, s2p[4] = {0.0, 0.0, 0.0, 0.0};
-    // Only row group q = 0 (rows < 32) meets the diagonal; row groups at or beyond m are
-    // all-zero and skipped (wave-uniform branch).  Four partial sums break the FMA chains.
+  const int c16 = lane & 15, g4 = lane >> 4;
+  // ---- P1: thread (rg, cq) loads rows i = rg + 32 q (q < 16) of panel column cq straight
+  //      into registers (row k0+cq of the symmetric A; all 16 loads in flight at once)
+  double a[16];
+  {
+    const double* src = A + (int64_t)(k0 + cq) * n + r0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      if (q > 0 && 32 * q >= m) continue;
       const int i = rg + 32 * q;
-      if constexpr (j < BB) {
-        x[q] = row_bcast<j < BB ? j : 0>(a[q]);
+      a[q] = (i < m) ? src[i] : 0.0;
+    }
+  }
+  if (tk) tk[0] = (long long)__builtin_amdgcn_s_memtime();
+  // ---- P2: Householder QR of the m x 16 panel in REGISTERS: column j reaches the 16 lanes
+  //      of a row group by a row_newbcast DPP move; one barrier per column (cross-wave sums,
+  //      ping-pong buffers).
+  static_for<0, BB>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    const int par = j & 1;
+    double x[16];
+    double s1p[4] = {0.0, 0.0, 0.0, 0.0};
+    // Only row group q = 0 (rows < 32) meets the diagonal; groups of four row groups at or
+    // beyond m are all-zero and skipped (one wave-uniform branch per four).  Four partial
+    // sums break the FMA chain.
+#pragma unroll
+    for (int q4 = 0; q4 < 16; q4 += 4) {
+      if (q4 > 0 && 32 * q4 >= m) continue;
+#pragma unroll
+      for (int q = q4; q < q4 + 4; ++q) {
+        const int i = rg + 32 * q;
+        x[q] = row_bcast<j>(a[q]);
         s1p[q & 3] += (q > 0 || i > j) ? x[q] * a[q] : 0.0;
       }
-      if constexpr (j > 0) {
-        const double vex = (q > 0 || i > cq) ? a[q] : ((i == cq && i < m) ? 1.0 : 0.0);
-        s2p[q & 3] += vp[q] * vex;
-      }
     }
-    double s1 = (s1p[0] + s1p[1]) + (s1p[2] + s1p[3]);
-    double s2 = (s2p[0] + s2p[1]) + (s2p[2] + s2p[3]);
-    s1 += __shfl_xor(s1, 16, 64);
-    s1 += __shfl_xor(s1, 32, 64);
-    s2 += __shfl_xor(s2, 16, 64);
-    s2 += __shfl_xor(s2, 32, 64);
-    if (lane < 16) {
-      redf[par * 256 + wid * 16 + lane] = s1;
-      redf[512 + par * 256 + wid * 16 + lane] = s2;
-    }
-    if constexpr (j < BB) {
-      if (rg == j) redf[1024 + par * 16 + cq] = a[0];     // row j (q = 0)
-    }
+    // sum over the wave's 4 row groups (lanes l, l^16, l^32, l^48): VALU lane swaps
+    const double s1 = rowgroup_sum((s1p[0] + s1p[1]) + (s1p[2] + s1p[3]));
+    if (lane < 16) redf[par * 256 + wid * 16 + lane] = s1;
+    if (rg == j) redf[512 + par * 16 + cq] = a[0];       // row j (q = 0)
     __syncthreads();
-    if constexpr (j > 0) {
-      if (t < BB) {
-        double g = 0.0;
+    double xn2 = 0.0, dc = 0.0;
 #pragma unroll
-        for (int w = 0; w < NWR; ++w) g += redf[512 + par * 256 + w * 16 + t];
-        Gs[t][j - 1] = g;                                 // G[t][j-1]
-      }
+    for (int w = 0; w < NWR; ++w) {
+      xn2 += redf[par * 256 + w * 16 + j];
+      dc += redf[par * 256 + w * 16 + cq];
     }
-    if constexpr (j < BB) {
-      double xn2 = 0.0, dc = 0.0;
+    const double alpha = redf[512 + par * 16 + j];
+    const double vjc = redf[512 + par * 16 + cq];
+    double tau, beta, scal;
+    if (xn2 == 0.0) {
+      tau = 0.0; beta = alpha; scal = 0.0;
+    } else {
+      beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
+      tau = (beta - alpha) / beta;
+      scal = 1.0 / (alpha - beta);
+    }
+    const double wc = tau * (vjc + scal * dc);
 #pragma unroll
-      for (int w = 0; w < NWR; ++w) {
-        xn2 += redf[par * 256 + w * 16 + j];
-        dc += redf[par * 256 + w * 16 + cq];
-      }
-      const double alpha = redf[1024 + par * 16 + j];
-      const double vjc = redf[1024 + par * 16 + cq];
-      double tau, beta, scal;
-      if (xn2 == 0.0) {
-        tau = 0.0; beta = alpha; scal = 0.0;
-      } else {
-        beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
-        tau = (beta - alpha) / beta;
-        scal = 1.0 / (alpha - beta);
-      }
-      const double wc = tau * (vjc + scal * dc);
+    for (int q4 = 0; q4 < 16; q4 += 4) {
+      if (q4 > 0 && 32 * q4 >= m) continue;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        if (q > 0 && 32 * q >= m) continue;
+      for (int q = q4; q < q4 + 4; ++q) {
         const int i = rg + 32 * q;
         if (q == 0) {
           const double v = (i > j) ? x[q] * scal : ((i == j && i < m) ? 1.0 : 0.0);
-          if (cq > j) a[q] -= v * wc;
-          else if (cq == j) a[q] = (i > j) ? v : ((i == j) ? beta : a[q]);
-          vp[q] = v;
+          const double diag = (i > j) ? v : ((i == j) ? beta : a[q]);
+          a[q] = (cq > j) ? a[q] - v * wc : ((cq == j) ? diag : a[q]);
         } else {
           const double v = x[q] * scal;
           a[q] = (cq > j) ? a[q] - v * wc : ((cq == j) ? v : a[q]);
-          vp[q] = v;
         }
       }
-      if (t == 0) taus[j] = tau;
     }
+    if (t == 0) taus[j] = tau;
   });
   // explicit V -> Vs (MFMA operand); V (strictly lower) and R (upper) -> A's panel columns
 #pragma unroll
@@ -254,6 +249,26 @@ __device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n,
     const int i = rg + 32 * q;
     Vs[i][cq] = (i > cq) ? a[q] : ((i == cq && i < m) ? 1.0 : 0.0);
     if (i < m) A[(int64_t)(r0 + i) * n + k0 + cq] = a[q];
+  }
+  __syncthreads();
+  if (tk) tk[1] = (long long)__builtin_amdgcn_s_memtime();
+  // ---- G = V^T V (dlarft dots) on MFMA: wave w sums rows [64 w, 64 w + 64)
+  {
+    double4_t g = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 64; k += 4) {
+      const double v = Vs[wid * 64 + k + g4][c16];
+      g = mfma_f64_16x16x4(v, v, g);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) redf[wid * 256 + PFML_F64_CROW(lane, r) * BB + c16] = g[r];
+  }
+  __syncthreads();
+  if (t < BB * BB) {
+    double g = 0.0;
+#pragma unroll
+    for (int w = 0; w < NWR; ++w) g += redf[w * 256 + t];
+    Gs[t / BB][t % BB] = g;
   }
   __syncthreads();
   // ---- T (dlarft, forward columnwise): T[j][j] = tau_j,
@@ -487,15 +502,16 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
 // whole step).  Per panel p the host issues three launches over all cells:
 //
 //   (mk_init  copies the scaled window sums once)
-//   mk_panel  1 WG / cell      P1 + P2 + T (band_panel_factor), U = V T, z <- Q_p^T z;
+//   mk_panel  1 WG / cell      P1 + P2 + T (band_panel_factor), U = V T;
 //                              V and U to the cell's global panel buffers
-//   mk_x      m/64 WGs / cell  X = A22 U (16 rows per wave) and the partial V_I^T X_I
+//   mk_x      m/64 WGs / cell  X = A22 U (16 rows per wave), partials V_I^T X_I, V_I^T z_I
 //   mk_trail  one WG per 32x32 lower tile of A22:  M = T^T sum(V_I^T X_I),
 //                              W = X - 1/2 V M for the tile's rows and columns, then
 //                              A22 -= V W^T + W V^T (MFMA), off-diagonal tiles mirrored so A
 //                              stays bitwise symmetric
 //
-// and one mk_extract launch copies the lower band out at the end.  Kernel boundaries are the
+// and one mk_extract launch copies the lower band out at the end.  rbar rides along as
+// z <- Q_p^T z: V_I^T z_I partials in mk_x, the update of block I's rows in tile (I, 0).  Kernel boundaries are the
 // only inter-workgroup synchronisation.
 // ---------------------------------------------------------------------------------------
 constexpr int MK_XR = 64;              // mk_x rows per workgroup (4 waves x 16)
@@ -524,11 +540,11 @@ __global__ __launch_bounds__(256) void band_mk_init_kernel(
 }
 
 __global__ __launch_bounds__(NTR) void band_mk_panel_kernel(
-    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work, int p) {
+    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work, int p,
+    long long* __restrict__ tim) {
   __shared__ double Vs[BMP][LS];
   __shared__ double Gs[BB][LS];         // dlarft dots G
   __shared__ double red[NWR][BB * BB];
-  __shared__ double red2[NWR][BB];
   __shared__ double Ts[BB][LS];
   __shared__ double taus[BB];
   const RidgeCellDesc cd = cells[blockIdx.x];
@@ -538,10 +554,14 @@ __global__ __launch_bounds__(NTR) void band_mk_panel_kernel(
   const int t = threadIdx.x, lane = t & 63;
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
   const int c16 = lane & 15, g4 = lane >> 4;
-  const int cq = t & 15, rg = t >> 4;
   BandWork bw(work + cd.work, n, L);
   double* A = bw.A;
-  band_panel_factor(A, n, k0, r0, m, Vs, Gs, &red[0][0], Ts, taus, bw.T + (int64_t)p * BB * BB);
+  const bool timed = tim != nullptr && t == 0;
+  long long tk[6];
+  if (timed) tk[5] = (long long)__builtin_amdgcn_s_memtime();
+  band_panel_factor(A, n, k0, r0, m, Vs, Gs, &red[0][0], Ts, taus, bw.T + (int64_t)p * BB * BB,
+                    timed ? tk : nullptr);
+  if (timed) tk[2] = (long long)__builtin_amdgcn_s_memtime();
   // U = V T -> Ug, V -> Vg (all BMP rows: rows >= m are zero)
 #pragma unroll
   for (int q = 0; q < BMP / 16 / NWR; ++q) {
@@ -553,35 +573,15 @@ __global__ __launch_bounds__(NTR) void band_mk_panel_kernel(
     for (int r = 0; r < 4; ++r) bw.Ug[(i0 + g4 + 4 * r) * BB + c16] = acc[r];
   }
   for (int e = t; e < BMP * BB; e += NTR) bw.Vg[e] = Vs[e / BB][e % BB];
-  // z <- Q_p^T z = z - V (T^T (V^T z))
-  {
-    double s = 0.0;
-    for (int i = rg; i < m; i += 32) s += Vs[i][cq] * bw.z[r0 + i];
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
-    if (lane < 16) red2[wid][lane] = s;
-  }
-  __syncthreads();
-  double zv[BB], zt[BB];
-#pragma unroll
-  for (int a = 0; a < BB; ++a) {
-    double s = 0.0;
-#pragma unroll
-    for (int w = 0; w < NWR; ++w) s += red2[w][a];
-    zv[a] = s;
-  }
-#pragma unroll
-  for (int c = 0; c < BB; ++c) {
-    double s = 0.0;
-#pragma unroll
-    for (int a = 0; a <= c; ++a) s += Ts[a][c] * zv[a];
-    zt[c] = s;
-  }
-  for (int i = t; i < m; i += NTR) {
-    double s = 0.0;
-#pragma unroll
-    for (int c = 0; c < BB; ++c) s += Vs[i][c] * zt[c];
-    bw.z[r0 + i] -= s;
+  if (timed) tk[3] = (long long)__builtin_amdgcn_s_memtime();
+  if (timed) {   // cycles: load | QR | G,T | U,V stores | -   (accumulated over panels)
+    tk[4] = (long long)__builtin_amdgcn_s_memtime();
+    long long* o = tim + (int64_t)blockIdx.x * 8;
+    o[0] += tk[0] - tk[5];
+    o[1] += tk[1] - tk[0];
+    o[2] += tk[2] - tk[1];
+    o[3] += tk[3] - tk[2];
+    o[4] += tk[4] - tk[3];
   }
 }
 
@@ -589,6 +589,7 @@ __global__ __launch_bounds__(256) void band_mk_x_kernel(const RidgeCellDesc* __r
                                                         int L, double* __restrict__ work, int p,
                                                         int nxb) {
   __shared__ double red[4][BB * BB];
+  __shared__ double redz[4][BB];
   const int cell = blockIdx.x / nxb, xb = blockIdx.x % nxb;
   const RidgeCellDesc cd = cells[cell];
   const int n = cd.n;
@@ -604,6 +605,7 @@ __global__ __launch_bounds__(256) void band_mk_x_kernel(const RidgeCellDesc* __r
   const int i0 = xb * MK_XR + 16 * wid;          // this wave's 16 rows of X
   double4_t X = {0.0, 0.0, 0.0, 0.0};
   double4_t Pp = {0.0, 0.0, 0.0, 0.0};
+  double4_t Pz = {0.0, 0.0, 0.0, 0.0};            // V_I^T z_I in column 0 (z as B column 0)
   if (i0 < m) {
     // X[i][:] = sum_k A22[k][i] U[k][:]  (A symmetric: row k, 16 contiguous columns)
     const int col = r0 + min(i0 + c16, m - 1);
@@ -628,15 +630,24 @@ __global__ __launch_bounds__(256) void band_mk_x_kernel(const RidgeCellDesc* __r
     for (int r = 0; r < 4; ++r)
       if (i0 + g4 + 4 * r >= m) X[r] = 0.0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      Pp = mfma_f64_16x16x4(Vg[(i0 + 4 * r + g4) * BB + c16], X[r], Pp);
+    for (int r = 0; r < 4; ++r) {
+      const int row = i0 + 4 * r + g4;
+      const double va = Vg[row * BB + c16];
+      Pp = mfma_f64_16x16x4(va, X[r], Pp);
+      Pz = mfma_f64_16x16x4(va, (c16 == 0 && row < m) ? bw.z[r0 + row] : 0.0, Pz);
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) bw.Xg[(i0 + g4 + 4 * r) * BB + c16] = X[r];
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[wid][(g4 + 4 * r) * BB + c16] = Pp[r];
+  if (c16 == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) redz[wid][g4 + 4 * r] = Pz[r];
+  }
   __syncthreads();
   bw.Pg[xb * BB * BB + t] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+  if (t < BB) bw.Pzg[xb * BB + t] = redz[0][t] + redz[1][t] + redz[2][t] + redz[3][t];
 }
 
 __global__ __launch_bounds__(256) void band_mk_trail_kernel(const RidgeCellDesc* __restrict__ cells,
@@ -646,6 +657,8 @@ __global__ __launch_bounds__(256) void band_mk_trail_kernel(const RidgeCellDesc*
   __shared__ double Ms[BB][LS];
   __shared__ double Vl[2 * MK_TS][LS];
   __shared__ double Wl[2 * MK_TS][LS];
+  __shared__ double Zv[BB];
+  __shared__ double Zt[BB];
   const int cell = blockIdx.x / ntile, tile = blockIdx.x % ntile;
   int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
   if (I * (I + 1) / 2 > tile) --I;
@@ -660,12 +673,17 @@ __global__ __launch_bounds__(256) void band_mk_trail_kernel(const RidgeCellDesc*
   const int c16 = lane & 15, g4 = lane >> 4;
   BandWork bw(work + cd.work, n, L);
   double* __restrict__ A = bw.A;
-  // M = T^T sum_b P_b
+  // M = T^T sum_b P_b   (tiles (I, 0) also sum the V^T z partials: z rows of block I)
+  const int nxb = (m + MK_XR - 1) / MK_XR;
   {
-    const int nxb = (m + MK_XR - 1) / MK_XR;
     double s = 0.0;
     for (int b = 0; b < nxb; ++b) s += bw.Pg[b * BB * BB + t];
     Ps[t / BB][t % BB] = s;
+    if (J == 0 && t < BB) {
+      double z = 0.0;
+      for (int b = 0; b < nxb; ++b) z += bw.Pzg[b * BB + t];
+      Zv[t] = z;
+    }
   }
   // V rows of the I block (local 0..31) and the J block (local 32..63)
   for (int e = t; e < 2 * MK_TS * BB; e += 256) {
@@ -681,6 +699,12 @@ __global__ __launch_bounds__(256) void band_mk_trail_kernel(const RidgeCellDesc*
 #pragma unroll
     for (int c = 0; c < BB; ++c) s += Tp[c * BB + a] * Ps[c][b];
     Ms[a][b] = s;
+    if (J == 0 && t < BB) {                    // zt = T^T (V^T z)
+      double z = 0.0;
+#pragma unroll
+      for (int c = 0; c < BB; ++c) z += Tp[c * BB + t] * Zv[c];
+      Zt[t] = z;
+    }
   }
   __syncthreads();
   // W = X - 1/2 V M for the same 64 rows
@@ -691,6 +715,15 @@ __global__ __launch_bounds__(256) void band_mk_trail_kernel(const RidgeCellDesc*
 #pragma unroll
     for (int a = 0; a < BB; ++a) s += Vl[lr][a] * Ms[a][c];
     Wl[lr][c] = (gi < m) ? bw.Xg[gi * BB + c] - 0.5 * s : 0.0;
+  }
+  if (J == 0 && t < MK_TS) {                   // z <- Q_p^T z on the rows of block I
+    const int gi = I * MK_TS + t;
+    if (gi < m) {
+      double v = 0.0;
+#pragma unroll
+      for (int c = 0; c < BB; ++c) v += Vl[t][c] * Zt[c];
+      bw.z[r0 + gi] -= v;
+    }
   }
   __syncthreads();
   // wave -> 16 x 16 sub-tile (si, sj); on a diagonal tile the upper sub-tile is the mirror
@@ -932,6 +965,7 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
     }
     __syncthreads();
   }
+  __syncthreads();                     // (no panels: the Ys load still needs the barrier)
   double* out = beta_out + cd.out;
   for (int e = t; e < lw * n; e += NTB) {
     const int c = e / n, i = e % n;
@@ -944,7 +978,7 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
 extern "C" int64_t pfml_ridge_band_work_doubles(int n, int L) {
   const int64_t np = (n + BB - 1) / BB;
   return (int64_t)n * n + (int64_t)n * LS + n + np * BB * BB + (int64_t)L * n +
-         (int64_t)L * n * LS + 3LL * BMP * BB + (int64_t)(BMP / MK_XR) * BB * BB;
+         (int64_t)L * n * LS + 3LL * BMP * BB + (int64_t)(BMP / MK_XR) * (BB * BB + BB);
 }
 
 extern "C" int pfml_ridge_band_nmax() { return BNMAX; }
@@ -958,8 +992,10 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   // band_mode 1 (or PFML_BAND_MODE=single, or phase timing): one workgroup per cell for the
   // whole reduction; 2 / default: the multi-workgroup form, three launches per panel.
   const char* mode = getenv("PFML_BAND_MODE");
-  const bool single = tim != nullptr || band_mode == 1 ||
-                      (band_mode == 0 && mode && mode[0] == 's');
+  // (phase timing: the single kernel unless PFML_BAND_MODE=multi)
+  const bool env_multi = mode && mode[0] == 'm';
+  const bool single = band_mode == 1 || (band_mode == 0 && mode && mode[0] == 's') ||
+                      (tim != nullptr && band_mode == 0 && !env_multi);
   if (single) {
     hipLaunchKernelGGL(ridge_band_reduce_kernel, dim3(ncells), dim3(NTR), 0, st, SD, ldS, Sr, cd,
                        L, work, tim);
@@ -972,7 +1008,8 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
       const int nxb = (mmax + MK_XR - 1) / MK_XR;
       const int tt = (mmax + MK_TS - 1) / MK_TS;
       const int ntile = tt * (tt + 1) / 2;
-      hipLaunchKernelGGL(band_mk_panel_kernel, dim3(ncells), dim3(NTR), 0, st, cd, L, work, p);
+      hipLaunchKernelGGL(band_mk_panel_kernel, dim3(ncells), dim3(NTR), 0, st, cd, L, work, p,
+                         tim);
       hipLaunchKernelGGL(band_mk_x_kernel, dim3(ncells * nxb), dim3(256), 0, st, cd, L, work, p,
                          nxb);
       hipLaunchKernelGGL(band_mk_trail_kernel, dim3(ncells * ntile), dim3(256), 0, st, cd, L,
