@@ -16,7 +16,10 @@
 
 namespace {
 
-constexpr int BM = 64, BK = 16, NCOL = 112, NTILE = NCOL / 16, PAD = 16;
+constexpr int BM = 64, BK = 16, NCOL = 112, NTILE = NCOL / 16;
+// LDS row strides: k-rows 1 apart must land 32 banks apart (a 32-lane ds_read_b64 group reads
+// rows k and k+1), i.e. a stride = 16 (mod 32) doubles: 64 + 16 for D, 112 + 0 for beta.
+constexpr int PAD = 16, PADB = 0;
 
 struct JobDesc {
   int64_t d_off;     // offset of D_t (P x P, ld ldD)
@@ -31,7 +34,7 @@ __global__ __launch_bounds__(256) void quadform_kernel(
     const double* __restrict__ Bt, int64_t ldB, const JobDesc* __restrict__ jobs,
     const int* __restrict__ tile_job, int L, double* __restrict__ partial) {
   __shared__ double As[2][BK][BM + PAD];
-  __shared__ double Bs[2][BK][NCOL + PAD];
+  __shared__ double Bs[2][BK][NCOL + PADB];
   __shared__ double red[4][NCOL];
 
   const int tile = blockIdx.x;
