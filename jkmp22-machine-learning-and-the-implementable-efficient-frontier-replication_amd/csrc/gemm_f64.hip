@@ -8,16 +8,21 @@
 // are fused as row/column scales of the epilogue, so they cost O(MN) instead of a GEMM.
 //
 // Tiling: BM x BN output tile per 256-thread workgroup (4 waves, 2 x 2), BK = 16 staged in
-// LDS in k-major layout with a 16-double pad per row (a row stride of 32 banks mod 64, so the
-// two 16-lane halves of a 32-lane ds_read_b64 group never hit the same bank).  Each wave owns
-// a (BM/2) x (BN/2) sub-tile = (BM/32) x (BN/32) MFMA 16x16 accumulators.  Double-buffered
-// LDS: the global loads of K-step t+1 are issued into registers before the MFMAs of step t.
+// LDS.  Each operand keeps the layout it has in global memory, so the LDS stores are as
+// conflict-free as the coalesced global loads: an operand contiguous along k (A not
+// transposed, B transposed) is stored [row][k] with a row stride of 18 doubles (the 16 rows x
+// 2 k of one ds_read_b64 group then hit 32 distinct bank pairs), one contiguous along its
+// row/column index is stored [k][index] with a 16-double pad (stride = 32 banks mod 64).
+// Each wave owns a (BM/2) x (BN/2) sub-tile = (BM/32) x (BN/32) MFMA 16x16 accumulators.
+// Double-buffered LDS: the global loads of K-step t+1 are issued into registers before the
+// MFMAs of step t.
 #include "common.h"
 
 namespace {
 
 constexpr int BK = 16;
-constexpr int PAD = 16;
+constexpr int PAD = 16;      // [k][index] layouts
+constexpr int KS = BK + 2;   // [index][k] layouts: row stride in doubles
 
 template <bool TA, bool TB, int BM, int BN>
 __global__ __launch_bounds__(256) void dgemm_kernel(
@@ -29,8 +34,13 @@ __global__ __launch_bounds__(256) void dgemm_kernel(
     const double* __restrict__ cs, int64_t scs) {
   constexpr int TM = BM / 32, TN = BN / 32;         // MFMA tiles per wave (M, N)
   constexpr int LA = BM * BK / 256, LB = BN * BK / 256;  // elements loaded per thread
-  __shared__ double As[2][BK][BM + PAD];
-  __shared__ double Bs[2][BK][BN + PAD];
+  // A: TA ? [k][i] : [i][k];  B: TB ? [j][k] : [k][j]   (flat, see the header)
+  constexpr int ASZ = TA ? BK * (BM + PAD) : BM * KS;
+  constexpr int BSZ = TB ? BN * KS : BK * (BN + PAD);
+  __shared__ double As[2][ASZ];
+  __shared__ double Bs[2][BSZ];
+  auto aidx = [](int i, int k) { return TA ? k * (BM + PAD) + i : i * KS + k; };
+  auto bidx = [](int k, int j) { return TB ? j * KS + k : k * (BN + PAD) + j; };
 
   const int b = blockIdx.y;
   A += (int64_t)b * sA;
@@ -80,14 +90,14 @@ __global__ __launch_bounds__(256) void dgemm_kernel(
       const int e = t + q * 256;
       int i, k;
       if (TA) { k = e / BM; i = e % BM; } else { i = e / BK; k = e % BK; }
-      As[buf][k][i] = ra[q];
+      As[buf][aidx(i, k)] = ra[q];
     }
 #pragma unroll
     for (int q = 0; q < LB; ++q) {
       const int e = t + q * 256;
       int j, k;
       if (TB) { j = e / BK; k = e % BK; } else { k = e / BN; j = e % BN; }
-      Bs[buf][k][j] = rb[q];
+      Bs[buf][bidx(k, j)] = rb[q];
     }
   };
 
@@ -102,9 +112,9 @@ __global__ __launch_bounds__(256) void dgemm_kernel(
     for (int kk = 0; kk < BK; kk += 4) {
       double a[TM], bb[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = As[cur][kk + (lane >> 4)][wm * (BM / 2) + i * 16 + (lane & 15)];
+      for (int i = 0; i < TM; ++i) a[i] = As[cur][aidx(wm * (BM / 2) + i * 16 + (lane & 15), kk + (lane >> 4))];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bb[j] = Bs[cur][kk + (lane >> 4)][wn * (BN / 2) + j * 16 + (lane & 15)];
+      for (int j = 0; j < TN; ++j) bb[j] = Bs[cur][bidx(kk + (lane >> 4), wn * (BN / 2) + j * 16 + (lane & 15))];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll

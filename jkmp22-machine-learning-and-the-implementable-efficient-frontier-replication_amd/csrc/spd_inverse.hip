@@ -75,7 +75,12 @@ __global__ __launch_bounds__(256) void gj_rowpanel_kernel(const double* __restri
   const int b = blockIdx.y;
   const double* Ab = A + (int64_t)b * sA;
   const int t = threadIdx.x;
-  for (int e = t; e < nb * nb; e += 256) P[e / nb][e % nb] = Pbuf[(int64_t)b * NB * NB + (e / nb) * NB + (e % nb)];
+  // the full NB x NB tile: entries beyond nb must read as 0 (the product below runs over all
+  // NB columns, and 0 * uninitialised LDS can be NaN)
+  for (int e = t; e < NB * NB; e += 256) {
+    const int i = e / NB, q = e % NB;
+    P[i][q] = (i < nb && q < nb) ? Pbuf[(int64_t)b * NB * NB + i * NB + q] : 0.0;
+  }
   __syncthreads();
   const int j = blockIdx.x * 256 + t;
   if (j >= n) return;

@@ -235,15 +235,17 @@ def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         Sigma.diagonal(dim1=1, dim2=2).add_(iv)
         m = la.m_func(Sigma, lam, wv, rfv, mu, gamma, cfg.run.iterations, mask=mask)
 
-        # (24): Horner chains over [S^{g=0} | ... | S^{g=G-1} | I]
+        # (24): Horner chains over [S^{g=0} | ... | S^{g=G-1} | I]; with identical signals for
+        # every g (quirk Q1, compat mode) one block is carried and shared
         Dg = gt_t[idx_t]                                           # [B, 13, N]
-        GP = G * P
+        Gc = 1 if same_w else G
+        GP = Gc * P
         Wd = GP + N
         eye = torch.eye(N, dtype=torch.float64, device=dev).expand(B, N, N)
 
         def aug(th):
             Tm = torch.empty((B, N, Wd), dtype=torch.float64, device=dev)
-            for g in range(G):
+            for g in range(Gc):
                 Tm[:, :, g * P:(g + 1) * P] = S_all[g][:, th]
             Tm[:, :, GP:] = eye
             return Tm
@@ -270,6 +272,15 @@ def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         SO = gemm(Xl, gemm(Fb, XtO)) + iv.unsqueeze(-1) * omega               # Sigma omega
         lw = lam * wv.view(B, 1)
         for g in range(G):
+            if g >= Gc:                                  # shared block (quirk Q1)
+                d_out[g, b0:b0 + B] = d_out[0, b0:b0 + B]
+                r_out[g, b0:b0 + B] = r_out[0, b0:b0 + B]
+                if keep_risk_tc:
+                    risk_out[g, b0:b0 + B] = risk_out[0, b0:b0 + B]
+                    tc_out[g, b0:b0 + B] = tc_out[0, b0:b0 + B]
+                for bi in range(B):
+                    signal_t[g][b0 + bi] = signal_t[0][b0 + bi]
+                continue
             sl = slice(g * P, (g + 1) * P)
             og, cg = omega[:, :, sl].contiguous(), omega_chg[:, :, sl].contiguous()
             risk = gemm(og, SO[:, :, sl].contiguous(), trans_a=True, alpha=gamma)

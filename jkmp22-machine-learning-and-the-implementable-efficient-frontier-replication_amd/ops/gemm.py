@@ -1,10 +1,19 @@
 """fp64 batched GEMM with fused diagonal scalings.
 
 ``gemm(A, B)`` computes ``alpha * diag(rs) @ op(A) @ op(B) @ diag(cs) + beta * C`` for 2-D or
-3-D (batched) fp64 tensors.  On a HIP device it runs ``pfml_dgemm`` (csrc/gemm_f64.hip,
-v_mfma_f64_16x16x4_f64); on CPU it is the torch fp64 oracle.
+3-D (batched) fp64 tensors.  On CPU it is the torch fp64 oracle.  On a HIP device:
+
+* a product with a fused diagonal scaling runs ``pfml_dgemm`` (csrc/gemm_f64.hip,
+  v_mfma_f64_16x16x4_f64, scales in the epilogue);
+* a plain product (no scaling) is a library GEMM and goes to rocBLAS through torch
+  (``baddbmm``), which sustains 40-66 TF/s fp64 on the S4 shapes against 19-40 TF/s for the
+  hand-written tile (tools/bench_gemm.py, profiles/r01_gemm_own_vs_rocblas.json).
+
+``backend="own"`` (or PFML_GEMM=own) forces the hand-written kernel, ``"blas"`` rocBLAS.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -19,10 +28,23 @@ def _bstride(x3, batch):
     return 0 if (x3.shape[0] == 1 and batch > 1) else x3.stride(0)
 
 
+def _blas_gemm(A3, B3, trans_a, trans_b, alpha, beta, C3) -> None:
+    a = A3.transpose(1, 2) if trans_a else A3
+    b = B3.transpose(1, 2) if trans_b else B3
+    if a.shape[0] != C3.shape[0]:
+        a = a.expand(C3.shape[0], -1, -1)
+    if b.shape[0] != C3.shape[0]:
+        b = b.expand(C3.shape[0], -1, -1)
+    if beta == 0.0:
+        torch.bmm(a, b, out=C3) if alpha == 1.0 else C3.copy_(torch.bmm(a, b).mul_(alpha))
+    else:
+        C3.baddbmm_(a, b, beta=beta, alpha=alpha)
+
+
 def gemm(A: torch.Tensor, B: torch.Tensor, *, trans_a: bool = False, trans_b: bool = False,
          alpha: float = 1.0, beta: float = 0.0, out: torch.Tensor | None = None,
-         row_scale: torch.Tensor | None = None, col_scale: torch.Tensor | None = None
-         ) -> torch.Tensor:
+         row_scale: torch.Tensor | None = None, col_scale: torch.Tensor | None = None,
+         backend: str = "auto") -> torch.Tensor:
     squeeze = A.dim() == 2 and B.dim() == 2 and (out is None or out.dim() == 2)
     A3, B3 = _as3(A), _as3(B)
     batch = max(A3.shape[0], B3.shape[0])
@@ -40,7 +62,12 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, trans_a: bool = False, trans_b: bo
     rs3 = None if row_scale is None else (row_scale.unsqueeze(0) if row_scale.dim() == 1 else row_scale)
     cs3 = None if col_scale is None else (col_scale.unsqueeze(0) if col_scale.dim() == 1 else col_scale)
 
-    if nat.is_device(A):
+    if backend == "auto":
+        backend = os.environ.get("PFML_GEMM", "auto")
+    if (nat.is_device(A) and backend != "own" and rs3 is None and cs3 is None
+            and C3.stride(-1) == 1 and (backend == "blas" or A.dtype == torch.float64)):
+        _blas_gemm(A3, B3, trans_a, trans_b, float(alpha), float(beta), C3)
+    elif nat.is_device(A):
         if A.dtype != torch.float64:
             raise TypeError("pfml_dgemm is fp64-only")
         # a transposed view is consumed as-is by flipping the operand's transpose flag

@@ -45,6 +45,14 @@ def spd_inverse(A: torch.Tensor, inplace: bool = False) -> torch.Tensor:
         if bad.numel():
             COUNTERS.add("linalg.spd_inverse_lu_fallback", int(bad.numel()))
             src = A.unsqueeze(0) if squeeze else A
+            import os
+            if os.environ.get("PFML_DEBUG_INV"):
+                for b in bad.tolist()[:4]:
+                    M = src[b]
+                    print(f"[spd_inverse] bad b={b} n={M.shape[-1]} nan={int(torch.isnan(M).sum())} "
+                          f"absmax={float(M.abs().max()):.3e} "
+                          f"diagmin={float(torch.diagonal(M).min()):.3e} "
+                          f"asym={float((M - M.T).abs().max()):.3e}", flush=True)
             X[bad] = torch.linalg.inv(src[bad])
     else:
         X.copy_(torch.linalg.inv(X))
