@@ -83,6 +83,47 @@ def one_step(reals: PfmlReals, cfg: Config, engine=None):
     return res, out
 
 
+def s4_stress(args) -> None:
+    """BASELINE config 4 (3000-stock universe): per-month S4 cost at a large N (Barra Sigma,
+    m_func with its 20+ N x N inversions, the (24) Horner chains over [S | I] of width
+    2P + N, the LU solves and the (25) products), months batched to fill HBM."""
+    from pfml.data.synthetic import engine_inputs
+    from pfml.models.pfml_inputs import build_inputs
+    from pfml.utils.dates import pfml_date_grids
+    env = pdist.init(args.device)
+    dev = env.device
+    cfg = Config.default()
+    cfg.run.compat_mode = False
+    chars, barra, wealth, rf = engine_inputs(n_stocks=args.stocks)
+    g = pfml_date_grids(int(barra.months.min()), 11, cfg.settings["split"]["test_end"], 1971, 10)
+    months = g["m2"][-args.s4_stress:]
+    mine = months[np.asarray(list(coll.contiguous_split(len(months), env.world_size, env.rank)))]
+    for _ in range(args.warmup):
+        build_inputs(cfg, chars, barra, wealth, rf, dev, months=mine[: max(1, len(mine) // 4)])
+    pdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats(dev)
+    t0 = time.perf_counter()
+    out = build_inputs(cfg, chars, barra, wealth, rf, dev, months=mine)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    pdist.barrier()
+    dt = coll.all_reduce_max(time.perf_counter() - t0, device=dev)
+    finite = bool(torch.isfinite(out.reals.denom).all().item())
+    peak = torch.cuda.max_memory_allocated(dev) / 2**30 if dev.type == "cuda" else 0.0
+    if env.is_main:
+        print(json.dumps({
+            "metric": "S4 PFML input construction (m_func, (24), (25)) months/s",
+            "value": round(len(months) / dt, 3), "unit": "months/s", "n_gpus": env.world_size,
+            "ms_per_month": round(1000 * dt / len(months), 2), "higher_is_better": True,
+            "dtype": "fp64", "data": "synthetic engine inputs (no WRDS/JKP data available)",
+            "config": {"n_stocks": args.stocks, "months": len(months), "P": cfg.p_max + 1,
+                       "G": len(cfg.g_vec), "peak_hbm_gib": round(peak, 1),
+                       "outputs_finite": finite}}), flush=True)
+    pdist.shutdown()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,7 +135,12 @@ def main():
     ap.add_argument("--with-inputs", action="store_true",
                     help="time S4 (PFML input construction for every month) + S5 + S6")
     ap.add_argument("--stocks", type=int, default=500)
+    ap.add_argument("--s4-stress", type=int, default=0, metavar="MONTHS",
+                    help="auxiliary: time only the S4 input construction of the last MONTHS "
+                         "PFML months for a --stocks universe (e.g. the 3000-stock stress)")
     args = ap.parse_args()
+    if args.s4_stress:
+        return s4_stress(args)
 
     env = pdist.init(args.device)
     dev = env.device

@@ -166,7 +166,7 @@ class RunOptions:
     device: str = "auto"               # auto | cpu | cuda
     world_size: int = 1
     iterations: int = 10               # m_func fixed-point steps (hard-coded 10 in reference)
-    month_batch: int = 64              # PFML months processed per device batch (S4)
+    month_batch: int = 0               # PFML months per batch (S4); 0 = sized to free memory
     data_dir: str = "Data"
     artifact_dir: str = "artifacts"
     check: bool = False                # compare device results against the CPU oracle

@@ -241,6 +241,8 @@ extern "C" int64_t pfml_lu_solve_work_doubles(int n, int m, int batch) {
 }
 
 // Solve A X = B in place for `batch` augmented systems (see header); X overwrites B.
+extern "C" int pfml_lu_solve_max_n() { return PMAX; }
+
 extern "C" hipError_t pfml_lu_solve(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
                                     int b0, int batch, double* work, int* status,
                                     hipStream_t st) {

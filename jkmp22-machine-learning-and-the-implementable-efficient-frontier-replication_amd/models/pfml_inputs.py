@@ -123,6 +123,25 @@ def vol_scales(panel: Panel, barra: BarraCov, months: np.ndarray) -> np.ndarray:
     return s.fillna(med).to_numpy()
 
 
+def auto_month_batch(n_stocks: int, gp: int, device, cap: int = 256) -> int:
+    """Months per S4 batch from the memory one month's working set needs (fp64): the
+    13-month signal window (13 N GP), the Horner chains and solves (~6 N (GP + N)) and ~14
+    N x N matrices of m_func / Sigma.  A device batch takes up to 60 % of free HBM (288 GB on
+    MI355X: ~256 months at N = 500, ~75 at N = 3000), a host batch 25 % of available RAM."""
+    per = 8.0 * (13.0 * n_stocks * gp + 6.0 * n_stocks * (gp + n_stocks) + 14.0 * n_stocks ** 2)
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        free, _ = torch.cuda.mem_get_info(dev)
+        budget = 0.6 * free
+    else:
+        try:
+            import psutil
+            budget = 0.25 * psutil.virtual_memory().available
+        except Exception:                                   # pragma: no cover
+            budget = 4e9
+    return int(max(1, min(cap, budget // per)))
+
+
 def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.DataFrame,
                  risk_free: pd.DataFrame, device, months: np.ndarray | None = None,
                  keep_risk_tc: bool = False, batch: int | None = None) -> PfmlInputs:
@@ -175,6 +194,10 @@ def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
     signal_t = [[None] * T for _ in range(G)]
     Rpad = len(panel.mi)
     bsz = batch or cfg.run.month_batch
+    if not bsz or bsz <= 0:
+        nmax = max(len(panel.valid_rows(int(d))) for d in months) if T else 1
+        bsz = auto_month_batch(nmax, G * P, dev)
+        log.info(f"PFML inputs: {bsz} months per batch (N <= {nmax})")
 
     for b0 in range(0, T, bsz):
         bm = months[b0: b0 + bsz]

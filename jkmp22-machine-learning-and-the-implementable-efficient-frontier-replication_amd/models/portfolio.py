@@ -115,7 +115,10 @@ def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
     K = barra.X.shape[1]
     # ---- batched m_t for every OOS month (K19) --------------------------------------
     ms = []
-    chunk = max(1, int(cfg.run.month_batch))
+    chunk = int(cfg.run.month_batch)
+    if chunk <= 0:
+        from .pfml_inputs import auto_month_batch
+        chunk = auto_month_batch(N, 0, dev)
     for c0 in range(0, B, chunk):
         cm = months[c0:c0 + chunk]
         Bc = len(cm)

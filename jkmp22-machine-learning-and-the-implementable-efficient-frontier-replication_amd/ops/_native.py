@@ -47,6 +47,7 @@ def _declare_hip(lib):
     lib.pfml_lu_solve.restype = I
     lib.pfml_lu_solve_work_doubles.argtypes = [I, I, I]
     lib.pfml_lu_solve_work_doubles.restype = L
+    lib.pfml_lu_solve_max_n.restype = I
     lib.pfml_spd_blockinv.argtypes = [P, L, L, I, I, I, P, P, P]
     lib.pfml_spd_blockinv.restype = I
     lib.pfml_spd_block_size.restype = I

@@ -89,10 +89,18 @@ def _spd_inverse_blocked(X: torch.Tensor, status: torch.Tensor) -> None:
         X[:, k0:k0 + nb, k0:k0 + nb] = Pk
 
 
+def _lu_max_n() -> int:
+    return int(nat.hip_lib().pfml_lu_solve_max_n())
+
+
 def solve_augmented(M: torch.Tensor, n: int, m: int, a0: int, b0: int) -> torch.Tensor:
     """In-place solve of augmented systems: rows of M [B, n, W] hold A at columns a0..a0+n and
-    B at b0..b0+m; on return the B columns hold X = A^-1 B (returned as a view)."""
-    if nat.is_device(M):
+    B at b0..b0+m; on return the B columns hold X = A^-1 B (returned as a view).
+
+    Device: csrc/lu_solve.hip (blocked LU with partial pivoting, the pivot panel in LDS) up to
+    n = pfml_lu_solve_max_n() (1024); larger systems (the 3000-stock stress) take the library
+    (rocSOLVER) LU through torch."""
+    if nat.is_device(M) and n <= _lu_max_n():
         if not M.is_contiguous():
             raise ValueError("solve_augmented: contiguous storage required")
         Bt, nn, W = M.shape
