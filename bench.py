@@ -135,6 +135,9 @@ def main():
     ap.add_argument("--with-inputs", action="store_true",
                     help="time S4 (PFML input construction for every month) + S5 + S6")
     ap.add_argument("--stocks", type=int, default=500)
+    ap.add_argument("--tiny", action="store_true",
+                    help="CI only: p in {8, 16}, 180 months (exercises the multi-rank path on "
+                         "CPU/gloo; not the benchmark config)")
     ap.add_argument("--s4-stress", type=int, default=0, metavar="MONTHS",
                     help="auxiliary: time only the S4 input construction of the last MONTHS "
                          "PFML months for a --stocks universe (e.g. the 3000-stock stress)")
@@ -145,6 +148,10 @@ def main():
     env = pdist.init(args.device)
     dev = env.device
     cfg = Config.default()
+    if args.tiny:
+        cfg = cfg.override(["pf_ml.p_vec=[8,16]", "pf.dates.start_year=2008",
+                            "pf.dates.end_yr=2020"])
+        args.months, args.stocks = min(args.months, 180), min(args.stocks, 40)
     n_solves = (len(cfg.g_vec) * len(cfg.hp_years) * len(cfg.p_vec) * len(cfg.l_vec))
     n_util = n_solves * 12
 
@@ -163,7 +170,7 @@ def main():
         args.months = len(months)
         reals = None
     else:
-        reals = synthetic_reals(cfg, dev, n_months=args.months)
+        reals = synthetic_reals(cfg, dev, n_months=args.months, n_stocks=args.stocks)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t_setup = time.perf_counter() - t_setup

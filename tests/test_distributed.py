@@ -90,3 +90,28 @@ def test_collectives_gloo(tmp_path):
         assert d["g"][:, 0].tolist() == [0.0, 1.0, 1.0, 2.0, 2.0, 2.0]
         assert d["pre"].item() == sum(range(1, r + 1))
         assert d["mx"] == 2.0
+
+
+def test_bench_contract_two_ranks_gloo(tmp_path):
+    """bench.py under the driver's exact launcher (torch.distributed.run, 2 ranks, 127.0.0.1):
+    one JSON line from rank 0 with the contract keys, timing max-reduced over ranks."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=root)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+           "--tiny", "--device", "cpu"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=str(tmp_path),
+                       env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in rec, k
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
+    assert rec["value"] > 0 and rec["config"]["outputs_finite"]
