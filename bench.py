@@ -117,7 +117,7 @@ def s4_stress(args) -> None:
             "metric": "S4 PFML input construction (m_func, (24), (25)) months/s",
             "value": round(len(months) / dt, 3), "unit": "months/s", "n_gpus": env.world_size,
             "ms_per_month": round(1000 * dt / len(months), 2), "higher_is_better": True,
-            "dtype": "fp64", "data": "synthetic engine inputs (no WRDS/JKP data available)",
+            "dtype": "fp64" if args.precision == "fp64" else f"fp64 (S4 GEMMs {args.precision})", "data": "synthetic engine inputs (no WRDS/JKP data available)",
             "config": {"n_stocks": args.stocks, "months": len(months), "P": cfg.p_max + 1,
                        "G": len(cfg.g_vec), "peak_hbm_gib": round(peak, 1),
                        "outputs_finite": finite}}), flush=True)
@@ -135,6 +135,9 @@ def main():
     ap.add_argument("--with-inputs", action="store_true",
                     help="time S4 (PFML input construction for every month) + S5 + S6")
     ap.add_argument("--stocks", type=int, default=500)
+    ap.add_argument("--precision", default="fp64", choices=["fp64", "bf16", "fp8"],
+                    help="with --with-inputs: S4 covariance / RFF / risk GEMMs on bf16 or fp8 "
+                         "MFMA (experimental; error vs fp64 reported); solves stay fp64")
     ap.add_argument("--tiny", action="store_true",
                     help="CI only: p in {8, 16}, 180 months (exercises the multi-rank path on "
                          "CPU/gloo; not the benchmark config)")
@@ -161,6 +164,7 @@ def main():
         from pfml.data.synthetic import engine_inputs
         from pfml.utils.dates import pfml_date_grids
         cfg.run.compat_mode = False          # distinct RFF draw per g: no Q1 duplication
+        cfg.run.precision = args.precision
         chars, barra, wealth, rf = engine_inputs(n_stocks=args.stocks)
         g = pfml_date_grids(int(barra.months.min()), 11, cfg.settings["split"]["test_end"],
                             1971, 10)
@@ -192,6 +196,15 @@ def main():
     value = n_solves / (ms / 1000.0)
     # sanity: finite outputs
     finite = bool(torch.isfinite(res.obj).all().item())
+    prec_err = None
+    if args.with_inputs and args.precision != "fp64":
+        from pfml.models.pfml_inputs import build_inputs
+        lo = build_inputs(cfg, *engine[:4], dev, months=engine[5]).reals
+        cfg.run.precision = "fp64"
+        hi = build_inputs(cfg, *engine[:4], dev, months=engine[5]).reals
+        rel = lambda a, b: float((a - b).norm() / b.norm())                       # noqa: E731
+        prec_err = {"denom_rel_fro": rel(lo.denom, hi.denom),
+                    "r_tilde_rel": rel(lo.r_tilde, hi.r_tilde)}
     if env.is_main:
         rec = {
             "metric": METRIC,
@@ -204,7 +217,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": round(value / BASELINE_SOLVES_PER_S, 2),
-            "dtype": "fp64",
+            "dtype": "fp64" if args.precision == "fp64" else f"fp64 (S4 GEMMs {args.precision})",
             "data": "synthetic (per-month PFML summands of production shape: 710 months, "
                     "P=513, denom_t = X'X/500 with X~N(0,1); no WRDS/JKP data available)",
             "config": {
@@ -218,6 +231,7 @@ def main():
                 "setup_s": round(t_setup, 2),
                 "outputs_finite": finite,
                 "includes_s4_inputs": bool(args.with_inputs),
+                "s4_precision_error_vs_fp64": prec_err,
             },
         }
         print(json.dumps(rec), flush=True)

@@ -162,7 +162,10 @@ class RunOptions:
     # RFF weight matrix is supplied), Q2 (validation rows accumulate across g), Q3
     # (pf.csv eom_ret == eom).  False gives the corrected behaviour.
     compat_mode: bool = True
-    precision: str = "fp64"            # fp64 | fp32 (experimental, error reported vs fp64)
+    # fp64 (production) | bf16 | fp8: the S4 covariance (K1), RFF (K13) and risk GEMMs on
+    # low-precision MFMA with fp32 accumulation; solves stay fp64 (bench --precision reports
+    # the error vs fp64)
+    precision: str = "fp64"
     device: str = "auto"               # auto | cpu | cuda
     world_size: int = 1
     iterations: int = 10               # m_func fixed-point steps (hard-coded 10 in reference)

@@ -35,7 +35,7 @@ import torch
 from ..config import Config, get_features, interleaved_order
 from ..data import io
 from ..ops import linalg as la
-from ..ops.gemm import gemm
+from ..ops.gemm import gemm, gemm_prec
 from ..ops.panel import rff_features, standardize_signals
 from ..utils.dates import month_index, pfml_date_grids
 from ..utils.log import get_logger
@@ -152,6 +152,7 @@ def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
     G, Pm = len(cfg.g_vec), cfg.p_max
     P = Pm + 1
     dev = torch.device(device)
+    prec = cfg.run.precision         # fp64 | bf16 | fp8: the covariance / RFF / risk GEMMs
     panel = Panel.from_chars(chars, features)
     grids = pfml_date_grids(int(barra.months.min()), lb, cfg.settings["split"]["test_end"],
                             cfg.settings["pf"]["dates"]["start_year"],
@@ -170,7 +171,7 @@ def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         if g > 0 and same_w:
             rffs.append(rffs[0])          # quirk Q1: identical inputs for every g
             continue
-        R = rff_features(Xf, torch.as_tensor(W[g], dtype=torch.float64, device=dev))
+        R = rff_features(Xf, torch.as_tensor(W[g], dtype=torch.float64, device=dev), prec)
         rffs.append(torch.cat([R, torch.zeros((1, P), dtype=R.dtype, device=dev)]))  # pad row
     del Xf
     range_pop()
@@ -254,7 +255,7 @@ def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         lam = torch.as_tensor(lam_h, device=dev)
         r = torch.as_tensor(r_h, device=dev)
         XF = gemm(Xl, Fb)
-        Sigma = gemm(XF, Xl, trans_b=True)
+        Sigma = gemm_prec(XF, Xl, prec, trans_b=True)            # K1: Barra covariance
         Sigma.diagonal(dim1=1, dim2=2).add_(iv)
         m = la.m_func(Sigma, lam, wv, rfv, mu, gamma, cfg.run.iterations, mask=mask)
 
@@ -306,7 +307,7 @@ def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
                 continue
             sl = slice(g * P, (g + 1) * P)
             og, cg = omega[:, :, sl].contiguous(), omega_chg[:, :, sl].contiguous()
-            risk = gemm(og, SO[:, :, sl].contiguous(), trans_a=True, alpha=gamma)
+            risk = gemm_prec(og, SO[:, :, sl].contiguous(), prec, trans_a=True, alpha=gamma)
             tc = gemm(cg, lw.unsqueeze(-1) * cg, trans_a=True)
             d_out[g, b0:b0 + B] = risk + tc
             r_out[g, b0:b0 + B] = rt_[:, sl]

@@ -13,11 +13,17 @@
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 
 import torch
 
 from . import _native as nat
+
+_P, _I, _L, _D = C.c_void_p, C.c_int, C.c_int64, C.c_double
+nat.register_hip("pfml_gemm_lowp", [_I, _I, _I, _I, _I, _I, _I, _D, _P, _L, _L, _P, _L, _L, _D,
+                                    _P, _L, _L, _P, _P, _P])
+LOWP_FORMATS = {"bf16": 1, "fp8": 2}
 
 
 def _as3(x):
@@ -106,3 +112,58 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, trans_a: bool = False, trans_b: bo
             r = r + beta * C3
         C3.copy_(r.expand_as(C3))
     return out.squeeze(0) if squeeze and out.dim() == 3 else out
+
+
+def _quantize(x: torch.Tensor, fmt: str) -> torch.Tensor:
+    """CPU oracle of the kernel's operand rounding (bf16 RNE; e4m3 of x * 448 / amax)."""
+    if fmt == "bf16":
+        return x.float().to(torch.bfloat16).double()
+    amax = float(x.abs().max())
+    s = 448.0 / amax if amax > 0 else 1.0
+    q = (x.float() * s).clamp(-448, 448).to(torch.float8_e4m3fn).double()
+    return q / s
+
+
+def gemm_lowp(A: torch.Tensor, B: torch.Tensor, fmt: str, *, trans_a: bool = False,
+              trans_b: bool = False, alpha: float = 1.0, beta: float = 0.0,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """alpha op(A) op(B) + beta C with bf16 / fp8-e4m3 operands and fp32 accumulation
+    (csrc/gemm_lowp.hip); fp64 in and out.  CPU: the same operand rounding in torch."""
+    code = LOWP_FORMATS[fmt]
+    squeeze = A.dim() == 2 and B.dim() == 2 and (out is None or out.dim() == 2)
+    A3, B3 = _as3(A), _as3(B)
+    batch = max(A3.shape[0], B3.shape[0])
+    M = A3.shape[2] if trans_a else A3.shape[1]
+    K = A3.shape[1] if trans_a else A3.shape[2]
+    N = B3.shape[1] if trans_b else B3.shape[2]
+    if out is None:
+        out = torch.empty((batch, M, N), dtype=torch.float64, device=A.device)
+    C3 = _as3(out)
+    if nat.is_device(A):
+        A3 = A3.contiguous() if A3.stride(-1) != 1 else A3
+        B3 = B3.contiguous() if B3.stride(-1) != 1 else B3
+        amax_a = A3.abs().amax().reshape(1).double() if fmt == "fp8" else None
+        amax_b = B3.abs().amax().reshape(1).double() if fmt == "fp8" else None
+        nat.check(nat.hip_lib().pfml_gemm_lowp(
+            code, int(trans_a), int(trans_b), M, N, K, batch, float(alpha),
+            A3.data_ptr(), A3.stride(1), _bstride(A3, batch),
+            B3.data_ptr(), B3.stride(1), _bstride(B3, batch), float(beta),
+            C3.data_ptr(), C3.stride(1), C3.stride(0), nat.ptr(amax_a), nat.ptr(amax_b),
+            nat.stream_of(A)), "pfml_gemm_lowp")
+    else:
+        a = _quantize(A3, fmt)
+        b = _quantize(B3, fmt)
+        a = a.transpose(1, 2) if trans_a else a
+        b = b.transpose(1, 2) if trans_b else b
+        r = alpha * torch.matmul(a, b)
+        if beta != 0.0:
+            r = r + beta * C3
+        C3.copy_(r.expand_as(C3))
+    return out.squeeze(0) if squeeze and out.dim() == 3 else out
+
+
+def gemm_prec(A: torch.Tensor, B: torch.Tensor, precision: str = "fp64", **kw) -> torch.Tensor:
+    """``gemm`` at the configured precision: fp64 (production) or a bf16 / fp8 experiment."""
+    if precision in LOWP_FORMATS:
+        return gemm_lowp(A, B, precision, **kw)
+    return gemm(A, B, **kw)

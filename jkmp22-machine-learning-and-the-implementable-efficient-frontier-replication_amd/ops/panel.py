@@ -10,17 +10,18 @@ import ctypes as C
 import torch
 
 from . import _native as nat
-from .gemm import gemm
+from .gemm import gemm_prec
 
 nat.register_hip("pfml_rff_sincos", [C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p])
 nat.register_hip("pfml_standardize", [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
                                       C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p])
 
 
-def rff_features(X: torch.Tensor, W: torch.Tensor) -> torch.Tensor:
-    """[R, k] x [k, P/2] -> [R, P+1] rows [1, cos z1, sin z1, cos z2, sin z2, ...]."""
+def rff_features(X: torch.Tensor, W: torch.Tensor, precision: str = "fp64") -> torch.Tensor:
+    """[R, k] x [k, P/2] -> [R, P+1] rows [1, cos z1, sin z1, cos z2, sin z2, ...].
+    ``precision`` bf16 / fp8: X W on the low-precision MFMA GEMM (experimental configs)."""
     R, half = X.shape[0], W.shape[1]
-    Z = gemm(X, W)
+    Z = gemm_prec(X, W, precision)
     out = torch.empty((R, 2 * half + 1), dtype=X.dtype, device=X.device)
     if nat.is_device(X):
         Zc = Z.contiguous()

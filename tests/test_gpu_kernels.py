@@ -182,3 +182,24 @@ def test_band_reduction_modes(gpu, mode, monkeypatch):
     out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
     rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
     assert rel < 1e-8, rel
+
+
+@pytest.mark.parametrize("fmt", ["bf16", "fp8"])
+@pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True)])
+def test_gemm_lowp(gpu, fmt, ta, tb):
+    """Low-precision MFMA GEMM (bf16 / fp8-e4m3 operands, fp32 accumulate): matches the CPU
+    oracle with the same operand rounding, and the fp64 product within the format's error."""
+    from pfml.ops.gemm import gemm_lowp
+    b, M, N, K = 3, 100, 70, 150
+    A = _rand(b, K, M, seed=71) if ta else _rand(b, M, K, seed=71)
+    B = _rand(b, N, K, seed=72) if tb else _rand(b, K, N, seed=72)
+    C0 = _rand(b, M, N, seed=73)
+    ref = gemm_lowp(A, B, fmt, trans_a=ta, trans_b=tb, alpha=0.5, beta=0.25, out=C0.clone())
+    out = gemm_lowp(A.to(gpu), B.to(gpu), fmt, trans_a=ta, trans_b=tb, alpha=0.5, beta=0.25,
+                    out=C0.to(gpu)).cpu()
+    scale = ref.abs().max().item()
+    assert (out - ref).abs().max().item() / scale < (2e-6 if fmt == "bf16" else 2e-2)
+    a = A.transpose(1, 2) if ta else A
+    bb = B.transpose(1, 2) if tb else B
+    exact = 0.5 * a @ bb + 0.25 * C0
+    assert (out - exact).abs().max().item() / scale < (1e-2 if fmt == "bf16" else 1e-1)
