@@ -51,3 +51,85 @@ extern "C" hipError_t pfml_segsum(const double* X, int64_t E, const int* seg_sta
   }
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------
+// Expanding-window sums of symmetric month matrices (K14, fused prefix):
+//   out[g, s] = sum over segments s' <= s of sum_{t in [start_s', stop_s')} X[g, t]
+// X: [G, T, P, P] (each X[g, t] symmetric), out: [G, S, P, P] (full, symmetric).
+// Pass 1 sums every (row, segment) over the UPPER triangle only (half the bytes of a dense
+// pass, one workgroup per (row, segment, g) for full-chip parallelism) into out; pass 2 runs
+// the prefix over segments in place and mirrors (i, j) to (j, i).  The dense segment sums +
+// torch cumsum it replaces read 2x and wrote 3x as much.
+namespace {
+
+__global__ __launch_bounds__(256) void wsum_upper_kernel(const double* __restrict__ X, int P,
+                                                         int T, const int* __restrict__ seg_start,
+                                                         const int* __restrict__ seg_stop,
+                                                         int nseg, double* __restrict__ out) {
+  const int i = blockIdx.x, s = blockIdx.y, g = blockIdx.z;
+  const int a = seg_start[s], b = seg_stop[s];
+  const int64_t PP = (int64_t)P * P;
+  const double* src = X + (int64_t)g * T * PP + (int64_t)i * P;
+  double* dst = out + ((int64_t)g * nseg + s) * PP + (int64_t)i * P;
+  for (int j = i + threadIdx.x; j < P; j += 256) {
+    double acc0 = 0.0, acc1 = 0.0;
+    int tm = a;
+    for (; tm + 2 <= b; tm += 2) {
+      acc0 += src[(int64_t)tm * PP + j];
+      acc1 += src[(int64_t)(tm + 1) * PP + j];
+    }
+    if (tm < b) acc0 += src[(int64_t)tm * PP + j];
+    dst[j] = acc0 + acc1;
+  }
+}
+
+// pass 2 on 32 x 32 tiles (I <= J) of the upper triangle: running sum over segments in
+// registers, tile (I, J) and its transpose (J, I) both written row-contiguous via LDS
+__global__ __launch_bounds__(256) void wsum_prefix_mirror_kernel(int P, int nseg,
+                                                                 double* __restrict__ out) {
+  __shared__ double Ts[32][33];
+  const int g = blockIdx.y;
+  int tile = blockIdx.x;
+  const int nt = (P + 31) / 32;
+  int I = 0;                                    // upper tiles enumerated row by row
+  while (tile >= nt - I) { tile -= nt - I; ++I; }
+  const int J = I + tile;
+  const int64_t PP = (int64_t)P * P;
+  double* og = out + (int64_t)g * nseg * PP;
+  const int t = threadIdx.x, c = t & 31, r0 = t >> 5;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int s = 0; s < nseg; ++s) {
+    double* o = og + (int64_t)s * PP;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
+      const bool valid = i < P && j < P && (I != J || c >= r);
+      if (valid) acc[q] += o[(int64_t)i * P + j];
+      Ts[r][c] = acc[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = r0 + 8 * q;
+      const int i = I * 32 + r, j = J * 32 + c;
+      if (i < P && j < P) o[(int64_t)i * P + j] = (I != J || c >= r) ? Ts[r][c] : Ts[c][r];
+      const int i2 = J * 32 + r, j2 = I * 32 + c;     // transposed tile
+      if (I != J && i2 < P && j2 < P) o[(int64_t)i2 * P + j2] = Ts[c][r];
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+extern "C" hipError_t pfml_window_prefix_sym(const double* X, int P, int T, int G,
+                                             const int* seg_start, const int* seg_stop, int nseg,
+                                             double* out, hipStream_t st) {
+  if (nseg <= 0 || P <= 0 || G <= 0) return hipSuccess;
+  hipLaunchKernelGGL(wsum_upper_kernel, dim3(P, nseg, G), dim3(256), 0, st, X, P, T, seg_start,
+                     seg_stop, nseg, out);
+  const int nt = (P + 31) / 32;
+  hipLaunchKernelGGL(wsum_prefix_mirror_kernel, dim3(nt * (nt + 1) / 2, G), dim3(256), 0, st, P,
+                     nseg, out);
+  return hipGetLastError();
+}

@@ -28,7 +28,7 @@ import pandas as pd
 import torch
 
 from ..config import Config
-from ..ops.ridge import _HostClock, ridge_utilities, segment_sums
+from ..ops.ridge import _HostClock, ridge_utilities, segment_sums, window_prefix_sym
 from ..parallel import collectives as coll
 from ..parallel.dist import env as dist_env
 from ..utils.dates import mi_from_ym, month_end
@@ -119,9 +119,9 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
     starts = np.concatenate([np.asarray(st, np.int64) + g * T for g in range(G)]).astype(np.int32)
     stops = np.concatenate([np.asarray(sp, np.int64) + g * T for g in range(G)]).astype(np.int32)
     if nseg:
-        SD = segment_sums(reals.denom.reshape(G * T, P, P), starts, stops).view(G, nseg, P, P)
+        # running sums at every block end in one pass over the symmetric upper triangles
+        SD = window_prefix_sym(reals.denom, st, sp)
         Sr = segment_sums(reals.r_tilde.reshape(G * T, P), starts, stops).view(G, nseg, P)
-        SD = torch.cumsum(SD, dim=1)
         Sr = torch.cumsum(Sr, dim=1)
         totD, totr = SD[:, -1], Sr[:, -1]
     else:

@@ -6,6 +6,8 @@ PFML_Search_Coef.py:131-133; r'b - 1/2 b'Db per month, PFML_hp_reals.py:94).
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 import torch
 
@@ -36,6 +38,36 @@ def segment_sums(X: torch.Tensor, starts, stops) -> torch.Tensor:
     else:
         for s in range(S):
             out[s] = X[starts[s]:stops[s]].sum(0)
+    return out
+
+
+nat.register_hip("pfml_window_prefix_sym", [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                            C.c_void_p, C.c_int, C.c_void_p, C.c_void_p])
+
+
+def window_prefix_sym(X: torch.Tensor, starts, stops) -> torch.Tensor:
+    """out[g, s] = sum of X[g, t] over the months of segments 0..s (X: [G, T, P, P], every
+    X[g, t] symmetric).  Device: one pass over the upper triangles (csrc/segsum.hip)."""
+    G, T, P, _ = X.shape
+    starts = np.asarray(starts, dtype=np.int32)
+    stops = np.asarray(stops, dtype=np.int32)
+    S = len(starts)
+    out = torch.empty((G, S, P, P), dtype=X.dtype, device=X.device)
+    if S == 0:
+        return out
+    if nat.is_device(X):
+        if X.dtype != torch.float64 or not X.is_contiguous():
+            raise ValueError("window_prefix_sym: contiguous fp64 required")
+        st, sp = upload([starts, stops], X.device)
+        nat.check(nat.hip_lib().pfml_window_prefix_sym(X.data_ptr(), P, T, G, st.data_ptr(),
+                                                       sp.data_ptr(), S, out.data_ptr(),
+                                                       nat.stream_of(X)),
+                  "pfml_window_prefix_sym")
+        return out
+    acc = torch.zeros((G, P, P), dtype=X.dtype)
+    for s in range(S):
+        acc = acc + X[:, starts[s]:stops[s]].sum(1)
+        out[:, s] = acc
     return out
 
 

@@ -203,3 +203,19 @@ def test_gemm_lowp(gpu, fmt, ta, tb):
     bb = B.transpose(1, 2) if tb else B
     exact = 0.5 * a @ bb + 0.25 * C0
     assert (out - exact).abs().max().item() / scale < (1e-2 if fmt == "bf16" else 1e-1)
+
+
+def test_window_prefix_sym(gpu):
+    """Fused expanding-window sums over the upper triangles of symmetric month matrices."""
+    from pfml.ops.ridge import window_prefix_sym
+    X = _rand(2, 40, 37, 37, seed=81)
+    X = X + X.transpose(-1, -2)
+    st, sp = [0, 7, 9, 20], [7, 9, 20, 40]
+    ref = window_prefix_sym(X, st, sp)
+    out = window_prefix_sym(X.to(gpu), st, sp).cpu()
+    assert torch.allclose(out, ref, rtol=1e-13, atol=1e-12)
+    assert torch.equal(out, out.transpose(-1, -2))
+    gap_st, gap_sp = [0, 10], [5, 40]          # months 5..9 belong to no segment
+    ref2 = window_prefix_sym(X, gap_st, gap_sp)
+    assert torch.allclose(window_prefix_sym(X.to(gpu), gap_st, gap_sp).cpu(), ref2,
+                          rtol=1e-13, atol=1e-12)
