@@ -17,9 +17,11 @@
 namespace {
 
 constexpr int BM = 64, BK = 16, NCOL = 112, NTILE = NCOL / 16;
-// LDS row strides: k-rows 1 apart must land 32 banks apart (a 32-lane ds_read_b64 group reads
-// rows k and k+1), i.e. a stride = 16 (mod 32) doubles: 64 + 16 for D, 112 + 0 for beta.
-constexpr int PAD = 16, PADB = 0;
+// Both operands are staged k-contiguous, as they sit in HBM ([row][k] for D, [lambda][k] for
+// beta), with a row stride of BK + 2 = 18 doubles: the coalesced global rows are stored
+// without bank conflicts, and a fragment read (16 rows x 2 k per 32-lane group) hits 32
+// distinct bank pairs.  (A [k][row] image made every staging store a 16-way conflict.)
+constexpr int KS = BK + 2;
 
 struct JobDesc {
   int64_t d_off;     // offset of D_t (P x P, ld ldD)
@@ -33,8 +35,8 @@ __global__ __launch_bounds__(256) void quadform_kernel(
     const double* __restrict__ D, int64_t ldD, const double* __restrict__ R,
     const double* __restrict__ Bt, int64_t ldB, const JobDesc* __restrict__ jobs,
     const int* __restrict__ tile_job, int L, double* __restrict__ partial) {
-  __shared__ double As[2][BK][BM + PAD];
-  __shared__ double Bs[2][BK][NCOL + PADB];
+  __shared__ double As[2][BM][KS];
+  __shared__ double Bs[2][NCOL][KS];
   __shared__ double red[4][NCOL];
 
   const int tile = blockIdx.x;
@@ -79,21 +81,21 @@ __global__ __launch_bounds__(256) void quadform_kernel(
 #pragma unroll
     for (int q = 0; q < AQ; ++q) {
       const int e = t + q * 256, i = e / BK, k = e % BK;
-      As[buf][k][i] = ra[q];
+      As[buf][i][k] = ra[q];
     }
 #pragma unroll
     for (int q = 0; q < BQ; ++q) {
       const int e = t + q * 256, l = e / BK, k = e % BK;
-      if (e < NCOL * BK) Bs[buf][k][l] = rb[q];
+      if (e < NCOL * BK) Bs[buf][l][k] = rb[q];
     }
   };
   auto compute = [&](int buf) {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
-      const double a = As[buf][kk + (lane >> 4)][w * 16 + (lane & 15)];
+      const double a = As[buf][w * 16 + (lane & 15)][kk + (lane >> 4)];
 #pragma unroll
       for (int q = 0; q < NTILE; ++q)
-        acc[q] = mfma_f64_16x16x4(a, Bs[buf][kk + (lane >> 4)][q * 16 + (lane & 15)], acc[q]);
+        acc[q] = mfma_f64_16x16x4(a, Bs[buf][q * 16 + (lane & 15)][kk + (lane >> 4)], acc[q]);
     }
   };
   gload(i0, ra0, rb0);

@@ -122,7 +122,7 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
         # running sums at every block end in one pass over the symmetric upper triangles
         SD = window_prefix_sym(reals.denom, st, sp)
         Sr = segment_sums(reals.r_tilde.reshape(G * T, P), starts, stops).view(G, nseg, P)
-        Sr = torch.cumsum(Sr, dim=1)
+        Sr = _cumsum0(Sr.transpose(0, 1)).transpose(0, 1)
         totD, totr = SD[:, -1], Sr[:, -1]
     else:
         SD = torch.zeros((G, 0, P, P), dtype=torch.float64, device=dev)
@@ -190,6 +190,14 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
 # ---------------------------------------------------------------------------------------
 # Scores (K17): expanding mean by (p, l) over eom_ret, dense rank per eom_ret.
 # ---------------------------------------------------------------------------------------
+def _cumsum0(x: torch.Tensor) -> torch.Tensor:
+    """cumsum along dim 0 as an innermost-dim scan (the outer-dim scan kernel of torch-ROCm
+    takes ~0.2-0.4 ms on these [months, cells] shapes; the innermost one ~30 us)."""
+    n = x.shape[0]
+    y = x.reshape(n, -1).t().contiguous().cumsum(dim=1)
+    return y.t().reshape(x.shape)
+
+
 def validation_scores(obj: torch.Tensor, frame_g: int, compat: bool):
     """cum_obj and dense rank for the validation frame of ``frame_g``.
 
@@ -202,7 +210,7 @@ def validation_scores(obj: torch.Tensor, frame_g: int, compat: bool):
     nV, k, nP, L = seq.shape
     flat = seq.reshape(nV * k, nP, L)
     cnt = torch.arange(1, nV * k + 1, dtype=flat.dtype, device=flat.device).view(-1, 1, 1)
-    cum = (torch.cumsum(flat, dim=0) / cnt).view(nV, k, nP, L)
+    cum = (_cumsum0(flat) / cnt).view(nV, k, nP, L)
     # dense rank (descending) within each month over k * nP * L rows
     vals = cum.reshape(nV, -1)
     sv, idx = torch.sort(vals, dim=1, descending=True, stable=True)
