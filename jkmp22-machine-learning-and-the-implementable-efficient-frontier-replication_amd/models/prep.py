@@ -74,10 +74,17 @@ def wealth_func(wealth_end: float, end: pd.Timestamp, market: pd.DataFrame,
 
 
 def lead_returns(monthly: pd.DataFrame, h: int) -> pd.DataFrame:
-    """ret_ld1 of long_horizon_ret (General_functions.py:222-288), zero-imputed.
+    """ret_ld1 of long_horizon_ret (General_functions.py:222-288), zero-imputed."""
+    return long_horizon_ret(monthly, h, "zero")[["id", "eom", "ret_ld1"]]
+
+
+def long_horizon_ret(monthly: pd.DataFrame, h: int, impute: str = "zero") -> pd.DataFrame:
+    """long_horizon_ret (General_functions.py:222-288): columns id, eom, ret_ld1..ret_ld{h}.
 
     Builds the dense (id, date) grid between each id's first and last valid return over the
-    set of dates present in the data, forms leads 1..h, drops rows with all h leads missing.
+    set of dates present in the data, forms leads 1..h, drops rows with all h leads missing,
+    then fills the remaining gaps with zero or the per-eom mean / median of that lead (any
+    other ``impute`` leaves them NaN, as the reference does).
     """
     m = monthly.dropna(subset=["ret_exc"])
     mi = month_index(m["eom"])
@@ -111,9 +118,14 @@ def lead_returns(monthly: pd.DataFrame, h: int) -> pd.DataFrame:
     all_missing = np.isnan(leads).all(axis=1)
     log.info(f"All missing excludes {all_missing.mean() * 100:.2f}% of the observations")
     keep = ~all_missing
-    r1 = np.nan_to_num(leads[keep, 0], nan=0.0)
     from ..utils.dates import month_end
-    return pd.DataFrame({"id": gid[keep], "eom": month_end(gdate[keep]), "ret_ld1": r1})
+    out = pd.DataFrame({"id": gid[keep], "eom": month_end(gdate[keep])})
+    lead = pd.DataFrame(leads[keep], columns=[f"ret_ld{l}" for l in range(1, h + 1)])
+    if impute == "zero":
+        lead = lead.fillna(0.0)
+    elif impute in ("mean", "median"):
+        lead = lead.fillna(lead.groupby(out["eom"].to_numpy()).transform(impute))
+    return pd.concat([out, lead], axis=1)
 
 
 def size_screen(chars: pd.DataFrame, type_: str) -> None:
