@@ -14,13 +14,13 @@
 // resident in LDS: 16x fewer passes over the trailing matrix than one pass per reflector.
 // Then every lambda is an independent banded Cholesky solve (B + l I) y = Q^T rbar (one wave
 // per lambda, register window with DPP broadcasts, O(n BB^2)), and beta = Q y is a blocked-WY back-transform
-// (MFMA, Y chunk of 16 lambdas resident in LDS).
+// (MFMA, Y chunk of 16 lambdas resident in registers).
 //
 //   kernel 1  band_mk_{panel,x,trail}_kernel three launches per panel, many workgroups per
 //                                            cell (ridge_band_reduce_kernel: one 512-thread
 //                                            workgroup per cell, PFML_BAND_MODE=single)
 //   kernel 2  ridge_band_solve_kernel        4 lambdas per wave (16-lane DPP rows)
-//   kernel 3  ridge_band_backtransform_kernel one 256-thread workgroup per (cell, 16 lambdas)
+//   kernel 3  ridge_band_backtransform_kernel one 512-thread workgroup per (cell, 16 lambdas)
 //
 // A non-positive Cholesky pivot (Dbar + l I not numerically SPD, e.g. l = 0 on a singular
 // Dbar) marks that lambda's beta NaN; ops/ridge.py recomputes exactly those systems with a
@@ -97,6 +97,16 @@ __device__ __forceinline__ double dpp_mov(double v) {
   const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
   return __hiloint2double(hi, lo);
+}
+
+// 1/sqrt(x) to full fp64 accuracy: v_rsq_f64 refined by Newton steps, a short dependent
+// chain in place of the IEEE sqrt and divide sequences on the banded Cholesky's pivot path.
+__device__ __forceinline__ double rsqrt_f64(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+#pragma unroll
+  for (int it = 0; it < 3; ++it) y = y * fma(-h * y, y, 1.5);
+  return y;
 }
 
 __device__ __forceinline__ double row16_sum(double v) {
@@ -375,7 +385,11 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) red[wid][(g4 + 4 * r) * BB + c16] = Pp[r];
       double s = 0.0;
-      for (int i = rg; i < m; i += 32) s += Vs[i][cq] * bw.z[r0 + i];
+#pragma unroll
+      for (int q = 0; q < BMP / 32; ++q) {    // all loads in flight (V rows >= m are zero)
+        const int i = rg + 32 * q;
+        s += Vs[i][cq] * bw.z[r0 + min(i, m - 1)];
+      }
       s += __shfl_xor(s, 16, 64);
       s += __shfl_xor(s, 32, 64);
       if (lane < 16) red2[wid][lane] = s;
@@ -435,39 +449,50 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
     BAND_TMARK(5)
     // ---- P6: A22 -= V W^T + W V^T on the LOWER block triangle (K = 32 MFMA per 16x16 tile,
     //      TBR tiles per pass); each off-diagonal tile is also stored transposed, so A stays
-    //      bitwise symmetric at half the MFMA work.
+    //      bitwise symmetric at half the MFMA work.  The A tiles of a wave's NEXT pass are
+    //      loaded before this pass's MFMAs, so a wave exposes one memory latency instead of
+    //      one per pass (passes touch disjoint lower tiles; mirrored stores land in the upper
+    //      triangle, which no pass reads).
     {
       const int ntt = nI * (nI + 1) / 2;
-      for (int tb = wid * TBR; tb < ntt; tb += NWR * TBR) {
-        double4_t acc[TBR];
-        int offn[TBR][4], offt[TBR][4], ia[TBR], jb[TBR];
+      double4_t nxt[TBR];
+      int ni0[TBR], nj0[TBR];
+      auto fetch = [&](int tb) {
 #pragma unroll
         for (int u = 0; u < TBR; ++u) {
           const int tile = min(tb + u, ntt - 1);
-          const bool tv = tb + u < ntt;
           int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
           if (I * (I + 1) / 2 > tile) --I;
           if ((I + 1) * (I + 2) / 2 <= tile) ++I;
-          const int Jt = tile - I * (I + 1) / 2;
-          const int i0 = I * 16, j0 = Jt * 16;
-          ia[u] = i0 + c16;
-          jb[u] = j0 + c16;
+          ni0[u] = (tb + u < ntt) ? I * 16 : BMP;      // BMP: beyond every row, a no-op tile
+          nj0[u] = (tile - I * (I + 1) / 2) * 16;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int i = i0 + g4 + 4 * r, jj = j0 + c16;
-            const bool ok = tv && i < m && jj < m;
-            offn[u][r] = ok ? (r0 + i) * n + r0 + jj : -1;
-            offt[u][r] = (ok && I != Jt) ? (r0 + jj) * n + r0 + i : -1;
-            acc[u][r] = ok ? A[offn[u][r]] : 0.0;
+            const int i = ni0[u] + g4 + 4 * r, jj = nj0[u] + c16;
+            nxt[u][r] = (i < m && jj < m) ? A[(int64_t)(r0 + i) * n + r0 + jj] : 0.0;
           }
         }
+      };
+      int tb = wid * TBR;
+      if (tb < ntt) fetch(tb);
+      for (; tb < ntt; tb += NWR * TBR) {
+        double4_t acc[TBR];
+        int ci0[TBR], cj0[TBR];
 #pragma unroll
         for (int u = 0; u < TBR; ++u) {
+          acc[u] = nxt[u];
+          ci0[u] = ni0[u];
+          cj0[u] = nj0[u];
+        }
+        if (tb + NWR * TBR < ntt) fetch(tb + NWR * TBR);
+#pragma unroll
+        for (int u = 0; u < TBR; ++u) {
+          const int ia = min(ci0[u], BMP - 16) + c16, jb = cj0[u] + c16;
 #pragma unroll
           for (int s = 0; s < 8; ++s) {
             const int kk = 4 * (s & 3) + g4;
-            const double av = (s < 4) ? Vs[ia[u]][kk] : Ws[ia[u]][kk];
-            const double bv = (s < 4) ? Ws[jb[u]][kk] : Vs[jb[u]][kk];
+            const double av = (s < 4) ? Vs[ia][kk] : Ws[ia][kk];
+            const double bv = (s < 4) ? Ws[jb][kk] : Vs[jb][kk];
             acc[u] = mfma_f64_16x16x4(-av, bv, acc[u]);
           }
         }
@@ -475,8 +500,11 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
         for (int u = 0; u < TBR; ++u)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            if (offn[u][r] >= 0) A[offn[u][r]] = acc[u][r];
-            if (offt[u][r] >= 0) A[offt[u][r]] = acc[u][r];
+            const int i = ci0[u] + g4 + 4 * r, jj = cj0[u] + c16;
+            if (i < m && jj < m) {
+              A[(int64_t)(r0 + i) * n + r0 + jj] = acc[u][r];
+              if (ci0[u] != cj0[u]) A[(int64_t)(r0 + jj) * n + r0 + i] = acc[u][r];
+            }
           }
       }
     }
@@ -827,7 +855,7 @@ __global__ __launch_bounds__(NTS) void ridge_band_solve_kernel(
       const bool pl = (p == u);                  // pivot lane: holds row j, takes row j+16
       const double piv = row_bcast<u>(w[u]);
       ok = ok && (piv > 0.0);
-      const double inv = 1.0 / sqrt(piv);
+      const double inv = rsqrt_f64(piv);
       const double yj = row_bcast<u>(zr) * inv;
       if (pl) {                                  // exec-masked 64-bit moves, no selects
 #pragma unroll
@@ -895,81 +923,132 @@ __global__ __launch_bounds__(NTS) void ridge_band_solve_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// kernel 3: beta = Q y, blocked WY, one workgroup per (cell, chunk of 16 lambdas).
+// kernel 3: beta = Q y, blocked WY, one workgroup per (cell, chunk of LC = 16 lambdas).
+//
+// The chunk's Y (n x 16) lives in REGISTERS: wave w owns the 16-row blocks b = w + 8 q, one
+// double4 per block in the MFMA C layout (row 16 b + g4 + 4 r, lambda c16) - which is also
+// the B-operand layout of P = V^T Y, so Y never round-trips through LDS.  Per panel
+// (backwards) each wave holds V_p of its live blocks (b > p) in A-operand order, loaded one
+// panel AHEAD (the loads of panel p-1 are in flight while panel p computes); the 8 partial P
+// meet in LDS (ping-pong buffers: one barrier per panel), every wave forms M = T P itself,
+// re-reads its V blocks transposed through a wave-private LDS image (no barrier) and updates
+// Y_b -= V_b M.
 // ---------------------------------------------------------------------------------------
+constexpr int NBW = (BNMAX / 16 + NWB - 1) / NWB;   // row blocks per wave
+
 __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
-    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work,
+    const RidgeCellDesc* __restrict__ cells, int ncells, int L, double* __restrict__ work,
     double* __restrict__ beta_out, int64_t ldo) {
-  __shared__ double Ys[BNMAX][LS];
-  __shared__ double Vb[BMP][LS];       // V_p (unit lower trapezoid), staged once per panel
-  __shared__ double red[NWB][BB * BB];
+  __shared__ double red[2][NWB][BB * BB];
+  __shared__ double Vw[NWB][NBW][BB][LS];         // wave-private V_b images (transpose)
+  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so logical id
+  // xcd * (grid / 8) + slot puts the chunks of one cell on ONE XCD, where they share the
+  // cell's V panels in that XCD's L2 (grid padded to a multiple of 8 by the launcher)
   const int nch = (L + LC - 1) / LC;
-  const int cell = blockIdx.x / nch, ch = blockIdx.x % nch;
+  const int logical = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if (logical >= ncells * nch) return;
+  const int cell = logical / nch, ch = logical % nch;
   const RidgeCellDesc cd = cells[cell];
   const int n = cd.n;
-  const int t = threadIdx.x, lane = t & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c16 = lane & 15, g4 = lane >> 4;
   BandWork bw(work + cd.work, n, L);
-  const double* A = bw.A;
+  const double* __restrict__ A = bw.A;
   const int l0 = ch * LC;
-  const int lw = min(LC, L - l0);
-  for (int e = t; e < BNMAX * LC; e += NTB) {
-    const int c = e / BNMAX, i = e % BNMAX;
-    Ys[i][c] = (c < lw && i < n) ? bw.Yt[(int64_t)(l0 + c) * n + i] : 0.0;
-  }
-  const int np = (n - 1) / BB;    // panels: k0 = 16 p with k0 + 16 < n
-  for (int p = np - 1; p >= 0; --p) {
-    const int k0 = p * BB, r0 = k0 + BB, m = n - r0;
-    // V_p -> Vb: the strictly-lower part lives in A's panel columns (16 contiguous doubles per
-    // row); every load of the panel is in flight at once (one memory latency per panel)
-    for (int e = t; e < m * BB; e += NTB) {
-      const int i = e / BB, c = e % BB;
-      Vb[i][c] = (i > c) ? A[(int64_t)(r0 + i) * n + k0 + c] : (i == c ? 1.0 : 0.0);
+  const bool lok = c16 < min(LC, L - l0);
+  const int nb = (n + 15) >> 4;
+  const double* __restrict__ yc = bw.Yt + (int64_t)(l0 + (lok ? c16 : 0)) * n;
+  double4_t Y[NBW];
+#pragma unroll
+  for (int q = 0; q < NBW; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 16 * (wid + NWB * q) + g4 + 4 * r;
+      Y[q][r] = (lok && i < n) ? yc[i] : 0.0;
     }
-    __syncthreads();
-    // P = V^T Y[r0:]  (K over rows, 4-row MFMA steps split across the waves)
-    double4_t Pp = {0.0, 0.0, 0.0, 0.0};
-    for (int k = 4 * wid; k < m; k += 4 * NWB) {
-      const int i = k + g4;
-      const bool in = i < m;
-      Pp = mfma_f64_16x16x4(in ? Vb[i][c16] : 0.0, in ? Ys[r0 + i][c16] : 0.0, Pp);
+  // va[q][r] = V_p[16 b - r0 + 4 r + g4][c16] for the live blocks b = wid + 8 q of panel p
+  const int lo_a = g4 * n + c16;
+  double vn[NBW][4], tn[4];
+  auto fetch = [&](int p) {
+    const int k0 = p * BB, r0 = k0 + BB, m = n - r0;
+    const double* Ap = A + (int64_t)r0 * n + k0;   // &V_p[0][0] (wave-uniform)
+#pragma unroll
+    for (int q = 0; q < NBW; ++q) {
+      const int b = wid + NWB * q;
+      const bool live = b > p && b < nb;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ib = 16 * b - r0 + 4 * r, i = ib + g4;
+        double v = 0.0;
+        if (live && i < m && i > c16)
+          v = *reinterpret_cast<const double*>(
+              reinterpret_cast<const char*>(Ap + (int64_t)ib * n) + (unsigned)lo_a * 8u);
+        vn[q][r] = (live && i == c16 && i < m) ? 1.0 : v;
+      }
+    }
+    const double* Tp = bw.T + (int64_t)p * BB * BB;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tn[r] = Tp[c16 * BB + 4 * r + g4];
+  };
+  const int np = (n - 1) / BB;    // panels: k0 = 16 p with k0 + 16 < n
+  if (np > 0) fetch(np - 1);
+  for (int p = np - 1; p >= 0; --p) {
+    double (*rp)[BB * BB] = red[p & 1];
+    double va[NBW][4], tv[4];
+#pragma unroll
+    for (int q = 0; q < NBW; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) va[q][r] = vn[q][r];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tv[r] = tn[r];
+    if (p > 0) fetch(p - 1);                        // next panel's V in flight from here on
+    // P_w = sum over live blocks of V_b^T Y_b; V_b also to the wave's LDS image
+    double4_t Pp[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};   // two MFMA chains
+#pragma unroll
+    for (int q = 0; q < NBW; ++q) {
+      const int b = wid + NWB * q;
+      if (b > p && b < nb) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          Vw[wid][q][4 * r + g4][c16] = va[q][r];
+          Pp[r & 1] = mfma_f64_16x16x4(va[q][r], Y[q][r], Pp[r & 1]);
+        }
+      }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[wid][(g4 + 4 * r) * BB + c16] = Pp[r];
+    for (int r = 0; r < 4; ++r) rp[wid][(g4 + 4 * r) * BB + c16] = Pp[0][r] + Pp[1][r];
     __syncthreads();
-    // M = T P
-    const double* Tp = bw.T + (int64_t)p * BB * BB;
+    // M = T P (every wave)
     double4_t Mm = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       double pv = 0.0;
 #pragma unroll
-      for (int w = 0; w < NWB; ++w) pv += red[w][(4 * r + g4) * BB + c16];
-      Mm = mfma_f64_16x16x4(Tp[c16 * BB + 4 * r + g4], pv, Mm);
+      for (int w = 0; w < NWB; ++w) pv += rp[w][(4 * r + g4) * BB + c16];
+      Mm = mfma_f64_16x16x4(tv[r], pv, Mm);
     }
-    // Y[r0:] -= V M   (row blocks I = wid + NWB q)
-    const int nI = (m + 15) >> 4;
-    for (int I = wid; I < nI; I += NWB) {
-      const int i0 = I * 16;
-      const int ia = min(i0 + c16, m - 1);
-      const double vs = (i0 + c16 < m) ? 1.0 : 0.0;
-      double4_t acc = {0.0, 0.0, 0.0, 0.0};
+    // Y_b -= V_b M   (A operand V_b[c16][4 r + g4] from the wave's own image)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(vs * Vb[ia][4 * r + g4], Mm[r], acc);
+    for (int q = 0; q < NBW; ++q) {
+      const int b = wid + NWB * q;
+      if (b > p && b < nb) {
+        double4_t acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = i0 + g4 + 4 * r;
-        if (i < m) Ys[r0 + i][c16] -= acc[r];
+        for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vw[wid][q][c16][4 * r + g4], Mm[r], acc);
+        Y[q] -= acc;
       }
     }
-    __syncthreads();
   }
-  __syncthreads();                     // (no panels: the Ys load still needs the barrier)
-  double* out = beta_out + cd.out;
-  for (int e = t; e < lw * n; e += NTB) {
-    const int c = e / n, i = e % n;
-    out[(int64_t)(l0 + c) * ldo + i] = Ys[i][c];
+  if (lok) {
+    double* __restrict__ out = beta_out + cd.out + (int64_t)(l0 + c16) * ldo;
+#pragma unroll
+    for (int q = 0; q < NBW; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * (wid + NWB * q) + g4 + 4 * r;
+        if (i < n) out[i] = Y[q][r];
+      }
   }
 }
 
@@ -1020,7 +1099,7 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   hipLaunchKernelGGL(ridge_band_solve_kernel, dim3(ncells * ((L + 15) / 16)), dim3(NTS), 0, st,
                      cd, lvec, L, work, tim, ncells);
   const int nch = (L + LC - 1) / LC;
-  hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3(ncells * nch), dim3(NTB), 0, st, cd,
-                     L, work, beta_out, ldo);
+  hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3((ncells * nch + 7) & ~7), dim3(NTB), 0,
+                     st, cd, ncells, L, work, beta_out, ldo);
   return hipGetLastError();
 }
