@@ -6,8 +6,8 @@ month) from Python, :62-130) with one batched device pipeline:
 
 1. window sums   - one segmented-sum pass over the resident [G, T, P, P] / [G, T, P] stacks
                    (burn-in block + one block per hp year), prefix over blocks (K14);
-2. ridge grid    - one Householder tridiagonalisation per (g, year, p) cell and a
-                   tridiagonal solve per lambda (K15, csrc/ridge.hip);
+2. ridge grid    - band reduction (bandwidth 16) per (g, year, p) cell, a banded Cholesky
+                   per lambda and a blocked-WY back-transform (K15, csrc/ridge_band.hip);
 3. utilities     - fused D_t B GEMM + dot epilogue per (cell, validation month) (K16);
 4. scores        - expanding mean by (p, l) and dense rank per month (K17), in torch.
 
@@ -16,8 +16,8 @@ Signals are kept in the interleaved order [constant, cos1, sin1, cos2, sin2, ...
 
 Distributed: hp years are split contiguously over ranks.  Each rank sums only its own
 window blocks; the cross-rank exclusive prefix of the block totals is ONE all-gather of a
-P x P matrix per g per rank and the per-month utilities are all-gathered at
-the end (a few MB).
+P x P matrix per g per rank and the per-month utilities are ONE all-gather at
+the end (a few MB; every rank's row count follows from the shared plan).
 """
 from __future__ import annotations
 
@@ -175,14 +175,20 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
     range_pop()
 
     th("grid_search.ridge_utilities")
-    vm = np.asarray(reals.months, dtype=np.int64)[v_m]
-    vy = np.asarray(years, dtype=np.int64)[yl[v_yi]] if nYl else np.zeros(0, np.int64)
+    v_y = yl[v_yi] if nYl else np.zeros(0, np.int64)
     if gather and env.is_dist:
+        # every rank's share of the validation rows follows from the global plan: ONE
+        # all-gather of the utilities; months and years are rebuilt locally
         range_push("search.gather")
-        obj = coll.all_gather_varlen(obj)
-        vm = coll.all_gather_varlen(torch.as_tensor(vm, device=dev)).cpu().numpy()
-        vy = coll.all_gather_varlen(torch.as_tensor(vy, device=dev)).cpu().numpy()
+        nv_all = np.asarray(plan.val_stop, np.int64) - np.asarray(plan.val_start, np.int64)
+        counts = [int(nv_all[list(coll.contiguous_split(len(years), env.world_size, r))].sum())
+                  for r in range(env.world_size)]
+        obj = coll.all_gather_known(obj, counts)
+        v_m = np.concatenate([np.arange(a, b) for a, b in zip(plan.val_start, plan.val_stop)])
+        v_y = np.repeat(np.arange(len(years)), nv_all)
         range_pop()
+    vm = np.asarray(reals.months, dtype=np.int64)[v_m]
+    vy = np.asarray(years, dtype=np.int64)[v_y]
     return GridResult(years=years, p_vec=p_vec, l_vec=cfg.l_vec, years_local=years[yl],
                       beta=beta, val_months=vm, val_year=vy, obj=obj)
 
@@ -253,8 +259,9 @@ def gather_beta(grid: GridResult) -> tuple[np.ndarray, torch.Tensor]:
     """All hp years' coefficients on every rank: (years, beta [G, nY, nP, L, P])."""
     env = dist_env()
     b = grid.beta.permute(1, 0, 2, 3, 4).contiguous()       # [nYl, G, nP, L, P]
-    yrs = torch.as_tensor(grid.years_local, device=b.device)
-    if env.is_dist:
-        b = coll.all_gather_varlen(b)
-        yrs = coll.all_gather_varlen(yrs)
-    return yrs.cpu().numpy(), b.permute(1, 0, 2, 3, 4).contiguous()
+    if not env.is_dist:
+        return np.asarray(grid.years_local), b.permute(1, 0, 2, 3, 4).contiguous()
+    nY = len(grid.years)
+    counts = [len(coll.contiguous_split(nY, env.world_size, r)) for r in range(env.world_size)]
+    b = coll.all_gather_known(b, counts)                    # years split contiguously
+    return np.asarray(grid.years), b.permute(1, 0, 2, 3, 4).contiguous()

@@ -41,6 +41,27 @@ def all_gather_varlen(x: torch.Tensor) -> torch.Tensor:
     return torch.cat(parts, 0)
 
 
+def all_gather_known(x: torch.Tensor, counts) -> torch.Tensor:
+    """all_gather_varlen when every rank's first-dim size is already known everywhere (e.g.
+    from a plan all ranks share): ONE collective, no size exchange and no host round trip."""
+    e = env()
+    if not e.is_dist:
+        return x
+    counts = [int(c) for c in counts]
+    if len(counts) != e.world_size or x.shape[0] != counts[e.rank]:
+        raise ValueError(f"all_gather_known: rank {e.rank} holds {x.shape[0]} rows, "
+                         f"counts {counts}")
+    m = max(counts)
+    if m == 0:
+        return x
+    pad = x.contiguous()
+    if x.shape[0] < m:
+        pad = torch.zeros((m, *x.shape[1:]), dtype=x.dtype, device=x.device)
+        pad[: x.shape[0]] = x
+    g = all_gather_cat(pad)
+    return torch.cat([g[r * m: r * m + counts[r]] for r in range(e.world_size)], 0)
+
+
 def exclusive_prefix_sum(total: torch.Tensor) -> torch.Tensor:
     """Sum of ``total`` over all lower ranks (zeros on rank 0): cross-GPU exclusive scan."""
     e = env()

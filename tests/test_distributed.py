@@ -49,6 +49,7 @@ def _worker(rank, world, port, out_dir, task):
             years, beta = gather_beta(res)
             if rank == 0:
                 torch.save({"obj": res.obj, "vm": torch.as_tensor(res.val_months),
+                            "vy": torch.as_tensor(res.val_year),
                             "beta": beta, "years": torch.as_tensor(years)},
                            os.path.join(out_dir, "grid.pt"))
         elif task == "coll":
@@ -56,7 +57,9 @@ def _worker(rank, world, port, out_dir, task):
             g = coll.all_gather_varlen(x)
             pre = coll.exclusive_prefix_sum(torch.tensor([float(rank + 1)]))
             mx = coll.all_reduce_max(float(rank))
-            torch.save({"g": g, "pre": pre, "mx": mx}, os.path.join(out_dir, f"coll{rank}.pt"))
+            k = coll.all_gather_known(torch.full((rank, 2), float(rank)), [0, 1, 2])
+            torch.save({"g": g, "pre": pre, "mx": mx, "k": k},
+                       os.path.join(out_dir, f"coll{rank}.pt"))
     finally:
         pdist.shutdown()
 
@@ -78,6 +81,8 @@ def test_grid_search_sharded_matches_single(world, tmp_path):
     _run(world, "grid", tmp_path)
     got = torch.load(os.path.join(tmp_path, "grid.pt"), weights_only=True)
     assert np.array_equal(got["vm"].numpy(), ref.val_months)
+    assert np.array_equal(got["vy"].numpy(), ref.val_year)
+    assert np.array_equal(got["years"].numpy(), np.asarray(cfg.hp_years))
     assert torch.allclose(got["obj"], ref.obj, rtol=1e-10, atol=1e-13)
     assert torch.allclose(got["beta"], ref_beta, rtol=1e-9, atol=1e-12)
 
@@ -90,6 +95,7 @@ def test_collectives_gloo(tmp_path):
         assert d["g"][:, 0].tolist() == [0.0, 1.0, 1.0, 2.0, 2.0, 2.0]
         assert d["pre"].item() == sum(range(1, r + 1))
         assert d["mx"] == 2.0
+        assert d["k"][:, 0].tolist() == [1.0, 2.0, 2.0]
 
 
 def test_bench_contract_two_ranks_gloo(tmp_path):
