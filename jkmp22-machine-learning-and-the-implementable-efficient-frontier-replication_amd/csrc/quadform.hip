@@ -63,30 +63,32 @@ __global__ __launch_bounds__(256) void quadform_kernel(
   // two register sets: the global loads of step k+2 are in flight while step k is computed
   // from LDS and step k+1 is written to the other LDS buffer (prefetch distance 2).
   double ra0[AQ], rb0[BQ], ra1[AQ], rb1[BQ];
+  // Loads are unconditional (indices clamped into the matrix) and the masking / diagonal
+  // weight is applied when the registers are written to LDS: a load under a branch with its
+  // use in the same block made the compiler wait for every D element right after issuing it.
   auto gload = [&](int k0, double (&ra)[AQ], double (&rb)[BQ]) {
+#pragma unroll
+    for (int q = 0; q < AQ; ++q) {
+      const int e = t + q * 256, i = e / BK, k = e % BK;
+      ra[q] = Dm[(int64_t)min(i0 + i, n - 1) * ldD + min(k0 + k, n - 1)];
+    }
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) {
+      const int e = min(t + q * 256, NCOL * BK - 1), l = e / BK, k = e % BK;
+      rb[q] = bt[(int64_t)min(l, L - 1) * ldB + min(k0 + k, n - 1)];
+    }
+  };
+  auto sstore = [&](int buf, int k0, const double (&ra)[AQ], const double (&rb)[BQ]) {
     const double wdiag = (k0 < i0 + BM) ? 0.5 : 1.0;
 #pragma unroll
     for (int q = 0; q < AQ; ++q) {
       const int e = t + q * 256, i = e / BK, k = e % BK;
-      const int gi = i0 + i, gk = k0 + k;
-      ra[q] = (gi < n && gk < n) ? wdiag * Dm[(int64_t)gi * ldD + gk] : 0.0;
-    }
-#pragma unroll
-    for (int q = 0; q < BQ; ++q) {
-      const int e = t + q * 256, l = e / BK, k = e % BK, gk = k0 + k;
-      rb[q] = (e < NCOL * BK && l < L && gk < n) ? bt[(int64_t)l * ldB + gk] : 0.0;
-    }
-  };
-  auto sstore = [&](int buf, const double (&ra)[AQ], const double (&rb)[BQ]) {
-#pragma unroll
-    for (int q = 0; q < AQ; ++q) {
-      const int e = t + q * 256, i = e / BK, k = e % BK;
-      As[buf][i][k] = ra[q];
+      As[buf][i][k] = (i0 + i < n && k0 + k < n) ? wdiag * ra[q] : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < BQ; ++q) {
       const int e = t + q * 256, l = e / BK, k = e % BK;
-      if (e < NCOL * BK) Bs[buf][l][k] = rb[q];
+      if (e < NCOL * BK) Bs[buf][l][k] = (l < L && k0 + k < n) ? rb[q] : 0.0;
     }
   };
   auto compute = [&](int buf) {
@@ -99,20 +101,20 @@ __global__ __launch_bounds__(256) void quadform_kernel(
     }
   };
   gload(i0, ra0, rb0);
-  sstore(0, ra0, rb0);
+  sstore(0, i0, ra0, rb0);
   if (i0 + BK < n) gload(i0 + BK, ra1, rb1);
   __syncthreads();
   for (int k0 = i0;;) {
     if (k0 + 2 * BK < n) gload(k0 + 2 * BK, ra0, rb0);
     compute(0);
     if (k0 + BK >= n) break;
-    sstore(1, ra1, rb1);
+    sstore(1, k0 + BK, ra1, rb1);
     __syncthreads();
     k0 += BK;
     if (k0 + 2 * BK < n) gload(k0 + 2 * BK, ra1, rb1);
     compute(1);
     if (k0 + BK >= n) break;
-    sstore(0, ra0, rb0);
+    sstore(0, k0 + BK, ra0, rb0);
     __syncthreads();
     k0 += BK;
   }

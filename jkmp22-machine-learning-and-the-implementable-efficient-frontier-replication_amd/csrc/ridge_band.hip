@@ -143,12 +143,13 @@ __device__ __forceinline__ void band_x_accum(const double* __restrict__ A, int n
   int col[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) col[q] = min((wid + NWR * q) * 16 + c16, m - 1);
-  int k = 0;
-  for (; k + 32 <= m; k += 32) {
+  // whole 32-row chunks: rows past m are clamped (valid memory) and meet U rows that are
+  // zero, so the ragged end costs no extra, serially exposed, load latencies
+  for (int k = 0; k < m; k += 32) {
     double a[8][NQ], b[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const double* arow = A + (int64_t)(r0 + k + 4 * u + g4) * n + r0;
+      const double* arow = A + (int64_t)(r0 + min(k + 4 * u + g4, m - 1)) * n + r0;
 #pragma unroll
       for (int q = 0; q < NQ; ++q) a[u][q] = arow[col[q]];
       b[u] = Ws[k + 4 * u + g4][c16];
@@ -157,13 +158,6 @@ __device__ __forceinline__ void band_x_accum(const double* __restrict__ A, int n
     for (int u = 0; u < 8; ++u)
 #pragma unroll
       for (int q = 0; q < NQ; ++q) X[q] = mfma_f64_16x16x4(a[u][q], b[u], X[q]);
-  }
-  for (; k < m; k += 4) {
-    const int kr = min(k + g4, m - 1);             // U rows >= m are zero
-    const double* arow = A + (int64_t)(r0 + kr) * n + r0;
-    const double b = Ws[k + g4][c16];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) X[q] = mfma_f64_16x16x4(arow[col[q]], b, X[q]);
   }
 }
 
@@ -320,6 +314,7 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
   __shared__ double red2[NWR][BB];
   __shared__ double Ts[BB][LS];
   __shared__ double taus[BB];
+  __shared__ double zs[BNMAX];         // z = Q^T rbar, LDS-resident during the reduction
 
   const RidgeCellDesc cd = cells[blockIdx.x];
   const int n = cd.n;
@@ -336,7 +331,7 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
     double* arow = A + (int64_t)i * n;
     for (int j = lane; j < n; j += 64) arow[j] = srow[j] * sc;
   }
-  for (int i = t; i < n; i += NTR) bw.z[i] = Sr[cd.rsrc + i] * sc;
+  for (int i = t; i < n; i += NTR) zs[i] = Sr[cd.rsrc + i] * sc;
   __syncthreads();
 
   if (tim != nullptr && threadIdx.x == 0) tlast = (long long)__builtin_amdgcn_s_memtime();
@@ -388,7 +383,7 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
 #pragma unroll
       for (int q = 0; q < BMP / 32; ++q) {    // all loads in flight (V rows >= m are zero)
         const int i = rg + 32 * q;
-        s += Vs[i][cq] * bw.z[r0 + min(i, m - 1)];
+        s += Vs[i][cq] * zs[r0 + min(i, m - 1)];
       }
       s += __shfl_xor(s, 16, 64);
       s += __shfl_xor(s, 32, 64);
@@ -417,7 +412,7 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
         double s = 0.0;
 #pragma unroll
         for (int c = 0; c < BB; ++c) s += Vs[i][c] * zt[c];
-        bw.z[r0 + i] -= s;
+        zs[r0 + i] -= s;
       }
     }
     // M = T^T (V^T X) ; W_I = X_I - 1/2 V_I M  -> Ws
@@ -515,6 +510,7 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
   if (tim != nullptr && threadIdx.x == 0)
     for (int q = 0; q < 8; ++q) tim[(int64_t)blockIdx.x * 8 + q] = tacc[q];
 #undef BAND_TMARK
+  for (int i = t; i < n; i += NTR) bw.z[i] = zs[i];
   // ---- row-major lower band: LB[r][s] = B[r][r-16+s]  (s = 16: diagonal)
   for (int e = t; e < n * LS; e += NTR) {
     const int r = e / LS, c = r - BB + e % LS;
@@ -638,20 +634,15 @@ __global__ __launch_bounds__(256) void band_mk_x_kernel(const RidgeCellDesc* __r
     // X[i][:] = sum_k A22[k][i] U[k][:]  (A symmetric: row k, 16 contiguous columns)
     const int col = r0 + min(i0 + c16, m - 1);
     const double* Ab = A + (int64_t)r0 * n + col;
-    int k = 0;
-    for (; k + 32 <= m; k += 32) {
+    for (int k = 0; k < m; k += 32) {            // rows past m: clamped, U rows zero
       double a[8], b[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        a[u] = Ab[(int64_t)(k + 4 * u + g4) * n];
+        a[u] = Ab[(int64_t)min(k + 4 * u + g4, m - 1) * n];
         b[u] = Ug[(k + 4 * u + g4) * BB + c16];
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) X = mfma_f64_16x16x4(a[u], b[u], X);
-    }
-    for (; k < m; k += 4) {
-      const int kr = min(k + g4, m - 1);          // U rows >= m are zero
-      X = mfma_f64_16x16x4(Ab[(int64_t)kr * n], Ug[(k + g4) * BB + c16], X);
     }
     // rows >= m of X are duplicates of row m-1: zero them; partial V_I^T X_I
 #pragma unroll
@@ -941,13 +932,11 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
     double* __restrict__ beta_out, int64_t ldo) {
   __shared__ double red[2][NWB][BB * BB];
   __shared__ double Vw[NWB][NBW][BB][LS];         // wave-private V_b images (transpose)
-  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so logical id
-  // xcd * (grid / 8) + slot puts the chunks of one cell on ONE XCD, where they share the
-  // cell's V panels in that XCD's L2 (grid padded to a multiple of 8 by the launcher)
+  // (the chunks of a cell are adjacent in dispatch order, so they run together and share
+  // the cell's V panels through the caches; an XCD-grouped order measured slower)
   const int nch = (L + LC - 1) / LC;
-  const int logical = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
-  if (logical >= ncells * nch) return;
-  const int cell = logical / nch, ch = logical % nch;
+  if ((int)blockIdx.x >= ncells * nch) return;
+  const int cell = blockIdx.x / nch, ch = blockIdx.x % nch;
   const RidgeCellDesc cd = cells[cell];
   const int n = cd.n;
   const int lane = threadIdx.x & 63;
@@ -1099,7 +1088,7 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   hipLaunchKernelGGL(ridge_band_solve_kernel, dim3(ncells * ((L + 15) / 16)), dim3(NTS), 0, st,
                      cd, lvec, L, work, tim, ncells);
   const int nch = (L + LC - 1) / LC;
-  hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3((ncells * nch + 7) & ~7), dim3(NTB), 0,
-                     st, cd, ncells, L, work, beta_out, ldo);
+  hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3(ncells * nch), dim3(NTB), 0, st, cd,
+                     ncells, L, work, beta_out, ldo);
   return hipGetLastError();
 }
