@@ -172,8 +172,11 @@ __global__ __launch_bounds__(256) void lu_snapshot_kernel(const double* __restri
   if (i >= n) return;
   const double* src = M + (int64_t)b * sM + (int64_t)i * ldm + a0 + k0;
   double* dst = Cbuf + ((int64_t)b * n + i) * NB;
+  double v[NB];
 #pragma unroll
-  for (int q = 0; q < NB; ++q) dst[q] = (q < nb) ? src[q] : 0.0;
+  for (int q = 0; q < NB; ++q) v[q] = src[min(q, nb - 1)];     // all loads in flight
+#pragma unroll
+  for (int q = 0; q < NB; ++q) dst[q] = (q < nb) ? v[q] : 0.0;
 }
 
 // rows outside block k: M_i -= C_i R ; block rows: M_k = R   (live columns only)
@@ -193,13 +196,22 @@ __global__ __launch_bounds__(256) void lu_update_kernel(double* __restrict__ M, 
   const int I0 = (blockIdx.x / tc) * BT, V0 = (blockIdx.x % tc) * BT;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = w >> 1, wn = w & 1;
-  for (int e = t; e < BT * NB; e += 256) {
-    const int i = e / NB, q = e % NB;
-    Cs[q][i] = (I0 + i < n) ? Cb[(int64_t)(I0 + i) * NB + q] : 0.0;
+  // staging: every load in flight at once (clamped, unconditional), masked at the LDS store
+  constexpr int QS = BT * NB / 256;
+  double cv[QS], rv[QS];
+#pragma unroll
+  for (int u = 0; u < QS; ++u) {
+    const int e = t + u * 256;
+    cv[u] = Cb[(int64_t)min(I0 + e / NB, n - 1) * NB + e % NB];
+    rv[u] = Rb[(int64_t)min(e / BT, nb - 1) * nlive + min(V0 + e % BT, nlive - 1)];
   }
-  for (int e = t; e < NB * BT; e += 256) {
-    const int q = e / BT, j = e % BT;
-    Rs[q][j] = (V0 + j < nlive && q < nb) ? Rb[(int64_t)q * nlive + V0 + j] : 0.0;
+#pragma unroll
+  for (int u = 0; u < QS; ++u) {
+    const int e = t + u * 256;
+    const int i = e / NB, q = e % NB;
+    Cs[q][i] = (I0 + i < n) ? cv[u] : 0.0;
+    const int q2 = e / BT, j = e % BT;
+    Rs[q2][j] = (V0 + j < nlive && q2 < nb) ? rv[u] : 0.0;
   }
   __syncthreads();
   double4_t acc[2][2];
@@ -219,6 +231,20 @@ __global__ __launch_bounds__(256) void lu_update_kernel(double* __restrict__ M, 
 #pragma unroll
       for (int y = 0; y < 2; ++y) acc[x][y] = mfma_f64_16x16x4(a[x], bb[y], acc[x][y]);
   }
+  // epilogue: gather the old values (and the new block rows) first, then write - one memory
+  // latency for the tile instead of one read-modify-write round trip per element
+  double old[2][2][4], nrow[2][2][4];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = min(I0 + wm * 32 + x * 16 + PFML_F64_CROW(lane, r), n - 1);
+        const int v = min(V0 + wn * 32 + y * 16 + (lane & 15), nlive - 1);
+        old[x][y][r] = Mb[(int64_t)i * ldm + live_col(v, nA, a_first, b0)];
+        nrow[x][y][r] = Rb[(int64_t)min(max(i - k0, 0), nb - 1) * nlive + v];
+      }
 #pragma unroll
   for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -228,9 +254,8 @@ __global__ __launch_bounds__(256) void lu_update_kernel(double* __restrict__ M, 
         const int i = I0 + wm * 32 + x * 16 + PFML_F64_CROW(lane, r);
         const int v = V0 + wn * 32 + y * 16 + (lane & 15);
         if (i >= n || v >= nlive) continue;
-        double* p = Mb + (int64_t)i * ldm + live_col(v, nA, a_first, b0);
-        if (i >= k0 && i < k0 + nb) *p = Rb[(int64_t)(i - k0) * nlive + v];
-        else *p -= acc[x][y][r];
+        Mb[(int64_t)i * ldm + live_col(v, nA, a_first, b0)] =
+            (i >= k0 && i < k0 + nb) ? nrow[x][y][r] : old[x][y][r] - acc[x][y][r];
       }
 }
 

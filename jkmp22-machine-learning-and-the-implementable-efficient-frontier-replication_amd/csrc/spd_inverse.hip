@@ -232,22 +232,39 @@ __global__ __launch_bounds__(256) void spd_blockinv_kernel(const double* __restr
                                                             int nb, double* __restrict__ Pout,
                                                             int* __restrict__ status) {
   __shared__ double P[NBL][NBL + 1];
+  constexpr int EPT = NBL * NBL / 256;            // elements per thread (fixed 64 x 64 frame)
   const int b = blockIdx.x;
   const double* Ab = A + (int64_t)b * sA + (int64_t)k0 * lda + k0;
   const int t = threadIdx.x;
-  for (int e = t; e < nb * nb; e += 256) P[e / nb][e % nb] = Ab[(int64_t)(e / nb) * lda + e % nb];
+  // element u of this thread: (i, j) = (e / NBL, e % NBL), e = t + 256 u; frame entries past
+  // nb hold the identity, so the elimination below needs no bounds tests
+  {
+    double v[EPT];
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {            // every load in flight at once
+      const int e = t + 256 * u, i = e / NBL, j = e % NBL;
+      v[u] = Ab[(int64_t)min(i, nb - 1) * lda + min(j, nb - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+      const int e = t + 256 * u, i = e / NBL, j = e % NBL;
+      P[i][j] = (i < nb && j < nb) ? v[u] : (i == j ? 1.0 : 0.0);
+    }
+  }
   __syncthreads();
   for (int p = 0; p < nb; ++p) {
+    // P[p][p], P[i][p], P[p][j] are only rewritten after the next barrier, so reading the
+    // pivot needs no barrier of its own
     const double piv = P[p][p];
     if (t == 0 && (!(piv > 0.0) || !isfinite(piv))) status[b] = 1;
     const double inv = 1.0 / piv;
-    __syncthreads();
-    for (int e = t; e < nb * nb; e += 256) {
-      const int i = e / nb, j = e % nb;
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+      const int e = t + 256 * u, i = e / NBL, j = e % NBL;
       if (i != p && j != p) P[i][j] -= P[i][p] * P[p][j] * inv;
     }
     __syncthreads();
-    if (t < nb && t != p) {
+    if (t < NBL && t != p) {
       P[p][t] *= inv;
       P[t][p] *= -inv;
     }
@@ -255,7 +272,11 @@ __global__ __launch_bounds__(256) void spd_blockinv_kernel(const double* __restr
     __syncthreads();
   }
   double* Pb = Pout + (int64_t)b * NBL * NBL;
-  for (int e = t; e < nb * nb; e += 256) Pb[(e / nb) * NBL + e % nb] = P[e / nb][e % nb];
+#pragma unroll
+  for (int u = 0; u < EPT; ++u) {
+    const int e = t + 256 * u, i = e / NBL, j = e % NBL;
+    if (i < nb && j < nb) Pb[i * NBL + j] = P[i][j];
+  }
 }
 }  // namespace
 
