@@ -27,6 +27,7 @@ struct JobDesc {
   int64_t d_off;     // offset of D_t (P x P, ld ldD)
   int64_t r_off;     // offset of r_t
   int64_t b_off;     // offset of beta block [L][ldB]
+  int64_t o_off;     // offset of this job's L utilities in obj
   int n;             // p + 1
   int ptile0;        // first partial slot of this job
 };
@@ -154,7 +155,7 @@ __global__ void quadform_reduce_kernel(const double* __restrict__ partial,
   const int nt = (jd.n + BM - 1) / BM;
   double s = 0.0;
   for (int q = 0; q < nt; ++q) s += partial[(int64_t)(jd.ptile0 + q) * L + l];
-  obj[(int64_t)j * L + l] = s;
+  obj[jd.o_off + l] = s;
 }
 
 }  // namespace

@@ -93,6 +93,65 @@ class GridResult:
     timings: dict = field(default_factory=dict)
 
 
+_SETUP: dict = {}
+
+
+def _search_setup(months: np.ndarray, years: np.ndarray, p_vec, G: int, T: int, world: int,
+                  rank: int, dev, l_vec: np.ndarray) -> dict:
+    """Everything of a grid search that depends only on its shape - the window plan, this
+    rank's segments, cells and validation jobs, and the device copies of the segment bounds -
+    built once per shape and reused by every later search (no host planning, no host->device
+    copies in the steady state)."""
+    key = (months.tobytes(), np.asarray(years).tobytes(), tuple(p_vec), G, T, world, rank,
+           str(dev), l_vec.tobytes())
+    hit = _SETUP.get(key)
+    if hit is not None:
+        return hit
+    plan = make_plan(months, years)
+    yl = np.asarray(list(coll.contiguous_split(len(years), world, rank)))
+    nYl = len(yl)
+    nP = len(p_vec)
+    st = [int(plan.seg_start[i]) for i in yl]
+    sp = [int(plan.seg_stop[i]) for i in yl]
+    if nYl and yl[0] == 0:
+        st = [0] + st
+        sp = [plan.burn_stop] + sp
+    nseg = len(st)
+    starts = np.concatenate([np.asarray(st, np.int64) + g * T for g in range(G)]).astype(np.int32)
+    stops = np.concatenate([np.asarray(sp, np.int64) + g * T for g in range(G)]).astype(np.int32)
+    pv = np.asarray(p_vec, dtype=np.int64)
+    gg, yy, pp = np.meshgrid(np.arange(G), np.arange(nYl), np.arange(nP), indexing="ij")
+    cell_src = (gg * nYl + yy).reshape(-1)                 # cell order [g][year][p]
+    cell_n = (pv[pp] + 1).reshape(-1)
+    cnt = np.maximum(np.asarray(plan.count, dtype=np.int64)[yl], 1) if nYl else np.zeros(0)
+    cell_scale = (1.0 / cnt[yy].astype(np.float64)).reshape(-1)
+    # job order: [val month][g][p]  -> obj reshapes to [nValLocal, G, nP, L]
+    vs = np.asarray(plan.val_start, dtype=np.int64)[yl] if nYl else np.zeros(0, np.int64)
+    ve = np.asarray(plan.val_stop, dtype=np.int64)[yl] if nYl else np.zeros(0, np.int64)
+    nv = ve - vs
+    v_yi = np.repeat(np.arange(nYl), nv)                   # local year index per val row
+    v_m = (np.concatenate([np.arange(a, b) for a, b in zip(vs, ve)])
+           if nYl else np.zeros(0, np.int64))
+    nVr = len(v_m)
+    vi, g2, p2 = np.meshgrid(np.arange(nVr), np.arange(G), np.arange(nP), indexing="ij")
+    jc = ((g2 * nYl + v_yi[vi]) * nP + p2).reshape(-1)
+    jm = (g2 * T + v_m[vi]).reshape(-1)
+    jn = (pv[p2] + 1).reshape(-1)
+    out = dict(plan=plan, yl=yl, nYl=nYl, st=st, sp=sp, nseg=nseg, starts=starts, stops=stops,
+               cell_src=np.asarray(cell_src), cell_n=np.asarray(cell_n),
+               cell_scale=np.asarray(cell_scale), v_yi=v_yi, v_m=v_m, nVr=nVr,
+               jc=np.asarray(jc), jm=np.asarray(jm), jn=np.asarray(jn), dev_bounds=None,
+               lvec=torch.as_tensor(l_vec, dtype=torch.float64, device=dev))
+    if nseg and dev is not None and dev.type == "cuda":
+        from ..ops.ridge import upload
+        out["dev_bounds"] = upload([np.asarray(st, np.int32), np.asarray(sp, np.int32),
+                                    starts, stops], dev)
+    if len(_SETUP) > 32:
+        _SETUP.clear()
+    _SETUP[key] = out
+    return out
+
+
 def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridResult:
     th = _HostClock()
     env = dist_env()
@@ -101,27 +160,21 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
     years = cfg.hp_years
     p_vec = cfg.p_vec
     nP = len(p_vec)
-    lvec = torch.as_tensor(cfg.l_vec, dtype=torch.float64, device=dev)
+    su = _search_setup(np.asarray(reals.months, dtype=np.int64), np.asarray(years), p_vec, G, T,
+                       env.world_size, env.rank, dev, np.asarray(cfg.l_vec, dtype=np.float64))
+    lvec = su["lvec"]
     L = lvec.numel()
-    plan = make_plan(reals.months, years)
-
-    yl = np.asarray(list(coll.contiguous_split(len(years), env.world_size, env.rank)))
-    nYl = len(yl)
+    plan, yl, nYl, nseg = su["plan"], su["yl"], su["nYl"], su["nseg"]
 
     # ---- 1. window sums over this rank's blocks ------------------------------------
     range_push("search.window_sums")
-    st = [plan.seg_start[i] for i in yl]
-    sp = [plan.seg_stop[i] for i in yl]
-    if nYl and yl[0] == 0:
-        st = [0] + st
-        sp = [plan.burn_stop] + sp
-    nseg = len(st)
-    starts = np.concatenate([np.asarray(st, np.int64) + g * T for g in range(G)]).astype(np.int32)
-    stops = np.concatenate([np.asarray(sp, np.int64) + g * T for g in range(G)]).astype(np.int32)
     if nseg:
         # running sums at every block end in one pass over the symmetric upper triangles
-        SD = window_prefix_sym(reals.denom, st, sp)
-        Sr = segment_sums(reals.r_tilde.reshape(G * T, P), starts, stops).view(G, nseg, P)
+        db = su["dev_bounds"]
+        SD = window_prefix_sym(reals.denom, su["st"], su["sp"],
+                               dev_bounds=None if db is None else db[:2])
+        Sr = segment_sums(reals.r_tilde.reshape(G * T, P), su["starts"], su["stops"],
+                          dev_bounds=None if db is None else db[2:]).view(G, nseg, P)
         Sr = _cumsum0(Sr.transpose(0, 1)).transpose(0, 1)
         totD, totr = SD[:, -1], Sr[:, -1]
     else:
@@ -138,40 +191,18 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
         SD, Sr = SD[:, 1:], Sr[:, 1:]
     range_pop()
 
-    # ---- 2. ridge grid ---------------------------------------------------------------
+    # ---- 2. ridge grid + 3. utilities for every (cell, validation month) -------------
     th("grid_search.window_sums")
     range_push("search.ridge_utilities")
-    pv = np.asarray(p_vec, dtype=np.int64)
-    gg, yy, pp = np.meshgrid(np.arange(G), np.arange(nYl), np.arange(nP), indexing="ij")
-    cell_src = (gg * nYl + yy).reshape(-1)                 # cell order [g][year][p]
-    cell_n = (pv[pp] + 1).reshape(-1)
-    cnt = np.maximum(np.asarray(plan.count, dtype=np.int64)[yl], 1) if nYl else np.zeros(0)
-    cell_scale = (1.0 / cnt[yy].astype(np.float64)).reshape(-1)
-
-    # ---- 3. utilities for every (cell, validation month) ------------------------------
-    # job order: [val month][g][p]  -> obj reshapes to [nValLocal, G, nP, L]
-    vs = np.asarray(plan.val_start, dtype=np.int64)[yl] if nYl else np.zeros(0, np.int64)
-    ve = np.asarray(plan.val_stop, dtype=np.int64)[yl] if nYl else np.zeros(0, np.int64)
-    nv = ve - vs
-    v_yi = np.repeat(np.arange(nYl), nv)                   # local year index per val row
-    v_m = (np.concatenate([np.arange(a, b) for a, b in zip(vs, ve)])
-           if nYl else np.zeros(0, np.int64))
-    val_rows = list(zip(v_m.tolist(), yl[v_yi].tolist()))
-    nVr = len(v_m)
-    vi, g2, p2 = np.meshgrid(np.arange(nVr), np.arange(G), np.arange(nP), indexing="ij")
-    jc = ((g2 * nYl + v_yi[vi]) * nP + p2).reshape(-1)
-    jm = (g2 * T + v_m[vi]).reshape(-1)
-    jn = (pv[p2] + 1).reshape(-1)
+    v_yi, v_m = su["v_yi"], su["v_m"]
     th("grid_search.plan")
     # ridge grid + utilities, big-n cells overlapped with the rest on a second stream
     beta, obj = ridge_utilities(SD.reshape(G * nYl, P, P), Sr.reshape(G * nYl, P),
-                                np.asarray(cell_src), np.asarray(cell_n),
-                                np.asarray(cell_scale), lvec,
+                                su["cell_src"], su["cell_n"], su["cell_scale"], lvec,
                                 reals.denom.reshape(G * T, P, P),
-                                reals.r_tilde.reshape(G * T, P), np.asarray(jc),
-                                np.asarray(jm), np.asarray(jn))
+                                reals.r_tilde.reshape(G * T, P), su["jc"], su["jm"], su["jn"])
     beta = beta.view(G, nYl, nP, L, P)
-    obj = obj.view(len(val_rows), G, nP, L)
+    obj = obj.view(su["nVr"], G, nP, L)
     range_pop()
 
     th("grid_search.ridge_utilities")

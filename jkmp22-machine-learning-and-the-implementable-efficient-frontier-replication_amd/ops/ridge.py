@@ -15,12 +15,13 @@ from . import _native as nat
 
 CELL_DTYPE = np.dtype([("src", "<i8"), ("rsrc", "<i8"), ("work", "<i8"), ("out", "<i8"),
                        ("n", "<i4"), ("_pad", "<i4"), ("scale", "<f8")])
-JOB_DTYPE = np.dtype([("d_off", "<i8"), ("r_off", "<i8"), ("b_off", "<i8"), ("n", "<i4"),
-                      ("ptile0", "<i4")])
+JOB_DTYPE = np.dtype([("d_off", "<i8"), ("r_off", "<i8"), ("b_off", "<i8"), ("o_off", "<i8"),
+                      ("n", "<i4"), ("ptile0", "<i4")])
 
 
-def segment_sums(X: torch.Tensor, starts, stops) -> torch.Tensor:
-    """out[s] = X[starts[s]:stops[s]].sum(0) for X of shape [T, ...]."""
+def segment_sums(X: torch.Tensor, starts, stops, dev_bounds=None) -> torch.Tensor:
+    """out[s] = X[starts[s]:stops[s]].sum(0) for X of shape [T, ...].  ``dev_bounds``:
+    device int32 copies of (starts, stops), e.g. from a cached plan (no host->device copy)."""
     T = X.shape[0]
     tail = X.shape[1:]
     starts = np.asarray(starts, dtype=np.int32)
@@ -31,8 +32,7 @@ def segment_sums(X: torch.Tensor, starts, stops) -> torch.Tensor:
         if X.dtype != torch.float64 or not X.is_contiguous():
             raise ValueError("segment_sums: contiguous fp64 required")
         E = X[0].numel() if T > 0 else int(np.prod(tail))
-        st = torch.as_tensor(starts, device=X.device)
-        sp = torch.as_tensor(stops, device=X.device)
+        st, sp = dev_bounds if dev_bounds is not None else upload([starts, stops], X.device)
         nat.check(nat.hip_lib().pfml_segsum(X.data_ptr(), E, st.data_ptr(), sp.data_ptr(), S,
                                             out.data_ptr(), nat.stream_of(X)), "pfml_segsum")
     else:
@@ -45,7 +45,7 @@ nat.register_hip("pfml_window_prefix_sym", [C.c_void_p, C.c_int, C.c_int, C.c_in
                                             C.c_void_p, C.c_int, C.c_void_p, C.c_void_p])
 
 
-def window_prefix_sym(X: torch.Tensor, starts, stops) -> torch.Tensor:
+def window_prefix_sym(X: torch.Tensor, starts, stops, dev_bounds=None) -> torch.Tensor:
     """out[g, s] = sum of X[g, t] over the months of segments 0..s (X: [G, T, P, P], every
     X[g, t] symmetric).  Device: one pass over the upper triangles (csrc/segsum.hip)."""
     G, T, P, _ = X.shape
@@ -58,7 +58,7 @@ def window_prefix_sym(X: torch.Tensor, starts, stops) -> torch.Tensor:
     if nat.is_device(X):
         if X.dtype != torch.float64 or not X.is_contiguous():
             raise ValueError("window_prefix_sym: contiguous fp64 required")
-        st, sp = upload([starts, stops], X.device)
+        st, sp = dev_bounds if dev_bounds is not None else upload([starts, stops], X.device)
         nat.check(nat.hip_lib().pfml_window_prefix_sym(X.data_ptr(), P, T, G, st.data_ptr(),
                                                        sp.data_ptr(), S, out.data_ptr(),
                                                        nat.stream_of(X)),
@@ -254,6 +254,39 @@ def band_policy(cell_n: np.ndarray) -> tuple[int, bool]:
     return mode, two
 
 
+_UTIL_PLANS: dict = {}
+
+
+def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell, job_month,
+                    job_n) -> dict:
+    """Launch plan of ridge_utilities on a device, cached: the descriptors depend only on the
+    grid's shape (cells, jobs, P, L), so repeated grid searches (every step of a run, every
+    benchmark step) reuse the uploaded device copies and skip all host planning.  Each group's
+    cells / jobs write straight into the full beta / obj arrays (global out offsets)."""
+    key = (P, L, str(dev), cell_src.tobytes(), cell_n.tobytes(), cell_scale.tobytes(),
+           job_cell.tobytes(), job_month.tobytes(), job_n.tobytes())
+    hit = _UTIL_PLANS.get(key)
+    if hit is not None:
+        return hit
+    big = cell_n == cell_n.max()
+    groups, arrays = [], []
+    for grp in (big, ~big):
+        cells = np.nonzero(grp)[0]
+        jobs = np.nonzero(grp[job_cell])[0]
+        rp = ridge_plan(P, L, cell_src[cells], cell_n[cells], cell_scale[cells])
+        # ridge_plan orders cells big-first and numbers outputs 0..: map to global rows
+        rp["desc"]["out"] = cells[rp["desc"]["out"] // (L * P)].astype(np.int64) * L * P
+        qp = quad_plan(P, L, P, job_cell[jobs], job_month[jobs], job_n[jobs], job_out=jobs)
+        groups.append((cells, jobs, rp, qp))
+        arrays += [rp["desc"], qp["desc"], qp["tile_job"]]
+    dv = upload(arrays, dev)                     # all descriptors, one async copy
+    plan = {"groups": groups, "dv": dv}
+    if len(_UTIL_PLANS) > 64:
+        _UTIL_PLANS.clear()
+    _UTIL_PLANS[key] = plan
+    return plan
+
+
 def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_scale,
                     lvec: torch.Tensor, D: torch.Tensor, R: torch.Tensor, job_cell, job_month,
                     job_n) -> tuple[torch.Tensor, torch.Tensor]:
@@ -262,11 +295,12 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     On a device the cells split into the largest-n group and the rest; each group's
     ridge -> utilities chain is issued on its own HIP stream, the big group first, so the
     small cells' whole chain runs on the CUs the big cells' one-workgroup-per-cell band
-    reductions leave idle.  Non-SPD repairs (rare) are applied once at the end, and the
-    utilities of repaired cells recomputed.
+    reductions leave idle.  Both chains write their rows of beta / obj in place.  Non-SPD
+    repairs (rare) are applied once at the end, and the utilities of repaired cells
+    recomputed.
     """
     cell_src, cell_n = np.asarray(cell_src), np.asarray(cell_n)
-    cell_scale = np.asarray(cell_scale)
+    cell_scale = np.asarray(cell_scale, dtype=np.float64)
     job_cell, job_month, job_n = (np.asarray(job_cell), np.asarray(job_month),
                                   np.asarray(job_n))
     mode, two = band_policy(cell_n)
@@ -278,48 +312,25 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     L = int(lvec.numel())
     nc = len(cell_src)
     dev = SD.device
+    plan = _utilities_plan(P, L, dev, cell_src, cell_n, cell_scale, job_cell, job_month, job_n)
+    th("plans")
     beta = torch.zeros((nc, L, P), dtype=SD.dtype, device=dev)
     obj = torch.empty((len(job_cell), L), dtype=SD.dtype, device=dev)
     SD, Sr, D, R = SD.contiguous(), Sr.contiguous(), D.contiguous(), R.contiguous()
     lv = lvec.to(device=dev, dtype=torch.float64).contiguous()
-    big = cell_n == cell_n.max()
-    groups = []
-    for grp in (big, ~big):
-        cells = np.nonzero(grp)[0]
-        remap = np.full(nc, -1, dtype=np.int64)
-        remap[cells] = np.arange(len(cells))
-        jobs = np.nonzero(grp[job_cell])[0]
-        rp = ridge_plan(P, L, cell_src[cells], cell_n[cells], cell_scale[cells])
-        qp = quad_plan(P, L, P, remap[job_cell[jobs]], job_month[jobs], job_n[jobs])
-        groups.append((cells, jobs, rp, qp))
-    arrays = []
-    for _, _, rp, qp in groups:
-        arrays += [rp["desc"], qp["desc"], qp["tile_job"]]
-    th("plans")
-    dv = upload(arrays, dev)                     # all descriptors, one async copy
-    th("upload")
     cur = torch.cuda.current_stream(dev)
     side = _side_stream(dev)
     side.wait_stream(cur)
-    outs = []
+    dv = plan["dv"]
     for gi, stream in ((0, side), (1, cur)):     # big cells' factorisations issued first
-        cells, jobs, rp, qp = groups[gi]
+        _, _, rp, qp = plan["groups"][gi]
         with torch.cuda.stream(stream):
-            b = torch.zeros((len(cells), L, P), dtype=SD.dtype, device=dev)
-            ridge_launch(rp, dv[3 * gi], SD, Sr, lv, b, mode)
-            o = torch.empty((len(jobs), L), dtype=SD.dtype, device=dev)
-            quad_launch(qp, dv[3 * gi + 1], dv[3 * gi + 2], D, R, b, o)
-        outs.append((cells, jobs, b, o))
+            ridge_launch(rp, dv[3 * gi], SD, Sr, lv, beta, mode)
+            quad_launch(qp, dv[3 * gi + 1], dv[3 * gi + 2], D, R, beta, obj)
     th("launch")
     cur.wait_stream(side)
-    for t in (SD, Sr, D, R, lv, *dv):
+    for t in (SD, Sr, D, R, lv, beta, obj):
         t.record_stream(side)
-    for cells, jobs, b, o in outs:
-        b.record_stream(cur)
-        o.record_stream(cur)
-        beta.index_copy_(0, torch.as_tensor(cells, device=dev), b)
-        obj.index_copy_(0, torch.as_tensor(jobs, device=dev), o)
-    th("merge")
     fixed = repair_nonspd(beta, SD, Sr, cell_src, cell_n, cell_scale, lv)
     th("repair_check")
     if len(fixed):
@@ -329,8 +340,9 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     return beta, obj
 
 
-def quad_plan(P: int, L: int, Pb: int, job_cell, job_month, job_n) -> dict:
-    """Host-side descriptors of one utilities launch (JOB_DTYPE + row-tile -> job map)."""
+def quad_plan(P: int, L: int, Pb: int, job_cell, job_month, job_n, job_out=None) -> dict:
+    """Host-side descriptors of one utilities launch (JOB_DTYPE + row-tile -> job map).
+    ``job_out``: row of each job in the obj array the launch writes (default: 0..nj-1)."""
     lib = nat.hip_lib()
     if lib.pfml_quadform_job_desc_size() != JOB_DTYPE.itemsize:
         raise RuntimeError("JobDesc layout mismatch between python and libpfml_hip")
@@ -343,6 +355,8 @@ def quad_plan(P: int, L: int, Pb: int, job_cell, job_month, job_n) -> dict:
     desc["d_off"] = np.asarray(job_month, np.int64) * P * P
     desc["r_off"] = np.asarray(job_month, np.int64) * P
     desc["b_off"] = np.asarray(job_cell, np.int64) * L * Pb
+    desc["o_off"] = (np.arange(nj, dtype=np.int64) if job_out is None
+                     else np.asarray(job_out, np.int64)) * L
     desc["n"] = job_n.astype(np.int32)
     desc["ptile0"] = pt0
     tile_job = np.repeat(np.arange(nj, dtype=np.int32), ntile)
