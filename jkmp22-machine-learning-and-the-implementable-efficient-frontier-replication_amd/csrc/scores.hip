@@ -1,0 +1,153 @@
+// Validation scores (K17; PFML_hp_reals.py:104-125): for one validation frame of the
+// utilities obj[nV][G][C] (C = nP * L hyper-parameter combinations) and the g-range [g0, g1)
+// it holds (all g' <= g in reference-compat mode, quirk Q2):
+//
+//   cum[r][c]  = mean of seq[0..r][c]   over the frame's rows r = v * k + kk (k = g1 - g0),
+//                seq[v * k + kk][c] = obj[v][g0 + kk][c]           (expanding mean by (p, l))
+//   rank[v][i] = dense descending rank of cum[v * k + i / C][i % C] among the month's k * C
+//                values (torch.sort semantics: NaN above everything, every NaN distinct)
+//
+// Two launches replace the ~25 small torch kernels (sort, scans, scatters) per frame:
+//   prefix_mean_kernel  16 columns x 16 row chunks per workgroup: chunk sums, LDS offsets,
+//                       chunk rescans (loads batched and clamped)
+//   dense_rank_kernel   one workgroup per month: bitonic sort of <= 1024 (key, index) pairs in
+//                       LDS, adjacent-difference + block scan for the dense rank, scatter back
+#include "common.h"
+
+namespace {
+
+constexpr int RK_N = 1024;          // max values per month (k * C <= 1024)
+constexpr int RK_T = 256;
+
+constexpr int PM_COLS = 16, PM_RG = 16;   // prefix mean: 16 columns x 16 row chunks per WG
+
+__global__ __launch_bounds__(256) void prefix_mean_kernel(const double* __restrict__ obj, int nV,
+                                                          int G, int g0, int k, int C,
+                                                          double* __restrict__ cum) {
+  // thread (rg, cg): rows [rg * chunk, (rg + 1) * chunk) of column c; chunk sums meet in LDS
+  // for the cross-chunk offsets, then each chunk is rescanned.  Loads are clamped and batched
+  // (8 in flight), so a thread pays ~2 R / (8 PM_RG) memory latencies, not R.
+  __shared__ double part[PM_RG][PM_COLS];
+  const int cg = threadIdx.x % PM_COLS, rg = threadIdx.x / PM_COLS;
+  const int c = blockIdx.x * PM_COLS + cg;
+  const bool cv = c < C;
+  const int cc = cv ? c : C - 1;
+  const int R = nV * k;
+  const int chunk = (R + PM_RG - 1) / PM_RG;
+  const int r0 = rg * chunk, r1 = min(R, r0 + chunk);
+  auto at = [&](int r) {
+    const int v = r / k, kk = r - v * k;
+    return obj[((int64_t)v * G + g0 + kk) * C + cc];
+  };
+  double s = 0.0;
+  for (int r = r0; r < r1; r += 8) {
+    double x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = at(min(r + u, r1 - 1));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += (r + u < r1) ? x[u] : 0.0;
+  }
+  part[rg][cg] = s;
+  __syncthreads();
+  s = 0.0;
+  for (int q = 0; q < rg; ++q) s += part[q][cg];
+  for (int r = r0; r < r1; r += 8) {
+    double x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = at(min(r + u, r1 - 1));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (r + u < r1) {
+        s += x[u];
+        if (cv) cum[(int64_t)(r + u) * C + c] = s / (double)(r + u + 1);
+      }
+    }
+  }
+}
+
+// descending order with NaN first (torch.sort(descending=True) semantics); padding last
+__device__ __forceinline__ bool before(double a, int ia, double b, int ib) {
+  if (ia < 0) return false;                 // padding never precedes
+  if (ib < 0) return true;
+  const bool na = a != a, nb = b != b;
+  if (na != nb) return na;
+  if (na) return ia < ib;
+  return a > b || (a == b && ia < ib);
+}
+
+__global__ __launch_bounds__(RK_T) void dense_rank_kernel(const double* __restrict__ cum, int N,
+                                                          double* __restrict__ rank) {
+  __shared__ double key[RK_N];
+  __shared__ int idx[RK_N];
+  __shared__ int wsum[RK_T / 64];
+  const int v = blockIdx.x, t = threadIdx.x;
+  const double* src = cum + (int64_t)v * N;
+  for (int i = t; i < RK_N; i += RK_T) {
+    key[i] = src[min(i, N - 1)];            // (padding entries carry idx -1)
+    idx[i] = (i < N) ? i : -1;
+  }
+  __syncthreads();
+  // bitonic sort of RK_N elements, "before" order
+  for (int size = 2; size <= RK_N; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int p = t; p < RK_N / 2; p += RK_T) {
+        const int lo = 2 * p - (p & (stride - 1)), hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const double ka = key[lo], kb = key[hi];
+        const int ia = idx[lo], ib = idx[hi];
+        const bool swap = up ? before(kb, ib, ka, ia) : before(ka, ia, kb, ib);
+        if (swap) {
+          key[lo] = kb; key[hi] = ka;
+          idx[lo] = ib; idx[hi] = ia;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // dense rank: new[i] = (i == 0) || key[i] != key[i-1]; inclusive scan, 4 per thread
+  int nw[4], run = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = 4 * t + q;
+    const bool real = idx[i] >= 0;
+    nw[q] = real && (i == 0 || key[i] != key[i - 1]) ? 1 : 0;
+    run += nw[q];
+  }
+  // block exclusive scan of run
+  const int lane = t & 63, w = t >> 6;
+  int incl = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int base = 0;
+  for (int q = 0; q < w; ++q) base += wsum[q];
+  int acc = base + incl - run;
+  double* dst = rank + (int64_t)v * N;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = 4 * t + q;
+    acc += nw[q];
+    if (idx[i] >= 0) dst[idx[i]] = (double)acc;
+  }
+}
+
+}  // namespace
+
+extern "C" int pfml_scores_max_per_month() { return RK_N; }
+
+// obj [nV][G][C]; cum [nV * k][C]; rank [nV][k * C]; k = g1 - g0
+extern "C" hipError_t pfml_validation_scores(const double* obj, int nV, int G, int g0, int g1,
+                                             int C, double* cum, double* rank,
+                                             hipStream_t st) {
+  const int k = g1 - g0;
+  if (nV <= 0 || C <= 0 || k <= 0) return hipSuccess;
+  if (k * C > RK_N || g0 < 0 || g1 > G) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(prefix_mean_kernel, dim3((C + PM_COLS - 1) / PM_COLS), dim3(256), 0, st, obj,
+                     nV, G, g0, k, C, cum);
+  hipLaunchKernelGGL(dense_rank_kernel, dim3(nV), dim3(RK_T), 0, st, cum, k * C, rank);
+  return hipGetLastError();
+}

@@ -62,31 +62,46 @@ extern "C" hipError_t pfml_segsum(const double* X, int64_t E, const int* seg_sta
 // torch cumsum it replaces read 2x and wrote 3x as much.
 namespace {
 
+// Segment s's sums live in out[g][s - skip] for s >= skip and in scratch[g][s] for the
+// leading `skip` segments (e.g. the burn-in block, needed only as a prefix): the output is
+// the contiguous [G][nseg - skip] stack the ridge grid consumes, with no slicing copy.
+__device__ __forceinline__ double* seg_slot(double* out, double* scratch, int g, int s, int nseg,
+                                            int skip, int64_t PP) {
+  return s < skip ? scratch + ((int64_t)g * skip + s) * PP
+                  : out + ((int64_t)g * (nseg - skip) + (s - skip)) * PP;
+}
+
 __global__ __launch_bounds__(256) void wsum_upper_kernel(const double* __restrict__ X, int P,
                                                          int T, const int* __restrict__ seg_start,
                                                          const int* __restrict__ seg_stop,
-                                                         int nseg, double* __restrict__ out) {
+                                                         int nseg, int skip,
+                                                         double* __restrict__ out,
+                                                         double* __restrict__ scratch) {
   const int i = blockIdx.x, s = blockIdx.y, g = blockIdx.z;
   const int a = seg_start[s], b = seg_stop[s];
   const int64_t PP = (int64_t)P * P;
   const double* src = X + (int64_t)g * T * PP + (int64_t)i * P;
-  double* dst = out + ((int64_t)g * nseg + s) * PP + (int64_t)i * P;
+  double* dst = seg_slot(out, scratch, g, s, nseg, skip, PP) + (int64_t)i * P;
   for (int j = i + threadIdx.x; j < P; j += 256) {
-    double acc0 = 0.0, acc1 = 0.0;
+    // four independent chains: four month loads in flight per lane
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
     int tm = a;
-    for (; tm + 2 <= b; tm += 2) {
-      acc0 += src[(int64_t)tm * PP + j];
-      acc1 += src[(int64_t)(tm + 1) * PP + j];
+    for (; tm + 4 <= b; tm += 4) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += src[(int64_t)(tm + u) * PP + j];
     }
-    if (tm < b) acc0 += src[(int64_t)tm * PP + j];
-    dst[j] = acc0 + acc1;
+    for (; tm < b; ++tm) acc[0] += src[(int64_t)tm * PP + j];
+    dst[j] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   }
 }
 
 // pass 2 on 32 x 32 tiles (I <= J) of the upper triangle: running sum over segments in
-// registers, tile (I, J) and its transpose (J, I) both written row-contiguous via LDS
-__global__ __launch_bounds__(256) void wsum_prefix_mirror_kernel(int P, int nseg,
-                                                                 double* __restrict__ out) {
+// registers, tile (I, J) and its transpose (J, I) both written row-contiguous via LDS.  The
+// next segment's tile is loaded while the current one is written (loads clamped into the
+// matrix, masked on use).
+__global__ __launch_bounds__(256) void wsum_prefix_mirror_kernel(int P, int nseg, int skip,
+                                                                 double* __restrict__ out,
+                                                                 double* __restrict__ scratch) {
   __shared__ double Ts[32][33];
   const int g = blockIdx.y;
   int tile = blockIdx.x;
@@ -95,26 +110,40 @@ __global__ __launch_bounds__(256) void wsum_prefix_mirror_kernel(int P, int nseg
   while (tile >= nt - I) { tile -= nt - I; ++I; }
   const int J = I + tile;
   const int64_t PP = (int64_t)P * P;
-  double* og = out + (int64_t)g * nseg * PP;
   const int t = threadIdx.x, c = t & 31, r0 = t >> 5;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  double acc[4] = {0.0, 0.0, 0.0, 0.0}, nx[4];
+  auto fetch = [&](int s) {
+    const double* o = seg_slot(out, scratch, g, s, nseg, skip, PP);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = min(I * 32 + r0 + 8 * q, P - 1), j = min(J * 32 + c, P - 1);
+      nx[q] = o[(int64_t)i * P + j];
+    }
+  };
+  fetch(0);
   for (int s = 0; s < nseg; ++s) {
-    double* o = og + (int64_t)s * PP;
+    double cur[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cur[q] = nx[q];
+    if (s + 1 < nseg) fetch(s + 1);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
       const bool valid = i < P && j < P && (I != J || c >= r);
-      if (valid) acc[q] += o[(int64_t)i * P + j];
+      acc[q] += valid ? cur[q] : 0.0;
       Ts[r][c] = acc[q];
     }
     __syncthreads();
+    if (s >= skip) {
+      double* o = seg_slot(out, scratch, g, s, nseg, skip, PP);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = r0 + 8 * q;
-      const int i = I * 32 + r, j = J * 32 + c;
-      if (i < P && j < P) o[(int64_t)i * P + j] = (I != J || c >= r) ? Ts[r][c] : Ts[c][r];
-      const int i2 = J * 32 + r, j2 = I * 32 + c;     // transposed tile
-      if (I != J && i2 < P && j2 < P) o[(int64_t)i2 * P + j2] = Ts[c][r];
+      for (int q = 0; q < 4; ++q) {
+        const int r = r0 + 8 * q;
+        const int i = I * 32 + r, j = J * 32 + c;
+        if (i < P && j < P) o[(int64_t)i * P + j] = (I != J || c >= r) ? Ts[r][c] : Ts[c][r];
+        const int i2 = J * 32 + r, j2 = I * 32 + c;     // transposed tile
+        if (I != J && i2 < P && j2 < P) o[(int64_t)i2 * P + j2] = Ts[c][r];
+      }
     }
     __syncthreads();
   }
@@ -124,12 +153,14 @@ __global__ __launch_bounds__(256) void wsum_prefix_mirror_kernel(int P, int nseg
 
 extern "C" hipError_t pfml_window_prefix_sym(const double* X, int P, int T, int G,
                                              const int* seg_start, const int* seg_stop, int nseg,
-                                             double* out, hipStream_t st) {
+                                             int skip, double* out, double* scratch,
+                                             hipStream_t st) {
   if (nseg <= 0 || P <= 0 || G <= 0) return hipSuccess;
+  if (skip < 0 || skip > nseg || (skip > 0 && scratch == nullptr)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(wsum_upper_kernel, dim3(P, nseg, G), dim3(256), 0, st, X, P, T, seg_start,
-                     seg_stop, nseg, out);
+                     seg_stop, nseg, skip, out, scratch);
   const int nt = (P + 31) / 32;
   hipLaunchKernelGGL(wsum_prefix_mirror_kernel, dim3(nt * (nt + 1) / 2, G), dim3(256), 0, st, P,
-                     nseg, out);
+                     nseg, skip, out, scratch);
   return hipGetLastError();
 }

@@ -21,6 +21,7 @@ the end (a few MB; every rank's row count follows from the shared plan).
 """
 from __future__ import annotations
 
+import ctypes as C
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -28,11 +29,17 @@ import pandas as pd
 import torch
 
 from ..config import Config
+from ..ops import _native as nat
 from ..ops.ridge import _HostClock, ridge_utilities, segment_sums, window_prefix_sym
 from ..parallel import collectives as coll
 from ..parallel.dist import env as dist_env
 from ..utils.dates import mi_from_ym, month_end
 from ..utils.trace import range_push, range_pop
+
+
+nat.register_hip("pfml_validation_scores", [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                            C.c_int, C.c_void_p, C.c_void_p, C.c_void_p])
+nat.register_hip("pfml_scores_max_per_month", [])
 
 
 @dataclass
@@ -170,12 +177,14 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
     range_push("search.window_sums")
     if nseg:
         # running sums at every block end in one pass over the symmetric upper triangles
+        # (the burn-in block, rank 0 only, is a prefix segment and not an output row)
         db = su["dev_bounds"]
+        skip = nseg - nYl
         SD = window_prefix_sym(reals.denom, su["st"], su["sp"],
-                               dev_bounds=None if db is None else db[:2])
+                               dev_bounds=None if db is None else db[:2], skip=skip)
         Sr = segment_sums(reals.r_tilde.reshape(G * T, P), su["starts"], su["stops"],
                           dev_bounds=None if db is None else db[2:]).view(G, nseg, P)
-        Sr = _cumsum0(Sr.transpose(0, 1)).transpose(0, 1)
+        Sr = _cumsum0(Sr.transpose(0, 1)).transpose(0, 1)[:, skip:]
         totD, totr = SD[:, -1], Sr[:, -1]
     else:
         SD = torch.zeros((G, 0, P, P), dtype=torch.float64, device=dev)
@@ -187,8 +196,6 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
         off = coll.exclusive_prefix_sum(flat)
         SD = SD + off[:, : P * P].view(G, 1, P, P)
         Sr = Sr + off[:, P * P:].view(G, 1, P)
-    if nseg > nYl:                       # drop the burn-in prefix row
-        SD, Sr = SD[:, 1:], Sr[:, 1:]
     range_pop()
 
     # ---- 2. ridge grid + 3. utilities for every (cell, validation month) -------------
@@ -243,8 +250,19 @@ def validation_scores(obj: torch.Tensor, frame_g: int, compat: bool):
     (p, l, eom_ret)); otherwise only g's own rows.
     Returns (obj_seq, cum, rank) each [nVal, k, nP, L] with k = frame_g+1 (compat) or 1.
     """
-    seq = obj[:, : frame_g + 1] if compat else obj[:, frame_g: frame_g + 1]
+    g0, g1 = (0, frame_g + 1) if compat else (frame_g, frame_g + 1)
+    seq = obj[:, g0:g1]
     nV, k, nP, L = seq.shape
+    if nat.is_device(obj) and k * nP * L <= nat.hip_lib().pfml_scores_max_per_month():
+        # csrc/scores.hip: chunked prefix mean + per-month bitonic dense rank, two launches
+        o = obj.contiguous()
+        cum = torch.empty((nV, k, nP, L), dtype=obj.dtype, device=obj.device)
+        rank = torch.empty_like(cum)
+        nat.check(nat.hip_lib().pfml_validation_scores(o.data_ptr(), nV, o.shape[1], g0, g1,
+                                                       nP * L, cum.data_ptr(), rank.data_ptr(),
+                                                       nat.stream_of(o)),
+                  "pfml_validation_scores")
+        return seq, cum, rank
     flat = seq.reshape(nV * k, nP, L)
     cnt = torch.arange(1, nV * k + 1, dtype=flat.dtype, device=flat.device).view(-1, 1, 1)
     cum = (_cumsum0(flat) / cnt).view(nV, k, nP, L)

@@ -42,32 +42,38 @@ def segment_sums(X: torch.Tensor, starts, stops, dev_bounds=None) -> torch.Tenso
 
 
 nat.register_hip("pfml_window_prefix_sym", [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
-                                            C.c_void_p, C.c_int, C.c_void_p, C.c_void_p])
+                                            C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                            C.c_void_p])
 
 
-def window_prefix_sym(X: torch.Tensor, starts, stops, dev_bounds=None) -> torch.Tensor:
-    """out[g, s] = sum of X[g, t] over the months of segments 0..s (X: [G, T, P, P], every
-    X[g, t] symmetric).  Device: one pass over the upper triangles (csrc/segsum.hip)."""
+def window_prefix_sym(X: torch.Tensor, starts, stops, dev_bounds=None,
+                      skip: int = 0) -> torch.Tensor:
+    """out[g, s - skip] = sum of X[g, t] over the months of segments 0..s, for s >= skip (X:
+    [G, T, P, P], every X[g, t] symmetric; the first ``skip`` segments only feed the prefix).
+    Device: one pass over the upper triangles (csrc/segsum.hip), contiguous output."""
     G, T, P, _ = X.shape
     starts = np.asarray(starts, dtype=np.int32)
     stops = np.asarray(stops, dtype=np.int32)
     S = len(starts)
-    out = torch.empty((G, S, P, P), dtype=X.dtype, device=X.device)
+    out = torch.empty((G, max(S - skip, 0), P, P), dtype=X.dtype, device=X.device)
     if S == 0:
         return out
     if nat.is_device(X):
         if X.dtype != torch.float64 or not X.is_contiguous():
             raise ValueError("window_prefix_sym: contiguous fp64 required")
         st, sp = dev_bounds if dev_bounds is not None else upload([starts, stops], X.device)
-        nat.check(nat.hip_lib().pfml_window_prefix_sym(X.data_ptr(), P, T, G, st.data_ptr(),
-                                                       sp.data_ptr(), S, out.data_ptr(),
-                                                       nat.stream_of(X)),
-                  "pfml_window_prefix_sym")
+        scratch = (torch.empty((G, skip, P, P), dtype=X.dtype, device=X.device) if skip
+                   else None)
+        nat.check(nat.hip_lib().pfml_window_prefix_sym(
+            X.data_ptr(), P, T, G, st.data_ptr(), sp.data_ptr(), S, int(skip), out.data_ptr(),
+            scratch.data_ptr() if scratch is not None else None, nat.stream_of(X)),
+            "pfml_window_prefix_sym")
         return out
     acc = torch.zeros((G, P, P), dtype=X.dtype)
     for s in range(S):
         acc = acc + X[:, starts[s]:stops[s]].sum(1)
-        out[:, s] = acc
+        if s >= skip:
+            out[:, s - skip] = acc
     return out
 
 

@@ -219,3 +219,25 @@ def test_window_prefix_sym(gpu):
     ref2 = window_prefix_sym(X, gap_st, gap_sp)
     assert torch.allclose(window_prefix_sym(X.to(gpu), gap_st, gap_sp).cpu(), ref2,
                           rtol=1e-13, atol=1e-12)
+    for skip in (1, 2):                         # prefix-only leading segments
+        got = window_prefix_sym(X.to(gpu), st, sp, skip=skip).cpu()
+        assert got.shape == (2, 4 - skip, 37, 37) and got.is_contiguous()
+        assert torch.allclose(got, ref[:, skip:], rtol=1e-13, atol=1e-12)
+        assert torch.equal(got, got.transpose(-1, -2))
+
+
+@pytest.mark.parametrize("compat", [True, False])
+def test_validation_scores_kernel(gpu, compat):
+    """csrc/scores.hip (prefix mean + per-month dense rank) vs the torch path on CPU, incl.
+    exact ties across (p, l) cells and a NaN."""
+    from pfml.models.search import validation_scores
+    g = torch.Generator().manual_seed(5)
+    obj = torch.randn(37, 2, 4, 101, generator=g, dtype=torch.float64)
+    obj[:, :, 1, :] = obj[:, :, 0, :]                     # exact ties
+    obj[3, 1, 2, 7] = float("nan")
+    for fg in (0, 1):
+        ref = validation_scores(obj, fg, compat)
+        got = validation_scores(obj.to(gpu), fg, compat)
+        assert torch.allclose(got[0].cpu(), ref[0], rtol=0, atol=0, equal_nan=True)
+        assert torch.allclose(got[1].cpu(), ref[1], rtol=1e-12, atol=1e-14, equal_nan=True)
+        assert torch.equal(got[2].cpu(), ref[2])
