@@ -5,7 +5,7 @@
 // the EWMA idiosyncratic vol is a numba @njit kernel, Estimate Covariance Matrix.py:345-386).
 // They are sequential per group, touch each row once and are a one-shot cost, so they live in
 // C++ on the host (OpenMP over groups) rather than on the GPU; the EWMA scan has a HIP
-// counterpart (csrc/ewma.hip) used when the daily residual panel is device-resident.
+// counterpart (csrc/risk.hip) used when the daily residual panel is device-resident.
 //
 // All entry points take rows sorted by (group, time) and a CSR-style group_start array of
 // length ngroups + 1.

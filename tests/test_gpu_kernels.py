@@ -241,3 +241,26 @@ def test_validation_scores_kernel(gpu, compat):
         assert torch.allclose(got[0].cpu(), ref[0], rtol=0, atol=0, equal_nan=True)
         assert torch.allclose(got[1].cpu(), ref[1], rtol=1e-12, atol=1e-14, equal_nan=True)
         assert torch.equal(got[2].cpu(), ref[2])
+
+
+def test_grid_search_bitwise_deterministic(gpu):
+    """Replays of the device grid search are bitwise identical (fixed tilings and reduction
+    orders, no float atomics; SURVEY §5.2 deterministic replay), incl. the cached-plan path."""
+    from pfml.config import Config
+    from pfml.models.search import PfmlReals, grid_search, validation_scores
+    from pfml.utils.dates import mi_from_ym
+    cfg = Config.default().override(["pf_ml.p_vec=[16,64]", "pf.dates.start_year=2001",
+                                     "pf.dates.end_yr=2006"])
+    G, P = 2, 65
+    months = np.arange(mi_from_ym(1994, 3), mi_from_ym(2006, 11) + 1)
+    T = len(months)
+    X = _rand(G * T, 80, P, seed=91).to(gpu)
+    D = (X.transpose(1, 2) @ X / 80).view(G, T, P, P).contiguous()
+    r = (0.1 * _rand(G, T, P, seed=92)).to(gpu)
+    runs = []
+    for _ in range(3):
+        res = grid_search(PfmlReals(months, r, D), cfg)
+        runs.append((res.beta.cpu(), res.obj.cpu(), validation_scores(res.obj, 1, True)[2].cpu()))
+    for b, o, k in runs[1:]:
+        assert torch.equal(b, runs[0][0]) and torch.equal(o, runs[0][1])
+        assert torch.equal(k, runs[0][2])
