@@ -2,7 +2,7 @@
 generation and the headline benchmark.
 
     python -m pfml synth-data   --data-dir Data [--small] [--set run.synthetic.n_stocks=500]
-    python -m pfml main         --data-dir Data [--device cuda] [--checkpoint]
+    python -m pfml main         --data-dir Data [--device cuda] [--checkpoint] [--check]
     python -m pfml prepare-data | estimate-cov | pfml-input | pfml-search-coef | pfml-hp-reals
                    | pfml-aim | pfml-hps | pfml-best-hps | get-additional-data | sp500-subset
     python -m pfml stages a,b,c  (several stages in one process)
@@ -29,6 +29,8 @@ def _cfg(a) -> Config:
         cfg.run.artifact_dir = a.artifact_dir
     if a.corrected:
         cfg.run.compat_mode = False
+    if a.check:
+        cfg.run.check = True
     if a.profile:
         cfg.run.profile = True
         from .utils import trace
@@ -49,6 +51,8 @@ def main(argv=None) -> int:
     ap.add_argument("--checkpoint", action="store_true", help="write artifacts + resume")
     ap.add_argument("--corrected", action="store_true", help="disable reference quirks Q1-Q3")
     ap.add_argument("--profile", action="store_true", help="roctx ranges + plots")
+    ap.add_argument("--check", action="store_true",
+                    help="compare sampled device results against the fp64 CPU oracle")
     ap.add_argument("--small", action="store_true", help="synth-data: 50-stock test panel")
     a = ap.parse_args(argv)
     cfg = _cfg(a)

@@ -34,7 +34,10 @@ from ..ops.ridge import _HostClock, ridge_utilities, segment_sums, window_prefix
 from ..parallel import collectives as coll
 from ..parallel.dist import env as dist_env
 from ..utils.dates import mi_from_ym, month_end
+from ..utils.log import get_logger
 from ..utils.trace import range_push, range_pop
+
+log = get_logger("search")
 
 
 nat.register_hip("pfml_validation_scores", [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -229,6 +232,55 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
     vy = np.asarray(years, dtype=np.int64)[v_y]
     return GridResult(years=years, p_vec=p_vec, l_vec=cfg.l_vec, years_local=years[yl],
                       beta=beta, val_months=vm, val_year=vy, obj=obj)
+
+
+def check_against_oracle(grid: GridResult, reals: PfmlReals, cfg: Config, ncells: int = 3,
+                         seed: int = 0) -> dict:
+    """``--check``: recompute a few (g, year, p) cells of this rank from scratch
+    with the fp64 CPU oracle - expanding-window sums by plain summation, one
+    ``torch.linalg.solve`` per lambda, quadratic forms one by one - and report the max
+    relative error of the device coefficients and utilities (the largest-n cell is always
+    among them)."""
+    from ..ops.ridge import quadform_utilities, ridge_grid
+    months = np.asarray(reals.months, dtype=np.int64)
+    plan = make_plan(months, np.asarray(grid.years))
+    yl = np.nonzero(np.isin(np.asarray(grid.years), np.asarray(grid.years_local)))[0]
+    G, nP = reals.G, len(grid.p_vec)
+    if len(yl) == 0:
+        return {"cells": 0}
+    rng = np.random.default_rng(seed)
+    picks = {(0, len(yl) - 1, nP - 1)}
+    while len(picks) < min(ncells, G * len(yl) * nP):
+        picks.add((int(rng.integers(G)), int(rng.integers(len(yl))), int(rng.integers(nP))))
+    lv = torch.as_tensor(grid.l_vec, dtype=torch.float64)
+    denom, rt = reals.denom.cpu(), reals.r_tilde.cpu()
+    obj_host = grid.obj.cpu()
+    v_rows = {}
+    if obj_host.shape[0] == len(grid.val_months):       # gathered or single-rank utilities
+        for i, (vm, vy) in enumerate(zip(grid.val_months, grid.val_year)):
+            v_rows.setdefault(int(vy), []).append((i, int(vm)))
+    eb = eo = 0.0
+    for g, yi, pi in sorted(picks):
+        y = int(yl[yi])
+        n = int(grid.p_vec[pi]) + 1
+        stop = int(plan.seg_stop[y])
+        SD = denom[g, :stop].sum(0)[None]
+        Sr = rt[g, :stop].sum(0)[None]
+        ref = ridge_grid(SD, Sr, np.array([0]), np.array([n]),
+                         np.array([1.0 / max(int(plan.count[y]), 1)]), lv)[0]
+        got = grid.beta[g, yi, pi].cpu()
+        eb = max(eb, float(((got - ref).norm(dim=-1) / ref.norm(dim=-1).clamp_min(1e-300)).max()))
+        rows = v_rows.get(int(grid.years[y]), [])
+        if rows:
+            jm = np.array([g * len(months) + int(np.searchsorted(months, vm)) for _, vm in rows])
+            oref = quadform_utilities(denom.reshape(-1, *denom.shape[2:]),
+                                      rt.reshape(-1, rt.shape[-1]), ref[None],
+                                      np.zeros(len(rows), np.int64), jm, np.full(len(rows), n))
+            ogot = obj_host[[i for i, _ in rows], g, pi]
+            eo = max(eo, float(((ogot - oref).abs() / oref.abs().clamp_min(1e-12)).max()))
+    out = {"cells": len(picks), "beta_max_rel_err": eb, "obj_max_rel_err": eo}
+    log.info(f"check vs CPU oracle on {len(picks)} cells: beta {eb:.2e}, utilities {eo:.2e}")
+    return out
 
 
 # ---------------------------------------------------------------------------------------

@@ -218,6 +218,9 @@ class Pipeline:
     def _pfml_search_coef(self):
         self._ensure_reals()
         grid = search.grid_search(self.state["reals"], self.cfg)
+        if self.cfg.run.check:
+            metric(stage="pfml-search-coef", check=search.check_against_oracle(
+                grid, self.state["reals"], self.cfg), rank=self.env.rank)
         years, beta = search.gather_beta(grid)
         self.state["grid"], self.state["beta_years"], self.state["beta"] = grid, years, beta
         if self.checkpoint and self.env.is_main:

@@ -1,0 +1,46 @@
+"""``--check``: the sampled fp64 CPU-oracle comparison of the grid search."""
+import numpy as np
+import pytest
+import torch
+
+
+def _reals(device):
+    from pfml.config import Config
+    from pfml.models.search import PfmlReals
+    from pfml.utils.dates import mi_from_ym
+    cfg = Config.default().override(["pf_ml.p_vec=[8,16]", "pf.dates.start_year=2002",
+                                     "pf.dates.end_yr=2006"])
+    G, P = 2, 17
+    months = np.arange(mi_from_ym(1995, 1), mi_from_ym(2006, 11) + 1)
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(G * len(months), 30, P, generator=g, dtype=torch.float64)
+    D = (X.transpose(1, 2) @ X / 30).view(G, len(months), P, P)
+    r = 0.1 * torch.randn(G, len(months), P, generator=g, dtype=torch.float64)
+    return cfg, PfmlReals(months, r.to(device), D.to(device).contiguous())
+
+
+def _run(device):
+    from pfml.models.search import check_against_oracle, grid_search
+    cfg, reals = _reals(device)
+    grid = grid_search(reals, cfg)
+    return check_against_oracle(grid, reals, cfg, ncells=4)
+
+
+def test_check_cpu():
+    out = _run("cpu")
+    assert out["cells"] == 4
+    assert out["beta_max_rel_err"] < 1e-10 and out["obj_max_rel_err"] < 1e-10
+
+
+@pytest.mark.gpu
+def test_check_gpu(gpu):
+    out = _run(gpu)
+    assert out["cells"] == 4
+    assert out["beta_max_rel_err"] < 1e-8 and out["obj_max_rel_err"] < 1e-8
+
+
+def test_cli_check_flag():
+    from pfml.cli import main
+    import argparse  # noqa: F401
+    with pytest.raises(SystemExit):
+        main(["--help"])
