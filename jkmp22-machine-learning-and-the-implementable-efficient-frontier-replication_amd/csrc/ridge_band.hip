@@ -109,6 +109,14 @@ __device__ __forceinline__ double rsqrt_f64(double x) {
   return y;
 }
 
+// 1/x to full fp64 accuracy: v_rcp_f64 refined by Newton steps (e = 1 - x y, y += y e)
+__device__ __forceinline__ double rcp_f64(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+#pragma unroll
+  for (int it = 0; it < 3; ++it) y = fma(y, fma(-x, y, 1.0), y);
+  return y;
+}
+
 __device__ __forceinline__ double row16_sum(double v) {
   v += dpp_mov<0xB1>(v);      // quad_perm [1,0,3,2]
   v += dpp_mov<0x4E>(v);      // quad_perm [2,3,0,1]
@@ -224,9 +232,15 @@ __device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n,
     if (xn2 == 0.0) {
       tau = 0.0; beta = alpha; scal = 0.0;
     } else {
-      beta = -copysign(sqrt(alpha * alpha + xn2), alpha);
-      tau = (beta - alpha) / beta;
-      scal = 1.0 / (alpha - beta);
+      // beta = -sign(alpha) ||x||, tau = 1 + |alpha| / ||x||, 1 / (alpha - beta) =
+      // sign(alpha) / (|alpha| + ||x||): one rsq and one rcp chain (Newton-refined) instead
+      // of the IEEE sqrt and two divide sequences on the per-column critical path
+      const double nrm2 = fma(alpha, alpha, xn2);
+      const double rn = rsqrt_f64(nrm2);
+      const double nrm = nrm2 * rn;
+      beta = -copysign(nrm, alpha);
+      tau = fma(fabs(alpha), rn, 1.0);
+      scal = copysign(rcp_f64(fabs(alpha) + nrm), alpha);
     }
     const double wc = tau * (vjc + scal * dc);
 #pragma unroll
