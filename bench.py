@@ -135,9 +135,9 @@ def main():
     ap.add_argument("--with-inputs", action="store_true",
                     help="time S4 (PFML input construction for every month) + S5 + S6")
     ap.add_argument("--stocks", type=int, default=500)
-    ap.add_argument("--precision", default="fp64", choices=["fp64", "bf16", "fp8"],
-                    help="with --with-inputs: S4 covariance / RFF / risk GEMMs on bf16 or fp8 "
-                         "MFMA (experimental; error vs fp64 reported); solves stay fp64")
+    ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32", "bf16", "fp8"],
+                    help="with --with-inputs: S4 covariance / RFF / risk GEMMs in fp32, or on bf16 / "
+                         "fp8 MFMA (experimental; error vs fp64 reported); solves stay fp64")
     ap.add_argument("--tiny", action="store_true",
                     help="CI only: p in {8, 16}, 180 months (exercises the multi-rank path on "
                          "CPU/gloo; not the benchmark config)")

@@ -162,9 +162,9 @@ class RunOptions:
     # RFF weight matrix is supplied), Q2 (validation rows accumulate across g), Q3
     # (pf.csv eom_ret == eom).  False gives the corrected behaviour.
     compat_mode: bool = True
-    # fp64 (production) | bf16 | fp8: the S4 covariance (K1), RFF (K13) and risk GEMMs on
-    # low-precision MFMA with fp32 accumulation; solves stay fp64 (bench --precision reports
-    # the error vs fp64)
+    # fp64 (production) | fp32 | bf16 | fp8: the S4 covariance (K1), RFF (K13) and risk GEMMs
+    # in reduced precision (fp32 sgemm, or bf16 / fp8 MFMA with fp32 accumulation); solves
+    # stay fp64 (bench --precision reports the error vs fp64)
     precision: str = "fp64"
     device: str = "auto"               # auto | cpu | cuda
     world_size: int = 1

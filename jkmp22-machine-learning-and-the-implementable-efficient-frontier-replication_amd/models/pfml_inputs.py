@@ -152,7 +152,7 @@ def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
     G, Pm = len(cfg.g_vec), cfg.p_max
     P = Pm + 1
     dev = torch.device(device)
-    prec = cfg.run.precision         # fp64 | bf16 | fp8: the covariance / RFF / risk GEMMs
+    prec = cfg.run.precision         # fp64 | fp32 | bf16 | fp8: covariance / RFF / risk GEMMs
     panel = Panel.from_chars(chars, features)
     grids = pfml_date_grids(int(barra.months.min()), lb, cfg.settings["split"]["test_end"],
                             cfg.settings["pf"]["dates"]["start_year"],

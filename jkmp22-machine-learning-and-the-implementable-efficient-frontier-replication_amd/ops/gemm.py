@@ -162,8 +162,34 @@ def gemm_lowp(A: torch.Tensor, B: torch.Tensor, fmt: str, *, trans_a: bool = Fal
     return out.squeeze(0) if squeeze and out.dim() == 3 else out
 
 
+def gemm_fp32(A: torch.Tensor, B: torch.Tensor, *, trans_a: bool = False,
+              trans_b: bool = False, alpha: float = 1.0, beta: float = 0.0,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """alpha op(A) op(B) + beta C with fp32 operands and accumulation (rocBLAS sgemm: the f32
+    MFMA runs at twice the fp64 rate on gfx950), fp64 in and out."""
+    a = A.to(torch.float32)
+    b = B.to(torch.float32)
+    if trans_a:
+        a = a.transpose(-1, -2)
+    if trans_b:
+        b = b.transpose(-1, -2)
+    C = torch.matmul(a, b).to(torch.float64)
+    if alpha != 1.0:
+        C.mul_(alpha)
+    if out is None:
+        return C
+    if beta == 0.0:
+        out.copy_(C)
+    else:
+        out.mul_(beta).add_(C)
+    return out
+
+
 def gemm_prec(A: torch.Tensor, B: torch.Tensor, precision: str = "fp64", **kw) -> torch.Tensor:
-    """``gemm`` at the configured precision: fp64 (production) or a bf16 / fp8 experiment."""
+    """``gemm`` at the configured precision: fp64 (production) or an fp32 / bf16 / fp8
+    experiment."""
     if precision in LOWP_FORMATS:
         return gemm_lowp(A, B, precision, **kw)
+    if precision == "fp32":
+        return gemm_fp32(A, B, **kw)
     return gemm(A, B, **kw)

@@ -19,7 +19,7 @@ nat.register_hip("pfml_standardize", [C.c_void_p, C.c_int, C.c_void_p, C.c_void_
 
 def rff_features(X: torch.Tensor, W: torch.Tensor, precision: str = "fp64") -> torch.Tensor:
     """[R, k] x [k, P/2] -> [R, P+1] rows [1, cos z1, sin z1, cos z2, sin z2, ...].
-    ``precision`` bf16 / fp8: X W on the low-precision MFMA GEMM (experimental configs)."""
+    ``precision`` fp32 / bf16 / fp8: X W in reduced precision (experimental configs)."""
     R, half = X.shape[0], W.shape[1]
     Z = gemm_prec(X, W, precision)
     out = torch.empty((R, 2 * half + 1), dtype=X.dtype, device=X.device)

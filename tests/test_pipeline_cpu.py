@@ -205,3 +205,21 @@ def test_pipeline_cli_resume_and_fault_injection(small_data, tmp_path):
     assert np.allclose(summ1[["r", "sr"]].to_numpy(), summ2[["r", "sr"]].to_numpy(), rtol=1e-10)
     from pfml.utils.log import COUNTERS
     assert COUNTERS.as_dict().get("pfml_input.recomputed_months", 0) >= 1
+
+
+def test_gemm_fp32_precision_cpu():
+    """precision=fp32 (sgemm operands/accumulation, fp64 in/out) honours op flags, alpha/beta
+    and out, within fp32 rounding of the fp64 product."""
+    import torch
+    from pfml.ops.gemm import gemm, gemm_prec
+    g = torch.Generator().manual_seed(1)
+    A = torch.randn(3, 40, 30, generator=g, dtype=torch.float64)
+    B = torch.randn(3, 50, 40, generator=g, dtype=torch.float64)
+    C0 = torch.randn(3, 30, 50, generator=g, dtype=torch.float64)
+    ref = gemm(A, B, trans_a=True, trans_b=True, alpha=0.5)
+    got = gemm_prec(A, B, "fp32", trans_a=True, trans_b=True, alpha=0.5)
+    assert got.dtype == torch.float64
+    assert (got - ref).abs().max() / ref.abs().max() < 1e-5
+    out = C0.clone()
+    gemm_prec(A, B, "fp32", trans_a=True, trans_b=True, beta=2.0, out=out)
+    assert torch.allclose(out, 2.0 * C0 + gemm(A, B, trans_a=True, trans_b=True), atol=1e-4)
