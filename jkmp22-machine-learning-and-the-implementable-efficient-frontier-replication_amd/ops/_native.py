@@ -77,7 +77,8 @@ def hip_lib():
         return _hip
     with _lock:
         if _hip is None:
-            path = _build.HIP_LIB
+            # PFML_HIP_LIB: an alternative build of the kernels (A/B timing of two versions)
+            path = os.environ.get("PFML_HIP_LIB") or _build.HIP_LIB
             if not os.path.exists(path):
                 try:
                     _build.build_hip()
