@@ -264,19 +264,19 @@ _UTIL_PLANS: dict = {}
 
 
 def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell, job_month,
-                    job_n) -> dict:
+                    job_n, split: bool = True) -> dict:
     """Launch plan of ridge_utilities on a device, cached: the descriptors depend only on the
     grid's shape (cells, jobs, P, L), so repeated grid searches (every step of a run, every
     benchmark step) reuse the uploaded device copies and skip all host planning.  Each group's
     cells / jobs write straight into the full beta / obj arrays (global out offsets)."""
-    key = (P, L, str(dev), cell_src.tobytes(), cell_n.tobytes(), cell_scale.tobytes(),
+    key = (P, L, str(dev), split, cell_src.tobytes(), cell_n.tobytes(), cell_scale.tobytes(),
            job_cell.tobytes(), job_month.tobytes(), job_n.tobytes())
     hit = _UTIL_PLANS.get(key)
     if hit is not None:
         return hit
     big = cell_n == cell_n.max()
     groups, arrays = [], []
-    for grp in (big, ~big):
+    for grp in ((big, ~big) if split else (np.ones(len(cell_n), dtype=bool),)):
         cells = np.nonzero(grp)[0]
         jobs = np.nonzero(grp[job_cell])[0]
         rp = ridge_plan(P, L, cell_src[cells], cell_n[cells], cell_scale[cells])
@@ -298,45 +298,52 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
                     job_n) -> tuple[torch.Tensor, torch.Tensor]:
     """(beta, obj) = (ridge_grid(...), quadform_utilities(D, R, beta, jobs)).
 
-    On a device the cells split into the largest-n group and the rest; each group's
-    ridge -> utilities chain is issued on its own HIP stream, the big group first, so the
-    small cells' whole chain runs on the CUs the big cells' one-workgroup-per-cell band
-    reductions leave idle.  Both chains write their rows of beta / obj in place.  Non-SPD
-    repairs (rare) are applied once at the end, and the utilities of repaired cells
-    recomputed.
+    On a device with many big cells (one GPU holds the grid) the cells split into the
+    largest-n group and the rest; each group's ridge -> utilities chain is issued on its own
+    HIP stream, the big group first, so the small cells' whole chain runs on the CUs the big
+    cells' one-workgroup-per-cell band reductions leave idle.  With few (multi-GPU shards) one
+    chain in one stream.  Either way beta / obj rows are written in place from cached launch
+    plans, and the non-SPD check (one host sync) comes after the utilities are queued:
+    repairs (rare) are applied at the end and the utilities of repaired cells recomputed.
     """
     cell_src, cell_n = np.asarray(cell_src), np.asarray(cell_n)
     cell_scale = np.asarray(cell_scale, dtype=np.float64)
     job_cell, job_month, job_n = (np.asarray(job_cell), np.asarray(job_month),
                                   np.asarray(job_n))
     mode, two = band_policy(cell_n)
-    if not nat.is_device(SD) or len(np.unique(cell_n)) < 2 or not two:
+    if not nat.is_device(SD):
         beta = ridge_grid(SD, Sr, cell_src, cell_n, cell_scale, lvec, band_mode=mode)
         return beta, quadform_utilities(D, R, beta, job_cell, job_month, job_n)
+    split = two and len(np.unique(cell_n)) >= 2
     th = _HostClock()
     S, P, _ = SD.shape
     L = int(lvec.numel())
     nc = len(cell_src)
     dev = SD.device
-    plan = _utilities_plan(P, L, dev, cell_src, cell_n, cell_scale, job_cell, job_month, job_n)
+    plan = _utilities_plan(P, L, dev, cell_src, cell_n, cell_scale, job_cell, job_month, job_n,
+                           split=split)
     th("plans")
     beta = torch.zeros((nc, L, P), dtype=SD.dtype, device=dev)
     obj = torch.empty((len(job_cell), L), dtype=SD.dtype, device=dev)
     SD, Sr, D, R = SD.contiguous(), Sr.contiguous(), D.contiguous(), R.contiguous()
     lv = lvec.to(device=dev, dtype=torch.float64).contiguous()
     cur = torch.cuda.current_stream(dev)
-    side = _side_stream(dev)
-    side.wait_stream(cur)
     dv = plan["dv"]
-    for gi, stream in ((0, side), (1, cur)):     # big cells' factorisations issued first
+    streams = [cur]
+    if split:
+        side = _side_stream(dev)
+        side.wait_stream(cur)
+        streams = [side, cur]                    # big cells' factorisations issued first
+    for gi, stream in enumerate(streams):
         _, _, rp, qp = plan["groups"][gi]
         with torch.cuda.stream(stream):
             ridge_launch(rp, dv[3 * gi], SD, Sr, lv, beta, mode)
             quad_launch(qp, dv[3 * gi + 1], dv[3 * gi + 2], D, R, beta, obj)
     th("launch")
-    cur.wait_stream(side)
-    for t in (SD, Sr, D, R, lv, beta, obj):
-        t.record_stream(side)
+    if split:
+        cur.wait_stream(side)
+        for t in (SD, Sr, D, R, lv, beta, obj):
+            t.record_stream(side)
     fixed = repair_nonspd(beta, SD, Sr, cell_src, cell_n, cell_scale, lv)
     th("repair_check")
     if len(fixed):
