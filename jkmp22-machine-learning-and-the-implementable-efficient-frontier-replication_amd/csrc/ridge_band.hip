@@ -169,6 +169,272 @@ __device__ __forceinline__ void band_x_accum(const double* __restrict__ A, int n
   }
 }
 
+// ---- CholeskyQR2 panel factorisation with Householder reconstruction --------------------
+//
+// The column-by-column Householder QR below needs one barrier and a dependent rsq/rcp chain
+// per column (16 per panel, ~60 % of a panel's time at the multi-GPU shard sizes).  When the
+// panel is well conditioned it is factored instead as
+//
+//   P = Q1 R1, Q1 = P R1^-1  (G = P^T P on MFMA, 16x16 Cholesky in registers)   twice
+//   [S; 0] - Q = V U~        (LU without pivoting of the 16x16 top block, S_kk = sign of the
+//                             running pivot so |pivot| >= 1; Ballard et al., "Reconstructing
+//                             Householder vectors from TSQR")
+//   V2 = -Q2 U~^-1,  T = U~ S V1^-T,  R_house = S R2 R1
+//
+// which gives the same compact-WY (V unit lower trapezoidal, T upper) and band block as
+// dgeqrt up to the column signs, in five barriers (opt-in, PFML_BAND_QR=cqr: see the
+// launcher for the measured cost).  Every wave repeats the 16x16 work in
+// registers (lane c16 holds column c16, the 4 row groups redundantly; cross-lane values by
+// row_newbcast DPP), so no barrier distributes the small factors, and the accept/reject tests
+// come out identical in every wave.  A panel is rejected (-> the Householder path) when it
+// has fewer rows than columns, a first-pass pivot loses more than 10 digits relative to its
+// column norm, or the second-pass Gram is more than 1e-2 from the identity (the
+// CholeskyQR2 stability bound kappa(P) < ~1e7).
+template <int R>
+__device__ __forceinline__ double pick4(const double (&x)[BB], int g4) {   // x[4R + g4]
+  return g4 == 0 ? x[4 * R] : (g4 == 1 ? x[4 * R + 1] : (g4 == 2 ? x[4 * R + 2] : x[4 * R + 3]));
+}
+
+// G = P^T P of the BMP x 16 panel in Vs: per-wave MFMA partials -> redf, barrier, then every
+// wave sums the partials of column c16 (lanes g4 take waves g4, g4 + 4; row-group sum).
+__device__ __forceinline__ void cqr_gram(const double (*Vs)[LS], double* redf, int m, int wid,
+                                         int lane, double (&g)[BB]) {
+  const int c16 = lane & 15, g4 = lane >> 4;
+  double4_t acc = {0.0, 0.0, 0.0, 0.0};
+  if (wid * 64 < m) {
+#pragma unroll
+    for (int k = 0; k < 64; k += 4) {
+      const double v = Vs[wid * 64 + k + g4][c16];
+      acc = mfma_f64_16x16x4(v, v, acc);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) redf[wid * 256 + PFML_F64_CROW(lane, r) * BB + c16] = acc[r];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < BB; ++i)
+    g[i] = rowgroup_sum(redf[g4 * 256 + i * BB + c16] + redf[(g4 + 4) * 256 + i * BB + c16]);
+}
+
+// The 16x16 factor routines below accumulate with fmac_bcast<SEL, true> (one volatile
+// v_fmac_f64_dpp behind its own s_nop): as plain expressions the compiler hoists every
+// broadcast of a constant factor entry to the top of the unrolled substitution and spills
+// them, and no ordering of the builtins prevents that.
+
+// Upper Cholesky G = R^T R (lane c16 holds G[:, c16]): rc[i] = R[i][c16], di[i] = 1 / R[i][i].
+// False on a non-positive (or NaN) pivot; a near-dependence that still passes shows up as a
+// second-pass Gram far from the identity.
+__device__ __forceinline__ bool chol16(double (&g)[BB], double (&rc)[BB], double (&di)[BB],
+                                       int c16) {
+  bool ok = true;
+  static_for<0, BB>([&](auto K) {
+    constexpr int k = decltype(K)::value;
+    const double d = row_bcast<k>(g[k]);
+    ok = ok && (d > 0.0);
+    const double rinv = rsqrt_f64(ok ? d : 1.0);
+    const double rk = (c16 >= k) ? g[k] * rinv : 0.0;
+    const double nrk = -rk;
+    rc[k] = rk;
+    di[k] = rinv;
+    static_for<k + 1, BB>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      fmac_bcast<i, true>(g[i], rk, nrk);          // G[i][c16] -= R[k][i] R[k][c16]
+    });
+  });
+  return ok;
+}
+
+// X = U^-1 for upper U given by columns (lane c16: uc[i] = U[i][c16]) and di[i] = 1 / U[i][i];
+// x[i] = X[i][c16].  Only entries above the diagonal of uc are read.
+__device__ __forceinline__ void triu_inv16(const double (&uc)[BB], const double (&di)[BB],
+                                           double (&x)[BB], int c16) {
+  // right-looking: row k of X is final once the rows below it are; its update of the rows
+  // above is 16 independent accumulations (back-to-back FMAs, no dependent chain)
+  double acc[BB];
+#pragma unroll
+  for (int i = 0; i < BB; ++i) acc[i] = 0.0;
+  static_for<0, BB>([&](auto KK) {
+    constexpr int k = BB - 1 - decltype(KK)::value;
+    x[k] = ((c16 == k) ? 1.0 + acc[k] : acc[k]) * di[k];
+    const double nxk = -x[k];
+    static_for<0, k>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      fmac_bcast<k, true>(acc[i], uc[i], nxk);     // acc[i] -= U[i][k] X[k][c16]
+    });
+  });
+}
+
+// Vs[rows] <- sign * Vs[rows] X for the row blocks [16 b0, m) this wave owns (X by columns,
+// in place: a wave reads a block's 16 rows before it writes them).  When `Aout` is set the
+// result rows also go to the panel columns of A (rows i < m).
+__device__ __forceinline__ void cqr_apply(double (*Vs)[LS], const double (&x)[BB], int m, int wid,
+                                          int lane, int b0, double sign, double* Aout = nullptr,
+                                          int n = 0) {
+  const int c16 = lane & 15, g4 = lane >> 4;
+  double b[4];
+  b[0] = pick4<0>(x, g4);
+  b[1] = pick4<1>(x, g4);
+  b[2] = pick4<2>(x, g4);
+  b[3] = pick4<3>(x, g4);
+#pragma unroll
+  for (int q = 0; q < BMP / 16 / NWR; ++q) {
+    const int blk = wid + NWR * q, i0 = blk * 16;
+    if (blk < b0 || i0 >= m) continue;
+    double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vs[i0 + c16][4 * r + g4], b[r], acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + PFML_F64_CROW(lane, r);
+      Vs[i][c16] = sign * acc[r];
+      if (Aout != nullptr && i < m) Aout[(int64_t)i * n + c16] = sign * acc[r];
+    }
+  }
+}
+
+__device__ __forceinline__ bool band_panel_cqr(double* __restrict__ A, int n, int k0, int r0,
+                                               int m, double (*Vs)[LS], double* redf,
+                                               double (*Ts)[LS], double* __restrict__ Tglob,
+                                               long long* tk) {
+  if (m < BB) return false;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int c16 = lane & 15, g4 = lane >> 4;
+  // ---- P = rows k0..k0+15, columns r0.. of the symmetric A, transposed into Vs (32 lanes
+  //      per row: 256 B contiguous per load); rows >= m are zero
+  {
+    const int c = t >> 5, il = t & 31;
+    const double* src = A + (int64_t)(k0 + c) * n + r0;
+    double a[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = il + 32 * q;
+      a[q] = (i < m) ? src[i] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) Vs[il + 32 * q][c] = a[q];
+  }
+  __syncthreads();
+  if (tk) tk[0] = (long long)__builtin_amdgcn_s_memtime();
+  // ---- pass 1: G = P^T P, R1, Q1 = P R1^-1
+  double g[BB], rc1[BB], di[BB], x[BB];
+  cqr_gram(Vs, redf, m, wid, lane, g);
+  if (!chol16(g, rc1, di, c16)) {
+    __syncthreads();   // every wave is past its redf reads before the fallback reuses redf
+    return false;
+  }
+  triu_inv16(rc1, di, x, c16);
+  cqr_apply(Vs, x, m, wid, lane, 0, 1.0);
+  __syncthreads();
+  // ---- pass 2: G2 = Q1^T Q1 (~ I), R2, Q = Q1 R2^-1
+  double rc2[BB];
+  cqr_gram(Vs, redf, m, wid, lane, g);
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < BB; ++i) bad = bad || !(fabs(g[i] - (i == c16 ? 1.0 : 0.0)) < 1e-2);
+  bad = __any(bad);
+  if (bad || !chol16(g, rc2, di, c16)) {
+    __syncthreads();
+    return false;
+  }
+  triu_inv16(rc2, di, x, c16);
+  cqr_apply(Vs, x, m, wid, lane, 0, 1.0);
+  // R = R2 R1 (lane c16: rf[i] = R[i][c16])
+  double rf[BB];
+#pragma unroll
+  for (int i = 0; i < BB; ++i) rf[i] = 0.0;
+  static_for<0, BB>([&](auto K) {
+    constexpr int k = decltype(K)::value;
+    static_for<0, k + 1>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      fmac_bcast<k, true>(rf[i], rc2[i], rc1[k]);  // += R2[i][k] R1[k][c16]
+    });
+  });
+  if (wid == 0 && g4 == 0) {   // R parked in Ts until the band block is written
+#pragma unroll
+    for (int i = 0; i < BB; ++i) Ts[i][c16] = rf[i];
+  }
+  __syncthreads();
+  // ---- Householder reconstruction: LU of [S; 0] - Q (top block in registers)
+  double mm[BB];
+  unsigned neg = 0;                               // bit k set: S_kk = -1
+#pragma unroll
+  for (int i = 0; i < BB; ++i) mm[i] = -Vs[i][c16];
+  static_for<0, BB>([&](auto K) {
+    constexpr int k = decltype(K)::value;
+    const double d = row_bcast<k>(mm[k]);
+    const double s = (d >= 0.0) ? 1.0 : -1.0;
+    const double piv = d + s;                     // |piv| >= 1
+    const double pinv = rcp_f64(piv);
+    neg |= (d >= 0.0) ? 0u : (1u << k);
+    di[k] = pinv;
+    if (c16 == k) mm[k] = piv;
+    static_for<k + 1, BB>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      if (c16 == k) mm[i] *= pinv;                // L[i][k]
+    });
+    const double nuk = -mm[k];                    // -U~[k][c16]
+    static_for<k + 1, BB>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      double u = mm[i];
+      fmac_bcast<k, true>(u, mm[i], nuk);          // M[i][c16] -= L[i][k] U~[k][c16]
+      if (c16 > k) mm[i] = u;
+    });
+  });
+  // U~^-1 (x), V1^-1 (w: unit lower, forward substitution)
+  triu_inv16(mm, di, x, c16);
+  double w[BB];
+#pragma unroll
+  for (int i = 0; i < BB; ++i) w[i] = 0.0;
+  static_for<0, BB>([&](auto K) {                // right-looking forward substitution
+    constexpr int k = decltype(K)::value;
+    if (c16 == k) w[k] += 1.0;
+    const double nwk = -w[k];
+    static_for<k + 1, BB>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      fmac_bcast<k, true>(w[i], mm[i], nwk);       // W[i][c16] -= L[i][k] W[k][c16]
+    });
+  });
+  // V2 = -Q2 U~^-1 -> Vs rows >= 16 and A's panel columns
+  cqr_apply(Vs, x, m, wid, lane, 1, -1.0, A + (int64_t)r0 * n + k0, n);
+  // T = U~ S V1^-T: W^T through a wave-private LDS image (lane c16 needs row c16 of W)
+  double* wt = redf + wid * 256;
+  if (g4 == 0) {
+#pragma unroll
+    for (int i = 0; i < BB; ++i) wt[i * BB + c16] = w[i];
+  }
+  double wr[BB];                                  // (S W^T)[k][c16] = S_kk W[c16][k]
+#pragma unroll
+  for (int k = 0; k < BB; ++k) {
+    const double v = wt[c16 * BB + k];
+    wr[k] = ((neg >> k) & 1u) ? -v : v;
+  }
+  double tcol[BB];
+#pragma unroll
+  for (int i = 0; i < BB; ++i) tcol[i] = 0.0;
+  static_for<0, BB>([&](auto K) {
+    constexpr int k = decltype(K)::value;
+    static_for<0, k + 1>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      fmac_bcast<k, true>(tcol[i], mm[i], wr[k]);  // += U~[i][k] (S W^T)[k][c16]
+    });
+  });
+  __syncthreads();   // every wave has read the top block of Q
+  if (wid == 0 && g4 == 0) {
+#pragma unroll
+    for (int i = 0; i < BB; ++i) {
+      const double ri = ((neg >> i) & 1u) ? -Ts[i][c16] : Ts[i][c16];   // (S R)[i][c16]
+      Vs[i][c16] = (i > c16) ? mm[i] : (i == c16 ? 1.0 : 0.0);
+      A[(int64_t)(r0 + i) * n + k0 + c16] = (i > c16) ? mm[i] : ri;
+      Ts[i][c16] = tcol[i];
+      Tglob[i * BB + c16] = tcol[i];
+    }
+  }
+  __syncthreads();
+  if (tk) tk[1] = (long long)__builtin_amdgcn_s_memtime();
+  return true;
+}
+
 // P1 + P2 + T of one panel, by one NTR-thread workgroup: the m x 16 panel below the band
 // (columns r0.. of rows k0..k0+15 of the symmetric A) is QR-factored by Householder in
 // registers; V (unit lower trapezoid) -> Vs, V and R -> A's panel columns, the compact-WY T
@@ -176,8 +442,9 @@ __device__ __forceinline__ void band_x_accum(const double* __restrict__ A, int n
 __device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n, int k0, int r0,
                                                   int m, double (*Vs)[LS], double (*Gs)[LS],
                                                   double* redf, double (*Ts)[LS], double* taus,
-                                                  double* __restrict__ Tglob,
+                                                  double* __restrict__ Tglob, bool qr_fast,
                                                   long long* tk = nullptr) {
+  if (qr_fast && band_panel_cqr(A, n, k0, r0, m, Vs, redf, Ts, Tglob, tk)) return;
   const int t = threadIdx.x, lane = t & 63;
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
   const int cq = t & 15, rg = t >> 4;
@@ -309,6 +576,7 @@ __device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n,
   if (t < BB * BB) Tglob[t] = Ts[t / BB][t % BB];
 }
 
+template <bool qr_fast>
 __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
     const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
     const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work,
@@ -351,7 +619,8 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
   if (tim != nullptr && threadIdx.x == 0) tlast = (long long)__builtin_amdgcn_s_memtime();
   for (int k0 = 0; k0 + BB < n; k0 += BB) {
     const int r0 = k0 + BB, m = n - r0, p = k0 / BB;
-    band_panel_factor(A, n, k0, r0, m, Vs, Ws, &red[0][0], Ts, taus, bw.T + (int64_t)p * BB * BB);
+    band_panel_factor(A, n, k0, r0, m, Vs, Ws, &red[0][0], Ts, taus, bw.T + (int64_t)p * BB * BB,
+                      qr_fast);
     BAND_TMARK(1)
     // ---- U = V T -> Ws  (MFMA, all 32 row blocks so rows >= m read back as zero)
 #pragma unroll
@@ -577,6 +846,7 @@ __global__ __launch_bounds__(256) void band_mk_init_kernel(
     for (int i = threadIdx.x; i < n; i += 256) bw.z[i] = Sr[cd.rsrc + i] * sc;
 }
 
+template <bool qr_fast>
 __global__ __launch_bounds__(NTR) void band_mk_panel_kernel(
     const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work, int p,
     long long* __restrict__ tim) {
@@ -598,7 +868,7 @@ __global__ __launch_bounds__(NTR) void band_mk_panel_kernel(
   long long tk[6];
   if (timed) tk[5] = (long long)__builtin_amdgcn_s_memtime();
   band_panel_factor(A, n, k0, r0, m, Vs, Gs, &red[0][0], Ts, taus, bw.T + (int64_t)p * BB * BB,
-                    timed ? tk : nullptr);
+                    qr_fast, timed ? tk : nullptr);
   if (timed) tk[2] = (long long)__builtin_amdgcn_s_memtime();
   // U = V T -> Ug, V -> Vg (all BMP rows: rows >= m are zero)
 #pragma unroll
@@ -1078,9 +1348,20 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   const bool env_multi = mode && mode[0] == 'm';
   const bool single = band_mode == 1 || (band_mode == 0 && mode && mode[0] == 's') ||
                       (tim != nullptr && band_mode == 0 && !env_multi);
+  // panel QR: column-by-column Householder (default), or PFML_BAND_QR=cqr: CholeskyQR2 +
+  // Householder reconstruction with a per-panel fallback to Householder.  Measured on MI355X
+  // the CholeskyQR2 form is 6-10 % slower per reduction (profiles/r01_band_qr_ab.json): its
+  // 48 sequential 16x16 pivot steps (two Cholesky, one LU) cost more latency than the 16
+  // barrier-separated Householder columns they replace.
+  const char* qenv = getenv("PFML_BAND_QR");
+  const int qr_fast = (qenv && qenv[0] == 'c') ? 1 : 0;
   if (single) {
-    hipLaunchKernelGGL(ridge_band_reduce_kernel, dim3(ncells), dim3(NTR), 0, st, SD, ldS, Sr, cd,
-                       L, work, tim);
+    if (qr_fast)
+      hipLaunchKernelGGL(ridge_band_reduce_kernel<true>, dim3(ncells), dim3(NTR), 0, st, SD, ldS,
+                         Sr, cd, L, work, tim);
+    else
+      hipLaunchKernelGGL(ridge_band_reduce_kernel<false>, dim3(ncells), dim3(NTR), 0, st, SD, ldS,
+                         Sr, cd, L, work, tim);
   } else {
     const int npan = (nmax - 1) / BB;
     hipLaunchKernelGGL(band_mk_init_kernel, dim3(ncells * MK_INIT_WG), dim3(256), 0, st, SD, ldS,
@@ -1090,8 +1371,12 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
       const int nxb = (mmax + MK_XR - 1) / MK_XR;
       const int tt = (mmax + MK_TS - 1) / MK_TS;
       const int ntile = tt * (tt + 1) / 2;
-      hipLaunchKernelGGL(band_mk_panel_kernel, dim3(ncells), dim3(NTR), 0, st, cd, L, work, p,
-                         tim);
+      if (qr_fast)
+        hipLaunchKernelGGL(band_mk_panel_kernel<true>, dim3(ncells), dim3(NTR), 0, st, cd, L,
+                           work, p, tim);
+      else
+        hipLaunchKernelGGL(band_mk_panel_kernel<false>, dim3(ncells), dim3(NTR), 0, st, cd, L,
+                           work, p, tim);
       hipLaunchKernelGGL(band_mk_x_kernel, dim3(ncells * nxb), dim3(256), 0, st, cd, L, work, p,
                          nxb);
       hipLaunchKernelGGL(band_mk_trail_kernel, dim3(ncells * ntile), dim3(256), 0, st, cd, L,

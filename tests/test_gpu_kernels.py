@@ -184,6 +184,30 @@ def test_band_reduction_modes(gpu, mode, monkeypatch):
     assert rel < 1e-8, rel
 
 
+@pytest.mark.parametrize("qr", ["cqr", "householder"])
+@pytest.mark.parametrize("mode", ["single", "multi"])
+@pytest.mark.parametrize("n_obs", [700, 90])
+def test_band_panel_qr(gpu, qr, mode, n_obs, monkeypatch):
+    """Panel QR of the band reduction: the column-by-column Householder QR (default) and the
+    opt-in CholeskyQR2 + Householder reconstruction give the LU-solve oracle's ridge solutions.  With
+    n_obs = 90 every window sum has rank 90 < n, so the trailing panels are rank-deficient and
+    the CholeskyQR2 path must hand them to the Householder fallback."""
+    from pfml.ops.ridge import ridge_grid
+    monkeypatch.setenv("PFML_BAND_MODE", mode)
+    monkeypatch.setenv("PFML_BAND_QR", qr)
+    P = 513
+    SD = _spd_stack(2, P, n_obs=n_obs, seed=63)
+    Sr = _rand(2, P, seed=64)
+    lam = np.exp(np.linspace(-10, 10, 100)) if n_obs > P else np.exp(np.linspace(-2, 10, 40))
+    lv = torch.tensor(list(lam), dtype=torch.float64)
+    src, nn = np.array([0, 1, 0, 1]), np.array([513, 513, 257, 100])
+    sc = np.full(len(src), 1.5e-3)
+    ref = ridge_grid(SD, Sr, src, nn, sc, lv)
+    out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
+    rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
+    assert rel < 1e-8, rel
+
+
 @pytest.mark.parametrize("fmt", ["bf16", "fp8"])
 @pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True)])
 def test_gemm_lowp(gpu, fmt, ta, tb):
