@@ -1,56 +1,165 @@
-// Batched, strided fp64 GEMM on CDNA4 matrix cores (v_mfma_f64_16x16x4_f64).
+// Batched, strided fp64 GEMM on CDNA4 matrix cores (v_mfma_f64_16x16x4_f64) with the
+// prologue / epilogue fusions of the PFML input stage:
 //
-//   C[b] = alpha * diag(rs[b]) * op(A[b]) * op(B[b]) * diag(cs[b]) + beta * C[b]
+//   C[b] = alpha * diag(rs) * op(A) * diag(ks) * op(B) * diag(cs) + beta * C[b]
+//          + E[b][:, :e_cols]                       (addend block, e.g. S_theta)
+//          + diag(dv or dval) on columns diag_col0..  (identity / idiosyncratic variance)
 //
-// This is the workhorse of the PFML engine: the reference
-// runs every one of these products as an OpenBLAS dgemm, often with a dense diagonal matrix
-// as one operand (`m @ np.diag(gt)`, `np.diag(1/vol) @ s`, ...).  Here the diagonal factors
-// are fused as row/column scales of the epilogue, so they cost O(MN) instead of a GEMM.
+// The reference runs every one of these as an OpenBLAS dgemm, often with a dense diagonal
+// matrix as an operand (`m @ np.diag(gt)`, `np.diag(1/vol) @ s`, PFML_Input_Data.py:386-459)
+// plus separate additions; here the diagonal factors are applied while the tile is staged
+// (ks) or in the epilogue, so the Horner step of (24)
+//     T_theta = [S_theta | I] + m diag(D_theta) T_{theta+1}
+// is ONE launch that reads m, D_theta, T_{theta+1} and S_theta once and writes T_theta once.
 //
-// Tiling: BM x BN output tile per 256-thread workgroup (4 waves, 2 x 2), BK = 16 staged in
-// LDS.  Each operand keeps the layout it has in global memory, so the LDS stores are as
-// conflict-free as the coalesced global loads: an operand contiguous along k (A not
-// transposed, B transposed) is stored [row][k] with a row stride of 18 doubles (the 16 rows x
-// 2 k of one ds_read_b64 group then hit 32 distinct bank pairs), one contiguous along its
-// row/column index is stored [k][index] with a 16-double pad (stride = 32 banks mod 64).
-// Each wave owns a (BM/2) x (BN/2) sub-tile = (BM/32) x (BN/32) MFMA 16x16 accumulators.
-// Double-buffered LDS: the global loads of K-step t+1 are issued into registers before the
-// MFMAs of step t.
+// Tiling: BM x BN output tile per 256-thread workgroup (4 waves as 2 x 2), each wave a
+// (BM/2) x (BN/2) block of 16 x 16 MFMA accumulators; BK = 16 staged per step.
+//  * Global -> registers with 16-byte (2 x fp64) loads along each operand's contiguous
+//    dimension (W = 2; W = 1 for odd leading dimensions), clamped unconditional addresses
+//    (no per-element branches), issued for step s+1 before the MFMAs of step s.
+//  * LDS keeps each operand in its global orientation: k-contiguous operands as [idx][k] with a
+//    row stride of BK + 2 doubles (the 16 rows x 2 k of a ds_read_b64 half-wave hit 32
+//    distinct bank pairs), index-contiguous ones as [k][idx] with a +16 pad (2 k-rows land on
+//    opposite bank halves).  Both conflict-free for the MFMA fragment reads, 16-B aligned for
+//    ds_write_b128.  Two buffers, one barrier per K-step.
+//  * 1-D grid over (matrix, tile) with the bijective XCD remap (common.h): the tiles of one
+//    matrix run on one XCD and share its L2 (A row panels / B column panels).
 #include "common.h"
+#include <type_traits>
 
 namespace {
 
 constexpr int BK = 16;
-constexpr int PAD = 16;      // [k][index] layouts
-constexpr int KS = BK + 2;   // [index][k] layouts: row stride in doubles
+constexpr int KS = BK + 2;       // [idx][k] row stride (doubles)
 
-template <bool TA, bool TB, int BM, int BN>
-__global__ __launch_bounds__(256) void dgemm_kernel(
-    int M, int N, int K, double alpha,
+struct Epi {
+  double alpha, beta;
+  const double* rs; int64_t srs;      // row scale
+  const double* cs; int64_t scs;      // column scale
+  const double* ks; int64_t sks;      // k scale (between op(A) and op(B))
+  const double* E; int64_t lde, sE;   // addend on columns [0, e_cols)
+  int e_cols;
+  int diag_col0;                      // diagonal add: column j == diag_col0 + row i
+  double dval;                        //   value (when dv == nullptr)
+  const double* dv; int64_t sdv;      //   or per-row vector
+  int has_diag;
+  const double* es; int64_t ses;      // addend row scale (null: 1)
+};
+
+typedef double double2_t __attribute__((ext_vector_type(2)));
+
+template <int W> struct Ld;
+template <> struct Ld<1> {
+  using T = double;
+  static __device__ __forceinline__ T load(const double* p) { return *p; }
+  static __device__ __forceinline__ void store(double* p, T v) { *p = v; }
+  static __device__ __forceinline__ double get(T v, int) { return v; }
+  static __device__ __forceinline__ void set(T& v, int, double x) { v = x; }
+  static __device__ __forceinline__ T zero() { return 0.0; }
+};
+template <> struct Ld<2> {
+  using T = double2_t;
+  static __device__ __forceinline__ T load(const double* p) {
+    return *reinterpret_cast<const double2_t*>(p);
+  }
+  static __device__ __forceinline__ void store(double* p, T v) {
+    *reinterpret_cast<double2_t*>(p) = v;
+  }
+  static __device__ __forceinline__ double get(T v, int e) { return e ? v.y : v.x; }
+  static __device__ __forceinline__ void set(T& v, int e, double x) { if (e) v.y = x; else v.x = x; }
+  static __device__ __forceinline__ T zero() { return double2_t{0.0, 0.0}; }
+};
+
+// One operand tile of R (= BM or BN) indices x BK k-values.
+//   KCONTIG: global element (idx, k) at base[(r0 + idx) * ld + k0 + k], LDS [idx][k] (stride KS)
+//   else   : global element (idx, k) at base[(k0 + k) * ld + r0 + idx], LDS [k][idx] (R + 16)
+// load() only issues the (clamped, always valid) global loads; the bounds mask and the k-scale
+// are applied in store(), after the MFMAs of the current step, so nothing consumes a load
+// result early and the compiler keeps the whole next tile in flight across the MFMA block.
+template <int R, bool KCONTIG, int W>
+struct Operand {
+  static constexpr int S = R + 16;
+  static constexpr int SIZE = KCONTIG ? R * KS : BK * S;
+  static constexpr int NV = R * BK / W / 256;       // vector loads per thread
+  static_assert(NV >= 1, "tile too small for 256 threads");
+  using L = Ld<W>;
+  typename L::T v[NV];
+  // k-scale values of the staged step: W consecutive k (KCONTIG) or one k per load
+  typename std::conditional<KCONTIG, typename L::T, double>::type sc[NV];
+  const double* p[NV];                              // row / column base of each load
+  bool rowok[NV];
+
+  static __device__ __forceinline__ void coords(int e, int& idx, int& k) {
+    if (KCONTIG) { idx = e / (BK / W); k = (e % (BK / W)) * W; }
+    else         { k = e / (R / W); idx = (e % (R / W)) * W; }
+  }
+  __device__ __forceinline__ void init(const double* __restrict__ base, int64_t ld, int r0,
+                                       int rmax, int t) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      int idx, k;
+      coords(t + q * 256, idx, k);
+      const int gi = r0 + idx;
+      rowok[q] = gi < rmax;
+      const int ci = rowok[q] ? gi : rmax - W;       // W-aligned chunks: in or out entirely
+      p[q] = KCONTIG ? base + (int64_t)ci * ld : base + ci;
+    }
+  }
+  template <bool KSC>
+  __device__ __forceinline__ void load(int64_t ld, int k0, int kmax, const double* ks, int t) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      int idx, k;
+      coords(t + q * 256, idx, k);
+      const int ck = min(k0 + k, kmax - (KCONTIG ? W : 1));
+      v[q] = L::load(KCONTIG ? p[q] + ck : p[q] + (int64_t)ck * ld);
+      if constexpr (KSC) {
+        if constexpr (KCONTIG) sc[q] = L::load(ks + ck);     // W consecutive k (16-B aligned)
+        else sc[q] = ks[ck];
+      }
+    }
+  }
+  template <bool KSC>
+  __device__ __forceinline__ void store(double* __restrict__ lds, int k0, int kmax, int t) {
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      int idx, k;
+      coords(t + q * 256, idx, k);
+      const bool ok = rowok[q] && (k0 + k < kmax);
+      typename L::T x = v[q];
+      if constexpr (KSC) x = x * sc[q];
+      L::store(lds + (KCONTIG ? idx * KS + k : k * S + idx), ok ? x : L::zero());
+    }
+  }
+  static __device__ __forceinline__ double frag(const double* __restrict__ lds, int idx, int k) {
+    return lds[KCONTIG ? idx * KS + k : k * S + idx];
+  }
+};
+
+template <bool TA, bool TB, int BM, int BN, int W, bool KSC>
+__global__ __launch_bounds__(256, 2) void dgemm_kernel(
+    int M, int N, int K, int tiles_m, int tiles_n, int nwg,
     const double* __restrict__ A, int64_t lda, int64_t sA,
     const double* __restrict__ B, int64_t ldb, int64_t sB,
-    double beta, double* __restrict__ C, int64_t ldc, int64_t sC,
-    const double* __restrict__ rs, int64_t srs,
-    const double* __restrict__ cs, int64_t scs) {
-  constexpr int TM = BM / 32, TN = BN / 32;         // MFMA tiles per wave (M, N)
-  constexpr int LA = BM * BK / 256, LB = BN * BK / 256;  // elements loaded per thread
-  // A: TA ? [k][i] : [i][k];  B: TB ? [j][k] : [k][j]   (flat, see the header)
-  constexpr int ASZ = TA ? BK * (BM + PAD) : BM * KS;
-  constexpr int BSZ = TB ? BN * KS : BK * (BN + PAD);
-  __shared__ double As[2][ASZ];
-  __shared__ double Bs[2][BSZ];
-  auto aidx = [](int i, int k) { return TA ? k * (BM + PAD) + i : i * KS + k; };
-  auto bidx = [](int k, int j) { return TB ? j * KS + k : k * (BN + PAD) + j; };
+    double* __restrict__ C, int64_t ldc, int64_t sC, Epi ep) {
+  constexpr int TM = BM / 32, TN = BN / 32;         // 16x16 accumulators per wave (M, N)
+  using OA = Operand<BM, !TA, W>;                   // A stored M x K: contiguous along k
+  using OB = Operand<BN, TB, W>;                    // B stored N x K (TB): contiguous along k
+  __shared__ double As[2][OA::SIZE];
+  __shared__ double Bs[2][OB::SIZE];
 
-  const int b = blockIdx.y;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int tiles = tiles_m * tiles_n;
+  const int b = wg / tiles;
+  const int tile = wg - b * tiles;
+  const int bm = (tile % tiles_m) * BM, bn = (tile / tiles_m) * BN;
   A += (int64_t)b * sA;
   B += (int64_t)b * sB;
   C += (int64_t)b * sC;
-  const int tiles_n = (N + BN - 1) / BN;
-  const int tile = blockIdx.x;
-  const int bm = (tile / tiles_n) * BM, bn = (tile % tiles_n) * BN;
+  const double* ks = ep.ks ? ep.ks + (int64_t)b * ep.sks : nullptr;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int wm = w >> 1, wn = w & 1;
+  const int li = lane & 15, lk = lane >> 4;
 
   double4_t acc[TM][TN];
 #pragma unroll
@@ -58,74 +167,49 @@ __global__ __launch_bounds__(256) void dgemm_kernel(
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = double4_t{0.0, 0.0, 0.0, 0.0};
 
-  double ra[LA], rb[LB];
-  // global -> registers for the K-step starting at k0
-  auto load = [&](int k0) {
-#pragma unroll
-    for (int q = 0; q < LA; ++q) {
-      const int e = t + q * 256;
-      int i, k;
-      if (TA) { k = e / BM; i = e % BM; }            // A stored K x M: contiguous along i
-      else    { i = e / BK; k = e % BK; }            // A stored M x K: contiguous along k
-      const int gi = bm + i, gk = k0 + k;
-      double v = 0.0;
-      if (gi < M && gk < K) v = TA ? A[(int64_t)gk * lda + gi] : A[(int64_t)gi * lda + gk];
-      ra[q] = v;
-    }
-#pragma unroll
-    for (int q = 0; q < LB; ++q) {
-      const int e = t + q * 256;
-      int j, k;
-      if (TB) { j = e / BK; k = e % BK; }            // B stored N x K: contiguous along k
-      else    { k = e / BN; j = e % BN; }            // B stored K x N: contiguous along j
-      const int gj = bn + j, gk = k0 + k;
-      double v = 0.0;
-      if (gj < N && gk < K) v = TB ? B[(int64_t)gj * ldb + gk] : B[(int64_t)gk * ldb + gj];
-      rb[q] = v;
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int q = 0; q < LA; ++q) {
-      const int e = t + q * 256;
-      int i, k;
-      if (TA) { k = e / BM; i = e % BM; } else { i = e / BK; k = e % BK; }
-      As[buf][aidx(i, k)] = ra[q];
-    }
-#pragma unroll
-    for (int q = 0; q < LB; ++q) {
-      const int e = t + q * 256;
-      int j, k;
-      if (TB) { j = e / BK; k = e % BK; } else { k = e / BN; j = e % BN; }
-      Bs[buf][bidx(k, j)] = rb[q];
-    }
-  };
-
+  OA ra;
+  OB rb;
   const int nk = (K + BK - 1) / BK;
-  load(0);
-  store(0);
+  ra.init(A, lda, bm, M, t);
+  rb.init(B, ldb, bn, N, t);
+  ra.template load<false>(lda, 0, K, nullptr, t);
+  rb.template load<KSC>(ldb, 0, K, ks, t);
+  ra.template store<false>(As[0], 0, K, t);
+  rb.template store<KSC>(Bs[0], 0, K, t);
   __syncthreads();
   for (int s = 0; s < nk; ++s) {
     const int cur = s & 1;
-    if (s + 1 < nk) load((s + 1) * BK);
+    const bool more = s + 1 < nk;
+    if (more) {
+      ra.template load<false>(lda, (s + 1) * BK, K, nullptr, t);
+      rb.template load<KSC>(ldb, (s + 1) * BK, K, ks, t);
+    }
+    const double* as = As[cur];
+    const double* bs = Bs[cur];
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 4) {
       double a[TM], bb[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = As[cur][aidx(wm * (BM / 2) + i * 16 + (lane & 15), kk + (lane >> 4))];
+      for (int i = 0; i < TM; ++i) a[i] = OA::frag(as, wm * (BM / 2) + i * 16 + li, kk + lk);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bb[j] = Bs[cur][bidx(kk + (lane >> 4), wn * (BN / 2) + j * 16 + (lane & 15))];
+      for (int j = 0; j < TN; ++j) bb[j] = OB::frag(bs, wn * (BN / 2) + j * 16 + li, kk + lk);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f64_16x16x4(a[i], bb[j], acc[i][j]);
     }
-    if (s + 1 < nk) store(cur ^ 1);
+    if (more) {
+      ra.template store<false>(As[cur ^ 1], (s + 1) * BK, K, t);
+      rb.template store<KSC>(Bs[cur ^ 1], (s + 1) * BK, K, t);
+    }
     __syncthreads();
   }
 
-  const double* rsb = rs ? rs + (int64_t)b * srs : nullptr;
-  const double* csb = cs ? cs + (int64_t)b * scs : nullptr;
+  const double* rsb = ep.rs ? ep.rs + (int64_t)b * ep.srs : nullptr;
+  const double* csb = ep.cs ? ep.cs + (int64_t)b * ep.scs : nullptr;
+  const double* Eb = ep.E ? ep.E + (int64_t)b * ep.sE : nullptr;
+  const double* dvb = ep.dv ? ep.dv + (int64_t)b * ep.sdv : nullptr;
+  const double* esb = ep.es ? ep.es + (int64_t)b * ep.ses : nullptr;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -133,52 +217,115 @@ __global__ __launch_bounds__(256) void dgemm_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int gi = bm + wm * (BM / 2) + i * 16 + PFML_F64_CROW(lane, r);
-        const int gj = bn + wn * (BN / 2) + j * 16 + (lane & 15);
+        const int gj = bn + wn * (BN / 2) + j * 16 + li;
         if (gi < M && gj < N) {
-          double v = alpha * acc[i][j][r];
+          double v = ep.alpha * acc[i][j][r];
           if (rsb) v *= rsb[gi];
           if (csb) v *= csb[gj];
           double* cp = C + (int64_t)gi * ldc + gj;
-          if (beta != 0.0) v += beta * (*cp);
+          if (ep.beta != 0.0) v += ep.beta * (*cp);
+          if (Eb && gj < ep.e_cols) v += (esb ? esb[gi] : 1.0) * Eb[(int64_t)gi * ep.lde + gj];
+          if (ep.has_diag && gj - ep.diag_col0 == gi) v += dvb ? dvb[gi] : ep.dval;
           *cp = v;
         }
       }
 }
 
-template <int BM, int BN>
-hipError_t launch(int ta, int tb, int M, int N, int K, int batch, double alpha,
-                  const double* A, int64_t lda, int64_t sA, const double* B, int64_t ldb,
-                  int64_t sB, double beta, double* C, int64_t ldc, int64_t sC,
-                  const double* rs, int64_t srs, const double* cs, int64_t scs,
-                  hipStream_t st) {
-  dim3 grid(((M + BM - 1) / BM) * ((N + BN - 1) / BN), batch);
-  dim3 block(256);
-#define PFML_GEMM_CASE(TA_, TB_)                                                            \
-  hipLaunchKernelGGL((dgemm_kernel<TA_, TB_, BM, BN>), grid, block, 0, st, M, N, K, alpha, A, \
-                     lda, sA, B, ldb, sB, beta, C, ldc, sC, rs, srs, cs, scs)
-  if (!ta && !tb) PFML_GEMM_CASE(false, false);
-  else if (!ta && tb) PFML_GEMM_CASE(false, true);
-  else if (ta && !tb) PFML_GEMM_CASE(true, false);
-  else PFML_GEMM_CASE(true, true);
+template <int BM, int BN, int W>
+hipError_t launch(int ta, int tb, int M, int N, int K, int batch, const double* A, int64_t lda,
+                  int64_t sA, const double* B, int64_t ldb, int64_t sB, double* C, int64_t ldc,
+                  int64_t sC, const Epi& ep, hipStream_t st) {
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  const long nwg = (long)tm * tn * batch;
+  if (nwg > 0x7fffffffL) return hipErrorInvalidValue;
+#define PFML_GEMM_CASE(TA_, TB_, KS_)                                                       \
+  hipLaunchKernelGGL((dgemm_kernel<TA_, TB_, BM, BN, W, KS_>), dim3((unsigned)nwg), dim3(256),  \
+                     0, st, M, N, K, tm, tn, (int)nwg, A, lda, sA, B, ldb, sB, C, ldc, sC, ep)
+  const bool ksc = ep.ks != nullptr;
+  if (ksc) {
+    if (!ta && !tb) PFML_GEMM_CASE(false, false, true);
+    else if (!ta && tb) PFML_GEMM_CASE(false, true, true);
+    else if (ta && !tb) PFML_GEMM_CASE(true, false, true);
+    else PFML_GEMM_CASE(true, true, true);
+  } else {
+    if (!ta && !tb) PFML_GEMM_CASE(false, false, false);
+    else if (!ta && tb) PFML_GEMM_CASE(false, true, false);
+    else if (ta && !tb) PFML_GEMM_CASE(true, false, false);
+    else PFML_GEMM_CASE(true, true, false);
+  }
 #undef PFML_GEMM_CASE
   return hipGetLastError();
 }
 
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+template <int BM, int BN>
+hipError_t launch_w(int ta, int tb, int M, int N, int K, int batch, const double* A, int64_t lda,
+                    int64_t sA, const double* B, int64_t ldb, int64_t sB, double* C,
+                    int64_t ldc, int64_t sC, const Epi& ep, hipStream_t st) {
+  // 16-byte staging needs every contiguous dimension, leading dimension, batch stride and
+  // base pointer even / 16-B aligned (the S4 buffers are padded to make this so)
+  const int a_cont = ta ? M : K, b_cont = tb ? K : N;
+  const bool vec = (a_cont % 2 == 0) && (b_cont % 2 == 0) && (lda % 2 == 0) && (ldb % 2 == 0) &&
+                   (sA % 2 == 0) && (sB % 2 == 0) && aligned16(A) && aligned16(B) &&
+                   (!ep.ks || (aligned16(ep.ks) && ep.sks % 2 == 0));
+  if (vec)
+    return launch<BM, BN, 2>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, ep, st);
+  return launch<BM, BN, 1>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, ep, st);
+}
+
 }  // namespace
 
+// Host-side mirror of Epi for ctypes (same field order, plain C layout).
+struct PfmlGemmEpi {
+  double alpha, beta;
+  const double* rs; int64_t srs;
+  const double* cs; int64_t scs;
+  const double* ks; int64_t sks;
+  const double* E; int64_t lde, sE;
+  int e_cols;
+  int diag_col0;
+  double dval;
+  const double* dv; int64_t sdv;
+  int has_diag;
+  const double* es; int64_t ses;
+  int tile_cfg;      // 0 auto, 1: 128x128, 2: 128x64, 3: 64x64
+};
+
+extern "C" int pfml_gemm_epi_size() { return (int)sizeof(PfmlGemmEpi); }
+
+extern "C" hipError_t pfml_dgemm_ex(int ta, int tb, int M, int N, int K, int batch,
+                                    const double* A, int64_t lda, int64_t sA,
+                                    const double* B, int64_t ldb, int64_t sB,
+                                    double* C, int64_t ldc, int64_t sC,
+                                    const PfmlGemmEpi* h, hipStream_t st) {
+  if (M <= 0 || N <= 0 || batch <= 0) return hipSuccess;
+  Epi ep{h->alpha, h->beta, h->rs, h->srs, h->cs, h->scs, h->ks, h->sks, h->E, h->lde, h->sE,
+         h->e_cols, h->diag_col0, h->dval, h->dv, h->sdv, h->has_diag, h->es, h->ses};
+  int cfg = h->tile_cfg;
+  if (cfg == 0) {
+    // 64 x 64 tiles measure as fast as 128 x 128 on the S4 shapes (N ~ 500) and fill the chip
+    // better; 128 x 128 for large matrices (tools/bench_gemm2.py, profiles/r02_gemm_*.json)
+    cfg = (M >= 1024 && N >= 1024) ? 1 : 3;
+  }
+  if (cfg == 1)
+    return launch_w<128, 128>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, ep, st);
+  if (cfg == 2)
+    return launch_w<128, 64>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, ep, st);
+  return launch_w<64, 64>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, ep, st);
+}
+
+// Original ABI: alpha op(A) op(B) (row / column scaled) + beta C.
 extern "C" hipError_t pfml_dgemm(int ta, int tb, int M, int N, int K, int batch, double alpha,
                                  const double* A, int64_t lda, int64_t sA,
                                  const double* B, int64_t ldb, int64_t sB, double beta,
                                  double* C, int64_t ldc, int64_t sC,
                                  const double* rs, int64_t srs, const double* cs, int64_t scs,
                                  hipStream_t st) {
-  if (M <= 0 || N <= 0 || batch <= 0) return hipSuccess;
-  // Large problems: 128 x 128 tiles (4 x 4 accumulators per wave); small: 64 x 64 so that a
-  // batch of ~500 x 500 matrices still gives >> 256 workgroups.
-  const long tiles128 = (long)((M + 127) / 128) * ((N + 127) / 128) * batch;
-  if (tiles128 >= 512)
-    return launch<128, 128>(ta, tb, M, N, K, batch, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc,
-                            sC, rs, srs, cs, scs, st);
-  return launch<64, 64>(ta, tb, M, N, K, batch, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
-                        rs, srs, cs, scs, st);
+  PfmlGemmEpi h{};
+  h.alpha = alpha;
+  h.beta = beta;
+  h.rs = rs; h.srs = srs;
+  h.cs = cs; h.scs = scs;
+  return pfml_dgemm_ex(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, &h, st);
 }

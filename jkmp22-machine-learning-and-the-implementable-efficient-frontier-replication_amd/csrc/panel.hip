@@ -15,27 +15,34 @@
 namespace {
 
 __global__ __launch_bounds__(256) void rff_sincos_kernel(const double* __restrict__ Z, int64_t R,
-                                                         int half, double* __restrict__ out) {
+                                                         int half, double* __restrict__ out,
+                                                         int64_t ldo) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t P = 2 * (int64_t)half + 1;
   if (e >= R * (int64_t)half) return;
   const int64_t r = e / half;
   const int i = (int)(e % half);
   double s, c;
   sincos(Z[e], &s, &c);
-  double* o = out + r * P;
+  double* o = out + r * ldo;
   o[1 + 2 * i] = c;
   o[2 + 2 * i] = s;
-  if (i == 0) o[0] = 1.0;
+  if (i == 0) {
+    o[0] = 1.0;
+    for (int64_t q = 2 * (int64_t)half + 1; q < ldo; ++q) o[q] = 0.0;   // pad columns
+  }
 }
 
 // rows: [B*TH, N] panel row indices (pad rows point to an all-zero row), n_real: [B] real
-// rows per batch entry, vol: per panel row.  out: [B*TH, N, P]
+// rows per batch entry, vol: per panel row.  F: [*, ldf] panel signals (P real columns).
+// out element (b*TH + theta, i, c) at out + (b*TH + theta) * so + i * ldo + c, for c < Pw
+// (columns P..Pw-1 are written as zeros: the even-width padding of the S4 buffers).
 __global__ __launch_bounds__(256) void standardize_kernel(const double* __restrict__ F, int P,
+                                                          int64_t ldf,
                                                           const int64_t* __restrict__ rows,
                                                           const int* __restrict__ n_real, int TH,
                                                           int N, const double* __restrict__ vol,
-                                                          double* __restrict__ out) {
+                                                          double* __restrict__ out, int64_t ldo,
+                                                          int64_t so, int Pw) {
   __shared__ double red[4][64];
   __shared__ double colmean[64], colscale[64];
   const int bt = blockIdx.y;                  // (b, theta)
@@ -48,7 +55,7 @@ __global__ __launch_bounds__(256) void standardize_kernel(const double* __restri
   // pass 1: column sums over real rows
   double s = 0.0;
   if (c < P)
-    for (int i = part; i < n; i += 4) s += F[rw[i] * P + c];
+    for (int i = part; i < n; i += 4) s += F[rw[i] * ldf + c];
   red[part][lane] = s;
   __syncthreads();
   if (part == 0) {
@@ -61,7 +68,7 @@ __global__ __launch_bounds__(256) void standardize_kernel(const double* __restri
   double q = 0.0;
   if (c < P)
     for (int i = part; i < n; i += 4) {
-      const double x = F[rw[i] * P + c] - mu;
+      const double x = F[rw[i] * ldf + c] - mu;
       q += x * x;
     }
   red[part][lane] = q;
@@ -72,32 +79,35 @@ __global__ __launch_bounds__(256) void standardize_kernel(const double* __restri
   }
   __syncthreads();
   const double sc = colscale[lane];
-  double* o = out + (int64_t)bt * N * P;
-  if (c < P)
+  double* o = out + (int64_t)bt * so;
+  if (c < Pw)
     for (int i = part; i < N; i += 4) {
       double v = 0.0;
-      if (i < n) v = (F[rw[i] * P + c] - mu) * sc / vol[rw[i]];
-      o[(int64_t)i * P + c] = v;
+      if (i < n && c < P) v = (F[rw[i] * ldf + c] - mu) * sc / vol[rw[i]];
+      o[(int64_t)i * ldo + c] = v;
     }
 }
 
 }  // namespace
 
 extern "C" hipError_t pfml_rff_sincos(const double* Z, int64_t R, int half, double* out,
-                                      hipStream_t st) {
+                                      int64_t ldo, hipStream_t st) {
   const int64_t tot = R * (int64_t)half;
   if (tot <= 0) return hipSuccess;
+  if (ldo < 2 * (int64_t)half + 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL(rff_sincos_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, Z,
-                     R, half, out);
+                     R, half, out, ldo);
   return hipGetLastError();
 }
 
-extern "C" hipError_t pfml_standardize(const double* F, int P, const int64_t* rows,
+extern "C" hipError_t pfml_standardize(const double* F, int P, int64_t ldf, const int64_t* rows,
                                        const int* n_real, int B, int TH, int N,
-                                       const double* vol, double* out, hipStream_t st) {
+                                       const double* vol, double* out, int64_t ldo, int64_t so,
+                                       int Pw, hipStream_t st) {
   if (B <= 0 || N <= 0) return hipSuccess;
-  dim3 grid((P + 63) / 64, B * TH);
-  hipLaunchKernelGGL(standardize_kernel, grid, dim3(256), 0, st, F, P, rows, n_real, TH, N, vol,
-                     out);
+  if (Pw < P || ldo < Pw || ldf < P) return hipErrorInvalidValue;
+  dim3 grid((Pw + 63) / 64, B * TH);
+  hipLaunchKernelGGL(standardize_kernel, grid, dim3(256), 0, st, F, P, ldf, rows, n_real, TH, N,
+                     vol, out, ldo, so, Pw);
   return hipGetLastError();
 }

@@ -1,0 +1,173 @@
+// Elementwise stages of the per-month PFML step (S4, PFML_Input_Data.py:333-345 and
+// General_functions.py:919-963) fused into single passes over the [B, N, N] month batch.
+//
+// m_func works on the symmetric part of its matrices (Sigma from X F X' and every inverse
+// are symmetric in exact arithmetic; the reference symmetrises nothing, so rounding-level
+// asymmetry is removed here once per pass instead of by extra torch passes).  Every kernel
+// processes a 32 x 32 tile (I, J) and its mirror (J, I) through LDS, so one launch reads each
+// operand once and writes the symmetric result with coalesced stores:
+//
+//   MF_X      x    = s a_i a_j sym(Sigma)_ij                    (Lemma 1: w^-1 L^-1/2 gS L^-1/2)
+//   MF_FIX    Aq   = x + diag(y) - sym(mt) o sigma_gr           (the fixed-point argument, Q6)
+//             with sigma_gr = mask mask' + sym(Sigma)/c^2 and y_i = 1 + sigma_gr_ii, all formed
+//             from Sigma on the fly (no sigma_gr / x / base matrices are stored)
+//   MF_DB     M'   = I/2 + (mu^2 sym(M) + mu^-2 sym(Minv))/4    (Denman-Beavers update)
+//   MF_SHAT   out  = sym(X) + d I                                (sigma_hat = x + 2I, root + sigma_hat)
+//
+// Per-batch scalars (s = gamma / w, c = 1 + rf + mu, mu_DB) and per-row vectors (a = lambda^-1/2,
+// mask) are read from device memory: nothing here needs the host.
+#include "common.h"
+
+namespace {
+
+constexpr int TS = 32;
+
+enum Mode { MF_X = 0, MF_FIX = 1, MF_DB = 2, MF_SHAT = 3 };
+
+struct MfArgs {
+  int mode, B, N;
+  int64_t ld, sX;                 // layout of every [B, N, N] operand
+  const double* X;                // Sigma (X, FIX), M (DB), X (SHAT)
+  const double* Y;                // mt (FIX), Minv (DB), second addend (SHAT, may be null)
+  double* out;
+  const double* svec;             // [B] s (X, FIX) or mu (DB)
+  const double* cvec;             // [B] c (FIX)
+  const double* a;                // [B, N] lambda^-1/2 (X, FIX)
+  const double* mask;             // [B, N] (FIX)
+  int64_t sv;                     // batch stride of a / mask
+  double d;                       // diagonal add (SHAT)
+};
+
+__global__ __launch_bounds__(256) void mfunc_sym_kernel(MfArgs p) {
+  __shared__ double tx[TS][TS + 1], ty[TS][TS + 1];
+  const int tiles = (p.N + TS - 1) / TS;
+  const int b = blockIdx.y;
+  const int I0 = (blockIdx.x / tiles) * TS, J0 = (blockIdx.x % tiles) * TS;
+  const int tx_ = threadIdx.x & 31, ty_ = threadIdx.x >> 5;   // 32 x 8
+  const double* X = p.X + (int64_t)b * p.sX;
+  const double* Y = p.Y ? p.Y + (int64_t)b * p.sX : nullptr;
+  double* O = p.out + (int64_t)b * p.sX;
+  // mirror tile (J0.., I0..) into LDS transposed: tx[r][c] = X[J0 + c][I0 + r]
+  for (int r = ty_; r < TS; r += 8) {
+    const int gi = J0 + r, gj = I0 + tx_;
+    const bool ok = gi < p.N && gj < p.N;
+    tx[tx_][r] = ok ? X[(int64_t)gi * p.ld + gj] : 0.0;
+    if (Y) ty[tx_][r] = ok ? Y[(int64_t)gi * p.ld + gj] : 0.0;
+  }
+  __syncthreads();
+  const double s = p.svec ? p.svec[b] : 0.0;
+  const double c = p.cvec ? p.cvec[b] : 1.0;
+  const double* av = p.a ? p.a + (int64_t)b * p.sv : nullptr;
+  const double* mv = p.mask ? p.mask + (int64_t)b * p.sv : nullptr;
+  for (int r = ty_; r < TS; r += 8) {
+    const int i = I0 + r, j = J0 + tx_;
+    if (i >= p.N || j >= p.N) continue;
+    const int64_t o = (int64_t)i * p.ld + j;
+    const double xs = 0.5 * (X[o] + tx[r][tx_]);
+    const double ys = Y ? 0.5 * (Y[o] + ty[r][tx_]) : 0.0;
+    double v;
+    if (p.mode == MF_X) {
+      v = s * (av[i] * av[j]) * xs;
+    } else if (p.mode == MF_FIX) {
+      const double ic2 = 1.0 / (c * c);
+      const double mm = mv[i] * mv[j];
+      v = xs * (s * (av[i] * av[j]) - ys * ic2) - ys * mm;
+      if (i == j) v += 1.0 + mm + xs * ic2;
+    } else if (p.mode == MF_DB) {
+      const double mu2 = s * s;
+      v = 0.25 * (mu2 * xs + ys / mu2);
+      if (i == j) v += 0.5;
+    } else {
+      v = xs + ys;
+      if (i == j) v += p.d;
+    }
+    O[o] = v;
+  }
+}
+
+// Per-batch Frobenius norms of two [B, N, N] matrices -> DB scaling mu = (|Minv| / |M|)^(1/4)
+// (1 once the iteration runs unscaled).  Two phases: MU_SPLIT workgroups per matrix reduce
+// row slabs with 16-byte loads into partial sums, the last phase (one wave per matrix) adds
+// them in a fixed order (deterministic).
+constexpr int MU_SPLIT = 16;
+
+__global__ __launch_bounds__(256) void db_norm_partial_kernel(const double* __restrict__ M,
+                                                              const double* __restrict__ Minv,
+                                                              int N, int64_t ld, int64_t sX,
+                                                              double* __restrict__ part) {
+  __shared__ double red[8];
+  const int b = blockIdx.y, sl = blockIdx.x;
+  const double* A = M + (int64_t)b * sX;
+  const double* Bm = Minv + (int64_t)b * sX;
+  const int r0 = (int)((int64_t)N * sl / MU_SPLIT), r1 = (int)((int64_t)N * (sl + 1) / MU_SPLIT);
+  double sa = 0.0, sb = 0.0;
+  for (int i = r0; i < r1; ++i)
+    for (int j = threadIdx.x; j < N; j += 256) {
+      const double x = A[(int64_t)i * ld + j], y = Bm[(int64_t)i * ld + j];
+      sa += x * x;
+      sb += y * y;
+    }
+  const double ta = block_sum(sa, red);
+  const double tb = block_sum(sb, red + 4);
+  if (threadIdx.x == 0) {
+    part[((int64_t)b * MU_SPLIT + sl) * 2] = ta;
+    part[((int64_t)b * MU_SPLIT + sl) * 2 + 1] = tb;
+  }
+}
+
+__global__ __launch_bounds__(64) void db_mu_final_kernel(const double* __restrict__ part, int B,
+                                                         int unscaled, double* __restrict__ mu) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= B) return;
+  double ta = 0.0, tb = 0.0;
+  for (int q = 0; q < MU_SPLIT; ++q) {
+    ta += part[((int64_t)b * MU_SPLIT + q) * 2];
+    tb += part[((int64_t)b * MU_SPLIT + q) * 2 + 1];
+  }
+  mu[b] = unscaled ? 1.0 : sqrt(sqrt(sqrt(tb) / fmax(sqrt(ta), 1e-300)));
+}
+
+}  // namespace
+
+struct PfmlMfArgs {
+  int mode, B, N;
+  int64_t ld, sX;
+  const double* X;
+  const double* Y;
+  double* out;
+  const double* svec;
+  const double* cvec;
+  const double* a;
+  const double* mask;
+  int64_t sv;
+  double d;
+};
+
+extern "C" int pfml_mf_args_size() { return (int)sizeof(PfmlMfArgs); }
+
+extern "C" hipError_t pfml_mfunc_sym(const PfmlMfArgs* h, hipStream_t st) {
+  if (h->B <= 0 || h->N <= 0) return hipSuccess;
+  if (h->out == h->X || (h->Y && h->out == h->Y)) return hipErrorInvalidValue;   // tiles race
+  MfArgs p{h->mode, h->B, h->N, h->ld, h->sX, h->X, h->Y, h->out, h->svec, h->cvec, h->a,
+           h->mask, h->sv, h->d};
+  const int tiles = (h->N + TS - 1) / TS;
+  hipLaunchKernelGGL(mfunc_sym_kernel, dim3(tiles * tiles, h->B), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
+extern "C" int pfml_db_mu_work_doubles(int B) { return 2 * MU_SPLIT * B; }
+
+// work: pfml_db_mu_work_doubles(B) doubles of scratch
+extern "C" hipError_t pfml_db_mu(const double* M, const double* Minv, int B, int N, int64_t ld,
+                                 int64_t sX, int unscaled, double* mu, double* work,
+                                 hipStream_t st) {
+  if (B <= 0 || N <= 0) return hipSuccess;
+  if (unscaled) {
+    hipLaunchKernelGGL(db_mu_final_kernel, dim3((B + 63) / 64), dim3(64), 0, st, work, B, 1, mu);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(db_norm_partial_kernel, dim3(MU_SPLIT, B), dim3(256), 0, st, M, Minv, N, ld,
+                     sX, work);
+  hipLaunchKernelGGL(db_mu_final_kernel, dim3((B + 63) / 64), dim3(64), 0, st, work, B, 0, mu);
+  return hipGetLastError();
+}

@@ -6,17 +6,22 @@ a batched device pipeline over MONTHS (dates are independent given m_t, Sigma_t 
 
 1. RFF features for the whole panel: one fp64 MFMA GEMM X W + cos/sin (K13, once per g),
    stored in the interleaved order [constant, cos1, sin1, ...];
-2. vol scales sqrt(diag(Sigma_t)) = sqrt(rowsum((X F) o X) + ivol) without forming Sigma
-   (K1 diag epilogue, :274-307), cross-sectional median fill;
+2. vol scales sqrt(diag(Sigma_t)) = sqrt(rowsum((X F) o X) + ivol) per Barra row on the
+   device, without forming Sigma (:274-307), cross-sectional median fill (torch nanmedian);
 3. per batch of months (ragged universes padded block-diagonally):
    * signals: gather the 13 x N x P window, demean RFF columns, unit-norm every column, scale
      rows by 1/vol (K11/K12, :357-391);
-   * Sigma_t = X F X' + diag(ivol) (K1) and m_t = m_func(...) (K2/K3, Lemma 1);
+   * Sigma_t = X F X' + diag(ivol) as one GEMM with a diagonal-add epilogue (K1) and
+     m_tilde_t (K2/K3, Lemma 1, ops/linalg.m_tilde: fused symmetric passes + SPD inverses, no
+     host sync);
    * the aggregation (24) in Horner form over the augmented [S_{t-theta} | I] (K5/K6):
        T_11 = [S_11 | I],  T_theta = [S_theta | I] + (m D_theta) T_{theta+1}
      gives both sum_theta agg_theta S_{t-theta} and sum_theta agg_theta in 11 GEMMs per chain
      (the reference forms 22 N x N products plus 24 N x P products), with both g stacked in
-     the column dimension so m and the agg products are shared;
+     the column dimension so m and the agg products are shared.  Each step is ONE launch of
+     the fused GEMM (csrc/gemm_f64.hip): m = diag(a) m_tilde diag(1/a) and D_theta enter as
+     row / k scales, S_theta and the identity block as the epilogue addend - no m, m D or
+     [S | I] matrix is ever materialised;
    * omega = const^-1 Omega (pivoted LU solve, K7), omega_chg = omega - D_0 omega_l1;
    * r_tilde = omega' r, risk = gamma omega' Sigma omega (Sigma applied in low-rank form),
      tc = w omega_chg' Lambda omega_chg, denom = risk + tc (K8-K10).
@@ -35,7 +40,7 @@ import torch
 from ..config import Config, get_features, interleaved_order
 from ..data import io
 from ..ops import linalg as la
-from ..ops.gemm import gemm, gemm_prec
+from ..ops.gemm import gemm_fused, gemm_prec
 from ..ops.panel import rff_features, standardize_signals
 from ..utils.dates import month_index, pfml_date_grids
 from ..utils.log import get_logger
@@ -125,10 +130,11 @@ def vol_scales(panel: Panel, barra: BarraCov, months: np.ndarray) -> np.ndarray:
 
 def auto_month_batch(n_stocks: int, gp: int, device, cap: int = 256) -> int:
     """Months per S4 batch from the memory one month's working set needs (fp64): the
-    13-month signal window (13 N GP), the Horner chains and solves (~6 N (GP + N)) and ~14
-    N x N matrices of m_func / Sigma.  A device batch takes up to 60 % of free HBM (288 GB on
-    MI355X: ~256 months at N = 500, ~75 at N = 3000), a host batch 25 % of available RAM."""
-    per = 8.0 * (13.0 * n_stocks * gp + 6.0 * n_stocks * (gp + n_stocks) + 14.0 * n_stocks ** 2)
+    13-month signal window (13 N GP), four Horner buffers of N x (GP + N), ~8 N x N matrices of
+    m_func / Sigma and the (25) scratch.  A device batch takes up to 60 % of free HBM (288 GB on
+    MI355X: 256 months at N = 500, ~60 at N = 3000), a host batch 25 % of available RAM."""
+    per = 8.0 * (13.0 * n_stocks * gp + 5.0 * n_stocks * (gp + n_stocks) + 9.0 * n_stocks ** 2
+                 + 2.0 * gp * gp)
     dev = torch.device(device)
     if dev.type == "cuda":
         free, _ = torch.cuda.mem_get_info(dev)
@@ -142,17 +148,64 @@ def auto_month_batch(n_stocks: int, gp: int, device, cap: int = 256) -> int:
     return int(max(1, min(cap, budget // per)))
 
 
-def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.DataFrame,
+def _even(n: int) -> int:
+    return n + (n & 1)
+
+
+@dataclass
+class _Batch:
+    months: np.ndarray          # [B] month indices
+    ns: np.ndarray              # [B] universe sizes
+    idx: torch.Tensor           # [B, 13, N] panel rows (pad -> zero row Rpad), device
+    mask: torch.Tensor          # [B, N] 1 = real stock
+    n_real: torch.Tensor        # [B] int32
+    brow: torch.Tensor          # [B, N] Barra row of each stock (pad -> identity row)
+    fpos: torch.Tensor          # [B] Barra month position
+    lam: torch.Tensor           # [B, N] Kyle's lambda (pad: gamma / w)
+    r: torch.Tensor             # [B, N] ret_ld1 (pad 0)
+    w: torch.Tensor             # [B] wealth
+    rf: torch.Tensor            # [B]
+
+
+@dataclass
+class S4Plan:
+    """Everything of an S4 run that is layout, not arithmetic: panel / Barra row indices of
+    every month's 13-month window, per-batch padded index tensors, the device copies of the
+    raw panel and Barra arrays.  Built once per (data, months, device); ``run_plan`` does all
+    the math (RFF, vol scales, standardisation, Sigma, m_func, (24), (25)) on the device."""
+    months: np.ndarray
+    G: int                      # g values (output)
+    Gc: int                     # distinct signal blocks (1 under quirk Q1)
+    P: int                      # 2 * (p_max/2) + 1
+    Pp: int                     # P padded to even
+    N: int                      # padded universe width (even)
+    W: np.ndarray               # [G, k, P/2] RFF weights
+    same_w: bool
+    feats: torch.Tensor         # [R, k] ranked characteristics (device)
+    gt: torch.Tensor            # [R+1] (1+tr_ld0)/(1+mu_ld0), pad 1
+    vol_rows: torch.Tensor      # [Mv, nv] panel rows of each vol month (pad -> R)
+    vol_brow: torch.Tensor      # [Mv, nv] Barra row of each (pad / missing -> -1)
+    vol_fpos: torch.Tensor      # [Mv] Barra month position of each vol month
+    bX: torch.Tensor            # [Rb+1, K] Barra loadings (+ zero row)
+    biv: torch.Tensor           # [Rb+1] idiosyncratic variance (+ 1 for the pad row)
+    bF: torch.Tensor            # [Mb, K, K]
+    batches: list
+    sig_rows: list
+    sig_ids: list
+    R: int
+
+
+def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.DataFrame,
                  risk_free: pd.DataFrame, device, months: np.ndarray | None = None,
-                 keep_risk_tc: bool = False, batch: int | None = None) -> PfmlInputs:
+                 batch: int | None = None) -> S4Plan:
     features = get_features()
     pf = cfg.pf_set
-    gamma, mu = float(pf["gamma_rel"]), float(pf["mu"])
+    gamma = float(pf["gamma_rel"])
     lb = int(pf["lb_hor"])
     G, Pm = len(cfg.g_vec), cfg.p_max
     P = Pm + 1
+    Pp = _even(P)
     dev = torch.device(device)
-    prec = cfg.run.precision         # fp64 | fp32 | bf16 | fp8: covariance / RFF / risk GEMMs
     panel = Panel.from_chars(chars, features)
     grids = pfml_date_grids(int(barra.months.min()), lb, cfg.settings["split"]["test_end"],
                             cfg.settings["pf"]["dates"]["start_year"],
@@ -160,167 +213,272 @@ def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
     if months is None:
         months = grids["m2"]
     months = np.asarray(months, np.int64)
-
-    # ---- 1. RFF features (K13) and 2. vol scales ------------------------------------
-    range_push("pfml_inputs.rff")
     W = _rff_weights(cfg, len(features))
     same_w = all(np.array_equal(W[0], W[g]) for g in range(G))
-    Xf = torch.as_tensor(panel.feats, dtype=torch.float64, device=dev)
-    rffs = []
-    for g in range(G):
-        if g > 0 and same_w:
-            rffs.append(rffs[0])          # quirk Q1: identical inputs for every g
-            continue
-        R = rff_features(Xf, torch.as_tensor(W[g], dtype=torch.float64, device=dev), prec)
-        rffs.append(torch.cat([R, torch.zeros((1, P), dtype=R.dtype, device=dev)]))  # pad row
-    del Xf
-    range_pop()
-    lbm = grids["lb"]
-    lbm = lbm[(lbm >= months.min() - (lb + 1)) & (lbm <= months.max())]
-    vol = vol_scales(panel, barra, lbm)
-    vol_t = torch.as_tensor(np.r_[vol, 1.0], dtype=torch.float64, device=dev)
-    gt_all = (1.0 + panel.cols["tr_ld0"]) / (1.0 + panel.cols["mu_ld0"])
-    gt_all = np.nan_to_num(gt_all, nan=1.0)
-    gt_t = torch.as_tensor(np.r_[gt_all, 1.0], dtype=torch.float64, device=dev)
+    Gc = 1 if same_w else G
+    R = len(panel.mi)
     wmap = dict(zip(month_index(wealth["eom"]), wealth["wealth"].to_numpy(np.float64)))
     rfmap = dict(zip(month_index(risk_free["eom"]), risk_free["rf"].to_numpy(np.float64)))
     tc_on = bool(cfg.settings["Transaction_Costs"])
+    Rb = len(barra.ids)
+
+    # vol-scale months (:274-307): sqrt(diag Sigma) merged on (id, month), median fill
+    lbm = grids["lb"]
+    if len(months):
+        lbm = lbm[(lbm >= months.min() - (lb + 1)) & (lbm <= months.max())]
+    else:
+        lbm = lbm[:0]
+    vr, vb, vf = [], [], []
+    for mi in lbm:
+        a_, b_ = np.searchsorted(panel.mi, mi, "left"), np.searchsorted(panel.mi, mi, "right")
+        rows = np.arange(a_, b_)
+        brow = np.full(len(rows), -1, np.int64)
+        bp = 0
+        try:
+            bp = barra.month_pos(int(mi))
+            o0, o1 = barra.offsets[bp], barra.offsets[bp + 1]
+            pos = np.searchsorted(barra.ids[o0:o1], panel.ids[rows])
+            pos = np.clip(pos, 0, max(o1 - o0 - 1, 0))
+            hit = (o1 > o0) & (barra.ids[o0:o1][pos] == panel.ids[rows]) if o1 > o0 else \
+                np.zeros(len(rows), bool)
+            brow = np.where(hit, o0 + pos, -1)
+        except KeyError:
+            pass
+        vr.append(rows)
+        vb.append(brow)
+        vf.append(bp)
+    nv = max([len(x) for x in vr] + [1])
+    vol_rows = np.full((len(vr), nv), R, np.int64)
+    vol_brow = np.full((len(vr), nv), -1, np.int64)
+    for i, (x, y) in enumerate(zip(vr, vb)):
+        vol_rows[i, :len(x)] = x
+        vol_brow[i, :len(y)] = y
+
+    gt_all = np.nan_to_num((1.0 + panel.cols["tr_ld0"]) / (1.0 + panel.cols["mu_ld0"]), nan=1.0)
 
     T = len(months)
-    r_out = torch.zeros((G, T, P), dtype=torch.float64, device=dev)
-    d_out = torch.zeros((G, T, P, P), dtype=torch.float64, device=dev)
-    risk_out = torch.zeros_like(d_out) if keep_risk_tc else None
-    tc_out = torch.zeros_like(d_out) if keep_risk_tc else None
-    sig_rows, sig_ids = [], []
-    signal_t = [[None] * T for _ in range(G)]
-    Rpad = len(panel.mi)
+    nmax = max((len(panel.valid_rows(int(d))) for d in months), default=1)
+    Npad = _even(max(nmax, 2))
     bsz = batch or cfg.run.month_batch
     if not bsz or bsz <= 0:
-        nmax = max(len(panel.valid_rows(int(d))) for d in months) if T else 1
-        bsz = auto_month_batch(nmax, G * P, dev)
+        bsz = auto_month_batch(Npad, Gc * Pp, dev)
         log.info(f"PFML inputs: {bsz} months per batch (N <= {nmax})")
-
+    batches, sig_rows, sig_ids = [], [], []
     for b0 in range(0, T, bsz):
         bm = months[b0: b0 + bsz]
         B = len(bm)
-        range_push("pfml_inputs.batch")
-        rows_d = [panel.valid_rows(int(d)) for d in bm]
-        ns = np.array([len(r) for r in rows_d])
-        N = int(ns.max())
-        idx = np.full((B, lb + 2, N), Rpad, dtype=np.int64)
+        idx = np.full((B, lb + 2, Npad), R, dtype=np.int64)
+        brow = np.full((B, Npad), Rb, dtype=np.int64)
+        fpos = np.zeros(B, np.int64)
+        lam = np.empty((B, Npad))
+        rr = np.zeros((B, Npad))
+        ns = np.zeros(B, np.int64)
         for bi, d in enumerate(bm):
-            ids = panel.ids[rows_d[bi]]
+            rows_d = panel.valid_rows(int(d))
+            ids = panel.ids[rows_d]
+            n = len(ids)
+            ns[bi] = n
             for th in range(lb + 2):
                 r = panel.rows(int(d) - th, ids)
                 if np.any(r < 0):
                     raise ValueError(f"month {d}: universe lacks the {th}-month lookback rows")
-                idx[bi, th, : len(r)] = r
-            sig_rows.append(rows_d[bi])
-            sig_ids.append(ids)
-        idx_t = torch.as_tensor(idx, device=dev)
-        mask = torch.as_tensor((np.arange(N)[None, :] < ns[:, None]).astype(np.float64), device=dev)
-        wv = torch.as_tensor([wmap[int(d)] for d in bm], dtype=torch.float64, device=dev)
-        rfv = torch.as_tensor([rfmap[int(d)] for d in bm], dtype=torch.float64, device=dev)
-
-        # signals for every g: [G, B, 13, N, P]
-        S_all = []
-        for g in range(G):
-            if g > 0 and rffs[g] is rffs[0]:
-                S_all.append(S_all[0])
-                continue
-            S_all.append(standardize_signals(rffs[g], idx_t, mask, vol_t))
-        # Barra Sigma (padded: identity block), Lambda, returns
-        K = barra.X.shape[1]
-        Xl_h = np.zeros((B, N, K))
-        Fb_h = np.zeros((B, K, K))
-        iv_h = np.ones((B, N))
-        lam_h = np.empty((B, N))
-        r_h = np.zeros((B, N))
-        for bi, d in enumerate(bm):
-            ids = sig_ids[b0 + bi]
-            bids, X, F, ivol = barra.slice(int(d))
+                idx[bi, th, :n] = r
+            bp = barra.month_pos(int(d))
+            o0, o1 = barra.offsets[bp], barra.offsets[bp + 1]
+            bids = barra.ids[o0:o1]
             pos = np.searchsorted(bids, ids)
             if np.any(pos >= len(bids)) or np.any(bids[np.minimum(pos, len(bids) - 1)] != ids):
                 raise KeyError(f"month {d}: valid ids missing from the Barra universe")
-            n = len(ids)
-            Xl_h[bi, :n] = X[pos]
-            Fb_h[bi] = F
-            iv_h[bi, :n] = ivol[pos]
-            lam_h[bi] = gamma / float(wmap[int(d)])
-            lam_h[bi, :n] = panel.cols["lambda"][rows_d[bi]] if tc_on else 1e-16
-            r_h[bi, :n] = panel.cols["ret_ld1"][rows_d[bi]]
-        Xl = torch.as_tensor(Xl_h, device=dev)
-        Fb = torch.as_tensor(Fb_h, device=dev)
-        iv = torch.as_tensor(iv_h, device=dev)
-        lam = torch.as_tensor(lam_h, device=dev)
-        r = torch.as_tensor(r_h, device=dev)
-        XF = gemm(Xl, Fb)
-        Sigma = gemm_prec(XF, Xl, prec, trans_b=True)            # K1: Barra covariance
-        Sigma.diagonal(dim1=1, dim2=2).add_(iv)
-        m = la.m_func(Sigma, lam, wv, rfv, mu, gamma, cfg.run.iterations, mask=mask)
+            brow[bi, :n] = o0 + pos
+            fpos[bi] = bp
+            lam[bi] = gamma / float(wmap[int(d)])
+            lam[bi, :n] = panel.cols["lambda"][rows_d] if tc_on else 1e-16
+            rr[bi, :n] = panel.cols["ret_ld1"][rows_d]
+            sig_rows.append(rows_d)
+            sig_ids.append(ids)
+        mask = (np.arange(Npad)[None, :] < ns[:, None]).astype(np.float64)
+        tt = lambda x, dt=torch.float64: torch.as_tensor(x, dtype=dt, device=dev)  # noqa: E731
+        batches.append(_Batch(
+            months=bm, ns=ns, idx=tt(idx, torch.int64), mask=tt(mask),
+            n_real=tt(ns, torch.int32), brow=tt(brow, torch.int64), fpos=tt(fpos, torch.int64),
+            lam=tt(lam), r=tt(rr), w=tt([wmap[int(d)] for d in bm]),
+            rf=tt([rfmap[int(d)] for d in bm])))
+    K = barra.X.shape[1]
+    bX = np.concatenate([barra.X, np.zeros((1, K))])
+    biv = np.r_[barra.ivol, 1.0]
+    return S4Plan(
+        months=months, G=G, Gc=Gc, P=P, Pp=Pp, N=Npad, W=W, same_w=same_w,
+        feats=torch.as_tensor(panel.feats, dtype=torch.float64, device=dev),
+        gt=torch.as_tensor(np.r_[gt_all, 1.0], dtype=torch.float64, device=dev),
+        vol_rows=torch.as_tensor(vol_rows, device=dev),
+        vol_brow=torch.as_tensor(vol_brow, device=dev),
+        vol_fpos=torch.as_tensor(np.asarray(vf, np.int64), device=dev),
+        bX=torch.as_tensor(bX, dtype=torch.float64, device=dev),
+        biv=torch.as_tensor(biv, dtype=torch.float64, device=dev),
+        bF=torch.as_tensor(barra.F, dtype=torch.float64, device=dev),
+        batches=batches, sig_rows=sig_rows, sig_ids=sig_ids, R=R)
 
-        # (24): Horner chains over [S^{g=0} | ... | S^{g=G-1} | I]; with identical signals for
-        # every g (quirk Q1, compat mode) one block is carried and shared
-        Dg = gt_t[idx_t]                                           # [B, 13, N]
-        Gc = 1 if same_w else G
-        GP = Gc * P
-        Wd = GP + N
-        eye = torch.eye(N, dtype=torch.float64, device=dev).expand(B, N, N)
 
-        def aug(th):
-            Tm = torch.empty((B, N, Wd), dtype=torch.float64, device=dev)
-            for g in range(Gc):
-                Tm[:, :, g * P:(g + 1) * P] = S_all[g][:, th]
-            Tm[:, :, GP:] = eye
-            return Tm
+def _vol_device(plan: S4Plan) -> torch.Tensor:
+    """vol[r] = sqrt(diag Sigma_t)[r] for every panel row r of the vol months, NaN -> the
+    month's median (PFML_Input_Data.py:274-307); rows outside those months NaN; pad row 1.
+    diag(X F X')_i = sum_k (X F)_ik X_ik: per Barra row, no N x N matrix is formed."""
+    dev = plan.feats.device
+    vol = torch.full((plan.R + 1,), float("nan"), dtype=torch.float64, device=dev)
+    if plan.vol_rows.numel():
+        br = plan.vol_brow
+        ok = br >= 0
+        brc = torch.where(ok, br, torch.zeros_like(br))
+        Xr = plan.bX[brc]                                         # [Mv, nv, K]
+        Fm = plan.bF[plan.vol_fpos]                               # one F per vol month
+        d = (torch.bmm(Xr, Fm) * Xr).sum(-1) + plan.biv[brc]
+        v = torch.where(ok, d.sqrt(), torch.full_like(d, float("nan")))
+        real = plan.vol_rows < plan.R
+        v = torch.where(real, v, torch.full_like(v, float("nan")))
+        # pandas median: mean of the two middle values of the non-NaN entries (torch's
+        # nanmedian returns the lower one); NaN sorts last
+        sv = torch.sort(v, dim=1).values
+        cnt = (~torch.isnan(v)).sum(1, keepdim=True)
+        lo = ((cnt - 1).clamp_min(0)) // 2
+        hi = cnt // 2
+        hi = torch.minimum(hi, (cnt - 1).clamp_min(0))
+        med = 0.5 * (sv.gather(1, lo) + sv.gather(1, hi))
+        v = torch.where(torch.isnan(v), med.expand_as(v), v)
+        vol[plan.vol_rows[real]] = v[real]
+    vol[plan.R] = 1.0
+    return vol
 
-        Tc = aug(lb)
-        Ul = aug(lb + 1)
+
+def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False) -> "PfmlInputs":
+    """The S4 arithmetic for every month of the plan (device or CPU fp64 oracle)."""
+    pf = cfg.pf_set
+    gamma, mu = float(pf["gamma_rel"]), float(pf["mu"])
+    lb = int(pf["lb_hor"])
+    G, Gc, P, Pp, N = plan.G, plan.Gc, plan.P, plan.Pp, plan.N
+    GP = Gc * Pp
+    Wd = GP + N
+    dev = plan.feats.device
+    prec = cfg.run.precision         # fp64 | fp32 | bf16 | fp8: covariance / RFF / risk GEMMs
+    T = len(plan.months)
+
+    # ---- 1. RFF features (K13) and 2. vol scales -----------------------------------------
+    range_push("pfml_inputs.rff")
+    rffs = [rff_features(plan.feats, torch.as_tensor(plan.W[g], dtype=torch.float64, device=dev),
+                         prec, width=Pp, pad_rows=1) for g in range(Gc)]
+    vol = _vol_device(plan)
+    range_pop()
+
+    r_out = torch.zeros((G, T, P), dtype=torch.float64, device=dev)
+    d_out = torch.zeros((G, T, P, P), dtype=torch.float64, device=dev)
+    risk_out = torch.zeros_like(d_out) if keep_risk_tc else None
+    tc_out = torch.zeros_like(d_out) if keep_risk_tc else None
+    signal_t = [[None] * T for _ in range(G)]
+    b0 = 0
+    for bt in plan.batches:
+        B = len(bt.months)
+        range_push("pfml_inputs.batch")
+        # signals of every distinct g, written into one [B, 13, N, Gc*Pp] stack
+        S = torch.empty((B, lb + 2, N, GP), dtype=torch.float64, device=dev)
+        for g in range(Gc):
+            standardize_signals(rffs[g], bt.idx, bt.mask, vol, P=P,
+                                out=S[..., g * Pp:(g + 1) * Pp], n_real=bt.n_real)
+        # Barra Sigma = X F X' + diag(ivol) (K1; pad rows: X = 0, ivol = 1 -> identity block)
+        Xl = plan.bX[bt.brow]                                       # [B, N, K]
+        Fb = plan.bF[bt.fpos]                                       # [B, K, K]
+        iv = plan.biv[bt.brow]                                      # [B, N]
+        XF = torch.bmm(Xl, Fb)
+        Sigma = torch.empty((B, N, N), dtype=torch.float64, device=dev)
+        if prec == "fp64":
+            gemm_fused(XF, Xl, Sigma, trans_b=True, diag_col0=0, diag_vec=iv)
+        else:
+            gemm_prec(XF, Xl, prec, trans_b=True, out=Sigma)
+            Sigma.diagonal(dim1=1, dim2=2).add_(iv)
+        # m = diag(a) m_tilde diag(1/a) (Lemma 1); a and 1/a are folded into the Horner GEMMs
+        mt, a = la.m_tilde(Sigma, bt.lam, bt.w, bt.rf, mu, gamma, cfg.run.iterations,
+                           mask=bt.mask)
+        # (24) Horner chains over [S_theta | I], one fused GEMM launch per step:
+        #   T_theta = [S_theta | I] + diag(a) m_tilde diag(D_theta / a) T_{theta+1}
+        Dg = plan.gt[bt.idx]                                        # [B, 13, N]
+        ainv = 1.0 / a
+        Tc = [torch.empty((B, N, Wd), dtype=torch.float64, device=dev) for _ in range(2)]
+        Ul = [torch.empty((B, N, Wd), dtype=torch.float64, device=dev) for _ in range(2)]
+        eye = torch.eye(N, dtype=torch.float64, device=dev)
+        Tc[0][:, :, :GP] = S[:, lb]
+        Tc[0][:, :, GP:] = eye
+        Ul[0][:, :, :GP] = S[:, lb + 1]
+        Ul[0][:, :, GP:] = eye
+        cur = 0
         for th in range(lb - 1, -1, -1):
-            Mg = m * Dg[:, th].unsqueeze(1)                         # m diag(g_theta)
-            Tn = aug(th)
-            gemm(Mg, Tc, beta=1.0, out=Tn)
-            Tc = Tn
-            Mg1 = m * Dg[:, th + 1].unsqueeze(1)
-            Un = aug(th + 1)
-            gemm(Mg1, Ul, beta=1.0, out=Un)
-            Ul = Un
-        # omega = const^-1 Omega, solved in place on the augmented [Omega | const] rows
-        omega = la.solve_augmented(Tc, N, GP, a0=GP, b0=0)          # [B, N, GP]
-        omega_l1 = la.solve_augmented(Ul, N, GP, a0=GP, b0=0)
-        omega_chg = omega - Dg[:, 0].unsqueeze(-1) * omega_l1
-
-        # (25): r_tilde, risk, tc
-        rt_ = gemm(omega, r.unsqueeze(-1), trans_a=True).squeeze(-1)        # [B, GP]
-        XtO = gemm(Xl, omega, trans_a=True)                                  # [B, K, GP]
-        SO = gemm(Xl, gemm(Fb, XtO)) + iv.unsqueeze(-1) * omega               # Sigma omega
-        lw = lam * wv.view(B, 1)
+            gemm_fused(mt, Tc[cur], Tc[cur ^ 1], row_scale=a, k_scale=(Dg[:, th] * ainv),
+                       addend=S[:, th], addend_cols=GP, diag_col0=GP, diag_value=1.0)
+            gemm_fused(mt, Ul[cur], Ul[cur ^ 1], row_scale=a, k_scale=(Dg[:, th + 1] * ainv),
+                       addend=S[:, th + 1], addend_cols=GP, diag_col0=GP, diag_value=1.0)
+            cur ^= 1
+        T0, U0 = Tc[cur], Ul[cur]
+        sig0 = S[:, 0].clone()                                      # signal_t blocks
+        del S, Tc, Ul
+        # omega = const^-1 Omega, solved in place on the augmented [Omega | const] rows (K7)
+        omega = la.solve_augmented(T0, N, GP, a0=GP, b0=0)          # [B, N, GP] views
+        omega_l1 = la.solve_augmented(U0, N, GP, a0=GP, b0=0)
+        omega_chg = torch.addcmul(omega, Dg[:, 0].unsqueeze(-1), omega_l1, value=-1.0)
+        # (25): r_tilde = omega' r, risk = gamma omega' Sigma omega (Sigma in low-rank form:
+        # X (F (X' omega)) + ivol o omega), tc = w omega_chg' Lambda omega_chg, denom
+        omega = omega.contiguous()
+        omega_chg = omega_chg.contiguous()
+        rt_ = torch.bmm(omega.transpose(1, 2), bt.r.unsqueeze(-1)).squeeze(-1)   # [B, GP]
+        XtO = torch.empty((B, Xl.shape[2], GP), dtype=torch.float64, device=dev)
+        gemm_fused(Xl, omega, XtO, trans_a=True)
+        FXO = torch.bmm(Fb, XtO)
+        SO = torch.empty_like(omega)
+        gemm_fused(Xl, FXO, SO, addend=omega, addend_row_scale=iv)
+        lw = (bt.lam * bt.w.view(B, 1)).contiguous()
+        Dt = torch.empty((B, Pp, Pp), dtype=torch.float64, device=dev)
+        Dk = torch.empty_like(Dt) if keep_risk_tc else None
         for g in range(G):
+            sl = slice(b0, b0 + B)
             if g >= Gc:                                  # shared block (quirk Q1)
-                d_out[g, b0:b0 + B] = d_out[0, b0:b0 + B]
-                r_out[g, b0:b0 + B] = r_out[0, b0:b0 + B]
+                d_out[g, sl] = d_out[0, sl]
+                r_out[g, sl] = r_out[0, sl]
                 if keep_risk_tc:
-                    risk_out[g, b0:b0 + B] = risk_out[0, b0:b0 + B]
-                    tc_out[g, b0:b0 + B] = tc_out[0, b0:b0 + B]
+                    risk_out[g, sl] = risk_out[0, sl]
+                    tc_out[g, sl] = tc_out[0, sl]
                 for bi in range(B):
                     signal_t[g][b0 + bi] = signal_t[0][b0 + bi]
                 continue
-            sl = slice(g * P, (g + 1) * P)
-            og, cg = omega[:, :, sl].contiguous(), omega_chg[:, :, sl].contiguous()
-            risk = gemm_prec(og, SO[:, :, sl].contiguous(), prec, trans_a=True, alpha=gamma)
-            tc = gemm(cg, lw.unsqueeze(-1) * cg, trans_a=True)
-            d_out[g, b0:b0 + B] = risk + tc
-            r_out[g, b0:b0 + B] = rt_[:, sl]
+            cs = slice(g * Pp, (g + 1) * Pp)
+            og, cg, sg = omega[:, :, cs], omega_chg[:, :, cs], SO[:, :, cs]
+            if prec == "fp64":
+                gemm_fused(og, sg, Dt, trans_a=True, alpha=gamma)
+            else:
+                gemm_prec(og.contiguous(), sg.contiguous(), prec, trans_a=True, alpha=gamma,
+                          out=Dt)
             if keep_risk_tc:
-                risk_out[g, b0:b0 + B] = risk
-                tc_out[g, b0:b0 + B] = tc
+                risk_out[g, sl] = Dt[:, :P, :P]
+                gemm_fused(cg, cg, Dk, trans_a=True, k_scale=lw)
+                tc_out[g, sl] = Dk[:, :P, :P]
+                Dt.add_(Dk)
+            else:
+                gemm_fused(cg, cg, Dt, trans_a=True, k_scale=lw, beta=1.0)
+            d_out[g, sl] = Dt[:, :P, :P]
+            r_out[g, sl] = rt_[:, g * Pp:g * Pp + P]
             for bi in range(B):
-                signal_t[g][b0 + bi] = S_all[g][bi, 0, : ns[bi]].clone()
+                signal_t[g][b0 + bi] = sig0[bi, : int(bt.ns[bi]), g * Pp:g * Pp + P]
         range_pop()
-        log.info(f"PFML inputs: months {b0 + B}/{T}")
-    reals = PfmlReals(months=months, r_tilde=r_out, denom=d_out, risk=risk_out, tc=tc_out)
-    return PfmlInputs(reals=reals, months=months, signal_rows=sig_rows, signal_t=signal_t,
-                      rff_w=W, ids=sig_ids)
+        b0 += B
+        log.info(f"PFML inputs: months {b0}/{T}")
+    reals = PfmlReals(months=plan.months, r_tilde=r_out, denom=d_out, risk=risk_out, tc=tc_out)
+    return PfmlInputs(reals=reals, months=plan.months, signal_rows=plan.sig_rows,
+                      signal_t=signal_t, rff_w=plan.W, ids=plan.sig_ids)
+
+
+def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.DataFrame,
+                 risk_free: pd.DataFrame, device, months: np.ndarray | None = None,
+                 keep_risk_tc: bool = False, batch: int | None = None,
+                 plan: S4Plan | None = None) -> PfmlInputs:
+    """S4 for ``months`` (default dates_m2): ``make_s4_plan`` + ``run_plan``."""
+    if plan is None:
+        plan = make_s4_plan(cfg, chars, barra, wealth, risk_free, device, months, batch)
+    return run_plan(plan, cfg, keep_risk_tc)
 
 
 def to_reference_order(x: torch.Tensor, p_max: int, dims: tuple = (-1,)) -> torch.Tensor:

@@ -21,6 +21,19 @@ import torch
 from . import _native as nat
 
 _P, _I, _L, _D = C.c_void_p, C.c_int, C.c_int64, C.c_double
+
+
+class _Epi(C.Structure):
+    """Mirror of ``PfmlGemmEpi`` (csrc/gemm_f64.hip)."""
+    _fields_ = [("alpha", _D), ("beta", _D), ("rs", _P), ("srs", _L), ("cs", _P), ("scs", _L),
+                ("ks", _P), ("sks", _L), ("E", _P), ("lde", _L), ("sE", _L), ("e_cols", _I),
+                ("diag_col0", _I), ("dval", _D), ("dv", _P), ("sdv", _L), ("has_diag", _I),
+                ("es", _P), ("ses", _L), ("tile_cfg", _I)]
+
+
+nat.register_hip("pfml_dgemm_ex", [_I, _I, _I, _I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _L,
+                                   C.POINTER(_Epi), _P])
+nat.register_hip("pfml_gemm_epi_size", [])
 nat.register_hip("pfml_gemm_lowp", [_I, _I, _I, _I, _I, _I, _I, _D, _P, _L, _L, _P, _L, _L, _D,
                                     _P, _L, _L, _P, _P, _P])
 LOWP_FORMATS = {"bf16": 1, "fp8": 2}
@@ -193,3 +206,94 @@ def gemm_prec(A: torch.Tensor, B: torch.Tensor, precision: str = "fp64", **kw) -
     if precision == "fp32":
         return gemm_fp32(A, B, **kw)
     return gemm(A, B, **kw)
+
+
+def _vec3(v, batch):
+    """[n] or [B, n] scale vector -> (3-D-compatible tensor, batch stride)."""
+    if v is None:
+        return None, 0
+    v2 = v.unsqueeze(0) if v.dim() == 1 else v
+    if v2.stride(-1) != 1:
+        v2 = v2.contiguous()
+    return v2, (0 if (v2.shape[0] == 1 and batch > 1) else v2.stride(0))
+
+
+def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: bool = False,
+               trans_b: bool = False, alpha: float = 1.0, beta: float = 0.0,
+               row_scale: torch.Tensor | None = None, col_scale: torch.Tensor | None = None,
+               k_scale: torch.Tensor | None = None, addend: torch.Tensor | None = None,
+               addend_cols: int | None = None, diag_col0: int | None = None,
+               diag_value: float = 1.0, diag_vec: torch.Tensor | None = None,
+               addend_row_scale: torch.Tensor | None = None, tile_cfg: int = 0) -> torch.Tensor:
+    """out = alpha diag(rs) op(A) diag(ks) op(B) diag(cs) + beta out
+             + diag(es) addend[:, :, :addend_cols]  (on out's first addend_cols columns)
+             + diag(diag_vec or diag_value) placed at out[:, i, diag_col0 + i].
+
+    One launch of csrc/gemm_f64.hip on a HIP device (the Horner step of (24), Sigma = X F X'
+    + diag(ivol), ...); the same arithmetic in torch fp64 on CPU.  3-D batched operands
+    (batch stride 0 = broadcast); scale vectors are [n] or [B, n]."""
+    A3, B3, C3 = _as3(A), _as3(B), _as3(out)
+    batch = C3.shape[0]
+    M = A3.shape[2] if trans_a else A3.shape[1]
+    K = A3.shape[1] if trans_a else A3.shape[2]
+    N = B3.shape[1] if trans_b else B3.shape[2]
+    if (B3.shape[2] if trans_b else B3.shape[1]) != K or tuple(C3.shape[1:]) != (M, N):
+        raise ValueError(f"gemm_fused: shapes {tuple(A3.shape)} {tuple(B3.shape)} -> {tuple(C3.shape)}")
+    if addend is not None and addend_cols is None:
+        addend_cols = N
+    E3 = None if addend is None else _as3(addend)
+    if nat.is_device(A):
+        for x, nm in ((A3, "A"), (B3, "B"), (C3, "out")):
+            if x.stride(-1) != 1:
+                raise ValueError(f"gemm_fused: {nm} needs unit inner stride")
+        if E3 is not None and E3.stride(-1) != 1:
+            raise ValueError("gemm_fused: addend needs unit inner stride")
+        rs, srs = _vec3(row_scale, batch)
+        cs, scs = _vec3(col_scale, batch)
+        ks, sks = _vec3(k_scale, batch)
+        dv, sdv = _vec3(diag_vec, batch)
+        es, ses = _vec3(addend_row_scale, batch)
+        ep = _Epi(float(alpha), float(beta), nat.ptr(rs), srs, nat.ptr(cs), scs, nat.ptr(ks), sks,
+                  nat.ptr(E3), 0 if E3 is None else E3.stride(1),
+                  0 if E3 is None else _bstride(E3, batch), int(addend_cols or 0),
+                  int(diag_col0 or 0), float(diag_value), nat.ptr(dv), sdv,
+                  int(diag_col0 is not None), nat.ptr(es), ses, int(tile_cfg))
+        nat.check(nat.hip_lib().pfml_dgemm_ex(
+            int(trans_a), int(trans_b), M, N, K, batch,
+            A3.data_ptr(), A3.stride(1), _bstride(A3, batch),
+            B3.data_ptr(), B3.stride(1), _bstride(B3, batch),
+            C3.data_ptr(), C3.stride(1), C3.stride(0), C.byref(ep), nat.stream_of(A)),
+            "pfml_dgemm_ex")
+        return out
+    a = A3.transpose(1, 2) if trans_a else A3
+    b = B3.transpose(1, 2) if trans_b else B3
+    if k_scale is not None:
+        ksv = k_scale if k_scale.dim() == 2 else k_scale.unsqueeze(0)
+        b = b * ksv.unsqueeze(-1)
+    r = torch.matmul(a, b)
+    if row_scale is not None:
+        rsv = row_scale if row_scale.dim() == 2 else row_scale.unsqueeze(0)
+        r = r * rsv.unsqueeze(-1)
+    if col_scale is not None:
+        csv = col_scale if col_scale.dim() == 2 else col_scale.unsqueeze(0)
+        r = r * csv.unsqueeze(-2)
+    r = alpha * r
+    if beta != 0.0:
+        r = r + beta * C3
+    r = r.expand(batch, M, N).clone()
+    if E3 is not None and addend_cols:
+        Ea = E3[:, :, :addend_cols]
+        if addend_row_scale is not None:
+            esv = addend_row_scale if addend_row_scale.dim() == 2 else addend_row_scale.unsqueeze(0)
+            Ea = Ea * esv.unsqueeze(-1)
+        r[:, :, :addend_cols] += Ea
+    if diag_col0 is not None:
+        n = min(M, N - diag_col0)
+        ii = torch.arange(n, device=r.device)
+        if diag_vec is not None:
+            dvv = diag_vec if diag_vec.dim() == 2 else diag_vec.unsqueeze(0)
+            r[:, ii, diag_col0 + ii] += dvv[:, :n]
+        else:
+            r[:, ii, diag_col0 + ii] += diag_value
+    C3.copy_(r)
+    return out

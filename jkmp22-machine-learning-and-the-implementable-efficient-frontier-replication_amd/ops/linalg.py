@@ -11,10 +11,12 @@
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import torch
 
 from . import _native as nat
-from .gemm import gemm
+from .gemm import gemm, gemm_fused
 from ..utils.log import COUNTERS
 
 
@@ -22,8 +24,14 @@ def _eye_like(A: torch.Tensor) -> torch.Tensor:
     return torch.eye(A.shape[-1], dtype=A.dtype, device=A.device).expand_as(A)
 
 
-def spd_inverse(A: torch.Tensor, inplace: bool = False) -> torch.Tensor:
-    """Inverse of a batch [B, n, n] of SPD matrices."""
+def spd_inverse(A: torch.Tensor, inplace: bool = False,
+                status: torch.Tensor | None = None) -> torch.Tensor:
+    """Inverse of a batch [B, n, n] of SPD matrices.
+
+    Device: blocked Gauss-Jordan (csrc/spd_inverse.hip).  With ``status`` (a [B] int32 device
+    tensor) non-positive pivots are only flagged there - no host sync - and the caller repairs
+    the flagged matrices once, after a whole chain of inverses (m_func); without it a flagged
+    matrix is re-inverted by a pivoted LU here (one sync)."""
     squeeze = A.dim() == 2
     X = A if inplace else A.clone()
     if squeeze:
@@ -32,28 +40,21 @@ def spd_inverse(A: torch.Tensor, inplace: bool = False) -> torch.Tensor:
         X = X.contiguous() if not X.is_contiguous() else X
         B, n, _ = X.shape
         lib = nat.hip_lib()
-        status = torch.zeros(B, dtype=torch.int32, device=X.device)
+        st = status if status is not None else torch.zeros(B, dtype=torch.int32, device=X.device)
         if n >= _BLOCKED_MIN_N:
-            _spd_inverse_blocked(X, status)
+            _spd_inverse_blocked(X, st)
         else:
             work = torch.empty(lib.pfml_spd_inverse_work_doubles(n, B), dtype=torch.float64,
                                device=X.device)
             nat.check(lib.pfml_spd_inverse(X.data_ptr(), n, n, n * n, B, work.data_ptr(),
-                                           status.data_ptr(), nat.stream_of(X)),
+                                           st.data_ptr(), nat.stream_of(X)),
                       "pfml_spd_inverse")
-        bad = torch.nonzero(status).flatten()
-        if bad.numel():
-            COUNTERS.add("linalg.spd_inverse_lu_fallback", int(bad.numel()))
-            src = A.unsqueeze(0) if squeeze else A
-            import os
-            if os.environ.get("PFML_DEBUG_INV"):
-                for b in bad.tolist()[:4]:
-                    M = src[b]
-                    print(f"[spd_inverse] bad b={b} n={M.shape[-1]} nan={int(torch.isnan(M).sum())} "
-                          f"absmax={float(M.abs().max()):.3e} "
-                          f"diagmin={float(torch.diagonal(M).min()):.3e} "
-                          f"asym={float((M - M.T).abs().max()):.3e}", flush=True)
-            X[bad] = torch.linalg.inv(src[bad])
+        if status is None:
+            bad = torch.nonzero(st).flatten()
+            if bad.numel():
+                COUNTERS.add("linalg.spd_inverse_lu_fallback", int(bad.numel()))
+                src = A.unsqueeze(0) if squeeze else A
+                X[bad] = torch.linalg.inv(src[bad])
     else:
         X.copy_(torch.linalg.inv(X))
     return X.squeeze(0) if squeeze else X
@@ -63,9 +64,10 @@ _BLOCKED_MIN_N = 160
 
 
 def _spd_inverse_blocked(X: torch.Tensor, status: torch.Tensor) -> None:
-    """In-place SPD inverse with 128-wide Gauss-Jordan blocks: pivot block inverted in LDS
-    (csrc/spd_inverse.hip: pfml_spd_blockinv); row panel, rank-128 trailing update and column
-    panel as batched fp64 MFMA GEMMs."""
+    """In-place SPD inverse with 64-wide Gauss-Jordan blocks: pivot block inverted in LDS
+    (csrc/spd_inverse.hip: pfml_spd_blockinv); row panel, rank-64 trailing update and column
+    panel on the hand-written fp64 MFMA GEMM (csrc/gemm_f64.hip, 35 TF/s on the rank-64
+    update vs 28 for rocBLAS, profiles/r02_gemm_own_vs_rocblas.json)."""
     lib = nat.hip_lib()
     B, n, _ = X.shape
     NB = lib.pfml_spd_block_size()
@@ -80,12 +82,12 @@ def _spd_inverse_blocked(X: torch.Tensor, status: torch.Tensor) -> None:
                                         status.data_ptr(), st), "pfml_spd_blockinv")
         Pk = P[:, :nb, :nb]
         R = Rbuf[:, :nb, :]
-        gemm(Pk, X[:, k0:k0 + nb, :], out=R)                     # R = P A_k.
+        gemm_fused(Pk, X[:, k0:k0 + nb, :], R)                   # R = P A_k.
         C = Cbuf[:, :, :nb]
         C.copy_(X[:, :, k0:k0 + nb])                             # old column panel
-        gemm(C, R, alpha=-1.0, beta=1.0, out=X)                  # A -= C R   (rank nb)
+        gemm_fused(C, R, X, alpha=-1.0, beta=1.0)                # A -= C R   (rank nb)
         X[:, k0:k0 + nb, :] = R                                  # block rows
-        gemm(C, Pk, alpha=-1.0, out=X[:, :, k0:k0 + nb])         # block columns: -C P
+        gemm_fused(C, Pk, X[:, :, k0:k0 + nb], alpha=-1.0)       # block columns: -C P
         X[:, k0:k0 + nb, k0:k0 + nb] = Pk
 
 
@@ -138,12 +140,13 @@ def solve(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
 
 
 def sqrtm_spd(S: torch.Tensor, max_iter: int = 40, tol: float = 1e-13) -> torch.Tensor:
-    """Principal square root of a batch of symmetric PSD matrices.
+    """Principal square root of a batch of symmetric PSD matrices (reference/oracle form).
 
     Scaled product-form Denman-Beavers (Higham, Functions of Matrices, (6.29)):
         M_{k+1} = (I + (mu^2 M_k + mu^-2 M_k^-1)/2)/2,  Y_{k+1} = mu Y_k (I + mu^-2 M_k^-1)/2
     with M_0 = Y_0 = S and norm scaling mu^4 = ||M^-1||_F / ||M||_F; stops when every
-    ||M_k - I||_F < tol * sqrt(n).
+    ||M_k - I||_F < tol * sqrt(n).  The production path is ``_db_sqrt`` (fixed iteration count,
+    no host synchronisation).
     """
     M = S.clone()
     Y = S.clone()
@@ -170,6 +173,161 @@ def sqrtm_spd(S: torch.Tensor, max_iter: int = 40, tol: float = 1e-13) -> torch.
     return 0.5 * (Y + Y.transpose(-1, -2))
 
 
+# ---------------------------------------------------------------------------------------
+# Fused symmetric passes (csrc/s4.hip) and the device m_func
+# ---------------------------------------------------------------------------------------
+MF_X, MF_FIX, MF_DB, MF_SHAT = 0, 1, 2, 3
+
+
+class _MfArgs(C.Structure):
+    _fields_ = [("mode", C.c_int), ("B", C.c_int), ("N", C.c_int), ("ld", C.c_int64),
+                ("sX", C.c_int64), ("X", C.c_void_p), ("Y", C.c_void_p), ("out", C.c_void_p),
+                ("svec", C.c_void_p), ("cvec", C.c_void_p), ("a", C.c_void_p),
+                ("mask", C.c_void_p), ("sv", C.c_int64), ("d", C.c_double)]
+
+
+nat.register_hip("pfml_mfunc_sym", [C.POINTER(_MfArgs), C.c_void_p])
+nat.register_hip("pfml_mf_args_size", [])
+nat.register_hip("pfml_db_mu", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_int64,
+                                C.c_int, C.c_void_p, C.c_void_p, C.c_void_p])
+nat.register_hip("pfml_db_mu_work_doubles", [C.c_int])
+
+
+def _sym(x: torch.Tensor) -> torch.Tensor:
+    return 0.5 * (x + x.transpose(-1, -2))
+
+
+def mf_sym(mode: int, X: torch.Tensor, Y: torch.Tensor | None, out: torch.Tensor, *,
+           svec: torch.Tensor | None = None, cvec: torch.Tensor | None = None,
+           a: torch.Tensor | None = None, mask: torch.Tensor | None = None,
+           d: float = 0.0) -> torch.Tensor:
+    """One fused symmetric pass over a [B, N, N] batch (csrc/s4.hip, header for the modes);
+    the CPU branch is the torch oracle of the same formulas."""
+    B, N, _ = X.shape
+    if nat.is_device(X):
+        for t in (X, Y, out):
+            if t is not None and (not t.is_contiguous() or t.shape != X.shape):
+                raise ValueError("mf_sym: contiguous [B, N, N] operands required")
+        sv = 0 if a is None else a.stride(0)
+        if mask is not None and a is not None and mask.stride(0) != sv:
+            raise ValueError("mf_sym: a and mask need the same batch stride")
+        if mask is not None and a is None:
+            sv = mask.stride(0)
+        args = _MfArgs(mode, B, N, N, N * N, X.data_ptr(), nat.ptr(Y), out.data_ptr(),
+                       nat.ptr(svec), nat.ptr(cvec), nat.ptr(a), nat.ptr(mask), sv, float(d))
+        nat.check(nat.hip_lib().pfml_mfunc_sym(C.byref(args), nat.stream_of(X)), "pfml_mfunc_sym")
+        return out
+    xs = _sym(X)
+    ys = _sym(Y) if Y is not None else None
+    eye = torch.eye(N, dtype=X.dtype, device=X.device)
+    if mode == MF_X:
+        r = svec.view(B, 1, 1) * a.unsqueeze(-1) * a.unsqueeze(-2) * xs
+    elif mode == MF_FIX:
+        ic2 = (1.0 / (cvec * cvec)).view(B, 1, 1)
+        mm = mask.unsqueeze(-1) * mask.unsqueeze(-2)
+        r = xs * (svec.view(B, 1, 1) * a.unsqueeze(-1) * a.unsqueeze(-2) - ys * ic2) - ys * mm
+        r = r + torch.diag_embed(1.0 + torch.diagonal(mm, dim1=-2, dim2=-1)
+                                 + torch.diagonal(xs, dim1=-2, dim2=-1) * ic2.view(B, 1))
+    elif mode == MF_DB:
+        mu2 = (svec * svec).view(B, 1, 1)
+        r = 0.25 * (mu2 * xs + ys / mu2) + 0.5 * eye
+    else:
+        r = xs + (ys if ys is not None else 0.0) + d * eye
+    out.copy_(r)
+    return out
+
+
+def _db_mu(M: torch.Tensor, Minv: torch.Tensor, unscaled: bool, out: torch.Tensor) -> None:
+    B, N, _ = M.shape
+    if nat.is_device(M):
+        lib = nat.hip_lib()
+        work = torch.empty(lib.pfml_db_mu_work_doubles(B), dtype=torch.float64, device=M.device)
+        nat.check(lib.pfml_db_mu(M.data_ptr(), Minv.data_ptr(), B, N, N, N * N, int(unscaled),
+                                 out.data_ptr(), work.data_ptr(), nat.stream_of(M)), "pfml_db_mu")
+        return
+    if unscaled:
+        out.fill_(1.0)
+    else:
+        nm = torch.linalg.matrix_norm(M).clamp_min(1e-300)
+        out.copy_((torch.linalg.matrix_norm(Minv) / nm) ** 0.25)
+
+
+def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tensor | None,
+             ws: list) -> torch.Tensor:
+    """sqrtm(S) by ``iters`` scaled product-form Denman-Beavers steps with NO host sync:
+    norm scaling mu (computed on the device) for the first ``scaled_iters`` steps, then
+    quadratically convergent unscaled steps.  ws: 4 [B, N, N] work buffers."""
+    B, N, _ = S.shape
+    M, Y, Mi, Yn = ws
+    M.copy_(S)
+    Y.copy_(S)
+    mu = torch.empty(B, dtype=S.dtype, device=S.device)
+    for it in range(iters):
+        Mi.copy_(M)
+        spd_inverse(Mi, inplace=True, status=status)
+        _db_mu(M, Mi, it >= scaled_iters, mu)
+        # Y' = (mu/2) Y + (1/(2 mu)) Y M^-1 ;  M' = I/2 + (mu^2 M + mu^-2 M^-1)/4
+        rs = (0.5 / mu).view(B, 1).expand(B, N).contiguous()
+        es = (0.5 * mu).view(B, 1).expand(B, N).contiguous()
+        gemm_fused(Y, Mi, Yn, row_scale=rs, addend=Y, addend_row_scale=es)
+        Y, Yn = Yn, Y
+        mf_sym(MF_DB, M, Mi, Yn, svec=mu)        # Yn is free here: new M into it
+        M, Yn = Yn, M
+    ws[0], ws[1], ws[2], ws[3] = M, Y, Mi, Yn
+    return Y
+
+
+# Denman-Beavers steps: 8 reach 1e-14 parity with the reference's scipy sqrtm m_func on
+# production spectra (cond(x^2 + 4x) ~ 1e5-1e7, TC on and off; tests/test_gpu_pipeline.py,
+# tests/test_golden.py); one more for margin.  Norm scaling in the first 6.
+DB_ITERS = 9
+DB_SCALED_ITERS = 6
+
+
+def m_tilde(sigma: torch.Tensor, lam: torch.Tensor, w: torch.Tensor, rf: torch.Tensor,
+            mu: float, gamma: float, iterations: int = 10, mask: torch.Tensor | None = None,
+            db_iters: int = DB_ITERS) -> tuple[torch.Tensor, torch.Tensor]:
+    """m_tilde of Lemma 1 and a = lambda^-1/2, so that m = diag(a) m_tilde diag(1/a)
+    (General_functions.py:941-963).  All on the device with no host synchronisation except one
+    status check at the end (matrices whose SPD inverse met a non-positive pivot anywhere in
+    the chain are recomputed by the reference-form ``m_func_reference``)."""
+    B, N, _ = sigma.shape
+    dt, dev = sigma.dtype, sigma.device
+    if mask is None:
+        mask = torch.ones((B, N), dtype=dt, device=dev)
+    mask = mask.contiguous()
+    a = lam.rsqrt().contiguous()
+    s = (gamma / w).to(dt).contiguous()
+    c = (1.0 + rf + mu).to(dt).contiguous()
+    sigma = sigma.contiguous()
+    status = torch.zeros(B, dtype=torch.int32, device=dev) if nat.is_device(sigma) else None
+    x = torch.empty_like(sigma)
+    mf_sym(MF_X, sigma, None, x, svec=s, a=a)                   # x = s L^-1/2 S L^-1/2
+    S = torch.empty_like(sigma)
+    four = torch.full((B, N), 4.0, dtype=dt, device=dev)
+    gemm_fused(x, x, S, addend=x, addend_row_scale=four)         # sigma_hat^2 - 4I = x^2 + 4x
+    ws = [torch.empty_like(sigma) for _ in range(4)]
+    root = _db_sqrt(S, db_iters, DB_SCALED_ITERS, status, ws)
+    # m_tilde_0 = (sigma_hat - root)/2 = 2 (sigma_hat + root)^-1   (cancellation-free form)
+    mt = ws[2]
+    mf_sym(MF_SHAT, x, root, mt, d=2.0)
+    spd_inverse(mt, inplace=True, status=status)
+    mt.mul_(2.0)
+    Aq = ws[3]
+    for _ in range(iterations):
+        mf_sym(MF_FIX, sigma, mt, Aq, svec=s, cvec=c, a=a, mask=mask)
+        spd_inverse(Aq, inplace=True, status=status)
+        mt, Aq = Aq, mt
+    if status is not None:
+        bad = torch.nonzero(status).flatten()
+        if bad.numel():
+            COUNTERS.add("linalg.m_func_repaired", int(bad.numel()))
+            ref = m_func_reference(sigma[bad], lam[bad], w[bad], rf[bad], mu, gamma, iterations,
+                                   mask=mask[bad])
+            mt[bad] = ref * a[bad].unsqueeze(-2) / a[bad].unsqueeze(-1)
+    return mt, a
+
+
 def m_func(sigma: torch.Tensor, lam: torch.Tensor, w: torch.Tensor, rf: torch.Tensor,
            mu: float, gamma: float, iterations: int = 10,
            mask: torch.Tensor | None = None) -> torch.Tensor:
@@ -178,6 +336,16 @@ def m_func(sigma: torch.Tensor, lam: torch.Tensor, w: torch.Tensor, rf: torch.Te
     sigma: [B, N, N] Barra covariance (padded entries: identity block), lam: [B, N] Kyle's
     lambda, w: [B] wealth, rf: [B]; mask: [B, N] 1 for real stocks (0 = padding: the rank-one
     mu_bar mu_bar' term of sigma_gr is restricted to real stocks so the pad block decouples).
+    """
+    mt, a = m_tilde(sigma, lam, w, rf, mu, gamma, iterations, mask)
+    return mt * a.unsqueeze(-1) / a.unsqueeze(-2)
+
+
+def m_func_reference(sigma: torch.Tensor, lam: torch.Tensor, w: torch.Tensor, rf: torch.Tensor,
+                     mu: float, gamma: float, iterations: int = 10,
+                     mask: torch.Tensor | None = None) -> torch.Tensor:
+    """Reference-form m_func in plain torch ops (LU inverses, convergence-checked square root):
+    the repair path of ``m_tilde`` and the CPU oracle.
 
     m_tilde_0 = 1/2 (sigma_hat - sqrtm(sigma_hat^2 - 4I)) is evaluated in the algebraically
     identical, cancellation-free form 2 (sigma_hat + sqrtm(sigma_hat^2 - 4I))^-1.
@@ -188,19 +356,16 @@ def m_func(sigma: torch.Tensor, lam: torch.Tensor, w: torch.Tensor, rf: torch.Te
         mask = torch.ones((B, N), dtype=dt, device=sigma.device)
     c = (1.0 + rf + mu).view(B, 1, 1)
     I = _eye_like(sigma)
-    sig_gr = mask.unsqueeze(-1) * mask.unsqueeze(-2) + sigma / (c * c)
+    sig = _sym(sigma)
+    sig_gr = mask.unsqueeze(-1) * mask.unsqueeze(-2) + sig / (c * c)
     a = lam.rsqrt()                                              # Lambda^-1/2 diagonal
-    x = (gamma / w).view(B, 1, 1) * sigma * a.unsqueeze(-1) * a.unsqueeze(-2)
-    x = 0.5 * (x + x.transpose(-1, -2))
+    x = (gamma / w).view(B, 1, 1) * sig * a.unsqueeze(-1) * a.unsqueeze(-2)
     ydiag = 1.0 + torch.diagonal(sig_gr, dim1=-2, dim2=-1)
     sig_hat = x + 2.0 * I
-    S = gemm(sig_hat, sig_hat) - 4.0 * I
-    S = 0.5 * (S + S.transpose(-1, -2))
-    root = sqrtm_spd(S)
-    mt = 2.0 * spd_inverse(sig_hat + root)
+    S = _sym(x @ x + 4.0 * x)
+    root = sqrtm_spd(S.cpu()).to(sigma.device) if nat.is_device(S) else sqrtm_spd(S)
+    mt = 2.0 * torch.linalg.inv(_sym(sig_hat + root))
     base = x + torch.diag_embed(ydiag)
     for _ in range(iterations):
-        Aq = base - mt * sig_gr
-        Aq = 0.5 * (Aq + Aq.transpose(-1, -2))
-        mt = spd_inverse(Aq)
+        mt = torch.linalg.inv(_sym(base - _sym(mt) * sig_gr))
     return mt * a.unsqueeze(-1) / a.unsqueeze(-2)

@@ -12,45 +12,65 @@ import torch
 from . import _native as nat
 from .gemm import gemm_prec
 
-nat.register_hip("pfml_rff_sincos", [C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p])
-nat.register_hip("pfml_standardize", [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
-                                      C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p])
+nat.register_hip("pfml_rff_sincos", [C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int64,
+                                     C.c_void_p])
+nat.register_hip("pfml_standardize", [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
+                                      C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                      C.c_int64, C.c_int64, C.c_int, C.c_void_p])
 
 
-def rff_features(X: torch.Tensor, W: torch.Tensor, precision: str = "fp64") -> torch.Tensor:
-    """[R, k] x [k, P/2] -> [R, P+1] rows [1, cos z1, sin z1, cos z2, sin z2, ...].
-    ``precision`` fp32 / bf16 / fp8: X W in reduced precision (experimental configs)."""
+def rff_features(X: torch.Tensor, W: torch.Tensor, precision: str = "fp64",
+                 width: int | None = None, pad_rows: int = 0) -> torch.Tensor:
+    """[R, k] x [k, P/2] -> [R + pad_rows, width] rows [1, cos z1, sin z1, cos z2, sin z2, ...,
+    0 ...] (P = 2 (P/2) + 1 real columns; ``width`` >= P pads with zero columns, ``pad_rows``
+    appends all-zero rows).  X W is one fp64 MFMA GEMM, cos/sin one sincos kernel (two launches;
+    ``precision`` fp32 / bf16 / fp8 lowers X W for the experimental configs)."""
     R, half = X.shape[0], W.shape[1]
+    P = 2 * half + 1
+    width = width or P
     Z = gemm_prec(X, W, precision)
-    out = torch.empty((R, 2 * half + 1), dtype=X.dtype, device=X.device)
     if nat.is_device(X):
+        out = torch.empty((R + pad_rows, width), dtype=X.dtype, device=X.device)
+        if pad_rows:
+            out[R:].zero_()
         Zc = Z.contiguous()
-        nat.check(nat.hip_lib().pfml_rff_sincos(Zc.data_ptr(), R, half, out.data_ptr(),
+        nat.check(nat.hip_lib().pfml_rff_sincos(Zc.data_ptr(), R, half, out.data_ptr(), width,
                                                 nat.stream_of(X)), "pfml_rff_sincos")
     else:
-        out[:, 0] = 1.0
-        out[:, 1::2] = torch.cos(Z)
-        out[:, 2::2] = torch.sin(Z)
+        out = torch.zeros((R + pad_rows, width), dtype=X.dtype, device=X.device)
+        out[:R, 0] = 1.0
+        out[:R, 1:P:2] = torch.cos(Z)
+        out[:R, 2:P:2] = torch.sin(Z)
     return out
 
 
 def standardize_signals(F: torch.Tensor, idx: torch.Tensor, mask: torch.Tensor,
-                        vol: torch.Tensor) -> torch.Tensor:
+                        vol: torch.Tensor, P: int | None = None, out: torch.Tensor | None = None,
+                        n_real: torch.Tensor | None = None) -> torch.Tensor:
     """Gather + standardise the signal windows.
 
-    F: [R+1, P] panel features (last row all zero, used for padding), idx: [B, TH, N] rows,
-    mask: [B, N] 1 for real stocks (real rows first), vol: [R+1].  Returns [B, TH, N, P]."""
+    F: [R+1, >= P] panel features (last row all zero, used for padding; P real columns),
+    idx: [B, TH, N] rows, mask: [B, N] 1 for real stocks (real rows first), vol: [R+1].
+    Returns [B, TH, N, Pw]: ``out`` may be a column block view of a wider buffer (e.g. one g's
+    block of the [B, TH, N, G*Pw] S4 signal stack), columns P..Pw-1 come out zero."""
     B, TH, N = idx.shape
-    P = F.shape[1]
-    if nat.is_device(F):
+    P = P or F.shape[1]
+    if out is None:
         out = torch.empty((B, TH, N, P), dtype=F.dtype, device=F.device)
-        n_real = mask.sum(1).to(torch.int32).contiguous()
+    Pw = out.shape[-1]
+    if nat.is_device(F):
+        if out.stride(-1) != 1 or out.stride(1) != N * out.stride(2) or F.stride(-1) != 1:
+            raise ValueError("standardize_signals: unsupported output layout")
+        if n_real is None:
+            n_real = mask.sum(1).to(torch.int32)
+        n_real = n_real.to(torch.int32).contiguous()
         rows = idx.to(torch.int64).contiguous()
-        nat.check(nat.hip_lib().pfml_standardize(F.data_ptr(), P, rows.data_ptr(),
-                                                 n_real.data_ptr(), B, TH, N, vol.data_ptr(),
-                                                 out.data_ptr(), nat.stream_of(F)),
-                  "pfml_standardize")
+        nat.check(nat.hip_lib().pfml_standardize(
+            F.data_ptr(), P, F.stride(0), rows.data_ptr(), n_real.data_ptr(), B, TH, N,
+            vol.data_ptr(), out.data_ptr(), out.stride(2), out.stride(1), Pw,
+            nat.stream_of(F)), "pfml_standardize")
         return out
+    F = F[:, :P]
     S = F[idx]                                                  # [B, TH, N, P]
     m = mask.view(B, 1, N, 1)
     n = mask.sum(1).view(B, 1, 1, 1)
@@ -60,4 +80,6 @@ def standardize_signals(F: torch.Tensor, idx: torch.Tensor, mask: torch.Tensor,
     norm = torch.sqrt(1.0 / (S * S).sum(2, keepdim=True))
     S = S * norm
     v = vol[idx].unsqueeze(-1)
-    return S / v
+    out.zero_()
+    out[..., :P] = S / v
+    return out

@@ -55,6 +55,44 @@ def test_dgemm_matches_torch(gpu, ta, tb, shape):
         assert err2 < 1e-13, (be, err2)
 
 
+def test_gemm_epi_struct_matches():
+    import ctypes
+    from pfml.ops import _native as nat
+    from pfml.ops.gemm import _Epi
+    assert nat.hip_lib().pfml_gemm_epi_size() == ctypes.sizeof(_Epi)
+
+
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("cfg", [1, 2, 3])
+@pytest.mark.parametrize("shape", [(2, 37, 53, 29), (3, 130, 258, 100), (2, 96, 224, 96)])
+def test_gemm_fused_matches_torch(gpu, ta, tb, cfg, shape):
+    """Every fusion of csrc/gemm_f64.hip (k-scale prologue, row/col scale, beta, addend block,
+    diagonal vector) vs the fp64 torch oracle, for odd (scalar staging) and even (16-byte
+    staging) dimensions and every tile config."""
+    from pfml.ops.gemm import gemm_fused
+    b, M, N, K = shape
+    A = _rand(b, K, M, seed=1) if ta else _rand(b, M, K, seed=1)
+    B = _rand(b, N, K, seed=2) if tb else _rand(b, K, N, seed=2)
+    kw = dict(trans_a=ta, trans_b=tb, alpha=0.7, beta=0.3, row_scale=_rand(b, M, seed=3),
+              col_scale=_rand(N, seed=4), k_scale=_rand(b, K, seed=6),
+              addend=_rand(b, M, N // 2, seed=8), addend_cols=N // 2, diag_col0=N // 3,
+              diag_vec=_rand(b, M, seed=9), addend_row_scale=_rand(b, M, seed=11))
+    C0 = _rand(b, M, N, seed=5)
+    ref = gemm_fused(A, B, C0.clone(), **kw)
+    kd = {k: (v.to(gpu) if isinstance(v, torch.Tensor) else v) for k, v in kw.items()}
+    out = gemm_fused(A.to(gpu), B.to(gpu), C0.to(gpu), tile_cfg=cfg, **kd).cpu()
+    err = (out - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-13, err
+    # Horner form: identity block via a constant diagonal, broadcast A (batch stride 0)
+    E = _rand(b, M, 8, seed=10)
+    ref = gemm_fused(A[:1], B, C0.clone(), trans_a=ta, trans_b=tb, addend=E, addend_cols=8,
+                     diag_col0=8, diag_value=1.0)
+    out = gemm_fused(A[:1].to(gpu), B.to(gpu), C0.to(gpu), trans_a=ta, trans_b=tb,
+                     addend=E.to(gpu), addend_cols=8, diag_col0=8, diag_value=1.0,
+                     tile_cfg=cfg).cpu()
+    assert (out - ref).abs().max().item() / ref.abs().max().item() < 1e-13
+
+
 def test_segment_sums(gpu):
     from pfml.ops.ridge import segment_sums
     X = _rand(40, 7, 9, seed=7)

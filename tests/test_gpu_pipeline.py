@@ -40,11 +40,73 @@ def test_m_func_gpu_matches_cpu(gpu):
     F = np.stack([np.cov(rng.normal(size=(K, 200))) * 2e-2 for _ in range(B)])
     S = np.einsum("bik,bkl,bjl->bij", X, F, X) + np.stack([np.diag(rng.uniform(0.01, 0.03, N) ** 2 * 21) for _ in range(B)])
     lam = 0.2 / rng.uniform(1e7, 1e9, (B, N))
-    args = (torch.tensor(S), torch.tensor(lam), torch.tensor([1e10, 5e9, 2e10]),
-            torch.tensor([0.003, 0.001, 0.0]), 0.007, 10.0, 10)
+    f64 = dict(dtype=torch.float64)
+    args = (torch.tensor(S), torch.tensor(lam), torch.tensor([1e10, 5e9, 2e10], **f64),
+            torch.tensor([0.003, 0.001, 0.0], **f64), 0.007, 10.0, 10)
     ref = m_func(*args)
     got = m_func(*[a.to(gpu) if isinstance(a, torch.Tensor) else a for a in args]).cpu()
-    assert (got - ref).abs().max().item() / ref.abs().max().item() < 1e-10
+    assert (got - ref).abs().max().item() / ref.abs().max().item() < 1e-12
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("N", [37, 96])
+def test_mf_sym_modes(gpu, mode, N):
+    """csrc/s4.hip fused symmetric passes vs their torch oracle (asymmetric inputs, so the
+    LDS mirror-tile symmetrisation is exercised)."""
+    from pfml.ops.linalg import mf_sym
+    B = 3
+    X, Y = _rand(B, N, N, seed=1), _rand(B, N, N, seed=2)
+    kw = dict(svec=_rand(B, seed=3).abs() + 0.5, cvec=_rand(B, seed=4).abs() + 1.0,
+              a=_rand(B, N, seed=5).abs() + 0.1, mask=(torch.rand(B, N) > 0.2).double(), d=1.5)
+    ref = mf_sym(mode, X, Y, torch.empty_like(X), **kw)
+    kd = {k: (v.to(gpu) if isinstance(v, torch.Tensor) else v) for k, v in kw.items()}
+    got = mf_sym(mode, X.to(gpu), Y.to(gpu), torch.empty_like(X).to(gpu), **kd).cpu()
+    assert (got - ref).abs().max().item() / ref.abs().max().item() < 1e-14
+    assert torch.equal(got, got.transpose(1, 2))                  # exactly symmetric
+
+
+def test_db_sqrt_device_matches_eigh(gpu):
+    """Fixed-count, sync-free Denman-Beavers (device mu scaling) vs an eigh square root."""
+    from pfml.ops.linalg import DB_ITERS, DB_SCALED_ITERS, _db_sqrt
+    B, N = 2, 200
+    X = _rand(B, N + 40, N, seed=7)
+    S = X.transpose(1, 2) @ X / N
+    S = S @ S + 1e-3 * torch.eye(N, dtype=torch.float64)           # cond ~ 1e6
+    e, V = torch.linalg.eigh(S)
+    ref = V @ torch.diag_embed(e.sqrt()) @ V.transpose(1, 2)
+    st = torch.zeros(B, dtype=torch.int32, device=gpu)
+    Sd = S.to(gpu)
+    ws = [torch.empty_like(Sd) for _ in range(4)]
+    got = _db_sqrt(Sd, DB_ITERS, DB_SCALED_ITERS, st, ws).cpu()
+    assert int(st.sum()) == 0
+    assert (got - ref).abs().max().item() / ref.abs().max().item() < 1e-12
+
+
+@pytest.mark.parametrize("tc", [True, False])
+def test_m_tilde_production_shape(gpu, tc):
+    """m at N = 496 (padded S&P 500 width) on the device vs the reference-form torch m_func
+    (LU inverses, convergence-checked square root), with padded rows."""
+    from pfml.ops.linalg import m_func_reference, m_tilde
+    rng = np.random.default_rng(1)
+    B, N, K, n = 2, 496, 25, 489
+    X = rng.normal(size=(B, N, K))
+    X[:, n:] = 0.0
+    F = np.stack([np.cov(rng.normal(size=(K, 300))) * 21e-4 for _ in range(B)])
+    iv = rng.uniform(0.01, 0.03, (B, N)) ** 2 * 21
+    iv[:, n:] = 1.0
+    S = np.einsum("bik,bkl,bjl->bij", X, F, X) + np.stack([np.diag(v) for v in iv])
+    w = np.array([1e10, 3e9])
+    lam = 0.2 / rng.uniform(1e7, 1e9, (B, N)) if tc else np.full((B, N), 1e-16)
+    lam[:, n:] = 10.0 / w[:, None]
+    mask = np.zeros((B, N))
+    mask[:, :n] = 1.0
+    t = lambda v: torch.tensor(v, dtype=torch.float64)                      # noqa: E731
+    args = (t(S), t(lam), t(w), t([0.003, 0.001]), 0.007, 10.0, 10)
+    ref = m_func_reference(*args, mask=t(mask))
+    mt, a = m_tilde(*[x.to(gpu) if isinstance(x, torch.Tensor) else x for x in args],
+                    mask=t(mask).to(gpu))
+    got = (mt * a.unsqueeze(-1) / a.unsqueeze(-2)).cpu()
+    assert (got - ref).abs().max().item() / ref.abs().max().item() < 1e-12
 
 
 def test_rff_and_standardize(gpu):
@@ -63,6 +125,16 @@ def test_rff_and_standardize(gpu):
     ref = standardize_signals(Fz, idx, mask, vol)
     got = standardize_signals(Fz.to(gpu), idx.to(gpu), mask.to(gpu), vol.to(gpu)).cpu()
     assert torch.allclose(got, ref, rtol=1e-11, atol=1e-12)
+    # strided write into one g block of a padded, g-interleaved stack (S4 layout)
+    P = F.shape[1]
+    Fw = rff_features(X.to(gpu), W.to(gpu), width=P + 1, pad_rows=1)
+    assert torch.equal(Fw[:300, :P].cpu(), Fd) and not Fw[300:].any() and not Fw[:, P:].any()
+    stack = torch.full((2, 13, 40, 2 * (P + 1)), 7.0, dtype=torch.float64, device=gpu)
+    standardize_signals(Fw, idx.to(gpu), mask.to(gpu), vol.to(gpu), P=P,
+                        out=stack[..., P + 1:])
+    blk = stack[..., P + 1:].cpu()
+    assert torch.allclose(blk[..., :P], ref, rtol=1e-11, atol=1e-12)
+    assert not blk[..., P:].any() and bool((stack[..., :P + 1] == 7.0).all())
 
 
 def test_pfml_inputs_gpu_matches_cpu(gpu, small_data):
@@ -82,7 +154,11 @@ def test_pfml_inputs_gpu_matches_cpu(gpu, small_data):
     cpu = build_inputs(cfg, chars, barra, wealth, rf, "cpu", months=months)
     dev = build_inputs(cfg, chars, barra, wealth, rf, gpu, months=months)
     for a, b in [(dev.reals.r_tilde.cpu(), cpu.reals.r_tilde), (dev.reals.denom.cpu(), cpu.reals.denom)]:
-        assert (a - b).abs().max().item() / b.abs().max().item() < 1e-9
+        assert (a - b).abs().max().item() / b.abs().max().item() < 1e-11
+    for g in range(len(cpu.signal_t)):
+        for i in (0, 5, 23):
+            assert torch.allclose(dev.signal_t[g][i].cpu(), cpu.signal_t[g][i], rtol=1e-12,
+                                  atol=1e-13)
 
 
 def test_full_pipeline_gpu(gpu, small_data, tmp_path):
