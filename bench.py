@@ -19,6 +19,14 @@ end; the time reported is the max over ranks.
 
 Data: synthetic per-month summands of the production shape (no WRDS/JKP data exists here);
 random SPD denom_t = X_t'X_t / N with X_t ~ N(0,1) of shape 500 x 513 (S&P 500 universe).
+
+The same JSON line also carries the FULL grid-search wall-clock including the S4 input
+construction (``s4_s5_s6_wall_ms``: every PFML month's Barra Sigma, m_func, (24) Horner
+chains and (25) summands for 2 distinct g on a synthetic 500-stock universe, then S5 + S6),
+timed the same way (barrier + synchronize on both sides, max over ranks).  Multi-GPU: each
+rank builds the S4 summands of its own hp-year blocks plus the one-block validation halo
+(``search.local_month_range``) - no per-month matrix crosses ranks.  ``--no-inputs`` skips
+it; ``--with-inputs`` makes that full pipeline the timed step itself.
 """
 from __future__ import annotations
 
@@ -43,6 +51,8 @@ from pfml.parallel import dist as pdist  # noqa: E402
 from pfml.utils.dates import mi_from_ym  # noqa: E402
 
 BASELINE_SOLVES_PER_S = 808.0     # reference ridge grid, 8-core Xeon
+BASELINE_FULL_S = 3600.0          # ~1-1.5 h grid search incl. S4 (8-core Xeon)
+TINY = ["pf_ml.p_vec=[8,16]", "pf.dates.start_year=2008", "pf.dates.end_yr=2020"]
 METRIC = "PFML hp×window solves/sec (whole node); full grid-search wall-clock, S&P500"
 
 
@@ -69,10 +79,12 @@ def synthetic_reals(cfg: Config, device, n_months: int = 710, n_stocks: int = 50
 
 def one_step(reals: PfmlReals, cfg: Config, engine=None):
     if engine is not None:
-        # full grid-search wall-clock INCLUDING the S4 input construction of every month
-        from pfml.models.pfml_inputs import build_inputs
-        chars, barra, wealth, rf, dev, months = engine
-        reals = build_inputs(cfg, chars, barra, wealth, rf, dev, months=months).reals
+        # full grid-search wall-clock INCLUDING the S4 input construction of this rank's months
+        from pfml.models.pfml_inputs import run_plan
+        plan, all_months = engine
+        out = run_plan(plan, cfg).reals
+        reals = PfmlReals(months=out.months, r_tilde=out.r_tilde, denom=out.denom,
+                          all_months=all_months)
     res = grid_search(reals, cfg)
     G = res.obj.shape[1]
     out = []
@@ -81,6 +93,43 @@ def one_step(reals: PfmlReals, cfg: Config, engine=None):
         out.append(validation_scores(res.obj, g, cfg.run.compat_mode))
     th("validation_scores")
     return res, out
+
+
+def engine_setup(cfg: Config, env, n_stocks: int, precision: str = "fp64"):
+    """Synthetic post-prep panel + Barra model (engine_inputs) and this rank's S4 plan (index
+    layout and device copies only - the arithmetic is all in the timed step)."""
+    from pfml.data.synthetic import engine_inputs
+    from pfml.models.pfml_inputs import make_s4_plan
+    from pfml.models.search import local_month_range
+    from pfml.utils.dates import pfml_date_grids
+    cfg.run.compat_mode = False          # distinct RFF draw per g: no Q1 duplication
+    cfg.run.precision = precision
+    chars, barra, wealth, rf = engine_inputs(n_stocks=n_stocks)
+    g = pfml_date_grids(int(barra.months.min()), 11, cfg.settings["split"]["test_end"],
+                        int(cfg.settings["pf"]["dates"]["start_year"]),
+                        int(cfg.settings["pf"]["dates"]["split_years"]))
+    months = g["m2"]
+    lo, hi = local_month_range(months, cfg.hp_years, env.world_size, env.rank)
+    plan = make_s4_plan(cfg, chars, barra, wealth, rf, env.device, months[lo:hi])
+    return (plan, months), (chars, barra, wealth, rf)
+
+
+def timed(fn, steps: int, warmup: int, dev) -> float:
+    """ms per step: W untimed steps, then K steps bracketed by barrier + synchronize, max over
+    ranks."""
+    for _ in range(warmup):
+        fn()
+    pdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    pdist.barrier()
+    dt = coll.all_reduce_max(time.perf_counter() - t0, device=dev)
+    return 1000.0 * dt / max(1, steps)
 
 
 def s4_stress(args) -> None:
@@ -191,7 +240,11 @@ def main():
     ap.add_argument("--device", default="auto")
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--with-inputs", action="store_true",
-                    help="time S4 (PFML input construction for every month) + S5 + S6")
+                    help="time S4 (PFML input construction for every month) + S5 + S6 as the step")
+    ap.add_argument("--dump", default="",
+                    help="rank 0 saves the gathered utilities of the last step here (tests)")
+    ap.add_argument("--no-inputs", action="store_true",
+                    help="skip the extra full (S4 + S5 + S6) wall-clock measurement")
     ap.add_argument("--stocks", type=int, default=500)
     ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32", "bf16", "fp8"],
                     help="with --with-inputs: S4 covariance / RFF / risk GEMMs in fp32, or on bf16 / "
@@ -214,8 +267,7 @@ def main():
     dev = env.device
     cfg = Config.default()
     if args.tiny:
-        cfg = cfg.override(["pf_ml.p_vec=[8,16]", "pf.dates.start_year=2008",
-                            "pf.dates.end_yr=2020"])
+        cfg = cfg.override(TINY)
         args.months, args.stocks = min(args.months, 180), min(args.stocks, 40)
     n_solves = (len(cfg.g_vec) * len(cfg.hp_years) * len(cfg.p_vec) * len(cfg.l_vec))
     n_util = n_solves * 12
@@ -223,17 +275,8 @@ def main():
     t_setup = time.perf_counter()
     engine = None
     if args.with_inputs:
-        from pfml.data.synthetic import engine_inputs
-        from pfml.utils.dates import pfml_date_grids
-        cfg.run.compat_mode = False          # distinct RFF draw per g: no Q1 duplication
-        cfg.run.precision = args.precision
-        chars, barra, wealth, rf = engine_inputs(n_stocks=args.stocks)
-        g = pfml_date_grids(int(barra.months.min()), 11, cfg.settings["split"]["test_end"],
-                            1971, 10)
-        months = g["m2"]
-        mine = np.asarray(list(coll.contiguous_split(len(months), env.world_size, env.rank)))
-        engine = (chars, barra, wealth, rf, dev, months[mine])
-        args.months = len(months)
+        engine, _ = engine_setup(cfg, env, args.stocks, args.precision)
+        args.months = len(engine[1])
         reals = None
     else:
         reals = synthetic_reals(cfg, dev, n_months=args.months, n_stocks=args.stocks)
@@ -241,29 +284,48 @@ def main():
         torch.cuda.synchronize()
     t_setup = time.perf_counter() - t_setup
 
-    for _ in range(args.warmup):
-        one_step(reals, cfg, engine)
-    pdist.barrier()
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res, scores = one_step(reals, cfg, engine)
-    if dev.type == "cuda":
-        torch.cuda.synchronize()
-    pdist.barrier()
-    dt = time.perf_counter() - t0
-    dt = coll.all_reduce_max(dt, device=dev)
-    ms = 1000.0 * dt / max(1, args.steps)
+    box = {}
+
+    def step():
+        box["res"], box["scores"] = one_step(reals, cfg, engine)
+
+    ms = timed(step, args.steps, args.warmup, dev)
+    res = box["res"]
     value = n_solves / (ms / 1000.0)
     # sanity: finite outputs
     finite = bool(torch.isfinite(res.obj).all().item())
+    if args.dump and env.is_main:
+        torch.save({"obj": res.obj.cpu(), "val_months": torch.as_tensor(res.val_months),
+                    "val_year": torch.as_tensor(res.val_year)}, args.dump)
+    full = None
+    if not args.with_inputs and not args.no_inputs:
+        # the full grid-search wall-clock INCLUDING S4 (BASELINE.json's second metric)
+        del reals
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+        cfg_full = Config.default()
+        if args.tiny:
+            cfg_full = cfg_full.override(TINY)
+        t_s = time.perf_counter()
+        eng, _ = engine_setup(cfg_full, env, args.stocks, "fp64")
+        setup_full = time.perf_counter() - t_s
+        from pfml.models.pfml_inputs import run_plan
+        ms_s4 = timed(lambda: run_plan(eng[0], cfg_full), 1, 1, dev)
+        fbox = {}
+
+        def full_step():
+            fbox["res"], _ = one_step(None, cfg_full, eng)
+
+        ms_full = timed(full_step, max(1, min(args.steps, 2)), 1, dev)
+        full = {"s4_ms": round(ms_s4, 1), "s4_s5_s6_wall_ms": round(ms_full, 1),
+                "s4_months": int(len(eng[1])), "s4_setup_s": round(setup_full, 2),
+                "s4_outputs_finite": bool(torch.isfinite(fbox["res"].obj).all().item())}
     prec_err = None
     if args.with_inputs and args.precision != "fp64":
-        from pfml.models.pfml_inputs import build_inputs
-        lo = build_inputs(cfg, *engine[:4], dev, months=engine[5]).reals
+        from pfml.models.pfml_inputs import run_plan
+        lo = run_plan(engine[0], cfg).reals
         cfg.run.precision = "fp64"
-        hi = build_inputs(cfg, *engine[:4], dev, months=engine[5]).reals
+        hi = run_plan(engine[0], cfg).reals
         rel = lambda a, b: float((a - b).norm() / b.norm())                       # noqa: E731
         prec_err = {"denom_rel_fro": rel(lo.denom, hi.denom),
                     "r_tilde_rel": rel(lo.r_tilde, hi.r_tilde)}
@@ -294,8 +356,16 @@ def main():
                 "outputs_finite": finite,
                 "includes_s4_inputs": bool(args.with_inputs),
                 "s4_precision_error_vs_fp64": prec_err,
+                "ridge_solve_dtype": "fp64 (lambda = 0 / rank-deficient systems: bf16 cannot "
+                                     "carry them, SURVEY 7.4)",
             },
         }
+        if full is not None:
+            rec.update(full)
+            rec["full_vs_baseline"] = round(BASELINE_FULL_S / (full["s4_s5_s6_wall_ms"] / 1000.0), 1)
+            rec["config"]["full_pipeline"] = (
+                "S4 (Barra Sigma, m_func, (24) Horner chains, (25) summands; 2 distinct g, "
+                f"{args.stocks}-stock synthetic universe) + S5 + S6, all PFML months")
         print(json.dumps(rec), flush=True)
     pdist.shutdown()
 

@@ -47,12 +47,17 @@ nat.register_hip("pfml_scores_max_per_month", [])
 
 @dataclass
 class PfmlReals:
-    """Per-month PFML summands of (25) for every g (internal interleaved feature order)."""
+    """Per-month PFML summands of (25) for every g (internal interleaved feature order).
+
+    ``months`` are the months held here; with ``all_months`` set they are a contiguous window
+    of that global list (a rank's hp-year shard plus its validation halo, see
+    ``local_month_range``) and the search plans over the global list."""
     months: np.ndarray                 # [T] month indices, sorted ascending
     r_tilde: torch.Tensor              # [G, T, P]
     denom: torch.Tensor                # [G, T, P, P]
     risk: torch.Tensor | None = None   # [G, T, P, P] (kept for artifact parity)
     tc: torch.Tensor | None = None
+    all_months: np.ndarray | None = None
 
     @property
     def G(self):
@@ -90,6 +95,22 @@ def make_plan(months: np.ndarray, years: np.ndarray) -> SearchPlan:
                       burn_stop, count, val_start.astype(np.int64), val_stop.astype(np.int64))
 
 
+def local_month_range(all_months: np.ndarray, years: np.ndarray, world: int,
+                      rank: int) -> tuple[int, int]:
+    """[lo, hi) rows of ``all_months`` that the rank owning a contiguous share of the hp years
+    needs: its own expanding-window blocks (rank 0 also the burn-in), and the
+    validation months of its last year - the next year's block - as a halo.  Every rank thus
+    computes the S4 summands of its own months only; the window prefixes cross ranks as one
+    P x P all-gather of block totals, no per-month matrix is ever exchanged."""
+    plan = make_plan(np.asarray(all_months, np.int64), np.asarray(years))
+    yl = list(coll.contiguous_split(len(years), world, rank))
+    if not yl:
+        return 0, 0
+    lo = 0 if yl[0] == 0 else int(plan.seg_start[yl[0]])
+    hi = max(int(plan.seg_stop[yl[-1]]), int(plan.val_stop[yl[-1]]))
+    return lo, hi
+
+
 @dataclass
 class GridResult:
     years: np.ndarray
@@ -107,13 +128,14 @@ _SETUP: dict = {}
 
 
 def _search_setup(months: np.ndarray, years: np.ndarray, p_vec, G: int, T: int, world: int,
-                  rank: int, dev, l_vec: np.ndarray) -> dict:
+                  rank: int, dev, l_vec: np.ndarray, off: int = 0) -> dict:
     """Everything of a grid search that depends only on its shape - the window plan, this
     rank's segments, cells and validation jobs, and the device copies of the segment bounds -
     built once per shape and reused by every later search (no host planning, no host->device
-    copies in the steady state)."""
+    copies in the steady state).  ``months`` is the global month list; the T months held
+    locally start at global row ``off`` (all local row indices below are relative to it)."""
     key = (months.tobytes(), np.asarray(years).tobytes(), tuple(p_vec), G, T, world, rank,
-           str(dev), l_vec.tobytes())
+           str(dev), l_vec.tobytes(), off)
     hit = _SETUP.get(key)
     if hit is not None:
         return hit
@@ -121,11 +143,13 @@ def _search_setup(months: np.ndarray, years: np.ndarray, p_vec, G: int, T: int, 
     yl = np.asarray(list(coll.contiguous_split(len(years), world, rank)))
     nYl = len(yl)
     nP = len(p_vec)
-    st = [int(plan.seg_start[i]) for i in yl]
-    sp = [int(plan.seg_stop[i]) for i in yl]
+    st = [int(plan.seg_start[i]) - off for i in yl]
+    sp = [int(plan.seg_stop[i]) - off for i in yl]
     if nYl and yl[0] == 0:
-        st = [0] + st
-        sp = [plan.burn_stop] + sp
+        st = [0 - off] + st
+        sp = [plan.burn_stop - off] + sp
+    if any(a < 0 or b > T for a, b in zip(st, sp)):
+        raise ValueError(f"rank {rank}: local months [{off}, {off + T}) miss its window blocks")
     nseg = len(st)
     starts = np.concatenate([np.asarray(st, np.int64) + g * T for g in range(G)]).astype(np.int32)
     stops = np.concatenate([np.asarray(sp, np.int64) + g * T for g in range(G)]).astype(np.int32)
@@ -136,8 +160,10 @@ def _search_setup(months: np.ndarray, years: np.ndarray, p_vec, G: int, T: int, 
     cnt = np.maximum(np.asarray(plan.count, dtype=np.int64)[yl], 1) if nYl else np.zeros(0)
     cell_scale = (1.0 / cnt[yy].astype(np.float64)).reshape(-1)
     # job order: [val month][g][p]  -> obj reshapes to [nValLocal, G, nP, L]
-    vs = np.asarray(plan.val_start, dtype=np.int64)[yl] if nYl else np.zeros(0, np.int64)
-    ve = np.asarray(plan.val_stop, dtype=np.int64)[yl] if nYl else np.zeros(0, np.int64)
+    vs = np.asarray(plan.val_start, dtype=np.int64)[yl] - off if nYl else np.zeros(0, np.int64)
+    ve = np.asarray(plan.val_stop, dtype=np.int64)[yl] - off if nYl else np.zeros(0, np.int64)
+    if nYl and (vs.min() < 0 or ve.max() > T):
+        raise ValueError(f"rank {rank}: local months [{off}, {off + T}) miss its validation halo")
     nv = ve - vs
     v_yi = np.repeat(np.arange(nYl), nv)                   # local year index per val row
     v_m = (np.concatenate([np.arange(a, b) for a, b in zip(vs, ve)])
@@ -170,8 +196,14 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
     years = cfg.hp_years
     p_vec = cfg.p_vec
     nP = len(p_vec)
-    su = _search_setup(np.asarray(reals.months, dtype=np.int64), np.asarray(years), p_vec, G, T,
-                       env.world_size, env.rank, dev, np.asarray(cfg.l_vec, dtype=np.float64))
+    all_months = np.asarray(reals.months if reals.all_months is None else reals.all_months,
+                            dtype=np.int64)
+    row_off = int(np.searchsorted(all_months, int(reals.months[0]))) if len(reals.months) else 0
+    if len(reals.months) and not np.array_equal(all_months[row_off:row_off + T],
+                                                np.asarray(reals.months, np.int64)):
+        raise ValueError("grid_search: local months must be a contiguous window of all_months")
+    su = _search_setup(all_months, np.asarray(years), p_vec, G, T, env.world_size, env.rank, dev,
+                       np.asarray(cfg.l_vec, dtype=np.float64), row_off)
     lvec = su["lvec"]
     L = lvec.numel()
     plan, yl, nYl, nseg = su["plan"], su["yl"], su["nYl"], su["nseg"]
@@ -228,7 +260,9 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
         v_m = np.concatenate([np.arange(a, b) for a, b in zip(plan.val_start, plan.val_stop)])
         v_y = np.repeat(np.arange(len(years)), nv_all)
         range_pop()
-    vm = np.asarray(reals.months, dtype=np.int64)[v_m]
+    else:
+        v_m = v_m + row_off                               # local rows -> global rows
+    vm = all_months[v_m]
     vy = np.asarray(years, dtype=np.int64)[v_y]
     return GridResult(years=years, p_vec=p_vec, l_vec=cfg.l_vec, years_local=years[yl],
                       beta=beta, val_months=vm, val_year=vy, obj=obj)

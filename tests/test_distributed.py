@@ -42,9 +42,15 @@ def _worker(rank, world, port, out_dir, task):
     from pfml.parallel import dist as pdist
     env = pdist.init("cpu")
     try:
-        if task == "grid":
-            from pfml.models.search import gather_beta, grid_search
+        if task in ("grid", "grid_local"):
+            from pfml.models.search import (PfmlReals, gather_beta, grid_search,
+                                            local_month_range)
             cfg, reals = _small_reals()
+            if task == "grid_local":
+                # each rank holds ONLY its hp-year blocks + validation halo (S4 sharding)
+                lo, hi = local_month_range(reals.months, cfg.hp_years, world, rank)
+                reals = PfmlReals(reals.months[lo:hi], reals.r_tilde[:, lo:hi].clone(),
+                                  reals.denom[:, lo:hi].clone(), all_months=reals.months)
             res = grid_search(reals, cfg)
             years, beta = gather_beta(res)
             if rank == 0:
@@ -70,21 +76,34 @@ def _run(world, task, tmp_path):
                        join=True, start_method="fork")
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_grid_search_sharded_matches_single(world, tmp_path):
+@pytest.mark.parametrize("world,task", [(2, "grid"), (4, "grid"), (2, "grid_local"),
+                                        (3, "grid_local")])
+def test_grid_search_sharded_matches_single(world, task, tmp_path):
     from pfml.models.search import gather_beta, grid_search
     from pfml.parallel import dist as pdist
     pdist.set_env(None)
     cfg, reals = _small_reals()
     ref = grid_search(reals, cfg)
     _, ref_beta = gather_beta(ref)
-    _run(world, "grid", tmp_path)
+    _run(world, task, tmp_path)
     got = torch.load(os.path.join(tmp_path, "grid.pt"), weights_only=True)
     assert np.array_equal(got["vm"].numpy(), ref.val_months)
     assert np.array_equal(got["vy"].numpy(), ref.val_year)
     assert np.array_equal(got["years"].numpy(), np.asarray(cfg.hp_years))
     assert torch.allclose(got["obj"], ref.obj, rtol=1e-10, atol=1e-13)
     assert torch.allclose(got["beta"], ref_beta, rtol=1e-9, atol=1e-12)
+
+
+def test_local_month_ranges_cover_and_overlap_by_one_block():
+    from pfml.models.search import local_month_range, make_plan
+    cfg, reals = _small_reals()
+    years = np.asarray(cfg.hp_years)
+    plan = make_plan(reals.months, years)
+    for world in (2, 3, 5):
+        rng = [local_month_range(reals.months, years, world, r) for r in range(world)]
+        assert rng[0][0] == 0 and rng[-1][1] == int(plan.val_stop[-1])
+        for (a0, a1), (b0, b1) in zip(rng[:-1], rng[1:]):
+            assert b0 <= a1 and a1 - b0 <= 12          # halo = at most one year block
 
 
 def test_collectives_gloo(tmp_path):
@@ -121,3 +140,26 @@ def test_bench_contract_two_ranks_gloo(tmp_path):
         assert k in rec, k
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2"
     assert rec["value"] > 0 and rec["config"]["outputs_finite"]
+
+
+def test_bench_with_inputs_two_ranks_equals_one(tmp_path):
+    """bench.py --with-inputs: each rank builds the S4 summands of its own hp-year blocks +
+    validation halo only; the gathered utilities equal the single-process run."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=root)
+    common = [os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "0", "--tiny",
+              "--device", "cpu", "--with-inputs"]
+    r1 = subprocess.run([sys.executable, *common, "--dump", str(tmp_path / "w1.pt")],
+                        capture_output=True, text=True, timeout=600, env=env)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), *common,
+           "--gpus", "2", "--dump", str(tmp_path / "w2.pt")]
+    r2 = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    assert r2.returncode == 0, r2.stderr[-3000:]
+    a = torch.load(tmp_path / "w1.pt", weights_only=True)
+    b = torch.load(tmp_path / "w2.pt", weights_only=True)
+    assert torch.equal(a["val_months"], b["val_months"])
+    assert torch.allclose(a["obj"], b["obj"], rtol=1e-10, atol=1e-13)
