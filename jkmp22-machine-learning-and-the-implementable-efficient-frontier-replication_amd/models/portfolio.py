@@ -5,8 +5,9 @@
 * ``hps_bundle``       - PFML_hps.py: {g: {aim_pfs_list, validation, rff_w}};
 * ``best_hps``         - PFML_best_hps.py:263-308: cross-g rank-first selection;
 * ``pfml_weights``     - PFML_best_hps.py:137-218: value-weighted start, weight recursion (17)
-                         w_t = m_t w_start + (I - m_t) w_aim with all m_t computed as ONE batched
-                         device m_func (K19) and the sequential part reduced to GEMVs;
+                         w_t = m_t w_start + (I - m_t) w_aim: m_t batched per rank (K19), the
+                         chain as device GEMVs (no per-month host round trip), one N-vector
+                         hand-off between ranks;
 * ``pf_ts`` / ``pf_summary`` - :220-259, :326-358 (quirks Q3, Q18);
 * ``plots``            - cumulative-performance / hyper-parameter figures (matplotlib).
 """
@@ -20,7 +21,7 @@ import torch
 
 from ..config import Config
 from ..ops import linalg as la
-from ..ops.gemm import gemm
+from ..ops.gemm import gemm_fused
 from ..utils.dates import month_end, month_index
 from ..utils.log import get_logger
 from .risk import BarraCov
@@ -39,30 +40,90 @@ def _opt_hps(validation: pd.DataFrame, g: int) -> pd.DataFrame:
 def aim_portfolios(cfg: Config, validation: pd.DataFrame, beta_years: np.ndarray,
                    beta: torch.Tensor, signal_months: np.ndarray, signal_t: list,
                    signal_ids: list, oos_months: np.ndarray) -> dict:
-    """{g: {d: {'aim_pf': DataFrame(id, eom, w_aim), 'coef': ndarray}}} (internal order)."""
+    """{g: {d: {'aim_pf': DataFrame(id, eom, w_aim), 'coef': ndarray}}} (internal order).
+
+    w_aim = s_t beta (K18) for every month on the device, one host copy at the end."""
     G = beta.shape[0]
     p_vec = cfg.p_vec
     out = {}
     mpos = {int(m): i for i, m in enumerate(signal_months)}
+    byear = np.asarray(beta_years)
     for g in range(G):
         opt = _opt_hps(validation, g)
-        res = {}
+        sel = {int(y): (int(p), int(l)) for y, p, l in zip(opt["hp_end"], opt["p"], opt["l"])}
+        ws, coefs, meta = [], [], []
         for d in oos_months:
             oos_year = int(month_end(int(d) + 1).year[0])
-            row = opt[opt["hp_end"] == oos_year - 1]
-            if row.empty:
+            if oos_year - 1 not in sel:
                 raise KeyError(f"no December rank-1 hyper-parameters for {oos_year - 1}")
-            p, l = int(row["p"].iloc[0]), int(row["l"].iloc[0])
-            yi = int(np.nonzero(beta_years == oos_year)[0][0])
-            coef = beta[g, yi, p_vec.index(p), l, : p + 1]
+            p, l = sel[oos_year - 1]
+            hit = np.nonzero(byear == oos_year)[0]
+            if len(hit) == 0:
+                raise KeyError(f"coefficients of hp year {oos_year} are not on this rank")
+            coef = beta[g, int(hit[0]), p_vec.index(p), l, : p + 1]
             i = mpos[int(d)]
             s = signal_t[g][i][:, : p + 1]
-            w_aim = (s @ coef.to(s.device)).cpu().numpy()
-            res[int(d)] = {"aim_pf": pd.DataFrame({"id": signal_ids[i],
-                                                   "eom": month_end(int(d))[0],
-                                                   "w_aim": w_aim}),
-                           "coef": coef.cpu().numpy(), "p": p, "l": l}
+            ws.append(s @ coef.to(s.device))
+            coefs.append(coef)
+            meta.append((int(d), i, p, l))
+        if ws:
+            w_all = torch.cat(ws).cpu().numpy()
+            c_all = [c.cpu().numpy() for c in coefs]
+        res, o = {}, 0
+        for k, (d, i, p, l) in enumerate(meta):
+            n = len(signal_ids[i])
+            res[d] = {"aim_pf": pd.DataFrame({"id": signal_ids[i], "eom": month_end(d)[0],
+                                              "w_aim": w_all[o:o + n]}),
+                      "coef": c_all[k], "p": p, "l": l}
+            o += n
         out[g] = res
+    return out
+
+
+def gather_aims(local: dict, cfg: Config, device) -> dict:
+    """All-gather the per-rank aim portfolios (rows: g, month, id, w_aim; one coefficient
+    row per (g, month)) so every rank holds the full set.  Single process: identity."""
+    from ..parallel import collectives as coll
+    from ..parallel.dist import env as dist_env
+    if not dist_env().is_dist:
+        return local
+    Pm = cfg.p_max + 1
+    rows, crow = [], []
+    for g, per in local.items():
+        for d, a in per.items():
+            df = a["aim_pf"]
+            n = len(df)
+            rows.append(np.stack([np.full(n, g, np.float64), np.full(n, d, np.float64),
+                                  df["id"].to_numpy(np.float64),
+                                  df["w_aim"].to_numpy(np.float64)], axis=1))
+            c = np.zeros(4 + Pm)
+            c[:4] = (g, d, a["p"], a["l"])
+            c[4:4 + len(a["coef"])] = a["coef"]
+            crow.append(c)
+    dev = torch.device(device)
+    R = torch.as_tensor(np.concatenate(rows) if rows else np.zeros((0, 4)), dtype=torch.float64,
+                        device=dev)
+    Cc = torch.as_tensor(np.stack(crow) if crow else np.zeros((0, 4 + Pm)), dtype=torch.float64,
+                         device=dev)
+    R = coll.all_gather_varlen(R).cpu().numpy()
+    Cc = coll.all_gather_varlen(Cc).cpu().numpy()
+    out: dict = {}
+    key = R[:, 0] * 1e7 + R[:, 1]
+    order = np.argsort(key, kind="stable")
+    R = R[order]
+    bounds = np.flatnonzero(np.diff(R[:, 0] * 1e7 + R[:, 1])) + 1
+    parts = np.split(R, bounds) if len(R) else []
+    cmap = {(int(c[0]), int(c[1])): c for c in Cc}
+    for part in parts:
+        g, d = int(part[0, 0]), int(part[0, 1])
+        c = cmap[(g, d)]
+        p = int(c[2])
+        out.setdefault(g, {})[d] = {
+            "aim_pf": pd.DataFrame({"id": part[:, 2].astype(np.int64), "eom": month_end(d)[0],
+                                    "w_aim": part[:, 3]}),
+            "coef": c[4:4 + p + 1].copy(), "p": p, "l": int(c[3])}
+    for g in out:
+        out[g] = dict(sorted(out[g].items()))
     return out
 
 
@@ -89,94 +150,161 @@ def best_hps(hps: dict, oos_months: np.ndarray):
     return bh, chosen, pd.concat(aims, ignore_index=True)
 
 
-def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.DataFrame,
-                 risk_free: pd.DataFrame, aims: pd.DataFrame, oos_months: np.ndarray,
-                 device) -> pd.DataFrame:
-    """Weight recursion (17) (PFML_best_hps.py:168-218) -> weights.csv frame."""
-    dev = torch.device(device)
-    pf = cfg.pf_set
-    gamma, mu = float(pf["gamma_rel"]), float(pf["mu"])
-    tc_on = bool(cfg.settings["Transaction_Costs"])
+def _weights_plan(cfg: Config, chars: pd.DataFrame, wealth: pd.DataFrame, aims: pd.DataFrame,
+                  oos_months: np.ndarray) -> dict:
+    """Host layout of the recursion: the valid rows of every OOS month in id order, each
+    month's aim weights aligned to them, and the drift map from month t's rows to month t+1's
+    (position of each id of t+1 among t's rows, or -1 for a new name)."""
     mi_all = month_index(chars["eom"])
     data = chars[np.isin(mi_all, oos_months) & chars["valid"].to_numpy()].copy()
     data["mi"] = month_index(data["eom"])
     data = data.sort_values(["mi", "id"], kind="stable").reset_index(drop=True)
-    wmap = dict(zip(month_index(wealth["eom"]), wealth["wealth"].to_numpy(np.float64)))
-    mumap = dict(zip(month_index(wealth["eom"]), wealth["mu_ld1"].to_numpy(np.float64)))
-    rfmap = dict(zip(month_index(risk_free["eom"]), risk_free["rf"].to_numpy(np.float64)))
-    aim_key = month_index(aims["eom"]) * 10_000_000 + aims["id"].to_numpy(np.int64)
-    aim_val = dict(zip(aim_key, aims["w_aim"].to_numpy(np.float64)))
-
     months = np.asarray(oos_months, np.int64)
-    groups = [data.index[data["mi"] == d].to_numpy() for d in months]
-    ns = np.array([len(g) for g in groups])
-    N = int(ns.max())
+    mi = data["mi"].to_numpy()
+    starts = np.searchsorted(mi, months, "left")
+    stops = np.searchsorted(mi, months, "right")
+    ids_all = data["id"].to_numpy(np.int64)
+    aim_key = month_index(aims["eom"]) * 10_000_000 + aims["id"].to_numpy(np.int64)
+    order = np.argsort(aim_key, kind="stable")
+    ak, av = aim_key[order], aims["w_aim"].to_numpy(np.float64)[order]
+    key = mi * 10_000_000 + ids_all
+    p = np.clip(np.searchsorted(ak, key), 0, max(len(ak) - 1, 0))
+    w_aim = np.where((len(ak) > 0) & (ak[p] == key), av[p], np.nan) if len(ak) else \
+        np.full(len(key), np.nan)
+    nxt = np.full(len(data), -1, np.int64)            # row r of month t+1 -> row in month t
+    for t in range(len(months) - 1):
+        a0, a1, b0, b1 = starts[t], stops[t], starts[t + 1], stops[t + 1]
+        cur = ids_all[a0:a1]
+        q = np.clip(np.searchsorted(cur, ids_all[b0:b1]), 0, max(a1 - a0 - 1, 0))
+        hit = (a1 > a0) & (cur[q] == ids_all[b0:b1]) if a1 > a0 else np.zeros(b1 - b0, bool)
+        nxt[b0:b1] = np.where(hit, q, -1)
+    mumap = dict(zip(month_index(wealth["eom"]), wealth["mu_ld1"].to_numpy(np.float64)))
+    return dict(data=data, months=months, starts=starts, stops=stops, ids=ids_all,
+                w_aim=w_aim, nxt=nxt, mu=np.array([mumap[int(d)] for d in months]))
+
+
+def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.DataFrame,
+                 risk_free: pd.DataFrame, aims: pd.DataFrame, oos_months: np.ndarray,
+                 device) -> pd.DataFrame | None:
+    """Weight recursion (17) (PFML_best_hps.py:168-218) -> weights.csv frame (rank 0).
+
+    The OOS months are split contiguously over ranks.  Each rank computes m_t of ITS months as
+    batched device m_func (K19; m = diag(a) m_tilde diag(1/a), never formed), then runs its
+    part of the sequential chain on the device - w_opt = w_aim + m (w_start - w_aim), the
+    drift w_start(t+1) = w_opt (1 + tr_ld1) / (1 + mu_ld1) gathered through the id map, new
+    names 0 - with no host round trip per month.  The chain crosses ranks as ONE N-vector
+    hand-off (point-to-point, rank r -> r+1); the per-row weights are gathered at the end."""
+    from ..parallel import collectives as coll
+    from ..parallel.dist import env as dist_env
+    env = dist_env()
+    dev = torch.device(device)
+    pf = cfg.pf_set
+    gamma, mu = float(pf["gamma_rel"]), float(pf["mu"])
+    tc_on = bool(cfg.settings["Transaction_Costs"])
+    pl = _weights_plan(cfg, chars, wealth, aims, oos_months)
+    data, months, starts, stops = pl["data"], pl["months"], pl["starts"], pl["stops"]
     B = len(months)
+    ns = stops - starts
+    N = int(ns.max()) if B else 1
     K = barra.X.shape[1]
-    # ---- batched m_t for every OOS month (K19) --------------------------------------
-    ms = []
+    wmap = dict(zip(month_index(wealth["eom"]), wealth["wealth"].to_numpy(np.float64)))
+    rfmap = dict(zip(month_index(risk_free["eom"]), risk_free["rf"].to_numpy(np.float64)))
+    mine = np.asarray(list(coll.contiguous_split(B, env.world_size, env.rank)), np.int64)
+    f64 = dict(dtype=torch.float64, device=dev)
+    lam_col = data["lambda"].to_numpy(np.float64) if tc_on else None
+    tr1 = data["tr_ld1"].to_numpy(np.float64)
+    ids_all = pl["ids"]
+
+    # ---- batched m_t of this rank's months (K19) --------------------------------------
+    Bm = len(mine)
+    mt_all = torch.zeros((Bm, N, N), **f64)
+    a_all = torch.ones((Bm, N), **f64)
     chunk = int(cfg.run.month_batch)
     if chunk <= 0:
         from .pfml_inputs import auto_month_batch
         chunk = auto_month_batch(N, 0, dev)
-    for c0 in range(0, B, chunk):
-        cm = months[c0:c0 + chunk]
+    for c0 in range(0, Bm, chunk):
+        cm = mine[c0:c0 + chunk]
         Bc = len(cm)
-        Xl = torch.zeros((Bc, N, K), dtype=torch.float64, device=dev)
-        Fb = torch.zeros((Bc, K, K), dtype=torch.float64, device=dev)
-        iv = torch.ones((Bc, N), dtype=torch.float64, device=dev)
-        lam = torch.empty((Bc, N), dtype=torch.float64, device=dev)
-        mask = torch.zeros((Bc, N), dtype=torch.float64, device=dev)
-        for bi, d in enumerate(cm):
-            rows = groups[c0 + bi]
-            ids = data["id"].to_numpy(np.int64)[rows]
-            bids, X, F, ivol = barra.slice(int(d))
+        Xl = np.zeros((Bc, N, K))
+        Fb = np.zeros((Bc, K, K))
+        iv = np.ones((Bc, N))
+        lam = np.empty((Bc, N))
+        mask = np.zeros((Bc, N))
+        for bi, t in enumerate(cm):
+            d = int(months[t])
+            rows = np.arange(starts[t], stops[t])
+            ids = ids_all[rows]
+            bids, X, F, ivol = barra.slice(d)
             pos = np.searchsorted(bids, ids)
+            if np.any(pos >= len(bids)) or np.any(bids[np.minimum(pos, len(bids) - 1)] != ids):
+                raise KeyError(f"month {d}: OOS ids missing from the Barra universe")
             n = len(ids)
-            Xl[bi, :n] = torch.as_tensor(X[pos], device=dev)
-            Fb[bi] = torch.as_tensor(F, device=dev)
-            iv[bi, :n] = torch.as_tensor(ivol[pos], device=dev)
-            lam[bi] = gamma / wmap[int(d)]
-            lam_d = data["lambda"].to_numpy(np.float64)[rows] if tc_on else np.full(n, 1e-16)
-            lam[bi, :n] = torch.as_tensor(lam_d, device=dev)
+            Xl[bi, :n], Fb[bi], iv[bi, :n] = X[pos], F, ivol[pos]
+            lam[bi] = gamma / wmap[d]
+            lam[bi, :n] = lam_col[rows] if tc_on else 1e-16
             mask[bi, :n] = 1.0
-        Sig = gemm(gemm(Xl, Fb), Xl, trans_b=True)
-        Sig.diagonal(dim1=1, dim2=2).add_(iv)
-        wv = torch.as_tensor([wmap[int(d)] for d in cm], dtype=torch.float64, device=dev)
-        rfv = torch.as_tensor([rfmap[int(d)] for d in cm], dtype=torch.float64, device=dev)
-        ms.append(la.m_func(Sig, lam, wv, rfv, mu, gamma, cfg.run.iterations, mask=mask))
-    m_all = torch.cat(ms)
+        Xd, ivd = torch.as_tensor(Xl, **f64), torch.as_tensor(iv, **f64)
+        Sig = torch.empty((Bc, N, N), **f64)
+        gemm_fused(torch.bmm(Xd, torch.as_tensor(Fb, **f64)), Xd, Sig, trans_b=True,
+                   diag_col0=0, diag_vec=ivd)
+        wv = torch.as_tensor([wmap[int(months[t])] for t in cm], **f64)
+        rfv = torch.as_tensor([rfmap[int(months[t])] for t in cm], **f64)
+        mt, a = la.m_tilde(Sig, torch.as_tensor(lam, **f64), wv, rfv, mu, gamma,
+                           cfg.run.iterations, mask=torch.as_tensor(mask, **f64))
+        mt_all[c0:c0 + Bc] = mt
+        a_all[c0:c0 + Bc] = a
 
-    # ---- sequential recursion -------------------------------------------------------
-    ids_all = data["id"].to_numpy(np.int64)
-    me = data["me"].to_numpy(np.float64)
-    tr1 = data["tr_ld1"].to_numpy(np.float64)
-    w_start = np.full(len(data), np.nan)
-    w = np.full(len(data), np.nan)
-    g0 = groups[0]
-    w_start[g0] = me[g0] / me[g0].sum()                   # value-weighted initial portfolio
-    for t, d in enumerate(months):
-        rows = groups[t]
-        n = len(rows)
-        key = int(d) * 10_000_000 + ids_all[rows]
-        w_aim = np.array([aim_val.get(int(k), np.nan) for k in key])
-        mt = m_all[t, :n, :n]
-        ws = torch.as_tensor(w_start[rows], dtype=torch.float64, device=dev)
-        wa = torch.as_tensor(w_aim, dtype=torch.float64, device=dev)
-        w_opt = (wa + mt @ (ws - wa)).cpu().numpy()
-        w[rows] = w_opt
+    # ---- the sequential chain on the device ---------------------------------------------
+    def padded(vals: np.ndarray, fill: float) -> torch.Tensor:
+        out = np.full((Bm, N), fill)
+        for i, t in enumerate(mine):
+            out[i, :ns[t]] = vals[starts[t]:stops[t]]
+        return torch.as_tensor(out, **f64)
+
+    wa = padded(pl["w_aim"], 0.0)
+    grow = padded((1.0 + tr1), 1.0) / torch.as_tensor(1.0 + pl["mu"][mine], **f64).view(Bm, 1)
+    nmap = np.zeros((Bm, N), np.int64)
+    hit = np.zeros((Bm, N))
+    for i, t in enumerate(mine):
         if t + 1 < B:
-            nxt = groups[t + 1]
-            nxt_ids = ids_all[nxt]
-            drift = w_opt * (1.0 + tr1[rows]) / (1.0 + mumap[int(d)])
-            pos = np.searchsorted(ids_all[rows], nxt_ids)
-            pos = np.clip(pos, 0, n - 1)
-            hit = ids_all[rows][pos] == nxt_ids
-            w_start[nxt] = np.where(hit, drift[pos], 0.0)   # new names start at 0
-    out = pd.DataFrame({"eom": month_end(data["mi"].to_numpy()),
-                        "mu_ld1": [mumap[int(x)] for x in data["mi"]],
-                        "id": ids_all, "tr_ld1": tr1, "w_start": w_start, "w": w})
-    return out
+            q = pl["nxt"][starts[t + 1]:stops[t + 1]]
+            nmap[i, :len(q)] = np.maximum(q, 0)
+            hit[i, :len(q)] = q >= 0
+    nmap_t, hit_t = torch.as_tensor(nmap, device=dev), torch.as_tensor(hit, **f64)
+    ws0 = torch.zeros(N, **f64)
+    if Bm and mine[0] == 0:
+        g0 = np.arange(starts[0], stops[0])
+        me = data["me"].to_numpy(np.float64)[g0]
+        ws0[: len(g0)] = torch.as_tensor(me / me.sum(), **f64)    # value-weighted start
+    elif env.is_dist:
+        ws0 = coll.recv_prev(ws0)
+    Wst = torch.zeros((Bm, N), **f64)
+    Wopt = torch.zeros((Bm, N), **f64)
+    ws = ws0
+    for i in range(Bm):
+        Wst[i] = ws
+        d = (ws - wa[i]) / a_all[i]
+        wopt = wa[i] + a_all[i] * torch.mv(mt_all[i], d)
+        Wopt[i] = wopt
+        ws = (wopt * grow[i])[nmap_t[i]] * hit_t[i]                 # next month's w_start
+    if env.is_dist:
+        coll.send_next(ws)
+    # gather the per-row weights (rank order = month order)
+    sel = torch.as_tensor(np.arange(N)[None, :] < ns[mine][:, None], device=dev)
+    w_start_rows = coll.all_gather_varlen(Wst[sel])
+    w_rows = coll.all_gather_varlen(Wopt[sel])
+    if not env.is_main:
+        return None
+    w_start = w_start_rows.cpu().numpy()
+    w = w_rows.cpu().numpy()
+    # rows with a missing aim stay NaN like the reference's merge would leave them
+    nan_aim = np.isnan(pl["w_aim"])
+    w = np.where(nan_aim, np.nan, w)
+    mumap = dict(zip(month_index(wealth["eom"]), wealth["mu_ld1"].to_numpy(np.float64)))
+    return pd.DataFrame({"eom": month_end(data["mi"].to_numpy()),
+                         "mu_ld1": [mumap[int(x)] for x in data["mi"]],
+                         "id": ids_all, "tr_ld1": tr1, "w_start": w_start, "w": w})
 
 
 def pf_ts(weights: pd.DataFrame, chars: pd.DataFrame, wealth: pd.DataFrame,

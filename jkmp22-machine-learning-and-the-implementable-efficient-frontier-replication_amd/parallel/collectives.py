@@ -121,3 +121,20 @@ def weighted_split(weights, world: int) -> list[range]:
         bounds.append(b)
     bounds.append(n)
     return [range(bounds[i], bounds[i + 1]) for i in range(world)]
+
+
+def send_next(x: torch.Tensor) -> None:
+    """Point-to-point send to rank + 1 (a pipeline hand-off, e.g. the portfolio recursion's
+    w_start vector: N doubles over one xGMI link)."""
+    e = env()
+    if e.is_dist and e.rank + 1 < e.world_size:
+        dist.send(x.contiguous(), dst=e.rank + 1)
+
+
+def recv_prev(like: torch.Tensor) -> torch.Tensor:
+    """Receive the tensor ``send_next`` of rank - 1 sent (shape / dtype of ``like``)."""
+    e = env()
+    out = torch.empty_like(like)
+    if e.is_dist and e.rank > 0:
+        dist.recv(out, src=e.rank - 1)
+    return out

@@ -16,8 +16,20 @@ Stages (CLI names) and the reference script each one replaces:
 
 State flows in memory within one process; with ``checkpoint=True`` every stage also writes
 its artifact + done-marker (utils/artifacts.py) so a later run resumes from the first stage
-whose inputs changed.  Multi-GPU (torchrun): pfml-input shards months and pfml-search-coef
-shards hp years over ranks (RCCL), everything else runs on rank 0.
+whose inputs changed.
+
+Multi-GPU (torchrun, one rank per GPU, RCCL):
+  * pfml-input / pfml-search-coef: the hp years are split contiguously over ranks and each
+    rank builds the S4 summands of ITS window blocks plus the one-block validation halo
+    (search.local_month_range) - no per-month matrix crosses ranks; the expanding windows
+    need one P x P all-gather of block totals, the utilities one all-gather.  Both stages
+    keep per-rank artifacts and per-rank done markers: a resumed run recomputes only the
+    shards whose marker is missing or stale.
+  * pfml-aim: each rank forms the aim portfolios of the OOS months whose coefficients and
+    signals it holds (year Y's validation block is Y's OOS block); the aims (N doubles per
+    month) are all-gathered.
+  * pfml-best-hps: m_t of the OOS months sharded over ranks, the recursion chained across
+    ranks by one N-vector hand-off (portfolio.pfml_weights); CSVs written by rank 0.
 """
 from __future__ import annotations
 
@@ -36,7 +48,7 @@ from .models import search
 from .parallel import collectives as coll
 from .parallel import dist as pdist
 from .utils.artifacts import ArtifactStore
-from .utils.dates import month_index, pfml_date_grids
+from .utils.dates import month_end, month_index, pfml_date_grids
 from .utils.log import COUNTERS, get_logger, metric
 from .utils.trace import StageTimer
 
@@ -46,18 +58,22 @@ MAIN_STAGES = ["prepare-data", "estimate-cov", "pfml-input", "pfml-search-coef",
                "pfml-hp-reals", "pfml-aim", "pfml-hps", "pfml-best-hps"]
 ALL_STAGES = ["get-additional-data", "sp500-subset"] + MAIN_STAGES
 
-# settings sections each stage's output depends on (for resume keys)
+# settings sections (and run options) each stage's output depends on (for resume keys);
+# keys chain, so a change invalidates the stage and everything downstream
 _DEPS = {
     "prepare-data": ("screens", "split", "feat_prank", "feat_impute", "addition_n", "deletion_n",
                      "pi", "pf"),
     "estimate-cov": ("cov_set",),
-    "pfml-input": ("pf_ml", "Transaction_Costs", "seed_no"),
+    "pfml-input": ("pf_ml", "Transaction_Costs", "seed_no", "compat_mode", "precision",
+                   "iterations"),
     "pfml-search-coef": ("pf_ml", "pf"),
-    "pfml-hp-reals": ("pf_ml",),
+    "pfml-hp-reals": ("pf_ml", "compat_mode"),
     "pfml-aim": ("pf",),
     "pfml-hps": (),
-    "pfml-best-hps": (),
+    "pfml-best-hps": ("compat_mode", "iterations"),
 }
+# stages whose artifacts are per rank (resume per shard)
+_SHARDED = ("pfml-input", "pfml-search-coef")
 
 
 class Pipeline:
@@ -82,19 +98,34 @@ class Pipeline:
             if st not in ALL_STAGES:
                 raise ValueError(f"unknown stage {st!r}; choose from {ALL_STAGES}")
         for st in stages:
-            if self.checkpoint and self.store.is_done(st, self._keys[st]):
+            if self.checkpoint and self._all_done(st):
                 log.info(f"[{st}] up to date (resume)")
                 continue
             t0 = time.time()
             with self.timer(st):
                 getattr(self, "_" + st.replace("-", "_"))()
-            if self.checkpoint and self.env.is_main:
-                self.store.mark_done(st, self._keys[st], seconds=time.time() - t0)
+            if self.checkpoint:
+                if st in _SHARDED:
+                    self.store.mark_done(st, self._rank_key(st), rank=self.env.rank,
+                                         seconds=time.time() - t0)
+                elif self.env.is_main:
+                    self.store.mark_done(st, self._keys[st], seconds=time.time() - t0)
             pdist.barrier()
             metric(stage=st, seconds=round(time.time() - t0, 3), rank=self.env.rank,
                    world_size=self.env.world_size, fallbacks=COUNTERS.as_dict())
             log.info(f"[{st}] done in {time.time() - t0:.2f}s")
         return self.state
+
+    def _rank_key(self, st: str) -> str:
+        return f"{self._keys[st]}|w{self.env.world_size}"
+
+    def _all_done(self, st: str) -> bool:
+        """Resume decision, identical on every rank (stages contain collectives)."""
+        if st in _SHARDED:
+            mine = self.store.is_done(st, self._rank_key(st), rank=self.env.rank)
+        else:
+            mine = self.store.is_done(st, self._keys[st])
+        return coll.all_reduce_max(0.0 if mine else 1.0, device=self.device) == 0.0
 
     # ---------------------------------------------------------------------------------
     def _get_additional_data(self):
@@ -134,42 +165,33 @@ class Pipeline:
         self._load_common()
         st = self.state
         m2 = st["grids"]["m2"]
-        mine = np.asarray(list(coll.contiguous_split(len(m2), self.env.world_size,
-                                                     self.env.rank)))
-        months = m2[mine]
+        lo, hi = search.local_month_range(m2, self.cfg.hp_years, self.env.world_size,
+                                          self.env.rank)
+        months = m2[lo:hi]
+        if self.checkpoint and self.store.is_done("pfml-input", self._rank_key("pfml-input"),
+                                                  rank=self.env.rank):
+            log.info(f"[pfml-input] rank {self.env.rank}: shard up to date (resume)")
+            self._ensure_reals()
+            return
         res = pin.build_inputs(self.cfg, st["chars"], st["barra"], st["wealth"],
                                st["risk_free"], self.device, months=months)
         self._guard_inputs(res, months)
         R = res.reals
-        G = R.G
-        if self.env.is_dist:
-            r_t = coll.all_gather_varlen(R.r_tilde.permute(1, 0, 2).contiguous()).permute(1, 0, 2)
-            d_t = coll.all_gather_varlen(R.denom.permute(1, 0, 2, 3).contiguous()).permute(1, 0, 2, 3)
-            R = search.PfmlReals(months=m2, r_tilde=r_t.contiguous(), denom=d_t.contiguous())
-            sig = []
-            for g in range(G):
-                rows = torch.cat(res.signal_t[g]) if res.signal_t[g] else None
-                sig.append(coll.all_gather_varlen(rows))
-            counts = coll.all_gather_varlen(torch.as_tensor([len(x) for x in res.ids],
-                                                            device=self.device)).cpu().numpy()
-            ids_all = coll.all_gather_varlen(torch.as_tensor(np.concatenate(res.ids),
-                                                             device=self.device)).cpu().numpy()
-            offs = np.concatenate([[0], np.cumsum(counts)])
-            signal_t = [[sig[g][offs[i]:offs[i + 1]] for i in range(len(m2))] for g in range(G)]
-            ids = [ids_all[offs[i]:offs[i + 1]] for i in range(len(m2))]
-        else:
-            signal_t, ids = res.signal_t, res.ids
+        R = search.PfmlReals(months=months, r_tilde=R.r_tilde, denom=R.denom, all_months=m2)
         st["reals"] = R
-        st["signal_t"], st["signal_ids"], st["signal_months"] = signal_t, ids, m2
+        st["signal_t"], st["signal_ids"], st["signal_months"] = res.signal_t, res.ids, months
         st["rff_w"] = res.rff_w
-        if self.checkpoint and self.env.is_main:
-            payload = {"months": torch.as_tensor(R.months), "r_tilde": R.r_tilde,
-                       "denom": R.denom, "rff_w": torch.as_tensor(res.rff_w),
-                       "counts": torch.as_tensor([len(x) for x in ids]),
-                       "ids": torch.as_tensor(np.concatenate(ids))}
-            for g in range(G):
-                payload[f"sig{g}"] = torch.cat(signal_t[g])
-            self.store.save_tensors("pfml-input", "reals", payload)
+        if self.checkpoint:
+            payload = {"months": torch.as_tensor(months), "all_months": torch.as_tensor(m2),
+                       "r_tilde": R.r_tilde, "denom": R.denom,
+                       "rff_w": torch.as_tensor(res.rff_w),
+                       "counts": torch.as_tensor([len(x) for x in res.ids]),
+                       "ids": torch.as_tensor(np.concatenate(res.ids) if res.ids else
+                                              np.zeros(0, np.int64))}
+            for g in range(R.G):
+                payload[f"sig{g}"] = (torch.cat(res.signal_t[g]) if res.signal_t[g] else
+                                      torch.zeros((0, R.P), dtype=torch.float64))
+            self.store.save_tensors("pfml-input", f"reals.rank{self.env.rank}", payload)
 
     def _guard_inputs(self, res, months) -> None:
         """Failure detection: months whose summands are not finite are recomputed
@@ -201,10 +223,11 @@ class Pipeline:
     def _ensure_reals(self):
         if "reals" not in self.state:
             self._load_common()
-            t = self.store.load_tensors("pfml-input", "reals", device=self.device)
+            t = self.store.load_tensors("pfml-input", f"reals.rank{self.env.rank}",
+                                        device=self.device)
             st = self.state
-            st["reals"] = search.PfmlReals(months=t["months"].numpy(),
-                                           r_tilde=t["r_tilde"], denom=t["denom"])
+            st["reals"] = search.PfmlReals(months=t["months"].numpy(), r_tilde=t["r_tilde"],
+                                           denom=t["denom"], all_months=t["all_months"].numpy())
             counts = t["counts"].numpy()
             offs = np.concatenate([[0], np.cumsum(counts)])
             ids = t["ids"].numpy()
@@ -221,17 +244,20 @@ class Pipeline:
         if self.cfg.run.check:
             metric(stage="pfml-search-coef", check=search.check_against_oracle(
                 grid, self.state["reals"], self.cfg), rank=self.env.rank)
-        years, beta = search.gather_beta(grid)
-        self.state["grid"], self.state["beta_years"], self.state["beta"] = grid, years, beta
-        if self.checkpoint and self.env.is_main:
-            self.store.save_tensors("pfml-search-coef", "coef",
-                                    {"years": torch.as_tensor(years), "beta": beta,
-                                     "obj": grid.obj, "val_months": torch.as_tensor(grid.val_months),
+        # betas stay sharded: rank r holds the coefficients of its own hp years
+        self.state["grid"] = grid
+        self.state["beta_years"], self.state["beta"] = grid.years_local, grid.beta
+        if self.checkpoint:
+            self.store.save_tensors("pfml-search-coef", f"coef.rank{self.env.rank}",
+                                    {"years": torch.as_tensor(grid.years_local),
+                                     "beta": grid.beta, "obj": grid.obj,
+                                     "val_months": torch.as_tensor(grid.val_months),
                                      "val_year": torch.as_tensor(grid.val_year)})
 
     def _pfml_hp_reals_load(self):
         if "grid" not in self.state:
-            t = self.store.load_tensors("pfml-search-coef", "coef", device=self.device)
+            t = self.store.load_tensors("pfml-search-coef", f"coef.rank{self.env.rank}",
+                                        device=self.device)
             self.state["beta_years"], self.state["beta"] = t["years"].numpy(), t["beta"]
             self.state["grid"] = search.GridResult(
                 years=self.cfg.hp_years, p_vec=self.cfg.p_vec, l_vec=self.cfg.l_vec,
@@ -240,10 +266,12 @@ class Pipeline:
 
     def _pfml_hp_reals(self):
         self._pfml_hp_reals_load()
+        # every rank holds the gathered utilities: each builds the (deterministic) frame it
+        # needs for the aim selection, rank 0 writes validation.csv
+        val = search.validation_frame(self.state["grid"], self.cfg)
         if self.env.is_main:
-            val = search.validation_frame(self.state["grid"], self.cfg)
             io.write_csv(val, self.cfg.run.data_dir, "validation.csv")
-            self.state["validation"] = val
+        self.state["validation"] = val
 
     def _validation(self) -> pd.DataFrame:
         if "validation" not in self.state:
@@ -252,18 +280,22 @@ class Pipeline:
         return self.state["validation"]
 
     def _pfml_aim(self):
-        if not self.env.is_main:
-            return
         st = self.state
         self._load_common()
         if "signal_t" not in st:
             self._ensure_reals()
         if "beta" not in st:
             self._pfml_hp_reals_load()
-        st["aims"] = portfolio.aim_portfolios(self.cfg, self._validation(), st["beta_years"],
-                                              st["beta"], st["signal_months"], st["signal_t"],
-                                              st["signal_ids"], st["grids"]["oos"])
-        if self.checkpoint:
+        # the OOS months whose coefficients (year oos_year, quirk Q13) live on this rank; their
+        # signals are in this rank's validation halo
+        oos = st["grids"]["oos"]
+        oos_year = month_end(oos + 1).year.to_numpy()
+        mine = oos[np.isin(oos_year, np.asarray(st["beta_years"]))]
+        local = portfolio.aim_portfolios(self.cfg, self._validation(), st["beta_years"],
+                                         st["beta"], st["signal_months"], st["signal_t"],
+                                         st["signal_ids"], mine)
+        st["aims"] = portfolio.gather_aims(local, self.cfg, self.device)
+        if self.checkpoint and self.env.is_main:
             rows, coefs = [], {}
             for g, per in st["aims"].items():
                 for d, a in per.items():
@@ -285,29 +317,28 @@ class Pipeline:
                 "l": int(sub["l"].iloc[0])}
         self.state["aims"] = aims
         if "rff_w" not in self.state:
-            t = self.store.load_tensors("pfml-input", "reals")
+            t = self.store.load_tensors("pfml-input", f"reals.rank{self.env.rank}")
             self.state["rff_w"] = t["rff_w"].numpy()
 
     def _pfml_hps(self):
-        if not self.env.is_main:
-            return
         self._load_aims()
         self.state["hps"] = portfolio.hps_bundle(self.state["aims"], self._validation(),
                                                  self.state["rff_w"])
-        if self.checkpoint:
+        if self.checkpoint and self.env.is_main:
             np.savez(self.store.path("pfml-hps", "rff_w.npz"), rff_w=self.state["rff_w"])
 
     def _pfml_best_hps(self):
-        if not self.env.is_main:
-            return
         st = self.state
         self._load_common()
         oos = st["grids"]["oos"]
         if "hps" not in st:
             self._pfml_hps()
         best, chosen, aims = portfolio.best_hps(st["hps"], oos)
+        # m_t sharded over ranks, the recursion chained across them (rank 0 gets the frame)
         w = portfolio.pfml_weights(self.cfg, st["chars"], st["barra"], st["wealth"],
                                    st["risk_free"], aims, oos, self.device)
+        if not self.env.is_main:
+            return
         d = self.cfg.run.data_dir
         io.write_csv(w, d, "weights.csv")
         pf = portfolio.pf_ts(w, st["chars"], st["wealth"], compat=self.cfg.run.compat_mode)

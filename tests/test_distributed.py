@@ -1,6 +1,8 @@
-"""Multi-process (gloo, world_size 2 and 4) runs must reproduce the single-process results:
-hp-year sharded grid search with the cross-rank exclusive prefix of window sums, month
-sharded PFML inputs, and the collectives themselves."""
+"""Multi-process (gloo, world_size 2-4) runs must reproduce the single-process results: the
+hp-year sharded grid search (full and rank-local month windows), bench.py --with-inputs on 2
+ranks, the whole pipeline from pfml-input to pfml-best-hps on 2 and 3 ranks (S4 per rank on
+its hp-year blocks + validation halo, sharded aims and m_t, recursion chained across ranks),
+and the collectives themselves."""
 import os
 import socket
 
@@ -58,6 +60,11 @@ def _worker(rank, world, port, out_dir, task):
                             "vy": torch.as_tensor(res.val_year),
                             "beta": beta, "years": torch.as_tensor(years)},
                            os.path.join(out_dir, "grid.pt"))
+        elif task == "pipeline":
+            from pfml.pipeline import Pipeline
+            cfg = _PIPE_CFG[0].override([f"run.data_dir={out_dir}",
+                                         f"run.artifact_dir={os.path.join(out_dir, 'art')}"])
+            Pipeline(cfg, device="cpu", checkpoint=True).run(_PIPE_STAGES)
         elif task == "coll":
             x = torch.full((rank + 1, 3), float(rank))
             g = coll.all_gather_varlen(x)
@@ -68,6 +75,11 @@ def _worker(rank, world, port, out_dir, task):
                        os.path.join(out_dir, f"coll{rank}.pt"))
     finally:
         pdist.shutdown()
+
+
+_PIPE_CFG: list = []
+_PIPE_STAGES = ["pfml-input", "pfml-search-coef", "pfml-hp-reals", "pfml-aim", "pfml-hps",
+                "pfml-best-hps"]
 
 
 def _run(world, task, tmp_path):
@@ -163,3 +175,48 @@ def test_bench_with_inputs_two_ranks_equals_one(tmp_path):
     b = torch.load(tmp_path / "w2.pt", weights_only=True)
     assert torch.equal(a["val_months"], b["val_months"])
     assert torch.allclose(a["obj"], b["obj"], rtol=1e-10, atol=1e-13)
+
+
+def _copy_inputs(src: str, dst: str) -> None:
+    import shutil
+    os.makedirs(dst, exist_ok=True)
+    for n in os.listdir(src):
+        p = os.path.join(src, n)
+        if os.path.isfile(p):
+            shutil.copy(p, os.path.join(dst, n))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipeline_sharded_matches_single(world, small_data, tmp_path):
+    """The main pipeline from pfml-input to pfml-best-hps on ``world`` gloo ranks - S4 built
+    per rank on its hp-year blocks + validation halo (no denom all-gather), betas sharded,
+    aims formed where beta and signals live, m_t sharded and the weight recursion chained
+    across ranks - writes the same CSVs as one process."""
+    import pandas as pd
+    from pfml.parallel import dist as pdist
+    from pfml.pipeline import Pipeline
+    base = small_data.override(["pf.dates.start_year=1999", "pf.dates.end_yr=2012",
+                                "pf.dates.split_years=3"])
+    d1, d2 = str(tmp_path / "w1"), str(tmp_path / "wn")
+    _copy_inputs(small_data.run.data_dir, d1)
+    _copy_inputs(small_data.run.data_dir, d2)
+    pdist.set_env(None)
+    cfg1 = base.override([f"run.data_dir={d1}", f"run.artifact_dir={os.path.join(d1, 'art')}"])
+    Pipeline(cfg1, device="cpu").run(_PIPE_STAGES)
+    pdist.set_env(None)
+    _PIPE_CFG[:] = [base]
+    _run(world, "pipeline", d2)
+    for name in ("validation.csv", "weights.csv", "pf.csv", "pf_summary.csv"):
+        a = pd.read_csv(os.path.join(d1, name))
+        b = pd.read_csv(os.path.join(d2, name))
+        assert list(a.columns) == list(b.columns) and len(a) == len(b), name
+        for c in a.columns:
+            if a[c].dtype.kind in "fc":
+                assert np.allclose(a[c].to_numpy(), b[c].to_numpy(), rtol=1e-10, atol=1e-13,
+                                   equal_nan=True), (name, c)
+            else:
+                assert (a[c].astype(str) == b[c].astype(str)).all(), (name, c)
+    # per-rank done markers of the sharded stages
+    for st in ("pfml-input", "pfml-search-coef"):
+        for r in range(world):
+            assert os.path.exists(os.path.join(d2, "art", st, f"_DONE.rank{r}.json"))
