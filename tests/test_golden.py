@@ -15,7 +15,7 @@ def _npz(name):
     return np.load(os.path.join(G, name), allow_pickle=False)
 
 
-@pytest.mark.parametrize("tag", ["n40", "n25_notc"])
+@pytest.mark.parametrize("tag", ["n40", "n25_notc", "prod_tc", "prod_notc"])
 def test_m_func_golden(tag):
     from pfml.ops.linalg import m_func
     z = _npz(f"m_func_{tag}.npz")
@@ -23,7 +23,7 @@ def test_m_func_golden(tag):
     got = m_func(torch.tensor(z["sigma"])[None], torch.tensor(z["lam"])[None],
                  torch.tensor([w]), torch.tensor([rf]), float(mu), float(g), 10)[0].numpy()
     ref = z["m"]
-    assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-7
+    assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-12
 
 
 def test_create_cov_golden():

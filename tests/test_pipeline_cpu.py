@@ -150,9 +150,9 @@ def test_pfml_inputs_match_reference_order_oracle(small_data):
         e_rt = to_reference_order(out.reals.r_tilde[0, i], Pm).numpy()
         e_rk = to_reference_order(out.reals.risk[0, i], Pm, dims=(0, 1)).numpy()
         e_tc = to_reference_order(out.reals.tc[0, i], Pm, dims=(0, 1)).numpy()
-        assert np.abs(e_rt - rt).max() / np.abs(rt).max() < 1e-7
-        assert np.abs(e_rk - risk).max() / np.abs(risk).max() < 1e-7
-        assert np.abs(e_tc - tc).max() / np.abs(tc).max() < 1e-6
+        assert np.abs(e_rt - rt).max() / np.abs(rt).max() < 1e-10
+        assert np.abs(e_rk - risk).max() / np.abs(risk).max() < 1e-10
+        assert np.abs(e_tc - tc).max() / np.abs(tc).max() < 1e-10
         # compat (Q1): both g identical
         assert torch.equal(out.reals.denom[0, i], out.reals.denom[1, i])
 
@@ -167,9 +167,9 @@ def test_m_func_matches_sqrtm_reference():
     S = X @ F @ X.T + np.diag(rng.uniform(0.01, 0.03, N) ** 2 * 21)
     lam = 0.2 / rng.uniform(1e7, 1e9, N)
     ref = m_func_ref(3e9, 0.007, 0.002, S * 10, 10, lam, 10)
-    got = m_func(torch.tensor(S)[None], torch.tensor(lam)[None], torch.tensor([3e9]),
-                 torch.tensor([0.002]), 0.007, 10, 10)[0].numpy()
-    assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-7
+    got = m_func(torch.tensor(S)[None], torch.tensor(lam)[None], torch.tensor([3e9], dtype=torch.float64),
+                 torch.tensor([0.002], dtype=torch.float64), 0.007, 10, 10)[0].numpy()
+    assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-12
 
 
 def test_pipeline_cli_resume_and_fault_injection(small_data, tmp_path):

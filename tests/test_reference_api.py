@@ -35,7 +35,7 @@ def test_m_func(tag):
     z = _npz(f"m_func_{tag}.npz")
     w, mu, rf, g = z["scal"]
     got = ra.m_func(w, mu, rf, z["sigma"] * g, g, np.diag(z["lam"]), 10)
-    assert np.abs(got - z["m"]).max() / np.abs(z["m"]).max() < 1e-7
+    assert np.abs(got - z["m"]).max() / np.abs(z["m"]).max() < 1e-12
 
 
 def test_create_cov_and_lambda():

@@ -58,6 +58,24 @@ def main():
         np.savez(os.path.join(OUT, f"m_func_{tag}.npz"), sigma=S, lam=lam,
                  scal=np.array([w, mu, rf, g]), m=np.asarray(m))
 
+    # m_func on production-like spectra: a Barra Sigma of the engine's synthetic universe
+    # (25 factors, F = sample cov * 21e-4, ivol = U(.01,.03)^2 * 21), N = 120, wealth 1e10,
+    # TC on (lambda = 0.2 / U(1e7, 1e9): cond(x^2 + 4x) ~ 1e4) and off (lambda = 1e-16:
+    # x ~ 1e4..1e7, where the scipy sqrtm form cancels)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from pfml.data.synthetic import engine_inputs
+    _, barra, _, _ = engine_inputs(n_stocks=120)
+    ids, X, F, iv = barra.slice(int(barra.months[-3]))
+    S = X @ F @ X.T + np.diag(iv)
+    rng2 = np.random.default_rng(77)                  # own stream: other fixtures unchanged
+    for tag, lam in [("prod_tc", 0.2 / rng2.uniform(1e7, 1e9, len(ids))),
+                     ("prod_notc", np.full(len(ids), 1e-16))]:
+        w, mu, rf, g = 1e10, 0.007, 0.003, 10.0
+        m = gf["m_func"](w=w, mu=mu, rf=rf, sigma_gam=S * g, gam=g, K_Lambda=np.diag(lam),
+                         iterations=10)
+        np.savez_compressed(os.path.join(OUT, f"m_func_{tag}.npz"), sigma=S, lam=lam,
+                            scal=np.array([w, mu, rf, g]), m=np.real(np.asarray(m)))
+
     # create_cov (Barra (37)) with an id subset
     N, K = 30, 5
     ids = np.arange(100, 100 + N)
