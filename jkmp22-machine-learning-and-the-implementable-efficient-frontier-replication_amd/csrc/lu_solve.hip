@@ -18,14 +18,17 @@
 
 namespace {
 
-constexpr int NB = 16;
-constexpr int PMAX = 1024;      // panel rows held in LDS
+// Block width NB and the panel rows PMAX held in LDS: NB = 32 for n <= 512 (half the passes
+// over the augmented rows of NB = 16; the 512 x 33 panel is 135 KB of LDS), NB = 16 up to
+// n = 1024.  The trailing update is bandwidth-bound (each pass reads and writes the live
+// part of every row), so the pass count sets its time.
 
 // live column v (0 .. nlive-1) -> physical column
 __device__ __forceinline__ int live_col(int v, int nA_live, int a_first, int b0) {
   return v < nA_live ? a_first + v : b0 + (v - nA_live);
 }
 
+template <int NB, int PMAX>
 __global__ __launch_bounds__(256) void lu_pivot_kernel(const double* __restrict__ M, int n,
                                                        int64_t ldm, int64_t sM, int a0, int k0,
                                                        int nb, int* __restrict__ piv,
@@ -85,6 +88,7 @@ __global__ __launch_bounds__(256) void lu_pivot_kernel(const double* __restrict_
 }
 
 // apply the NB sequential row swaps of block k0 to every live column (+ block k's own A cols)
+template <int NB>
 __global__ __launch_bounds__(256) void lu_swap_kernel(double* __restrict__ M, int64_t ldm,
                                                       int64_t sM, int ncol, int a_first, int nA,
                                                       int b0, int k0, int nb,
@@ -108,6 +112,7 @@ __global__ __launch_bounds__(256) void lu_swap_kernel(double* __restrict__ M, in
 }
 
 // P = A_kk^-1 by Gauss-Jordan without pivoting (rows already pivoted)
+template <int NB>
 __global__ __launch_bounds__(256) void lu_blockinv_kernel(const double* __restrict__ M,
                                                           int64_t ldm, int64_t sM, int a0, int k0,
                                                           int nb, double* __restrict__ Pbuf) {
@@ -137,6 +142,7 @@ __global__ __launch_bounds__(256) void lu_blockinv_kernel(const double* __restri
 }
 
 // R = P M_k over live columns (excluding block k's own A columns) -> Rbuf [NB][nlive]
+template <int NB>
 __global__ __launch_bounds__(256) void lu_rowpanel_kernel(const double* __restrict__ M, int64_t ldm,
                                                           int64_t sM, int nlive, int a_first,
                                                           int nA, int b0, int k0, int nb,
@@ -164,6 +170,7 @@ __global__ __launch_bounds__(256) void lu_rowpanel_kernel(const double* __restri
   }
 }
 
+template <int NB>
 __global__ __launch_bounds__(256) void lu_snapshot_kernel(const double* __restrict__ M, int n,
                                                           int64_t ldm, int64_t sM, int a0, int k0,
                                                           int nb, double* __restrict__ Cbuf) {
@@ -180,6 +187,7 @@ __global__ __launch_bounds__(256) void lu_snapshot_kernel(const double* __restri
 }
 
 // rows outside block k: M_i -= C_i R ; block rows: M_k = R   (live columns only)
+template <int NB>
 __global__ __launch_bounds__(256) void lu_update_kernel(double* __restrict__ M, int n, int64_t ldm,
                                                         int64_t sM, int nlive, int a_first, int nA,
                                                         int b0, int k0, int nb,
@@ -259,44 +267,53 @@ __global__ __launch_bounds__(256) void lu_update_kernel(double* __restrict__ M, 
       }
 }
 
-}  // namespace
 
-extern "C" int64_t pfml_lu_solve_work_doubles(int n, int m, int batch) {
-  return (int64_t)batch * (NB * NB + (int64_t)NB * (n + m) + (int64_t)n * NB) + 2LL * batch * NB;
-}
-
-// Solve A X = B in place for `batch` augmented systems (see header); X overwrites B.
-extern "C" int pfml_lu_solve_max_n() { return PMAX; }
-
-extern "C" hipError_t pfml_lu_solve(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
-                                    int b0, int batch, double* work, int* status,
-                                    hipStream_t st) {
-  if (n <= 0 || batch <= 0) return hipSuccess;
-  if (n > PMAX) return hipErrorInvalidValue;
+template <int NB, int PMAX>
+hipError_t lu_solve_nb(double* M, int n, int m, int64_t ldm, int64_t sM, int a0, int b0,
+                       int batch, double* work, int* status, hipStream_t st) {
   double* Pbuf = work;
   double* Rbuf = Pbuf + (int64_t)batch * NB * NB;
   double* Cbuf = Rbuf + (int64_t)batch * NB * (n + m);
   int* piv = reinterpret_cast<int*>(Cbuf + (int64_t)batch * n * NB);
   for (int k0 = 0; k0 < n; k0 += NB) {
     const int nb = (n - k0 < NB) ? (n - k0) : NB;
-    hipLaunchKernelGGL(lu_pivot_kernel, dim3(batch), dim3(256), 0, st, M, n, ldm, sM, a0, k0, nb,
-                       piv, status);
+    hipLaunchKernelGGL((lu_pivot_kernel<NB, PMAX>), dim3(batch), dim3(256), 0, st, M, n, ldm, sM,
+                       a0, k0, nb, piv, status);
     const int nswap = (n - k0) + m;           // A cols >= k0 and all B cols
-    hipLaunchKernelGGL(lu_swap_kernel, dim3((nswap + 255) / 256, batch), dim3(256), 0, st, M, ldm,
-                       sM, nswap, a0 + k0, n - k0, b0, k0, nb, piv);
-    hipLaunchKernelGGL(lu_blockinv_kernel, dim3(batch), dim3(256), 0, st, M, ldm, sM, a0, k0, nb,
-                       Pbuf);
+    hipLaunchKernelGGL((lu_swap_kernel<NB>), dim3((nswap + 255) / 256, batch), dim3(256), 0, st,
+                       M, ldm, sM, nswap, a0 + k0, n - k0, b0, k0, nb, piv);
+    hipLaunchKernelGGL((lu_blockinv_kernel<NB>), dim3(batch), dim3(256), 0, st, M, ldm, sM, a0,
+                       k0, nb, Pbuf);
     const int nA = n - (k0 + nb);            // live A columns right of the block
     const int nlive = nA + m;
     if (nlive > 0) {
-      hipLaunchKernelGGL(lu_rowpanel_kernel, dim3((nlive + 255) / 256, batch), dim3(256), 0, st, M,
-                         ldm, sM, nlive, a0 + k0 + nb, nA, b0, k0, nb, Pbuf, Rbuf);
-      hipLaunchKernelGGL(lu_snapshot_kernel, dim3((n + 255) / 256, batch), dim3(256), 0, st, M, n,
-                         ldm, sM, a0, k0, nb, Cbuf);
+      hipLaunchKernelGGL((lu_rowpanel_kernel<NB>), dim3((nlive + 255) / 256, batch), dim3(256), 0,
+                         st, M, ldm, sM, nlive, a0 + k0 + nb, nA, b0, k0, nb, Pbuf, Rbuf);
+      hipLaunchKernelGGL((lu_snapshot_kernel<NB>), dim3((n + 255) / 256, batch), dim3(256), 0, st,
+                         M, n, ldm, sM, a0, k0, nb, Cbuf);
       const int tiles = ((n + 63) / 64) * ((nlive + 63) / 64);
-      hipLaunchKernelGGL(lu_update_kernel, dim3(tiles, batch), dim3(256), 0, st, M, n, ldm, sM,
-                         nlive, a0 + k0 + nb, nA, b0, k0, nb, Rbuf, Cbuf);
+      hipLaunchKernelGGL((lu_update_kernel<NB>), dim3(tiles, batch), dim3(256), 0, st, M, n, ldm,
+                         sM, nlive, a0 + k0 + nb, nA, b0, k0, nb, Rbuf, Cbuf);
     }
   }
   return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int64_t pfml_lu_solve_work_doubles(int n, int m, int batch) {
+  const int64_t NB = 32;                     // the larger block: enough for either variant
+  return (int64_t)batch * (NB * NB + NB * (n + m) + (int64_t)n * NB) + 2LL * batch * NB;
+}
+
+// Solve A X = B in place for `batch` augmented systems (see header); X overwrites B.
+extern "C" int pfml_lu_solve_max_n() { return 1024; }
+
+extern "C" hipError_t pfml_lu_solve(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
+                                    int b0, int batch, double* work, int* status,
+                                    hipStream_t st) {
+  if (n <= 0 || batch <= 0) return hipSuccess;
+  if (n <= 512) return lu_solve_nb<32, 512>(M, n, m, ldm, sM, a0, b0, batch, work, status, st);
+  if (n <= 1024) return lu_solve_nb<16, 1024>(M, n, m, ldm, sM, a0, b0, batch, work, status, st);
+  return hipErrorInvalidValue;
 }

@@ -43,7 +43,7 @@ from ..ops import linalg as la
 from ..ops.gemm import gemm_fused, gemm_prec
 from ..ops.panel import rff_features, standardize_signals
 from ..utils.dates import month_index, pfml_date_grids
-from ..utils.log import get_logger
+from ..utils.log import COUNTERS, get_logger
 from ..utils.trace import range_pop, range_push
 from .risk import BarraCov
 from .search import PfmlReals
@@ -373,6 +373,9 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False) -> "PfmlInpu
     risk_out = torch.zeros_like(d_out) if keep_risk_tc else None
     tc_out = torch.zeros_like(d_out) if keep_risk_tc else None
     signal_t = [[None] * T for _ in range(G)]
+    sing = torch.zeros(max((len(b.months) for b in plan.batches), default=0),
+                       dtype=torch.int32, device=dev)          # singular const flags (batch)
+    nsing_t = torch.zeros((), dtype=torch.int64, device=dev)  # running count, on device
     b0 = 0
     for bt in plan.batches:
         B = len(bt.months)
@@ -418,9 +421,11 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False) -> "PfmlInpu
         sig0 = S[:, 0].clone()                                      # signal_t blocks
         del S, Tc, Ul
         # omega = const^-1 Omega, solved in place on the augmented [Omega | const] rows (K7)
-        omega = la.solve_augmented(T0, N, GP, a0=GP, b0=0)          # [B, N, GP] views
-        omega_l1 = la.solve_augmented(U0, N, GP, a0=GP, b0=0)
+        omega = la.solve_augmented(T0, N, GP, a0=GP, b0=0, status=sing[:B])  # [B, N, GP]
+        omega_l1 = la.solve_augmented(U0, N, GP, a0=GP, b0=0, status=sing[:B])
         omega_chg = torch.addcmul(omega, Dg[:, 0].unsqueeze(-1), omega_l1, value=-1.0)
+        nsing_t += sing[:B].sum()
+        sing.zero_()
         # (25): r_tilde = omega' r, risk = gamma omega' Sigma omega (Sigma in low-rank form:
         # X (F (X' omega)) + ivol o omega), tc = w omega_chg' Lambda omega_chg, denom
         omega = omega.contiguous()
@@ -466,6 +471,10 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False) -> "PfmlInpu
         range_pop()
         b0 += B
         log.info(f"PFML inputs: months {b0}/{T}")
+    nsing = int(nsing_t.item())                                  # the one status sync of S4
+    if nsing:
+        COUNTERS.add("pfml_inputs.singular_const", nsing)
+        log.warning(f"PFML inputs: {nsing} month(s) with a numerically singular sum of agg")
     reals = PfmlReals(months=plan.months, r_tilde=r_out, denom=d_out, risk=risk_out, tc=tc_out)
     return PfmlInputs(reals=reals, months=plan.months, signal_rows=plan.sig_rows,
                       signal_t=signal_t, rff_w=plan.W, ids=plan.sig_ids)

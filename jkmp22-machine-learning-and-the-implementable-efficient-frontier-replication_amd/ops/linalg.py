@@ -95,13 +95,16 @@ def _lu_max_n() -> int:
     return int(nat.hip_lib().pfml_lu_solve_max_n())
 
 
-def solve_augmented(M: torch.Tensor, n: int, m: int, a0: int, b0: int) -> torch.Tensor:
+def solve_augmented(M: torch.Tensor, n: int, m: int, a0: int, b0: int,
+                    status: torch.Tensor | None = None) -> torch.Tensor:
     """In-place solve of augmented systems: rows of M [B, n, W] hold A at columns a0..a0+n and
     B at b0..b0+m; on return the B columns hold X = A^-1 B (returned as a view).
 
-    Device: csrc/lu_solve.hip (blocked LU with partial pivoting, the pivot panel in LDS) up to
-    n = pfml_lu_solve_max_n() (1024); larger systems (the 3000-stock stress) take the library
-    (rocSOLVER) LU through torch."""
+    Device: csrc/lu_solve.hip (blocked Gauss-Jordan with partial pivoting, the pivot panel in
+    LDS; 32-wide blocks up to n = 512, 16-wide up to 1024); larger systems (the 3000-stock
+    stress) take the library (rocSOLVER) LU through torch.  With ``status`` (a [B] int32
+    device tensor) singular systems are only flagged there (no host sync; the caller checks
+    once), otherwise they are counted here."""
     if nat.is_device(M) and n <= _lu_max_n():
         if not M.is_contiguous():
             raise ValueError("solve_augmented: contiguous storage required")
@@ -109,16 +112,21 @@ def solve_augmented(M: torch.Tensor, n: int, m: int, a0: int, b0: int) -> torch.
         lib = nat.hip_lib()
         work = torch.empty(lib.pfml_lu_solve_work_doubles(n, m, Bt), dtype=torch.float64,
                            device=M.device)
-        status = torch.zeros(Bt, dtype=torch.int32, device=M.device)
+        st = status if status is not None else torch.zeros(Bt, dtype=torch.int32,
+                                                           device=M.device)
         nat.check(lib.pfml_lu_solve(M.data_ptr(), n, m, W, nn * W, a0, b0, Bt, work.data_ptr(),
-                                    status.data_ptr(), nat.stream_of(M)), "pfml_lu_solve")
-        nbad = int(status.sum().item())
-        if nbad:
-            COUNTERS.add("linalg.singular_solve", nbad)
+                                    st.data_ptr(), nat.stream_of(M)), "pfml_lu_solve")
+        if status is None:
+            nbad = int(st.sum().item())
+            if nbad:
+                COUNTERS.add("linalg.singular_solve", nbad)
     else:
         X, info = torch.linalg.solve_ex(M[:, :, a0:a0 + n], M[:, :, b0:b0 + m])
-        if bool((info != 0).any()):
-            COUNTERS.add("linalg.singular_solve", int((info != 0).sum()))
+        bad = info != 0
+        if status is not None:
+            status |= bad.to(status.dtype)
+        elif bool(bad.any()):
+            COUNTERS.add("linalg.singular_solve", int(bad.sum()))
         M[:, :, b0:b0 + m] = X
     return M[:, :, b0:b0 + m]
 

@@ -174,7 +174,8 @@ def test_grid_search_gpu_matches_cpu(gpu):
     assert ro < 1e-8
 
 
-@pytest.mark.parametrize("n,m,b", [(17, 5, 2), (100, 37, 3), (513, 1026, 2)])
+@pytest.mark.parametrize("n,m,b", [(17, 5, 2), (64, 10, 2), (100, 37, 3), (490, 1028, 2),
+                                   (512, 20, 1), (513, 1026, 2)])
 def test_lu_solve_augmented(gpu, n, m, b):
     from pfml.ops.linalg import solve
     A = _rand(b, n, n, seed=n) + n ** 0.5 * torch.eye(n, dtype=torch.float64)
