@@ -63,14 +63,34 @@ def spd_inverse(A: torch.Tensor, inplace: bool = False,
 _BLOCKED_MIN_N = 160
 
 
+nat.register_hip("pfml_spd_blockinv128", [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int,
+                                          C.c_int, C.c_void_p, C.c_void_p, C.c_void_p])
+nat.register_hip("pfml_spd_inverse_sym", [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                          C.c_void_p])
+nat.register_hip("pfml_spd_inverse_sym_work_doubles", [C.c_int, C.c_int], C.c_int64)
+
+
 def _spd_inverse_blocked(X: torch.Tensor, status: torch.Tensor) -> None:
-    """In-place SPD inverse with 64-wide Gauss-Jordan blocks: pivot block inverted in LDS
-    (csrc/spd_inverse.hip: pfml_spd_blockinv); row panel, rank-64 trailing update and column
-    panel on the hand-written fp64 MFMA GEMM (csrc/gemm_f64.hip, 35 TF/s on the rank-64
-    update vs 28 for rocBLAS, profiles/r02_gemm_own_vs_rocblas.json)."""
+    """In-place SPD inverse by 64-wide Gauss-Jordan block steps: the pivot block inverted in
+    LDS (csrc/spd_inverse.hip), row panel, rank-64 trailing update and column panel on the
+    fused fp64 MFMA GEMM (csrc/gemm_f64.hip).  Measured on [256, 490, 490]
+    (tools/bench_inverse.py, profiles/r02_inverse_variants.json): 4.70 ms (12.8 TF/s); the
+    fused sign-symmetric 3-launch form (PFML_SPD_INV=sym, pfml_spd_inverse_sym) 4.83 ms and
+    128-wide blocks (PFML_SPD_INV=generic128) 6.0 ms - the rank-64 update pass is
+    bandwidth/latency-bound in every form."""
+    import os
     lib = nat.hip_lib()
     B, n, _ = X.shape
-    NB = lib.pfml_spd_block_size()
+    mode = os.environ.get("PFML_SPD_INV", "generic")
+    if mode == "sym":
+        work = torch.empty(lib.pfml_spd_inverse_sym_work_doubles(n, B), dtype=torch.float64,
+                           device=X.device)
+        nat.check(lib.pfml_spd_inverse_sym(X.data_ptr(), n, B, work.data_ptr(),
+                                           status.data_ptr(), nat.stream_of(X)),
+                  "pfml_spd_inverse_sym")
+        return
+    NB = 128 if mode == "generic128" else lib.pfml_spd_block_size()
+    blockinv = lib.pfml_spd_blockinv128 if NB == 128 else lib.pfml_spd_blockinv
     dev = X.device
     P = torch.empty((B, NB, NB), dtype=torch.float64, device=dev)
     Cbuf = torch.empty((B, n, NB), dtype=torch.float64, device=dev)
@@ -78,8 +98,8 @@ def _spd_inverse_blocked(X: torch.Tensor, status: torch.Tensor) -> None:
     st = nat.stream_of(X)
     for k0 in range(0, n, NB):
         nb = min(NB, n - k0)
-        nat.check(lib.pfml_spd_blockinv(X.data_ptr(), n, n * n, B, k0, nb, P.data_ptr(),
-                                        status.data_ptr(), st), "pfml_spd_blockinv")
+        nat.check(blockinv(X.data_ptr(), n, n * n, B, k0, nb, P.data_ptr(), status.data_ptr(),
+                           st), "pfml_spd_blockinv")
         Pk = P[:, :nb, :nb]
         R = Rbuf[:, :nb, :]
         gemm_fused(Pk, X[:, k0:k0 + nb, :], R)                   # R = P A_k.

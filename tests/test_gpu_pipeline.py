@@ -79,7 +79,8 @@ def test_db_sqrt_device_matches_eigh(gpu):
     ws = [torch.empty_like(Sd) for _ in range(4)]
     got = _db_sqrt(Sd, DB_ITERS, DB_SCALED_ITERS, st, ws).cpu()
     assert int(st.sum()) == 0
-    assert (got - ref).abs().max().item() / ref.abs().max().item() < 1e-12
+    # cond(S) ~ 1e6: eigh's own eigenvector error is ~1e-13 here
+    assert (got - ref).abs().max().item() / ref.abs().max().item() < 1e-11
 
 
 @pytest.mark.parametrize("tc", [True, False])
