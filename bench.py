@@ -241,6 +241,10 @@ def main():
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--with-inputs", action="store_true",
                     help="time S4 (PFML input construction for every month) + S5 + S6 as the step")
+    ap.add_argument("--rank-deficient", type=int, default=0, metavar="NT",
+                    help="synthetic denom_t of rank <= NT per month (X_t: NT x P, so early "
+                         "expanding windows are singular at lambda = 0 and exercise the device "
+                         "LU repair of the band path); reports the repair count")
     ap.add_argument("--dump", default="",
                     help="rank 0 saves the gathered utilities of the last step here (tests)")
     ap.add_argument("--no-inputs", action="store_true",
@@ -279,7 +283,8 @@ def main():
         args.months = len(engine[1])
         reals = None
     else:
-        reals = synthetic_reals(cfg, dev, n_months=args.months, n_stocks=args.stocks)
+        reals = synthetic_reals(cfg, dev, n_months=args.months,
+                                n_stocks=args.rank_deficient or args.stocks)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t_setup = time.perf_counter() - t_setup
@@ -292,8 +297,11 @@ def main():
     ms = timed(step, args.steps, args.warmup, dev)
     res = box["res"]
     value = n_solves / (ms / 1000.0)
-    # sanity: finite outputs
+    # sanity: finite outputs; device repairs (non-SPD ridge systems) of the last step
     finite = bool(torch.isfinite(res.obj).all().item())
+    from pfml.ops.ridge import repairs_done
+    from pfml.utils.log import COUNTERS
+    repairs = repairs_done() if dev.type == "cuda" else 0
     if args.dump and env.is_main:
         torch.save({"obj": res.obj.cpu(), "val_months": torch.as_tensor(res.val_months),
                     "val_year": torch.as_tensor(res.val_year)}, args.dump)
@@ -358,8 +366,15 @@ def main():
                 "s4_precision_error_vs_fp64": prec_err,
                 "ridge_solve_dtype": "fp64 (lambda = 0 / rank-deficient systems: bf16 cannot "
                                      "carry them, SURVEY 7.4)",
+                "rank_deficient_nt": args.rank_deficient or None,
             },
+            "repairs": repairs,
+            "fallbacks": COUNTERS.as_dict(),
         }
+        if args.rank_deficient:
+            rec["data"] = (f"synthetic rank-deficient summands: denom_t = X_t'X_t/NT with X_t "
+                           f"~ N(0,1) of shape {args.rank_deficient} x 513 (rank <= "
+                           f"{args.rank_deficient} per month), {args.months} months")
         if full is not None:
             rec.update(full)
             rec["full_vs_baseline"] = round(BASELINE_FULL_S / (full["s4_s5_s6_wall_ms"] / 1000.0), 1)

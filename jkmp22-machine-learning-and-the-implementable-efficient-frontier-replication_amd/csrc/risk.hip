@@ -6,8 +6,12 @@
 //                              Reference: Estimate Covariance Matrix.py:214-233 - one Python
 //                              iteration per day with a full-array boolean mask (≈182 s); here
 //                              rows are CSR-segmented by day and every day is one workgroup.
-//                              An exactly-zero pivot is LAPACK's LinAlgError: the day is flagged
-//                              (status = 1) and the host applies the reference's pinv fallback.
+//                              An exactly-zero pivot is LAPACK's LinAlgError; the reference then
+//                              uses coef = pinv(X'X) X'y (:226-229).  The same workgroup does
+//                              that on the device: [X'X | X'y] is rebuilt from the MFMA
+//                              accumulators, X'X = V diag(e) V' by cyclic Jacobi in LDS, and
+//                              coef = V diag(1/e) V' X'y over |e| > 1e-15 max|e| (numpy pinv's
+//                              default rcond on the singular values); status = 2 marks the day.
 //   K22  ewma_factor_cov_kernel per calc month-end: the trailing <= obs days of factor returns,
 //                              normalised EWMA weights for the correlation (hl_cor) and the
 //                              variance (hl_var), weighted means, centred weighted Gram matrices
@@ -99,23 +103,92 @@ __global__ __launch_bounds__(256) void daily_ols_kernel(
     __syncthreads();
   }
   if (bad_s) {
-    if (t == 0) status[d] = 1;
-    return;
-  }
-  // back substitution U beta = c (wave 0; lane j keeps beta_j)
-  if (w == 0) {
-    double bj = 0.0;
-    for (int i = K - 1; i >= 0; --i) {
-      const double part = (lane > i && lane < K) ? G[i][lane] * bj : 0.0;
-      const double s = wave_sum(part);
-      const double bi = (G[i][K] - s) / G[i][i];
-      if (lane == i) bj = bi;
+    // ---- pinv fallback: rebuild G = [X'X | X'y] from the accumulators ------------------
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) G[ti + PFML_F64_CROW(lane, r)][tj + (lane & 15)] = acc[r];
+    __shared__ double V[KP][KP + 1];
+    __shared__ double rot[2];
+    for (int e = t; e < KP * KP; e += 256) V[e / KP][e % KP] = (e / KP == e % KP) ? 1.0 : 0.0;
+    __syncthreads();
+    if (t < K) beta_s[t] = G[t][K];                          // X'y (G's column K)
+    // cyclic Jacobi sweeps on the K x K block (uniform control flow, threads k < K update
+    // column / row k); rotations below the classic threshold are skipped
+    for (int sweep = 0; sweep < 16; ++sweep) {
+      for (int pp = 0; pp < K - 1; ++pp)
+        for (int qq = pp + 1; qq < K; ++qq) {
+          __syncthreads();
+          if (t == 0) {
+            const double app = G[pp][pp], aqq = G[qq][qq], apq = G[pp][qq];
+            double c = 1.0, sn = 0.0;
+            if (fabs(apq) > 1e-300 && fabs(apq) > 1e-18 * sqrt(fabs(app * aqq))) {
+              const double th = (aqq - app) / (2.0 * apq);
+              const double tt = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+              c = 1.0 / sqrt(tt * tt + 1.0);
+              sn = tt * c;
+            }
+            rot[0] = c;
+            rot[1] = sn;
+          }
+          __syncthreads();
+          const double c = rot[0], sn = rot[1];
+          if (sn == 0.0) continue;                             // uniform: same in every thread
+          if (t < K) {                                         // columns p, q (A and V)
+            const double akp = G[t][pp], akq = G[t][qq];
+            G[t][pp] = c * akp - sn * akq;
+            G[t][qq] = sn * akp + c * akq;
+            const double vkp = V[t][pp], vkq = V[t][qq];
+            V[t][pp] = c * vkp - sn * vkq;
+            V[t][qq] = sn * vkp + c * vkq;
+          }
+          __syncthreads();
+          if (t < K) {                                         // rows p, q
+            const double apk = G[pp][t], aqk = G[qq][t];
+            G[pp][t] = c * apk - sn * aqk;
+            G[qq][t] = sn * apk + c * aqk;
+          }
+        }
     }
-    if (lane < K) {
-      beta_s[lane] = bj;
-      coef[(int64_t)d * K + lane] = bj;
+    __syncthreads();
+    // coef = V diag(1/e) V' X'y over |e| > 1e-15 max |e|
+    if (w == 0) {
+      double emax = 0.0;
+      for (int k = 0; k < K; ++k) emax = fmax(emax, fabs(G[k][k]));
+      const double cut = 1e-15 * emax;
+      double proj = 0.0;                                     // lane k: (V' X'y)_k / e_k
+      if (lane < K) {
+        for (int j = 0; j < K; ++j) proj += V[j][lane] * beta_s[j];
+        const double ek = G[lane][lane];
+        proj = (fabs(ek) > cut) ? proj / ek : 0.0;
+      }
+      double ci = 0.0;
+      for (int k = 0; k < K; ++k) {
+        const double pk = __shfl(proj, k, 64);
+        if (lane < K) ci += V[lane][k] * pk;
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (lane < K) {
+        beta_s[lane] = ci;
+        coef[(int64_t)d * K + lane] = ci;
+      }
+      if (lane == 0) status[d] = 2;
     }
-    if (lane == 0) status[d] = 0;
+  } else {
+    // back substitution U beta = c (wave 0; lane j keeps beta_j)
+    if (w == 0) {
+      double bj = 0.0;
+      for (int i = K - 1; i >= 0; --i) {
+        const double part = (lane > i && lane < K) ? G[i][lane] * bj : 0.0;
+        const double s = wave_sum(part);
+        const double bi = (G[i][K] - s) / G[i][i];
+        if (lane == i) bj = bi;
+      }
+      if (lane < K) {
+        beta_s[lane] = bj;
+        coef[(int64_t)d * K + lane] = bj;
+      }
+      if (lane == 0) status[d] = 0;
+    }
   }
   __syncthreads();
   for (int64_t r = a + t; r < b; r += 256) {

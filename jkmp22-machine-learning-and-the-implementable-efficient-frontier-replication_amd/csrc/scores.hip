@@ -2,14 +2,16 @@
 // utilities obj[nV][G][C] (C = nP * L hyper-parameter combinations) and the g-range [g0, g1)
 // it holds (all g' <= g in reference-compat mode, quirk Q2):
 //
-//   cum[r][c]  = mean of seq[0..r][c]   over the frame's rows r = v * k + kk (k = g1 - g0),
-//                seq[v * k + kk][c] = obj[v][g0 + kk][c]           (expanding mean by (p, l))
+//   cum[r][c]  = mean of the non-NaN seq[0..r][c] over the frame's rows r = v * k + kk
+//                (k = g1 - g0), seq[v * k + kk][c] = obj[v][g0 + kk][c]: pandas
+//                expanding().mean() by (p, l), NaN until the first finite value
 //   rank[v][i] = dense descending rank of cum[v * k + i / C][i % C] among the month's k * C
-//                values (torch.sort semantics: NaN above everything, every NaN distinct)
+//                values; NaN cum gets a NaN rank and is not counted (pandas
+//                rank(method='dense', ascending=False)), so a singular cell is never "rank 1"
 //
 // Two launches replace the ~25 small torch kernels (sort, scans, scatters) per frame:
 //   prefix_mean_kernel  16 columns x 16 row chunks per workgroup: chunk sums, LDS offsets,
-//                       chunk rescans (loads batched and clamped)
+//                       chunk rescans, NaN carry fix-up (loads batched and clamped)
 //   dense_rank_kernel   one workgroup per month: bitonic sort of <= 1024 (key, index) pairs in
 //                       LDS, adjacent-difference + block scan for the dense rank, scatter back
 #include "common.h"
@@ -24,10 +26,15 @@ constexpr int PM_COLS = 16, PM_RG = 16;   // prefix mean: 16 columns x 16 row ch
 __global__ __launch_bounds__(256) void prefix_mean_kernel(const double* __restrict__ obj, int nV,
                                                           int G, int g0, int k, int C,
                                                           double* __restrict__ cum) {
-  // thread (rg, cg): rows [rg * chunk, (rg + 1) * chunk) of column c; chunk sums meet in LDS
-  // for the cross-chunk offsets, then each chunk is rescanned.  Loads are clamped and batched
-  // (8 in flight), so a thread pays ~2 R / (8 PM_RG) memory latencies, not R.
+  // thread (rg, cg): rows [rg * chunk, (rg + 1) * chunk) of column c; chunk sums / counts of
+  // the non-NaN values meet in LDS for the cross-chunk offsets, then each chunk is rescanned.
+  // A NaN row must repeat the previous expanding mean BIT FOR BIT (pandas carries its running
+  // state; ties then rank alike): inside a chunk the thread repeats its own last value, and
+  // the NaN rows leading a chunk take the previous chunks' last value in a fix-up pass.
   __shared__ double part[PM_RG][PM_COLS];
+  __shared__ double pcnt[PM_RG][PM_COLS];
+  __shared__ double lastv[PM_RG][PM_COLS];
+  __shared__ int haslast[PM_RG][PM_COLS];
   const int cg = threadIdx.x % PM_COLS, rg = threadIdx.x / PM_COLS;
   const int c = blockIdx.x * PM_COLS + cg;
   const bool cv = c < C;
@@ -39,18 +46,30 @@ __global__ __launch_bounds__(256) void prefix_mean_kernel(const double* __restri
     const int v = r / k, kk = r - v * k;
     return obj[((int64_t)v * G + g0 + kk) * C + cc];
   };
-  double s = 0.0;
+  double s = 0.0, n = 0.0;
   for (int r = r0; r < r1; r += 8) {
     double x[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) x[u] = at(min(r + u, r1 - 1));
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s += (r + u < r1) ? x[u] : 0.0;
+    for (int u = 0; u < 8; ++u) {
+      const bool ok = (r + u < r1) && (x[u] == x[u]);
+      s += ok ? x[u] : 0.0;
+      n += ok ? 1.0 : 0.0;
+    }
   }
   part[rg][cg] = s;
+  pcnt[rg][cg] = n;
   __syncthreads();
   s = 0.0;
-  for (int q = 0; q < rg; ++q) s += part[q][cg];
+  n = 0.0;
+  for (int q = 0; q < rg; ++q) {
+    s += part[q][cg];
+    n += pcnt[q][cg];
+  }
+  int lead = 0;                 // NaN rows before the chunk's first finite value
+  bool seen = false;
+  double last = __builtin_nan("");
   for (int r = r0; r < r1; r += 8) {
     double x[8];
 #pragma unroll
@@ -58,19 +77,37 @@ __global__ __launch_bounds__(256) void prefix_mean_kernel(const double* __restri
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       if (r + u < r1) {
-        s += x[u];
-        if (cv) cum[(int64_t)(r + u) * C + c] = s / (double)(r + u + 1);
+        if (x[u] == x[u]) {
+          s += x[u];
+          n += 1.0;
+          last = s / n;
+          seen = true;
+        } else if (!seen) {
+          ++lead;
+        }
+        if (cv && seen) cum[(int64_t)(r + u) * C + c] = last;
       }
     }
   }
+  lastv[rg][cg] = last;
+  haslast[rg][cg] = seen ? 1 : 0;
+  __syncthreads();
+  if (lead > 0 && cv) {
+    // the value carried into this chunk: the last finite-based mean of the closest earlier
+    // chunk that had one (NaN if none: no finite value yet)
+    double carry = __builtin_nan("");
+    for (int q = rg - 1; q >= 0; --q)
+      if (haslast[q][cg]) { carry = lastv[q][cg]; break; }
+    for (int r = r0; r < r0 + lead; ++r) cum[(int64_t)r * C + c] = carry;
+  }
 }
 
-// descending order with NaN first (torch.sort(descending=True) semantics); padding last
+// descending order, NaN after every number (unranked), padding last
 __device__ __forceinline__ bool before(double a, int ia, double b, int ib) {
   if (ia < 0) return false;                 // padding never precedes
   if (ib < 0) return true;
   const bool na = a != a, nb = b != b;
-  if (na != nb) return na;
+  if (na != nb) return nb;
   if (na) return ia < ib;
   return a > b || (a == b && ia < ib);
 }
@@ -109,7 +146,7 @@ __global__ __launch_bounds__(RK_T) void dense_rank_kernel(const double* __restri
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int i = 4 * t + q;
-    const bool real = idx[i] >= 0;
+    const bool real = idx[i] >= 0 && key[i] == key[i];      // NaN: not ranked
     nw[q] = real && (i == 0 || key[i] != key[i - 1]) ? 1 : 0;
     run += nw[q];
   }
@@ -131,7 +168,7 @@ __global__ __launch_bounds__(RK_T) void dense_rank_kernel(const double* __restri
   for (int q = 0; q < 4; ++q) {
     const int i = 4 * t + q;
     acc += nw[q];
-    if (idx[i] >= 0) dst[idx[i]] = (double)acc;
+    if (idx[i] >= 0) dst[idx[i]] = (key[i] == key[i]) ? (double)acc : __builtin_nan("");
   }
 }
 

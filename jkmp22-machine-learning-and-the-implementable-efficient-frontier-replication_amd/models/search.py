@@ -350,14 +350,23 @@ def validation_scores(obj: torch.Tensor, frame_g: int, compat: bool):
                   "pfml_validation_scores")
         return seq, cum, rank
     flat = seq.reshape(nV * k, nP, L)
-    cnt = torch.arange(1, nV * k + 1, dtype=flat.dtype, device=flat.device).view(-1, 1, 1)
-    cum = (_cumsum0(flat) / cnt).view(nV, k, nP, L)
-    # dense rank (descending) within each month over k * nP * L rows
+    # pandas expanding().mean(): NaN skipped (NaN until the first finite value)
+    ok = ~torch.isnan(flat)
+    cnt = _cumsum0(ok.to(flat.dtype))
+    tot = _cumsum0(torch.where(ok, flat, torch.zeros_like(flat)))
+    cum = torch.where(cnt > 0, tot / cnt.clamp_min(1.0),
+                      torch.full_like(tot, float("nan"))).view(nV, k, nP, L)
+    # dense rank (descending) within each month over k * nP * L rows; NaN unranked
     vals = cum.reshape(nV, -1)
-    sv, idx = torch.sort(vals, dim=1, descending=True, stable=True)
+    isn = torch.isnan(vals)
+    key = torch.where(isn, torch.full_like(vals, float("-inf")), vals)
+    sv, idx = torch.sort(key, dim=1, descending=True, stable=True)
+    snan = torch.gather(isn, 1, idx)
     new = torch.ones_like(sv, dtype=torch.int64)
     new[:, 1:] = (sv[:, 1:] != sv[:, :-1]).to(torch.int64)
+    new[snan] = 0
     dense = torch.cumsum(new, dim=1).to(vals.dtype)
+    dense[snan] = float("nan")
     rank = torch.empty_like(vals)
     rank.scatter_(1, idx, dense)
     return seq, cum, rank.view(nV, k, nP, L)

@@ -146,6 +146,41 @@ def ridge_plan(P: int, L: int, cell_src, cell_n, cell_scale) -> dict:
     return {"desc": desc, "work": int(wsz.sum()), "nmax": int(cell_n.max()), "nc": nc}
 
 
+nat.register_hip("pfml_ridge_repair", [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int,
+                                       C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int64,
+                                       C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p])
+nat.register_hip("pfml_ridge_repair_work_doubles", [C.c_int], C.c_int64)
+
+# device repair counts of the most recent ridge launches (int32 device scalars; read them
+# only when reporting - reading forces a sync)
+LAST_REPAIRS: list = []
+
+
+def repair_launch(plan: dict, d_desc: torch.Tensor, SD: torch.Tensor, Sr: torch.Tensor,
+                  lv: torch.Tensor, beta: torch.Tensor) -> torch.Tensor:
+    """Queue the device repair of the NaN-marked (non-SPD) systems of one ridge launch
+    (csrc/ridge_repair.hip: pivoted-LU re-solve, np.linalg.solve semantics) on the current
+    stream; returns the device count of repaired systems (no host sync)."""
+    P = SD.shape[-1]
+    L = int(lv.numel())
+    lib = nat.hip_lib()
+    count = torch.zeros(1, dtype=torch.int32, device=SD.device)
+    cap = plan["nc"] * L
+    lst = torch.empty(cap, dtype=torch.int32, device=SD.device)
+    work = torch.empty(lib.pfml_ridge_repair_work_doubles(plan["nmax"]), dtype=torch.float64,
+                       device=SD.device)
+    nat.check(lib.pfml_ridge_repair(SD.data_ptr(), P, Sr.data_ptr(), d_desc.data_ptr(),
+                                    plan["nc"], plan["nmax"], lv.data_ptr(), L, beta.data_ptr(),
+                                    beta.shape[-1], lst.data_ptr(), count.data_ptr(), cap,
+                                    work.data_ptr(), nat.stream_of(SD)), "pfml_ridge_repair")
+    return count
+
+
+def repairs_done() -> int:
+    """Host read of the repair counts of the last grid launches (one sync)."""
+    return int(sum(int(c.item()) for c in LAST_REPAIRS))
+
+
 def ridge_launch(plan: dict, d_desc: torch.Tensor, SD: torch.Tensor, Sr: torch.Tensor,
                  lv: torch.Tensor, beta: torch.Tensor, band_mode: int = 0) -> None:
     P = SD.shape[-1]
@@ -164,8 +199,8 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
     """beta[c, l, :n_c] = solve(SD[src_c][:n,:n]*scale_c + l I, Sr[src_c][:n]*scale_c).
 
     SD: [S, P, P] running sums, Sr: [S, P]; returns [ncells, L, P] (zero beyond n_c).
-    ``repair=False`` leaves the band path's non-SPD markers (NaN rows) for the caller to
-    repair (``repair_nonspd``), so no device->host sync happens here.
+    Non-SPD systems (NaN-marked by the band path) are re-solved on the device by pivoted LU
+    (``repair_launch``, no host sync); ``repair=False`` leaves the NaN markers.
     """
     S, P, _ = SD.shape
     L = int(lvec.numel())
@@ -180,7 +215,7 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
         SDc, Src = SD.contiguous(), Sr.contiguous()
         ridge_launch(plan, d_desc, SDc, Src, lv, beta, band_mode)
         if repair:
-            repair_nonspd(beta, SDc, Src, cell_src, cell_n, cell_scale, lv)
+            LAST_REPAIRS[:] = [repair_launch(plan, d_desc, SDc, Src, lv, beta)]
         return beta
     eye_cache = {}
     lv = lvec.to(dtype=SD.dtype)
@@ -199,9 +234,9 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
 
 
 def repair_nonspd(beta, SD, Sr, cell_src, cell_n, cell_scale, lv) -> np.ndarray:
-    """The band path marks a (cell, lambda) whose banded Cholesky met a non-positive pivot
-    (Dbar + l I not numerically SPD) with NaN; re-solve exactly those systems with pivoted LU
-    (np.linalg.solve semantics, PFML_Search_Coef.py:131-133).  One device->host flag read."""
+    """Host-side reference of the repair: re-solve the NaN-marked (cell, lambda) systems with
+    torch's pivoted LU (np.linalg.solve semantics, PFML_Search_Coef.py:131-133).  The engine
+    uses the device form (``repair_launch``); this one is the test oracle."""
     bad = torch.isnan(beta).any(dim=-1)
     if not bool(bad.any()):
         return np.zeros(0, dtype=np.int64)
@@ -303,8 +338,8 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     HIP stream, the big group first, so the small cells' whole chain runs on the CUs the big
     cells' one-workgroup-per-cell band reductions leave idle.  With few (multi-GPU shards) one
     chain in one stream.  Either way beta / obj rows are written in place from cached launch
-    plans, and the non-SPD check (one host sync) comes after the utilities are queued:
-    repairs (rare) are applied at the end and the utilities of repaired cells recomputed.
+    plans, and the non-SPD systems are re-solved on the device between each group's ridge
+    grid and its utilities (``repair_launch``: no host sync, counts in ``LAST_REPAIRS``).
     """
     cell_src, cell_n = np.asarray(cell_src), np.asarray(cell_n)
     cell_scale = np.asarray(cell_scale, dtype=np.float64)
@@ -334,22 +369,19 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
         side = _side_stream(dev)
         side.wait_stream(cur)
         streams = [side, cur]                    # big cells' factorisations issued first
+    counts = []
     for gi, stream in enumerate(streams):
         _, _, rp, qp = plan["groups"][gi]
         with torch.cuda.stream(stream):
             ridge_launch(rp, dv[3 * gi], SD, Sr, lv, beta, mode)
+            counts.append(repair_launch(rp, dv[3 * gi], SD, Sr, lv, beta))
             quad_launch(qp, dv[3 * gi + 1], dv[3 * gi + 2], D, R, beta, obj)
     th("launch")
     if split:
         cur.wait_stream(side)
-        for t in (SD, Sr, D, R, lv, beta, obj):
+        for t in (SD, Sr, D, R, lv, beta, obj, *counts):
             t.record_stream(side)
-    fixed = repair_nonspd(beta, SD, Sr, cell_src, cell_n, cell_scale, lv)
-    th("repair_check")
-    if len(fixed):
-        jobs = np.nonzero(np.isin(job_cell, fixed))[0]
-        obj[torch.as_tensor(jobs, device=SD.device)] = quadform_utilities(
-            D, R, beta, job_cell[jobs], job_month[jobs], job_n[jobs])
+    LAST_REPAIRS[:] = counts
     return beta, obj
 
 

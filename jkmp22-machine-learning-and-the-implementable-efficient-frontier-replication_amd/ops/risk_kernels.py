@@ -1,7 +1,8 @@
 """Device ops of the Barra risk model (csrc/risk.hip).
 
-* ``daily_ols``       - per-day OLS without intercept on CSR day segments, pinv fallback for
-                        exactly singular days (Estimate Covariance Matrix.py:214-233);
+* ``daily_ols``       - per-day OLS without intercept on CSR day segments; exactly singular
+                        days take pinv(X'X) X'y (Estimate Covariance Matrix.py:214-233) inside
+                        the same kernel (cyclic Jacobi, numpy's rcond = 1e-15);
 * ``ewma_factor_cov`` - monthly factor covariance F = sd cor sd * 21 from EWMA-weighted
                         cov.wt / cor.wt over the trailing ``obs`` days (:297-335,
                         General_functions.py:745-835);
@@ -45,17 +46,12 @@ def daily_ols(X: torch.Tensor, y: torch.Tensor, offsets: torch.Tensor):
     nat.check(nat.hip_lib().pfml_daily_ols(X.data_ptr(), y.data_ptr(), off.data_ptr(), D, K,
                                            coef.data_ptr(), resid.data_ptr(), status.data_ptr(),
                                            nat.stream_of(X)), "pfml_daily_ols")
-    bad = torch.nonzero(status).flatten().tolist()
-    for d in bad:                      # LinAlgError -> pinv(X'X) X'y (reference :228-229)
-        a, b = int(offsets[d]), int(offsets[d + 1])
-        Xd, yd = X[a:b], y[a:b]
-        XtX = Xd.T @ Xd
-        c = torch.linalg.pinv(XtX) @ (Xd.T @ yd)
-        coef[d] = c
-        resid[a:b] = yd - Xd @ c
-    if bad:
-        COUNTERS.add("risk.ols_pinv_fallback", len(bad))
-    return coef, resid, len(bad)
+    # status 2: the day met an exact zero pivot (LinAlgError) and the kernel applied
+    # pinv(X'X) X'y itself (reference :228-229); one count read, no host recompute
+    nbad = int((status == 2).sum().item())
+    if nbad:
+        COUNTERS.add("risk.ols_pinv_fallback", nbad)
+    return coef, resid, nbad
 
 
 def _daily_ols_torch(X, y, offsets):
@@ -71,7 +67,7 @@ def _daily_ols_torch(X, y, offsets):
         c, info = torch.linalg.solve_ex(XtX, Xty)
         if int(info) != 0:
             nbad += 1
-            c = torch.linalg.pinv(XtX) @ Xty
+            c = torch.linalg.pinv(XtX, rtol=1e-15) @ Xty      # numpy's default rcond
         coef[d] = c
         resid[off[d]:off[d + 1]] = yd - Xd @ c
     if nbad:

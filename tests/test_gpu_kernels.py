@@ -327,3 +327,47 @@ def test_grid_search_bitwise_deterministic(gpu):
     for b, o, k in runs[1:]:
         assert torch.equal(b, runs[0][0]) and torch.equal(o, runs[0][1])
         assert torch.equal(k, runs[0][2])
+
+
+def test_ridge_device_repair_matches_lu(gpu):
+    """Systems the banded Cholesky cannot factor (here an indefinite Dbar: small lambda makes
+    Dbar + lambda I indefinite) are NaN-marked by the band path and re-solved on the device by
+    pivoted LU before the utilities run - no host round trip; betas match np.linalg.solve."""
+    from pfml.ops import ridge as rg
+    P = 65
+    X = _rand(2, 200, P, seed=61)
+    SD = X.transpose(1, 2) @ X / 200
+    e, V = torch.linalg.eigh(SD[1])
+    SD[1] = SD[1] - (e[0] + 0.7) * torch.outer(V[:, 0], V[:, 0]) * 2.0   # one eigen < 0
+    Sr = _rand(2, P, seed=62)
+    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
+    src, nn, sc = np.array([0, 1, 1]), np.array([65, 65, 33]), np.array([1.0, 1.0, 1.0])
+    ref = rg.ridge_grid(SD, Sr, src, nn, sc, lv)            # CPU: LU per lambda
+    out = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
+    assert rg.repairs_done() > 0
+    ok = torch.isfinite(ref).all(-1)
+    rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1).clamp_min(1e-300))[ok].max().item()
+    assert rel < 1e-9, rel
+    assert torch.isfinite(out[ok]).all()
+
+
+def test_validation_scores_nan_cells(gpu):
+    """A singular cell (NaN utilities) gets NaN cum_obj until its first finite value and a NaN
+    rank, and never takes rank 1 (pandas expanding().mean() / rank(method='dense'))."""
+    from pfml.models.search import validation_scores
+    obj = _rand(24, 2, 2, 101, seed=71)
+    obj[:, 0, 1, 7] = float("nan")                        # one cell singular throughout
+    obj[:5, 1, 0, 3] = float("nan")                        # another singular early on
+    for compat in (True, False):
+        _, c0, r0 = validation_scores(obj, 1, compat)
+        _, c1, r1 = validation_scores(obj.to(gpu), 1, compat)
+        c1, r1 = c1.cpu(), r1.cpu()
+        assert torch.equal(torch.isnan(c0), torch.isnan(c1))
+        assert torch.allclose(c0.nan_to_num(), c1.nan_to_num(), rtol=1e-13, atol=1e-15)
+        assert torch.equal(torch.isnan(r0), torch.isnan(r1))
+        assert torch.equal(r0.nan_to_num(-1), r1.nan_to_num(-1))
+        for v in range(24):
+            rv = r1[v].reshape(-1)
+            fin = rv[~torch.isnan(rv)]
+            assert fin.min() == 1 and torch.equal(torch.unique(fin),
+                                                  torch.arange(1, int(fin.max()) + 1).double())

@@ -34,6 +34,34 @@ def test_daily_ols_matches_lstsq(gpu):
     assert np.all(np.isfinite(coef)) and np.all(np.isfinite(resid))
 
 
+def test_daily_ols_pinv_on_device(gpu):
+    """Exactly singular days (duplicated factor column; an all-zero dummy) hit LinAlgError in
+    the reference and take pinv(X'X) X'y: the kernel does that itself (Jacobi) - the
+    minimum-norm coefficients match numpy's pinv, no host fallback runs."""
+    from pfml.ops.risk_kernels import daily_ols
+    rng = np.random.default_rng(3)
+    K = 25
+    sizes = [120, 80, 300]
+    off = np.r_[0, np.cumsum(sizes)]
+    X = rng.standard_normal((off[-1], K))
+    y = rng.standard_normal(off[-1]) * 0.02
+    X[off[0]:off[1], 24] = X[off[0]:off[1], 23]          # day 0: duplicated column
+    X[off[1]:off[2], 5] = 0.0                            # day 1: empty dummy column
+    coef, resid, nbad = daily_ols(torch.tensor(X, device=gpu), torch.tensor(y, device=gpu),
+                                  torch.tensor(off))
+    coef, resid = coef.cpu().numpy(), resid.cpu().numpy()
+    assert nbad == 2
+    for d in range(3):
+        a, b = off[d], off[d + 1]
+        Xd, yd = X[a:b], y[a:b]
+        try:
+            ref = np.linalg.solve(Xd.T @ Xd, Xd.T @ yd)
+        except np.linalg.LinAlgError:
+            ref = np.linalg.pinv(Xd.T @ Xd) @ (Xd.T @ yd)
+        assert np.allclose(coef[d], ref, rtol=1e-7, atol=1e-10), (d, np.abs(coef[d] - ref).max())
+        assert np.allclose(resid[a:b], yd - Xd @ ref, atol=1e-9), d
+
+
 def test_ewma_factor_cov_matches_cov_wt(gpu):
     from pfml.ops.risk_kernels import ewma_factor_cov
     rng = np.random.default_rng(1)

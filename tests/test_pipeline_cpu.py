@@ -223,3 +223,24 @@ def test_gemm_fp32_precision_cpu():
     out = C0.clone()
     gemm_prec(A, B, "fp32", trans_a=True, trans_b=True, beta=2.0, out=out)
     assert torch.allclose(out, 2.0 * C0 + gemm(A, B, trans_a=True, trans_b=True), atol=1e-4)
+
+
+def test_validation_scores_nan_semantics_cpu():
+    """pandas semantics of PFML_hp_reals.py:109-122 on a NaN utility: expanding mean skips
+    NaN, dense descending rank leaves NaN unranked."""
+    import pandas as pd
+    from pfml.models.search import validation_scores
+    g = torch.Generator().manual_seed(0)
+    obj = torch.randn(6, 1, 1, 4, generator=g, dtype=torch.float64)
+    obj[:2, 0, 0, 1] = float("nan")
+    obj[:, 0, 0, 3] = float("nan")
+    _, cum, rank = validation_scores(obj, 0, False)
+    df = pd.DataFrame({"obj": obj.reshape(6, 4).T.reshape(-1).numpy(),
+                       "l": np.repeat(np.arange(4), 6), "m": np.tile(np.arange(6), 4)})
+    df["cum"] = df.groupby("l")["obj"].transform(lambda x: x.expanding().mean())
+    df["rank"] = df.groupby("m")["cum"].rank(method="dense", ascending=False)
+    exp_c = df.pivot(index="m", columns="l", values="cum").to_numpy()
+    exp_r = df.pivot(index="m", columns="l", values="rank").to_numpy()
+    assert np.allclose(cum.reshape(6, 4).numpy(), exp_c, equal_nan=True, rtol=1e-14)
+    assert np.array_equal(np.nan_to_num(rank.reshape(6, 4).numpy(), nan=-1),
+                          np.nan_to_num(exp_r, nan=-1))
