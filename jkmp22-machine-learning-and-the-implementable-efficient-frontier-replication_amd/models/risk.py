@@ -145,9 +145,9 @@ def daily_ols(X: np.ndarray, y: np.ndarray, day: np.ndarray, device) -> tuple:
     return day[gs[:-1]], coef.cpu().numpy(), resid.cpu().numpy(), nbad
 
 
-def estimate_cov(cfg: Config, device: str = "cpu", write: bool = True) -> BarraCov:
-    s = cfg.settings
-    cs = s["cov_set"]
+def _load_risk_inputs(cfg: Config):
+    """Factors_processed (valid rows), the daily excess returns of those ids and the cluster
+    labels (Estimate Covariance Matrix.py:50-100)."""
     dd = cfg.run.data_dir
     features = get_features()
     chars = io.read_processed_chars(dd, features)
@@ -159,7 +159,204 @@ def estimate_cov(cfg: Config, device: str = "cpu", write: bool = True) -> BarraC
     valid_ids = chars["id"].unique()
     daily = daily[daily["ret_exc"].notna() & daily["id"].isin(valid_ids)].copy()
     labels = pd.read_csv(io.path(dd, "cluster_labels_processed.csv"))
+    return chars, daily, labels
 
+
+def estimate_cov(cfg: Config, device: str = "cpu", write: bool = True) -> BarraCov:
+    """S3 (Estimate Covariance Matrix.py): load, ``estimate_cov_frames``, write Barra_Cov."""
+    chars, daily, labels = _load_risk_inputs(cfg)
+    barra = estimate_cov_frames(chars, daily, labels, cfg.settings["cov_set"], device)
+    log.info(f"Barra covariance for {len(barra.months)} months, K = {len(barra.factors)} "
+             f"factors.")
+    if write:
+        barra.save(os.path.join(cfg.run.data_dir, "Barra_Cov.npz"))
+    return barra
+
+
+def _seg_zscore(X: torch.Tensor, g: torch.Tensor, G: int) -> torch.Tensor:
+    """(x - mean) / std per group g of the rows, column-wise, NaN skipped, ddof = 1 (pandas
+    groupby transform of ``(x - x.mean()) / x.std()``; two-pass like nanops.nanvar)."""
+    ok = torch.isfinite(X)
+    Xz = torch.where(ok, X, torch.zeros_like(X))
+    okf = ok.to(X.dtype)
+    cnt = torch.zeros((G, X.shape[1]), dtype=X.dtype, device=X.device).index_add_(0, g, okf)
+    sm = torch.zeros_like(cnt).index_add_(0, g, Xz)
+    mean = sm / cnt
+    dev = (X - mean[g])
+    ss = torch.zeros_like(cnt).index_add_(0, g, torch.where(ok, dev * dev, torch.zeros_like(X)))
+    std = torch.sqrt(ss / (cnt - 1.0))
+    std = torch.where(cnt > 1.0, std, torch.full_like(std, float("nan")))
+    return dev / std[g]
+
+
+def _seg_median(v: torch.Tensor, g: torch.Tensor, G: int) -> torch.Tensor:
+    """Median of the non-NaN values of each group (pandas median: mean of the two middle
+    values; NaN for an all-NaN / empty group) via two stable sorts on the device."""
+    key = torch.where(torch.isnan(v), torch.full_like(v, float("inf")), v)
+    o1 = torch.sort(key, stable=True).indices
+    o2 = torch.sort(g[o1], stable=True).indices
+    order = o1[o2]
+    sv = v[order]
+    size = torch.zeros(G, dtype=torch.int64, device=v.device).index_add_(
+        0, g, torch.ones_like(g))
+    cnt = torch.zeros(G, dtype=torch.int64, device=v.device).index_add_(
+        0, g, (~torch.isnan(v)).to(torch.int64))
+    start = torch.cumsum(size, 0) - size
+    lo = start + torch.clamp(cnt - 1, min=0) // 2
+    hi = start + cnt // 2
+    last = max(len(v) - 1, 0)
+    med = 0.5 * (sv[lo.clamp(max=last)] + sv[hi.clamp(max=last)])
+    return torch.where(cnt > 0, med, torch.full_like(med, float("nan")))
+
+
+def _codes(*cols) -> np.ndarray:
+    """Dense int64 codes of the rows' key tuples (order-preserving, NaN / None -> -1)."""
+    key = pd.MultiIndex.from_arrays([pd.Series(c) for c in cols])
+    codes, _ = pd.factorize(key)
+    return codes.astype(np.int64)
+
+
+def estimate_cov_frames(chars: pd.DataFrame, daily: pd.DataFrame, labels: pd.DataFrame,
+                        cs: dict, device: str = "cpu") -> BarraCov:
+    """The Barra model from in-memory frames, batched end to end (no per-day / per-month
+    Python loop, no groupby lambda, no frame merges over the daily panel):
+
+    * cluster ranks (K25): one GEMM; the per-month z-score of the clusters (:155-158) as a
+      segmented two-pass mean / std on the device (``_seg_zscore``);
+    * the daily <- previous-month exposure merge (:168-183) by integer (id, month) keys and a
+      sorted search, exposures gathered on the device;
+    * daily OLS (K21), EWMA factor cov (K22), EWMA idio vol (K23): csrc/risk.hip;
+    * the >= 200-of-252-days filter and last observation per month (:409-439) on index arrays;
+    * Barra assembly (:453-494) for all calc months at once: size-group medians and the
+      month-median fallback as segmented device medians (``_seg_median``, K27).
+    ``estimate_cov_frames_pandas`` is the previous, pandas-bound form (test oracle)."""
+    from ..ops.risk_kernels import daily_ols as _ols, ewma_factor_cov, ewma_vol as _ewma_vol
+    from ..ops.ridge import _HostClock
+    th = _HostClock()                                   # PFML_HOST_TIMING=1: section times
+    dev = torch.device(device)
+    f64 = dict(dtype=torch.float64, device=dev)
+    features = get_features()
+    chars = chars.sort_values(["eom", "id"], kind="stable").reset_index(drop=True)
+    clusters, R = cluster_ranks(chars, labels, features)
+    log.info(f"Cluster Labels are the following {clusters}")
+    ids_m = chars["id"].to_numpy(np.int64)
+    mi_m = month_index(chars["eom"])
+    industries = sorted(chars["ff12"].dropna().unique())
+    ff = chars["ff12"].to_numpy(object)
+    D = np.stack([(ff == ind).astype(np.float64) for ind in industries], axis=1) \
+        if industries else np.zeros((len(chars), 0))
+    mcode = np.searchsorted(np.unique(mi_m), mi_m)
+    Z = _seg_zscore(torch.as_tensor(R, **f64), torch.as_tensor(mcode, device=dev),
+                    int(mcode.max()) + 1 if len(mcode) else 0)
+    Fexp = torch.cat([torch.as_tensor(D, **f64), Z], dim=1)          # [rows, K] exposures
+    factor_cols = [str(i) for i in industries] + clusters
+    sg = chars["size_grp"]
+    row_ok = torch.isfinite(Fexp).all(1) & torch.as_tensor(
+        (sg.notna() & chars["ff12"].notna()).to_numpy(), device=dev)
+    log.info("Cluster Ranks Completed.")
+    th("s3.cluster_ranks+zscore")
+
+    # ---- daily <- exposures of the PREVIOUS month (eom_ret = eom + 1M), inner + dropna ------
+    dd_date = daily["date"].to_numpy().astype("datetime64[D]")
+    keep = dd_date >= np.datetime64(chars["eom"].min().date())
+    d_id = daily["id"].to_numpy(np.int64)[keep]
+    d_date = dd_date[keep]
+    d_ret = daily["ret_exc"].to_numpy(np.float64)[keep]
+    d_mi = month_index(d_date)
+    SH = np.int64(1 << 20)
+    mkey = ids_m * SH + (mi_m + 1)                                   # key of (id, eom_ret)
+    mo = np.argsort(mkey, kind="stable")
+    dkey = d_id * SH + d_mi
+    pos = np.clip(np.searchsorted(mkey[mo], dkey), 0, max(len(mkey) - 1, 0))
+    hit = (mkey[mo][pos] == dkey) if len(mkey) else np.zeros(len(dkey), bool)
+    mrow = mo[pos]
+    ok_rows = row_ok.cpu().numpy()
+    sel = hit & ok_rows[mrow] & np.isfinite(d_ret)
+    d_id, d_date, d_ret, mrow = d_id[sel], d_date[sel], d_ret[sel], mrow[sel]
+    dnum = d_date.astype(np.int64)
+    order = np.lexsort((d_id, dnum))                                  # (date, id)
+    d_id, dnum, d_ret, mrow = d_id[order], dnum[order], d_ret[order], mrow[order]
+    gs_day = rt.group_starts(dnum)
+    th("s3.daily_merge")
+    Xd = Fexp[torch.as_tensor(mrow, device=dev)].contiguous()
+    coef, resid_t, nbad = _ols(Xd, torch.as_tensor(d_ret, **f64), torch.as_tensor(gs_day))
+    days = dnum[gs_day[:-1]]
+    log.info(f"Factor Returns Completed ({len(days)} days, {nbad} pinv fallbacks).")
+    th("s3.daily_ols")
+
+    # ---- EWMA factor covariance per calc month (:275-338) --------------------------
+    obs = int(cs["obs"])
+    tr = np.arange(obs, 0, -1, dtype=np.float64)
+    w_cor = (0.5 ** (1.0 / cs["hl_cor"])) ** tr
+    w_var = (0.5 ** (1.0 / cs["hl_var"])) ** tr
+    if len(days) <= obs:
+        raise ValueError(f"need more than {obs} factor-return days, have {len(days)}")
+    day_dt = days.astype("datetime64[D]")
+    ref = pd.Timestamp(day_dt[obs])
+    min_date = ref.to_period("M").to_timestamp() - pd.offsets.MonthEnd(1)
+    eoms = chars["eom"].to_numpy().astype("datetime64[D]")
+    calc = np.unique(eoms[eoms >= np.datetime64(min_date.date())])
+    calc_mi = month_index(calc)
+    end_idx = np.searchsorted(day_dt, calc, side="right")
+    Fm = ewma_factor_cov(coef, end_idx, obs, w_cor, w_var, scale=21.0).cpu().numpy()
+    th("s3.ewma_factor_cov")
+
+    # ---- idiosyncratic EWMA vol (:345-442) -----------------------------------------
+    o2 = np.lexsort((dnum, d_id))                                     # (id, date)
+    s_id, s_date = d_id[o2], dnum[o2]
+    resid_s = resid_t[torch.as_tensor(o2, device=dev)]
+    gs_id = rt.group_starts(s_id)
+    lam = 0.5 ** (1.0 / cs["hl_stock_var"])
+    res_vol = _ewma_vol(resid_s, gs_id, lam, int(cs["initial_var_obs"])).cpu().numpy()
+    dpos = np.searchsorted(days, s_date)
+    td_252 = np.where(dpos >= 252, days[np.maximum(dpos - 252, 0)].astype(np.float64), np.nan)
+    d200 = rt.group_shift(s_date.astype(np.float64), gs_id, 200)
+    ok = (d200 >= td_252) & ~np.isnan(res_vol)
+    s_mi = month_index(s_date.astype("datetime64[D]"))
+    # the last observation per (id, month) among the rows that pass the filter
+    f_id, f_mi, f_date, f_vol = s_id[ok], s_mi[ok], s_date[ok], res_vol[ok]
+    flast = np.r_[(f_id[1:] != f_id[:-1]) | (f_mi[1:] != f_mi[:-1]), True] if len(f_id) else \
+        np.zeros(0, bool)
+    vkey = f_id[flast] * SH + f_mi[flast]
+    vval = f_vol[flast]
+    th("s3.idio_vol")
+
+    # ---- Barra assembly (:453-494), every calc month at once -----------------------------
+    in_calc = np.isin(mi_m, calc_mi)
+    rows = np.nonzero(in_calc)[0]                                     # (eom, id) order
+    rkey = ids_m[rows] * SH + mi_m[rows]
+    vo = np.argsort(vkey, kind="stable")
+    vp = np.clip(np.searchsorted(vkey[vo], rkey), 0, max(len(vkey) - 1, 0))
+    vhit = (vkey[vo][vp] == rkey) if len(vkey) else np.zeros(len(rkey), bool)
+    rv = np.where(vhit, vval[vo][vp], np.nan)
+    rv_t = torch.as_tensor(rv, **f64)
+    gcode = _codes(mi_m[rows], sg.to_numpy(object)[rows])
+    sg_nan = sg.isna().to_numpy()[rows]
+    G1 = int(gcode.max()) + 1 if len(gcode) else 0
+    med_g = _seg_median(rv_t, torch.as_tensor(gcode, device=dev), G1)[torch.as_tensor(gcode, device=dev)]
+    med_g = torch.where(torch.as_tensor(sg_nan, device=dev), torch.full_like(med_g, float("nan")),
+                        med_g)                                        # NaN size_grp: no group
+    mcode2 = np.searchsorted(calc_mi, mi_m[rows])
+    med_m = _seg_median(rv_t, torch.as_tensor(mcode2, device=dev), len(calc_mi))[
+        torch.as_tensor(mcode2, device=dev)]
+    med = torch.where(torch.isnan(med_g), med_m, med_g)
+    rv_f = torch.where(torch.isnan(rv_t), med, rv_t)
+    ivol = (rv_f * rv_f * 21.0).cpu().numpy()
+    off = np.concatenate([[0], np.cumsum(np.bincount(np.searchsorted(calc_mi, mi_m[rows]),
+                                                     minlength=len(calc_mi)))])
+    th("s3.barra_assembly")
+    return BarraCov(months=calc_mi.astype(np.int64), offsets=off.astype(np.int64),
+                    ids=ids_m[rows], X=Fexp[torch.as_tensor(rows, device=dev)].cpu().numpy(),
+                    ivol=ivol, F=Fm, factors=factor_cols)
+
+
+def estimate_cov_frames_pandas(chars: pd.DataFrame, daily: pd.DataFrame, labels: pd.DataFrame,
+                               cs: dict, device: str = "cpu") -> BarraCov:
+    """The round-1 pandas-bound form of ``estimate_cov_frames`` (groupby-lambda z-score,
+    frame merges over the daily panel, one loop iteration per calc month): the test oracle
+    and the host baseline of tools/bench_s3.py."""
+    features = get_features()
+    chars = chars.sort_values(["eom", "id"], kind="stable").reset_index(drop=True)
     clusters, R = cluster_ranks(chars, labels, features)
     log.info(f"Cluster Labels are the following {clusters}")
     cm = chars[["id", "eom", "size_grp", "ff12"]].copy()
@@ -185,6 +382,7 @@ def estimate_cov(cfg: Config, device: str = "cpu", write: bool = True) -> BarraC
     days, coef, resid, nbad = daily_ols(dm[factor_cols].to_numpy(np.float64),
                                         dm["ret_exc"].to_numpy(np.float64), dnum, device)
     log.info(f"Factor Returns Completed ({len(days)} days, {nbad} pinv fallbacks).")
+    th("s3.daily_ols")
 
     # ---- EWMA factor covariance per calc month (:275-338) --------------------------
     obs = int(cs["obs"])
@@ -236,10 +434,6 @@ def estimate_cov(cfg: Config, device: str = "cpu", write: bool = True) -> BarraC
         X_l.append(cd[factor_cols].to_numpy(np.float64))
         iv_l.append(cd["res_vol"].to_numpy(np.float64) ** 2 * 21.0)
         off.append(off[-1] + len(cd))
-    barra = BarraCov(months=calc_mi.astype(np.int64), offsets=np.asarray(off, np.int64),
-                     ids=np.concatenate(ids_l), X=np.concatenate(X_l), ivol=np.concatenate(iv_l),
-                     F=Fm, factors=factor_cols)
-    log.info(f"Barra covariance for {len(calc_mi)} months, K = {len(factor_cols)} factors.")
-    if write:
-        barra.save(os.path.join(dd, "Barra_Cov.npz"))
-    return barra
+    return BarraCov(months=calc_mi.astype(np.int64), offsets=np.asarray(off, np.int64),
+                    ids=np.concatenate(ids_l), X=np.concatenate(X_l), ivol=np.concatenate(iv_l),
+                    F=Fm, factors=factor_cols)

@@ -96,3 +96,18 @@ def test_ewma_vol_matches_numba_semantics(gpu):
     assert np.array_equal(np.isnan(out), np.isnan(ref))
     ok = ~np.isnan(ref)
     assert np.allclose(out[ok], ref[ok], rtol=1e-12, atol=0)
+
+
+def test_estimate_cov_device_matches_pandas_form(gpu, small_data):
+    """The batched S3 (segmented z-score / medians, integer-key merges) vs the pandas-bound
+    form, both with the HIP OLS / EWMA kernels (the CPU OLS differs on the thin early days,
+    where pinv of a numerically rank-deficient X'X is cutoff-sensitive)."""
+    from pfml.models import risk
+    chars, daily, labels = risk._load_risk_inputs(small_data)
+    cs = small_data.settings["cov_set"]
+    a = risk.estimate_cov_frames(chars, daily, labels, cs, "cuda")
+    b = risk.estimate_cov_frames_pandas(chars, daily, labels, cs, "cuda")
+    assert np.array_equal(a.ids, b.ids) and np.array_equal(a.offsets, b.offsets)
+    assert np.allclose(a.X, b.X, rtol=1e-12, atol=1e-12, equal_nan=True)
+    assert np.allclose(a.F, b.F, rtol=1e-9, atol=1e-12 * np.abs(b.F).max())
+    assert np.allclose(a.ivol, b.ivol, rtol=1e-9, atol=1e-10 * np.abs(b.ivol).max())

@@ -244,3 +244,19 @@ def test_validation_scores_nan_semantics_cpu():
     assert np.allclose(cum.reshape(6, 4).numpy(), exp_c, equal_nan=True, rtol=1e-14)
     assert np.array_equal(np.nan_to_num(rank.reshape(6, 4).numpy(), nan=-1),
                           np.nan_to_num(exp_r, nan=-1))
+
+
+def test_estimate_cov_batched_matches_pandas_form(small_data):
+    """S3 batched form (integer-key merges, segmented z-score / medians, no per-month loop)
+    equals the pandas-bound form (groupby lambdas, frame merges, month loop)."""
+    from pfml.models import risk
+    chars, daily, labels = risk._load_risk_inputs(small_data)
+    cs = small_data.settings["cov_set"]
+    a = risk.estimate_cov_frames(chars, daily, labels, cs, "cpu")
+    b = risk.estimate_cov_frames_pandas(chars, daily, labels, cs, "cpu")
+    assert np.array_equal(a.months, b.months) and np.array_equal(a.offsets, b.offsets)
+    assert np.array_equal(a.ids, b.ids) and a.factors == b.factors
+    assert np.allclose(a.X, b.X, rtol=1e-12, atol=1e-12, equal_nan=True)
+    # (atol relative to the scale: a stock whose residuals are rounding noise has ivol ~1e-31)
+    assert np.allclose(a.F, b.F, rtol=1e-10, atol=1e-12 * np.abs(b.F).max())
+    assert np.allclose(a.ivol, b.ivol, rtol=1e-10, atol=1e-10 * np.abs(b.ivol).max())
