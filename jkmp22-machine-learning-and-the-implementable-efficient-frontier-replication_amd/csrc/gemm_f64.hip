@@ -44,6 +44,8 @@ struct Epi {
   const double* dv; int64_t sdv;      //   or per-row vector
   int has_diag;
   const double* es; int64_t ses;      // addend row scale (null: 1)
+  int sincos;                         // RFF epilogue: C[i][1+2j] = cos v, C[i][2+2j] = sin v,
+                                      // C[i][0] = 1 (K13: cos/sin of X W, interleaved order)
 };
 
 typedef double double2_t __attribute__((ext_vector_type(2)));
@@ -218,6 +220,17 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(
       for (int r = 0; r < 4; ++r) {
         const int gi = bm + wm * (BM / 2) + i * 16 + PFML_F64_CROW(lane, r);
         const int gj = bn + wn * (BN / 2) + j * 16 + li;
+        if (ep.sincos) {
+          if (gi < M && gj < N) {
+            double sn, cs;
+            sincos(ep.alpha * acc[i][j][r], &sn, &cs);
+            double* row = C + (int64_t)gi * ldc;
+            row[1 + 2 * gj] = cs;
+            row[2 + 2 * gj] = sn;
+            if (gj == 0) row[0] = 1.0;
+          }
+          continue;
+        }
         if (gi < M && gj < N) {
           double v = ep.alpha * acc[i][j][r];
           if (rsb) v *= rsb[gi];
@@ -289,6 +302,7 @@ struct PfmlGemmEpi {
   const double* dv; int64_t sdv;
   int has_diag;
   const double* es; int64_t ses;
+  int sincos;
   int tile_cfg;      // 0 auto, 1: 128x128, 2: 128x64, 3: 64x64
 };
 
@@ -301,7 +315,8 @@ extern "C" hipError_t pfml_dgemm_ex(int ta, int tb, int M, int N, int K, int bat
                                     const PfmlGemmEpi* h, hipStream_t st) {
   if (M <= 0 || N <= 0 || batch <= 0) return hipSuccess;
   Epi ep{h->alpha, h->beta, h->rs, h->srs, h->cs, h->scs, h->ks, h->sks, h->E, h->lde, h->sE,
-         h->e_cols, h->diag_col0, h->dval, h->dv, h->sdv, h->has_diag, h->es, h->ses};
+         h->e_cols, h->diag_col0, h->dval, h->dv, h->sdv, h->has_diag, h->es, h->ses,
+         h->sincos};
   int cfg = h->tile_cfg;
   if (cfg == 0) {
     // 64 x 64 tiles measure as fast as 128 x 128 on the S4 shapes (N ~ 500) and fill the chip

@@ -382,7 +382,6 @@ def estimate_cov_frames_pandas(chars: pd.DataFrame, daily: pd.DataFrame, labels:
     days, coef, resid, nbad = daily_ols(dm[factor_cols].to_numpy(np.float64),
                                         dm["ret_exc"].to_numpy(np.float64), dnum, device)
     log.info(f"Factor Returns Completed ({len(days)} days, {nbad} pinv fallbacks).")
-    th("s3.daily_ols")
 
     # ---- EWMA factor covariance per calc month (:275-338) --------------------------
     obs = int(cs["obs"])

@@ -28,7 +28,7 @@ class _Epi(C.Structure):
     _fields_ = [("alpha", _D), ("beta", _D), ("rs", _P), ("srs", _L), ("cs", _P), ("scs", _L),
                 ("ks", _P), ("sks", _L), ("E", _P), ("lde", _L), ("sE", _L), ("e_cols", _I),
                 ("diag_col0", _I), ("dval", _D), ("dv", _P), ("sdv", _L), ("has_diag", _I),
-                ("es", _P), ("ses", _L), ("tile_cfg", _I)]
+                ("es", _P), ("ses", _L), ("sincos", _I), ("tile_cfg", _I)]
 
 
 nat.register_hip("pfml_dgemm_ex", [_I, _I, _I, _I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _L,
@@ -224,20 +224,27 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
                k_scale: torch.Tensor | None = None, addend: torch.Tensor | None = None,
                addend_cols: int | None = None, diag_col0: int | None = None,
                diag_value: float = 1.0, diag_vec: torch.Tensor | None = None,
-               addend_row_scale: torch.Tensor | None = None, tile_cfg: int = 0) -> torch.Tensor:
+               addend_row_scale: torch.Tensor | None = None, sincos: bool = False,
+               tile_cfg: int = 0) -> torch.Tensor:
     """out = alpha diag(rs) op(A) diag(ks) op(B) diag(cs) + beta out
              + diag(es) addend[:, :, :addend_cols]  (on out's first addend_cols columns)
              + diag(diag_vec or diag_value) placed at out[:, i, diag_col0 + i].
 
     One launch of csrc/gemm_f64.hip on a HIP device (the Horner step of (24), Sigma = X F X'
     + diag(ivol), ...); the same arithmetic in torch fp64 on CPU.  3-D batched operands
-    (batch stride 0 = broadcast); scale vectors are [n] or [B, n]."""
+    (batch stride 0 = broadcast); scale vectors are [n] or [B, n].
+
+    ``sincos=True`` (K13): v = alpha op(A) op(B) never stored - out (width >= 2 N + 1) gets
+    the row [1, cos v_1, sin v_1, cos v_2, sin v_2, ...] (columns past 2 N + 1 untouched)."""
     A3, B3, C3 = _as3(A), _as3(B), _as3(out)
     batch = C3.shape[0]
     M = A3.shape[2] if trans_a else A3.shape[1]
     K = A3.shape[1] if trans_a else A3.shape[2]
     N = B3.shape[1] if trans_b else B3.shape[2]
-    if (B3.shape[2] if trans_b else B3.shape[1]) != K or tuple(C3.shape[1:]) != (M, N):
+    if sincos:
+        if C3.shape[1] != M or C3.shape[2] < 2 * N + 1:
+            raise ValueError("gemm_fused(sincos): out must be [.., M, >= 2N + 1]")
+    elif (B3.shape[2] if trans_b else B3.shape[1]) != K or tuple(C3.shape[1:]) != (M, N):
         raise ValueError(f"gemm_fused: shapes {tuple(A3.shape)} {tuple(B3.shape)} -> {tuple(C3.shape)}")
     if addend is not None and addend_cols is None:
         addend_cols = N
@@ -257,7 +264,7 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
                   nat.ptr(E3), 0 if E3 is None else E3.stride(1),
                   0 if E3 is None else _bstride(E3, batch), int(addend_cols or 0),
                   int(diag_col0 or 0), float(diag_value), nat.ptr(dv), sdv,
-                  int(diag_col0 is not None), nat.ptr(es), ses, int(tile_cfg))
+                  int(diag_col0 is not None), nat.ptr(es), ses, int(sincos), int(tile_cfg))
         nat.check(nat.hip_lib().pfml_dgemm_ex(
             int(trans_a), int(trans_b), M, N, K, batch,
             A3.data_ptr(), A3.stride(1), _bstride(A3, batch),
@@ -278,6 +285,11 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
         csv = col_scale if col_scale.dim() == 2 else col_scale.unsqueeze(0)
         r = r * csv.unsqueeze(-2)
     r = alpha * r
+    if sincos:
+        C3[:, :, 0] = 1.0
+        C3[:, :, 1:2 * N + 1:2] = torch.cos(r)
+        C3[:, :, 2:2 * N + 1:2] = torch.sin(r)
+        return out
     if beta != 0.0:
         r = r + beta * C3
     r = r.expand(batch, M, N).clone()

@@ -1,6 +1,7 @@
 """Panel signal ops: RFF features (K13) and per-month standardisation (K11/K12).
 
-Device paths run csrc/panel.hip (+ pfml_dgemm for X W); CPU paths are the torch fp64 oracle
+Device paths run the fused GEMM (csrc/gemm_f64.hip, sincos epilogue) and csrc/panel.hip; CPU
+paths are the torch fp64 oracle
 of PFML_Input_Data.py:179-185 (cos/sin of X W) and :364-388 (demean, unit L2 norm, 1/vol).
 """
 from __future__ import annotations
@@ -10,7 +11,7 @@ import ctypes as C
 import torch
 
 from . import _native as nat
-from .gemm import gemm_prec
+from .gemm import gemm_fused, gemm_prec
 
 nat.register_hip("pfml_rff_sincos", [C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int64,
                                      C.c_void_p])
@@ -23,11 +24,21 @@ def rff_features(X: torch.Tensor, W: torch.Tensor, precision: str = "fp64",
                  width: int | None = None, pad_rows: int = 0) -> torch.Tensor:
     """[R, k] x [k, P/2] -> [R + pad_rows, width] rows [1, cos z1, sin z1, cos z2, sin z2, ...,
     0 ...] (P = 2 (P/2) + 1 real columns; ``width`` >= P pads with zero columns, ``pad_rows``
-    appends all-zero rows).  X W is one fp64 MFMA GEMM, cos/sin one sincos kernel (two launches;
-    ``precision`` fp32 / bf16 / fp8 lowers X W for the experimental configs)."""
+    appends all-zero rows).  fp64 on a device: ONE launch of the fused GEMM whose epilogue
+    writes cos / sin of each accumulator straight into the interleaved row (X W never
+    stored); ``precision`` fp32 / bf16 / fp8 (experimental configs): the lowered GEMM, then the
+    sincos kernel."""
     R, half = X.shape[0], W.shape[1]
     P = 2 * half + 1
     width = width or P
+    if nat.is_device(X) and precision == "fp64":
+        out = torch.empty((R + pad_rows, width), dtype=X.dtype, device=X.device)
+        if pad_rows:
+            out[R:].zero_()
+        if width > P:
+            out[:R, P:].zero_()
+        gemm_fused(X.contiguous(), W.contiguous(), out[:R], sincos=True)
+        return out
     Z = gemm_prec(X, W, precision)
     if nat.is_device(X):
         out = torch.empty((R + pad_rows, width), dtype=X.dtype, device=X.device)

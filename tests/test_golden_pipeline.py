@@ -30,7 +30,7 @@ def ref_run(tmp_path_factory):
     d = str(tmp_path_factory.mktemp("ref_pipeline"))
     cfg = mk.engine_inputs(d)
     mk.small_rff_w(d, len(get_features()), cfg.p_max // 2, seed=meta["rff_w_seed"])
-    if mk.input_checksum(d) != meta["input_checksum"]:
+    if not mk.fingerprint_matches(mk.input_fingerprint(d), meta["input_fingerprint"]):
         pytest.fail("regenerated L0-L3 inputs differ from the golden's (L2/L3 changed?): "
                     "re-freeze with tools/make_golden_pipeline.py")
     cfg = cfg.override([f"run.artifact_dir={os.path.join(d, 'art')}"])

@@ -26,7 +26,6 @@ engine-produced inputs is stored so the test detects an input drift.
 
     python tools/make_golden_pipeline.py [/root/reference]
 """
-import hashlib
 import json
 import os
 import pickle
@@ -70,17 +69,38 @@ def small_rff_w(data_dir: str, k: int, half: int, seed: int = 11) -> None:
     pd.DataFrame(W).to_csv(os.path.join(data_dir, "rff_w.csv"))
 
 
-def input_checksum(data_dir: str) -> str:
+def input_fingerprint(data_dir: str) -> dict:
+    """Per-array [size, NaN count, sum, sum |x|, sum x^2, <x, fixed random weights>] of the
+    L2/L3 inputs.  Compared at rtol 1e-9 (``fingerprint_matches``): an L2/L3 change shows,
+    rounding-level reorderings of the same arithmetic (a batched S3) do not."""
     from pfml.config import get_features
     from pfml.data import io
     from pfml.models.risk import BarraCov
     chars = io.read_processed_chars(data_dir, get_features())
     b = BarraCov.load(os.path.join(data_dir, "Barra_Cov.npz"))
-    h = hashlib.sha256()
-    for a in (chars.select_dtypes("number").to_numpy(np.float64), b.X, b.F, b.ivol,
-              b.ids.astype(np.float64)):
-        h.update(np.round(np.nan_to_num(a, nan=-7.0), 10).tobytes())
-    return h.hexdigest()[:16]
+    out = {}
+    for name, a in (("chars", chars.select_dtypes("number").to_numpy(np.float64)), ("X", b.X),
+                    ("F", b.F), ("ivol", b.ivol), ("ids", b.ids.astype(np.float64))):
+        a = np.asarray(a, np.float64).ravel()
+        nan = np.isnan(a)
+        v = a[~nan]
+        w = np.random.default_rng(5).uniform(0.5, 1.5, v.size)
+        out[name] = [float(a.size), float(nan.sum()), float(v.sum()), float(np.abs(v).sum()),
+                     float((v * v).sum()), float(v @ w)]
+    return out
+
+
+def fingerprint_matches(a: dict, b: dict, rtol: float = 1e-9) -> bool:
+    if set(a) != set(b):
+        return False
+    for k in a:
+        x, y = np.asarray(a[k]), np.asarray(b[k])
+        scale = max(float(np.abs(y[3])), 1.0)              # sum |x| bounds every entry
+        if x.shape != y.shape or x[0] != y[0] or x[1] != y[1]:
+            return False
+        if np.any(np.abs(x[2:] - y[2:]) > rtol * np.maximum(np.abs(y[2:]), scale)):
+            return False
+    return True
 
 
 def write_reference_barra(data_dir: str, dst: str) -> None:
@@ -201,7 +221,7 @@ def main():
     for n in ("weights.csv", "pf.csv", "pf_summary.csv"):
         shutil.copy(os.path.join(data, n), os.path.join(OUT, n))
     meta = {"overrides": OVERRIDES, "validation_rows": int(len(val)),
-            "input_checksum": input_checksum(data), "rff_w_seed": 11,
+            "input_fingerprint": input_fingerprint(data), "rff_w_seed": 11,
             "reference_scripts": SCRIPTS}
     with open(os.path.join(OUT, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
