@@ -8,8 +8,8 @@
 // standardize (K11/K12, :357-391): for each (month batch b, lag theta) tile of N gathered
 // rows x P columns: demean the RFF columns (not the constant), scale every column to unit
 // L2 norm over the N real rows, then divide each row by its stock's volatility.  One
-// workgroup per (b, theta, 64-column strip); rows streamed twice from L2 (sum, then sum of
-// squares of the demeaned values) and written once.
+// workgroup per (b, theta, 64-column strip); rows read twice (shifted first and second
+// moments in one pass, then the scaled write) and written once.
 #include "common.h"
 
 namespace {
@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void standardize_kernel(const double* __restri
                                                           int N, const double* __restrict__ vol,
                                                           double* __restrict__ out, int64_t ldo,
                                                           int64_t so, int Pw) {
-  __shared__ double red[4][64];
+  __shared__ double red[4][64], red2[4][64];
   __shared__ double colmean[64], colscale[64];
   const int bt = blockIdx.y;                  // (b, theta)
   const int b = bt / TH;
@@ -52,32 +52,43 @@ __global__ __launch_bounds__(256) void standardize_kernel(const double* __restri
   const int c = c0 + lane;
   const int n = n_real[b];
   const int64_t* rw = rows + (int64_t)bt * N;
-  // pass 1: column sums over real rows
-  double s = 0.0;
-  if (c < P)
-    for (int i = part; i < n; i += 4) s += F[rw[i] * ldf + c];
-  red[part][lane] = s;
-  __syncthreads();
-  if (part == 0) {
-    const double tot = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    colmean[lane] = (c == 0) ? 0.0 : tot / (double)n;     // constant column is not demeaned
-  }
-  __syncthreads();
-  // pass 2: sum of squares of the demeaned values
-  const double mu = colmean[lane];
-  double q = 0.0;
-  if (c < P)
-    for (int i = part; i < n; i += 4) {
-      const double x = F[rw[i] * ldf + c] - mu;
-      q += x * x;
+  // one pass: shifted sums S1 = sum (x - K), S2 = sum (x - K)^2 with K = the column's first
+  // real value, so sum (x - mean)^2 = S2 - S1^2 / n without the cancellation of raw moments
+  // (K is a sample of the column: |K - mean| is O(std), relative error O(eps)).  Four
+  // independent row streams per thread keep loads in flight.
+  const double K = (c < P && n > 0) ? F[rw[0] * ldf + c] : 0.0;
+  double s1 = 0.0, s2 = 0.0;
+  if (c < P) {
+    int i = part;
+    for (; i + 12 < n; i += 16) {
+      const double x0 = F[rw[i] * ldf + c] - K, x1 = F[rw[i + 4] * ldf + c] - K;
+      const double x2 = F[rw[i + 8] * ldf + c] - K, x3 = F[rw[i + 12] * ldf + c] - K;
+      s1 += (x0 + x1) + (x2 + x3);
+      s2 += (x0 * x0 + x1 * x1) + (x2 * x2 + x3 * x3);
     }
-  red[part][lane] = q;
+    for (; i < n; i += 4) {
+      const double x = F[rw[i] * ldf + c] - K;
+      s1 += x;
+      s2 += x * x;
+    }
+  }
+  red[part][lane] = s1;
+  red2[part][lane] = s2;
   __syncthreads();
   if (part == 0) {
-    const double tot = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    colscale[lane] = sqrt(1.0 / tot);
+    const double t1 = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    const double t2 = red2[0][lane] + red2[1][lane] + red2[2][lane] + red2[3][lane];
+    if (c == 0) {                                          // constant column: not demeaned
+      colmean[lane] = 0.0;
+      const double tk = t1 + (double)n * K;                // sum x
+      colscale[lane] = sqrt(1.0 / (t2 + 2.0 * K * tk - (double)n * K * K));
+    } else {
+      colmean[lane] = K + t1 / (double)n;
+      colscale[lane] = sqrt(1.0 / (t2 - t1 * t1 / (double)n));
+    }
   }
   __syncthreads();
+  const double mu = colmean[lane];
   const double sc = colscale[lane];
   double* o = out + (int64_t)bt * so;
   if (c < Pw)

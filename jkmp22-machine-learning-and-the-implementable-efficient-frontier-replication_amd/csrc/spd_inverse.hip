@@ -291,6 +291,91 @@ extern "C" hipError_t pfml_spd_blockinv128(const double* A, int64_t lda, int64_t
   return hipGetLastError();
 }
 
+namespace {
+// Register-resident 64 x 64 Gauss-Jordan inverse (no pivoting: SPD blocks).  The LDS form
+// above re-reads and re-writes the whole block from LDS at every pivot (4 LDS accesses per
+// element per step: LDS-bandwidth bound, ~80 us per batch of 256 blocks).  Here each of the
+// 256 threads keeps a 4 x 4 sub-block in registers; per pivot the owners of row p and column
+// p publish them to a double-buffered LDS line (one barrier per step, no second barrier: the
+// buffer written at step p + 2 is only rewritten after every thread has passed step p + 1's
+// barrier, i.e. finished reading it), and every thread applies the same update expression as
+// the LDS form, (a_ip a_pj) / piv, so both give bitwise-identical inverses.  Output to any
+// (ld, batch stride): in place (Pout = the block itself) or to a packed buffer.
+__global__ __launch_bounds__(256) void spd_leafinv_kernel(const double* __restrict__ A,
+                                                          int64_t lda, int64_t sA, int k0,
+                                                          int nb, double* Pout, int64_t ldp,
+                                                          int64_t sP, int* __restrict__ status) {
+  __shared__ double rowb[2][64], colb[2][64];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int rb = t >> 4, cb = t & 15;
+  const double* Ab = A + (int64_t)b * sA + (int64_t)k0 * lda + k0;
+  double a[4][4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int i = 4 * rb + u, j = 4 * cb + v;
+      a[u][v] = Ab[(int64_t)min(i, nb - 1) * lda + min(j, nb - 1)];
+    }
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int i = 4 * rb + u, j = 4 * cb + v;
+      if (!(i < nb && j < nb)) a[u][v] = (i == j) ? 1.0 : 0.0;
+    }
+  bool bad = false;
+  for (int p = 0; p < nb; ++p) {
+    const int buf = p & 1, pq = p >> 2, pr = p & 3;
+    if (rb == pq) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        double x = a[0][v];
+#pragma unroll
+        for (int u = 1; u < 4; ++u) x = (pr == u) ? a[u][v] : x;
+        rowb[buf][4 * cb + v] = x;
+      }
+    }
+    if (cb == pq) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        double x = a[u][0];
+#pragma unroll
+        for (int v = 1; v < 4; ++v) x = (pr == v) ? a[u][v] : x;
+        colb[buf][4 * rb + u] = x;
+      }
+    }
+    __syncthreads();
+    const double piv = rowb[buf][p];
+    bad |= !(piv > 0.0) || !isfinite(piv);
+    const double inv = 1.0 / piv;
+    double rp[4], cp[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) rp[v] = rowb[buf][4 * cb + v];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cp[u] = colb[buf][4 * rb + u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const bool ir = (4 * rb + u) == p, jc = (4 * cb + v) == p;
+        const double upd = a[u][v] - cp[u] * rp[v] * inv;
+        const double x = ir ? (jc ? inv : a[u][v] * inv) : (jc ? -a[u][v] * inv : upd);
+        a[u][v] = x;
+      }
+  }
+  if (t == 0 && bad) status[b] = 1;
+  double* Pb = Pout + (int64_t)b * sP;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int i = 4 * rb + u, j = 4 * cb + v;
+      if (i < nb && j < nb) Pb[(int64_t)i * ldp + j] = a[u][v];
+    }
+}
+}  // namespace
+
 extern "C" int pfml_spd_block_size() { return NBL; }
 
 extern "C" hipError_t pfml_spd_blockinv(const double* A, int64_t lda, int64_t sA, int batch,
@@ -298,8 +383,18 @@ extern "C" hipError_t pfml_spd_blockinv(const double* A, int64_t lda, int64_t sA
                                         hipStream_t st) {
   if (batch <= 0 || nb <= 0) return hipSuccess;
   if (nb > NBL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(spd_blockinv_kernel<NBL>, dim3(batch), dim3(256), 0, st, A, lda, sA, k0, nb,
-                     Pout, status);
+  hipLaunchKernelGGL(spd_leafinv_kernel, dim3(batch), dim3(256), 0, st, A, lda, sA, k0, nb, Pout,
+                     (int64_t)NBL, (int64_t)NBL * NBL, status);
+  return hipGetLastError();
+}
+
+// In-place inverse of the nb x nb (nb <= 64) diagonal block at (k0, k0) of each matrix.
+extern "C" hipError_t pfml_spd_leafinv_inplace(double* A, int64_t lda, int64_t sA, int batch,
+                                               int k0, int nb, int* status, hipStream_t st) {
+  if (batch <= 0 || nb <= 0) return hipSuccess;
+  if (nb > NBL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(spd_leafinv_kernel, dim3(batch), dim3(256), 0, st, A, lda, sA, k0, nb,
+                     A + (int64_t)k0 * lda + k0, lda, sA, status);
   return hipGetLastError();
 }
 

@@ -140,7 +140,7 @@ def _search_setup(months: np.ndarray, years: np.ndarray, p_vec, G: int, T: int, 
     if hit is not None:
         return hit
     plan = make_plan(months, years)
-    yl = np.asarray(list(coll.contiguous_split(len(years), world, rank)))
+    yl = np.asarray(list(coll.contiguous_split(len(years), world, rank)), dtype=np.int64)
     nYl = len(yl)
     nP = len(p_vec)
     st = [int(plan.seg_start[i]) - off for i in yl]

@@ -68,6 +68,65 @@ nat.register_hip("pfml_spd_blockinv128", [C.c_void_p, C.c_int64, C.c_int64, C.c_
 nat.register_hip("pfml_spd_inverse_sym", [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                           C.c_void_p])
 nat.register_hip("pfml_spd_inverse_sym_work_doubles", [C.c_int, C.c_int], C.c_int64)
+nat.register_hip("pfml_spd_leafinv_inplace", [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int,
+                                              C.c_int, C.c_void_p, C.c_void_p])
+
+SPD_INV_DEFAULT = "recursive"
+_REC_LEAF = 64
+_REC_BUFS: dict = {}
+
+
+def _rec_split(n: int) -> int:
+    """Leading block of a recursive split: a multiple of the leaf size, about n / 2."""
+    return _REC_LEAF * ((n + 2 * _REC_LEAF - 1) // (2 * _REC_LEAF))
+
+
+def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor) -> None:
+    """In-place SPD inverse by recursive 2 x 2 Schur-complement blocks:
+
+        X11 = A11^-1 (recursive),  W = X11 A12,  S = A22 - A21 W,  X22 = S^-1 (recursive),
+        X12 = -W X22,  X21 = -X22 W',  X11 -= X12 W'
+
+    Every off-diagonal step is one fused-GEMM launch whose inner dimension is the block size
+    (256 / 128 / 64 on the m_func shape) instead of the rank-64 updates of the Gauss-Jordan
+    form, so the pass is MFMA-bound rather than a bandwidth-bound sweep over the whole matrix
+    per 64 columns; the 64 x 64 leaves are the register-resident leaf kernel, in place
+    (csrc/spd_inverse.hip).  Schur complements of an SPD matrix are SPD, so no pivoting; a
+    non-positive leaf pivot flags ``status`` like the other forms.  One W buffer per depth
+    (the parent's W lives across the child's recursion)."""
+    lib = nat.hip_lib()
+    B, n, _ = X.shape
+    st = nat.stream_of(X)
+    ld, sX = X.stride(1), X.stride(0)
+
+    def buf(depth, h, m):
+        key = (X.device, B, depth)
+        w = _REC_BUFS.get(key)
+        if w is None or w.numel() < B * h * m:
+            w = torch.empty(B * h * m, dtype=torch.float64, device=X.device)
+            _REC_BUFS[key] = w
+        return w[:B * h * m].view(B, h, m)
+
+    def rec(r0, nn, depth):
+        if nn <= _REC_LEAF:
+            nat.check(lib.pfml_spd_leafinv_inplace(X.data_ptr(), ld, sX, B, r0, nn,
+                                                   status.data_ptr(), st),
+                      "pfml_spd_leafinv_inplace")
+            return
+        h = _rec_split(nn)
+        m = nn - h
+        a, c, e = r0, r0 + h, r0 + nn
+        rec(a, h, depth + 1)
+        W = buf(depth, h, m)
+        gemm_fused(X[:, a:c, a:c], X[:, a:c, c:e], W)                        # W = X11 A12
+        gemm_fused(X[:, c:e, a:c], W, X[:, c:e, c:e], alpha=-1.0, beta=1.0)  # S
+        rec(c, m, depth + 1)
+        gemm_fused(W, X[:, c:e, c:e], X[:, a:c, c:e], alpha=-1.0)            # X12
+        gemm_fused(X[:, c:e, c:e], W, X[:, c:e, a:c], trans_b=True, alpha=-1.0)   # X21
+        gemm_fused(X[:, a:c, c:e], W, X[:, a:c, a:c], trans_b=True, alpha=-1.0,
+                   beta=1.0)                                                  # X11 -= X12 W'
+
+    rec(0, n, 0)
 
 
 def _spd_inverse_blocked(X: torch.Tensor, status: torch.Tensor) -> None:
@@ -81,7 +140,10 @@ def _spd_inverse_blocked(X: torch.Tensor, status: torch.Tensor) -> None:
     import os
     lib = nat.hip_lib()
     B, n, _ = X.shape
-    mode = os.environ.get("PFML_SPD_INV", "generic")
+    mode = os.environ.get("PFML_SPD_INV", SPD_INV_DEFAULT)
+    if mode == "recursive":
+        _spd_inverse_recursive(X, status)
+        return
     if mode == "sym":
         work = torch.empty(lib.pfml_spd_inverse_sym_work_doubles(n, B), dtype=torch.float64,
                            device=X.device)

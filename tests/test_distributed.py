@@ -186,16 +186,17 @@ def _copy_inputs(src: str, dst: str) -> None:
             shutil.copy(p, os.path.join(dst, n))
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_pipeline_sharded_matches_single(world, small_data, tmp_path):
+@pytest.mark.parametrize("world,start", [(2, 1999), (3, 1999), (6, 2008)])
+def test_pipeline_sharded_matches_single(world, start, small_data, tmp_path):
     """The main pipeline from pfml-input to pfml-best-hps on ``world`` gloo ranks - S4 built
     per rank on its hp-year blocks + validation halo (no denom all-gather), betas sharded,
     aims formed where beta and signals live, m_t sharded and the weight recursion chained
-    across ranks - writes the same CSVs as one process."""
+    across ranks - writes the same CSVs as one process.  (6, 2008): five hp years on six
+    ranks, so one rank holds no year at all (empty shard: ADVICE r1)."""
     import pandas as pd
     from pfml.parallel import dist as pdist
     from pfml.pipeline import Pipeline
-    base = small_data.override(["pf.dates.start_year=1999", "pf.dates.end_yr=2012",
+    base = small_data.override([f"pf.dates.start_year={start}", "pf.dates.end_yr=2012",
                                 "pf.dates.split_years=3"])
     d1, d2 = str(tmp_path / "w1"), str(tmp_path / "wn")
     _copy_inputs(small_data.run.data_dir, d1)

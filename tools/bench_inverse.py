@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""SPD inverse on the m_func shape ([256, 490, 490] fp64): fused symmetric Gauss-Jordan steps
+"""SPD inverse on the m_func shape ([256, 490, 490] fp64): recursive Schur-complement blocks,
+fused symmetric Gauss-Jordan steps
 (csrc/spd_inverse.hip, 3 launches per block) vs the generic block steps (pivot kernel + fused
 GEMMs + copies) interleaved in one process (torch.linalg.inv / rocSOLVER getrf-batched fails to allocate
 at this batch)."""
@@ -22,7 +23,8 @@ def main():
     A = X.transpose(1, 2) @ X / n + 0.05 * torch.eye(n, dtype=torch.float64, device=dev)
     I = torch.eye(n, dtype=torch.float64, device=dev)
     res = {}
-    fns = {"fused_sym": ("sym", lambda: spd_inverse(A)), "generic": ("generic", lambda: spd_inverse(A)),
+    fns = {"recursive": ("recursive", lambda: spd_inverse(A)),
+           "fused_sym": ("sym", lambda: spd_inverse(A)), "generic": ("generic", lambda: spd_inverse(A)),
            "generic128": ("generic128", lambda: spd_inverse(A))}
     for k, (envv, f) in fns.items():
         os.environ["PFML_SPD_INV"] = envv

@@ -34,8 +34,8 @@ def main():
     risk.daily_ols = spy
     chars, daily, labels = risk._load_risk_inputs(cfg)
     cs = cfg.settings["cov_set"]
-    bg = risk.estimate_cov_frames(chars, daily, labels, cs, "cuda")
-    bc = risk.estimate_cov_frames(chars, daily, labels, cs, "cpu")
+    bg = risk.estimate_cov_frames_pandas(chars, daily, labels, cs, "cuda")
+    bc = risk.estimate_cov_frames_pandas(chars, daily, labels, cs, "cpu")
     X, y, day = cap["X"], cap["y"], cap["day"]
     _, cg, rg, ng = orig(X, y, day, "cuda")
     _, cc, rc, nc = orig(X, y, day, "cpu")
