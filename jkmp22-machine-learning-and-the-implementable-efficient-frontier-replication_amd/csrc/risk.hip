@@ -300,7 +300,12 @@ __global__ __launch_bounds__(256) void ewma_factor_cov_kernel(
   __syncthreads();
   for (int q = t; q < K * K; q += 256) {
     const int i = q / K, j = q % K;
-    const double cor = (i == j) ? 1.0 : C[0][i][j] / (sqrt(C[0][i][i]) * sqrt(C[0][j][j]));
+    // a factor with no exposure in the window (an industry without members: its daily OLS
+    // coefficient is the pinv's zero) has variance 0; its correlations are taken as 0 so F
+    // carries 0 there (the reference's pinv leaves ~1e-16 noise, i.e. F ~ 1e-32) instead of
+    // a NaN that would poison every Sigma of the month
+    const double dn = sqrt(C[0][i][i]) * sqrt(C[0][j][j]);
+    const double cor = (i == j) ? 1.0 : (dn > 0.0 ? C[0][i][j] / dn : 0.0);
     const double sdi = sqrt(C[1][i][i]), sdj = sqrt(C[1][j][j]);
     const int64_t o = (int64_t)bi * K * K + q;
     F[o] = sdi * cor * sdj * scale;

@@ -292,20 +292,21 @@ extern "C" hipError_t pfml_spd_blockinv128(const double* A, int64_t lda, int64_t
 }
 
 namespace {
-// Register-resident 64 x 64 Gauss-Jordan inverse (no pivoting: SPD blocks).  The LDS form
-// above re-reads and re-writes the whole block from LDS at every pivot (4 LDS accesses per
-// element per step: LDS-bandwidth bound, ~80 us per batch of 256 blocks).  Here each of the
-// 256 threads keeps a 4 x 4 sub-block in registers; per pivot the owners of row p and column
-// p publish them to a double-buffered LDS line (one barrier per step, no second barrier: the
-// buffer written at step p + 2 is only rewritten after every thread has passed step p + 1's
-// barrier, i.e. finished reading it), and every thread applies the same update expression as
-// the LDS form, (a_ip a_pj) / piv, so both give bitwise-identical inverses.  Output to any
+// Register-resident 64 x 64 Gauss-Jordan inverse (no pivoting: SPD blocks), 4 pivots per
+// barrier.  The LDS form above re-reads and re-writes the whole block from LDS at every pivot
+// (LDS-bandwidth bound, ~80 us per batch of 256 blocks) and a one-pivot register form is
+// bound by its 64 barrier + divide round trips (~50 us).  Here each of the 256 threads keeps a
+// 4 x 4 sub-block in registers; pivot block q (4 pivots) is exactly thread row / column block
+// q, so the owners publish whole register tiles to a double-buffered LDS line
+// (one barrier per step, no second barrier: the buffer written at step q + 2 is rewritten
+// only after every thread has passed step q + 1's barrier, i.e. finished reading it).  Frame
+// entries past nb hold the identity, so partial blocks need no special case.  Output to any
 // (ld, batch stride): in place (Pout = the block itself) or to a packed buffer.
 __global__ __launch_bounds__(256) void spd_leafinv_kernel(const double* __restrict__ A,
                                                           int64_t lda, int64_t sA, int k0,
                                                           int nb, double* Pout, int64_t ldp,
                                                           int64_t sP, int* __restrict__ status) {
-  __shared__ double rowb[2][64], colb[2][64];
+  __shared__ double rowb[2][4][64], colb[2][64][4];
   const int b = blockIdx.x, t = threadIdx.x;
   const int rb = t >> 4, cb = t & 15;
   const double* Ab = A + (int64_t)b * sA + (int64_t)k0 * lda + k0;
@@ -325,44 +326,85 @@ __global__ __launch_bounds__(256) void spd_leafinv_kernel(const double* __restri
       if (!(i < nb && j < nb)) a[u][v] = (i == j) ? 1.0 : 0.0;
     }
   bool bad = false;
-  for (int p = 0; p < nb; ++p) {
-    const int buf = p & 1, pq = p >> 2, pr = p & 3;
-    if (rb == pq) {
+  const int nq = (nb + 3) >> 2;
+  for (int q = 0; q < nq; ++q) {
+    const int buf = q & 1;
+    if (rb == q) {
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        double x = a[0][v];
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int u = 1; u < 4; ++u) x = (pr == u) ? a[u][v] : x;
-        rowb[buf][4 * cb + v] = x;
-      }
+        for (int v = 0; v < 4; ++v) rowb[buf][r][4 * cb + v] = a[r][v];
     }
-    if (cb == pq) {
+    if (cb == q) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        double x = a[u][0];
+      for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int v = 1; v < 4; ++v) x = (pr == v) ? a[u][v] : x;
-        colb[buf][4 * rb + u] = x;
-      }
+        for (int c = 0; c < 4; ++c) colb[buf][4 * rb + u][c] = a[u][c];
     }
     __syncthreads();
-    const double piv = rowb[buf][p];
-    bad |= !(piv > 0.0) || !isfinite(piv);
-    const double inv = 1.0 / piv;
-    double rp[4], cp[4];
+    // The 4 pivots of the block, replayed as SCALAR Gauss-Jordan steps on the thread's local
+    // 8 x 8 view M = [[P, rp], [cp, a]] (P = A_KK, rp = A_K,mycols, cp = A_myrows,K): every
+    // entry sees exactly the update sequence, and the expressions, of one-pivot-at-a-time GJ,
+    // so the result is bitwise that of the LDS kernel (an explicit P^-1 block step amplifies
+    // rounding by cond(P) on ill-conditioned Denman-Beavers iterates).
+    double P[4][4], rp[4][4], cp[4][4];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) rp[v] = rowb[buf][4 * cb + v];
+    for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) cp[u] = colb[buf][4 * rb + u];
+      for (int c = 0; c < 4; ++c) P[r][c] = rowb[buf][r][4 * q + c];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) rp[r][v] = rowb[buf][r][4 * cb + v];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const bool ir = (4 * rb + u) == p, jc = (4 * cb + v) == p;
-        const double upd = a[u][v] - cp[u] * rp[v] * inv;
-        const double x = ir ? (jc ? inv : a[u][v] * inv) : (jc ? -a[u][v] * inv : upd);
-        a[u][v] = x;
-      }
+      for (int c = 0; c < 4; ++c) cp[u][c] = colb[buf][4 * rb + u][c];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const double piv = P[p][p];
+      bad |= !(piv > 0.0) || !isfinite(piv);
+      const double inv = 1.0 / piv;
+      // a (rows != p, cols != p: always, the thread's rows / cols are outside K unless it
+      // owns the pivot block, whose result is then read from P / rp / cp below)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) a[u][v] -= cp[u][p] * rp[p][v] * inv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (r != p)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) rp[r][v] -= P[r][p] * rp[p][v] * inv;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (c != p) cp[u][c] -= cp[u][p] * P[p][c] * inv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (r != p && c != p) P[r][c] -= P[r][p] * P[p][c] * inv;
+      // pivot row / column scaling (old values of row p / column p used above)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) rp[p][v] *= inv;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) cp[u][p] *= -inv;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c != p) {
+          P[p][c] *= inv;
+          P[c][p] *= -inv;
+        }
+      P[p][p] = inv;
+    }
+    const bool inr = rb == q, inc = cb == q;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        a[u][v] = (inr && inc) ? P[u][v] : (inr ? rp[u][v] : (inc ? cp[u][v] : a[u][v]));
   }
   if (t == 0 && bad) status[b] = 1;
   double* Pb = Pout + (int64_t)b * sP;

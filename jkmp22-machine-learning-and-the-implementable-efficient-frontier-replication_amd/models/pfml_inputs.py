@@ -16,9 +16,10 @@ a batched device pipeline over MONTHS (dates are independent given m_t, Sigma_t 
      host sync);
    * the aggregation (24) in Horner form over the augmented [S_{t-theta} | I] (K5/K6):
        T_11 = [S_11 | I],  T_theta = [S_theta | I] + (m D_theta) T_{theta+1}
-     gives both sum_theta agg_theta S_{t-theta} and sum_theta agg_theta in 11 GEMMs per chain
-     (the reference forms 22 N x N products plus 24 N x P products), with both g stacked in
-     the column dimension so m and the agg products are shared.  Each step is ONE launch of
+     gives both sum_theta agg_theta S_{t-theta} and sum_theta agg_theta in 11 GEMMs (the
+     reference forms 22 N x N products plus 24 N x P products), with both g stacked in the
+     column dimension so m and the agg products are shared; the lag-1 sums of omega_l1 follow
+     as T_1 + (m D_1 ... m D_11) [S_12 | I], the product carried along the same launches.  Each step is ONE launch of
      the fused GEMM (csrc/gemm_f64.hip): m = diag(a) m_tilde diag(1/a) and D_theta enter as
      row / k scales, S_theta and the identity block as the epilogue addend - no m, m D or
      [S | I] matrix is ever materialised;
@@ -130,10 +131,10 @@ def vol_scales(panel: Panel, barra: BarraCov, months: np.ndarray) -> np.ndarray:
 
 def auto_month_batch(n_stocks: int, gp: int, device, cap: int = 256) -> int:
     """Months per S4 batch from the memory one month's working set needs (fp64): the
-    13-month signal window (13 N GP), four Horner buffers of N x (GP + N), ~8 N x N matrices of
+    13-month signal window (13 N GP), five Horner buffers of N x (GP + N) plus two N x N blocks, ~8 N x N matrices of
     m_func / Sigma and the (25) scratch.  A device batch takes up to 60 % of free HBM (288 GB on
     MI355X: 256 months at N = 500, ~60 at N = 3000), a host batch 25 % of available RAM."""
-    per = 8.0 * (13.0 * n_stocks * gp + 5.0 * n_stocks * (gp + n_stocks) + 9.0 * n_stocks ** 2
+    per = 8.0 * (13.0 * n_stocks * gp + 6.0 * n_stocks * (gp + n_stocks) + 11.0 * n_stocks ** 2
                  + 2.0 * gp * gp)
     dev = torch.device(device)
     if dev.type == "cuda":
@@ -399,27 +400,39 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False) -> "PfmlInpu
         # m = diag(a) m_tilde diag(1/a) (Lemma 1); a and 1/a are folded into the Horner GEMMs
         mt, a = la.m_tilde(Sigma, bt.lam, bt.w, bt.rf, mu, gamma, cfg.run.iterations,
                            mask=bt.mask)
-        # (24) Horner chains over [S_theta | I], one fused GEMM launch per step:
+        # (24) Horner chain over [S_theta | I | R], one fused GEMM launch per step:
         #   T_theta = [S_theta | I] + diag(a) m_tilde diag(D_theta / a) T_{theta+1}
+        # The lag-1 chain of omega_l1 (PFML_Input_Data.py:425-450: gtm_agg_l1, same m_t) is
+        #   U_0 = sum_{j=1..12} (prod_{tau=1..j-1} m D_tau) [S_j | I] = T_1 + Q [S_12 | I],
+        #   Q = m D_1 m D_2 ... m D_11,
+        # and Q rides along the T steps theta = 10..1 as an N-column block R (R_11 = m D_11,
+        # R_theta = m D_theta R_{theta+1}, no addend): 10 steps of width GP + 2N plus two of
+        # GP + N instead of 22 of GP + N (29 % fewer Horner flops at N = 490, GP = 1026).
         Dg = plan.gt[bt.idx]                                        # [B, 13, N]
         ainv = 1.0 / a
-        Tc = [torch.empty((B, N, Wd), dtype=torch.float64, device=dev) for _ in range(2)]
-        Ul = [torch.empty((B, N, Wd), dtype=torch.float64, device=dev) for _ in range(2)]
+        Wr = Wd + N
+        Tb = [torch.empty((B, N, Wr), dtype=torch.float64, device=dev) for _ in range(2)]
         eye = torch.eye(N, dtype=torch.float64, device=dev)
-        Tc[0][:, :, :GP] = S[:, lb]
-        Tc[0][:, :, GP:] = eye
-        Ul[0][:, :, :GP] = S[:, lb + 1]
-        Ul[0][:, :, GP:] = eye
+        Tb[0][:, :, :GP] = S[:, lb]
+        Tb[0][:, :, GP:Wd] = eye
+        gemm_fused(mt, eye, Tb[0][:, :, Wd:], row_scale=a, k_scale=(Dg[:, lb] * ainv))  # R_11
         cur = 0
-        for th in range(lb - 1, -1, -1):
-            gemm_fused(mt, Tc[cur], Tc[cur ^ 1], row_scale=a, k_scale=(Dg[:, th] * ainv),
+        for th in range(lb - 1, 0, -1):
+            gemm_fused(mt, Tb[cur], Tb[cur ^ 1], row_scale=a, k_scale=(Dg[:, th] * ainv),
                        addend=S[:, th], addend_cols=GP, diag_col0=GP, diag_value=1.0)
-            gemm_fused(mt, Ul[cur], Ul[cur ^ 1], row_scale=a, k_scale=(Dg[:, th + 1] * ainv),
-                       addend=S[:, th + 1], addend_cols=GP, diag_col0=GP, diag_value=1.0)
             cur ^= 1
-        T0, U0 = Tc[cur], Ul[cur]
+        T1 = Tb[cur]
+        T0 = torch.empty((B, N, Wd), dtype=torch.float64, device=dev)
+        gemm_fused(mt, T1[:, :, :Wd], T0, row_scale=a, k_scale=(Dg[:, 0] * ainv),
+                   addend=S[:, 0], addend_cols=GP, diag_col0=GP, diag_value=1.0)
+        SI = torch.empty((B, N, Wd), dtype=torch.float64, device=dev)
+        SI[:, :, :GP] = S[:, lb + 1]
+        SI[:, :, GP:] = eye
+        U0 = torch.empty_like(T0)
+        gemm_fused(T1[:, :, Wd:], SI, U0, addend=T1[:, :, :Wd], addend_cols=Wd)   # T_1 + Q [S_12|I]
+        del Tb, T1, SI
         sig0 = S[:, 0].clone()                                      # signal_t blocks
-        del S, Tc, Ul
+        del S
         # omega = const^-1 Omega, solved in place on the augmented [Omega | const] rows (K7)
         omega = la.solve_augmented(T0, N, GP, a0=GP, b0=0, status=sing[:B])  # [B, N, GP]
         omega_l1 = la.solve_augmented(U0, N, GP, a0=GP, b0=0, status=sing[:B])

@@ -123,7 +123,9 @@ def weighted_cov(X: torch.Tensor, w: torch.Tensor, cor: bool) -> torch.Tensor:
     if not cor:
         return cov
     sd = torch.sqrt(torch.diagonal(cov, dim1=1, dim2=2))
-    c = cov / (sd.unsqueeze(-1) * sd.unsqueeze(-2))
+    den = sd.unsqueeze(-1) * sd.unsqueeze(-2)
+    # zero-variance factor (no exposure in the window): correlations 0, as csrc/risk.hip
+    c = torch.where(den > 0, cov / torch.where(den > 0, den, 1.0), torch.zeros_like(cov))
     idx = torch.arange(c.shape[-1])
     c[:, idx, idx] = 1.0
     return c

