@@ -299,11 +299,138 @@ hipError_t lu_solve_nb(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// Two-level form (n <= 512): 128-wide outer panels.  The 32-wide inner steps above run on the
+// panel's own A columns plus a 128-column block Z of M (the inner update touches <= 256
+// columns instead of all n + m), and Z accumulates the panel's Gauss-Jordan transform:
+// the unit vector of each pivot row is placed in Z when its inner block is reached (after
+// that block's row swaps), so at the end Z = T E_K with T the panel's transform after all of
+// its swaps.  The rest of M (A columns right of the panel and the B columns) then takes the
+// swaps and T in one go:  R <- Perm R,  R_K <- Z_K R_K,  R_other <- R_other + Z_other R_K,
+// i.e. three K = 128 fp64 MFMA GEMMs per column range (csrc/gemm_f64.hip) in place of four
+// bandwidth-bound rank-32 passes over every live column.
+constexpr int LU_KB = 128;
+
+__global__ __launch_bounds__(256) void lu_zinit_kernel(double* __restrict__ M, int n, int64_t ldm,
+                                                       int64_t sM, int z0) {
+  const int b = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)n * LU_KB) return;
+  M[(int64_t)b * sM + (e / LU_KB) * ldm + z0 + e % LU_KB] = 0.0;
+}
+
+// unit entries of the current inner block's pivot rows: M[k0 + j][zc + j] = 1
+__global__ __launch_bounds__(64) void lu_zunit_kernel(double* __restrict__ M, int64_t ldm,
+                                                      int64_t sM, int k0, int zc, int nb) {
+  const int j = threadIdx.x;
+  if (j < nb) M[(int64_t)blockIdx.x * sM + (int64_t)(k0 + j) * ldm + zc + j] = 1.0;
+}
+
+// RK[b][r][v] = M[K0 + r][live column v]   (rest columns: A right of the panel, then B)
+__global__ __launch_bounds__(256) void lu_rk_kernel(const double* __restrict__ M, int64_t ldm,
+                                                    int64_t sM, int K0, int kb, int nrest,
+                                                    int a_first, int nA, int b0,
+                                                    double* __restrict__ RK) {
+  const int b = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)kb * nrest) return;
+  const int r = (int)(e / nrest), v = (int)(e % nrest);
+  RK[(int64_t)b * kb * nrest + e] =
+      M[(int64_t)b * sM + (int64_t)(K0 + r) * ldm + live_col(v, nA, a_first, b0)];
+}
+
 }  // namespace
 
+extern "C" hipError_t pfml_dgemm(int ta, int tb, int M, int N, int K, int batch, double alpha,
+                                 const double* A, int64_t lda, int64_t sA, const double* B,
+                                 int64_t ldb, int64_t sB, double beta, double* C, int64_t ldc,
+                                 int64_t sC, const double* rs, int64_t srs, const double* cs,
+                                 int64_t scs, hipStream_t st);
+
+namespace {
+
+hipError_t lu_solve_2level(double* M, int n, int m, int64_t ldm, int64_t sM, int a0, int b0,
+                           int z0, int batch, double* work, int* status, hipStream_t st) {
+  constexpr int NB = 32;
+  double* Pbuf = work;
+  double* Rbuf = Pbuf + (int64_t)batch * NB * NB;
+  double* Cbuf = Rbuf + (int64_t)batch * NB * (2 * LU_KB);
+  double* RK = Cbuf + (int64_t)batch * n * NB;
+  int* piv = reinterpret_cast<int*>(RK + (int64_t)batch * LU_KB * (n + m));
+  for (int K0 = 0; K0 < n; K0 += LU_KB) {
+    const int kb = (n - K0 < LU_KB) ? (n - K0) : LU_KB;
+    const int aend = K0 + kb;
+    hipLaunchKernelGGL(lu_zinit_kernel, dim3((n * LU_KB + 255) / 256, batch), dim3(256), 0, st, M,
+                       n, ldm, sM, z0);
+    for (int k0 = K0; k0 < aend; k0 += NB) {
+      const int nb = (aend - k0 < NB) ? (aend - k0) : NB;
+      int* pv = piv + (int64_t)((k0 - K0) / NB) * batch * NB;
+      hipLaunchKernelGGL((lu_pivot_kernel<NB, 512>), dim3(batch), dim3(256), 0, st, M, n, ldm, sM,
+                         a0, k0, nb, pv, status);
+      // live set of the inner step: A columns k0 .. aend (swap) / right of the block, and Z
+      const int nswap = (aend - k0) + kb;
+      hipLaunchKernelGGL((lu_swap_kernel<NB>), dim3((nswap + 255) / 256, batch), dim3(256), 0, st,
+                         M, ldm, sM, nswap, a0 + k0, aend - k0, z0, k0, nb, pv);
+      hipLaunchKernelGGL(lu_zunit_kernel, dim3(batch), dim3(64), 0, st, M, ldm, sM, k0,
+                         z0 + (k0 - K0), nb);
+      hipLaunchKernelGGL((lu_blockinv_kernel<NB>), dim3(batch), dim3(256), 0, st, M, ldm, sM, a0,
+                         k0, nb, Pbuf);
+      const int nA = aend - (k0 + nb);
+      const int nlive = nA + kb;
+      hipLaunchKernelGGL((lu_rowpanel_kernel<NB>), dim3((nlive + 255) / 256, batch), dim3(256), 0,
+                         st, M, ldm, sM, nlive, a0 + k0 + nb, nA, z0, k0, nb, Pbuf, Rbuf);
+      hipLaunchKernelGGL((lu_snapshot_kernel<NB>), dim3((n + 255) / 256, batch), dim3(256), 0, st,
+                         M, n, ldm, sM, a0, k0, nb, Cbuf);
+      const int tiles = ((n + 63) / 64) * ((nlive + 63) / 64);
+      hipLaunchKernelGGL((lu_update_kernel<NB>), dim3(tiles, batch), dim3(256), 0, st, M, n, ldm,
+                         sM, nlive, a0 + k0 + nb, nA, z0, k0, nb, Rbuf, Cbuf);
+    }
+    // the rest: swaps in sequence order, then R_K <- Z_K R_K, R_other += Z_other R_K
+    const int nAr = n - aend;
+    const int nrest = nAr + m;
+    if (nrest <= 0) continue;
+    for (int k0 = K0; k0 < aend; k0 += NB) {
+      const int nb = (aend - k0 < NB) ? (aend - k0) : NB;
+      const int* pv = piv + (int64_t)((k0 - K0) / NB) * batch * NB;
+      hipLaunchKernelGGL((lu_swap_kernel<NB>), dim3((nrest + 255) / 256, batch), dim3(256), 0, st,
+                         M, ldm, sM, nrest, a0 + aend, nAr, b0, k0, nb, pv);
+    }
+    hipLaunchKernelGGL(lu_rk_kernel, dim3((int)(((int64_t)kb * nrest + 255) / 256), batch),
+                       dim3(256), 0, st, M, ldm, sM, K0, kb, nrest, a0 + aend, nAr, b0, RK);
+    const int64_t sRK = (int64_t)kb * nrest;
+    const int ranges[2][3] = {{a0 + aend, nAr, 0}, {b0, m, nAr}};   // (column, width, RK offset)
+    for (int c = 0; c < 2; ++c) {
+      const int col = ranges[c][0], wdt = ranges[c][1], off = ranges[c][2];
+      if (wdt <= 0) continue;
+      const double* Bp = RK + off;
+      const double* Zr = M + z0;
+      hipError_t e;
+      if (K0 > 0 && (e = pfml_dgemm(0, 0, K0, wdt, kb, batch, 1.0, Zr, ldm, sM, Bp, nrest, sRK,
+                                    1.0, M + col, ldm, sM, nullptr, 0, nullptr, 0, st)) != hipSuccess)
+        return e;
+      if ((e = pfml_dgemm(0, 0, kb, wdt, kb, batch, 1.0, Zr + (int64_t)K0 * ldm, ldm, sM, Bp,
+                          nrest, sRK, 0.0, M + (int64_t)K0 * ldm + col, ldm, sM, nullptr, 0,
+                          nullptr, 0, st)) != hipSuccess)
+        return e;
+      if (n - aend > 0 &&
+          (e = pfml_dgemm(0, 0, n - aend, wdt, kb, batch, 1.0, Zr + (int64_t)aend * ldm, ldm, sM,
+                          Bp, nrest, sRK, 1.0, M + (int64_t)aend * ldm + col, ldm, sM, nullptr,
+                          0, nullptr, 0, st)) != hipSuccess)
+        return e;
+    }
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int pfml_lu_panel_cols() { return LU_KB; }
+
 extern "C" int64_t pfml_lu_solve_work_doubles(int n, int m, int batch) {
-  const int64_t NB = 32;                     // the larger block: enough for either variant
-  return (int64_t)batch * (NB * NB + NB * (n + m) + (int64_t)n * NB) + 2LL * batch * NB;
+  const int64_t NB = 32;                     // the larger block: enough for every variant
+  return (int64_t)batch * (NB * NB + NB * (n + m + 2 * LU_KB) + (int64_t)n * NB +
+                           (int64_t)LU_KB * (n + m)) +
+         (int64_t)batch * LU_KB;             // pivots (ints, 4 inner blocks of NB)
 }
 
 // Solve A X = B in place for `batch` augmented systems (see header); X overwrites B.
@@ -316,4 +443,13 @@ extern "C" hipError_t pfml_lu_solve(double* M, int n, int m, int64_t ldm, int64_
   if (n <= 512) return lu_solve_nb<32, 512>(M, n, m, ldm, sM, a0, b0, batch, work, status, st);
   if (n <= 1024) return lu_solve_nb<16, 1024>(M, n, m, ldm, sM, a0, b0, batch, work, status, st);
   return hipErrorInvalidValue;
+}
+
+// Two-level solve; M must hold LU_KB free columns at z0 (scratch for the panel transform).
+extern "C" hipError_t pfml_lu_solve2(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
+                                     int b0, int z0, int batch, double* work, int* status,
+                                     hipStream_t st) {
+  if (n <= 0 || batch <= 0) return hipSuccess;
+  if (n > 512) return hipErrorInvalidValue;
+  return lu_solve_2level(M, n, m, ldm, sM, a0, b0, z0, batch, work, status, st);
 }

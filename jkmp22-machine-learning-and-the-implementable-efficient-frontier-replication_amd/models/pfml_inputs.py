@@ -422,20 +422,23 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False) -> "PfmlInpu
                        addend=S[:, th], addend_cols=GP, diag_col0=GP, diag_value=1.0)
             cur ^= 1
         T1 = Tb[cur]
-        T0 = torch.empty((B, N, Wd), dtype=torch.float64, device=dev)
+        # T0 / U0 carry LU_PANEL_COLS scratch columns for the two-level solve below
+        Wz = Wd + la.LU_PANEL_COLS
+        T0f = torch.empty((B, N, Wz), dtype=torch.float64, device=dev)
+        U0f = torch.empty_like(T0f)
+        T0, U0 = T0f[:, :, :Wd], U0f[:, :, :Wd]
         gemm_fused(mt, T1[:, :, :Wd], T0, row_scale=a, k_scale=(Dg[:, 0] * ainv),
                    addend=S[:, 0], addend_cols=GP, diag_col0=GP, diag_value=1.0)
         SI = torch.empty((B, N, Wd), dtype=torch.float64, device=dev)
         SI[:, :, :GP] = S[:, lb + 1]
         SI[:, :, GP:] = eye
-        U0 = torch.empty_like(T0)
         gemm_fused(T1[:, :, Wd:], SI, U0, addend=T1[:, :, :Wd], addend_cols=Wd)   # T_1 + Q [S_12|I]
         del Tb, T1, SI
         sig0 = S[:, 0].clone()                                      # signal_t blocks
         del S
         # omega = const^-1 Omega, solved in place on the augmented [Omega | const] rows (K7)
-        omega = la.solve_augmented(T0, N, GP, a0=GP, b0=0, status=sing[:B])  # [B, N, GP]
-        omega_l1 = la.solve_augmented(U0, N, GP, a0=GP, b0=0, status=sing[:B])
+        omega = la.solve_augmented(T0f, N, GP, a0=GP, b0=0, status=sing[:B], z0=Wd)  # [B, N, GP]
+        omega_l1 = la.solve_augmented(U0f, N, GP, a0=GP, b0=0, status=sing[:B], z0=Wd)
         omega_chg = torch.addcmul(omega, Dg[:, 0].unsqueeze(-1), omega_l1, value=-1.0)
         nsing_t += sing[:B].sum()
         sing.zero_()

@@ -180,14 +180,22 @@ def _lu_max_n() -> int:
     return int(nat.hip_lib().pfml_lu_solve_max_n())
 
 
+LU_PANEL_COLS = 128            # scratch columns of the two-level solve (pfml_lu_panel_cols)
+nat.register_hip("pfml_lu_solve2", [C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_int64, C.c_int,
+                                    C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                    C.c_void_p])
+
+
 def solve_augmented(M: torch.Tensor, n: int, m: int, a0: int, b0: int,
-                    status: torch.Tensor | None = None) -> torch.Tensor:
+                    status: torch.Tensor | None = None, z0: int | None = None) -> torch.Tensor:
     """In-place solve of augmented systems: rows of M [B, n, W] hold A at columns a0..a0+n and
     B at b0..b0+m; on return the B columns hold X = A^-1 B (returned as a view).
 
     Device: csrc/lu_solve.hip (blocked Gauss-Jordan with partial pivoting, the pivot panel in
     LDS; 32-wide blocks up to n = 512, 16-wide up to 1024); larger systems (the 3000-stock
-    stress) take the library (rocSOLVER) LU through torch.  With ``status`` (a [B] int32
+    stress) take the library (rocSOLVER) LU through torch.  ``z0``: M holds LU_PANEL_COLS free
+    scratch columns there, and n <= 512 takes the two-level form (128-wide panels whose
+    transform reaches the other columns through K = 128 GEMMs).  With ``status`` (a [B] int32
     device tensor) singular systems are only flagged there (no host sync; the caller checks
     once), otherwise they are counted here."""
     if nat.is_device(M) and n <= _lu_max_n():
@@ -199,8 +207,16 @@ def solve_augmented(M: torch.Tensor, n: int, m: int, a0: int, b0: int,
                            device=M.device)
         st = status if status is not None else torch.zeros(Bt, dtype=torch.int32,
                                                            device=M.device)
-        nat.check(lib.pfml_lu_solve(M.data_ptr(), n, m, W, nn * W, a0, b0, Bt, work.data_ptr(),
-                                    st.data_ptr(), nat.stream_of(M)), "pfml_lu_solve")
+        if z0 is not None and n <= 512:
+            if z0 + LU_PANEL_COLS > W:
+                raise ValueError("solve_augmented: z0 needs LU_PANEL_COLS scratch columns")
+            nat.check(lib.pfml_lu_solve2(M.data_ptr(), n, m, W, nn * W, a0, b0, z0, Bt,
+                                         work.data_ptr(), st.data_ptr(), nat.stream_of(M)),
+                      "pfml_lu_solve2")
+        else:
+            nat.check(lib.pfml_lu_solve(M.data_ptr(), n, m, W, nn * W, a0, b0, Bt,
+                                        work.data_ptr(), st.data_ptr(), nat.stream_of(M)),
+                      "pfml_lu_solve")
         if status is None:
             nbad = int(st.sum().item())
             if nbad:

@@ -187,6 +187,29 @@ def test_lu_solve_augmented(gpu, n, m, b):
     assert rel < 1e-10, rel
 
 
+@pytest.mark.parametrize("n,m,b", [(490, 1026, 3), (512, 300, 2), (130, 70, 4), (100, 514, 2),
+                                   (257, 33, 3)])
+def test_lu_solve_two_level(gpu, n, m, b):
+    """Two-level solve (128-wide panels, transform block Z in scratch columns, K = 128 GEMM
+    updates) on the S4 layout [B | A | scratch] vs torch.linalg.solve; pivoting forced in
+    the first and in a later panel."""
+    from pfml.ops.linalg import LU_PANEL_COLS, solve_augmented
+    A = _rand(b, n, n, seed=n + 1) + 0.5 * n ** 0.5 * torch.eye(n, dtype=torch.float64)
+    A[:, 0, 0] = 1e-8
+    A[:, n // 2, n // 2] = 1e-9
+    Bm = _rand(b, n, m, seed=m + 3)
+    ref = torch.linalg.solve(A, Bm)
+    M = torch.full((b, n, m + n + LU_PANEL_COLS), float("nan"), dtype=torch.float64)
+    M[:, :, :m] = Bm
+    M[:, :, m:m + n] = A
+    Md = M.to(gpu)
+    st = torch.zeros(b, dtype=torch.int32, device=gpu)
+    got = solve_augmented(Md, n, m, a0=m, b0=0, status=st, z0=m + n).cpu()
+    assert int(st.sum()) == 0
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < 1e-11, rel
+
+
 @pytest.mark.parametrize("variant", ["unblocked", "blocked", "fast"])
 def test_ridge_variants_agree(gpu, variant, monkeypatch):
     """The three tridiagonalisation kernels (fused sweep / dlatrd-blocked / LDS fast path)
