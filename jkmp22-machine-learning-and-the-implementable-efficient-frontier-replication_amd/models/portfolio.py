@@ -21,10 +21,16 @@ import torch
 
 from ..config import Config
 from ..ops import linalg as la
+from ..ops import _native as nat
 from ..ops.gemm import gemm_fused
 from ..utils.dates import month_end, month_index
 from ..utils.log import get_logger
 from .risk import BarraCov
+
+_P, _I, _L = nat.C.c_void_p, nat.C.c_int, nat.C.c_int64
+nat.register_hip("pfml_weights_chain", [_P, _L, _L, _P, _P, _P, _P, _P, _L, _P, _I, _I, _P, _P,
+                                        _P, _P])
+nat.register_hip("pfml_weights_chain_max_n", [])
 
 log = get_logger("portfolio")
 
@@ -150,20 +156,40 @@ def best_hps(hps: dict, oos_months: np.ndarray):
     return bh, chosen, pd.concat(aims, ignore_index=True)
 
 
+def _exact_lookup(keys: np.ndarray, q: np.ndarray, what: str) -> np.ndarray:
+    """Positions of ``q`` in the sorted unique ``keys``; KeyError if any is absent."""
+    if len(q) == 0:
+        return np.zeros(0, np.int64)
+    p = np.clip(np.searchsorted(keys, q), 0, max(len(keys) - 1, 0))
+    if len(keys) == 0 or np.any(keys[p] != q):
+        raise KeyError(f"{what}: missing keys")
+    return p
+
+
+def _month_values(frame: pd.DataFrame, col: str, months: np.ndarray) -> np.ndarray:
+    mi = month_index(frame["eom"])
+    o = np.argsort(mi, kind="stable")
+    return frame[col].to_numpy(np.float64)[o][_exact_lookup(mi[o], np.asarray(months), col)]
+
+
 def _weights_plan(cfg: Config, chars: pd.DataFrame, wealth: pd.DataFrame, aims: pd.DataFrame,
                   oos_months: np.ndarray) -> dict:
-    """Host layout of the recursion: the valid rows of every OOS month in id order, each
-    month's aim weights aligned to them, and the drift map from month t's rows to month t+1's
-    (position of each id of t+1 among t's rows, or -1 for a new name)."""
+    """Host layout of the recursion, vectorised (no per-month Python loop): the valid rows of
+    every OOS month in id order (only the columns the recursion reads), each month's aim
+    weights aligned to them, the drift map from month t's rows to month t+1's (position of
+    each id of t+1 among t's rows, or -1 for a new name), and the month of every row."""
     mi_all = month_index(chars["eom"])
-    data = chars[np.isin(mi_all, oos_months) & chars["valid"].to_numpy()].copy()
-    data["mi"] = month_index(data["eom"])
+    sel = np.isin(mi_all, oos_months) & chars["valid"].to_numpy()
+    cols = [c for c in ("eom", "id", "me", "tr_ld1", "lambda") if c in chars.columns]
+    data = chars.loc[sel, cols].copy()
+    data["mi"] = mi_all[sel]
     data = data.sort_values(["mi", "id"], kind="stable").reset_index(drop=True)
     months = np.asarray(oos_months, np.int64)
     mi = data["mi"].to_numpy()
     starts = np.searchsorted(mi, months, "left")
     stops = np.searchsorted(mi, months, "right")
     ids_all = data["id"].to_numpy(np.int64)
+    trow = np.searchsorted(months, mi)                  # month position of every row
     aim_key = month_index(aims["eom"]) * 10_000_000 + aims["id"].to_numpy(np.int64)
     order = np.argsort(aim_key, kind="stable")
     ak, av = aim_key[order], aims["w_aim"].to_numpy(np.float64)[order]
@@ -171,16 +197,17 @@ def _weights_plan(cfg: Config, chars: pd.DataFrame, wealth: pd.DataFrame, aims: 
     p = np.clip(np.searchsorted(ak, key), 0, max(len(ak) - 1, 0))
     w_aim = np.where((len(ak) > 0) & (ak[p] == key), av[p], np.nan) if len(ak) else \
         np.full(len(key), np.nan)
-    nxt = np.full(len(data), -1, np.int64)            # row r of month t+1 -> row in month t
-    for t in range(len(months) - 1):
-        a0, a1, b0, b1 = starts[t], stops[t], starts[t + 1], stops[t + 1]
-        cur = ids_all[a0:a1]
-        q = np.clip(np.searchsorted(cur, ids_all[b0:b1]), 0, max(a1 - a0 - 1, 0))
-        hit = (a1 > a0) & (cur[q] == ids_all[b0:b1]) if a1 > a0 else np.zeros(b1 - b0, bool)
-        nxt[b0:b1] = np.where(hit, q, -1)
-    mumap = dict(zip(month_index(wealth["eom"]), wealth["mu_ld1"].to_numpy(np.float64)))
+    # row r of month t+1 -> row of the same id in month t (keys (t, id) are sorted)
+    tk = trow * 10_000_000 + ids_all
+    nxt = np.full(len(data), -1, np.int64)
+    later = trow >= 1
+    if later.any() and len(tk):
+        qk = (trow[later] - 1) * 10_000_000 + ids_all[later]
+        q = np.clip(np.searchsorted(tk, qk), 0, len(tk) - 1)
+        hit = tk[q] == qk
+        nxt[later] = np.where(hit, q - starts[trow[later] - 1], -1)
     return dict(data=data, months=months, starts=starts, stops=stops, ids=ids_all,
-                w_aim=w_aim, nxt=nxt, mu=np.array([mumap[int(d)] for d in months]))
+                w_aim=w_aim, nxt=nxt, trow=trow, mu=_month_values(wealth, "mu_ld1", months))
 
 
 def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.DataFrame,
@@ -194,26 +221,40 @@ def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
     drift w_start(t+1) = w_opt (1 + tr_ld1) / (1 + mu_ld1) gathered through the id map, new
     names 0 - with no host round trip per month.  The chain crosses ranks as ONE N-vector
     hand-off (point-to-point, rank r -> r+1); the per-row weights are gathered at the end."""
+    from ..ops.ridge import _HostClock
     from ..parallel import collectives as coll
     from ..parallel.dist import env as dist_env
+    th = _HostClock()
     env = dist_env()
     dev = torch.device(device)
     pf = cfg.pf_set
     gamma, mu = float(pf["gamma_rel"]), float(pf["mu"])
     tc_on = bool(cfg.settings["Transaction_Costs"])
     pl = _weights_plan(cfg, chars, wealth, aims, oos_months)
+    th("s9.plan")
     data, months, starts, stops = pl["data"], pl["months"], pl["starts"], pl["stops"]
     B = len(months)
     ns = stops - starts
     N = int(ns.max()) if B else 1
     K = barra.X.shape[1]
-    wmap = dict(zip(month_index(wealth["eom"]), wealth["wealth"].to_numpy(np.float64)))
-    rfmap = dict(zip(month_index(risk_free["eom"]), risk_free["rf"].to_numpy(np.float64)))
+    wvals = _month_values(wealth, "wealth", months)
+    rfvals = _month_values(risk_free, "rf", months)
     mine = np.asarray(list(coll.contiguous_split(B, env.world_size, env.rank)), np.int64)
     f64 = dict(dtype=torch.float64, device=dev)
     lam_col = data["lambda"].to_numpy(np.float64) if tc_on else None
     tr1 = data["tr_ld1"].to_numpy(np.float64)
     ids_all = pl["ids"]
+    trow = pl["trow"]
+    # Barra rows keyed (month, id): one sorted key array for every exact lookup below
+    bkey = np.repeat(barra.months.astype(np.int64), np.diff(barra.offsets)) * 10_000_000 + \
+        barra.ids.astype(np.int64)
+
+    def rows_of(tt: np.ndarray):
+        """(rows, batch index, column) of every data row of the months ``tt`` (in order)."""
+        n_t = ns[tt]
+        bi = np.repeat(np.arange(len(tt)), n_t)
+        col = np.arange(int(n_t.sum())) - np.repeat(np.cumsum(n_t) - n_t, n_t)
+        return starts[tt][bi] + col, bi, col
 
     # ---- batched m_t of this rank's months (K19) --------------------------------------
     Bm = len(mine)
@@ -226,51 +267,45 @@ def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
     for c0 in range(0, Bm, chunk):
         cm = mine[c0:c0 + chunk]
         Bc = len(cm)
+        rows, bi, col = rows_of(cm)
+        pos = _exact_lookup(bkey, months[trow[rows]] * 10_000_000 + ids_all[rows],
+                            "OOS ids missing from the Barra universe")
         Xl = np.zeros((Bc, N, K))
-        Fb = np.zeros((Bc, K, K))
         iv = np.ones((Bc, N))
-        lam = np.empty((Bc, N))
         mask = np.zeros((Bc, N))
-        for bi, t in enumerate(cm):
-            d = int(months[t])
-            rows = np.arange(starts[t], stops[t])
-            ids = ids_all[rows]
-            bids, X, F, ivol = barra.slice(d)
-            pos = np.searchsorted(bids, ids)
-            if np.any(pos >= len(bids)) or np.any(bids[np.minimum(pos, len(bids) - 1)] != ids):
-                raise KeyError(f"month {d}: OOS ids missing from the Barra universe")
-            n = len(ids)
-            Xl[bi, :n], Fb[bi], iv[bi, :n] = X[pos], F, ivol[pos]
-            lam[bi] = gamma / wmap[d]
-            lam[bi, :n] = lam_col[rows] if tc_on else 1e-16
-            mask[bi, :n] = 1.0
+        Xl[bi, col], iv[bi, col], mask[bi, col] = barra.X[pos], barra.ivol[pos], 1.0
+        Fb = barra.F[_exact_lookup(barra.months.astype(np.int64), months[cm], "Barra month")]
+        lam = np.repeat((gamma / wvals[cm])[:, None], N, axis=1)
+        lam[bi, col] = lam_col[rows] if tc_on else 1e-16
         Xd, ivd = torch.as_tensor(Xl, **f64), torch.as_tensor(iv, **f64)
         Sig = torch.empty((Bc, N, N), **f64)
         gemm_fused(torch.bmm(Xd, torch.as_tensor(Fb, **f64)), Xd, Sig, trans_b=True,
                    diag_col0=0, diag_vec=ivd)
-        wv = torch.as_tensor([wmap[int(months[t])] for t in cm], **f64)
-        rfv = torch.as_tensor([rfmap[int(months[t])] for t in cm], **f64)
-        mt, a = la.m_tilde(Sig, torch.as_tensor(lam, **f64), wv, rfv, mu, gamma,
-                           cfg.run.iterations, mask=torch.as_tensor(mask, **f64))
+        mt, a = la.m_tilde(Sig, torch.as_tensor(lam, **f64), torch.as_tensor(wvals[cm], **f64),
+                           torch.as_tensor(rfvals[cm], **f64), mu, gamma, cfg.run.iterations,
+                           mask=torch.as_tensor(mask, **f64))
         mt_all[c0:c0 + Bc] = mt
         a_all[c0:c0 + Bc] = a
+    th("s9.m_t")
 
     # ---- the sequential chain on the device ---------------------------------------------
+    rows, bi, col = rows_of(mine)
+
     def padded(vals: np.ndarray, fill: float) -> torch.Tensor:
         out = np.full((Bm, N), fill)
-        for i, t in enumerate(mine):
-            out[i, :ns[t]] = vals[starts[t]:stops[t]]
+        out[bi, col] = vals[rows]
         return torch.as_tensor(out, **f64)
 
     wa = padded(pl["w_aim"], 0.0)
     grow = padded((1.0 + tr1), 1.0) / torch.as_tensor(1.0 + pl["mu"][mine], **f64).view(Bm, 1)
     nmap = np.zeros((Bm, N), np.int64)
     hit = np.zeros((Bm, N))
-    for i, t in enumerate(mine):
-        if t + 1 < B:
-            q = pl["nxt"][starts[t + 1]:stops[t + 1]]
-            nmap[i, :len(q)] = np.maximum(q, 0)
-            hit[i, :len(q)] = q >= 0
+    has_next = np.nonzero(mine + 1 < B)[0]
+    if len(has_next):
+        r1, b1, c1 = rows_of(mine[has_next] + 1)
+        q = pl["nxt"][r1]
+        nmap[has_next[b1], c1] = np.maximum(q, 0)
+        hit[has_next[b1], c1] = q >= 0
     nmap_t, hit_t = torch.as_tensor(nmap, device=dev), torch.as_tensor(hit, **f64)
     ws0 = torch.zeros(N, **f64)
     if Bm and mine[0] == 0:
@@ -282,14 +317,27 @@ def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
     Wst = torch.zeros((Bm, N), **f64)
     Wopt = torch.zeros((Bm, N), **f64)
     ws = ws0
-    for i in range(Bm):
-        Wst[i] = ws
-        d = (ws - wa[i]) / a_all[i]
-        wopt = wa[i] + a_all[i] * torch.mv(mt_all[i], d)
-        Wopt[i] = wopt
-        ws = (wopt * grow[i])[nmap_t[i]] * hit_t[i]                 # next month's w_start
+    if nat.is_device(mt_all) and N <= int(nat.hip_lib().pfml_weights_chain_max_n()):
+        # one persistent-workgroup launch for the whole chain (csrc/weights.hip)
+        ws = torch.empty(N, **f64)
+        if Bm:
+            nat.check(nat.hip_lib().pfml_weights_chain(
+                mt_all.data_ptr(), N, N * N, a_all.data_ptr(), wa.data_ptr(),
+                grow.contiguous().data_ptr(), nmap_t.data_ptr(), hit_t.data_ptr(), N,
+                ws0.contiguous().data_ptr(), Bm, N, Wst.data_ptr(), Wopt.data_ptr(),
+                ws.data_ptr(), nat.stream_of(mt_all)), "pfml_weights_chain")
+        else:
+            ws.copy_(ws0)
+    else:
+        for i in range(Bm):
+            Wst[i] = ws
+            d = (ws - wa[i]) / a_all[i]
+            wopt = wa[i] + a_all[i] * torch.mv(mt_all[i], d)
+            Wopt[i] = wopt
+            ws = (wopt * grow[i])[nmap_t[i]] * hit_t[i]             # next month's w_start
     if env.is_dist:
         coll.send_next(ws)
+    th("s9.chain")
     # gather the per-row weights (rank order = month order)
     sel = torch.as_tensor(np.arange(N)[None, :] < ns[mine][:, None], device=dev)
     w_start_rows = coll.all_gather_varlen(Wst[sel])
@@ -301,10 +349,11 @@ def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
     # rows with a missing aim stay NaN like the reference's merge would leave them
     nan_aim = np.isnan(pl["w_aim"])
     w = np.where(nan_aim, np.nan, w)
-    mumap = dict(zip(month_index(wealth["eom"]), wealth["mu_ld1"].to_numpy(np.float64)))
-    return pd.DataFrame({"eom": month_end(data["mi"].to_numpy()),
-                         "mu_ld1": [mumap[int(x)] for x in data["mi"]],
-                         "id": ids_all, "tr_ld1": tr1, "w_start": w_start, "w": w})
+    out = pd.DataFrame({"eom": month_end(data["mi"].to_numpy()),
+                        "mu_ld1": pl["mu"][trow],
+                        "id": ids_all, "tr_ld1": tr1, "w_start": w_start, "w": w})
+    th("s9.gather+frame")
+    return out
 
 
 def pf_ts(weights: pd.DataFrame, chars: pd.DataFrame, wealth: pd.DataFrame,

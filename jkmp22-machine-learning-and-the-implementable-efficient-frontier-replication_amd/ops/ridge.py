@@ -78,18 +78,26 @@ def window_prefix_sym(X: torch.Tensor, starts, stops, dev_bounds=None,
 
 
 class _HostClock:
-    """PFML_HOST_TIMING=1: print host-side section times (microseconds) to stderr."""
+    """PFML_HOST_TIMING=1: print host-side section times (microseconds) to stderr;
+    PFML_HOST_TIMING=sync: synchronise the device at every mark (section = wall time of the
+    queued work)."""
 
     def __init__(self):
         import os
         import time
-        self.on = bool(os.environ.get("PFML_HOST_TIMING"))
+        v = os.environ.get("PFML_HOST_TIMING", "")
+        self.on = bool(v)
+        self.sync = v == "sync" and torch.cuda.is_available()
         self.time = time.perf_counter
+        if self.sync:
+            torch.cuda.synchronize()
         self.t = self.time()
 
     def __call__(self, what: str) -> None:
         if self.on:
             import sys
+            if self.sync:
+                torch.cuda.synchronize()
             now = self.time()
             print(f"[host] {what}: {1e6 * (now - self.t):.0f} us", file=sys.stderr)
             self.t = now

@@ -3,7 +3,9 @@
 small synthetic dataset): per-month r_tilde / risk / tc / denom (PFML_Input_Data.py:318-491),
 ridge coefficients incl. lambda = 0 (PFML_Search_Coef.py:102-137), validation.csv rows with the
 Q2 accumulation, expanding-mean cum_obj and dense rank (PFML_hp_reals.py:60-130), and
-weights.csv / pf.csv / pf_summary.csv (PFML_best_hps.py:137-358), compat mode, fp64 CPU path.
+weights.csv / pf.csv / pf_summary.csv (PFML_best_hps.py:137-358), compat mode, fp64; the CPU
+path, and (``-m gpu``) the whole pipeline on the device - every HIP stage against the
+reference's own numbers.
 """
 import json
 import os
@@ -17,10 +19,10 @@ G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_pipe
 RTOL = 1e-10
 
 
-@pytest.fixture(scope="module")
-def ref_run(tmp_path_factory):
+@pytest.fixture(scope="module", params=["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def ref_run(request, tmp_path_factory):
     """The golden's inputs regenerated through this engine's L0-L3 (deterministic), then the
-    engine's pipeline from pfml-input to pfml-best-hps on them."""
+    engine's pipeline from pfml-input to pfml-best-hps on them (CPU oracle or device)."""
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(G), "..", "..", "tools"))
     import make_golden_pipeline as mk
@@ -34,7 +36,7 @@ def ref_run(tmp_path_factory):
         pytest.fail("regenerated L0-L3 inputs differ from the golden's (L2/L3 changed?): "
                     "re-freeze with tools/make_golden_pipeline.py")
     cfg = cfg.override([f"run.artifact_dir={os.path.join(d, 'art')}"])
-    p = Pipeline(cfg, device="cpu")
+    p = Pipeline(cfg, device=request.param)
     p.run(["pfml-input", "pfml-search-coef", "pfml-hp-reals", "pfml-aim", "pfml-hps",
            "pfml-best-hps"])
     return cfg, p, d
@@ -55,14 +57,14 @@ def test_s4_summands_match_reference(ref_run):
     z = np.load(os.path.join(G, "s4_reals.npz"), allow_pickle=False)
     months = month_index(pd.to_datetime(z["months"]))
     st = p.state
-    out = build_inputs(cfg, st["chars"], st["barra"], st["wealth"], st["risk_free"], "cpu",
+    out = build_inputs(cfg, st["chars"], st["barra"], st["wealth"], st["risk_free"], p.device,
                        months=months, keep_risk_tc=True)
     Pm = cfg.p_max
     for i in range(len(months)):
-        rt = to_reference_order(out.reals.r_tilde[0, i], Pm).numpy()
-        rk = to_reference_order(out.reals.risk[0, i], Pm, dims=(0, 1)).numpy()
-        tc = to_reference_order(out.reals.tc[0, i], Pm, dims=(0, 1)).numpy()
-        dn = to_reference_order(out.reals.denom[0, i], Pm, dims=(0, 1)).numpy()
+        rt = to_reference_order(out.reals.r_tilde[0, i], Pm).cpu().numpy()
+        rk = to_reference_order(out.reals.risk[0, i], Pm, dims=(0, 1)).cpu().numpy()
+        tc = to_reference_order(out.reals.tc[0, i], Pm, dims=(0, 1)).cpu().numpy()
+        dn = to_reference_order(out.reals.denom[0, i], Pm, dims=(0, 1)).cpu().numpy()
         assert _rel(rt, z[f"r_tilde_{i}"]) < RTOL
         assert _rel(rk, z[f"risk_{i}"]) < RTOL
         assert _rel(tc, z[f"tc_{i}"]) < RTOL
@@ -76,7 +78,7 @@ def test_ridge_coefficients_match_reference(ref_run):
     years = list(np.asarray(grid.years_local))
     for key in z.files:
         y, pp, li = (int(v) for v in key.split("_"))
-        b = grid.beta[0, years.index(y), cfg.p_vec.index(pp), li, : pp + 1].numpy()
+        b = grid.beta[0, years.index(y), cfg.p_vec.index(pp), li, : pp + 1].cpu().numpy()
         h = pp // 2
         # internal [const, cos1, sin1, ...] -> reference [const, cos1..cos_h, sin1..sin_h]
         perm = np.r_[0, 1 + 2 * np.arange(h), 2 + 2 * np.arange(h)]
