@@ -12,18 +12,24 @@ import numpy as np
 import pandas as pd
 
 
+_EPOCH_MI = 1970 * 12                  # month index of numpy's datetime64[M] zero
+
+
 def month_index(dates) -> np.ndarray:
-    """Timestamp(s) -> integer month index (12*year + month-1)."""
+    """Timestamp(s) -> integer month index (12*year + month-1).  Naive datetime64 arrays take
+    a pure numpy path (datetime64[M] arithmetic); anything else goes through pandas."""
+    a = np.atleast_1d(np.asarray(dates))
+    if np.issubdtype(a.dtype, np.datetime64) and not np.isnat(a).any():
+        return a.astype("datetime64[M]").astype(np.int64) + _EPOCH_MI
     d = pd.DatetimeIndex(pd.to_datetime(np.atleast_1d(dates)))
     return (d.year.to_numpy().astype(np.int64) * 12 + d.month.to_numpy().astype(np.int64) - 1)
 
 
 def month_end(mi) -> pd.DatetimeIndex:
-    """Integer month index -> month-end Timestamp(s)."""
+    """Integer month index -> month-end Timestamp(s) (first day of the next month - 1 day)."""
     mi = np.atleast_1d(np.asarray(mi, dtype=np.int64))
-    y, m = mi // 12, mi % 12 + 1
-    first = pd.to_datetime({"year": y, "month": m, "day": np.ones_like(y)})
-    return pd.DatetimeIndex(first + pd.offsets.MonthEnd(0))
+    nxt = (mi - _EPOCH_MI + 1).astype("datetime64[M]").astype("datetime64[D]")
+    return pd.DatetimeIndex((nxt - np.timedelta64(1, "D")).astype("datetime64[ns]"))
 
 
 def eom(ts) -> pd.Timestamp:
