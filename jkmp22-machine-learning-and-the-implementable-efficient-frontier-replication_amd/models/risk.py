@@ -105,8 +105,10 @@ def cluster_ranks(chars: pd.DataFrame, labels: pd.DataFrame, features: list[str]
             if dirv == -1:
                 flip[fidx[c]] = True
     X = chars[feats].to_numpy(np.float64)
-    X = np.where(flip[None, :], 1.0 - X, X)
-    R = X @ M
+    # direction -1 members enter as 1 - x: folded into the weights, (1 - x) m = m - x m, so
+    # the panel is not copied ( R = X (s o M) + sum_flipped M, s = -1 on flipped rows )
+    sgn = np.where(flip, -1.0, 1.0)[:, None]
+    R = X @ (sgn * M) + M[flip].sum(0)[None, :]
     empty = M.sum(0) == 0
     R[:, empty] = np.nan
     return clusters, R
@@ -211,13 +213,6 @@ def _seg_median(v: torch.Tensor, g: torch.Tensor, G: int) -> torch.Tensor:
     return torch.where(cnt > 0, med, torch.full_like(med, float("nan")))
 
 
-def _codes(*cols) -> np.ndarray:
-    """Dense int64 codes of the rows' key tuples (order-preserving, NaN / None -> -1)."""
-    key = pd.MultiIndex.from_arrays([pd.Series(c) for c in cols])
-    codes, _ = pd.factorize(key)
-    return codes.astype(np.int64)
-
-
 def estimate_cov_frames(chars: pd.DataFrame, daily: pd.DataFrame, labels: pd.DataFrame,
                         cs: dict, device: str = "cpu") -> BarraCov:
     """The Barra model from in-memory frames, batched end to end (no per-day / per-month
@@ -238,15 +233,21 @@ def estimate_cov_frames(chars: pd.DataFrame, daily: pd.DataFrame, labels: pd.Dat
     dev = torch.device(device)
     f64 = dict(dtype=torch.float64, device=dev)
     features = get_features()
-    chars = chars.sort_values(["eom", "id"], kind="stable").reset_index(drop=True)
-    clusters, R = cluster_ranks(chars, labels, features)
-    log.info(f"Cluster Labels are the following {clusters}")
     ids_m = chars["id"].to_numpy(np.int64)
     mi_m = month_index(chars["eom"])
+    srt = (mi_m * (1 << 32) + ids_m) if len(ids_m) else mi_m
+    if not (np.all(srt[1:] >= srt[:-1]) and isinstance(chars.index, pd.RangeIndex)
+            and chars.index.start == 0 and chars.index.step == 1):
+        chars = chars.sort_values(["eom", "id"], kind="stable").reset_index(drop=True)
+        ids_m = chars["id"].to_numpy(np.int64)
+        mi_m = month_index(chars["eom"])
+    clusters, R = cluster_ranks(chars, labels, features)
+    log.info(f"Cluster Labels are the following {clusters}")
     industries = sorted(chars["ff12"].dropna().unique())
-    ff = chars["ff12"].to_numpy(object)
-    D = np.stack([(ff == ind).astype(np.float64) for ind in industries], axis=1) \
-        if industries else np.zeros((len(chars), 0))
+    icode = pd.Categorical(chars["ff12"], categories=industries).codes.astype(np.int64)
+    D = np.zeros((len(chars), len(industries)))
+    hasi = icode >= 0
+    D[np.nonzero(hasi)[0], icode[hasi]] = 1.0                          # one-hot, NaN row: 0
     mcode = np.searchsorted(np.unique(mi_m), mi_m)
     Z = _seg_zscore(torch.as_tensor(R, **f64), torch.as_tensor(mcode, device=dev),
                     int(mcode.max()) + 1 if len(mcode) else 0)
@@ -254,35 +255,45 @@ def estimate_cov_frames(chars: pd.DataFrame, daily: pd.DataFrame, labels: pd.Dat
     factor_cols = [str(i) for i in industries] + clusters
     sg = chars["size_grp"]
     row_ok = torch.isfinite(Fexp).all(1) & torch.as_tensor(
-        (sg.notna() & chars["ff12"].notna()).to_numpy(), device=dev)
+        (sg.notna().to_numpy() & hasi), device=dev)
     log.info("Cluster Ranks Completed.")
     th("s3.cluster_ranks+zscore")
 
     # ---- daily <- exposures of the PREVIOUS month (eom_ret = eom + 1M), inner + dropna ------
-    dd_date = daily["date"].to_numpy().astype("datetime64[D]")
-    keep = dd_date >= np.datetime64(chars["eom"].min().date())
-    d_id = daily["id"].to_numpy(np.int64)[keep]
-    d_date = dd_date[keep]
-    d_ret = daily["ret_exc"].to_numpy(np.float64)[keep]
-    d_mi = month_index(d_date)
+    # The daily panel (~9.4M rows at S&P 500 scale) is handled on the device: integer
+    # (id, month) keys, one sorted search into the monthly rows, compaction, and the (date, id)
+    # order as ONE sort of a dense int64 key; only per-day / per-month results come back.
+    i64 = dict(dtype=torch.int64, device=dev)
+    t_dn = torch.as_tensor(daily["date"].to_numpy().astype("datetime64[D]").astype(np.int64),
+                           **i64)
+    t_id = torch.as_tensor(daily["id"].to_numpy(np.int64), **i64)
+    t_ret = torch.as_tensor(daily["ret_exc"].to_numpy(np.float64), **f64)
+    keep = t_dn >= int(np.datetime64(chars["eom"].min().date(), "D").astype(np.int64))
+    ud, uinv = torch.unique(t_dn, return_inverse=True)
+    ud_mi = torch.as_tensor(month_index(ud.cpu().numpy().astype("datetime64[D]")), **i64)
     SH = np.int64(1 << 20)
     mkey = ids_m * SH + (mi_m + 1)                                   # key of (id, eom_ret)
     mo = np.argsort(mkey, kind="stable")
-    dkey = d_id * SH + d_mi
-    pos = np.clip(np.searchsorted(mkey[mo], dkey), 0, max(len(mkey) - 1, 0))
-    hit = (mkey[mo][pos] == dkey) if len(mkey) else np.zeros(len(dkey), bool)
-    mrow = mo[pos]
-    ok_rows = row_ok.cpu().numpy()
-    sel = hit & ok_rows[mrow] & np.isfinite(d_ret)
-    d_id, d_date, d_ret, mrow = d_id[sel], d_date[sel], d_ret[sel], mrow[sel]
-    dnum = d_date.astype(np.int64)
-    order = np.lexsort((d_id, dnum))                                  # (date, id)
-    d_id, dnum, d_ret, mrow = d_id[order], dnum[order], d_ret[order], mrow[order]
-    gs_day = rt.group_starts(dnum)
+    mkey_s = torch.as_tensor(mkey[mo], **i64)
+    dkey = t_id * int(SH) + ud_mi[uinv]
+    pos = torch.searchsorted(mkey_s, dkey).clamp_(max=max(len(mkey) - 1, 0))
+    hit = (mkey_s[pos] == dkey) if len(mkey) else torch.zeros_like(keep)
+    mrow = torch.as_tensor(mo, **i64)[pos]
+    sel = keep & hit & row_ok[mrow] & torch.isfinite(t_ret)
+    idx = torch.nonzero(sel).squeeze(1)
+    t_id, t_dn, t_ret, mrow = t_id[idx], t_dn[idx], t_ret[idx], mrow[idx]
+    ids_u = torch.unique(t_id)
+    code = torch.searchsorted(ids_u, t_id)
+    dmin = int(t_dn.min()) if len(t_dn) else 0
+    span = (int(t_dn.max()) - dmin + 1) if len(t_dn) else 1
+    order = torch.sort((t_dn - dmin) * len(ids_u) + code, stable=True).indices   # (date, id)
+    t_id, t_dn, t_ret, mrow, code = t_id[order], t_dn[order], t_ret[order], mrow[order], code[order]
+    udays, dcnt = torch.unique_consecutive(t_dn, return_counts=True)
+    gs_day = torch.cat([torch.zeros(1, **i64), torch.cumsum(dcnt, 0)])
     th("s3.daily_merge")
-    Xd = Fexp[torch.as_tensor(mrow, device=dev)].contiguous()
-    coef, resid_t, nbad = _ols(Xd, torch.as_tensor(d_ret, **f64), torch.as_tensor(gs_day))
-    days = dnum[gs_day[:-1]]
+    Xd = Fexp[mrow].contiguous()
+    coef, resid_t, nbad = _ols(Xd, t_ret, gs_day)
+    days = udays.cpu().numpy()
     log.info(f"Factor Returns Completed ({len(days)} days, {nbad} pinv fallbacks).")
     th("s3.daily_ols")
 
@@ -303,24 +314,35 @@ def estimate_cov_frames(chars: pd.DataFrame, daily: pd.DataFrame, labels: pd.Dat
     Fm = ewma_factor_cov(coef, end_idx, obs, w_cor, w_var, scale=21.0).cpu().numpy()
     th("s3.ewma_factor_cov")
 
-    # ---- idiosyncratic EWMA vol (:345-442) -----------------------------------------
-    o2 = np.lexsort((dnum, d_id))                                     # (id, date)
-    s_id, s_date = d_id[o2], dnum[o2]
-    resid_s = resid_t[torch.as_tensor(o2, device=dev)]
-    gs_id = rt.group_starts(s_id)
+    # ---- idiosyncratic EWMA vol (:345-442), on the device ---------------------------------
+    o2 = torch.sort(code * span + (t_dn - dmin), stable=True).indices   # (id, date)
+    s_id, s_dn = t_id[o2], t_dn[o2]
+    resid_s = resid_t[o2]
+    _, icnt = torch.unique_consecutive(s_id, return_counts=True)
+    gs_id = torch.cat([torch.zeros(1, **i64), torch.cumsum(icnt, 0)])
     lam = 0.5 ** (1.0 / cs["hl_stock_var"])
-    res_vol = _ewma_vol(resid_s, gs_id, lam, int(cs["initial_var_obs"])).cpu().numpy()
-    dpos = np.searchsorted(days, s_date)
-    td_252 = np.where(dpos >= 252, days[np.maximum(dpos - 252, 0)].astype(np.float64), np.nan)
-    d200 = rt.group_shift(s_date.astype(np.float64), gs_id, 200)
-    ok = (d200 >= td_252) & ~np.isnan(res_vol)
-    s_mi = month_index(s_date.astype("datetime64[D]"))
+    res_vol = _ewma_vol(resid_s, gs_id, lam, int(cs["initial_var_obs"]))
+    days_t = torch.as_tensor(days, **i64)
+    dpos = torch.searchsorted(days_t, s_dn)
+    nanv = torch.full(s_dn.shape, float("nan"), **f64)
+    td_252 = torch.where(dpos >= 252, days_t[(dpos - 252).clamp(min=0)].to(torch.float64), nanv)
+    row = torch.arange(len(s_dn), **i64)
+    src = row - 200                                                    # group_shift(., 200)
+    gstart = torch.repeat_interleave(gs_id[:-1], icnt)
+    d200 = torch.where(src >= gstart, s_dn[src.clamp(min=0)].to(torch.float64), nanv)
+    ok = (d200 >= td_252) & ~torch.isnan(res_vol)
+    day_mi = torch.as_tensor(month_index(days.astype("datetime64[D]")), **i64)
+    s_mi = day_mi[dpos]
     # the last observation per (id, month) among the rows that pass the filter
-    f_id, f_mi, f_date, f_vol = s_id[ok], s_mi[ok], s_date[ok], res_vol[ok]
-    flast = np.r_[(f_id[1:] != f_id[:-1]) | (f_mi[1:] != f_mi[:-1]), True] if len(f_id) else \
-        np.zeros(0, bool)
-    vkey = f_id[flast] * SH + f_mi[flast]
-    vval = f_vol[flast]
+    kidx = torch.nonzero(ok).squeeze(1)
+    f_id, f_mi, f_vol = s_id[kidx], s_mi[kidx], res_vol[kidx]
+    if len(f_id):
+        flast = torch.cat([(f_id[1:] != f_id[:-1]) | (f_mi[1:] != f_mi[:-1]),
+                           torch.ones(1, dtype=torch.bool, device=dev)])
+    else:
+        flast = torch.zeros(0, dtype=torch.bool, device=dev)
+    vkey = (f_id[flast] * int(SH) + f_mi[flast]).cpu().numpy()
+    vval = f_vol[flast].cpu().numpy()
     th("s3.idio_vol")
 
     # ---- Barra assembly (:453-494), every calc month at once -----------------------------
@@ -332,13 +354,18 @@ def estimate_cov_frames(chars: pd.DataFrame, daily: pd.DataFrame, labels: pd.Dat
     vhit = (vkey[vo][vp] == rkey) if len(vkey) else np.zeros(len(rkey), bool)
     rv = np.where(vhit, vval[vo][vp], np.nan)
     rv_t = torch.as_tensor(rv, **f64)
-    gcode = _codes(mi_m[rows], sg.to_numpy(object)[rows])
-    sg_nan = sg.isna().to_numpy()[rows]
-    G1 = int(gcode.max()) + 1 if len(gcode) else 0
-    med_g = _seg_median(rv_t, torch.as_tensor(gcode, device=dev), G1)[torch.as_tensor(gcode, device=dev)]
+    # (month, size group) groups as integer codes: month position x (size-group code + 1),
+    # a NaN size group gets its own slot and is masked below
+    mcode2 = np.searchsorted(calc_mi, mi_m[rows])
+    sgc = pd.Categorical(sg.to_numpy(object)[rows]).codes.astype(np.int64)
+    nsg = int(sgc.max()) + 2 if len(sgc) else 1
+    gcode = mcode2 * nsg + (sgc + 1)
+    sg_nan = sgc < 0
+    G1 = len(calc_mi) * nsg
+    gct = torch.as_tensor(gcode, device=dev)
+    med_g = _seg_median(rv_t, gct, G1)[gct]
     med_g = torch.where(torch.as_tensor(sg_nan, device=dev), torch.full_like(med_g, float("nan")),
                         med_g)                                        # NaN size_grp: no group
-    mcode2 = np.searchsorted(calc_mi, mi_m[rows])
     med_m = _seg_median(rv_t, torch.as_tensor(mcode2, device=dev), len(calc_mi))[
         torch.as_tensor(mcode2, device=dev)]
     med = torch.where(torch.isnan(med_g), med_m, med_g)

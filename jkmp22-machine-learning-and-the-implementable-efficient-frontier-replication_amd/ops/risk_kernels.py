@@ -129,9 +129,11 @@ def ewma_vol(x: torch.Tensor, groups, lam: float, start: int) -> torch.Tensor:
     """EWMA vol per group of rows (sorted by (group, time)); groups = CSR starts."""
     if not nat.is_device(x):
         from .. import runtime as rt
-        return torch.as_tensor(rt.ewma_vol(x.numpy(), np.asarray(groups), lam, start))
+        g = groups.cpu().numpy() if isinstance(groups, torch.Tensor) else np.asarray(groups)
+        return torch.as_tensor(rt.ewma_vol(x.numpy(), g, lam, start))
     xc = x.to(torch.float64).contiguous()
-    gs = torch.as_tensor(np.asarray(groups, np.int64), device=x.device)
+    gs = (groups.to(device=x.device, dtype=torch.int64) if isinstance(groups, torch.Tensor)
+          else torch.as_tensor(np.asarray(groups, np.int64), device=x.device))
     out = torch.empty_like(xc)
     nat.check(nat.hip_lib().pfml_ewma_vol(xc.data_ptr(), gs.data_ptr(), gs.numel() - 1,
                                           float(lam), int(start), out.data_ptr(),
