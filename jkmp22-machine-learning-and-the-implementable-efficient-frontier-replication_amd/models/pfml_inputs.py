@@ -4,10 +4,11 @@ The reference's hot loop (:318-491, 1.6-2.6 s per month on 8 CPU cores, pandas-b
 a batched device pipeline over MONTHS (dates are independent given m_t, Sigma_t and the
 13-month signal window) and over g (the g-dependent part is only the signal block):
 
-1. RFF features for the whole panel: one fp64 MFMA GEMM X W + cos/sin (K13, once per g),
-   stored in the interleaved order [constant, cos1, sin1, ...];
+1. RFF features for the whole panel: ONE fused GEMM launch per g whose epilogue writes
+   cos / sin of X W (K13) in the interleaved order [constant, cos1, sin1, ...];
 2. vol scales sqrt(diag(Sigma_t)) = sqrt(rowsum((X F) o X) + ivol) per Barra row on the
-   device, without forming Sigma (:274-307), cross-sectional median fill (torch nanmedian);
+   device, without forming Sigma (:274-307), NaN filled with the month's median (pandas
+   semantics: mean of the two middle values), on the device;
 3. per batch of months (ragged universes padded block-diagonally):
    * signals: gather the 13 x N x P window, demean RFF columns, unit-norm every column, scale
      rows by 1/vol (K11/K12, :357-391);

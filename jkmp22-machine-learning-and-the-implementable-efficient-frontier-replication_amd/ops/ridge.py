@@ -266,9 +266,9 @@ def repair_nonspd(beta, SD, Sr, cell_src, cell_n, cell_scale, lv) -> np.ndarray:
 _SIDE: dict = {}
 
 
-def _side_stream(dev: torch.device) -> torch.cuda.Stream:
-    """One cached secondary HIP stream per device (stream creation is not free)."""
-    key = dev.index if dev.index is not None else torch.cuda.current_device()
+def _side_stream(dev: torch.device, k: int = 0) -> torch.cuda.Stream:
+    """Cached secondary HIP streams per device (stream creation is not free)."""
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), k)
     if key not in _SIDE:
         _SIDE[key] = torch.cuda.Stream(device=dev)
     return _SIDE[key]
@@ -278,6 +278,18 @@ BAND_SINGLE, BAND_MULTI = 1, 2
 # Above this many largest-n cells per launch the one-workgroup-per-cell reduction (throughput
 # form) beats the multi-workgroup one (latency form); measured on MI355X, tools/bench_band.py.
 BAND_MULTI_MAX_CELLS = 64
+# Hybrid (one GPU holds the whole grid): this many of the largest-n cells take the
+# multi-workgroup reduction on a third stream while the rest keep one workgroup per cell, so
+# the CUs the single-workgroup cells leave idle also work on big cells.  PFML_BAND_HYBRID
+# overrides (0 = off).
+BAND_HYBRID_CELLS = 0
+
+
+def _hybrid_cells(nbig: int) -> int:
+    import os
+    v = os.environ.get("PFML_BAND_HYBRID")
+    k = int(v) if v else BAND_HYBRID_CELLS
+    return max(0, min(k, nbig - 1))
 
 
 def band_policy(cell_n: np.ndarray) -> tuple[int, bool]:
@@ -318,15 +330,24 @@ def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell,
     if hit is not None:
         return hit
     big = cell_n == cell_n.max()
+    nhy = _hybrid_cells(int(big.sum())) if split else 0
+    if split and nhy:
+        # the first nhy big cells (in cell order) -> multi-workgroup group
+        hy = big & (np.cumsum(big) <= nhy)
+        parts = ((big & ~hy, BAND_SINGLE), (hy, BAND_MULTI), (~big, BAND_SINGLE))
+    elif split:
+        parts = ((big, BAND_SINGLE), (~big, BAND_SINGLE))
+    else:
+        parts = ((np.ones(len(cell_n), dtype=bool), None),)
     groups, arrays = [], []
-    for grp in ((big, ~big) if split else (np.ones(len(cell_n), dtype=bool),)):
+    for grp, gmode in parts:
         cells = np.nonzero(grp)[0]
         jobs = np.nonzero(grp[job_cell])[0]
         rp = ridge_plan(P, L, cell_src[cells], cell_n[cells], cell_scale[cells])
         # ridge_plan orders cells big-first and numbers outputs 0..: map to global rows
         rp["desc"]["out"] = cells[rp["desc"]["out"] // (L * P)].astype(np.int64) * L * P
         qp = quad_plan(P, L, P, job_cell[jobs], job_month[jobs], job_n[jobs], job_out=jobs)
-        groups.append((cells, jobs, rp, qp))
+        groups.append((cells, jobs, rp, qp, gmode))
         arrays += [rp["desc"], qp["desc"], qp["tile_job"]]
     dv = upload(arrays, dev)                     # all descriptors, one async copy
     plan = {"groups": groups, "dv": dv}
@@ -372,23 +393,23 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     lv = lvec.to(device=dev, dtype=torch.float64).contiguous()
     cur = torch.cuda.current_stream(dev)
     dv = plan["dv"]
-    streams = [cur]
-    if split:
-        side = _side_stream(dev)
-        side.wait_stream(cur)
-        streams = [side, cur]                    # big cells' factorisations issued first
+    ng = len(plan["groups"])
+    # big cells' factorisations issued first, on side streams; the small cells on `cur`
+    streams = [_side_stream(dev, k) for k in range(ng - 1)] + [cur]
+    for st in streams[:-1]:
+        st.wait_stream(cur)
     counts = []
     for gi, stream in enumerate(streams):
-        _, _, rp, qp = plan["groups"][gi]
+        _, _, rp, qp, gmode = plan["groups"][gi]
         with torch.cuda.stream(stream):
-            ridge_launch(rp, dv[3 * gi], SD, Sr, lv, beta, mode)
+            ridge_launch(rp, dv[3 * gi], SD, Sr, lv, beta, mode if gmode is None else gmode)
             counts.append(repair_launch(rp, dv[3 * gi], SD, Sr, lv, beta))
             quad_launch(qp, dv[3 * gi + 1], dv[3 * gi + 2], D, R, beta, obj)
     th("launch")
-    if split:
-        cur.wait_stream(side)
+    for st in streams[:-1]:
+        cur.wait_stream(st)
         for t in (SD, Sr, D, R, lv, beta, obj, *counts):
-            t.record_stream(side)
+            t.record_stream(st)
     LAST_REPAIRS[:] = counts
     return beta, obj
 

@@ -246,6 +246,36 @@ def test_band_reduction_modes(gpu, mode, monkeypatch):
     assert rel < 1e-8, rel
 
 
+@pytest.mark.parametrize("hybrid", ["0", "3"])
+def test_ridge_utilities_stream_groups(gpu, hybrid, monkeypatch):
+    """ridge_utilities with the big cells split over streams (single-workgroup group, and with
+    PFML_BAND_HYBRID=3 three big cells in a multi-workgroup group on a third stream) gives the
+    CPU oracle's betas and utilities."""
+    from pfml.ops.ridge import ridge_utilities
+    monkeypatch.setenv("PFML_BAND_MODE", "")
+    monkeypatch.setenv("PFML_BAND_HYBRID", hybrid)
+    monkeypatch.setattr("pfml.ops.ridge.BAND_MULTI_MAX_CELLS", 2)   # force the split form
+    P = 513
+    SD = _spd_stack(3, P, n_obs=700, seed=65)
+    Sr = _rand(3, P, seed=66)
+    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
+    src = np.array([0, 1, 2, 1, 0, 2, 2, 0])
+    nn = np.array([513, 513, 65, 257, 513, 129, 513, 65])
+    sc = np.full(len(src), 1.5e-3)
+    D = _spd_stack(4, P, n_obs=600, seed=67) * 1e-3
+    R = _rand(4, P, seed=68)
+    jc = np.repeat(np.arange(len(src)), 2)
+    jm = np.tile(np.array([1, 3]), len(src))
+    jn = nn[jc]
+    rb, ro = ridge_utilities(SD, Sr, src, nn, sc, lv, D, R, jc, jm, jn)
+    gb, go = ridge_utilities(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu), D.to(gpu),
+                             R.to(gpu), jc, jm, jn)
+    torch.cuda.synchronize()
+    rel = ((gb.cpu() - rb).norm(dim=-1) / rb.norm(dim=-1).clamp(min=1e-300)).max().item()
+    assert rel < 1e-8, rel
+    assert torch.allclose(go.cpu(), ro, rtol=1e-8, atol=1e-12 * ro.abs().max().item())
+
+
 @pytest.mark.parametrize("qr", ["cqr", "householder"])
 @pytest.mark.parametrize("mode", ["single", "multi"])
 @pytest.mark.parametrize("n_obs", [700, 90])
