@@ -430,6 +430,18 @@ extern "C" hipError_t pfml_spd_blockinv(const double* A, int64_t lda, int64_t sA
   return hipGetLastError();
 }
 
+// Inverse of the nb x nb (nb <= 64) diagonal block at (k0, k0) of A written to the block at
+// (k0, k0) of P (any leading dims / batch strides; P == A: in place).
+extern "C" hipError_t pfml_spd_leafinv_to(const double* A, int64_t lda, int64_t sA, double* P,
+                                          int64_t ldp, int64_t sP, int batch, int k0, int nb,
+                                          int* status, hipStream_t st) {
+  if (batch <= 0 || nb <= 0) return hipSuccess;
+  if (nb > NBL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(spd_leafinv_kernel, dim3(batch), dim3(256), 0, st, A, lda, sA, k0, nb,
+                     P + (int64_t)k0 * ldp + k0, ldp, sP, status);
+  return hipGetLastError();
+}
+
 // In-place inverse of the nb x nb (nb <= 64) diagonal block at (k0, k0) of each matrix.
 extern "C" hipError_t pfml_spd_leafinv_inplace(double* A, int64_t lda, int64_t sA, int batch,
                                                int k0, int nb, int* status, hipStream_t st) {

@@ -24,6 +24,20 @@ def _eye_like(A: torch.Tensor) -> torch.Tensor:
     return torch.eye(A.shape[-1], dtype=A.dtype, device=A.device).expand_as(A)
 
 
+def spd_inverse_into(A: torch.Tensor, out: torch.Tensor, status: torch.Tensor) -> torch.Tensor:
+    """out = A^-1 for a device batch [B, n, n] of SPD matrices without modifying or copying A
+    (the recursive form reads A and writes only ``out``); other forms copy A into out first.
+    Non-positive pivots are flagged in ``status`` (no host sync)."""
+    import os
+    B, n, _ = A.shape
+    if (nat.is_device(A) and n >= _BLOCKED_MIN_N and A.is_contiguous() and out.is_contiguous()
+            and os.environ.get("PFML_SPD_INV", SPD_INV_DEFAULT) == "recursive"):
+        _spd_inverse_recursive(out, status, src=A)
+        return out
+    out.copy_(A)
+    return spd_inverse(out, inplace=True, status=status)
+
+
 def spd_inverse(A: torch.Tensor, inplace: bool = False,
                 status: torch.Tensor | None = None) -> torch.Tensor:
     """Inverse of a batch [B, n, n] of SPD matrices.
@@ -70,6 +84,9 @@ nat.register_hip("pfml_spd_inverse_sym", [C.c_void_p, C.c_int, C.c_int, C.c_void
 nat.register_hip("pfml_spd_inverse_sym_work_doubles", [C.c_int, C.c_int], C.c_int64)
 nat.register_hip("pfml_spd_leafinv_inplace", [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int,
                                               C.c_int, C.c_void_p, C.c_void_p])
+nat.register_hip("pfml_spd_leafinv_to", [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
+                                         C.c_int64, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                         C.c_void_p])
 
 SPD_INV_DEFAULT = "recursive"
 _REC_LEAF = 64
@@ -81,8 +98,10 @@ def _rec_split(n: int) -> int:
     return _REC_LEAF * ((n + 2 * _REC_LEAF - 1) // (2 * _REC_LEAF))
 
 
-def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor) -> None:
-    """In-place SPD inverse by recursive 2 x 2 Schur-complement blocks:
+def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor,
+                           src: torch.Tensor | None = None) -> None:
+    """SPD inverse by recursive 2 x 2 Schur-complement blocks, into X (from ``src`` when given:
+    the source is only read, so no copy of it is made; else in place):
 
         X11 = A11^-1 (recursive),  W = X11 A12,  S = A22 - A21 W,  X22 = S^-1 (recursive),
         X12 = -W X22,  X21 = -X22 W',  X11 -= X12 W'
@@ -90,7 +109,7 @@ def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor) -> None:
     Every product is one fused-GEMM launch whose inner dimension is the block size
     (256 / 128 / 64 on the m_func shape) instead of the rank-64 updates of the Gauss-Jordan
     form, so the pass is MFMA-bound rather than a bandwidth-bound sweep over the whole matrix
-    per 64 columns; the 64 x 64 leaves are the register-resident leaf kernel, in place
+    per 64 columns; the 64 x 64 leaves are the register-resident leaf kernel
     (csrc/spd_inverse.hip).  Schur complements of an SPD matrix are SPD, so no pivoting; a
     non-positive leaf pivot flags ``status`` like the other forms.  One W buffer per depth
     (the parent's W lives across the child's recursion)."""
@@ -107,20 +126,24 @@ def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor) -> None:
             _REC_BUFS[key] = w
         return w[:B * h * m].view(B, h, m)
 
-    def rec(r0, nn, depth):
+    def rec(r0, nn, depth, A):
         if nn <= _REC_LEAF:
-            nat.check(lib.pfml_spd_leafinv_inplace(X.data_ptr(), ld, sX, B, r0, nn,
-                                                   status.data_ptr(), st),
-                      "pfml_spd_leafinv_inplace")
+            nat.check(lib.pfml_spd_leafinv_to(A.data_ptr(), A.stride(1), A.stride(0),
+                                              X.data_ptr(), ld, sX, B, r0, nn,
+                                              status.data_ptr(), st), "pfml_spd_leafinv_to")
             return
         h = _rec_split(nn)
         m = nn - h
         a, c, e = r0, r0 + h, r0 + nn
-        rec(a, h, depth + 1)
+        rec(a, h, depth + 1, A)
         W = buf(depth, h, m)
-        gemm_fused(X[:, a:c, a:c], X[:, a:c, c:e], W)                        # W = X11 A12
-        gemm_fused(X[:, c:e, a:c], W, X[:, c:e, c:e], alpha=-1.0, beta=1.0)  # S
-        rec(c, m, depth + 1)
+        gemm_fused(X[:, a:c, a:c], A[:, a:c, c:e], W)                        # W = X11 A12
+        if A is X:
+            gemm_fused(X[:, c:e, a:c], W, X[:, c:e, c:e], alpha=-1.0, beta=1.0)  # S
+        else:
+            gemm_fused(A[:, c:e, a:c], W, X[:, c:e, c:e], alpha=-1.0,
+                       addend=A[:, c:e, c:e], addend_cols=m)                  # S = A22 - A21 W
+        rec(c, m, depth + 1, X)
         gemm_fused(W, X[:, c:e, c:e], X[:, a:c, c:e], alpha=-1.0)            # X12
         # X21 = -X22 W' as its own product, not X12^T: the two carry independent rounding,
         # and the Denman-Beavers iterate Y M^-1 (which sees both triangles) measured 20x
@@ -129,7 +152,7 @@ def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor) -> None:
         gemm_fused(X[:, a:c, c:e], W, X[:, a:c, a:c], trans_b=True, alpha=-1.0,
                    beta=1.0)                                                  # X11 -= X12 W'
 
-    rec(0, n, 0)
+    rec(0, n, 0, X if src is None else src)
 
 
 def _spd_inverse_blocked(X: torch.Tensor, status: torch.Tensor) -> None:
@@ -372,8 +395,7 @@ def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tenso
     Y.copy_(S)
     mu = torch.empty(B, dtype=S.dtype, device=S.device)
     for it in range(iters):
-        Mi.copy_(M)
-        spd_inverse(Mi, inplace=True, status=status)
+        spd_inverse_into(M, Mi, status)
         _db_mu(M, Mi, it >= scaled_iters, mu)
         # Y' = (mu/2) Y + (1/(2 mu)) Y M^-1 ;  M' = I/2 + (mu^2 M + mu^-2 M^-1)/4
         rs = (0.5 / mu).view(B, 1).expand(B, N).contiguous()
