@@ -280,8 +280,10 @@ BAND_SINGLE, BAND_MULTI = 1, 2
 BAND_MULTI_MAX_CELLS = 64
 # Hybrid (one GPU holds the whole grid): this many of the largest-n cells take the
 # multi-workgroup reduction on a third stream while the rest keep one workgroup per cell, so
-# the CUs the single-workgroup cells leave idle also work on big cells.  PFML_BAND_HYBRID
-# overrides (0 = off).
+# the CUs the single-workgroup cells leave idle also work on big cells.  Measured on MI355X
+# (profiles/r02_band_hybrid_ab.json): 16 / 32 / 48 hybrid cells give 7.05 / 7.54 / 7.59 ms
+# per grid step against 6.59 ms with none - the multi-workgroup cells' three launches per panel
+# contend with the one-workgroup cells - so it is off.  PFML_BAND_HYBRID overrides.
 BAND_HYBRID_CELLS = 0
 
 
