@@ -114,6 +114,29 @@ def engine_setup(cfg: Config, env, n_stocks: int, precision: str = "fp64"):
     return (plan, months), (chars, barra, wealth, rf)
 
 
+def graphed(fn, dev):
+    """Capture one step into a HIP graph (torch.cuda.graph -> hipStreamBeginCapture; the side
+    streams of the ridge grid join the capture through their event waits).  Returns the replay
+    function - every kernel of the step runs on each replay, only the host-side launch work is
+    gone - or None when the step cannot be captured."""
+    try:
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            fn()                                   # plans, allocator state, code objects
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn()
+        torch.cuda.synchronize(dev)
+        return g.replay
+    except Exception as e:                         # noqa: BLE001 - fall back to eager launches
+        print(f"[bench] graph capture failed, eager launches: {type(e).__name__}: {e}",
+              file=sys.stderr)
+        return None
+
+
 def timed(fn, steps: int, warmup: int, dev) -> float:
     """ms per step: W untimed steps, then K steps bracketed by barrier + synchronize, max over
     ranks."""
@@ -239,6 +262,9 @@ def main():
     ap.add_argument("--months", type=int, default=710)
     ap.add_argument("--device", default="auto")
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
+                    help="replay the step as a captured HIP graph (one rank, grid step without "
+                         "S4; falls back to eager launches if the capture fails)")
     ap.add_argument("--with-inputs", action="store_true",
                     help="time S4 (PFML input construction for every month) + S5 + S6 as the step")
     ap.add_argument("--rank-deficient", type=int, default=0, metavar="NT",
@@ -294,7 +320,14 @@ def main():
     def step():
         box["res"], box["scores"] = one_step(reals, cfg, engine)
 
-    ms = timed(step, args.steps, args.warmup, dev)
+    use_graph = False
+    if args.graph and dev.type == "cuda" and not env.is_dist and engine is None:
+        rep = graphed(step, dev)
+        if rep is not None:
+            use_graph = True
+            ms = timed(rep, args.steps, args.warmup, dev)
+    if not use_graph:
+        ms = timed(step, args.steps, args.warmup, dev)
     res = box["res"]
     value = n_solves / (ms / 1000.0)
     # sanity: finite outputs; device repairs (non-SPD ridge systems) of the last step
@@ -367,6 +400,7 @@ def main():
                 "ridge_solve_dtype": "fp64 (lambda = 0 / rank-deficient systems: bf16 cannot "
                                      "carry them, SURVEY 7.4)",
                 "rank_deficient_nt": args.rank_deficient or None,
+                "hip_graph": use_graph,
             },
             "repairs": repairs,
             "fallbacks": COUNTERS.as_dict(),

@@ -338,7 +338,8 @@ def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell,
         hy = big & (np.cumsum(big) <= nhy)
         parts = ((big & ~hy, BAND_SINGLE), (hy, BAND_MULTI), (~big, BAND_SINGLE))
     elif split:
-        parts = ((big, BAND_SINGLE), (~big, BAND_SINGLE))
+        # big cells in the launch's mode; the small ones always one workgroup per cell
+        parts = ((big, None), (~big, BAND_SINGLE))
     else:
         parts = ((np.ones(len(cell_n), dtype=bool), None),)
     groups, arrays = [], []

@@ -175,3 +175,33 @@ def test_full_pipeline_gpu(gpu, small_data, tmp_path):
         assert list(df.columns) == CSV_COLUMNS[name]
     s = pd.read_csv(os.path.join(cfg.run.data_dir, "pf_summary.csv"))
     assert np.isfinite(s[["r", "sd", "sr", "obj"]].to_numpy()).all()
+
+
+def test_grid_step_hip_graph_replay_matches_eager(gpu):
+    """bench.py --graph: the grid step captured as a HIP graph (side streams joined through
+    event waits) replays to exactly the eager step's utilities and scores."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    from pfml.config import Config
+    from pfml.parallel import dist as pdist
+    pdist.set_env(None)
+    cfg = Config.default().override(bench.TINY + ["pf_ml.p_vec=[8,16,64]"])
+    reals = bench.synthetic_reals(cfg, gpu, n_months=180, n_stocks=40, seed=3)
+    res_e, sc_e = bench.one_step(reals, cfg)
+    ref_obj = res_e.obj.clone()
+    ref_rank = [s[2].clone() for s in sc_e]
+    box = {}
+
+    def step():
+        box["res"], box["sc"] = bench.one_step(reals, cfg)
+
+    rep = bench.graphed(step, gpu)
+    assert rep is not None
+    box["res"].obj.zero_()
+    rep()
+    torch.cuda.synchronize()
+    assert torch.equal(box["res"].obj, ref_obj)
+    for s, r in zip(box["sc"], ref_rank):
+        assert torch.equal(torch.nan_to_num(s[2], nan=-1.0), torch.nan_to_num(r, nan=-1.0))

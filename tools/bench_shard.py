@@ -3,7 +3,8 @@
 W-rank run (its hp-year shard; collectives are no-ops) and report the slowest rank per W.
 
 This is the compute part of `bench.py --gpus W` (the driver runs the real multi-GPU bench);
-it shows whether the per-rank work shrinks as 1/W or hits a latency floor."""
+it shows whether the per-rank work shrinks as 1/W or hits a latency floor.  PFML_SHARD_GRAPH=1
+replays each rank's step as a captured HIP graph."""
 import json
 import os
 import sys
@@ -29,11 +30,14 @@ def main():
         per_rank = []
         for r in (only if only is not None else range(W)):
             pdist.set_env(pdist.DistEnv(rank=r, world_size=W, device=dev))
-            bench.one_step(reals, cfg)
+            fn = lambda: bench.one_step(reals, cfg)                 # noqa: E731
+            if os.environ.get("PFML_SHARD_GRAPH"):                  # per-rank HIP graph replay
+                fn = bench.graphed(fn, dev) or fn
+            fn()
             torch.cuda.synchronize()
             t = time.perf_counter()
             for _ in range(steps):
-                bench.one_step(reals, cfg)
+                fn()
             torch.cuda.synchronize()
             per_rank.append(1e3 * (time.perf_counter() - t) / steps)
         out[f"w{W}_max_ms"] = round(max(per_rank), 3)
