@@ -13,10 +13,22 @@
 // partial; a second tiny kernel sums the partials in a fixed order (bitwise reproducible, no
 // float atomics).
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
-constexpr int BM = 64, BK = 16, NCOL = 112, NTILE = NCOL / 16;
+constexpr int BK = 16, NCOL = 112, NTILE = NCOL / 16;
+// Row tile: 64 rows / 4 waves (default) or 128 rows / 8 waves (PFML_QUAD_ROWS=128: every beta
+// tile staged in LDS feeds twice the MFMAs, half the workgroups and prologues).  Measured on
+// the headline step: 6.64 ms (64) vs 6.76 ms (128) - the longer triangular K loops of the
+// 128-row tiles cost more than the shared beta staging saves - so 64 stays the default.
+int quad_rows() {
+  static int r = [] {
+    const char* e = getenv("PFML_QUAD_ROWS");
+    return (e && atoi(e) == 128) ? 128 : 64;
+  }();
+  return r;
+}
 // Both operands are staged k-contiguous, as they sit in HBM ([row][k] for D, [lambda][k] for
 // beta), with a row stride of BK + 2 = 18 doubles: the coalesced global rows are stored
 // without bank conflicts, and a fragment read (16 rows x 2 k per 32-lane group) hits 32
@@ -32,13 +44,16 @@ struct JobDesc {
   int ptile0;        // first partial slot of this job
 };
 
-__global__ __launch_bounds__(256) void quadform_kernel(
+template <int BM>
+__global__ __launch_bounds__(BM * 4) void quadform_kernel(
     const double* __restrict__ D, int64_t ldD, const double* __restrict__ R,
     const double* __restrict__ Bt, int64_t ldB, const JobDesc* __restrict__ jobs,
     const int* __restrict__ tile_job, int L, double* __restrict__ partial) {
+  constexpr int NT = BM * 4;                      // threads: one wave per 16 rows
+  constexpr int NW = NT / 64;
   __shared__ double As[2][BM][KS];
   __shared__ double Bs[2][NCOL][KS];
-  __shared__ double red[4][NCOL];
+  __shared__ double red[NW][NCOL];
 
   const int tile = blockIdx.x;
   const int j = tile_job[tile];
@@ -59,8 +74,8 @@ __global__ __launch_bounds__(256) void quadform_kernel(
   // walks K >= I, with the diagonal block weighted 1/2, so  acc = U_I / 2  and half the
   // flops and D bytes of the full product are spent.  K tiles are double-buffered in LDS
   // and prefetched two steps ahead through registers (one barrier per K step).
-  constexpr int AQ = (BM * BK) / 256;             // D elements per thread per K step
-  constexpr int BQ = (NCOL * BK + 255) / 256;     // beta elements per thread per K step
+  constexpr int AQ = (BM * BK) / NT;              // D elements per thread per K step
+  constexpr int BQ = (NCOL * BK + NT - 1) / NT;   // beta elements per thread per K step
   // two register sets: the global loads of step k+2 are in flight while step k is computed
   // from LDS and step k+1 is written to the other LDS buffer (prefetch distance 2).
   double ra0[AQ], rb0[BQ], ra1[AQ], rb1[BQ];
@@ -70,12 +85,12 @@ __global__ __launch_bounds__(256) void quadform_kernel(
   auto gload = [&](int k0, double (&ra)[AQ], double (&rb)[BQ]) {
 #pragma unroll
     for (int q = 0; q < AQ; ++q) {
-      const int e = t + q * 256, i = e / BK, k = e % BK;
+      const int e = t + q * NT, i = e / BK, k = e % BK;
       ra[q] = Dm[(int64_t)min(i0 + i, n - 1) * ldD + min(k0 + k, n - 1)];
     }
 #pragma unroll
     for (int q = 0; q < BQ; ++q) {
-      const int e = min(t + q * 256, NCOL * BK - 1), l = e / BK, k = e % BK;
+      const int e = min(t + q * NT, NCOL * BK - 1), l = e / BK, k = e % BK;
       rb[q] = bt[(int64_t)min(l, L - 1) * ldB + min(k0 + k, n - 1)];
     }
   };
@@ -83,12 +98,12 @@ __global__ __launch_bounds__(256) void quadform_kernel(
     const double wdiag = (k0 < i0 + BM) ? 0.5 : 1.0;
 #pragma unroll
     for (int q = 0; q < AQ; ++q) {
-      const int e = t + q * 256, i = e / BK, k = e % BK;
+      const int e = t + q * NT, i = e / BK, k = e % BK;
       As[buf][i][k] = (i0 + i < n && k0 + k < n) ? wdiag * ra[q] : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < BQ; ++q) {
-      const int e = t + q * 256, l = e / BK, k = e % BK;
+      const int e = t + q * NT, l = e / BK, k = e % BK;
       if (e < NCOL * BK) Bs[buf][l][k] = (l < L && k0 + k < n) ? rb[q] : 0.0;
     }
   };
@@ -140,14 +155,16 @@ __global__ __launch_bounds__(256) void quadform_kernel(
   }
   __syncthreads();
   if (t < NCOL) {
-    const double s = red[0][t] + red[1][t] + red[2][t] + red[3][t];
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) s += red[q][t];
     if (t < L) partial[(int64_t)tile * L + t] = s;
   }
 }
 
 __global__ void quadform_reduce_kernel(const double* __restrict__ partial,
                                        const JobDesc* __restrict__ jobs, int njobs, int L,
-                                       double* __restrict__ obj) {
+                                       int BM, double* __restrict__ obj) {
   const int j = blockIdx.x;
   const int l = threadIdx.x;
   if (j >= njobs || l >= L) return;
@@ -161,7 +178,7 @@ __global__ void quadform_reduce_kernel(const double* __restrict__ partial,
 }  // namespace
 
 extern "C" int pfml_quadform_job_desc_size() { return (int)sizeof(JobDesc); }
-extern "C" int pfml_quadform_rows_per_tile() { return BM; }
+extern "C" int pfml_quadform_rows_per_tile() { return quad_rows(); }
 
 extern "C" hipError_t pfml_quadform(const double* D, int64_t ldD, const double* R,
                                     const double* Bt, int64_t ldB, const void* jobs, int njobs,
@@ -169,9 +186,14 @@ extern "C" hipError_t pfml_quadform(const double* D, int64_t ldD, const double* 
                                     double* obj, hipStream_t st) {
   if (njobs <= 0) return hipSuccess;
   if (L > NCOL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(quadform_kernel, dim3(ntiles), dim3(256), 0, st, D, ldD, R, Bt, ldB,
-                     static_cast<const JobDesc*>(jobs), tile_job, L, partial);
+  const int bm = quad_rows();
+  if (bm == 128)
+    hipLaunchKernelGGL(quadform_kernel<128>, dim3(ntiles), dim3(512), 0, st, D, ldD, R, Bt, ldB,
+                       static_cast<const JobDesc*>(jobs), tile_job, L, partial);
+  else
+    hipLaunchKernelGGL(quadform_kernel<64>, dim3(ntiles), dim3(256), 0, st, D, ldD, R, Bt, ldB,
+                       static_cast<const JobDesc*>(jobs), tile_job, L, partial);
   hipLaunchKernelGGL(quadform_reduce_kernel, dim3(njobs), dim3(128), 0, st, partial,
-                     static_cast<const JobDesc*>(jobs), njobs, L, obj);
+                     static_cast<const JobDesc*>(jobs), njobs, L, bm, obj);
   return hipGetLastError();
 }
