@@ -174,6 +174,7 @@ class RunOptions:
     artifact_dir: str = "artifacts"
     check: bool = False                # compare device results against the CPU oracle
     profile: bool = False              # emit roctx ranges + stage timing JSONL
+    plots: bool = True                 # the reference's figures as PNGs under <data_dir>/plots
     fault_inject: str = ""             # e.g. "s4:shard=1" to poison a shard (tests recovery)
     synthetic: dict = field(default_factory=lambda: {
         "n_stocks": 500, "n_features": 115, "start": "1952-01-31", "end": "2023-12-31",

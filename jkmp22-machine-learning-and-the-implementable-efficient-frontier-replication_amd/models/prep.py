@@ -10,6 +10,8 @@ percentile ranks run in the native host runtime (runtime/panel.cpp).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import pandas as pd
 
@@ -311,6 +313,8 @@ def prepare_data(cfg: Config, write: bool = True) -> dict:
     vpct = round(chars["valid"].mean() * 100, 2)
     mpct = round(chars.loc[chars["valid"], "me"].sum() / chars["me"].sum() * 100, 2)
     log.info(f"   The valid_data subset has {vpct}% of the observations and {mpct}% of the market cap")
+    if cfg.run.plots and write:
+        universe_plot(chars, os.path.join(dd, "plots"))
 
     if write:
         io.write_csv(wealth, dd, "wealth_processed.csv")
@@ -320,3 +324,35 @@ def prepare_data(cfg: Config, write: bool = True) -> dict:
         out["eom_ret"] = out["eom_ret"].dt.strftime("%Y-%m-%d")
         io.sql_write(io.path(dd, "JKP_US_SP500.db"), "Factors_processed", out)
     return {"chars": chars, "wealth": wealth, "cluster_labels": labels}
+
+
+def universe_counts(chars: pd.DataFrame) -> pd.DataFrame:
+    """Valid stocks per month (Prepare_Data.py:459-462)."""
+    v = chars.loc[chars["valid"].astype(bool)]
+    return v.groupby("eom").size().reset_index(name="N")
+
+
+def universe_plot(chars: pd.DataFrame, out_dir: str) -> list[str]:
+    """The investable-universe figure of Prepare_Data.py:464-471 (valid stocks per eom, a
+    scatter with a zero line) as a PNG, plus its data as universe_counts.csv."""
+    os.makedirs(out_dir, exist_ok=True)
+    vc = universe_counts(chars)
+    f0 = os.path.join(out_dir, "universe_counts.csv")
+    vc.assign(eom=pd.to_datetime(vc["eom"]).dt.strftime("%Y-%m-%d")).to_csv(f0, index=False)
+    try:
+        import matplotlib
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+    except ImportError:
+        log.info("matplotlib not available: universe plot skipped")
+        return [f0]
+    fig = plt.figure(figsize=(10, 6))
+    plt.scatter(pd.to_datetime(vc["eom"]), vc["N"])
+    plt.xlabel("eom")
+    plt.ylabel("Valid stocks")
+    plt.axhline(y=0, color="grey", linestyle="--")
+    plt.title("Investable Universe Over Time")
+    f1 = os.path.join(out_dir, "investable_universe.png")
+    fig.savefig(f1, dpi=100)
+    plt.close(fig)
+    return [f0, f1]

@@ -346,7 +346,7 @@ class Pipeline:
         summ = portfolio.pf_summary(pf, float(self.cfg.pf_set["gamma_rel"]))
         io.write_csv(summ, d, "pf_summary.csv")
         st.update(best_hps=best, best_hps_list=chosen, weights=w, pf=pf, pf_summary=summ)
-        if self.cfg.run.profile:
+        if self.cfg.run.plots:
             portfolio.plots(pf, best, float(self.cfg.pf_set["gamma_rel"]),
                             os.path.join(d, "plots"))
         log.info("pf_summary:\n" + summ.to_string(index=False))

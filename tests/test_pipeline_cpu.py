@@ -260,3 +260,17 @@ def test_estimate_cov_batched_matches_pandas_form(small_data):
     # (atol relative to the scale: a stock whose residuals are rounding noise has ivol ~1e-31)
     assert np.allclose(a.F, b.F, rtol=1e-10, atol=1e-12 * np.abs(b.F).max())
     assert np.allclose(a.ivol, b.ivol, rtol=1e-10, atol=1e-10 * np.abs(b.ivol).max())
+
+
+def test_universe_plot_and_counts(small_data):
+    """Prepare_Data.py:459-477: the investable-universe figure and its per-month valid counts
+    are written next to the processed data."""
+    from pfml.data import io
+    from pfml.config import get_features
+    d = os.path.join(small_data.run.data_dir, "plots")
+    assert os.path.exists(os.path.join(d, "investable_universe.png"))
+    vc = pd.read_csv(os.path.join(d, "universe_counts.csv"))
+    chars = io.read_processed_chars(small_data.run.data_dir, get_features())
+    ref = chars.loc[chars["valid"].astype(bool)].groupby("eom").size()
+    assert vc["N"].tolist() == ref.tolist()
+    assert vc["N"].sum() == int(chars["valid"].sum())
