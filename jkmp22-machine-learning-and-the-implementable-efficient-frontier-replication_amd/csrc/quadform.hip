@@ -8,8 +8,8 @@
 // on fp64 MFMA (upper block triangle only: D_t is symmetric) and folds the two reductions
 // into the epilogue, so U never leaves registers.
 //
-// Tile: 64 rows of D x 112 lambda columns (L <= 112) per 256-thread workgroup; each wave owns
-// 16 rows x 7 MFMA 16x16 accumulators.  Every workgroup writes a deterministic per-row-tile
+// Tile: 64 rows of D x 112 lambda columns (L <= 112) per 256-thread workgroup (3 per CU); each
+// wave owns 16 rows x 7 MFMA 16x16 accumulators.  Every workgroup writes a deterministic per-row-tile
 // partial; a second tiny kernel sums the partials in a fixed order (bitwise reproducible, no
 // float atomics).
 #include "common.h"
@@ -29,6 +29,10 @@ int quad_rows() {
   }();
   return r;
 }
+int quad_pf() {
+  const char* e = getenv("PFML_QUAD_PF");
+  return (e && atoi(e) == 2) ? 2 : 1;
+}
 // Both operands are staged k-contiguous, as they sit in HBM ([row][k] for D, [lambda][k] for
 // beta), with a row stride of BK + 2 = 18 doubles: the coalesced global rows are stored
 // without bank conflicts, and a fragment read (16 rows x 2 k per 32-lane group) hits 32
@@ -44,8 +48,15 @@ struct JobDesc {
   int ptile0;        // first partial slot of this job
 };
 
-template <int BM>
-__global__ __launch_bounds__(BM * 4) void quadform_kernel(
+// PF: global->register prefetch distance.  PF = 1 (default): one register set and the
+// epilogue's cross-wave sums in the A staging buffer, so the kernel fits 3 workgroups per CU
+// (155 VGPRs, 51.6 KB LDS) and the other workgroups hide the shorter prefetch.  PF = 2
+// (PFML_QUAD_PF=2): two register sets, the loads of step k+2 in flight while step k computes,
+// 222 VGPRs + AGPRs, 2 workgroups per CU.  Measured (tools/bench_quad.py, n = 513 jobs of the
+// headline step): 1.20 ms (PF 1) vs 1.33 ms (PF 2); headline step 6.37-6.49 vs 6.52-6.60 ms
+// (profiles/r02_quad_pf_ab.json).
+template <int BM, int PF>
+__global__ __launch_bounds__(BM * 4, PF == 1 ? 3 : 1) void quadform_kernel(
     const double* __restrict__ D, int64_t ldD, const double* __restrict__ R,
     const double* __restrict__ Bt, int64_t ldB, const JobDesc* __restrict__ jobs,
     const int* __restrict__ tile_job, int L, double* __restrict__ partial) {
@@ -53,7 +64,9 @@ __global__ __launch_bounds__(BM * 4) void quadform_kernel(
   constexpr int NW = NT / 64;
   __shared__ double As[2][BM][KS];
   __shared__ double Bs[2][NCOL][KS];
-  __shared__ double red[NW][NCOL];
+  __shared__ double red_own[PF == 1 ? 1 : NW][NCOL];
+  static_assert(NW * NCOL <= 2 * BM * KS, "cross-wave sums must fit in the A buffers");
+  double (*red)[NCOL] = PF == 1 ? reinterpret_cast<double (*)[NCOL]>(&As[0][0][0]) : red_own;
 
   const int tile = blockIdx.x;
   const int j = tile_job[tile];
@@ -116,6 +129,23 @@ __global__ __launch_bounds__(BM * 4) void quadform_kernel(
         acc[q] = mfma_f64_16x16x4(a, Bs[buf][q * 16 + (lane & 15)][kk + (lane >> 4)], acc[q]);
     }
   };
+  if constexpr (PF == 1) {
+    gload(i0, ra0, rb0);
+    sstore(0, i0, ra0, rb0);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = i0;;) {
+      const bool more = k0 + BK < n;
+      if (more) gload(k0 + BK, ra0, rb0);
+      compute(buf);
+      if (!more) break;
+      sstore(buf ^ 1, k0 + BK, ra0, rb0);
+      __syncthreads();
+      k0 += BK;
+      buf ^= 1;
+    }
+    __syncthreads();                          // red reuses As
+  } else {
   gload(i0, ra0, rb0);
   sstore(0, i0, ra0, rb0);
   if (i0 + BK < n) gload(i0 + BK, ra1, rb1);
@@ -133,6 +163,7 @@ __global__ __launch_bounds__(BM * 4) void quadform_kernel(
     sstore(0, k0 + BK, ra0, rb0);
     __syncthreads();
     k0 += BK;
+  }
   }
 
   // epilogue: sum over this wave's 16 rows of  beta_l[i] * (r_i - 1/2 U[i][l])
@@ -188,11 +219,14 @@ extern "C" hipError_t pfml_quadform(const double* D, int64_t ldD, const double* 
   if (L > NCOL) return hipErrorInvalidValue;
   const int bm = quad_rows();
   if (bm == 128)
-    hipLaunchKernelGGL(quadform_kernel<128>, dim3(ntiles), dim3(512), 0, st, D, ldD, R, Bt, ldB,
-                       static_cast<const JobDesc*>(jobs), tile_job, L, partial);
+    hipLaunchKernelGGL((quadform_kernel<128, 2>), dim3(ntiles), dim3(512), 0, st, D, ldD, R, Bt,
+                       ldB, static_cast<const JobDesc*>(jobs), tile_job, L, partial);
+  else if (quad_pf() == 1)
+    hipLaunchKernelGGL((quadform_kernel<64, 1>), dim3(ntiles), dim3(256), 0, st, D, ldD, R, Bt,
+                       ldB, static_cast<const JobDesc*>(jobs), tile_job, L, partial);
   else
-    hipLaunchKernelGGL(quadform_kernel<64>, dim3(ntiles), dim3(256), 0, st, D, ldD, R, Bt, ldB,
-                       static_cast<const JobDesc*>(jobs), tile_job, L, partial);
+    hipLaunchKernelGGL((quadform_kernel<64, 2>), dim3(ntiles), dim3(256), 0, st, D, ldD, R, Bt,
+                       ldB, static_cast<const JobDesc*>(jobs), tile_job, L, partial);
   hipLaunchKernelGGL(quadform_reduce_kernel, dim3(njobs), dim3(128), 0, st, partial,
                      static_cast<const JobDesc*>(jobs), njobs, L, bm, obj);
   return hipGetLastError();
