@@ -1080,12 +1080,17 @@ __global__ __launch_bounds__(256) void band_mk_extract_kernel(
 // Lane p of a row holds the band row r (r = p mod 16) of the 16-row window j+1..j+16 (the
 // retiring pivot lane takes row j+16 in the same step), columns j..j+16 in 17 registers
 // (slot k <-> column j+k, shifted one slot per step).  Every cross-lane value is a
-// row_newbcast DPP move (no LDS), so a step is ~60 VALU ops and 4 independent solves share
-// each instruction.  Slots right of a row's diagonal hold garbage that is never read.
+// row_newbcast DPP move, and 4 independent solves share each instruction.  The entering rows
+// (the same for the workgroup's 16 lambdas) are staged in LDS one block ahead and read by the
+// pivot lane straight into its window (exec-masked ds_reads in flight during the pivot's rsq
+// chain; measured 543 / 860 us vs 593 / 928 us for the big / small cells of the headline step
+// with a 17-register row prefetch and VALU moves).  Slots right of a row's diagonal hold
+// garbage that is never read.
 // ---------------------------------------------------------------------------------------
 constexpr int NTS = 256;      // 4 waves x 4 rows = 16 lambdas per workgroup
 
-__global__ __launch_bounds__(NTS) void ridge_band_solve_kernel(
+// 158 VGPRs: 3 waves per SIMD (the entering rows come from LDS, not a register prefetch).
+__global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
     const RidgeCellDesc* __restrict__ cells, const double* __restrict__ lvec, int L,
     double* __restrict__ work, long long* __restrict__ tim, int ncells) {
   const long long t_start = (long long)__builtin_amdgcn_s_memtime();
@@ -1106,13 +1111,18 @@ __global__ __launch_bounds__(NTS) void ridge_band_solve_kernel(
 
   // w: 32 slots; within a 16-step block at phase u, slot u + k <-> column j + k (k <= 16), so
   // the window never shifts inside a block (one 16-slot move per block).  Rows >= n are
-  // identity rows (band_row), so every block is a full, branch-free 16 steps.
+  // identity rows, so every block is a full, branch-free 16 steps.  The band rows entering
+  // during a block are the same for all 16 lambdas of the workgroup: they are staged in LDS one
+  // block ahead (double buffer, one barrier per block) and each lane reads its row at the
+  // block start, instead of a second 17-register prefetch per lane (occupancy: VGPRs).
+  __shared__ double LBs[2][BB][LS];
   const int npad = (n + 15) & ~15;
-  double w[2 * BB], nx[LS], nx2[LS];
-  auto band_row = [&](int r, double (&dst)[LS]) {
-#pragma unroll
-    for (int s = 0; s < LS; ++s)
-      dst[s] = (r < n) ? LB[(int64_t)r * LS + s] + (s == BB ? lam : 0.0) : (s == BB ? 1.0 : 0.0);
+  double w[2 * BB];
+  auto stage_rows = [&](int r0s, int buf) {       // rows r0s .. r0s + 15 -> LBs[buf]
+    for (int e = threadIdx.x; e < BB * LS; e += NTS) {
+      const int r = r0s + e / LS, s = e % LS;
+      LBs[buf][e / LS][s] = (r < n) ? LB[(int64_t)r * LS + s] : (s == BB ? 1.0 : 0.0);
+    }
   };
   // window at j = 0: lane p holds row p, slot k <-> column k
 #pragma unroll
@@ -1120,27 +1130,33 @@ __global__ __launch_bounds__(NTS) void ridge_band_solve_kernel(
     w[k] = (k <= p && p < n) ? LB[(int64_t)p * LS + BB - p + k] + (k == p ? lam : 0.0)
                              : (k == p ? 1.0 : 0.0);
   double zr = (p < n) ? z[p] : 0.0;
-  band_row(p + BB, nx);                            // taken by lane p at step p
+  stage_rows(BB, 0);                               // block 0's entering rows 16..31
   double znx = (p + BB < n) ? z[p + BB] : 0.0;
   bool ok = true;
+  __syncthreads();
 
   for (int j0 = 0; j0 < npad; j0 += 16) {
-    // rows entering during the NEXT block, one block of latency to land
-    band_row(j0 + 2 * BB + p, nx2);
+    const int sb = (j0 >> 4) & 1;
+    // this block's entering row for lane p (row j0 + 16 + p, taken at step p), then the NEXT
+    // block's rows to the other buffer
+    const double lam_in = (j0 + BB + p < n) ? lam : 0.0;   // diagonal shift of the entering row
+    stage_rows(j0 + 2 * BB, sb ^ 1);
     const double znx2 = (j0 + 2 * BB + p < n) ? z[j0 + 2 * BB + p] : 0.0;
     static_for<0, 16>([&](auto U) {
       constexpr int u = decltype(U)::value;
       const int j = j0 + u;
       const bool pl = (p == u);                  // pivot lane: holds row j, takes row j+16
       const double piv = row_bcast<u>(w[u]);
-      ok = ok && (piv > 0.0);
-      const double inv = rsqrt_f64(piv);
-      const double yj = row_bcast<u>(zr) * inv;
-      if (pl) {                                  // exec-masked 64-bit moves, no selects
-#pragma unroll
-        for (int s = 0; s < LS; ++s) w[u + s] = nx[s];
+      const double zpiv = row_bcast<u>(zr);      // (read before the pivot lane's zr changes)
+      if (pl) {                                  // exec-masked LDS reads straight into the
+#pragma unroll                                   // window (no VALU moves), in flight during
+        for (int s = 0; s < LS; ++s) w[u + s] = LBs[sb][u][s];   // the pivot's rsq chain
+        w[u + BB] += lam_in;
         zr = znx;
       }
+      ok = ok && (piv > 0.0);
+      const double inv = rsqrt_f64(piv);
+      const double yj = zpiv * inv;
       const double lval = w[u] * inv;            // l_i, i = (p - u) mod 16, pivot lane: i = 16
       if (lv && j < n) {                         // uniform branch
         double* lr = Lrow + (int64_t)j * LS;
@@ -1157,20 +1173,21 @@ __global__ __launch_bounds__(NTS) void ridge_band_solve_kernel(
     });
 #pragma unroll
     for (int s = 0; s < BB; ++s) w[s] = w[s + BB];
-#pragma unroll
-    for (int s = 0; s < LS; ++s) nx[s] = nx2[s];
     znx = znx2;
+    __syncthreads();                               // next block's rows staged; this buffer free
   }
   // back substitution L^T x = y, x overwrites y.  Lane (j+i) mod 16 holds x_{j+i}.  The
   // factor columns of a 16-step block are loaded together (one memory latency per block).
   __syncthreads();
   const long long t_mid = (long long)__builtin_amdgcn_s_memtime();
   double xr = 0.0;
-  for (int jt = npad - 1; jt >= 0; jt -= 16) {
-    double pli[16], pinv[16], py[16];
-    static_for<0, 16>([&](auto V) {
+  // (two halves of 8 steps: the loads of a half in flight together, half the registers)
+  for (int jt = npad - 1; jt >= 0; jt -= 8) {
+    double pli[8], pinv[8], py[8];
+    const int uo = (jt & 15) == 15 ? 0 : 8;      // step v of this half: j & 15 = 15 - v - uo
+    static_for<0, 8>([&](auto V) {
       constexpr int v = decltype(V)::value;
-      constexpr int u = 15 - v;                  // j & 15 of step j = jt - v
+      const int u = 15 - v - uo;                 // j & 15 of step j = jt - v
       const int j = jt - v;
       const int i = (p - u) & 15;
       const bool in = j < n;
@@ -1178,19 +1195,19 @@ __global__ __launch_bounds__(NTS) void ridge_band_solve_kernel(
       pinv[v] = in ? Lrow[(int64_t)j * LS] : 1.0;
       py[v] = in ? yl[j] : 0.0;
     });
-    static_for<0, 16>([&](auto V) {
+    static_for<0, 8>([&](auto V) {
       constexpr int v = decltype(V)::value;
-      constexpr int u = 15 - v;
+      const int u = 15 - v - uo;
       const double s = row16_sum(pli[v] * xr);
       const double xj = (py[v] - s) * pinv[v];
       xr = (p == u) ? xj : xr;
       py[v] = xj;
     });
     if (lv) {
-      static_for<0, 16>([&](auto V) {
+      static_for<0, 8>([&](auto V) {
         constexpr int v = decltype(V)::value;
         const int j = jt - v;
-        if (j < n && p == 15 - v) yl[j] = ok ? py[v] : __builtin_nan("");
+        if (j < n && p == 15 - v - uo) yl[j] = ok ? py[v] : __builtin_nan("");
       });
     }
   }
