@@ -9,10 +9,22 @@
 // rows x P columns: demean the RFF columns (not the constant), scale every column to unit
 // L2 norm over the N real rows, then divide each row by its stock's volatility.  One
 // workgroup per (b, theta, 64-column strip); rows read twice (shifted first and second
-// moments in one pass, then the scaled write) and written once.
+// moments in one pass, then the scaled write) and written once, 8 gathered rows in flight per
+// thread in both passes.
 #include "common.h"
 
 namespace {
+
+// blockIdx.y -> (b, theta) tile: tiles are enumerated along the diagonals d = b - theta, so
+// the TH tiles that gather the SAME month's rows (lag theta of month b reads month b - theta)
+// are dispatched together and share those rows through the caches (row-major (b, theta) order
+// re-read every gathered row from HBM once per lag).  Returns -1 for the padding slots of the
+// first / last diagonals.
+__device__ __forceinline__ int diag_tile(int y, int B, int TH) {
+  const int d = y / TH, th = y - d * TH;
+  const int b = d - (TH - 1) + th;
+  return (b < 0 || b >= B) ? -1 : b * TH + th;
+}
 
 __global__ __launch_bounds__(256) void rff_sincos_kernel(const double* __restrict__ Z, int64_t R,
                                                          int half, double* __restrict__ out,
@@ -39,13 +51,15 @@ __global__ __launch_bounds__(256) void rff_sincos_kernel(const double* __restric
 __global__ __launch_bounds__(256) void standardize_kernel(const double* __restrict__ F, int P,
                                                           int64_t ldf,
                                                           const int64_t* __restrict__ rows,
-                                                          const int* __restrict__ n_real, int TH,
-                                                          int N, const double* __restrict__ vol,
+                                                          const int* __restrict__ n_real, int B,
+                                                          int TH, int N,
+                                                          const double* __restrict__ vol,
                                                           double* __restrict__ out, int64_t ldo,
                                                           int64_t so, int Pw) {
   __shared__ double red[4][64], red2[4][64];
   __shared__ double colmean[64], colscale[64];
-  const int bt = blockIdx.y;                  // (b, theta)
+  const int bt = diag_tile(blockIdx.y, B, TH);   // (b, theta)
+  if (bt < 0) return;
   const int b = bt / TH;
   const int c0 = blockIdx.x * 64;
   const int t = threadIdx.x, lane = t & 63, part = t >> 6;   // 4 row partitions
@@ -60,11 +74,13 @@ __global__ __launch_bounds__(256) void standardize_kernel(const double* __restri
   double s1 = 0.0, s2 = 0.0;
   if (c < P) {
     int i = part;
-    for (; i + 12 < n; i += 16) {
-      const double x0 = F[rw[i] * ldf + c] - K, x1 = F[rw[i + 4] * ldf + c] - K;
-      const double x2 = F[rw[i + 8] * ldf + c] - K, x3 = F[rw[i + 12] * ldf + c] - K;
-      s1 += (x0 + x1) + (x2 + x3);
-      s2 += (x0 * x0 + x1 * x1) + (x2 * x2 + x3 * x3);
+    for (; i + 28 < n; i += 32) {
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = F[rw[i + 4 * u] * ldf + c] - K;
+      s1 += ((x[0] + x[1]) + (x[2] + x[3])) + ((x[4] + x[5]) + (x[6] + x[7]));
+      s2 += ((x[0] * x[0] + x[1] * x[1]) + (x[2] * x[2] + x[3] * x[3])) +
+            ((x[4] * x[4] + x[5] * x[5]) + (x[6] * x[6] + x[7] * x[7]));
     }
     for (; i < n; i += 4) {
       const double x = F[rw[i] * ldf + c] - K;
@@ -91,12 +107,96 @@ __global__ __launch_bounds__(256) void standardize_kernel(const double* __restri
   const double mu = colmean[lane];
   const double sc = colscale[lane];
   double* o = out + (int64_t)bt * so;
-  if (c < Pw)
-    for (int i = part; i < N; i += 4) {
-      double v = 0.0;
-      if (i < n && c < P) v = (F[rw[i] * ldf + c] - mu) * sc / vol[rw[i]];
-      o[(int64_t)i * ldo + c] = v;
+  // scaled write: 8 rows per thread per iteration, every load issued before the first use (a
+  // row-at-a-time loop waited on each gathered row's index and value in turn)
+  if (c < Pw) {
+    const int cc = min(c, P - 1);
+    for (int i0 = part; i0 < N; i0 += 32) {
+      int64_t ri[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) ri[u] = rw[min(i0 + 4 * u, N - 1)];
+      double x[8], vv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        x[u] = F[ri[u] * ldf + cc];
+        vv[u] = vol[ri[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + 4 * u;
+        if (i < N) o[(int64_t)i * ldo + c] = (i < n && c < P) ? (x[u] - mu) * sc / vv[u] : 0.0;
+      }
     }
+  }
+}
+
+// Register-resident form for N <= 16 * RPT rows (the S&P 500 universe): 1024 threads per
+// (b, theta, 64-column strip), thread (part = t >> 6, lane) holds rows part + 16 u (u < RPT)
+// of column c0 + lane in registers, so the gathered rows are read from HBM ONCE (the two-pass
+// kernel above reads them twice; the stage is HBM-bound on those gathered reads + the write).
+template <int RPT>
+__global__ __launch_bounds__(1024) void standardize_reg_kernel(
+    const double* __restrict__ F, int P, int64_t ldf, const int64_t* __restrict__ rows,
+    const int* __restrict__ n_real, int B, int TH, int N, const double* __restrict__ vol,
+    double* __restrict__ out, int64_t ldo, int64_t so, int Pw) {
+  constexpr int NP = 16;
+  __shared__ double red[NP][64], red2[NP][64];
+  __shared__ double colmean[64], colscale[64];
+  const int bt = diag_tile(blockIdx.y, B, TH);
+  if (bt < 0) return;
+  const int b = bt / TH;
+  const int c0 = blockIdx.x * 64;
+  const int t = threadIdx.x, lane = t & 63;
+  const int part = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int c = c0 + lane;
+  const int cc = min(c, P - 1);
+  const int n = n_real[b];
+  // row indices are < 2^31: read their low words (halves the scalar registers they take)
+  const int* rw = reinterpret_cast<const int*>(rows + (int64_t)bt * N);
+  const double K = (n > 0) ? F[(int64_t)rw[0] * ldf + cc] : 0.0;
+  double x[RPT];
+#pragma unroll
+  for (int u = 0; u < RPT; ++u) {
+    const int i = part + NP * u;
+    x[u] = (i < n) ? F[(int64_t)rw[2 * i] * ldf + cc] : K;          // rows >= n: x - K = 0
+  }
+  double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+  for (int u = 0; u < RPT; ++u) {
+    const double d = x[u] - K;
+    s1 += d;
+    s2 += d * d;
+  }
+  red[part][lane] = s1;
+  red2[part][lane] = s2;
+  __syncthreads();
+  if (part == 0) {
+    double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      t1 += red[q][lane];
+      t2 += red2[q][lane];
+    }
+    if (c == 0) {                                          // constant column: not demeaned
+      colmean[lane] = 0.0;
+      const double tk = t1 + (double)n * K;
+      colscale[lane] = sqrt(1.0 / (t2 + 2.0 * K * tk - (double)n * K * K));
+    } else {
+      colmean[lane] = K + t1 / (double)n;
+      colscale[lane] = sqrt(1.0 / (t2 - t1 * t1 / (double)n));
+    }
+  }
+  __syncthreads();
+  if (c >= Pw) return;
+  const double mu = colmean[lane];
+  const double sc = colscale[lane];
+  double* o = out + (int64_t)bt * so;
+#pragma unroll
+  for (int u = 0; u < RPT; ++u) {
+    const int i = part + NP * u;
+    if (i < N)
+      o[(int64_t)i * ldo + c] = (i < n && c < P) ? (x[u] - mu) * sc / vol[rw[2 * i]] : 0.0;
+  }
 }
 
 }  // namespace
@@ -117,8 +217,12 @@ extern "C" hipError_t pfml_standardize(const double* F, int P, int64_t ldf, cons
                                        int Pw, hipStream_t st) {
   if (B <= 0 || N <= 0) return hipSuccess;
   if (Pw < P || ldo < Pw || ldf < P) return hipErrorInvalidValue;
-  dim3 grid((Pw + 63) / 64, B * TH);
-  hipLaunchKernelGGL(standardize_kernel, grid, dim3(256), 0, st, F, P, ldf, rows, n_real, TH, N,
-                     vol, out, ldo, so, Pw);
+  dim3 grid((Pw + 63) / 64, (B + TH - 1) * TH);     // diagonal order (diag_tile)
+  if (N <= 16 * 32)
+    hipLaunchKernelGGL(standardize_reg_kernel<32>, grid, dim3(1024), 0, st, F, P, ldf, rows,
+                       n_real, B, TH, N, vol, out, ldo, so, Pw);
+  else
+    hipLaunchKernelGGL(standardize_kernel, grid, dim3(256), 0, st, F, P, ldf, rows, n_real, B, TH,
+                       N, vol, out, ldo, so, Pw);
   return hipGetLastError();
 }
