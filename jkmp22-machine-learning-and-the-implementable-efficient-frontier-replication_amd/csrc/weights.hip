@@ -7,16 +7,17 @@
 // Every month depends on the previous one; each month is one launch of ROWS_WG-row
 // workgroups (all launched from the host loop below, no host round trip): every workgroup
 // rebuilds the N-vector d of its month in LDS from the previous month's w_opt (drift gather),
-// then computes its rows of m_tilde_t d with one wave per row (coalesced row reads, shuffle
-// reduction).  m_tilde_t (N x N, the only large operand) is read once per month spread over
-// N / ROWS_WG CUs - a single persistent workgroup was bound by one CU's bandwidth (39 ms for
-// 360 months at N = 500).
+// then computes its rows of m_tilde_t d with one wave per row (coalesced row reads, 8 loads per
+// lane in flight, shuffle reduction).  m_tilde_t (N x N, the only large operand) is read once
+// per month spread over N / ROWS_WG workgroups, so a month costs about one memory round trip:
+// a single persistent workgroup was bound by one CU's bandwidth (39 ms for 360 months at
+// N = 500), 16-row workgroups walking their rows one load pair at a time by latency (14 ms).
 #include "common.h"
 
 namespace {
 
 constexpr int WT = 256;
-constexpr int ROWS_WG = 16;            // 4 waves x 4 rows
+constexpr int ROWS_WG = 4;             // 4 waves x 1 row
 constexpr int WMAX = 4096;             // N held in LDS (32 KB)
 
 __global__ __launch_bounds__(WT) void weights_month_kernel(
@@ -53,22 +54,26 @@ __global__ __launch_bounds__(WT) void weights_month_kernel(
   if (last) return;
   __syncthreads();
   const double* M = mt + (int64_t)m * sm;
-  for (int r = 0; r < ROWS_WG / 4; ++r) {
-    const int i = blockIdx.x * ROWS_WG + w * (ROWS_WG / 4) + r;
-    if (i >= N) break;
-    const double* row = M + (int64_t)i * ldm;
-    double s0 = 0.0, s1 = 0.0;
-    int j = lane;
-    for (; j + 64 < N; j += 128) {
-      s0 += row[j] * d[j];
-      s1 += row[j + 64] * d[j + 64];
-    }
-    if (j < N) s0 += row[j] * d[j];
-    double s = s0 + s1;
+  const int i = blockIdx.x * ROWS_WG + w;
+  if (i >= N) return;
+  const double* row = M + (int64_t)i * ldm;
+  double s = 0.0;
+  for (int j0 = 0; j0 < N; j0 += 8 * 64) {
+    double x[8];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-    if (lane == 0) Wopt[(int64_t)m * sv + i] = wam[i] + am[i] * s;
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + 64 * u + lane;
+      x[u] = (j < N) ? row[j] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int j = j0 + 64 * u + lane;
+      s += (j < N) ? x[u] * d[j] : 0.0;
+    }
   }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) Wopt[(int64_t)m * sv + i] = wam[i] + am[i] * s;
 }
 
 }  // namespace

@@ -179,20 +179,35 @@ def _weights_plan(cfg: Config, chars: pd.DataFrame, wealth: pd.DataFrame, aims: 
     weights aligned to them, the drift map from month t's rows to month t+1's (position of
     each id of t+1 among t's rows, or -1 for a new name), and the month of every row."""
     mi_all = month_index(chars["eom"])
-    sel = np.isin(mi_all, oos_months) & chars["valid"].to_numpy()
-    cols = [c for c in ("eom", "id", "me", "tr_ld1", "lambda") if c in chars.columns]
-    data = chars.loc[sel, cols].copy()
-    data["mi"] = mi_all[sel]
-    data = data.sort_values(["mi", "id"], kind="stable").reset_index(drop=True)
     months = np.asarray(oos_months, np.int64)
+    # OOS membership by a month lookup table (months are a short integer range)
+    if len(months):
+        lo = int(min(months.min(), mi_all.min())) if len(mi_all) else int(months.min())
+        hi = int(max(months.max(), mi_all.max())) if len(mi_all) else int(months.max())
+        lut = np.zeros(hi - lo + 1, bool)
+        lut[months - lo] = True
+        in_oos = lut[mi_all - lo]
+    else:
+        in_oos = np.zeros(len(mi_all), bool)
+    rows = np.nonzero(in_oos & chars["valid"].to_numpy())[0]
+    ids_sel = chars["id"].to_numpy(np.int64)[rows]
+    # (mi, id) order: one int64 key, sorted only if the panel is not already in that order
+    skey = mi_all[rows] * 10_000_000 + ids_sel
+    if len(skey) > 1 and not (skey[1:] >= skey[:-1]).all():
+        rows = rows[np.argsort(skey, kind="stable")]
+    cols = [c for c in ("id", "me", "tr_ld1", "lambda") if c in chars.columns]
+    data = pd.DataFrame({c: chars[c].to_numpy()[rows] for c in cols})
+    data["mi"] = mi_all[rows]
     mi = data["mi"].to_numpy()
     starts = np.searchsorted(mi, months, "left")
     stops = np.searchsorted(mi, months, "right")
     ids_all = data["id"].to_numpy(np.int64)
     trow = np.searchsorted(months, mi)                  # month position of every row
     aim_key = month_index(aims["eom"]) * 10_000_000 + aims["id"].to_numpy(np.int64)
-    order = np.argsort(aim_key, kind="stable")
-    ak, av = aim_key[order], aims["w_aim"].to_numpy(np.float64)[order]
+    ak, av = aim_key, aims["w_aim"].to_numpy(np.float64)
+    if len(ak) > 1 and not (ak[1:] >= ak[:-1]).all():     # sort only if not already sorted
+        order = np.argsort(aim_key, kind="stable")
+        ak, av = ak[order], av[order]
     key = mi * 10_000_000 + ids_all
     p = np.clip(np.searchsorted(ak, key), 0, max(len(ak) - 1, 0))
     w_aim = np.where((len(ak) > 0) & (ak[p] == key), av[p], np.nan) if len(ak) else \

@@ -20,6 +20,11 @@ def month_index(dates) -> np.ndarray:
     a pure numpy path (datetime64[M] arithmetic); anything else goes through pandas."""
     a = np.atleast_1d(np.asarray(dates))
     if np.issubdtype(a.dtype, np.datetime64) and not np.isnat(a).any():
+        if a.size > 4096:
+            # panels repeat few distinct dates: convert the distinct values only (the
+            # datetime64[M] cast is calendar arithmetic per element)
+            codes, uniq = pd.factorize(a.view(np.int64), sort=False)
+            return (uniq.view(a.dtype).astype("datetime64[M]").astype(np.int64) + _EPOCH_MI)[codes]
         return a.astype("datetime64[M]").astype(np.int64) + _EPOCH_MI
     d = pd.DatetimeIndex(pd.to_datetime(np.atleast_1d(dates)))
     return (d.year.to_numpy().astype(np.int64) * 12 + d.month.to_numpy().astype(np.int64) - 1)
@@ -28,6 +33,9 @@ def month_index(dates) -> np.ndarray:
 def month_end(mi) -> pd.DatetimeIndex:
     """Integer month index -> month-end Timestamp(s) (first day of the next month - 1 day)."""
     mi = np.atleast_1d(np.asarray(mi, dtype=np.int64))
+    if mi.size > 4096:                  # few distinct months: convert those, then take
+        codes, uniq = pd.factorize(mi, sort=False)
+        return month_end(uniq)[codes]
     nxt = (mi - _EPOCH_MI + 1).astype("datetime64[M]").astype("datetime64[D]")
     return pd.DatetimeIndex((nxt - np.timedelta64(1, "D")).astype("datetime64[ns]"))
 
