@@ -43,7 +43,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 import pfml  # noqa: E402
 from pfml.config import Config  # noqa: E402
-from pfml.models.search import PfmlReals, grid_search, validation_scores  # noqa: E402
+from pfml.models.search import PfmlReals, grid_search, validation_scores_all  # noqa: E402
 from pfml.ops.gemm import gemm  # noqa: E402
 from pfml.ops.ridge import _HostClock  # noqa: E402
 from pfml.parallel import collectives as coll  # noqa: E402
@@ -86,11 +86,8 @@ def one_step(reals: PfmlReals, cfg: Config, engine=None):
         reals = PfmlReals(months=out.months, r_tilde=out.r_tilde, denom=out.denom,
                           all_months=all_months)
     res = grid_search(reals, cfg)
-    G = res.obj.shape[1]
-    out = []
     th = _HostClock()
-    for g in range(G):
-        out.append(validation_scores(res.obj, g, cfg.run.compat_mode))
+    out = validation_scores_all(res.obj, cfg.run.compat_mode)     # every frame, 2 launches
     th("validation_scores")
     return res, out
 

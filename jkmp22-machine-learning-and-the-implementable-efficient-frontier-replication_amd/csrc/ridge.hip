@@ -790,6 +790,9 @@ __global__ __launch_bounds__(NT) void ridge_backtransform_kernel(
   // (YREG rows per lane); reflectors staged one step ahead through a 3-deep LDS ring so each
   // reflector costs exactly one barrier.
   double* out = beta_out + cd.out;
+  // padding columns [n, ldo) of every lambda row are zero: the caller's beta needs no fill
+  for (int64_t e = t; e < (int64_t)L * (ldo - n); e += NT)
+    out[(e / (ldo - n)) * ldo + n + e % (ldo - n)] = 0.0;
   if ((n + NW - 1) / NW <= YREG && n <= RMAX) {
     // reflector ring: 3 blocks of KB rows; block b+1 is written to LDS while block b is in use
     // and block b+2 is in flight in registers (loads get KB reflectors of time to land).

@@ -1253,6 +1253,11 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
   const bool lok = c16 < min(LC, L - l0);
   const int nb = (n + 15) >> 4;
   const double* __restrict__ yc = bw.Yt + (int64_t)(l0 + (lok ? c16 : 0)) * n;
+  {   // padding columns [n, ldo) of this chunk's lambda rows are zero (no fill by the caller)
+    const int lc = min(LC, L - l0), pad = (int)(ldo - n);
+    double* __restrict__ o = beta_out + cd.out + (int64_t)l0 * ldo + n;
+    for (int e = threadIdx.x; e < lc * pad; e += NTB) o[(int64_t)(e / pad) * ldo + e % pad] = 0.0;
+  }
   double4_t Y[NBW];
 #pragma unroll
   for (int q = 0; q < NBW; ++q)

@@ -9,7 +9,8 @@
 //                values; NaN cum gets a NaN rank and is not counted (pandas
 //                rank(method='dense', ascending=False)), so a singular cell is never "rank 1"
 //
-// Two launches replace the ~25 small torch kernels (sort, scans, scatters) per frame:
+// Two launches replace the ~25 small torch kernels (sort, scans, scatters) per frame, and
+// pfml_validation_scores_all does every frame of a grid search in the same two launches:
 //   prefix_mean_kernel  16 columns x 16 row chunks per workgroup: chunk sums, LDS offsets,
 //                       chunk rescans, NaN carry fix-up (loads batched and clamped)
 //   dense_rank_kernel   one workgroup per month: bitonic sort of <= 1024 (key, index) pairs in
@@ -23,9 +24,29 @@ constexpr int RK_T = 256;
 
 constexpr int PM_COLS = 16, PM_RG = 16;   // prefix mean: 16 columns x 16 row chunks per WG
 
+// Frames: blockIdx.y = f of nF frames; frame f covers g in [f0 + f, f1 + f) clipped as
+// (g0, g1) = compat ? (0, f + 1) : (f, f + 1) when `multi`, else the single (g0, g0 + k).  Its
+// cum rows start at cum + cum_off(f) (frame sizes nV * k_f * C before it).
+__device__ __forceinline__ void frame_of(int f, bool multi, bool compat, int g0s, int ks,
+                                         int nV, int C, int& g0, int& k, int64_t& off) {
+  if (!multi) {
+    g0 = g0s; k = ks; off = 0;
+    return;
+  }
+  g0 = compat ? 0 : f;
+  k = compat ? f + 1 : 1;
+  // sum of the earlier frames' k: compat f (f + 1) / 2, else f
+  off = (int64_t)nV * C * (compat ? (int64_t)f * (f + 1) / 2 : f);
+}
+
 __global__ __launch_bounds__(256) void prefix_mean_kernel(const double* __restrict__ obj, int nV,
-                                                          int G, int g0, int k, int C,
-                                                          double* __restrict__ cum) {
+                                                          int G, int g0s, int ks, int C,
+                                                          double* __restrict__ cum_all,
+                                                          int multi, int compat) {
+  int g0, k;
+  int64_t coff;
+  frame_of(blockIdx.y, multi, compat, g0s, ks, nV, C, g0, k, coff);
+  double* __restrict__ cum = cum_all + coff;
   // thread (rg, cg): rows [rg * chunk, (rg + 1) * chunk) of column c; chunk sums / counts of
   // the non-NaN values meet in LDS for the cross-chunk offsets, then each chunk is rescanned.
   // A NaN row must repeat the previous expanding mean BIT FOR BIT (pandas carries its running
@@ -112,22 +133,33 @@ __device__ __forceinline__ bool before(double a, int ia, double b, int ib) {
   return a > b || (a == b && ia < ib);
 }
 
-__global__ __launch_bounds__(RK_T) void dense_rank_kernel(const double* __restrict__ cum, int N,
-                                                          double* __restrict__ rank) {
+__global__ __launch_bounds__(RK_T) void dense_rank_kernel(const double* __restrict__ cum_all,
+                                                          int Ns, int nV, int C,
+                                                          double* __restrict__ rank_all,
+                                                          int multi, int compat) {
   __shared__ double key[RK_N];
   __shared__ int idx[RK_N];
   __shared__ int wsum[RK_T / 64];
+  int g0, k;
+  int64_t off;
+  frame_of(blockIdx.y, multi, compat, 0, Ns / max(C, 1), nV, C, g0, k, off);
+  const int N = multi ? k * C : Ns;
+  const double* __restrict__ cum = cum_all + off;
+  double* __restrict__ rank = rank_all + off;
+  // sort width: the next power of two >= N (a 404-value month sorts 512, not 1024)
+  int NS = 2;
+  while (NS < N) NS <<= 1;
   const int v = blockIdx.x, t = threadIdx.x;
   const double* src = cum + (int64_t)v * N;
-  for (int i = t; i < RK_N; i += RK_T) {
+  for (int i = t; i < NS; i += RK_T) {
     key[i] = src[min(i, N - 1)];            // (padding entries carry idx -1)
     idx[i] = (i < N) ? i : -1;
   }
   __syncthreads();
-  // bitonic sort of RK_N elements, "before" order
-  for (int size = 2; size <= RK_N; size <<= 1) {
+  // bitonic sort of NS elements, "before" order
+  for (int size = 2; size <= NS; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int p = t; p < RK_N / 2; p += RK_T) {
+      for (int p = t; p < NS / 2; p += RK_T) {
         const int lo = 2 * p - (p & (stride - 1)), hi = lo + stride;
         const bool up = (lo & size) == 0;
         const double ka = key[lo], kb = key[hi];
@@ -146,7 +178,7 @@ __global__ __launch_bounds__(RK_T) void dense_rank_kernel(const double* __restri
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int i = 4 * t + q;
-    const bool real = idx[i] >= 0 && key[i] == key[i];      // NaN: not ranked
+    const bool real = i < NS && idx[i] >= 0 && key[i] == key[i];   // NaN: not ranked
     nw[q] = real && (i == 0 || key[i] != key[i - 1]) ? 1 : 0;
     run += nw[q];
   }
@@ -168,7 +200,7 @@ __global__ __launch_bounds__(RK_T) void dense_rank_kernel(const double* __restri
   for (int q = 0; q < 4; ++q) {
     const int i = 4 * t + q;
     acc += nw[q];
-    if (idx[i] >= 0) dst[idx[i]] = (key[i] == key[i]) ? (double)acc : __builtin_nan("");
+    if (i < NS && idx[i] >= 0) dst[idx[i]] = (key[i] == key[i]) ? (double)acc : __builtin_nan("");
   }
 }
 
@@ -184,7 +216,23 @@ extern "C" hipError_t pfml_validation_scores(const double* obj, int nV, int G, i
   if (nV <= 0 || C <= 0 || k <= 0) return hipSuccess;
   if (k * C > RK_N || g0 < 0 || g1 > G) return hipErrorInvalidValue;
   hipLaunchKernelGGL(prefix_mean_kernel, dim3((C + PM_COLS - 1) / PM_COLS), dim3(256), 0, st, obj,
-                     nV, G, g0, k, C, cum);
-  hipLaunchKernelGGL(dense_rank_kernel, dim3(nV), dim3(RK_T), 0, st, cum, k * C, rank);
+                     nV, G, g0, k, C, cum, 0, 0);
+  hipLaunchKernelGGL(dense_rank_kernel, dim3(nV), dim3(RK_T), 0, st, cum, k * C, nV, C, rank, 0,
+                     0);
+  return hipGetLastError();
+}
+
+// Every frame f = 0 .. G-1 of one grid search in two launches (blockIdx.y = frame): frame f
+// holds g' <= f (compat, quirk Q2) or g = f alone.  cum / rank: the frames' [nV, k_f, C]
+// blocks back to back (k_f = f + 1 or 1).
+extern "C" hipError_t pfml_validation_scores_all(const double* obj, int nV, int G, int C,
+                                                 int compat, double* cum, double* rank,
+                                                 hipStream_t st) {
+  if (nV <= 0 || C <= 0 || G <= 0) return hipSuccess;
+  if ((compat ? G : 1) * C > RK_N) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(prefix_mean_kernel, dim3((C + PM_COLS - 1) / PM_COLS, G), dim3(256), 0, st,
+                     obj, nV, G, 0, 1, C, cum, 1, compat);
+  hipLaunchKernelGGL(dense_rank_kernel, dim3(nV, G), dim3(RK_T), 0, st, cum, C, nV, C, rank, 1,
+                     compat);
   return hipGetLastError();
 }

@@ -43,6 +43,8 @@ log = get_logger("search")
 nat.register_hip("pfml_validation_scores", [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
                                             C.c_int, C.c_void_p, C.c_void_p, C.c_void_p])
 nat.register_hip("pfml_scores_max_per_month", [])
+nat.register_hip("pfml_validation_scores_all", [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                C.c_void_p, C.c_void_p, C.c_void_p])
 
 
 @dataclass
@@ -372,6 +374,32 @@ def validation_scores(obj: torch.Tensor, frame_g: int, compat: bool):
     return seq, cum, rank.view(nV, k, nP, L)
 
 
+def validation_scores_all(obj: torch.Tensor, compat: bool) -> list:
+    """validation_scores for every frame g = 0 .. G-1; on the device all frames go through
+    ONE prefix-mean and ONE dense-rank launch (csrc/scores.hip, blockIdx.y = frame)."""
+    nV, G, nP, L = obj.shape
+    kmax = G if compat else 1
+    if not (nat.is_device(obj) and kmax * nP * L <= nat.hip_lib().pfml_scores_max_per_month()):
+        return [validation_scores(obj, g, compat) for g in range(G)]
+    o = obj.contiguous()
+    ks = [(g + 1) if compat else 1 for g in range(G)]
+    tot = nV * sum(ks) * nP * L
+    cum_all = torch.empty(tot, dtype=obj.dtype, device=obj.device)
+    rank_all = torch.empty_like(cum_all)
+    nat.check(nat.hip_lib().pfml_validation_scores_all(o.data_ptr(), nV, G, nP * L, int(compat),
+                                                       cum_all.data_ptr(), rank_all.data_ptr(),
+                                                       nat.stream_of(o)),
+              "pfml_validation_scores_all")
+    out, off = [], 0
+    for g, k in enumerate(ks):
+        n = nV * k * nP * L
+        g0 = 0 if compat else g
+        out.append((obj[:, g0:g0 + k], cum_all[off:off + n].view(nV, k, nP, L),
+                    rank_all[off:off + n].view(nV, k, nP, L)))
+        off += n
+    return out
+
+
 def validation_frame(grid: GridResult, cfg: Config) -> pd.DataFrame:
     """validation.csv (columns eom, eom_ret, obj, l, p, hp_end, cum_obj, rank, g)."""
     compat = cfg.run.compat_mode
@@ -383,8 +411,7 @@ def validation_frame(grid: GridResult, cfg: Config) -> pd.DataFrame:
     eom = month_end(vm)
     eom_ret = month_end(vm + 1)
     nP, L = len(grid.p_vec), len(grid.l_vec)
-    for g in range(G):
-        seq, cum, rank = validation_scores(obj, g, compat)
+    for g, (seq, cum, rank) in enumerate(validation_scores_all(obj, compat)):
         nV, k = seq.shape[:2]
         # rows sorted by (p, l, eom_ret, g') as the reference's stable sort leaves them
         o = seq.permute(2, 3, 0, 1).reshape(-1).cpu().numpy()

@@ -390,7 +390,9 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     plan = _utilities_plan(P, L, dev, cell_src, cell_n, cell_scale, job_cell, job_month, job_n,
                            split=split)
     th("plans")
-    beta = torch.zeros((nc, L, P), dtype=SD.dtype, device=dev)
+    # every [L, P] block is written whole by the ridge grid (zero padding past n included), so
+    # no fill on the stream the big cells' chain forks from
+    beta = torch.empty((nc, L, P), dtype=SD.dtype, device=dev)
     obj = torch.empty((len(job_cell), L), dtype=SD.dtype, device=dev)
     SD, Sr, D, R = SD.contiguous(), Sr.contiguous(), D.contiguous(), R.contiguous()
     lv = lvec.to(device=dev, dtype=torch.float64).contiguous()

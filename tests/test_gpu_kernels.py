@@ -359,6 +359,25 @@ def test_validation_scores_kernel(gpu, compat):
         assert torch.equal(got[2].cpu(), ref[2])
 
 
+@pytest.mark.parametrize("compat", [True, False])
+@pytest.mark.parametrize("G,nP", [(2, 4), (3, 2)])
+def test_validation_scores_all_frames(gpu, compat, G, nP):
+    """All frames in one prefix-mean + one dense-rank launch (blockIdx.y = frame, sort width
+    sized per frame) give the per-frame kernels' cum_obj and ranks bitwise, and the CPU path's."""
+    from pfml.models.search import validation_scores, validation_scores_all
+    g = torch.Generator().manual_seed(9)
+    obj = torch.randn(29, G, nP, 101, generator=g, dtype=torch.float64)
+    obj[:, :, 1, :] = obj[:, :, 0, :]                     # exact ties
+    obj[2, 0, 1, 5] = float("nan")
+    allf = validation_scores_all(obj.to(gpu), compat)
+    for fg in range(G):
+        one = validation_scores(obj.to(gpu), fg, compat)
+        ref = validation_scores(obj, fg, compat)
+        for a, b, c in zip(allf[fg], one, ref):
+            assert torch.equal(torch.nan_to_num(a.cpu(), nan=-7.0), torch.nan_to_num(b.cpu(), nan=-7.0))
+            assert torch.allclose(a.cpu(), c, rtol=1e-12, atol=1e-14, equal_nan=True)
+
+
 def test_grid_search_bitwise_deterministic(gpu):
     """Replays of the device grid search are bitwise identical (fixed tilings and reduction
     orders, no float atomics; SURVEY §5.2 deterministic replay), incl. the cached-plan path."""
