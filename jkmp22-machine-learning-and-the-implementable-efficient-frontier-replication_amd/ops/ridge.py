@@ -276,8 +276,11 @@ def _side_stream(dev: torch.device, k: int = 0) -> torch.cuda.Stream:
 
 BAND_SINGLE, BAND_MULTI = 1, 2
 # Above this many largest-n cells per launch the one-workgroup-per-cell reduction (throughput
-# form) beats the multi-workgroup one (latency form); measured on MI355X, tools/bench_band.py.
-BAND_MULTI_MAX_CELLS = 64
+# form, big cells on their own stream) beats the multi-workgroup one (latency form); measured
+# on MI355X, tools/bench_band.py, and in the strong-scaling rehearsal: 53 big cells per rank
+# (2 ranks) 4.51 ms single + 2 streams vs 4.65 multi, 26-27 (4 ranks) 3.64 vs 3.18
+# (tools/gpu_shard_modes2.sh, profiles/r02_shard_modes.txt).
+BAND_MULTI_MAX_CELLS = 48
 # Hybrid (one GPU holds the whole grid): this many of the largest-n cells take the
 # multi-workgroup reduction on a third stream while the rest keep one workgroup per cell, so
 # the CUs the single-workgroup cells leave idle also work on big cells.  Measured on MI355X
