@@ -743,7 +743,8 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
 #pragma unroll
         for (int u = 0; u < TBR; ++u) {
           const int tile = min(tb + u, ntt - 1);
-          int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+          // fp32 root (8 tile + 1 < 2^24 is exact; the two fix-ups below absorb any rounding)
+          int I = (int)((__builtin_sqrtf(8.0f * (float)tile + 1.0f) - 1.0f) * 0.5f);
           if (I * (I + 1) / 2 > tile) --I;
           if ((I + 1) * (I + 2) / 2 <= tile) ++I;
           ni0[u] = (tb + u < ntt) ? I * 16 : BMP;      // BMP: beyond every row, a no-op tile
@@ -967,7 +968,7 @@ __global__ __launch_bounds__(256) void band_mk_trail_kernel(const RidgeCellDesc*
   __shared__ double Zv[BB];
   __shared__ double Zt[BB];
   const int cell = blockIdx.x / ntile, tile = blockIdx.x % ntile;
-  int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+  int I = (int)((__builtin_sqrtf(8.0f * (float)tile + 1.0f) - 1.0f) * 0.5f);   // + fix-ups
   if (I * (I + 1) / 2 > tile) --I;
   if ((I + 1) * (I + 2) / 2 <= tile) ++I;
   const int J = tile - I * (I + 1) / 2;           // lower tile (I, J), I >= J
