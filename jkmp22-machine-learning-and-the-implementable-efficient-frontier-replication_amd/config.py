@@ -175,7 +175,7 @@ class RunOptions:
     check: bool = False                # compare device results against the CPU oracle
     profile: bool = False              # emit roctx ranges + stage timing JSONL
     plots: bool = True                 # the reference's figures as PNGs under <data_dir>/plots
-    fault_inject: str = ""             # e.g. "s4:shard=1" to poison a shard (tests recovery)
+    fault_inject: str = ""             # "pfml-input" / "pfml-search-coef": poison a month / a cell (tests recovery)
     synthetic: dict = field(default_factory=lambda: {
         "n_stocks": 500, "n_features": 115, "start": "1952-01-31", "end": "2023-12-31",
         "n_factors_cluster": 13, "seed": 0,

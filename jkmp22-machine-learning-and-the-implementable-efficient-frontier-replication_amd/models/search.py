@@ -319,6 +319,61 @@ def check_against_oracle(grid: GridResult, reals: PfmlReals, cfg: Config, ncells
     return out
 
 
+def nonfinite_cells(grid: GridResult) -> list:
+    """(g, local year, p) cells whose coefficients are not finite for some lambda (after the
+    device repair a non-finite cell means a fault, or a system singular even for pivoted LU)."""
+    G, nYl, nP = grid.beta.shape[:3]
+    out = []
+    if nYl == 0:
+        return out
+    for pi, p in enumerate(grid.p_vec):
+        ok = torch.isfinite(grid.beta[:, :, pi, :, : int(p) + 1]).flatten(2).all(-1)   # [G, nYl]
+        for g, yi in torch.nonzero(~ok).cpu().numpy():
+            out.append((int(g), int(yi), pi))
+    return sorted(out)
+
+
+def recompute_cells(grid: GridResult, reals: PfmlReals, cells) -> dict:
+    """Failure recovery: recompute the coefficients of ``cells`` [(g, local
+    year, p)] and their validation utilities from scratch with the fp64 CPU oracle - window
+    sums by plain summation, one pivoted-LU solve per lambda (np.linalg.solve semantics: an
+    exactly singular system stays NaN, where the reference raises) - and write them back into
+    ``grid``.  Needs every month from the first one on this rank (world 1, or the rank that
+    holds the burn-in); returns counts."""
+    from ..ops.ridge import quadform_utilities, ridge_grid
+    months = np.asarray(reals.months, dtype=np.int64)
+    allm = np.asarray(reals.months if reals.all_months is None else reals.all_months, np.int64)
+    if len(cells) and (len(months) == 0 or months[0] != allm[0]):
+        raise RuntimeError("recompute_cells: this rank lacks the months before its windows")
+    plan = make_plan(months, np.asarray(grid.years))
+    yl = np.nonzero(np.isin(np.asarray(grid.years), np.asarray(grid.years_local)))[0]
+    lv = torch.as_tensor(grid.l_vec, dtype=torch.float64)
+    denom, rt = reals.denom.cpu(), reals.r_tilde.cpu()
+    rows_of = {}
+    if grid.obj.shape[0] == len(grid.val_months):
+        for i, (vm, vy) in enumerate(zip(grid.val_months, grid.val_year)):
+            rows_of.setdefault(int(vy), []).append((i, int(vm)))
+    still = 0
+    for g, yi, pi in cells:
+        y = int(yl[yi])
+        n = int(grid.p_vec[pi]) + 1
+        stop = int(plan.seg_stop[y])
+        SD = denom[g, :stop].sum(0)[None]
+        Sr = rt[g, :stop].sum(0)[None]
+        b = ridge_grid(SD, Sr, np.array([0]), np.array([n]),
+                       np.array([1.0 / max(int(plan.count[y]), 1)]), lv)[0]
+        grid.beta[g, yi, pi] = b.to(grid.beta.device)
+        still += int(not bool(torch.isfinite(b[:, :n]).all()))
+        rows = rows_of.get(int(grid.years[y]), [])
+        if rows:
+            jm = np.array([g * len(months) + int(np.searchsorted(months, vm)) for _, vm in rows])
+            o = quadform_utilities(denom.reshape(-1, *denom.shape[2:]),
+                                   rt.reshape(-1, rt.shape[-1]), b[None],
+                                   np.zeros(len(rows), np.int64), jm, np.full(len(rows), n))
+            grid.obj[[i for i, _ in rows], g, pi] = o.to(grid.obj.device)
+    return {"recomputed": len(cells), "singular": still}
+
+
 # ---------------------------------------------------------------------------------------
 # Scores (K17): expanding mean by (p, l) over eom_ret, dense rank per eom_ret.
 # ---------------------------------------------------------------------------------------

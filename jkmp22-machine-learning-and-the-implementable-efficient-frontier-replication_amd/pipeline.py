@@ -238,9 +238,32 @@ class Pipeline:
             st["signal_months"] = st["reals"].months
             st["rff_w"] = t["rff_w"].numpy()
 
+    def _guard_grid(self, grid) -> None:
+        """Failure detection for S5: (g, year, p) cells whose coefficients are not
+        finite after the device repair are recomputed with the fp64 CPU oracle (coefficients
+        and their validation utilities).  A shard that cannot rebuild its window sums (it
+        lacks the burn-in months) raises before writing its done marker, so a resumed run
+        recomputes just that shard.  ``run.fault_inject = "pfml-search-coef"`` poisons one
+        cell of every shard to exercise this path."""
+        if self.cfg.run.fault_inject.startswith("pfml-search-coef") and grid.beta.shape[1]:
+            grid.beta[0, 0, -1, len(grid.l_vec) // 2, 0] = float("nan")
+            COUNTERS.add("fault_injected")
+        bad = search.nonfinite_cells(grid)
+        if not bad:
+            return
+        log.warning(f"non-finite coefficients in {len(bad)} cell(s) on rank "
+                    f"{self.env.rank}: recomputing on the CPU oracle")
+        res = search.recompute_cells(grid, self.state["reals"], bad)
+        COUNTERS.add("pfml_search.recomputed_cells", res["recomputed"])
+        if res["singular"]:
+            COUNTERS.add("pfml_search.singular_cells", res["singular"])
+            log.warning(f"{res['singular']} cell(s) singular even for pivoted LU: NaN kept "
+                        "(never ranked; the reference raises here)")
+
     def _pfml_search_coef(self):
         self._ensure_reals()
         grid = search.grid_search(self.state["reals"], self.cfg)
+        self._guard_grid(grid)
         if self.cfg.run.check:
             metric(stage="pfml-search-coef", check=search.check_against_oracle(
                 grid, self.state["reals"], self.cfg), rank=self.env.rank)

@@ -174,7 +174,8 @@ def test_m_func_matches_sqrtm_reference():
 
 def test_pipeline_cli_resume_and_fault_injection(small_data, tmp_path):
     """End-to-end S4..S9 through the CLI entry point; a checkpointed rerun resumes (skips
-    every stage); a poisoned shard is detected and recomputed to identical outputs."""
+    every stage); a poisoned S4 month and a poisoned S5 coefficient cell are detected and
+    recomputed to identical outputs."""
     import shutil
     from pfml.cli import main
     from pfml.pipeline import Pipeline
@@ -205,6 +206,11 @@ def test_pipeline_cli_resume_and_fault_injection(small_data, tmp_path):
     assert np.allclose(summ1[["r", "sr"]].to_numpy(), summ2[["r", "sr"]].to_numpy(), rtol=1e-10)
     from pfml.utils.log import COUNTERS
     assert COUNTERS.as_dict().get("pfml_input.recomputed_months", 0) >= 1
+    # S5: a poisoned coefficient cell is recomputed on the CPU oracle -> identical outputs
+    assert main(["stages", stages] + base + ["--set", "run.fault_inject=pfml-search-coef"]) == 0
+    pf3 = pd.read_csv(os.path.join(d, "pf.csv"))
+    assert np.allclose(pf1[["r", "tc"]].to_numpy(), pf3[["r", "tc"]].to_numpy(), rtol=1e-10)
+    assert COUNTERS.as_dict().get("pfml_search.recomputed_cells", 0) >= 1
 
 
 def test_gemm_fp32_precision_cpu():

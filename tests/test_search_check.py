@@ -44,3 +44,39 @@ def test_cli_check_flag():
     import argparse  # noqa: F401
     with pytest.raises(SystemExit):
         main(["--help"])
+
+
+def test_nonfinite_cells_recomputed_on_cpu_oracle():
+    """S5 failure recovery: a poisoned (g, year, p) cell is detected and its
+    coefficients and validation utilities are recomputed from scratch by the fp64 CPU oracle,
+    matching the clean grid search."""
+    import numpy as np
+    import torch
+    from pfml.config import Config
+    from pfml.models.search import (PfmlReals, grid_search, nonfinite_cells, recompute_cells)
+    from pfml.utils.dates import mi_from_ym
+    cfg = Config.default().override(["pf_ml.p_vec=[8,16]", "pf.dates.start_year=2001",
+                                     "pf.dates.end_yr=2006"])
+    G, P = 2, 17
+    months = np.arange(mi_from_ym(1995, 1), mi_from_ym(2006, 11) + 1)
+    T = len(months)
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(G * T, 30, P, generator=g, dtype=torch.float64)
+    D = (X.transpose(1, 2) @ X / 30).view(G, T, P, P)
+    r = 0.1 * torch.randn(G, T, P, generator=g, dtype=torch.float64)
+    reals = PfmlReals(months, r, D)
+    clean = grid_search(reals, cfg)
+    grid = grid_search(reals, cfg)
+    assert nonfinite_cells(grid) == []
+    grid.beta[1, 2, 1, 40, 3] = float("nan")
+    grid.beta[0, 0, 0, :, 0] = float("inf")
+    yi = 2
+    rows = np.nonzero(grid.val_year == grid.years_local[yi])[0]
+    grid.obj[rows, 1, 1] = float("nan")
+    bad = nonfinite_cells(grid)
+    assert bad == [(0, 0, 0), (1, 2, 1)]
+    res = recompute_cells(grid, reals, bad)
+    assert res == {"recomputed": 2, "singular": 0}
+    assert nonfinite_cells(grid) == []
+    assert torch.allclose(grid.beta, clean.beta, rtol=1e-10, atol=1e-14)
+    assert torch.allclose(grid.obj, clean.obj, rtol=1e-10, atol=1e-14)
