@@ -360,6 +360,24 @@ class Pipeline:
         # m_t sharded over ranks, the recursion chained across them (rank 0 gets the frame)
         w = portfolio.pfml_weights(self.cfg, st["chars"], st["barra"], st["wealth"],
                                    st["risk_free"], aims, oos, self.device)
+        # failure detection: the chained w_start is finite by construction (value
+        # weights, drift, 0 for new names); a non-finite one means a fault in the device chain
+        # -> the recursion is recomputed on the CPU (a collective decision: every rank reruns)
+        bad = 0
+        if self.env.is_main:
+            if self.cfg.run.fault_inject.startswith("pfml-best-hps") and len(w):
+                w.loc[w.index[len(w) // 2], "w_start"] = float("nan")
+                COUNTERS.add("fault_injected")
+            bad = int((~np.isfinite(w["w_start"].to_numpy())).sum())
+        bad = coll.broadcast_object(bad) if self.env.is_dist else bad
+        if bad:
+            log.warning(f"non-finite w_start in {bad} row(s): weight recursion recomputed on "
+                        "the CPU")
+            COUNTERS.add("pfml_best_hps.recomputed", 1)
+            w = portfolio.pfml_weights(self.cfg, st["chars"], st["barra"], st["wealth"],
+                                       st["risk_free"], aims, oos, torch.device("cpu"))
+            if self.env.is_main and not np.isfinite(w["w_start"].to_numpy()).all():
+                raise FloatingPointError("w_start stays non-finite on the CPU recursion")
         if not self.env.is_main:
             return
         d = self.cfg.run.data_dir

@@ -174,7 +174,7 @@ def test_m_func_matches_sqrtm_reference():
 
 def test_pipeline_cli_resume_and_fault_injection(small_data, tmp_path):
     """End-to-end S4..S9 through the CLI entry point; a checkpointed rerun resumes (skips
-    every stage); a poisoned S4 month and a poisoned S5 coefficient cell are detected and
+    every stage); a poisoned S4 month, S5 coefficient cell and S9 w_start are detected and
     recomputed to identical outputs."""
     import shutil
     from pfml.cli import main
@@ -211,6 +211,12 @@ def test_pipeline_cli_resume_and_fault_injection(small_data, tmp_path):
     pf3 = pd.read_csv(os.path.join(d, "pf.csv"))
     assert np.allclose(pf1[["r", "tc"]].to_numpy(), pf3[["r", "tc"]].to_numpy(), rtol=1e-10)
     assert COUNTERS.as_dict().get("pfml_search.recomputed_cells", 0) >= 1
+    # S9: a poisoned w_start is detected and the recursion recomputed -> identical outputs
+    assert main(["stages", "pfml-best-hps"] + base + ["--checkpoint", "--set",
+                                                       "run.fault_inject=pfml-best-hps"]) == 0
+    pf4 = pd.read_csv(os.path.join(d, "pf.csv"))
+    assert np.allclose(pf1[["r", "tc"]].to_numpy(), pf4[["r", "tc"]].to_numpy(), rtol=1e-10)
+    assert COUNTERS.as_dict().get("pfml_best_hps.recomputed", 0) >= 1
 
 
 def test_gemm_fp32_precision_cpu():
