@@ -914,7 +914,8 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
                                              const void* cells, int ncells, int nmax,
                                              const double* lvec, int L, double* work,
                                              double* beta_out, int64_t ldo, int band_mode,
-                                             long long* tim, hipStream_t st);
+                                             long long* tim, int* lu_list, int* lu_count,
+                                             int lu_cap, hipStream_t st);
 
 // Workspace per cell: enough for whichever path the launcher picks (band path: ridge_band.hip).
 extern "C" int64_t pfml_ridge_work_doubles(int n, int L) {
@@ -927,11 +928,15 @@ static long long* g_ridge_timing = nullptr;
 // Debug: per-cell phase cycle counters of the fast tridiagonalisation (8 per cell).
 extern "C" void pfml_ridge_set_timing(long long* buf) { g_ridge_timing = buf; }
 
-// band_mode: 0 = PFML_BAND_MODE / default, 1 = one workgroup per cell, 2 = multi-workgroup
+// band_mode: 0 = PFML_BAND_MODE / default, 1 = one workgroup per cell, 2 = multi-workgroup.
+// lu_list / lu_count / lu_cap (band path only; count zeroed by the caller, nullptr = off): the
+// in-band pivoted-LU repair of non-SPD lambdas; the tridiagonal path leaves its NaN markers
+// to the dense repair (ridge_repair.hip).
 extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const double* Sr,
                                       const void* cells, int ncells, int nmax,
                                       const double* lvec, int L, double* work, double* beta_out,
-                                      int64_t ldo, int band_mode, hipStream_t st) {
+                                      int64_t ldo, int band_mode, int* lu_list, int* lu_count,
+                                      int lu_cap, hipStream_t st) {
   if (ncells <= 0) return hipSuccess;
   if (L > 128 || nmax > NMAX) return hipErrorInvalidValue;
   const CellDesc* cd = static_cast<const CellDesc*>(cells);
@@ -943,7 +948,8 @@ extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const doubl
   if (!force_unblocked && !force_blocked && !force_fast && !getenv("PFML_RIDGE_UNBLOCKED") &&
       nmax <= pfml_ridge_band_nmax())
     return pfml_ridge_band_launch(SD, ldS, Sr, cells, ncells, nmax, lvec, L, work, beta_out,
-                                  ldo, band_mode, g_ridge_timing, st);
+                                  ldo, band_mode, g_ridge_timing, lu_list, lu_count, lu_cap,
+                                  st);
   if (force_unblocked || (getenv("PFML_RIDGE_UNBLOCKED") != nullptr))
     hipLaunchKernelGGL(ridge_tridiag_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr, cd, L,
                        work);

@@ -23,8 +23,8 @@
 //   kernel 3  ridge_band_backtransform_kernel one 512-thread workgroup per (cell, 16 lambdas)
 //
 // A non-positive Cholesky pivot (Dbar + l I not numerically SPD, e.g. l = 0 on a singular
-// Dbar) marks that lambda's beta NaN; ops/ridge.py recomputes exactly those systems with a
-// pivoted LU so the result matches the reference's np.linalg.solve semantics.
+// Dbar) marks that lambda's y NaN; kernel 2b re-solves exactly those systems in the band
+// domain by LU with partial pivoting (np.linalg.solve semantics) before the back-transform.
 #include "common.h"
 #include "ridge_desc.h"
 #include <cstdlib>
@@ -1220,6 +1220,146 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
+// kernel 2b: the lambdas whose banded Cholesky failed (Dbar + l I not numerically SPD: l = 0
+// on a rank-deficient Dbar, PFML_Search_Coef.py:131-133 / General_functions.py:81) are
+// re-solved IN THE BAND DOMAIN by LU with partial pivoting (the LAPACK dgbtf2 pivot order) on
+// (B + l I) y = z, before the back-transform turns y into beta = Q y.  Q is orthogonal, so this
+// is a backward-stable solve of (Dbar + l I) beta = rbar, the system np.linalg.solve sees, at
+// O(n BB^2) per system instead of the O(n^3) dense pivoted LU it replaces.
+//
+//   band_lu_flag_kernel  one thread per (cell, lambda): a NaN-marked y appends it to a list
+//   ridge_band_lu_kernel LU_WG one-wave workgroups walk the list.  Window of the 17 live rows
+//                        (slot = row mod 17) x 33 columns (slot = column mod 33: with
+//                        pivoting U has upper bandwidth 2 BB) in LDS; the pivot row goes to
+//                        an LDS copy of U, then 16 x 32 lanes eliminate and the row 17 below
+//                        enters the freed slot.  Back substitution from LDS, y written back.
+//                        An exactly zero pivot (singular: the reference raises LinAlgError)
+//                        leaves the NaN.
+// ---------------------------------------------------------------------------------------
+constexpr int LR = BB + 1;          // live rows of the pivoting window
+constexpr int UW = 2 * BB + 1;      // U row width (upper bandwidth 2 BB after pivoting)
+constexpr int LU_WG = 128;
+
+__global__ __launch_bounds__(256) void band_lu_flag_kernel(const RidgeCellDesc* __restrict__ cells,
+                                                           int ncells, int L,
+                                                           double* __restrict__ work,
+                                                           int* __restrict__ list,
+                                                           int* __restrict__ count, int cap) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ncells * L) return;
+  const int c = e / L, l = e % L;
+  const RidgeCellDesc cd = cells[c];
+  const BandWork bw(work + cd.work, cd.n, L);
+  const double y0 = bw.Yt[(int64_t)l * cd.n];
+  if (y0 != y0) {
+    const int slot = atomicAdd(count, 1);
+    if (slot < cap) list[slot] = e;
+  }
+}
+
+__global__ __launch_bounds__(64) void ridge_band_lu_kernel(
+    const RidgeCellDesc* __restrict__ cells, const double* __restrict__ lvec, int L,
+    double* __restrict__ work, const int* __restrict__ list, const int* __restrict__ count,
+    int cap) {
+  __shared__ double Us[BNMAX][UW];    // U rows: Us[k][c] = U[k][k + c]
+  __shared__ double ys[BNMAX];        // L^-1 z, then y
+  __shared__ double W[LR][UW];        // live rows k..k+16, columns k..k+32 (both mod-indexed)
+  __shared__ double Z[LR];
+  const int total = min(*count, cap);
+  const int lane = threadIdx.x;
+  for (int q = blockIdx.x; q < total; q += gridDim.x) {
+    const int e = list[q];
+    const RidgeCellDesc cd = cells[e / L];
+    const int l = e % L, n = cd.n;
+    BandWork bw(work + cd.work, n, L);
+    const double lam = lvec[l];
+    const double* __restrict__ LB = bw.LB;
+    // B(r, c) + lam delta_rc for |r - c| <= BB (symmetric band, lower half stored)
+    auto band = [&](int r, int c) -> double {
+      if (r >= n || c >= n || c < 0 || abs(r - c) > BB) return 0.0;
+      const int hi = max(r, c), lo = min(r, c);
+      return LB[(int64_t)hi * LS + lo - hi + BB] + (r == c ? lam : 0.0);
+    };
+    for (int x = lane; x < LR * UW; x += 64) W[x / UW][x % UW] = band(x / UW, x % UW);
+    if (lane < LR) Z[lane] = lane < n ? bw.z[lane] : 0.0;
+    __syncthreads();
+    bool singular = false;
+    for (int k = 0; k < n; ++k) {
+      const int ks = k % LR, kc = k % UW;
+      // pivot: first max |W[k + i][k]|, i = 0..16 (idamax order)
+      double a = (lane < LR && k + lane < n) ? fabs(W[(k + lane) % LR][kc]) : -1.0;
+      int ia = lane;
+#pragma unroll
+      for (int off = 16; off > 0; off >>= 1) {
+        const double oa = __shfl_xor(a, off, 32);
+        const int oi = __shfl_xor(ia, off, 32);
+        if (oa > a || (oa == a && oi < ia)) { a = oa; ia = oi; }
+      }
+      const int ip = __shfl(ia, 0);
+      if (ip != 0) {
+        const int ps = (k + ip) % LR;
+        if (lane < UW) {
+          const double t0 = W[ks][lane];
+          W[ks][lane] = W[ps][lane];
+          W[ps][lane] = t0;
+        }
+        if (lane == 0) {
+          const double t0 = Z[ks];
+          Z[ks] = Z[ps];
+          Z[ps] = t0;
+        }
+      }
+      __syncthreads();
+      const double piv = W[ks][kc];
+      if (piv == 0.0 || piv != piv) { singular = true; break; }
+      const double rp = 1.0 / piv;
+      const double zk = Z[ks];
+      if (lane < UW) Us[k][lane] = W[ks][(k + lane) % UW];
+      if (lane == 0) ys[k] = zk;
+      // eliminate rows k+1..k+16, columns k+1..k+32: lane -> column 1 + (lane & 31), rows
+      // 1 + (lane >> 5) + 2 t
+      const int c = 1 + (lane & 31);
+      const double uc = W[ks][(k + c) % UW];
+      double zm = 0.0;
+      if (lane < BB && k + 1 + lane < n) zm = W[(k + 1 + lane) % LR][kc] * rp;
+#pragma unroll
+      for (int t = 0; t < BB / 2; ++t) {
+        const int i = 1 + (lane >> 5) + 2 * t;
+        if (k + i < n) {
+          const int rs = (k + i) % LR;
+          const double m = W[rs][kc] * rp;
+          W[rs][(k + c) % UW] -= m * uc;
+        }
+      }
+      if (lane < BB && k + 1 + lane < n) Z[(k + 1 + lane) % LR] -= zm * zk;
+      __syncthreads();
+      // row k + 17 enters the pivot row's slot (columns k+1 .. k+33); the other rows' column
+      // k slot becomes column k + 33, zero for them
+      const int r = k + LR;
+      if (lane < UW) {
+        const int col = k + 1 + lane;
+        W[ks][col % UW] = band(r, col);
+      }
+      if (lane < BB) W[(k + 1 + lane) % LR][kc] = 0.0;
+      if (lane == 0) Z[ks] = r < n ? bw.z[r] : 0.0;
+      __syncthreads();
+    }
+    if (!singular) {
+      for (int k = n - 1; k >= 0; --k) {
+        double s = (lane >= 1 && lane < UW && k + lane < n) ? Us[k][lane] * ys[k + lane] : 0.0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        if (lane == 0) ys[k] = (ys[k] - s) / Us[k][0];
+        __syncthreads();
+      }
+      double* __restrict__ yl = bw.Yt + (int64_t)l * n;
+      for (int j = lane; j < n; j += 64) yl[j] = ys[j];
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // kernel 3: beta = Q y, blocked WY, one workgroup per (cell, chunk of LC = 16 lambdas).
 //
 // The chunk's Y (n x 16) lives in REGISTERS: wave w owns the 16-row blocks b = w + 8 q, one
@@ -1366,7 +1506,8 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
                                              const void* cells, int ncells, int nmax,
                                              const double* lvec, int L, double* work,
                                              double* beta_out, int64_t ldo, int band_mode,
-                                             long long* tim, hipStream_t st) {
+                                             long long* tim, int* lu_list, int* lu_count,
+                                             int lu_cap, hipStream_t st) {
   const RidgeCellDesc* cd = static_cast<const RidgeCellDesc*>(cells);
   // band_mode 1 (or PFML_BAND_MODE=single, or phase timing): one workgroup per cell for the
   // whole reduction; 2 / default: the multi-workgroup form, three launches per panel.
@@ -1413,6 +1554,12 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   }
   hipLaunchKernelGGL(ridge_band_solve_kernel, dim3(ncells * ((L + 15) / 16)), dim3(NTS), 0, st,
                      cd, lvec, L, work, tim, ncells);
+  if (lu_count != nullptr) {   // non-SPD lambdas: pivoted banded LU (zeroed count, cap list)
+    hipLaunchKernelGGL(band_lu_flag_kernel, dim3((ncells * L + 255) / 256), dim3(256), 0, st, cd,
+                       ncells, L, work, lu_list, lu_count, lu_cap);
+    hipLaunchKernelGGL(ridge_band_lu_kernel, dim3(LU_WG), dim3(64), 0, st, cd, lvec, L, work,
+                       lu_list, lu_count, lu_cap);
+  }
   const int nch = (L + LC - 1) / LC;
   hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3(ncells * nch), dim3(NTB), 0, st, cd,
                      ncells, L, work, beta_out, ldo);

@@ -28,11 +28,12 @@ def _declare_hip(lib):
     P, I, L, D = C.c_void_p, C.c_int, C.c_int64, C.c_double
     lib.pfml_dgemm.argtypes = [I, I, I, I, I, I, D, P, L, L, P, L, L, D, P, L, L, P, L, P, L, P]
     lib.pfml_dgemm.restype = I
-    lib.pfml_ridge_grid.argtypes = [P, L, P, P, I, I, P, I, P, P, L, I, P]
+    lib.pfml_ridge_grid.argtypes = [P, L, P, P, I, I, P, I, P, P, L, I, P, P, I, P]
     lib.pfml_ridge_grid.restype = I
     lib.pfml_ridge_work_doubles.argtypes = [I, I]
     lib.pfml_ridge_work_doubles.restype = L
     lib.pfml_ridge_cell_desc_size.restype = I
+    lib.pfml_ridge_band_nmax.restype = I
     lib.pfml_quadform.argtypes = [P, L, P, P, L, P, I, P, I, I, P, P, P]
     lib.pfml_quadform.restype = I
     lib.pfml_quadform_job_desc_size.restype = I

@@ -189,16 +189,38 @@ def repairs_done() -> int:
     return int(sum(int(c.item()) for c in LAST_REPAIRS))
 
 
+def band_path(plan: dict) -> bool:
+    """True when the launch takes the band path (ridge_band.hip), whose non-SPD lambdas are
+    repaired in the band domain inside the launch; the tridiagonal path (n > 528 or
+    PFML_RIDGE_VARIANT) leaves NaN markers for ``repair_launch``."""
+    import os
+    return (plan["nmax"] <= nat.hip_lib().pfml_ridge_band_nmax()
+            and not os.environ.get("PFML_RIDGE_VARIANT", "band").startswith(("u", "bl", "f", "t"))
+            and not os.environ.get("PFML_RIDGE_UNBLOCKED"))
+
+
 def ridge_launch(plan: dict, d_desc: torch.Tensor, SD: torch.Tensor, Sr: torch.Tensor,
-                 lv: torch.Tensor, beta: torch.Tensor, band_mode: int = 0) -> None:
+                 lv: torch.Tensor, beta: torch.Tensor, band_mode: int = 0,
+                 repair: bool = True) -> torch.Tensor | None:
+    """Queue one ridge-grid launch; returns the device count of non-SPD systems re-solved by
+    the band path's pivoted banded LU (kernel 2b of ridge_band.hip), None when the launch has
+    no in-band repair (``repair=False`` or the tridiagonal path)."""
     P = SD.shape[-1]
     L = int(lv.numel())
     work = torch.empty(plan["work"], dtype=torch.float64, device=SD.device)
+    count = lst = None
+    if repair and band_path(plan):
+        count = torch.zeros(1, dtype=torch.int32, device=SD.device)
+        lst = torch.empty(plan["nc"] * L, dtype=torch.int32, device=SD.device)
     nat.check(nat.hip_lib().pfml_ridge_grid(SD.data_ptr(), P, Sr.data_ptr(), d_desc.data_ptr(),
                                             plan["nc"], plan["nmax"], lv.data_ptr(), L,
                                             work.data_ptr(), beta.data_ptr(), beta.shape[-1],
-                                            int(band_mode), nat.stream_of(SD)),
+                                            int(band_mode),
+                                            lst.data_ptr() if lst is not None else None,
+                                            count.data_ptr() if count is not None else None,
+                                            plan["nc"] * L, nat.stream_of(SD)),
               "pfml_ridge_grid")
+    return count
 
 
 def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n: np.ndarray,
@@ -207,8 +229,9 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
     """beta[c, l, :n_c] = solve(SD[src_c][:n,:n]*scale_c + l I, Sr[src_c][:n]*scale_c).
 
     SD: [S, P, P] running sums, Sr: [S, P]; returns [ncells, L, P] (zero beyond n_c).
-    Non-SPD systems (NaN-marked by the band path) are re-solved on the device by pivoted LU
-    (``repair_launch``, no host sync); ``repair=False`` leaves the NaN markers.
+    Non-SPD systems (NaN-marked by the banded Cholesky) are re-solved on the device by a
+    pivoted banded LU before the back-transform (band path) or a dense pivoted LU after it
+    (tridiagonal path, ``repair_launch``), no host sync; ``repair=False`` leaves the NaNs.
     """
     S, P, _ = SD.shape
     L = int(lvec.numel())
@@ -221,9 +244,10 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
         (d_desc,) = upload([plan["desc"]], SD.device)
         lv = lvec.to(device=SD.device, dtype=torch.float64).contiguous()
         SDc, Src = SD.contiguous(), Sr.contiguous()
-        ridge_launch(plan, d_desc, SDc, Src, lv, beta, band_mode)
+        count = ridge_launch(plan, d_desc, SDc, Src, lv, beta, band_mode, repair=repair)
         if repair:
-            LAST_REPAIRS[:] = [repair_launch(plan, d_desc, SDc, Src, lv, beta)]
+            LAST_REPAIRS[:] = [count if count is not None
+                               else repair_launch(plan, d_desc, SDc, Src, lv, beta)]
         return beta
     eye_cache = {}
     lv = lvec.to(dtype=SD.dtype)
@@ -373,8 +397,8 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     HIP stream, the big group first, so the small cells' whole chain runs on the CUs the big
     cells' one-workgroup-per-cell band reductions leave idle.  With few (multi-GPU shards) one
     chain in one stream.  Either way beta / obj rows are written in place from cached launch
-    plans, and the non-SPD systems are re-solved on the device between each group's ridge
-    grid and its utilities (``repair_launch``: no host sync, counts in ``LAST_REPAIRS``).
+    plans, and the non-SPD systems are re-solved on the device inside each group's ridge
+    launch (pivoted banded LU; no host sync, counts in ``LAST_REPAIRS``).
     """
     cell_src, cell_n = np.asarray(cell_src), np.asarray(cell_n)
     cell_scale = np.asarray(cell_scale, dtype=np.float64)
@@ -410,8 +434,8 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     for gi, stream in enumerate(streams):
         _, _, rp, qp, gmode = plan["groups"][gi]
         with torch.cuda.stream(stream):
-            ridge_launch(rp, dv[3 * gi], SD, Sr, lv, beta, mode if gmode is None else gmode)
-            counts.append(repair_launch(rp, dv[3 * gi], SD, Sr, lv, beta))
+            cnt = ridge_launch(rp, dv[3 * gi], SD, Sr, lv, beta, mode if gmode is None else gmode)
+            counts.append(cnt if cnt is not None else repair_launch(rp, dv[3 * gi], SD, Sr, lv, beta))
             quad_launch(qp, dv[3 * gi + 1], dv[3 * gi + 2], D, R, beta, obj)
     th("launch")
     for st in streams[:-1]:

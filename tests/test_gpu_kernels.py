@@ -401,19 +401,21 @@ def test_grid_search_bitwise_deterministic(gpu):
         assert torch.equal(k, runs[0][2])
 
 
-def test_ridge_device_repair_matches_lu(gpu):
+@pytest.mark.parametrize("P", [65, 513])
+def test_ridge_device_repair_matches_lu(gpu, P):
     """Systems the banded Cholesky cannot factor (here an indefinite Dbar: small lambda makes
     Dbar + lambda I indefinite) are NaN-marked by the band path and re-solved on the device by
-    pivoted LU before the utilities run - no host round trip; betas match np.linalg.solve."""
+    a pivoted banded LU before the back-transform - no host round trip; betas match
+    np.linalg.solve (dense pivoted LU).  P = 513: production-size cells (n = 513 / 257 / 20)."""
     from pfml.ops import ridge as rg
-    P = 65
-    X = _rand(2, 200, P, seed=61)
-    SD = X.transpose(1, 2) @ X / 200
+    X = _rand(2, max(200, 2 * P), P, seed=61)
+    SD = X.transpose(1, 2) @ X / X.shape[1]
     e, V = torch.linalg.eigh(SD[1])
     SD[1] = SD[1] - (e[0] + 0.7) * torch.outer(V[:, 0], V[:, 0]) * 2.0   # one eigen < 0
     Sr = _rand(2, P, seed=62)
     lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
-    src, nn, sc = np.array([0, 1, 1]), np.array([65, 65, 33]), np.array([1.0, 1.0, 1.0])
+    src, sc = np.array([0, 1, 1, 1]), np.array([1.0, 1.0, 1.0, 1.0])
+    nn = np.array([P, P, (P + 1) // 2, 20])
     ref = rg.ridge_grid(SD, Sr, src, nn, sc, lv)            # CPU: LU per lambda
     out = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
     assert rg.repairs_done() > 0
