@@ -212,7 +212,13 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
 
     # ---- 1. window sums over this rank's blocks ------------------------------------
     range_push("search.window_sums")
-    if nseg:
+    ready = None
+    if nseg and _pipelined_sums(dev, env, G, su["cell_n"]):
+        # one g at a time: g's big cells start their band reductions while the next g's sums
+        # stream (ridge_utilities waits per group on these events, not on the whole pass)
+        SD, Sr, ready = _window_sums_pipelined(reals, su, G, P, nseg, nYl)
+        totD = totr = None
+    elif nseg:
         # running sums at every block end in one pass over the symmetric upper triangles
         # (the burn-in block, rank 0 only, is a prefix segment and not an output row)
         db = su["dev_bounds"]
@@ -244,7 +250,8 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
     beta, obj = ridge_utilities(SD.reshape(G * nYl, P, P), Sr.reshape(G * nYl, P),
                                 su["cell_src"], su["cell_n"], su["cell_scale"], lvec,
                                 reals.denom.reshape(G * T, P, P),
-                                reals.r_tilde.reshape(G * T, P), su["jc"], su["jm"], su["jn"])
+                                reals.r_tilde.reshape(G * T, P), su["jc"], su["jm"], su["jn"],
+                                ready=ready)
     beta = beta.view(G, nYl, nP, L, P)
     obj = obj.view(su["nVr"], G, nP, L)
     range_pop()
@@ -377,6 +384,61 @@ def recompute_cells(grid: GridResult, reals: PfmlReals, cells) -> dict:
 # ---------------------------------------------------------------------------------------
 # Scores (K17): expanding mean by (p, l) over eom_ret, dense rank per eom_ret.
 # ---------------------------------------------------------------------------------------
+def _pipelined_sums(dev, env, G: int, cell_n) -> bool:
+    """Per-g pipelined window sums (opt-in, PFML_PIPE_SUMS=1): one device holding the whole
+    grid (not a multi-rank shard), 2 g (three streams in all) and the two-stream band policy
+    (many big cells).  Measured on MI355X (profiles/r02_pipe_sums_ab.json): eager launches
+    6.06-6.11 vs 6.48-6.54 ms per step, but under HIP-graph replay (the default) 6.00 vs
+    6.02-6.10 ms - the graph executor regroups the three branches onto its own queues and the
+    g = 1 big cells then wait ~0.3 ms for CUs behind the small cells - so it stays off."""
+    import os
+    from ..ops.ridge import band_policy
+    if (dev.type != "cuda" or env.is_dist or G != 2
+            or os.environ.get("PFML_PIPE_SUMS", "0") != "1"):
+        return False
+    return band_policy(np.asarray(cell_n))[1]
+
+
+def _window_sums_pipelined(reals: PfmlReals, su: dict, G: int, P: int, nseg: int, nYl: int):
+    """Window sums of every g into one [G, nYl, P, P] stack, g after g: g = 0 on the current
+    stream, g > 0 on a side stream chained after g - 1 (the passes are HBM-bound, so running
+    them concurrently would only delay g = 0); the r̄ sums (tiny) lead that side stream.
+    Returns (SD, Sr, ready) with ready as ridge_utilities takes it.  Three streams in all:
+    current, this side stream, and the small cells' stream in ridge_utilities."""
+    from ..ops.ridge import _side_stream
+    dev = reals.denom.device
+    T = reals.denom.shape[1]
+    db = su["dev_bounds"]
+    skip = nseg - nYl
+    cur = torch.cuda.current_stream(dev)
+    side = _side_stream(dev, 16)
+    side.wait_stream(cur)
+    SD = torch.empty((G, nYl, P, P), dtype=torch.float64, device=dev)
+    with torch.cuda.stream(side):
+        Sr = segment_sums(reals.r_tilde.reshape(G * T, P), su["starts"], su["stops"],
+                          dev_bounds=None if db is None else db[2:]).view(G, nseg, P)
+        Sr = _cumsum0(Sr.transpose(0, 1)).transpose(0, 1)[:, skip:].contiguous()
+        ev_r = torch.cuda.Event()
+        ev_r.record(side)
+    events = []
+    for g in range(G):
+        st = cur if g == 0 else side
+        if g > 0:
+            st.wait_event(events[-1])
+        with torch.cuda.stream(st):
+            window_prefix_sym(reals.denom[g:g + 1], su["st"], su["sp"],
+                              dev_bounds=None if db is None else db[:2], skip=skip,
+                              out=SD[g:g + 1])
+            ev = torch.cuda.Event()
+            ev.record(st)
+        events.append(ev)
+    # big cells of g run on the stream that summed g (g = 0: after its sums on cur; g > 0:
+    # after its sums on the side stream); only the r̄ sums need an event wait
+    ready = {"key": su["cell_src"] // max(nYl, 1), "streams": [cur] + [side] * (G - 1),
+             "events": [[ev_r]] + [[]] * (G - 1), "all": [events[-1], ev_r]}
+    return SD, Sr, ready
+
+
 def _cumsum0(x: torch.Tensor) -> torch.Tensor:
     """cumsum along dim 0 as an innermost-dim scan (the outer-dim scan kernel of torch-ROCm
     takes ~0.2-0.4 ms on these [months, cells] shapes; the innermost one ~30 us)."""

@@ -8,6 +8,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+import os
+
 import numpy as np
 import torch
 
@@ -47,15 +49,19 @@ nat.register_hip("pfml_window_prefix_sym", [C.c_void_p, C.c_int, C.c_int, C.c_in
 
 
 def window_prefix_sym(X: torch.Tensor, starts, stops, dev_bounds=None,
-                      skip: int = 0) -> torch.Tensor:
+                      skip: int = 0, out: torch.Tensor | None = None) -> torch.Tensor:
     """out[g, s - skip] = sum of X[g, t] over the months of segments 0..s, for s >= skip (X:
     [G, T, P, P], every X[g, t] symmetric; the first ``skip`` segments only feed the prefix).
-    Device: one pass over the upper triangles (csrc/segsum.hip), contiguous output."""
+    Device: one pass over the upper triangles (csrc/segsum.hip), contiguous output (``out``:
+    a preallocated contiguous [G, S - skip, P, P] destination, e.g. one g's slice)."""
     G, T, P, _ = X.shape
     starts = np.asarray(starts, dtype=np.int32)
     stops = np.asarray(stops, dtype=np.int32)
     S = len(starts)
-    out = torch.empty((G, max(S - skip, 0), P, P), dtype=X.dtype, device=X.device)
+    if out is None:
+        out = torch.empty((G, max(S - skip, 0), P, P), dtype=X.dtype, device=X.device)
+    elif out.shape != (G, max(S - skip, 0), P, P) or not out.is_contiguous():
+        raise ValueError("window_prefix_sym: out must be a contiguous [G, S - skip, P, P] tensor")
     if S == 0:
         return out
     if nat.is_device(X):
@@ -348,19 +354,24 @@ _UTIL_PLANS: dict = {}
 
 
 def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell, job_month,
-                    job_n, split: bool = True) -> dict:
+                    job_n, split: bool = True, big_key: np.ndarray | None = None) -> dict:
     """Launch plan of ridge_utilities on a device, cached: the descriptors depend only on the
     grid's shape (cells, jobs, P, L), so repeated grid searches (every step of a run, every
     benchmark step) reuse the uploaded device copies and skip all host planning.  Each group's
     cells / jobs write straight into the full beta / obj arrays (global out offsets)."""
     key = (P, L, str(dev), split, cell_src.tobytes(), cell_n.tobytes(), cell_scale.tobytes(),
-           job_cell.tobytes(), job_month.tobytes(), job_n.tobytes())
+           job_cell.tobytes(), job_month.tobytes(), job_n.tobytes(),
+           None if big_key is None else big_key.tobytes())
     hit = _UTIL_PLANS.get(key)
     if hit is not None:
         return hit
     big = cell_n == cell_n.max()
     nhy = _hybrid_cells(int(big.sum())) if split else 0
-    if split and nhy:
+    if split and big_key is not None:
+        # one big-cell group per key (pipelined window sums), then the small cells
+        parts = tuple((big & (big_key == k), None) for k in np.unique(big_key[big]))
+        parts += ((~big, BAND_SINGLE),)
+    elif split and nhy:
         # the first nhy big cells (in cell order) -> multi-workgroup group
         hy = big & (np.cumsum(big) <= nhy)
         parts = ((big & ~hy, BAND_SINGLE), (hy, BAND_MULTI), (~big, BAND_SINGLE))
@@ -389,7 +400,7 @@ def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell,
 
 def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_scale,
                     lvec: torch.Tensor, D: torch.Tensor, R: torch.Tensor, job_cell, job_month,
-                    job_n) -> tuple[torch.Tensor, torch.Tensor]:
+                    job_n, ready: dict | None = None) -> tuple[torch.Tensor, torch.Tensor]:
     """(beta, obj) = (ridge_grid(...), quadform_utilities(D, R, beta, jobs)).
 
     On a device with many big cells (one GPU holds the grid) the cells split into the
@@ -399,6 +410,12 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     chain in one stream.  Either way beta / obj rows are written in place from cached launch
     plans, and the non-SPD systems are re-solved on the device inside each group's ridge
     launch (pivoted banded LU; no host sync, counts in ``LAST_REPAIRS``).
+
+    ``ready`` (grid_search's pipelined window sums): {"key": per-cell group key (the cell's
+    g), "streams": per key the stream that produced its sums, "events": per key the extra
+    events it waits for, "all": events after which every input is complete}.  The big cells
+    then split by key into one chain per key, issued on that key's stream so it starts as soon
+    as its own sums are done; the small cells wait for "all" on a side stream.
     """
     cell_src, cell_n = np.asarray(cell_src), np.asarray(cell_n)
     cell_scale = np.asarray(cell_scale, dtype=np.float64)
@@ -409,13 +426,16 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
         beta = ridge_grid(SD, Sr, cell_src, cell_n, cell_scale, lvec, band_mode=mode)
         return beta, quadform_utilities(D, R, beta, job_cell, job_month, job_n)
     split = two and len(np.unique(cell_n)) >= 2
+    if not split:
+        ready = None
     th = _HostClock()
     S, P, _ = SD.shape
     L = int(lvec.numel())
     nc = len(cell_src)
     dev = SD.device
     plan = _utilities_plan(P, L, dev, cell_src, cell_n, cell_scale, job_cell, job_month, job_n,
-                           split=split)
+                           split=split,
+                           big_key=None if ready is None else np.asarray(ready["key"]))
     th("plans")
     # every [L, P] block is written whole by the ridge grid (zero padding past n included), so
     # no fill on the stream the big cells' chain forks from
@@ -427,18 +447,36 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     dv = plan["dv"]
     ng = len(plan["groups"])
     # big cells' factorisations issued first, on side streams; the small cells on `cur`
-    streams = [_side_stream(dev, k) for k in range(ng - 1)] + [cur]
-    for st in streams[:-1]:
-        st.wait_stream(cur)
+    if ready is None:
+        streams = [_side_stream(dev, k) for k in range(ng - 1)] + [cur]
+        for st in streams[:-1]:
+            st.wait_stream(cur)
+    else:
+        # group k < ng - 1 holds the big cells of key k (in key order) and runs on the stream
+        # that produced key k's sums (stream order = the dependency, and no more streams than
+        # hardware queues: two streams sharing a queue serialise); the small cells wait for
+        # everything on one more side stream
+        streams = list(ready["streams"]) + [_side_stream(dev, 0)]
+        for k, st in enumerate(streams[:-1]):
+            for ev in ready["events"][k]:
+                st.wait_event(ev)
+        for ev in ready["all"]:
+            streams[-1].wait_event(ev)
     counts = []
-    for gi, stream in enumerate(streams):
+    order = list(range(ng))
+    if ready is not None and os.environ.get("PFML_PIPE_ORDER", "small_first") == "small_first":
+        order = [ng - 1] + order[:-1]            # (graph branch layout: see grid_search)
+    for gi in order:
+        stream = streams[gi]
         _, _, rp, qp, gmode = plan["groups"][gi]
         with torch.cuda.stream(stream):
             cnt = ridge_launch(rp, dv[3 * gi], SD, Sr, lv, beta, mode if gmode is None else gmode)
             counts.append(cnt if cnt is not None else repair_launch(rp, dv[3 * gi], SD, Sr, lv, beta))
             quad_launch(qp, dv[3 * gi + 1], dv[3 * gi + 2], D, R, beta, obj)
     th("launch")
-    for st in streams[:-1]:
+    for st in streams:
+        if st == cur:
+            continue
         cur.wait_stream(st)
         for t in (SD, Sr, D, R, lv, beta, obj, *counts):
             t.record_stream(st)

@@ -401,6 +401,46 @@ def test_grid_search_bitwise_deterministic(gpu):
         assert torch.equal(k, runs[0][2])
 
 
+def test_grid_search_pipelined_sums_bitwise(gpu, monkeypatch):
+    """Per-g pipelined window sums (g's big cells start while g + 1's sums stream; 3 ridge
+    groups on their own streams) give the same betas / utilities bit for bit as the one-pass
+    sums + 2 groups, eager and under HIP-graph capture."""
+    from pfml.config import Config
+    from pfml.models.search import PfmlReals, grid_search
+    from pfml.utils.dates import mi_from_ym
+    monkeypatch.setenv("PFML_BAND_MODE", "single")
+    monkeypatch.setenv("PFML_RIDGE_STREAMS", "2")
+    cfg = Config.default().override(["pf_ml.p_vec=[16,64]", "pf.dates.start_year=2001",
+                                     "pf.dates.end_yr=2006"])
+    G, P = 2, 65
+    months = np.arange(mi_from_ym(1994, 3), mi_from_ym(2006, 11) + 1)
+    T = len(months)
+    X = _rand(G * T, 80, P, seed=93).to(gpu)
+    D = (X.transpose(1, 2) @ X / 80).view(G, T, P, P).contiguous()
+    r = (0.1 * _rand(G, T, P, seed=94)).to(gpu)
+    reals = PfmlReals(months, r, D)
+    out = {}
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("PFML_PIPE_SUMS", pipe)
+        res = grid_search(reals, cfg)
+        out[pipe] = (res.beta.cpu(), res.obj.cpu())
+        if pipe == "1":                               # captured replay of the pipelined form
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                grid_search(reals, cfg)
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                res_g = grid_search(reals, cfg)
+            g.replay()
+            torch.cuda.synchronize()
+            out["graph"] = (res_g.beta.cpu(), res_g.obj.cpu())
+    for k in ("1", "graph"):
+        assert torch.equal(out[k][0], out["0"][0]) and torch.equal(out[k][1], out["0"][1]), k
+
+
 @pytest.mark.parametrize("P", [65, 513])
 def test_ridge_device_repair_matches_lu(gpu, P):
     """Systems the banded Cholesky cannot factor (here an indefinite Dbar: small lambda makes
