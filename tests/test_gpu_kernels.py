@@ -340,6 +340,14 @@ def test_window_prefix_sym(gpu):
         assert got.shape == (2, 4 - skip, 37, 37) and got.is_contiguous()
         assert torch.allclose(got, ref[:, skip:], rtol=1e-13, atol=1e-12)
         assert torch.equal(got, got.transpose(-1, -2))
+    for P in (64, 513):                         # even P; P + 1 > 512 (three entries per lane)
+        Y = _rand(1, 12, P, P, seed=82 + P)
+        Y = Y + Y.transpose(-1, -2)
+        st2, sp2 = [0, 2, 5, 11], [2, 5, 11, 12]
+        ref3 = window_prefix_sym(Y, st2, sp2, skip=1)
+        got = window_prefix_sym(Y.to(gpu), st2, sp2, skip=1).cpu()
+        assert torch.allclose(got, ref3, rtol=1e-13, atol=1e-12)
+        assert torch.equal(got, got.transpose(-1, -2))
 
 
 @pytest.mark.parametrize("compat", [True, False])
