@@ -14,11 +14,19 @@ import torch.distributed as dist
 from .dist import env
 
 
+def _staged(x: torch.Tensor) -> bool:
+    """gloo over device tensors (PFML_DIST_BACKEND=gloo: several ranks sharing one GPU, a
+    rehearsal of the multi-GPU path where RCCL cannot run): the message goes via the host."""
+    return env().backend == "gloo" and x.is_cuda
+
+
 def all_gather_cat(x: torch.Tensor) -> torch.Tensor:
     """Concatenate equally-shaped tensors of every rank along dim 0 (rank order)."""
     e = env()
     if not e.is_dist:
         return x
+    if _staged(x):
+        return all_gather_cat(x.cpu()).to(x.device)
     x = x.contiguous()
     out = torch.empty((e.world_size * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=x.device)
     dist.all_gather_into_tensor(out, x)
@@ -78,6 +86,8 @@ def all_reduce_max(v: float, device=None) -> float:
     if not e.is_dist:
         return float(v)
     t = torch.tensor([float(v)], dtype=torch.float64, device=device or e.device)
+    if _staged(t):
+        t = t.cpu()
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -85,7 +95,12 @@ def all_reduce_max(v: float, device=None) -> float:
 def all_reduce_sum_(t: torch.Tensor) -> torch.Tensor:
     e = env()
     if e.is_dist:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        if _staged(t):
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t
 
 
@@ -128,7 +143,7 @@ def send_next(x: torch.Tensor) -> None:
     w_start vector: N doubles over one xGMI link)."""
     e = env()
     if e.is_dist and e.rank + 1 < e.world_size:
-        dist.send(x.contiguous(), dst=e.rank + 1)
+        dist.send(x.cpu() if _staged(x) else x.contiguous(), dst=e.rank + 1)
 
 
 def recv_prev(like: torch.Tensor) -> torch.Tensor:
@@ -136,5 +151,10 @@ def recv_prev(like: torch.Tensor) -> torch.Tensor:
     e = env()
     out = torch.empty_like(like)
     if e.is_dist and e.rank > 0:
-        dist.recv(out, src=e.rank - 1)
+        if _staged(out):
+            h = torch.empty_like(out, device="cpu")
+            dist.recv(h, src=e.rank - 1)
+            out.copy_(h)
+        else:
+            dist.recv(out, src=e.rank - 1)
     return out

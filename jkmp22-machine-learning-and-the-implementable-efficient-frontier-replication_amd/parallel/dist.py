@@ -55,9 +55,12 @@ def init(device: str = "auto", timeout_s: int = 600) -> DistEnv:
     if ws > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = "nccl" if dev.type == "cuda" else "gloo"
+        # PFML_DIST_BACKEND=gloo with GPUs: ranks may share a device (a rehearsal of the
+        # multi-GPU path on a one-GPU box; collectives stage through the host)
+        backend = os.environ.get("PFML_DIST_BACKEND", backend)
         if not dist.is_initialized():
             kw = {}
-            if dev.type == "cuda":
+            if dev.type == "cuda" and backend == "nccl":
                 kw["device_id"] = dev
             dist.init_process_group(backend=backend, rank=rank, world_size=ws,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
