@@ -11,7 +11,7 @@
 //
 // Two launches replace the ~25 small torch kernels (sort, scans, scatters) per frame, and
 // pfml_validation_scores_all does every frame of a grid search in the same two launches:
-//   prefix_mean_kernel  16 columns x 16 row chunks per workgroup: chunk sums, LDS offsets,
+//   prefix_mean_kernel  4 columns x 64 row chunks per workgroup: chunk sums, LDS offsets,
 //                       chunk rescans, NaN carry fix-up (loads batched and clamped)
 //   dense_rank_kernel   one workgroup per month: bitonic sort of <= 1024 (key, index) pairs in
 //                       LDS, adjacent-difference + block scan for the dense rank, scatter back
@@ -22,7 +22,8 @@ namespace {
 constexpr int RK_N = 1024;          // max values per month (k * C <= 1024)
 constexpr int RK_T = 256;
 
-constexpr int PM_COLS = 16, PM_RG = 16;   // prefix mean: 16 columns x 16 row chunks per WG
+constexpr int PM_COLS = 4, PM_RG = 64;    // prefix mean: 4 columns x 64 row chunks per WG
+                                          // (short chunks: fewer dependent load rounds)
 
 // Frames: blockIdx.y = f of nF frames; frame f covers g in [f0 + f, f1 + f) clipped as
 // (g0, g1) = compat ? (0, f + 1) : (f, f + 1) when `multi`, else the single (g0, g0 + k).  Its
