@@ -14,7 +14,7 @@
 //   prefix_mean_kernel  4 columns x 64 row chunks per workgroup: chunk sums, LDS offsets,
 //                       chunk rescans, NaN carry fix-up (loads batched and clamped)
 //   dense_rank_kernel   one workgroup per month: bitonic sort of <= 1024 (key, index) pairs in
-//                       LDS, adjacent-difference + block scan for the dense rank, scatter back
+//                       LDS (one 16-byte element each, order-preserving 64-bit keys), adjacent-difference + block scan for the dense rank, scatter back
 #include "common.h"
 
 namespace {
@@ -124,22 +124,25 @@ __global__ __launch_bounds__(256) void prefix_mean_kernel(const double* __restri
   }
 }
 
-// descending order, NaN after every number (unranked), padding last
-__device__ __forceinline__ bool before(double a, int ia, double b, int ib) {
-  if (ia < 0) return false;                 // padding never precedes
-  if (ib < 0) return true;
-  const bool na = a != a, nb = b != b;
-  if (na != nb) return nb;
-  if (na) return ia < ib;
-  return a > b || (a == b && ia < ib);
+// Sort key of one value: an unsigned 64-bit word whose ASCENDING order is the rank order -
+// descending value (order-preserving bit map of the double, then inverted), every NaN after
+// every number (unranked), padding after everything; +0 and -0 share a key (equal values rank
+// alike).  Ties are broken by the index, so the sort is a total order on (key, index).
+__device__ __forceinline__ unsigned long long rank_key(double x) {
+  if (x != x) return ~0ull - 1;
+  if (x == 0.0) x = 0.0;
+  const unsigned long long u = __double_as_longlong(x);
+  const unsigned long long asc = (u >> 63) ? ~u : (u | (1ull << 63));   // ascending in x
+  return ~asc - 2;                                                     // descending, < NaN
 }
+constexpr unsigned long long PAD_KEY = ~0ull;
 
 __global__ __launch_bounds__(RK_T) void dense_rank_kernel(const double* __restrict__ cum_all,
                                                           int Ns, int nV, int C,
                                                           double* __restrict__ rank_all,
                                                           int multi, int compat) {
-  __shared__ double key[RK_N];
-  __shared__ int idx[RK_N];
+  // (key, index) pairs as one 16-byte LDS element: one ds_read_b128 / ds_write_b128 each
+  __shared__ ulonglong2 el[RK_N];
   __shared__ int wsum[RK_T / 64];
   int g0, k;
   int64_t off;
@@ -153,34 +156,37 @@ __global__ __launch_bounds__(RK_T) void dense_rank_kernel(const double* __restri
   const int v = blockIdx.x, t = threadIdx.x;
   const double* src = cum + (int64_t)v * N;
   for (int i = t; i < NS; i += RK_T) {
-    key[i] = src[min(i, N - 1)];            // (padding entries carry idx -1)
-    idx[i] = (i < N) ? i : -1;
+    ulonglong2 e;
+    e.x = (i < N) ? rank_key(src[i]) : PAD_KEY;
+    e.y = (unsigned long long)i;                     // padding: indices >= N
+    el[i] = e;
   }
   __syncthreads();
-  // bitonic sort of NS elements, "before" order
+  // bitonic sort of NS (key, index) pairs, ascending
   for (int size = 2; size <= NS; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int p = t; p < NS / 2; p += RK_T) {
         const int lo = 2 * p - (p & (stride - 1)), hi = lo + stride;
         const bool up = (lo & size) == 0;
-        const double ka = key[lo], kb = key[hi];
-        const int ia = idx[lo], ib = idx[hi];
-        const bool swap = up ? before(kb, ib, ka, ia) : before(ka, ia, kb, ib);
-        if (swap) {
-          key[lo] = kb; key[hi] = ka;
-          idx[lo] = ib; idx[hi] = ia;
+        const ulonglong2 a = el[lo], b = el[hi];
+        const bool gt = a.x > b.x || (a.x == b.x && a.y > b.y);
+        if (gt == up) {
+          el[lo] = b;
+          el[hi] = a;
         }
       }
       __syncthreads();
     }
   }
-  // dense rank: new[i] = (i == 0) || key[i] != key[i-1]; inclusive scan, 4 per thread
+  // dense rank: new[i] = (i == 0) || key[i] != key[i-1] among the ranked (finite) keys;
+  // inclusive scan, 4 per thread
+  constexpr unsigned long long NAN_KEY = ~0ull - 1;
   int nw[4], run = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int i = 4 * t + q;
-    const bool real = i < NS && idx[i] >= 0 && key[i] == key[i];   // NaN: not ranked
-    nw[q] = real && (i == 0 || key[i] != key[i - 1]) ? 1 : 0;
+    const bool real = i < NS && el[i].x < NAN_KEY;
+    nw[q] = real && (i == 0 || el[i].x != el[i - 1].x) ? 1 : 0;
     run += nw[q];
   }
   // block exclusive scan of run
@@ -201,7 +207,8 @@ __global__ __launch_bounds__(RK_T) void dense_rank_kernel(const double* __restri
   for (int q = 0; q < 4; ++q) {
     const int i = 4 * t + q;
     acc += nw[q];
-    if (i < NS && idx[i] >= 0) dst[idx[i]] = (key[i] == key[i]) ? (double)acc : __builtin_nan("");
+    if (i < NS && el[i].x != PAD_KEY)
+      dst[el[i].y] = (el[i].x < NAN_KEY) ? (double)acc : __builtin_nan("");
   }
 }
 

@@ -481,6 +481,9 @@ def validation_scores(obj: torch.Tensor, frame_g: int, compat: bool):
     key = torch.where(isn, torch.full_like(vals, float("-inf")), vals)
     sv, idx = torch.sort(key, dim=1, descending=True, stable=True)
     snan = torch.gather(isn, 1, idx)
+    # NaN after every number, a real -inf included (stable: value order kept within groups)
+    o2 = torch.sort(snan.to(torch.int8), dim=1, stable=True)[1]
+    sv, idx, snan = sv.gather(1, o2), idx.gather(1, o2), snan.gather(1, o2)
     new = torch.ones_like(sv, dtype=torch.int64)
     new[:, 1:] = (sv[:, 1:] != sv[:, :-1]).to(torch.int64)
     new[snan] = 0

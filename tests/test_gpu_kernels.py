@@ -493,3 +493,19 @@ def test_validation_scores_nan_cells(gpu):
             fin = rv[~torch.isnan(rv)]
             assert fin.min() == 1 and torch.equal(torch.unique(fin),
                                                   torch.arange(1, int(fin.max()) + 1).double())
+
+
+def test_validation_rank_ties_zeros_infs(gpu):
+    """Dense rank on the device (order-preserving 64-bit sort keys) on exact ties, +0 / -0
+    (one rank), +-inf and NaN, against the CPU (pandas-semantics) ranks."""
+    from pfml.models.search import validation_scores
+    obj = torch.round(_rand(24, 2, 2, 101, seed=72) * 4) / 4   # many exact ties
+    obj[:, 0, 0, :10] = 0.0
+    obj[:, 1, 0, 10:20] = -0.0
+    obj[3, 0, 1, 5] = float("inf")
+    obj[4, 1, 1, 6] = -float("inf")
+    obj[:, 1, 1, 50] = float("nan")
+    for compat in (True, False):
+        _, _, r0 = validation_scores(obj, 1, compat)
+        _, _, r1 = validation_scores(obj.to(gpu), 1, compat)
+        assert torch.equal(r0.nan_to_num(-1), r1.cpu().nan_to_num(-1))
