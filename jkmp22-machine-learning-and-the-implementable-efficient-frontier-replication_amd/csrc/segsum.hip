@@ -164,3 +164,56 @@ extern "C" hipError_t pfml_window_prefix_sym(const double* X, int P, int T, int 
                      nseg, skip, out, scratch);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------
+// Expanding-window sums of the month VECTORS (r_tilde) in one launch:
+//   out[g, s - skip, c] = sum over segments s' <= s of sum_{t in [start_s', stop_s')} X[g, t, c]
+// X: [G, T, E], out: [G, nseg - skip, E].  Workgroup (64 columns, g): its 16 row groups sum
+// the segments (eight months in flight per lane) into LDS, then one row group runs the
+// prefix over the segments in segment order.  Replaces segment sums + a transposing copy,
+// a scan and two copies (~55 us of small launches ahead of the ridge grid).
+namespace {
+constexpr int WV_COLS = 64, WV_SEG = 128, WV_T = 1024, WV_RG = WV_T / WV_COLS;
+__global__ __launch_bounds__(WV_T) void window_prefix_vec_kernel(
+    const double* __restrict__ X, int64_t E, int T, const int* __restrict__ seg_start,
+    const int* __restrict__ seg_stop, int nseg, int skip, double* __restrict__ out) {
+  __shared__ double part[WV_SEG][WV_COLS];
+  const int lc = threadIdx.x % WV_COLS, ry = threadIdx.x / WV_COLS;
+  const int g = blockIdx.y, c = blockIdx.x * WV_COLS + lc;
+  const bool cv = c < E;
+  const double* src = X + (int64_t)g * T * E + (cv ? c : 0);
+  for (int s = ry; s < nseg; s += WV_RG) {
+    const int a = seg_start[s], b = seg_stop[s];
+    double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int tm = a; tm < b; tm += 8) {          // eight months in flight
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = (tm + u < b) ? src[(int64_t)(tm + u) * E] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += x[u];
+    }
+    part[s][lc] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  }
+  __syncthreads();
+  if (ry == 0 && cv) {
+    double run = 0.0;
+    double* o = out + (int64_t)g * (nseg - skip) * E + c;
+    for (int s = 0; s < nseg; ++s) {
+      run += part[s][lc];
+      if (s >= skip) o[(int64_t)(s - skip) * E] = run;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int pfml_window_prefix_vec_max_segments() { return WV_SEG; }
+
+extern "C" hipError_t pfml_window_prefix_vec(const double* X, int64_t E, int T, int G,
+                                             const int* seg_start, const int* seg_stop, int nseg,
+                                             int skip, double* out, hipStream_t st) {
+  if (nseg <= 0 || E <= 0 || G <= 0 || nseg - skip <= 0) return hipSuccess;
+  if (nseg > WV_SEG || skip < 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(window_prefix_vec_kernel, dim3((unsigned)((E + WV_COLS - 1) / WV_COLS), G),
+                     dim3(WV_T), 0, st, X, E, T, seg_start, seg_stop, nseg, skip, out);
+  return hipGetLastError();
+}

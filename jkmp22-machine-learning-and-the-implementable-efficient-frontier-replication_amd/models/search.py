@@ -30,7 +30,7 @@ import torch
 
 from ..config import Config
 from ..ops import _native as nat
-from ..ops.ridge import _HostClock, ridge_utilities, segment_sums, window_prefix_sym
+from ..ops.ridge import _HostClock, ridge_utilities, window_prefix_sym, window_prefix_vec
 from ..parallel import collectives as coll
 from ..parallel.dist import env as dist_env
 from ..utils.dates import mi_from_ym, month_end
@@ -225,9 +225,8 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
         skip = nseg - nYl
         SD = window_prefix_sym(reals.denom, su["st"], su["sp"],
                                dev_bounds=None if db is None else db[:2], skip=skip)
-        Sr = segment_sums(reals.r_tilde.reshape(G * T, P), su["starts"], su["stops"],
-                          dev_bounds=None if db is None else db[2:]).view(G, nseg, P)
-        Sr = _cumsum0(Sr.transpose(0, 1)).transpose(0, 1)[:, skip:]
+        Sr = window_prefix_vec(reals.r_tilde.contiguous(), su["st"], su["sp"],
+                               dev_bounds=None if db is None else db[:2], skip=skip)
         totD, totr = SD[:, -1], Sr[:, -1]
     else:
         SD = torch.zeros((G, 0, P, P), dtype=torch.float64, device=dev)
@@ -415,9 +414,8 @@ def _window_sums_pipelined(reals: PfmlReals, su: dict, G: int, P: int, nseg: int
     side.wait_stream(cur)
     SD = torch.empty((G, nYl, P, P), dtype=torch.float64, device=dev)
     with torch.cuda.stream(side):
-        Sr = segment_sums(reals.r_tilde.reshape(G * T, P), su["starts"], su["stops"],
-                          dev_bounds=None if db is None else db[2:]).view(G, nseg, P)
-        Sr = _cumsum0(Sr.transpose(0, 1)).transpose(0, 1)[:, skip:].contiguous()
+        Sr = window_prefix_vec(reals.r_tilde.contiguous(), su["st"], su["sp"],
+                               dev_bounds=None if db is None else db[:2], skip=skip)
         ev_r = torch.cuda.Event()
         ev_r.record(side)
     events = []

@@ -43,6 +43,39 @@ def segment_sums(X: torch.Tensor, starts, stops, dev_bounds=None) -> torch.Tenso
     return out
 
 
+nat.register_hip("pfml_window_prefix_vec", [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_void_p,
+                                            C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p])
+nat.register_hip("pfml_window_prefix_vec_max_segments", [], C.c_int)
+
+
+def window_prefix_vec(X: torch.Tensor, starts, stops, dev_bounds=None,
+                      skip: int = 0) -> torch.Tensor:
+    """out[g, s - skip] = sum of X[g, t] over the months of segments 0..s, for s >= skip (X:
+    [G, T, E], e.g. the r_tilde vectors).  Device: one launch (csrc/segsum.hip); contiguous
+    [G, S - skip, E] output."""
+    G, T, E = X.shape
+    starts = np.asarray(starts, dtype=np.int32)
+    stops = np.asarray(stops, dtype=np.int32)
+    S = len(starts)
+    out = torch.empty((G, max(S - skip, 0), E), dtype=X.dtype, device=X.device)
+    if S - skip <= 0:
+        return out
+    if nat.is_device(X) and S <= nat.hip_lib().pfml_window_prefix_vec_max_segments():
+        if X.dtype != torch.float64 or not X.is_contiguous():
+            raise ValueError("window_prefix_vec: contiguous fp64 required")
+        st, sp = dev_bounds if dev_bounds is not None else upload([starts, stops], X.device)
+        nat.check(nat.hip_lib().pfml_window_prefix_vec(
+            X.data_ptr(), E, T, G, st.data_ptr(), sp.data_ptr(), S, int(skip), out.data_ptr(),
+            nat.stream_of(X)), "pfml_window_prefix_vec")
+        return out
+    acc = torch.zeros((G, E), dtype=X.dtype, device=X.device)
+    for s in range(S):
+        acc = acc + X[:, starts[s]:stops[s]].sum(1)
+        if s >= skip:
+            out[:, s - skip] = acc
+    return out
+
+
 nat.register_hip("pfml_window_prefix_sym", [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                             C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                             C.c_void_p])

@@ -321,6 +321,17 @@ def test_gemm_lowp(gpu, fmt, ta, tb):
     assert (out - exact).abs().max().item() / scale < (1e-2 if fmt == "bf16" else 1e-1)
 
 
+def test_window_prefix_vec(gpu):
+    """One-launch expanding-window sums of month vectors (r_tilde), incl. gaps and skip."""
+    from pfml.ops.ridge import window_prefix_vec
+    X = _rand(2, 40, 513, seed=83)
+    for st, sp, skip in (([0, 7, 9, 20], [7, 9, 20, 40], 0), ([0, 10, 11], [5, 11, 40], 1)):
+        ref = window_prefix_vec(X, st, sp, skip=skip)
+        got = window_prefix_vec(X.to(gpu), st, sp, skip=skip).cpu()
+        assert got.shape == ref.shape and got.is_contiguous()
+        assert torch.allclose(got, ref, rtol=1e-13, atol=1e-13)
+
+
 def test_window_prefix_sym(gpu):
     """Fused expanding-window sums over the upper triangles of symmetric month matrices."""
     from pfml.ops.ridge import window_prefix_sym
