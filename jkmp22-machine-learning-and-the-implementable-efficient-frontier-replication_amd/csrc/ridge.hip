@@ -929,7 +929,8 @@ static long long* g_ridge_timing = nullptr;
 extern "C" void pfml_ridge_set_timing(long long* buf) { g_ridge_timing = buf; }
 
 // band_mode: 0 = PFML_BAND_MODE / default, 1 = one workgroup per cell, 2 = multi-workgroup.
-// lu_list / lu_count / lu_cap (band path only; count zeroed by the caller, nullptr = off): the
+// lu_list / lu_count / lu_cap (band path only; count zeroed on the stream by the banded solve,
+// nullptr = off): the
 // in-band pivoted-LU repair of non-SPD lambdas; the tridiagonal path leaves its NaN markers
 // to the dense repair (ridge_repair.hip).
 extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const double* Sr,

@@ -1093,8 +1093,11 @@ constexpr int NTS = 256;      // 4 waves x 4 rows = 16 lambdas per workgroup
 // 158 VGPRs: 3 waves per SIMD (the entering rows come from LDS, not a register prefetch).
 __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
     const RidgeCellDesc* __restrict__ cells, const double* __restrict__ lvec, int L,
-    double* __restrict__ work, long long* __restrict__ tim, int ncells) {
+    double* __restrict__ work, long long* __restrict__ tim, int ncells,
+    int* __restrict__ lu_count) {
   const long long t_start = (long long)__builtin_amdgcn_s_memtime();
+  // the repair list count of kernel 2b starts at zero (no separate fill launch)
+  if (lu_count != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *lu_count = 0;
   const int nb = (L + 15) / 16;
   const int cell = blockIdx.x / nb;
   const RidgeCellDesc cd = cells[cell];
@@ -1553,8 +1556,8 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
     hipLaunchKernelGGL(band_mk_extract_kernel, dim3(ncells), dim3(256), 0, st, cd, L, work);
   }
   hipLaunchKernelGGL(ridge_band_solve_kernel, dim3(ncells * ((L + 15) / 16)), dim3(NTS), 0, st,
-                     cd, lvec, L, work, tim, ncells);
-  if (lu_count != nullptr) {   // non-SPD lambdas: pivoted banded LU (zeroed count, cap list)
+                     cd, lvec, L, work, tim, ncells, lu_count);
+  if (lu_count != nullptr) {   // non-SPD lambdas: pivoted banded LU (count zeroed by kernel 2)
     hipLaunchKernelGGL(band_lu_flag_kernel, dim3((ncells * L + 255) / 256), dim3(256), 0, st, cd,
                        ncells, L, work, lu_list, lu_count, lu_cap);
     hipLaunchKernelGGL(ridge_band_lu_kernel, dim3(LU_WG), dim3(64), 0, st, cd, lvec, L, work,

@@ -249,7 +249,7 @@ def ridge_launch(plan: dict, d_desc: torch.Tensor, SD: torch.Tensor, Sr: torch.T
     work = torch.empty(plan["work"], dtype=torch.float64, device=SD.device)
     count = lst = None
     if repair and band_path(plan):
-        count = torch.zeros(1, dtype=torch.int32, device=SD.device)
+        count = torch.empty(1, dtype=torch.int32, device=SD.device)   # zeroed by the solve
         lst = torch.empty(plan["nc"] * L, dtype=torch.int32, device=SD.device)
     nat.check(nat.hip_lib().pfml_ridge_grid(SD.data_ptr(), P, Sr.data_ptr(), d_desc.data_ptr(),
                                             plan["nc"], plan["nmax"], lv.data_ptr(), L,
