@@ -68,10 +68,14 @@ __global__ __launch_bounds__(BM * 4, PF == 1 ? 3 : 1) void quadform_kernel(
   static_assert(NW * NCOL <= 2 * BM * KS, "cross-wave sums must fit in the A buffers");
   double (*red)[NCOL] = PF == 1 ? reinterpret_cast<double (*)[NCOL]>(&As[0][0][0]) : red_own;
 
+  // tile_job[tile] = job << 5 | row tile: the host lists the tiles longest-first (all row
+  // tiles 0, then all 1, ...: the triangular K loop shrinks with the row tile), so the launch
+  // ends on short tiles instead of a 33-step one; the partial slot stays ptile0 + rt
   const int tile = blockIdx.x;
-  const int j = tile_job[tile];
+  const int tj = tile_job[tile];
+  const int j = tj >> 5;
   const JobDesc jd = jobs[j];
-  const int rt = tile - jd.ptile0;           // row tile within the job
+  const int rt = tj & 31;                    // row tile within the job
   const int i0 = rt * BM;
   const int n = jd.n;
   const double* Dm = D + jd.d_off;
@@ -189,7 +193,7 @@ __global__ __launch_bounds__(BM * 4, PF == 1 ? 3 : 1) void quadform_kernel(
     double s = 0.0;
 #pragma unroll
     for (int q = 0; q < NW; ++q) s += red[q][t];
-    if (t < L) partial[(int64_t)tile * L + t] = s;
+    if (t < L) partial[(int64_t)(jd.ptile0 + rt) * L + t] = s;
   }
 }
 

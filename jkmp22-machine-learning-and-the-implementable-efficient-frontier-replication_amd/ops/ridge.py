@@ -536,7 +536,15 @@ def quad_plan(P: int, L: int, Pb: int, job_cell, job_month, job_n, job_out=None)
                      else np.asarray(job_out, np.int64)) * L
     desc["n"] = job_n.astype(np.int32)
     desc["ptile0"] = pt0
-    tile_job = np.repeat(np.arange(nj, dtype=np.int32), ntile)
+    # tiles longest-first (row tile 0 of every job, then row tile 1, ...): the triangular K
+    # loop of row tile rt is ~(n - 64 rt) long, so the launch ends on the short tiles;
+    # entry = job << 5 | rt (the kernel writes partial slot ptile0 + rt)
+    if nj and int(ntile.max()) > 32:
+        raise ValueError("quad_plan: more than 32 row tiles per job (n > 32 * rows)")
+    jj = np.repeat(np.arange(nj, dtype=np.int64), ntile)
+    rt = np.arange(len(jj), dtype=np.int64) - np.repeat(pt0.astype(np.int64), ntile)
+    order = np.lexsort((jj, rt))
+    tile_job = ((jj[order] << 5) | rt[order]).astype(np.int32)
     return {"desc": desc, "tile_job": tile_job, "nj": nj}
 
 
