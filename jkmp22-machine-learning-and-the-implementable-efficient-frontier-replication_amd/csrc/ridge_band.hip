@@ -1235,7 +1235,7 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
 //                        (slot = row mod 17) x 33 columns (slot = column mod 33: with
 //                        pivoting U has upper bandwidth 2 BB) in LDS; the pivot row goes to
 //                        an LDS copy of U, then 16 x 32 lanes eliminate and the row 17 below
-//                        enters the freed slot.  Back substitution from LDS, y written back.
+//                        enters the freed slot (its loads issued two steps ahead).  Back substitution from LDS, y written back.
 //                        An exactly zero pivot (singular: the reference raises LinAlgError)
 //                        leaves the NaN.
 // ---------------------------------------------------------------------------------------
@@ -1286,8 +1286,19 @@ __global__ __launch_bounds__(64) void ridge_band_lu_kernel(
     for (int x = lane; x < LR * UW; x += 64) W[x / UW][x % UW] = band(x / UW, x % UW);
     if (lane < LR) Z[lane] = lane < n ? bw.z[lane] : 0.0;
     __syncthreads();
-    bool singular = false;
-    for (int k = 0; k < n; ++k) {
+    // entering rows prefetched two steps ahead (their global loads overlap two steps of
+    // elimination instead of stalling each step): the k loop is unrolled by two with one
+    // register pair per parity, loads are unconditional (clamped) and the masks are applied
+    // where the values are used - a select right after a load, a load under a branch or a
+    // register copy would each wait for the load at once
+    auto fetch = [&](int k, double& ev, double& zv) {
+      const int r = k + LR, c = k + 1 + lane;
+      const int hi = max(r, c), lo = min(r, c);
+      ev = LB[(int64_t)min(hi, n - 1) * LS + max(0, min(BB, lo - hi + BB))];
+      zv = bw.z[min(r, n - 1)];
+    };
+    // one elimination step; false on an exactly zero / NaN pivot
+    auto step = [&](int k, double& ev, double& zv) -> bool {
       const int ks = k % LR, kc = k % UW;
       // pivot: first max |W[k + i][k]|, i = 0..16 (idamax order)
       double a = (lane < LR && k + lane < n) ? fabs(W[(k + lane) % LR][kc]) : -1.0;
@@ -1314,7 +1325,7 @@ __global__ __launch_bounds__(64) void ridge_band_lu_kernel(
       }
       __syncthreads();
       const double piv = W[ks][kc];
-      if (piv == 0.0 || piv != piv) { singular = true; break; }
+      if (piv == 0.0 || piv != piv) return false;
       const double rp = 1.0 / piv;
       const double zk = Z[ks];
       if (lane < UW) Us[k][lane] = W[ks][(k + lane) % UW];
@@ -1338,14 +1349,22 @@ __global__ __launch_bounds__(64) void ridge_band_lu_kernel(
       __syncthreads();
       // row k + 17 enters the pivot row's slot (columns k+1 .. k+33); the other rows' column
       // k slot becomes column k + 33, zero for them
-      const int r = k + LR;
-      if (lane < UW) {
-        const int col = k + 1 + lane;
-        W[ks][col % UW] = band(r, col);
-      }
+      const int r = k + LR, col = k + 1 + lane;
+      if (lane < UW)
+        W[ks][col % UW] = (r < n && col < n) ? ev + (r == col ? lam : 0.0) : 0.0;
       if (lane < BB) W[(k + 1 + lane) % LR][kc] = 0.0;
-      if (lane == 0) Z[ks] = r < n ? bw.z[r] : 0.0;
+      if (lane == 0) Z[ks] = r < n ? zv : 0.0;
+      fetch(k + 2, ev, zv);
       __syncthreads();
+      return true;
+    };
+    double eA, zA, eB, zB;
+    fetch(0, eA, zA);
+    fetch(1, eB, zB);
+    bool singular = false;
+    for (int k = 0; k < n; k += 2) {
+      if (!step(k, eA, zA)) { singular = true; break; }
+      if (k + 1 < n && !step(k + 1, eB, zB)) { singular = true; break; }
     }
     if (!singular) {
       for (int k = n - 1; k >= 0; --k) {
