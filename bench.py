@@ -71,7 +71,7 @@ def synthetic_reals(cfg: Config, device, n_months: int = 710, n_stocks: int = 50
         for a in range(0, n_months, chunk):
             b = min(n_months, a + chunk)
             X = torch.randn((b - a, n_stocks, P), generator=gen, dtype=torch.float64, device=device)
-            gemm(X, X, trans_a=True, alpha=1.0 / n_stocks, out=denom[g, a:b])
+            gemm(X, X, trans_a=True, alpha=1.0 / n_stocks, out=denom[g, a:b], backend="own")
             del X
         r[g] = 0.05 * torch.randn((n_months, P), generator=gen, dtype=torch.float64, device=device)
     return PfmlReals(months=months, r_tilde=r, denom=denom)

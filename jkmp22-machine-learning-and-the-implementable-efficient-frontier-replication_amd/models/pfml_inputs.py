@@ -42,7 +42,7 @@ import torch
 from ..config import Config, get_features, interleaved_order
 from ..data import io
 from ..ops import linalg as la
-from ..ops.gemm import gemm_fused, gemm_prec
+from ..ops.gemm import gemm, gemm_fused, gemm_prec
 from ..ops.panel import rff_features, standardize_signals
 from ..utils.dates import month_index, pfml_date_grids
 from ..utils.log import COUNTERS, get_logger
@@ -333,7 +333,7 @@ def _vol_device(plan: S4Plan) -> torch.Tensor:
         brc = torch.where(ok, br, torch.zeros_like(br))
         Xr = plan.bX[brc]                                         # [Mv, nv, K]
         Fm = plan.bF[plan.vol_fpos]                               # one F per vol month
-        d = (torch.bmm(Xr, Fm) * Xr).sum(-1) + plan.biv[brc]
+        d = (gemm(Xr, Fm, backend="own") * Xr).sum(-1) + plan.biv[brc]
         v = torch.where(ok, d.sqrt(), torch.full_like(d, float("nan")))
         real = plan.vol_rows < plan.R
         v = torch.where(real, v, torch.full_like(v, float("nan")))
@@ -391,7 +391,7 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False) -> "PfmlInpu
         Xl = plan.bX[bt.brow]                                       # [B, N, K]
         Fb = plan.bF[bt.fpos]                                       # [B, K, K]
         iv = plan.biv[bt.brow]                                      # [B, N]
-        XF = torch.bmm(Xl, Fb)
+        XF = gemm(Xl, Fb, backend="own")                             # in-house fp64 MFMA GEMM
         Sigma = torch.empty((B, N, N), dtype=torch.float64, device=dev)
         if prec == "fp64":
             gemm_fused(XF, Xl, Sigma, trans_b=True, diag_col0=0, diag_vec=iv)
@@ -447,10 +447,11 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False) -> "PfmlInpu
         # X (F (X' omega)) + ivol o omega), tc = w omega_chg' Lambda omega_chg, denom
         omega = omega.contiguous()
         omega_chg = omega_chg.contiguous()
-        rt_ = torch.bmm(omega.transpose(1, 2), bt.r.unsqueeze(-1)).squeeze(-1)   # [B, GP]
+        rt_ = gemm(omega, bt.r.unsqueeze(-1).contiguous(), trans_a=True,
+                   backend="own").squeeze(-1)                                # [B, GP]
         XtO = torch.empty((B, Xl.shape[2], GP), dtype=torch.float64, device=dev)
         gemm_fused(Xl, omega, XtO, trans_a=True)
-        FXO = torch.bmm(Fb, XtO)
+        FXO = gemm(Fb, XtO, backend="own")
         SO = torch.empty_like(omega)
         gemm_fused(Xl, FXO, SO, addend=omega, addend_row_scale=iv)
         lw = (bt.lam * bt.w.view(B, 1)).contiguous()
