@@ -25,7 +25,7 @@ construction (``s4_s5_s6_wall_ms``: every PFML month's Barra Sigma, m_func, (24)
 chains and (25) summands for 2 distinct g on a synthetic 500-stock universe, then S5 + S6),
 timed the same way (barrier + synchronize on both sides, max over ranks).  Multi-GPU: each
 rank builds the S4 summands of its own hp-year blocks plus the one-block validation halo
-(``search.local_month_range``) - no per-month matrix crosses ranks.  ``--no-inputs`` skips
+(``search.local_month_rows``) - no per-month matrix crosses ranks.  ``--no-inputs`` skips
 it; ``--with-inputs`` makes that full pipeline the timed step itself.
 """
 from __future__ import annotations
@@ -97,7 +97,7 @@ def engine_setup(cfg: Config, env, n_stocks: int, precision: str = "fp64"):
     layout and device copies only - the arithmetic is all in the timed step)."""
     from pfml.data.synthetic import engine_inputs
     from pfml.models.pfml_inputs import make_s4_plan
-    from pfml.models.search import local_month_range
+    from pfml.models.search import local_month_rows
     from pfml.utils.dates import pfml_date_grids
     cfg.run.compat_mode = False          # distinct RFF draw per g: no Q1 duplication
     cfg.run.precision = precision
@@ -106,8 +106,8 @@ def engine_setup(cfg: Config, env, n_stocks: int, precision: str = "fp64"):
                         int(cfg.settings["pf"]["dates"]["start_year"]),
                         int(cfg.settings["pf"]["dates"]["split_years"]))
     months = g["m2"]
-    lo, hi = local_month_range(months, cfg.hp_years, env.world_size, env.rank)
-    plan = make_s4_plan(cfg, chars, barra, wealth, rf, env.device, months[lo:hi])
+    rows = local_month_rows(months, cfg.hp_years, env.world_size, env.rank)
+    plan = make_s4_plan(cfg, chars, barra, wealth, rf, env.device, months[rows])
     return (plan, months), (chars, barra, wealth, rf)
 
 

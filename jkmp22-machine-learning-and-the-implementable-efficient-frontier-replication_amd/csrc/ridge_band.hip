@@ -43,13 +43,18 @@ constexpr int NTB = 512;            // back-transform kernel: 8 waves
 constexpr int NWB = NTB / 64;
 constexpr int LC = 16;              // lambdas per back-transform workgroup
 
-// Per-cell workspace layout (doubles).
+// Per-cell workspace layout (doubles).  A has room for the padded npad x npad matrix of the
+// fused path (npad = n rounded up to 16); the single / multi-workgroup paths use its first
+// n x n doubles with leading dimension n.
+__host__ __device__ __forceinline__ int band_npad(int n) { return (n + BB - 1) & ~(BB - 1); }
+
 struct BandWork {
-  double *A, *LB, *z, *T, *Yt, *Lf, *Vg, *Ug, *Xg, *Pg, *Pzg;
+  double *A, *LB, *z, *T, *Yt, *Lf, *Vg, *Ug, *Xg, *Pg, *Pzg, *F;
   __device__ BandWork(double* w, int n, int L) {
     const int np = (n + BB - 1) / BB;
-    A = w;                                   // n x n working matrix (V_p / R_p stored below)
-    LB = A + (int64_t)n * n;                 // n x LS lower band: LB[r][s] = B[r][r-16+s]
+    const int npad = band_npad(n);
+    A = w;                                   // working matrix (V_p / R_p stored below)
+    LB = A + (int64_t)npad * npad;           // n x LS lower band: LB[r][s] = B[r][r-16+s]
     z = LB + (int64_t)n * LS;                // Q^T rbar
     T = z + n;                               // np x 16 x 16 compact-WY T_p
     Yt = T + (int64_t)np * BB * BB;          // L x n   solutions y_l, then beta_l
@@ -59,7 +64,20 @@ struct BandWork {
     Xg = Ug + BMP * BB;                      //                        X = A U  (BMP x 16)
     Pg = Xg + BMP * BB;                      //                        V_I^T X_I partials
     Pzg = Pg + (BMP / 64) * BB * BB;         //                        V_I^T z_I partials
+    F = Pzg + (BMP / 64) * BB;               // fused path: V, W (x2 by panel parity), X
   }
+};
+
+// Fused-path scratch: V and W of a panel (double-buffered by panel parity) and X of the
+// current panel, row-major [npad][16] with ABSOLUTE row indices (rows < r0 unused).
+struct FusedWork {
+  double* f;
+  int64_t s;                                 // npad * 16
+  __device__ FusedWork(double* f_, int npad) : f(f_), s((int64_t)npad * BB) {}
+  // (arithmetic selection: an indexed pointer array would live in scratch)
+  __device__ double* V(int par) const { return f + (par & 1) * s; }
+  __device__ double* W(int par) const { return f + (2 + (par & 1)) * s; }
+  __device__ double* X() const { return f + 4 * s; }
 };
 
 // DPP helpers (gfx950: row_newbcast broadcasts one lane of each 16-lane row).
@@ -443,11 +461,14 @@ __device__ __forceinline__ bool band_panel_cqr(double* __restrict__ A, int n, in
 // (columns r0.. of rows k0..k0+15 of the symmetric A) is QR-factored by Householder in
 // registers; V (unit lower trapezoid) -> Vs, V and R -> A's panel columns, the compact-WY T
 // (dlarft) -> Ts and Tglob.  Ends with a barrier.  `redf` needs 2 x 256 + 32 doubles.
+// `n` is A's leading dimension.  `Pn` (fused path): the panel is read from this LDS image
+// (Pn[i][c] = panel row i, column c; it may alias Vs) instead of A's mirror row.
 __device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n, int k0, int r0,
                                                   int m, double (*Vs)[LS], double (*Gs)[LS],
                                                   double* redf, double (*Ts)[LS], double* taus,
                                                   double* __restrict__ Tglob, bool qr_fast,
-                                                  long long* tk = nullptr) {
+                                                  long long* tk = nullptr,
+                                                  const double (*Pn)[LS] = nullptr) {
   if (qr_fast && band_panel_cqr(A, n, k0, r0, m, Vs, redf, Ts, Tglob, tk)) return;
   const int t = threadIdx.x, lane = t & 63;
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -456,7 +477,13 @@ __device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n,
   // ---- P1: thread (rg, cq) loads rows i = rg + 32 q (q < 16) of panel column cq straight
   //      into registers (row k0+cq of the symmetric A; all 16 loads in flight at once)
   double a[16];
-  {
+  if (Pn != nullptr) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = rg + 32 * q;
+      a[q] = (i < m) ? Pn[i][cq] : 0.0;
+    }
+  } else {
     const double* src = A + (int64_t)(k0 + cq) * n + r0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -803,6 +830,355 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
   for (int e = t; e < n * LS; e += NTR) {
     const int r = e / LS, c = r - BB + e % LS;
     bw.LB[e] = (c >= 0) ? A[(int64_t)r * n + c] : 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// kernel 1, fused form (band_mode 3): one workgroup per cell, ONE pass over the trailing
+// matrix per panel instead of two, bitwise equal to ridge_band_reduce_kernel.
+//
+// The one-workgroup kernel above reads the trailing matrix A22 once for X = A22 U and
+// reads + writes its lower triangle (mirrored stores) for the rank-32 update, with ~20 CU
+// barriers and three serial phases per panel.  Here the update of panel p-1 and X of panel p
+// share one pass:
+//
+//   A  strip   column block p (rows >= 16 p) gets update p-1 in registers: its diagonal tile
+//              is final (band), the rest is the panel of p, handed to the QR through LDS
+//   B  QR      Householder panel factorisation (band_panel_factor, panel from LDS)
+//   C  U       U = V_p T_p (LDS)
+//   D  pass    every trailing tile (I, J): A_IJ -= V_I W_J' + W_I V_J' (panel p-1), then
+//              X_J += A_IJ' U_I (the tile's MFMA C layout IS the A-operand layout of A_IJ', so
+//              no transpose), stored back.  Wave w owns the columns J = w (mod 8) and forms
+//              X_J completely in registers - no cross-wave reduction.
+//   E  W       V_p' X, z <- Q_p' z, M = T' V' X, W = X - V M / 2: the same arithmetic, lane
+//              map and summation order as the one-workgroup kernel (X staged through a
+//              per-cell scratch), V_p and W_p to the scratch for the next pass.
+//
+// The matrix is stored FULL (both triangles) in a zero-padded npad x npad array, so every
+// tile is a whole 16 x 16 MFMA tile and X_J needs no upper-triangle mirror reads.  An upper
+// tile (I < J) applies the two rank-16 halves in the opposite order (W_I V_J' first), which
+// makes it bitwise the transpose of tile (J, I) - exactly the value the one-workgroup kernel
+// mirrors into the upper triangle - and X accumulates over the same rows in the same order,
+// so the band, V, T and z are bitwise those of ridge_band_reduce_kernel.
+// ---------------------------------------------------------------------------------------
+constexpr int FJ = 2;                   // columns per wave per pass group (registers)
+
+template <bool TIMED>
+__global__ __launch_bounds__(NTR) void band_fused_kernel(
+    const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
+    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work,
+    long long* __restrict__ tim) {
+  // optional per-phase cycle accounting (TIMED: thread 0; tools/bench_ridge.py --timing)
+  long long tacc[TIMED ? 8 : 1] = {0};
+  long long tlast = 0;
+#define FUSED_TMARK(ph)                                                  \
+  if (TIMED && threadIdx.x == 0) {                                       \
+    const long long now = (long long)__builtin_amdgcn_s_memtime();       \
+    tacc[ph] += now - tlast;                                             \
+    tlast = now;                                                         \
+  }
+  __shared__ double Vs[BMP][LS];       // panel of p (QR input), then V_p
+  __shared__ double Us[BMP][LS];       // QR's G scratch, then U_p = V_p T_p
+  __shared__ double red[NWR][BB * BB];
+  __shared__ double red2[NWR][BB];
+  __shared__ double Ts[BB][LS];
+  __shared__ double taus[BB];
+  __shared__ double zs[BNMAX];
+
+  const RidgeCellDesc cd = cells[blockIdx.x];
+  const int n = cd.n;
+  const int nb = (n + BB - 1) / BB, npad = nb * BB, lda = npad;
+  const int npan = (n - 1) / BB;               // panels: k0 = 16 p with k0 + 16 < n
+  const int t_ = threadIdx.x, lane_ = t_ & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t_ >> 6);
+  const int c16_ = lane_ & 15, g4_ = lane_ >> 4;
+  const int cq_ = t_ & 15, rg_ = t_ >> 4;
+  BandWork bw(work + cd.work, n, L);
+  FusedWork fw(bw.F, npad);
+  double* __restrict__ A = bw.A;
+  {
+    const double* S = SD + cd.src;
+    const double sc = cd.scale;
+    for (int i = wid; i < npad; i += NWR) {
+      const double* srow = S + (int64_t)i * ldS;
+      double* arow = A + (int64_t)i * lda;
+      for (int j = lane_; j < npad; j += 64) arow[j] = (i < n && j < n) ? srow[j] * sc : 0.0;
+    }
+    for (int i = t_; i < npad; i += NTR) zs[i] = (i < n) ? Sr[cd.rsrc + i] * sc : 0.0;
+  }
+  __syncthreads();
+  if (TIMED && threadIdx.x == 0) tlast = (long long)__builtin_amdgcn_s_memtime();
+
+  for (int p = 0; p < npan; ++p) {
+    const int k0 = p * BB, r0 = k0 + BB, m = n - r0;
+    const int mb = nb - p - 1;                  // trailing row / column blocks
+    // lane indices laundered per panel: otherwise the compiler hoists every lane-dependent LDS
+    // and global offset of the five phases out of the panel loop and keeps them live across
+    // the register-hungry QR (~70 VGPRs spilled)
+    int c16 = c16_, g4 = g4_, cq = cq_, rg = rg_, t = t_, lane = lane_;
+    asm volatile("" : "+v"(c16), "+v"(g4), "+v"(cq), "+v"(rg), "+v"(t), "+v"(lane));
+    // tile (I, J) element (16 I + g4 + 4 r, 16 J + c16): this lane's offset for r = 0
+    auto toff = [&](int I, int J) -> int64_t {
+      return (int64_t)(16 * I + g4) * lda + 16 * J + c16;
+    };
+    // A-operand chunks s of rows 16 B .. of a [npad][16] scratch: X[16 B + c16][4 s + g4]
+    auto aops = [&](const double* __restrict__ X, int B, double (&o)[4]) {
+  #pragma unroll
+      for (int s = 0; s < 4; ++s) o[s] = X[(16 * B + c16) * BB + 4 * s + g4];
+    };
+    const double* __restrict__ Vq = fw.V(p + 1);   // V, W of panel p - 1
+    const double* __restrict__ Wq = fw.W(p + 1);
+    // ---- A: strip = column block p, row blocks p .. nb-1
+    {
+      double cV[4], cW[4];
+      if (p > 0) {
+        aops(Vq, p, cV);
+        aops(Wq, p, cW);
+      }
+      for (int it = wid; it < nb - p; it += NWR) {
+        const int I = p + it;
+        double4_t c;
+        const int64_t o = toff(I, p);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c[r] = A[o + (int64_t)4 * r * lda];
+        if (p > 0) {
+          double rV[4], rW[4];
+          aops(Vq, I, rV);
+          aops(Wq, I, rW);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) c = mfma_f64_16x16x4(-rV[s], cW[s], c);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) c = mfma_f64_16x16x4(-rW[s], cV[s], c);
+        }
+        if (it == 0) {
+          if (p > 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) A[o + (int64_t)4 * r * lda] = c[r];
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Vs[16 * (it - 1) + g4 + 4 * r][c16] = c[r];
+        }
+      }
+    }
+    __syncthreads();
+    FUSED_TMARK(1)
+    // ---- B: QR of the panel (rows r0 .., from Vs) -> V_p (Vs), T_p, R / V into A
+    band_panel_factor(A, lda, k0, r0, m, Vs, Us, &red[0][0], Ts, taus,
+                      bw.T + (int64_t)p * BB * BB, false, nullptr, Vs);
+    FUSED_TMARK(2)
+    asm volatile("" : "+v"(c16), "+v"(g4), "+v"(cq), "+v"(rg), "+v"(t), "+v"(lane));
+    // ---- C: U = V T -> Us (all 32 row blocks: rows >= m read back as zero)
+#pragma unroll
+    for (int q = 0; q < BMP / 16 / NWR; ++q) {
+      const int i0 = (wid + NWR * q) * 16;
+      double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vs[i0 + c16][4 * r + g4], Ts[4 * r + g4][c16], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Us[i0 + g4 + 4 * r][c16] = acc[r];
+    }
+    __syncthreads();
+    FUSED_TMARK(3)
+    // ---- D: fused pass over the trailing tiles; wave wid owns columns J = wid (mod 8), taken
+    //      FJ at a time (the row operands are re-read per group: L1 hits)
+    {
+      const int J0 = p + 1 + ((wid - (p + 1)) % NWR + NWR) % NWR;
+      int nj = 0;
+      for (int J = J0; J < nb; J += NWR) ++nj;
+      for (int jg = 0; jg < nj; jg += FJ) {
+        double cV[FJ][4], cW[FJ][4];
+        double4_t X[FJ];
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+          X[j] = double4_t{0.0, 0.0, 0.0, 0.0};
+          if (p > 0 && jg + j < nj) {
+            aops(Vq, J0 + NWR * (jg + j), cV[j]);
+            aops(Wq, J0 + NWR * (jg + j), cW[j]);
+          }
+        }
+        for (int I = p + 1; I < nb; ++I) {
+          double rV[4], rW[4], ub[4];
+          if (p > 0) {
+            aops(Vq, I, rV);
+            aops(Wq, I, rW);
+          }
+          const int il = 16 * (I - p - 1);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ub[r] = Us[il + 4 * r + g4][c16];
+          double4_t c[FJ];
+#pragma unroll
+          for (int j = 0; j < FJ; ++j) {
+            if (jg + j < nj) {
+              const double* __restrict__ tp = A + toff(I, J0 + NWR * (jg + j));
+#pragma unroll
+              for (int r = 0; r < 4; ++r) c[j][r] = tp[4 * r * lda];
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < FJ; ++j) {
+            if (jg + j < nj) {
+              const int J = J0 + NWR * (jg + j);
+              if (p > 0) {
+                if (I < J) {            // upper tile: the mirror's order (bitwise transpose)
+#pragma unroll
+                  for (int s = 0; s < 4; ++s) c[j] = mfma_f64_16x16x4(-rW[s], cV[j][s], c[j]);
+#pragma unroll
+                  for (int s = 0; s < 4; ++s) c[j] = mfma_f64_16x16x4(-rV[s], cW[j][s], c[j]);
+                } else {
+#pragma unroll
+                  for (int s = 0; s < 4; ++s) c[j] = mfma_f64_16x16x4(-rV[s], cW[j][s], c[j]);
+#pragma unroll
+                  for (int s = 0; s < 4; ++s) c[j] = mfma_f64_16x16x4(-rW[s], cV[j][s], c[j]);
+                }
+                double* __restrict__ tp = A + toff(I, J);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) tp[4 * r * lda] = c[j][r];
+              }
+#pragma unroll
+              for (int r = 0; r < 4; ++r) X[j] = mfma_f64_16x16x4(c[j][r], ub[r], X[j]);
+            }
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) {
+          if (jg + j < nj) {
+            const int J = J0 + NWR * (jg + j);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) fw.X()[(16 * J + g4 + 4 * r) * BB + c16] = X[j][r];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    FUSED_TMARK(4)
+    // ---- E: P = V' X (per-wave partials over blocks wid + 8 q), V' z, exactly as the
+    //      one-workgroup kernel
+    const int nI = mb;
+    const int nq = (nI > wid) ? (nI - wid + NWR - 1) / NWR : 0;
+    double4_t Xc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      Xc[q] = double4_t{0.0, 0.0, 0.0, 0.0};
+      if (q < nq) {
+        const int i0 = (wid + NWR * q) * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Xc[q][r] = fw.X()[(r0 + i0 + g4 + 4 * r) * BB + c16];
+      }
+    }
+    {
+      double4_t Pp = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (q < nq) {
+          const int i0 = (wid + NWR * q) * 16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Pp = mfma_f64_16x16x4(Vs[i0 + 4 * r + g4][c16], Xc[q][r], Pp);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wid][(g4 + 4 * r) * BB + c16] = Pp[r];
+      double s = 0.0;
+#pragma unroll
+      for (int q = 0; q < BMP / 32; ++q) {
+        const int i = rg + 32 * q;
+        s += Vs[i][cq] * zs[r0 + min(i, m - 1)];
+      }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (lane < 16) red2[wid][lane] = s;
+    }
+    __syncthreads();
+    {
+      double zv[BB];
+#pragma unroll
+      for (int a = 0; a < BB; ++a) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < NWR; ++w) s += red2[w][a];
+        zv[a] = s;
+      }
+      double zt[BB];
+#pragma unroll
+      for (int c = 0; c < BB; ++c) {
+        double s = 0.0;
+#pragma unroll
+        for (int a = 0; a <= c; ++a) s += Ts[a][c] * zv[a];
+        zt[c] = s;
+      }
+      for (int i = t; i < m; i += NTR) {
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < BB; ++c) s += Vs[i][c] * zt[c];
+        zs[r0 + i] -= s;
+      }
+    }
+    {
+      double4_t Mm = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double pv = 0.0;
+#pragma unroll
+        for (int w = 0; w < NWR; ++w) pv += red[w][(4 * r + g4) * BB + c16];
+        Mm = mfma_f64_16x16x4(Ts[4 * r + g4][c16], pv, Mm);
+      }
+      double* __restrict__ Wn = fw.W(p);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (q < nq) {
+          const int i0 = (wid + NWR * q) * 16;
+          double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vs[i0 + c16][4 * r + g4], Mm[r], acc);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = i0 + g4 + 4 * r;
+            Wn[(r0 + i) * BB + c16] = (i < m) ? Xc[q][r] - 0.5 * acc[r] : 0.0;
+          }
+        }
+      }
+      double* __restrict__ Vn = fw.V(p);
+      for (int e = t; e < mb * BB * BB; e += NTR) Vn[(int64_t)r0 * BB + e] = Vs[e / BB][e % BB];
+    }
+    __syncthreads();
+    FUSED_TMARK(5)
+  }
+  const int t = t_, c16 = c16_, g4 = g4_;
+  auto toff = [&](int I, int J) -> int64_t {
+    return (int64_t)(16 * I + g4) * lda + 16 * J + c16;
+  };
+  auto aops = [&](const double* __restrict__ X, int B, double (&o)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) o[s] = X[(16 * B + c16) * BB + 4 * s + g4];
+  };
+  // the last diagonal tile (block nb - 1) gets the last panel's update
+  if (npan > 0 && wid == 0) {
+    const int p = npan, I = nb - 1;
+    const double* __restrict__ Vq = fw.V(p + 1);
+    const double* __restrict__ Wq = fw.W(p + 1);
+    double rV[4], rW[4];
+    aops(Vq, I, rV);
+    aops(Wq, I, rW);
+    double4_t c;
+    const int64_t o = toff(I, I);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) c[r] = A[o + (int64_t)4 * r * lda];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) c = mfma_f64_16x16x4(-rV[s], rW[s], c);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) c = mfma_f64_16x16x4(-rW[s], rV[s], c);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) A[o + (int64_t)4 * r * lda] = c[r];
+  }
+  __syncthreads();
+  FUSED_TMARK(6)
+  if (TIMED && threadIdx.x == 0)
+    for (int q = 0; q < 8; ++q) tim[(int64_t)blockIdx.x * 8 + q] = tacc[q];
+#undef FUSED_TMARK
+  for (int i = t; i < n; i += NTR) bw.z[i] = zs[i];
+  for (int e = t; e < n * LS; e += NTR) {
+    const int r = e / LS, c = r - BB + e % LS;
+    bw.LB[e] = (c >= 0) ? A[(int64_t)r * lda + c] : 0.0;
   }
 }
 
@@ -1397,7 +1773,7 @@ constexpr int NBW = (BNMAX / 16 + NWB - 1) / NWB;   // row blocks per wave
 
 __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
     const RidgeCellDesc* __restrict__ cells, int ncells, int L, double* __restrict__ work,
-    double* __restrict__ beta_out, int64_t ldo) {
+    double* __restrict__ beta_out, int64_t ldo, int fused) {
   __shared__ double red[2][NWB][BB * BB];
   __shared__ double Vw[NWB][NBW][BB][LS];         // wave-private V_b images (transpose)
   // (the chunks of a cell are adjacent in dispatch order, so they run together and share
@@ -1430,11 +1806,12 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
       Y[q][r] = (lok && i < n) ? yc[i] : 0.0;
     }
   // va[q][r] = V_p[16 b - r0 + 4 r + g4][c16] for the live blocks b = wid + 8 q of panel p
-  const int lo_a = g4 * n + c16;
+  const int lda = fused ? band_npad(n) : n;       // A's leading dimension (fused: padded)
+  const int lo_a = g4 * lda + c16;
   double vn[NBW][4], tn[4];
   auto fetch = [&](int p) {
     const int k0 = p * BB, r0 = k0 + BB, m = n - r0;
-    const double* Ap = A + (int64_t)r0 * n + k0;   // &V_p[0][0] (wave-uniform)
+    const double* Ap = A + (int64_t)r0 * lda + k0; // &V_p[0][0] (wave-uniform)
 #pragma unroll
     for (int q = 0; q < NBW; ++q) {
       const int b = wid + NWB * q;
@@ -1445,7 +1822,7 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
         double v = 0.0;
         if (live && i < m && i > c16)
           v = *reinterpret_cast<const double*>(
-              reinterpret_cast<const char*>(Ap + (int64_t)ib * n) + (unsigned)lo_a * 8u);
+              reinterpret_cast<const char*>(Ap + (int64_t)ib * lda) + (unsigned)lo_a * 8u);
         vn[q][r] = (live && i == c16 && i < m) ? 1.0 : v;
       }
     }
@@ -1518,8 +1895,10 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
 
 extern "C" int64_t pfml_ridge_band_work_doubles(int n, int L) {
   const int64_t np = (n + BB - 1) / BB;
-  return (int64_t)n * n + (int64_t)n * LS + n + np * BB * BB + (int64_t)L * n +
-         (int64_t)L * n * LS + 3LL * BMP * BB + (int64_t)(BMP / MK_XR) * (BB * BB + BB);
+  const int64_t npad = band_npad(n);
+  return npad * npad + (int64_t)n * LS + n + np * BB * BB + (int64_t)L * n +
+         (int64_t)L * n * LS + 3LL * BMP * BB + (int64_t)(BMP / MK_XR) * (BB * BB + BB) +
+         5LL * npad * BB;
 }
 
 extern "C" int pfml_ridge_band_nmax() { return BNMAX; }
@@ -1536,6 +1915,8 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   const char* mode = getenv("PFML_BAND_MODE");
   // (phase timing: the single kernel unless PFML_BAND_MODE=multi)
   const bool env_multi = mode && mode[0] == 'm';
+  // band_mode 3 (or PFML_BAND_MODE=fused): the fused one-workgroup kernel
+  const bool fused = band_mode == 3 || (band_mode == 0 && mode && mode[0] == 'f');
   const bool single = band_mode == 1 || (band_mode == 0 && mode && mode[0] == 's') ||
                       (tim != nullptr && band_mode == 0 && !env_multi);
   // panel QR: column-by-column Householder (default), or PFML_BAND_QR=cqr: CholeskyQR2 +
@@ -1545,7 +1926,14 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   // barrier-separated Householder columns they replace.
   const char* qenv = getenv("PFML_BAND_QR");
   const int qr_fast = (qenv && qenv[0] == 'c') ? 1 : 0;
-  if (single) {
+  if (fused) {
+    if (tim != nullptr)
+      hipLaunchKernelGGL(band_fused_kernel<true>, dim3(ncells), dim3(NTR), 0, st, SD, ldS, Sr, cd,
+                         L, work, tim);
+    else
+      hipLaunchKernelGGL(band_fused_kernel<false>, dim3(ncells), dim3(NTR), 0, st, SD, ldS, Sr, cd,
+                         L, work, tim);
+  } else if (single) {
     if (qr_fast)
       hipLaunchKernelGGL(ridge_band_reduce_kernel<true>, dim3(ncells), dim3(NTR), 0, st, SD, ldS,
                          Sr, cd, L, work, tim);
@@ -1584,6 +1972,6 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   }
   const int nch = (L + LC - 1) / LC;
   hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3(ncells * nch), dim3(NTB), 0, st, cd,
-                     ncells, L, work, beta_out, ldo);
+                     ncells, L, work, beta_out, ldo, fused ? 1 : 0);
   return hipGetLastError();
 }

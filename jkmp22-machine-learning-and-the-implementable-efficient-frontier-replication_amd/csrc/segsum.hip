@@ -217,3 +217,223 @@ extern "C" hipError_t pfml_window_prefix_vec(const double* X, int64_t E, int T, 
                      dim3(WV_T), 0, st, X, E, T, seg_start, seg_stop, nseg, skip, out);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------
+// Canonical chunked expanding-window sums (bitwise the same on every world size).
+//
+// A running sum over the segments of ONE rank re-associates differently for every sharding
+// (world 1: ((S0 + S1) + S2) + ..., world N: (S_k + ...) + prefix of the lower ranks), so
+// the utilities of an N-rank run differed from the 1-rank run in the last bits (2e-10 rel.)
+// and a near-tie rank could flip.  The sums therefore follow ONE fixed association,
+// independent of the world size:
+//   * the months are cut into 2C canonical chunks: C burn-in pieces and C groups of whole
+//     hp-year blocks (search.win_layout; C = 8 covers world 1, 2, 4, 8);
+//   * chunk total T = left fold of its segment sums from 0 (kernel A, on the chunk's owner);
+//   * E = left fold of the C burn-in totals, P_0 = E, P_{c+1} = P_c + TY_c;
+//   * the window of a year in chunk c = left fold of c's year segments starting from P_c
+//     (kernel B).
+// Ranks own whole chunks; the totals cross ranks by one all-gather (P x P per owned chunk)
+// and kernel B reads them through a canonical slot map, so no reordering copy.  Totals are
+// chunk-major: slot k, g at tot + k * tstride + g * (P P or E).
+namespace {
+
+__device__ __forceinline__ bool tile_upper(int I, int J, int i, int j, int r, int c, int P) {
+  return i < P && j < P && (I != J || c >= r);
+}
+
+// tot slot[lc] (upper triangle) = left fold of segments [cs[lc], ce[lc]) from 0
+__global__ __launch_bounds__(256) void wsum_chunk_totals_kernel(
+    int P, int nseg, int skip, const double* __restrict__ out, const double* __restrict__ scratch,
+    int nlc, const int* __restrict__ cs, const int* __restrict__ ce, const int* __restrict__ slot,
+    double* __restrict__ tot, int64_t tstride) {
+  const int g = blockIdx.y;
+  int tile = blockIdx.x;
+  const int nt = (P + 31) / 32;
+  int I = 0;
+  while (tile >= nt - I) { tile -= nt - I; ++I; }
+  const int J = I + tile;
+  const int64_t PP = (int64_t)P * P;
+  const int t = threadIdx.x, c = t & 31, r0 = t >> 5;
+  for (int lc = 0; lc < nlc; ++lc) {
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int s = cs[lc]; s < ce[lc]; ++s) {
+      const double* o = seg_slot(const_cast<double*>(out), const_cast<double*>(scratch), g, s,
+                                 nseg, skip, PP);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
+        if (tile_upper(I, J, i, j, r, c, P)) acc[q] += o[(int64_t)i * P + j];
+      }
+    }
+    double* d = tot + (int64_t)slot[lc] * tstride + (int64_t)g * PP;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
+      if (tile_upper(I, J, i, j, r, c, P)) d[(int64_t)i * P + j] = acc[q];
+    }
+  }
+}
+
+// windows: E = fold(tot[sb[k]]), P_0 = E; chunk c with local year segments [ys[c], ye[c]):
+// acc = P_c, acc += seg s, out[s - skip] = acc (full, mirrored); P_{c+1} = P_c + tot[sy[c]].
+// Chunks past the last local one are not visited.
+__global__ __launch_bounds__(256) void wsum_chunk_prefix_kernel(
+    int P, int nseg, int skip, double* __restrict__ out, double* __restrict__ scratch, int C,
+    const int* __restrict__ sb, const int* __restrict__ sy, const int* __restrict__ ys,
+    const int* __restrict__ ye, const double* __restrict__ tot, int64_t tstride, int clast) {
+  __shared__ double Ts[32][33];
+  const int g = blockIdx.y;
+  int tile = blockIdx.x;
+  const int nt = (P + 31) / 32;
+  int I = 0;
+  while (tile >= nt - I) { tile -= nt - I; ++I; }
+  const int J = I + tile;
+  const int64_t PP = (int64_t)P * P;
+  const int t = threadIdx.x, c = t & 31, r0 = t >> 5;
+  const double* tg = tot + (int64_t)g * PP;     // slot k at tg + k * tstride
+  double pc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int k = 0; k < C; ++k) {
+    const double* o = tg + (int64_t)sb[k] * tstride;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
+      if (tile_upper(I, J, i, j, r, c, P)) pc[q] += o[(int64_t)i * P + j];
+    }
+  }
+  for (int ch = 0; ch <= clast; ++ch) {
+    double acc[4] = {pc[0], pc[1], pc[2], pc[3]};
+    for (int s = ys[ch]; s < ye[ch]; ++s) {
+      const double* o = seg_slot(out, scratch, g, s, nseg, skip, PP);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
+        const double v = tile_upper(I, J, i, j, r, c, P) ? o[(int64_t)i * P + j] : 0.0;
+        acc[q] += v;
+        Ts[r][c] = acc[q];
+      }
+      __syncthreads();
+      if (s >= skip) {
+        double* w = seg_slot(out, scratch, g, s, nseg, skip, PP);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = r0 + 8 * q;
+          const int i = I * 32 + r, j = J * 32 + c;
+          if (i < P && j < P) w[(int64_t)i * P + j] = (I != J || c >= r) ? Ts[r][c] : Ts[c][r];
+          const int i2 = J * 32 + r, j2 = I * 32 + c;
+          if (I != J && i2 < P && j2 < P) w[(int64_t)i2 * P + j2] = Ts[c][r];
+        }
+      }
+      __syncthreads();
+    }
+    if (ch < clast) {
+      const double* o = tg + (int64_t)sy[ch] * tstride;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
+        if (tile_upper(I, J, i, j, r, c, P)) pc[q] += o[(int64_t)i * P + j];
+      }
+    }
+  }
+}
+
+// vectors (r_tilde): mode 0 = chunk totals into tot[g][slot[lc]][E], mode 1 = windows into
+// out[g][s - skip][E].  Segment sums as window_prefix_vec_kernel (eight months in flight).
+__global__ __launch_bounds__(WV_T) void wvec_chunk_kernel(
+    const double* __restrict__ X, int64_t E, int T, const int* __restrict__ seg_start,
+    const int* __restrict__ seg_stop, int nseg, int skip, int mode, int nlc,
+    const int* __restrict__ cs, const int* __restrict__ ce, const int* __restrict__ slot, int C,
+    const int* __restrict__ sb, const int* __restrict__ sy, const int* __restrict__ ys,
+    const int* __restrict__ ye, int clast, double* __restrict__ tot, int64_t tstride,
+    double* __restrict__ out) {
+  __shared__ double part[WV_SEG][WV_COLS];
+  const int lc = threadIdx.x % WV_COLS, ry = threadIdx.x / WV_COLS;
+  const int g = blockIdx.y, col = blockIdx.x * WV_COLS + lc;
+  const bool cv = col < E;
+  const double* src = X + (int64_t)g * T * E + (cv ? col : 0);
+  for (int s = ry; s < nseg; s += WV_RG) {
+    const int a = seg_start[s], b = seg_stop[s];
+    double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int tm = a; tm < b; tm += 8) {
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = (tm + u < b) ? src[(int64_t)(tm + u) * E] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += x[u];
+    }
+    part[s][lc] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  }
+  __syncthreads();
+  if (ry != 0 || !cv) return;
+  double* tg = tot + (int64_t)g * E + col;     // slot k at tg + k * tstride
+  if (mode == 0) {
+    for (int k = 0; k < nlc; ++k) {
+      double acc = 0.0;
+      for (int s = cs[k]; s < ce[k]; ++s) acc += part[s][lc];
+      tg[(int64_t)slot[k] * tstride] = acc;
+    }
+    return;
+  }
+  double pc = 0.0;
+  for (int k = 0; k < C; ++k) pc += tg[(int64_t)sb[k] * tstride];
+  double* o = out + (int64_t)g * (nseg - skip) * E + col;
+  for (int ch = 0; ch <= clast; ++ch) {
+    double acc = pc;
+    for (int s = ys[ch]; s < ye[ch]; ++s) {
+      acc += part[s][lc];
+      if (s >= skip) o[(int64_t)(s - skip) * E] = acc;
+    }
+    if (ch < clast) pc += tg[(int64_t)sy[ch] * tstride];
+  }
+}
+
+}  // namespace
+
+// Kernel A for the matrices: segment sums (upper triangles) into the out / scratch slots,
+// then the local chunk totals.  idx = [cs, ce, slot] (3 x nlc int32, device).
+extern "C" hipError_t pfml_wsum_chunk_totals(const double* X, int P, int T, int G,
+                                             const int* seg_start, const int* seg_stop, int nseg,
+                                             int skip, double* out, double* scratch, int nlc,
+                                             const int* idx, double* tot, int64_t tstride,
+                                             hipStream_t st) {
+  if (nseg <= 0 || P <= 0 || G <= 0) return hipSuccess;
+  if (skip < 0 || skip > nseg || (skip > 0 && scratch == nullptr)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(wsum_upper_kernel, dim3(P, nseg, G), dim3(256), 0, st, X, P, T, seg_start,
+                     seg_stop, nseg, skip, out, scratch);
+  if (nlc > 0) {
+    const int nt = (P + 31) / 32;
+    hipLaunchKernelGGL(wsum_chunk_totals_kernel, dim3(nt * (nt + 1) / 2, G), dim3(256), 0, st, P,
+                       nseg, skip, out, scratch, nlc, idx, idx + nlc, idx + 2 * nlc, tot,
+                       tstride);
+  }
+  return hipGetLastError();
+}
+
+// Kernel B for the matrices.  cidx = [sb, sy, ys, ye] (4 x C int32, device).
+extern "C" hipError_t pfml_wsum_chunk_prefix(int P, int G, int nseg, int skip, double* out,
+                                             double* scratch, int C, const int* cidx,
+                                             const double* tot, int64_t tstride, int clast,
+                                             hipStream_t st) {
+  if (nseg <= 0 || P <= 0 || G <= 0 || clast < 0) return hipSuccess;
+  const int nt = (P + 31) / 32;
+  hipLaunchKernelGGL(wsum_chunk_prefix_kernel, dim3(nt * (nt + 1) / 2, G), dim3(256), 0, st, P,
+                     nseg, skip, out, scratch, C, cidx, cidx + C, cidx + 2 * C, cidx + 3 * C, tot,
+                     tstride, clast);
+  return hipGetLastError();
+}
+
+// Vectors, both kernels (mode 0 / 1); idx and cidx as above.
+extern "C" hipError_t pfml_wvec_chunk(const double* X, int64_t E, int T, int G,
+                                      const int* seg_start, const int* seg_stop, int nseg,
+                                      int skip, int mode, int nlc, const int* idx, int C,
+                                      const int* cidx, int clast, double* tot, int64_t tstride,
+                                      double* out, hipStream_t st) {
+  if (nseg <= 0 || E <= 0 || G <= 0) return hipSuccess;
+  if (nseg > WV_SEG || skip < 0) return hipErrorInvalidValue;
+  if (mode == 1 && (clast < 0 || nseg - skip <= 0)) return hipSuccess;
+  if (mode == 0 && nlc <= 0) return hipSuccess;
+  hipLaunchKernelGGL(wvec_chunk_kernel, dim3((unsigned)((E + WV_COLS - 1) / WV_COLS), G),
+                     dim3(WV_T), 0, st, X, E, T, seg_start, seg_stop, nseg, skip, mode, nlc, idx,
+                     idx + nlc, idx + 2 * nlc, C, cidx, cidx + C, cidx + 2 * C, cidx + 3 * C,
+                     clast, tot, tstride, out);
+  return hipGetLastError();
+}

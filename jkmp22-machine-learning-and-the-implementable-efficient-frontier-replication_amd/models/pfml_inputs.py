@@ -249,7 +249,12 @@ def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         vr.append(rows)
         vb.append(brow)
         vf.append(bp)
-    nv = max([len(x) for x in vr] + [1])
+    # padded widths from the WHOLE PFML date grid, not this rank's months: every month's
+    # matrices then have one shape on every rank / batch split, so a month's summands are
+    # bitwise the same however the months are sharded (canonical N-rank == 1-rank results)
+    lb_all = grids["lb"]
+    nv = max([int(np.searchsorted(panel.mi, mi, "right") - np.searchsorted(panel.mi, mi, "left"))
+              for mi in lb_all] + [len(x) for x in vr] + [1])
     vol_rows = np.full((len(vr), nv), R, np.int64)
     vol_brow = np.full((len(vr), nv), -1, np.int64)
     for i, (x, y) in enumerate(zip(vr, vb)):
@@ -259,7 +264,8 @@ def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
     gt_all = np.nan_to_num((1.0 + panel.cols["tr_ld0"]) / (1.0 + panel.cols["mu_ld0"]), nan=1.0)
 
     T = len(months)
-    nmax = max((len(panel.valid_rows(int(d))) for d in months), default=1)
+    nmax = max((len(panel.valid_rows(int(d))) for d in np.union1d(grids["m2"], months)),
+               default=1)
     Npad = _even(max(nmax, 2))
     bsz = batch or cfg.run.month_batch
     if not bsz or bsz <= 0:

@@ -14,10 +14,14 @@ month) from Python, :62-130) with one batched device pipeline:
 Signals are kept in the interleaved order [constant, cos1, sin1, cos2, sin2, ...]
 (config.interleaved_order) so every hyper-parameter p uses the LEADING (p+1) x (p+1) block.
 
-Distributed: hp years are split contiguously over ranks.  Each rank sums only its own
-window blocks; the cross-rank exclusive prefix of the block totals is ONE all-gather of a
-P x P matrix per g per rank and the per-month utilities are ONE all-gather at
-the end (a few MB; every rank's row count follows from the shared plan).
+Distributed: the months are cut into 2 C canonical chunks (C = 8 burn-in pieces, C groups of
+whole hp-year blocks; ``win_layout``) that ranks own whole, so S4 months balance across ranks
+(the burn-in is spread) and every world size adds the same numbers in the same order: chunk
+totals are left folds of their segment sums, the prefix over chunks is a left fold in chunk
+order, and a window is the left fold of its chunk's year segments from that prefix - N-rank
+results are BITWISE the 1-rank results.  The chunk totals cross ranks by ONE all-gather (a
+P x P matrix per owned chunk per g) and the per-month utilities are ONE
+all-gather at the end (a few MB; every rank's row count follows from the shared plan).
 """
 from __future__ import annotations
 
@@ -51,9 +55,9 @@ nat.register_hip("pfml_validation_scores_all", [C.c_void_p, C.c_int, C.c_int, C.
 class PfmlReals:
     """Per-month PFML summands of (25) for every g (internal interleaved feature order).
 
-    ``months`` are the months held here; with ``all_months`` set they are a contiguous window
-    of that global list (a rank's hp-year shard plus its validation halo, see
-    ``local_month_range``) and the search plans over the global list."""
+    ``months`` are the months held here; with ``all_months`` set they are a sorted subset of
+    that global list (a rank's chunks plus its validation halo, see ``local_month_rows``) and
+    the search plans over the global list."""
     months: np.ndarray                 # [T] month indices, sorted ascending
     r_tilde: torch.Tensor              # [G, T, P]
     denom: torch.Tensor                # [G, T, P, P]
@@ -97,20 +101,66 @@ def make_plan(months: np.ndarray, years: np.ndarray) -> SearchPlan:
                       burn_stop, count, val_start.astype(np.int64), val_stop.astype(np.int64))
 
 
-def local_month_range(all_months: np.ndarray, years: np.ndarray, world: int,
-                      rank: int) -> tuple[int, int]:
-    """[lo, hi) rows of ``all_months`` that the rank owning a contiguous share of the hp years
-    needs: its own expanding-window blocks (rank 0 also the burn-in), and the
-    validation months of its last year - the next year's block - as a halo.  Every rank thus
-    computes the S4 summands of its own months only; the window prefixes cross ranks as one
-    P x P all-gather of block totals, no per-month matrix is ever exchanged."""
-    plan = make_plan(np.asarray(all_months, np.int64), np.asarray(years))
-    yl = list(coll.contiguous_split(len(years), world, rank))
-    if not yl:
-        return 0, 0
-    lo = 0 if yl[0] == 0 else int(plan.seg_start[yl[0]])
-    hi = max(int(plan.seg_stop[yl[-1]]), int(plan.val_stop[yl[-1]]))
-    return lo, hi
+NCHUNK = 8            # canonical chunks per kind (covers world 1, 2, 4, 8 bitwise alike)
+
+
+@dataclass
+class WinLayout:
+    """World-size independent cut of the month axis for the window sums: C burn-in pieces
+    (global month rows [a, b), near-equal, possibly empty) and C groups of consecutive hp
+    years.  Chunk c of either kind belongs to rank c * world // C."""
+    C: int
+    burn: list
+    ychunks: list
+
+
+def win_layout(plan: "SearchPlan", nY: int, world: int) -> WinLayout:
+    C = max(NCHUNK, int(world))
+    nb = int(plan.burn_stop)
+    burn = [(r.start, r.stop) for r in (coll.contiguous_split(nb, C, k) for k in range(C))]
+    ych = [coll.contiguous_split(nY, C, c) for c in range(C)]
+    return WinLayout(C, burn, ych)
+
+
+def chunk_owner(c: int, C: int, world: int) -> int:
+    return c * world // C
+
+
+def rank_years(nY: int, world: int, rank: int) -> np.ndarray:
+    """hp-year indices owned by ``rank`` (contiguous: its year chunks are consecutive)."""
+    C = max(NCHUNK, int(world))
+    ys = [y for c in range(C) if chunk_owner(c, C, world) == rank
+          for y in coll.contiguous_split(nY, C, c)]
+    return np.asarray(ys, dtype=np.int64)
+
+
+def local_month_rows(all_months: np.ndarray, years: np.ndarray, world: int,
+                     rank: int) -> np.ndarray:
+    """Global rows of ``all_months`` whose S4 summands ``rank`` computes:
+    its burn-in pieces, the blocks of its hp years and the validation months of its last
+    year (the next block: a one-block halo).  Sorted; not contiguous in general (the burn-in
+    pieces are spread over the ranks so the S4 months balance).  Every rank thus builds the
+    summands of its own months only; window prefixes cross ranks as P x P chunk totals."""
+    all_months = np.asarray(all_months, np.int64)
+    plan = make_plan(all_months, np.asarray(years))
+    lay = win_layout(plan, len(years), world)
+    rows = []
+    for k, (a, b) in enumerate(lay.burn):
+        if chunk_owner(k, lay.C, world) == rank:
+            rows.append(np.arange(a, b))
+    yl = rank_years(len(years), world, rank)
+    for y in yl:
+        rows.append(np.arange(int(plan.seg_start[y]), int(plan.seg_stop[y])))
+    if len(yl):
+        rows.append(np.arange(int(plan.val_start[yl[-1]]), int(plan.val_stop[yl[-1]])))
+    if not rows:
+        return np.zeros(0, np.int64)
+    return np.unique(np.concatenate(rows)).astype(np.int64)
+
+
+def s4_month_counts(all_months: np.ndarray, years: np.ndarray, world: int) -> list:
+    """S4 months per rank (load balance report)."""
+    return [len(local_month_rows(all_months, years, world, r)) for r in range(world)]
 
 
 @dataclass
@@ -122,50 +172,94 @@ class GridResult:
     beta: torch.Tensor                 # [G, nY_local, nP, L, P] (zero beyond p+1)
     val_months: np.ndarray             # [nVal] month indices of all validation rows
     val_year: np.ndarray               # [nVal] hp_end of each validation month
-    obj: torch.Tensor                  # [nVal, G, nP, L]  (all ranks, gathered)
+    obj: torch.Tensor                  # [nVal, G, nP, L]  (all ranks once gathered)
     timings: dict = field(default_factory=dict)
+    # this rank's window sums (SD [G, nYl, P, P], Sr [G, nYl, P]) and the bookkeeping of
+    # gather_grid (utilities local until gathered)
+    window: tuple | None = None
+    gathered: bool = True
+    all_months: np.ndarray | None = None
 
 
 _SETUP: dict = {}
 
 
 def _search_setup(months: np.ndarray, years: np.ndarray, p_vec, G: int, T: int, world: int,
-                  rank: int, dev, l_vec: np.ndarray, off: int = 0) -> dict:
-    """Everything of a grid search that depends only on its shape - the window plan, this
-    rank's segments, cells and validation jobs, and the device copies of the segment bounds -
-    built once per shape and reused by every later search (no host planning, no host->device
-    copies in the steady state).  ``months`` is the global month list; the T months held
-    locally start at global row ``off`` (all local row indices below are relative to it)."""
+                  rank: int, dev, l_vec: np.ndarray, rows: np.ndarray) -> dict:
+    """Everything of a grid search that depends only on its shape - the window plan and
+    canonical chunk layout, this rank's segments, chunk slots, cells and validation jobs, and
+    their device copies - built once per shape and reused by every later search (no host
+    planning, no host->device copies in the steady state).  ``months`` is the global month
+    list; the T months held locally are the global rows ``rows`` (sorted)."""
     key = (months.tobytes(), np.asarray(years).tobytes(), tuple(p_vec), G, T, world, rank,
-           str(dev), l_vec.tobytes(), off)
+           str(dev), l_vec.tobytes(), rows.tobytes())
     hit = _SETUP.get(key)
     if hit is not None:
         return hit
     plan = make_plan(months, years)
-    yl = np.asarray(list(coll.contiguous_split(len(years), world, rank)), dtype=np.int64)
+    lay = win_layout(plan, len(years), world)
+    C = lay.C
+    yl = rank_years(len(years), world, rank)
     nYl = len(yl)
     nP = len(p_vec)
-    st = [int(plan.seg_start[i]) - off for i in yl]
-    sp = [int(plan.seg_stop[i]) - off for i in yl]
-    if nYl and yl[0] == 0:
-        st = [0 - off] + st
-        sp = [plan.burn_stop - off] + sp
-    if any(a < 0 or b > T for a, b in zip(st, sp)):
-        raise ValueError(f"rank {rank}: local months [{off}, {off + T}) miss its window blocks")
+
+    def loc(a: int, b: int, what: str) -> tuple[int, int]:
+        la, lb = int(np.searchsorted(rows, a)), int(np.searchsorted(rows, b))
+        if lb - la != b - a:
+            raise ValueError(f"rank {rank}: local months miss the rows [{a}, {b}) of its {what}")
+        return la, lb
+
+    # segments in month order: the owned burn-in pieces (prefix only), then the owned years
+    own = [c for c in range(C) if chunk_owner(c, C, world) == rank]
+    st, sp, chunk_seg = [], [], []                    # chunk_seg: (kind, c, s0, s1)
+    for k in own:
+        a, b = loc(*lay.burn[k], "burn-in piece")
+        chunk_seg.append(("b", k, len(st), len(st) + 1))
+        st.append(a)
+        sp.append(b)
+    skip = len(st)
+    yseg = {}
+    for c in own:
+        s0 = len(st)
+        for y in lay.ychunks[c]:
+            a, b = loc(int(plan.seg_start[y]), int(plan.seg_stop[y]), "window blocks")
+            st.append(a)
+            sp.append(b)
+        chunk_seg.append(("y", c, s0, len(st)))
+        yseg[c] = (s0, len(st))
     nseg = len(st)
-    starts = np.concatenate([np.asarray(st, np.int64) + g * T for g in range(G)]).astype(np.int32)
-    stops = np.concatenate([np.asarray(sp, np.int64) + g * T for g in range(G)]).astype(np.int32)
+    # canonical slots of the gathered chunk totals: rank blocks in rank order, each rank's
+    # chunks as listed above (burn pieces, then year chunks, ascending)
+    counts, sb, sy, off = [], [0] * C, [0] * C, 0
+    for r in range(world):
+        ro = [c for c in range(C) if chunk_owner(c, C, world) == r]
+        for i, k in enumerate(ro):
+            sb[k] = off + i
+        for i, c in enumerate(ro):
+            sy[c] = off + len(ro) + i
+        counts.append(2 * len(ro))
+        off += 2 * len(ro)
+    clast = max(own) if nYl else -1
+    ys = [yseg.get(c, (0, 0))[0] for c in range(C)]
+    ye = [yseg.get(c, (0, 0))[1] for c in range(C)]
+    cs = np.asarray([x[2] for x in chunk_seg], np.int32)
+    ce = np.asarray([x[3] for x in chunk_seg], np.int32)
+    slot = np.arange(len(chunk_seg), dtype=np.int32)          # local totals: local order
+    if world == 1:
+        tot_slots = (np.asarray(sb, np.int32), np.asarray(sy, np.int32))
+    else:
+        tot_slots = (np.asarray(sb, np.int32), np.asarray(sy, np.int32))
     pv = np.asarray(p_vec, dtype=np.int64)
     gg, yy, pp = np.meshgrid(np.arange(G), np.arange(nYl), np.arange(nP), indexing="ij")
     cell_src = (gg * nYl + yy).reshape(-1)                 # cell order [g][year][p]
     cell_n = (pv[pp] + 1).reshape(-1)
     cnt = np.maximum(np.asarray(plan.count, dtype=np.int64)[yl], 1) if nYl else np.zeros(0)
     cell_scale = (1.0 / cnt[yy].astype(np.float64)).reshape(-1)
-    # job order: [val month][g][p]  -> obj reshapes to [nValLocal, G, nP, L]
-    vs = np.asarray(plan.val_start, dtype=np.int64)[yl] - off if nYl else np.zeros(0, np.int64)
-    ve = np.asarray(plan.val_stop, dtype=np.int64)[yl] - off if nYl else np.zeros(0, np.int64)
-    if nYl and (vs.min() < 0 or ve.max() > T):
-        raise ValueError(f"rank {rank}: local months [{off}, {off + T}) miss its validation halo")
+    # validation jobs: [val month][g][p]  -> obj reshapes to [nValLocal, G, nP, L]
+    vrows = ([loc(int(plan.val_start[y]), int(plan.val_stop[y]), "validation halo")
+              for y in yl] if nYl else [])
+    vs = np.asarray([a for a, _ in vrows], np.int64)
+    ve = np.asarray([b for _, b in vrows], np.int64)
     nv = ve - vs
     v_yi = np.repeat(np.arange(nYl), nv)                   # local year index per val row
     v_m = (np.concatenate([np.arange(a, b) for a, b in zip(vs, ve)])
@@ -175,19 +269,39 @@ def _search_setup(months: np.ndarray, years: np.ndarray, p_vec, G: int, T: int, 
     jc = ((g2 * nYl + v_yi[vi]) * nP + p2).reshape(-1)
     jm = (g2 * T + v_m[vi]).reshape(-1)
     jn = (pv[p2] + 1).reshape(-1)
-    out = dict(plan=plan, yl=yl, nYl=nYl, st=st, sp=sp, nseg=nseg, starts=starts, stops=stops,
+    out = dict(plan=plan, layout=lay, yl=yl, nYl=nYl, st=st, sp=sp, nseg=nseg, skip=skip,
+               cs=cs, ce=ce, slot=slot, sb=tot_slots[0], sy=tot_slots[1],
+               ys=np.asarray(ys, np.int32), ye=np.asarray(ye, np.int32), clast=clast,
+               counts=counts, nlc=len(chunk_seg),
                cell_src=np.asarray(cell_src), cell_n=np.asarray(cell_n),
                cell_scale=np.asarray(cell_scale), v_yi=v_yi, v_m=v_m, nVr=nVr,
-               jc=np.asarray(jc), jm=np.asarray(jm), jn=np.asarray(jn), dev_bounds=None,
+               jc=np.asarray(jc), jm=np.asarray(jm), jn=np.asarray(jn), dev_idx=None,
                lvec=torch.as_tensor(l_vec, dtype=torch.float64, device=dev))
     if nseg and dev is not None and dev.type == "cuda":
         from ..ops.ridge import upload
-        out["dev_bounds"] = upload([np.asarray(st, np.int32), np.asarray(sp, np.int32),
-                                    starts, stops], dev)
+        out["dev_idx"] = upload([np.asarray(st, np.int32), np.asarray(sp, np.int32),
+                                 np.concatenate([cs, ce, slot]).astype(np.int32),
+                                 np.concatenate([out["sb"], out["sy"], out["ys"],
+                                                 out["ye"]]).astype(np.int32)], dev)
     if len(_SETUP) > 32:
         _SETUP.clear()
     _SETUP[key] = out
     return out
+
+
+def window_sums(reals: "PfmlReals", su: dict) -> tuple[torch.Tensor, torch.Tensor]:
+    """Expanding-window sums (SD [G, nYl, P, P], Sr [G, nYl, P]) of this rank's hp years in
+    the canonical chunk order (see the module docstring): local chunk totals, ONE all-gather
+    of them, then the windows.  Device: csrc/segsum.hip (segment sums + totals, windows);
+    CPU: the same folds in torch."""
+    from ..ops.ridge import chunk_totals, chunk_windows
+    X, R = reals.denom, reals.r_tilde.contiguous()
+    totD, totR, scratch = chunk_totals(X, R, su)
+    if dist_env().is_dist:
+        # [nlc, G, ...] chunk-major: one known-size all-gather of every rank's chunk totals
+        totD = coll.all_gather_known(totD, [c for c in su["counts"]])
+        totR = coll.all_gather_known(totR, [c for c in su["counts"]])
+    return chunk_windows(X, R, su, totD, totR, scratch)
 
 
 def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridResult:
@@ -200,44 +314,20 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
     nP = len(p_vec)
     all_months = np.asarray(reals.months if reals.all_months is None else reals.all_months,
                             dtype=np.int64)
-    row_off = int(np.searchsorted(all_months, int(reals.months[0]))) if len(reals.months) else 0
-    if len(reals.months) and not np.array_equal(all_months[row_off:row_off + T],
-                                                np.asarray(reals.months, np.int64)):
-        raise ValueError("grid_search: local months must be a contiguous window of all_months")
+    rows = np.searchsorted(all_months, np.asarray(reals.months, np.int64)).astype(np.int64)
+    if len(rows) and (int(rows.max()) >= len(all_months)
+                      or not np.array_equal(all_months[rows], np.asarray(reals.months))):
+        raise ValueError("grid_search: local months must be a subset of all_months")
     su = _search_setup(all_months, np.asarray(years), p_vec, G, T, env.world_size, env.rank, dev,
-                       np.asarray(cfg.l_vec, dtype=np.float64), row_off)
+                       np.asarray(cfg.l_vec, dtype=np.float64), rows)
     lvec = su["lvec"]
     L = lvec.numel()
-    plan, yl, nYl, nseg = su["plan"], su["yl"], su["nYl"], su["nseg"]
+    plan, yl, nYl = su["plan"], su["yl"], su["nYl"]
 
-    # ---- 1. window sums over this rank's blocks ------------------------------------
+    # ---- 1. window sums over this rank's chunks (canonical order; one all-gather) -----
     range_push("search.window_sums")
+    SD, Sr = window_sums(reals, su)
     ready = None
-    if nseg and _pipelined_sums(dev, env, G, su["cell_n"]):
-        # one g at a time: g's big cells start their band reductions while the next g's sums
-        # stream (ridge_utilities waits per group on these events, not on the whole pass)
-        SD, Sr, ready = _window_sums_pipelined(reals, su, G, P, nseg, nYl)
-        totD = totr = None
-    elif nseg:
-        # running sums at every block end in one pass over the symmetric upper triangles
-        # (the burn-in block, rank 0 only, is a prefix segment and not an output row)
-        db = su["dev_bounds"]
-        skip = nseg - nYl
-        SD = window_prefix_sym(reals.denom, su["st"], su["sp"],
-                               dev_bounds=None if db is None else db[:2], skip=skip)
-        Sr = window_prefix_vec(reals.r_tilde.contiguous(), su["st"], su["sp"],
-                               dev_bounds=None if db is None else db[:2], skip=skip)
-        totD, totr = SD[:, -1], Sr[:, -1]
-    else:
-        SD = torch.zeros((G, 0, P, P), dtype=torch.float64, device=dev)
-        Sr = torch.zeros((G, 0, P), dtype=torch.float64, device=dev)
-        totD = torch.zeros((G, P, P), dtype=torch.float64, device=dev)
-        totr = torch.zeros((G, P), dtype=torch.float64, device=dev)
-    if env.is_dist:
-        flat = torch.cat([totD.reshape(G, -1), totr], dim=1)
-        off = coll.exclusive_prefix_sum(flat)
-        SD = SD + off[:, : P * P].view(G, 1, P, P)
-        Sr = Sr + off[:, P * P:].view(G, 1, P)
     range_pop()
 
     # ---- 2. ridge grid + 3. utilities for every (cell, validation month) -------------
@@ -257,70 +347,117 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
 
     th("grid_search.ridge_utilities")
     v_y = yl[v_yi] if nYl else np.zeros(0, np.int64)
-    if gather and env.is_dist:
-        # every rank's share of the validation rows follows from the global plan: ONE
-        # all-gather of the utilities; months and years are rebuilt locally
-        range_push("search.gather")
-        nv_all = np.asarray(plan.val_stop, np.int64) - np.asarray(plan.val_start, np.int64)
-        counts = [int(nv_all[list(coll.contiguous_split(len(years), env.world_size, r))].sum())
-                  for r in range(env.world_size)]
-        obj = coll.all_gather_known(obj, counts)
-        v_m = np.concatenate([np.arange(a, b) for a, b in zip(plan.val_start, plan.val_stop)])
-        v_y = np.repeat(np.arange(len(years)), nv_all)
-        range_pop()
-    else:
-        v_m = v_m + row_off                               # local rows -> global rows
-    vm = all_months[v_m]
-    vy = np.asarray(years, dtype=np.int64)[v_y]
-    return GridResult(years=years, p_vec=p_vec, l_vec=cfg.l_vec, years_local=years[yl],
-                      beta=beta, val_months=vm, val_year=vy, obj=obj)
+    v_m = rows[v_m] if len(v_m) else v_m                 # local rows -> global rows
+    res = GridResult(years=years, p_vec=p_vec, l_vec=cfg.l_vec, years_local=years[yl],
+                     beta=beta, val_months=all_months[v_m],
+                     val_year=np.asarray(years, dtype=np.int64)[v_y], obj=obj,
+                     window=(SD, Sr), gathered=not env.is_dist, all_months=all_months)
+    return gather_grid(res) if gather else res
+
+
+def gather_grid(grid: GridResult) -> GridResult:
+    """ONE all-gather of the per-(month, cell) utilities of every rank (each rank's row count
+    follows from the shared plan); validation months and years rebuilt locally.  No-op on one
+    rank or when already gathered."""
+    env = dist_env()
+    if grid.gathered or not env.is_dist:
+        grid.gathered = True
+        return grid
+    range_push("search.gather")
+    years = np.asarray(grid.years)
+    plan = make_plan(grid.all_months, years)
+    nv_all = np.asarray(plan.val_stop, np.int64) - np.asarray(plan.val_start, np.int64)
+    counts = [int(nv_all[rank_years(len(years), env.world_size, r)].sum())
+              for r in range(env.world_size)]
+    grid.obj = coll.all_gather_known(grid.obj, counts)
+    v_m = np.concatenate([np.arange(a, b) for a, b in zip(plan.val_start, plan.val_stop)])
+    grid.val_months = grid.all_months[v_m]
+    grid.val_year = years.astype(np.int64)[np.repeat(np.arange(len(years)), nv_all)]
+    grid.gathered = True
+    range_pop()
+    return grid
+
+
+def _local_val_rows(grid: GridResult, reals: PfmlReals) -> dict:
+    """{hp year: [(row in grid.obj, local month row)]} of this rank's validation months (the
+    utilities of a not-yet-gathered grid, or the gathered rows whose months are local)."""
+    months = np.asarray(reals.months, dtype=np.int64)
+    out = {}
+    for i, (vm, vy) in enumerate(zip(grid.val_months, grid.val_year)):
+        j = int(np.searchsorted(months, vm))
+        if j < len(months) and months[j] == vm:
+            out.setdefault(int(vy), []).append((i, j))
+    return out
+
+
+def _oracle_cell(grid: GridResult, reals: PfmlReals, g: int, yi: int, pi: int, SD=None,
+                 Sr=None):
+    """fp64 CPU oracle of one (g, local year, p) cell: one pivoted-LU solve per lambda
+    (np.linalg.solve semantics) on the window sums ``SD``/``Sr`` (default: the grid's own),
+    and its validation utilities on this rank's months.  Returns (beta [L, P], [(row,
+    utilities [L])])."""
+    from ..ops.ridge import quadform_utilities, ridge_grid
+    years = np.asarray(grid.years)
+    plan = make_plan(grid.all_months if grid.all_months is not None else reals.months, years)
+    y = int(np.nonzero(years == grid.years_local[yi])[0][0])
+    n = int(grid.p_vec[pi]) + 1
+    if SD is None:
+        SD, Sr = grid.window[0][g, yi].cpu(), grid.window[1][g, yi].cpu()
+    lv = torch.as_tensor(grid.l_vec, dtype=torch.float64)
+    b = ridge_grid(SD[None], Sr[None], np.array([0]), np.array([n]),
+                   np.array([1.0 / max(int(plan.count[y]), 1)]), lv)[0]
+    rows = _local_val_rows(grid, reals).get(int(years[y]), [])
+    util = []
+    if rows:
+        denom, rt = reals.denom.cpu(), reals.r_tilde.cpu()
+        T = denom.shape[1]
+        jm = np.array([g * T + j for _, j in rows])
+        o = quadform_utilities(denom.reshape(-1, *denom.shape[2:]), rt.reshape(-1, rt.shape[-1]),
+                               b[None], np.zeros(len(rows), np.int64), jm, np.full(len(rows), n))
+        util = [(i, o[k]) for k, (i, _) in enumerate(rows)]
+    return b, util
 
 
 def check_against_oracle(grid: GridResult, reals: PfmlReals, cfg: Config, ncells: int = 3,
                          seed: int = 0) -> dict:
-    """``--check``: recompute a few (g, year, p) cells of this rank from scratch
-    with the fp64 CPU oracle - expanding-window sums by plain summation, one
-    ``torch.linalg.solve`` per lambda, quadratic forms one by one - and report the max
-    relative error of the device coefficients and utilities (the largest-n cell is always
-    among them)."""
-    from ..ops.ridge import quadform_utilities, ridge_grid
-    months = np.asarray(reals.months, dtype=np.int64)
-    plan = make_plan(months, np.asarray(grid.years))
-    yl = np.nonzero(np.isin(np.asarray(grid.years), np.asarray(grid.years_local)))[0]
+    """``--check``: recompute a few (g, year, p) cells of this rank with the
+    fp64 CPU oracle - one ``torch.linalg.solve`` per lambda, quadratic forms one by one - and
+    report the max relative error of the device coefficients and utilities (the largest-n cell
+    is always among them).  The expanding-window sums are re-added by plain summation when
+    this rank holds every month up to the window (one rank); a shard checks the solves and
+    utilities on its own window sums and reports the window sums as unchecked."""
+    years = np.asarray(grid.years)
+    nYl = len(grid.years_local)
     G, nP = reals.G, len(grid.p_vec)
-    if len(yl) == 0:
+    if nYl == 0:
         return {"cells": 0}
+    months = np.asarray(reals.months, dtype=np.int64)
+    allm = grid.all_months if grid.all_months is not None else months
+    full = len(months) == len(allm)
+    plan = make_plan(allm, years)
     rng = np.random.default_rng(seed)
-    picks = {(0, len(yl) - 1, nP - 1)}
-    while len(picks) < min(ncells, G * len(yl) * nP):
-        picks.add((int(rng.integers(G)), int(rng.integers(len(yl))), int(rng.integers(nP))))
-    lv = torch.as_tensor(grid.l_vec, dtype=torch.float64)
-    denom, rt = reals.denom.cpu(), reals.r_tilde.cpu()
+    picks = {(0, nYl - 1, nP - 1)}
+    while len(picks) < min(ncells, G * nYl * nP):
+        picks.add((int(rng.integers(G)), int(rng.integers(nYl)), int(rng.integers(nP))))
     obj_host = grid.obj.cpu()
-    v_rows = {}
-    if obj_host.shape[0] == len(grid.val_months):       # gathered or single-rank utilities
-        for i, (vm, vy) in enumerate(zip(grid.val_months, grid.val_year)):
-            v_rows.setdefault(int(vy), []).append((i, int(vm)))
-    eb = eo = 0.0
+    eb = eo = ew = 0.0
     for g, yi, pi in sorted(picks):
-        y = int(yl[yi])
-        n = int(grid.p_vec[pi]) + 1
-        stop = int(plan.seg_stop[y])
-        SD = denom[g, :stop].sum(0)[None]
-        Sr = rt[g, :stop].sum(0)[None]
-        ref = ridge_grid(SD, Sr, np.array([0]), np.array([n]),
-                         np.array([1.0 / max(int(plan.count[y]), 1)]), lv)[0]
+        SD = Sr = None
+        if full:
+            y = int(np.nonzero(years == grid.years_local[yi])[0][0])
+            stop = int(plan.seg_stop[y])
+            SD = reals.denom[g, :stop].cpu().sum(0)
+            Sr = reals.r_tilde[g, :stop].cpu().sum(0)
+            wd = grid.window[0][g, yi].cpu()
+            ew = max(ew, float((wd - SD).abs().max() / SD.abs().max().clamp_min(1e-300)))
+        ref, util = _oracle_cell(grid, reals, g, yi, pi, SD, Sr)
         got = grid.beta[g, yi, pi].cpu()
         eb = max(eb, float(((got - ref).norm(dim=-1) / ref.norm(dim=-1).clamp_min(1e-300)).max()))
-        rows = v_rows.get(int(grid.years[y]), [])
-        if rows:
-            jm = np.array([g * len(months) + int(np.searchsorted(months, vm)) for _, vm in rows])
-            oref = quadform_utilities(denom.reshape(-1, *denom.shape[2:]),
-                                      rt.reshape(-1, rt.shape[-1]), ref[None],
-                                      np.zeros(len(rows), np.int64), jm, np.full(len(rows), n))
-            ogot = obj_host[[i for i, _ in rows], g, pi]
+        for i, oref in util:
+            ogot = obj_host[i, g, pi]
             eo = max(eo, float(((ogot - oref).abs() / oref.abs().clamp_min(1e-12)).max()))
-    out = {"cells": len(picks), "beta_max_rel_err": eb, "obj_max_rel_err": eo}
+    out = {"cells": len(picks), "beta_max_rel_err": eb, "obj_max_rel_err": eo,
+           "window_sums_max_rel_err": ew if full else None}
     log.info(f"check vs CPU oracle on {len(picks)} cells: beta {eb:.2e}, utilities {eo:.2e}")
     return out
 
@@ -341,102 +478,28 @@ def nonfinite_cells(grid: GridResult) -> list:
 
 def recompute_cells(grid: GridResult, reals: PfmlReals, cells) -> dict:
     """Failure recovery: recompute the coefficients of ``cells`` [(g, local
-    year, p)] and their validation utilities from scratch with the fp64 CPU oracle - window
-    sums by plain summation, one pivoted-LU solve per lambda (np.linalg.solve semantics: an
-    exactly singular system stays NaN, where the reference raises) - and write them back into
-    ``grid``.  Needs every month from the first one on this rank (world 1, or the rank that
-    holds the burn-in); returns counts."""
-    from ..ops.ridge import quadform_utilities, ridge_grid
-    months = np.asarray(reals.months, dtype=np.int64)
-    allm = np.asarray(reals.months if reals.all_months is None else reals.all_months, np.int64)
-    if len(cells) and (len(months) == 0 or months[0] != allm[0]):
-        raise RuntimeError("recompute_cells: this rank lacks the months before its windows")
-    plan = make_plan(months, np.asarray(grid.years))
-    yl = np.nonzero(np.isin(np.asarray(grid.years), np.asarray(grid.years_local)))[0]
-    lv = torch.as_tensor(grid.l_vec, dtype=torch.float64)
-    denom, rt = reals.denom.cpu(), reals.r_tilde.cpu()
-    rows_of = {}
-    if grid.obj.shape[0] == len(grid.val_months):
-        for i, (vm, vy) in enumerate(zip(grid.val_months, grid.val_year)):
-            rows_of.setdefault(int(vy), []).append((i, int(vm)))
+    year, p)] and their validation utilities with the fp64 CPU oracle - one pivoted-LU solve
+    per lambda (np.linalg.solve semantics: an exactly singular system stays NaN, where the
+    reference raises) on the rank's own window sums (kept by grid_search; the fault being
+    repaired is in the solves, the summands were checked finite in S4) - and write them back
+    into ``grid``.  Works on every rank: call it before ``gather_grid`` (the utilities are
+    still local).  Returns counts."""
+    if grid.gathered and dist_env().is_dist:
+        raise RuntimeError("recompute_cells: repair the local grid before gather_grid")
     still = 0
     for g, yi, pi in cells:
-        y = int(yl[yi])
         n = int(grid.p_vec[pi]) + 1
-        stop = int(plan.seg_stop[y])
-        SD = denom[g, :stop].sum(0)[None]
-        Sr = rt[g, :stop].sum(0)[None]
-        b = ridge_grid(SD, Sr, np.array([0]), np.array([n]),
-                       np.array([1.0 / max(int(plan.count[y]), 1)]), lv)[0]
+        b, util = _oracle_cell(grid, reals, g, yi, pi)
         grid.beta[g, yi, pi] = b.to(grid.beta.device)
         still += int(not bool(torch.isfinite(b[:, :n]).all()))
-        rows = rows_of.get(int(grid.years[y]), [])
-        if rows:
-            jm = np.array([g * len(months) + int(np.searchsorted(months, vm)) for _, vm in rows])
-            o = quadform_utilities(denom.reshape(-1, *denom.shape[2:]),
-                                   rt.reshape(-1, rt.shape[-1]), b[None],
-                                   np.zeros(len(rows), np.int64), jm, np.full(len(rows), n))
-            grid.obj[[i for i, _ in rows], g, pi] = o.to(grid.obj.device)
+        for i, o in util:
+            grid.obj[i, g, pi] = o.to(grid.obj.device)
     return {"recomputed": len(cells), "singular": still}
 
 
 # ---------------------------------------------------------------------------------------
 # Scores (K17): expanding mean by (p, l) over eom_ret, dense rank per eom_ret.
 # ---------------------------------------------------------------------------------------
-def _pipelined_sums(dev, env, G: int, cell_n) -> bool:
-    """Per-g pipelined window sums (opt-in, PFML_PIPE_SUMS=1): one device holding the whole
-    grid (not a multi-rank shard), 2 g (three streams in all) and the two-stream band policy
-    (many big cells).  Measured on MI355X (profiles/r02_pipe_sums_ab.json): eager launches
-    6.06-6.11 vs 6.48-6.54 ms per step, but under HIP-graph replay (the default) 6.00 vs
-    6.02-6.10 ms - the graph executor regroups the three branches onto its own queues and the
-    g = 1 big cells then wait ~0.3 ms for CUs behind the small cells - so it stays off."""
-    import os
-    from ..ops.ridge import band_policy
-    if (dev.type != "cuda" or env.is_dist or G != 2
-            or os.environ.get("PFML_PIPE_SUMS", "0") != "1"):
-        return False
-    return band_policy(np.asarray(cell_n))[1]
-
-
-def _window_sums_pipelined(reals: PfmlReals, su: dict, G: int, P: int, nseg: int, nYl: int):
-    """Window sums of every g into one [G, nYl, P, P] stack, g after g: g = 0 on the current
-    stream, g > 0 on a side stream chained after g - 1 (the passes are HBM-bound, so running
-    them concurrently would only delay g = 0); the r̄ sums (tiny) lead that side stream.
-    Returns (SD, Sr, ready) with ready as ridge_utilities takes it.  Three streams in all:
-    current, this side stream, and the small cells' stream in ridge_utilities."""
-    from ..ops.ridge import _side_stream
-    dev = reals.denom.device
-    T = reals.denom.shape[1]
-    db = su["dev_bounds"]
-    skip = nseg - nYl
-    cur = torch.cuda.current_stream(dev)
-    side = _side_stream(dev, 16)
-    side.wait_stream(cur)
-    SD = torch.empty((G, nYl, P, P), dtype=torch.float64, device=dev)
-    with torch.cuda.stream(side):
-        Sr = window_prefix_vec(reals.r_tilde.contiguous(), su["st"], su["sp"],
-                               dev_bounds=None if db is None else db[:2], skip=skip)
-        ev_r = torch.cuda.Event()
-        ev_r.record(side)
-    events = []
-    for g in range(G):
-        st = cur if g == 0 else side
-        if g > 0:
-            st.wait_event(events[-1])
-        with torch.cuda.stream(st):
-            window_prefix_sym(reals.denom[g:g + 1], su["st"], su["sp"],
-                              dev_bounds=None if db is None else db[:2], skip=skip,
-                              out=SD[g:g + 1])
-            ev = torch.cuda.Event()
-            ev.record(st)
-        events.append(ev)
-    # big cells of g run on the stream that summed g (g = 0: after its sums on cur; g > 0:
-    # after its sums on the side stream); only the r̄ sums need an event wait
-    ready = {"key": su["cell_src"] // max(nYl, 1), "streams": [cur] + [side] * (G - 1),
-             "events": [[ev_r]] + [[]] * (G - 1), "all": [events[-1], ev_r]}
-    return SD, Sr, ready
-
-
 def _cumsum0(x: torch.Tensor) -> torch.Tensor:
     """cumsum along dim 0 as an innermost-dim scan (the outer-dim scan kernel of torch-ROCm
     takes ~0.2-0.4 ms on these [months, cells] shapes; the innermost one ~30 us)."""
@@ -551,6 +614,6 @@ def gather_beta(grid: GridResult) -> tuple[np.ndarray, torch.Tensor]:
     if not env.is_dist:
         return np.asarray(grid.years_local), b.permute(1, 0, 2, 3, 4).contiguous()
     nY = len(grid.years)
-    counts = [len(coll.contiguous_split(nY, env.world_size, r)) for r in range(env.world_size)]
+    counts = [len(rank_years(nY, env.world_size, r)) for r in range(env.world_size)]
     b = coll.all_gather_known(b, counts)                    # years split contiguously
     return np.asarray(grid.years), b.permute(1, 0, 2, 3, 4).contiguous()

@@ -380,8 +380,13 @@ def _db_mu(M: torch.Tensor, Minv: torch.Tensor, unscaled: bool, out: torch.Tenso
     if unscaled:
         out.fill_(1.0)
     else:
+        # (ratio)^(1/4) as two IEEE square roots: torch's CPU pow is vectorised over the batch
+        # and not correctly rounded, so x ** 0.25 differed in the last bit between a month in
+        # a vector lane and one in the scalar tail - a month's m_tilde then depended on the
+        # months batched with it (the S4 summands must be bitwise the same however the months
+        # are sharded)
         nm = torch.linalg.matrix_norm(M).clamp_min(1e-300)
-        out.copy_((torch.linalg.matrix_norm(Minv) / nm) ** 0.25)
+        out.copy_((torch.linalg.matrix_norm(Minv) / nm).sqrt().sqrt())
 
 
 def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tensor | None,

@@ -116,6 +116,107 @@ def window_prefix_sym(X: torch.Tensor, starts, stops, dev_bounds=None,
     return out
 
 
+nat.register_hip("pfml_wsum_chunk_totals", [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                            C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                            C.c_int, C.c_void_p, C.c_void_p, C.c_int64,
+                                            C.c_void_p])
+nat.register_hip("pfml_wsum_chunk_prefix", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                            C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                            C.c_int64, C.c_int, C.c_void_p])
+nat.register_hip("pfml_wvec_chunk", [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_void_p,
+                                     C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                     C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int64,
+                                     C.c_void_p, C.c_void_p])
+
+
+def _fold_months(X: torch.Tensor, a: int, b: int) -> torch.Tensor:
+    """CPU segment sum: left fold over months a .. b-1 of X [G, T, ...] (a fixed order, the
+    same on every rank that holds these months)."""
+    acc = torch.zeros_like(X[:, 0])
+    for t in range(a, b):
+        acc = acc + X[:, t]
+    return acc
+
+
+def chunk_totals(X: torch.Tensor, R: torch.Tensor, su: dict):
+    """Kernel A of the canonical chunked window sums (models/search.py): segment sums of this
+    rank's segments and the totals of its chunks, chunk-major [nlc, G, P, P] / [nlc, G, P].
+    Returns (totD, totR, bufs); ``bufs`` carries the segment sums to ``chunk_windows``."""
+    G, T, P, _ = X.shape
+    nlc, nseg, skip, nYl = su["nlc"], su["nseg"], su["skip"], su["nYl"]
+    totD = torch.empty((nlc, G, P, P), dtype=X.dtype, device=X.device)
+    totR = torch.empty((nlc, G, P), dtype=X.dtype, device=X.device)
+    out = torch.empty((G, nYl, P, P), dtype=X.dtype, device=X.device)
+    if nat.is_device(X):
+        if X.dtype != torch.float64 or not X.is_contiguous():
+            raise ValueError("chunk_totals: contiguous fp64 required")
+        scratch = (torch.empty((G, skip, P, P), dtype=X.dtype, device=X.device) if skip
+                   else None)
+        st, sp, idx, cidx = su["dev_idx"]
+        lib = nat.hip_lib()
+        s = nat.stream_of(X)
+        nat.check(lib.pfml_wsum_chunk_totals(
+            X.data_ptr(), P, T, G, st.data_ptr(), sp.data_ptr(), nseg, skip, out.data_ptr(),
+            scratch.data_ptr() if scratch is not None else None, nlc, idx.data_ptr(),
+            totD.data_ptr(), G * P * P, s), "pfml_wsum_chunk_totals")
+        nat.check(lib.pfml_wvec_chunk(
+            R.data_ptr(), P, T, G, st.data_ptr(), sp.data_ptr(), nseg, skip, 0, nlc,
+            idx.data_ptr(), su["layout"].C, cidx.data_ptr(), su["clast"], totR.data_ptr(), G * P,
+            None, s), "pfml_wvec_chunk")
+        return totD, totR, {"out": out, "scratch": scratch}
+    segD = [_fold_months(X, a, b) for a, b in zip(su["st"], su["sp"])]
+    segR = [_fold_months(R, a, b) for a, b in zip(su["st"], su["sp"])]
+    for lc in range(nlc):
+        accD, accR = torch.zeros_like(X[:, 0]), torch.zeros_like(R[:, 0])
+        for s in range(int(su["cs"][lc]), int(su["ce"][lc])):
+            accD = accD + segD[s]
+            accR = accR + segR[s]
+        totD[lc], totR[lc] = accD, accR
+    return totD, totR, {"out": out, "segD": segD, "segR": segR}
+
+
+def chunk_windows(X: torch.Tensor, R: torch.Tensor, su: dict, totD: torch.Tensor,
+                  totR: torch.Tensor, bufs: dict) -> tuple[torch.Tensor, torch.Tensor]:
+    """Kernel B of the canonical chunked window sums: E = fold of the burn-in totals, then per
+    year chunk the fold of its segments from the prefix P_c (``totD``/``totR``: every chunk's
+    total, gathered, in the canonical slot order of ``su``).  Returns (SD, Sr)."""
+    G, T, P, _ = X.shape
+    nseg, skip, nYl, clast = su["nseg"], su["skip"], su["nYl"], su["clast"]
+    C = su["layout"].C
+    out = bufs["out"]
+    Sr = torch.empty((G, nYl, P), dtype=X.dtype, device=X.device)
+    if nat.is_device(X):
+        st, sp, idx, cidx = su["dev_idx"]
+        lib = nat.hip_lib()
+        s = nat.stream_of(X)
+        scratch = bufs["scratch"]
+        nat.check(lib.pfml_wsum_chunk_prefix(
+            P, G, nseg, skip, out.data_ptr(), scratch.data_ptr() if scratch is not None else None,
+            C, cidx.data_ptr(), totD.data_ptr(), G * P * P, clast, s), "pfml_wsum_chunk_prefix")
+        nat.check(lib.pfml_wvec_chunk(
+            R.data_ptr(), P, T, G, st.data_ptr(), sp.data_ptr(), nseg, skip, 1, 0,
+            idx.data_ptr(), C, cidx.data_ptr(), clast, totR.data_ptr(), G * P, Sr.data_ptr(), s),
+            "pfml_wvec_chunk")
+        return out, Sr
+    segD, segR = bufs["segD"], bufs["segR"]
+    pD, pR = torch.zeros_like(X[:, 0]), torch.zeros_like(R[:, 0])
+    for k in range(C):
+        pD = pD + totD[int(su["sb"][k])]
+        pR = pR + totR[int(su["sb"][k])]
+    for c in range(clast + 1):
+        aD, aR = pD, pR
+        for s in range(int(su["ys"][c]), int(su["ye"][c])):
+            aD = aD + segD[s]
+            aR = aR + segR[s]
+            if s >= skip:
+                out[:, s - skip] = aD
+                Sr[:, s - skip] = aR
+        if c < clast:
+            pD = pD + totD[int(su["sy"][c])]
+            pR = pR + totR[int(su["sy"][c])]
+    return out, Sr
+
+
 class _HostClock:
     """PFML_HOST_TIMING=1: print host-side section times (microseconds) to stderr;
     PFML_HOST_TIMING=sync: synchronise the device at every mark (section = wall time of the
@@ -337,7 +438,7 @@ def _side_stream(dev: torch.device, k: int = 0) -> torch.cuda.Stream:
     return _SIDE[key]
 
 
-BAND_SINGLE, BAND_MULTI = 1, 2
+BAND_SINGLE, BAND_MULTI, BAND_FUSED = 1, 2, 3
 # Above this many largest-n cells per launch the one-workgroup-per-cell reduction (throughput
 # form, big cells on their own stream) beats the multi-workgroup one (latency form); measured
 # on MI355X, tools/bench_band.py, and in the strong-scaling rehearsal: 53 big cells per rank
@@ -376,7 +477,9 @@ def band_policy(cell_n: np.ndarray) -> tuple[int, bool]:
         mode = BAND_SINGLE
     elif env == "m":
         mode = BAND_MULTI
-    two = mode == BAND_SINGLE
+    elif env == "f":
+        mode = BAND_FUSED
+    two = mode in (BAND_SINGLE, BAND_FUSED)
     v = os.environ.get("PFML_RIDGE_STREAMS")
     if v:
         two = v.strip() == "2"
@@ -403,14 +506,15 @@ def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell,
     if split and big_key is not None:
         # one big-cell group per key (pipelined window sums), then the small cells
         parts = tuple((big & (big_key == k), None) for k in np.unique(big_key[big]))
-        parts += ((~big, BAND_SINGLE),)
+        parts += ((~big, None),)
     elif split and nhy:
         # the first nhy big cells (in cell order) -> multi-workgroup group
         hy = big & (np.cumsum(big) <= nhy)
         parts = ((big & ~hy, BAND_SINGLE), (hy, BAND_MULTI), (~big, BAND_SINGLE))
     elif split:
-        # big cells in the launch's mode; the small ones always one workgroup per cell
-        parts = ((big, None), (~big, BAND_SINGLE))
+        # big cells in the launch's mode; the small ones too (one workgroup per cell: the
+        # split form is only taken with the single or the fused reduction)
+        parts = ((big, None), (~big, None))
     else:
         parts = ((np.ones(len(cell_n), dtype=bool), None),)
     groups, arrays = [], []

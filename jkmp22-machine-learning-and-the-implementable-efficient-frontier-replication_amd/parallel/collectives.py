@@ -14,10 +14,19 @@ import torch.distributed as dist
 from .dist import env
 
 
+def _comm_device(x: torch.Tensor) -> torch.device:
+    """Where a collective on ``x`` must run: gloo takes host tensors (PFML_DIST_BACKEND=gloo:
+    several ranks sharing one GPU, a rehearsal of the multi-GPU path where RCCL cannot run),
+    RCCL device tensors - so a CPU tensor under RCCL (e.g. the S9 CPU recompute of a failure
+    recovery) is staged through this rank's GPU, a device tensor under gloo through the host."""
+    e = env()
+    if e.backend == "gloo":
+        return torch.device("cpu")
+    return e.device if e.device.type == "cuda" else x.device
+
+
 def _staged(x: torch.Tensor) -> bool:
-    """gloo over device tensors (PFML_DIST_BACKEND=gloo: several ranks sharing one GPU, a
-    rehearsal of the multi-GPU path where RCCL cannot run): the message goes via the host."""
-    return env().backend == "gloo" and x.is_cuda
+    return x.device != _comm_device(x)
 
 
 def all_gather_cat(x: torch.Tensor) -> torch.Tensor:
@@ -26,7 +35,7 @@ def all_gather_cat(x: torch.Tensor) -> torch.Tensor:
     if not e.is_dist:
         return x
     if _staged(x):
-        return all_gather_cat(x.cpu()).to(x.device)
+        return all_gather_cat(x.to(_comm_device(x))).to(x.device)
     x = x.contiguous()
     out = torch.empty((e.world_size * x.shape[0], *x.shape[1:]), dtype=x.dtype, device=x.device)
     dist.all_gather_into_tensor(out, x)
@@ -86,8 +95,7 @@ def all_reduce_max(v: float, device=None) -> float:
     if not e.is_dist:
         return float(v)
     t = torch.tensor([float(v)], dtype=torch.float64, device=device or e.device)
-    if _staged(t):
-        t = t.cpu()
+    t = t.to(_comm_device(t))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -96,7 +104,7 @@ def all_reduce_sum_(t: torch.Tensor) -> torch.Tensor:
     e = env()
     if e.is_dist:
         if _staged(t):
-            h = t.cpu()
+            h = t.to(_comm_device(t))
             dist.all_reduce(h, op=dist.ReduceOp.SUM)
             t.copy_(h)
         else:
@@ -143,7 +151,7 @@ def send_next(x: torch.Tensor) -> None:
     w_start vector: N doubles over one xGMI link)."""
     e = env()
     if e.is_dist and e.rank + 1 < e.world_size:
-        dist.send(x.cpu() if _staged(x) else x.contiguous(), dst=e.rank + 1)
+        dist.send(x.to(_comm_device(x)).contiguous(), dst=e.rank + 1)
 
 
 def recv_prev(like: torch.Tensor) -> torch.Tensor:
@@ -152,7 +160,7 @@ def recv_prev(like: torch.Tensor) -> torch.Tensor:
     out = torch.empty_like(like)
     if e.is_dist and e.rank > 0:
         if _staged(out):
-            h = torch.empty_like(out, device="cpu")
+            h = torch.empty_like(out, device=_comm_device(out))
             dist.recv(h, src=e.rank - 1)
             out.copy_(h)
         else:

@@ -19,10 +19,11 @@ its artifact + done-marker (utils/artifacts.py) so a later run resumes from the 
 whose inputs changed.
 
 Multi-GPU (torchrun, one rank per GPU, RCCL):
-  * pfml-input / pfml-search-coef: the hp years are split contiguously over ranks and each
-    rank builds the S4 summands of ITS window blocks plus the one-block validation halo
-    (search.local_month_range) - no per-month matrix crosses ranks; the expanding windows
-    need one P x P all-gather of block totals, the utilities one all-gather.  Both stages
+  * pfml-input / pfml-search-coef: the months are cut into canonical chunks (burn-in pieces
+    and groups of hp years, search.win_layout) that ranks own whole; each rank builds the S4
+    summands of ITS chunks plus the one-block validation halo (search.local_month_rows) - no
+    per-month matrix crosses ranks, the S4 months balance, and the expanding windows need one
+    all-gather of P x P chunk totals (bitwise the 1-rank sums), the utilities one.  Both stages
     keep per-rank artifacts and per-rank done markers: a resumed run recomputes only the
     shards whose marker is missing or stale.
   * pfml-aim: each rank forms the aim portfolios of the OOS months whose coefficients and
@@ -165,9 +166,8 @@ class Pipeline:
         self._load_common()
         st = self.state
         m2 = st["grids"]["m2"]
-        lo, hi = search.local_month_range(m2, self.cfg.hp_years, self.env.world_size,
-                                          self.env.rank)
-        months = m2[lo:hi]
+        months = m2[search.local_month_rows(m2, self.cfg.hp_years, self.env.world_size,
+                                            self.env.rank)]
         if self.checkpoint and self.store.is_done("pfml-input", self._rank_key("pfml-input"),
                                                   rank=self.env.rank):
             log.info(f"[pfml-input] rank {self.env.rank}: shard up to date (resume)")
@@ -239,31 +239,35 @@ class Pipeline:
             st["rff_w"] = t["rff_w"].numpy()
 
     def _guard_grid(self, grid) -> None:
-        """Failure detection for S5: (g, year, p) cells whose coefficients are not
-        finite after the device repair are recomputed with the fp64 CPU oracle (coefficients
-        and their validation utilities).  A shard that cannot rebuild its window sums (it
-        lacks the burn-in months) raises before writing its done marker, so a resumed run
-        recomputes just that shard.  ``run.fault_inject = "pfml-search-coef"`` poisons one
-        cell of every shard to exercise this path."""
+        """Failure detection for S5, run on every rank BEFORE the utilities are
+        gathered: (g, year, p) cells whose coefficients are not finite after the device repair
+        are re-solved with the fp64 CPU oracle on the rank's own window sums, and their
+        validation utilities recomputed, so the gathered frame - and every rank's choice of
+        hyper-parameters - is built from repaired rows.  Whether a cell stayed singular is
+        decided collectively (one max all-reduce) so that no rank raises alone while its
+        peers wait in the gather.  ``run.fault_inject = "pfml-search-coef"`` poisons one cell
+        of every shard to exercise this path."""
         if self.cfg.run.fault_inject.startswith("pfml-search-coef") and grid.beta.shape[1]:
             grid.beta[0, 0, -1, len(grid.l_vec) // 2, 0] = float("nan")
             COUNTERS.add("fault_injected")
         bad = search.nonfinite_cells(grid)
-        if not bad:
-            return
-        log.warning(f"non-finite coefficients in {len(bad)} cell(s) on rank "
-                    f"{self.env.rank}: recomputing on the CPU oracle")
-        res = search.recompute_cells(grid, self.state["reals"], bad)
-        COUNTERS.add("pfml_search.recomputed_cells", res["recomputed"])
-        if res["singular"]:
+        res = {"recomputed": 0, "singular": 0}
+        if bad:
+            log.warning(f"non-finite coefficients in {len(bad)} cell(s) on rank "
+                        f"{self.env.rank}: recomputing on the CPU oracle")
+            res = search.recompute_cells(grid, self.state["reals"], bad)
+            COUNTERS.add("pfml_search.recomputed_cells", res["recomputed"])
+        singular = coll.all_reduce_max(float(res["singular"]), device=self.device)
+        if singular:
             COUNTERS.add("pfml_search.singular_cells", res["singular"])
-            log.warning(f"{res['singular']} cell(s) singular even for pivoted LU: NaN kept "
-                        "(never ranked; the reference raises here)")
+            log.warning(f"{res['singular']} cell(s) on rank {self.env.rank} singular even for "
+                        "pivoted LU: NaN kept (never ranked; the reference raises here)")
 
     def _pfml_search_coef(self):
         self._ensure_reals()
-        grid = search.grid_search(self.state["reals"], self.cfg)
+        grid = search.grid_search(self.state["reals"], self.cfg, gather=False)
         self._guard_grid(grid)
+        grid = search.gather_grid(grid)
         if self.cfg.run.check:
             metric(stage="pfml-search-coef", check=search.check_against_oracle(
                 grid, self.state["reals"], self.cfg), rank=self.env.rank)

@@ -46,13 +46,13 @@ def _worker(rank, world, port, out_dir, task):
     try:
         if task in ("grid", "grid_local"):
             from pfml.models.search import (PfmlReals, gather_beta, grid_search,
-                                            local_month_range)
+                                            local_month_rows)
             cfg, reals = _small_reals()
             if task == "grid_local":
-                # each rank holds ONLY its hp-year blocks + validation halo (S4 sharding)
-                lo, hi = local_month_range(reals.months, cfg.hp_years, world, rank)
-                reals = PfmlReals(reals.months[lo:hi], reals.r_tilde[:, lo:hi].clone(),
-                                  reals.denom[:, lo:hi].clone(), all_months=reals.months)
+                # each rank holds ONLY its chunks' months + validation halo (S4 sharding)
+                rows = local_month_rows(reals.months, cfg.hp_years, world, rank)
+                reals = PfmlReals(reals.months[rows], reals.r_tilde[:, rows].clone(),
+                                  reals.denom[:, rows].clone(), all_months=reals.months)
             res = grid_search(reals, cfg)
             years, beta = gather_beta(res)
             if rank == 0:
@@ -102,20 +102,31 @@ def test_grid_search_sharded_matches_single(world, task, tmp_path):
     assert np.array_equal(got["vm"].numpy(), ref.val_months)
     assert np.array_equal(got["vy"].numpy(), ref.val_year)
     assert np.array_equal(got["years"].numpy(), np.asarray(cfg.hp_years))
-    assert torch.allclose(got["obj"], ref.obj, rtol=1e-10, atol=1e-13)
-    assert torch.allclose(got["beta"], ref_beta, rtol=1e-9, atol=1e-12)
+    # canonical chunked window sums: BITWISE the one-process coefficients and utilities
+    assert torch.equal(got["obj"], ref.obj)
+    assert torch.equal(got["beta"], ref_beta)
 
 
-def test_local_month_ranges_cover_and_overlap_by_one_block():
-    from pfml.models.search import local_month_range, make_plan
+def test_local_month_rows_cover_once_plus_halo():
+    """Every month is computed by exactly one rank, plus each rank's one-block validation
+    halo; the burn-in is spread, so S4 months balance (max / mean <= 1.15 at world 8 on the
+    production date grid)."""
+    from pfml.config import Config
+    from pfml.models.search import local_month_rows, make_plan, s4_month_counts
+    from pfml.utils.dates import mi_from_ym
     cfg, reals = _small_reals()
     years = np.asarray(cfg.hp_years)
     plan = make_plan(reals.months, years)
-    for world in (2, 3, 5):
-        rng = [local_month_range(reals.months, years, world, r) for r in range(world)]
-        assert rng[0][0] == 0 and rng[-1][1] == int(plan.val_stop[-1])
-        for (a0, a1), (b0, b1) in zip(rng[:-1], rng[1:]):
-            assert b0 <= a1 and a1 - b0 <= 12          # halo = at most one year block
+    for world in (2, 3, 5, 8):
+        rows = [local_month_rows(reals.months, years, world, r) for r in range(world)]
+        allr = np.concatenate(rows)
+        assert set(allr.tolist()) == set(range(int(plan.val_stop[-1])))
+        extra = len(allr) - len(np.unique(allr))
+        assert extra <= 12 * (world - 1)                # halos only
+    prod = Config.default()
+    m2 = np.arange(mi_from_ym(1963, 1), mi_from_ym(2023, 11) + 1)     # 731 PFML months
+    cnt = np.asarray(s4_month_counts(m2, np.asarray(prod.hp_years), 8))
+    assert cnt.max() / cnt.mean() <= 1.15, cnt
 
 
 def test_collectives_gloo(tmp_path):
@@ -174,7 +185,7 @@ def test_bench_with_inputs_two_ranks_equals_one(tmp_path):
     a = torch.load(tmp_path / "w1.pt", weights_only=True)
     b = torch.load(tmp_path / "w2.pt", weights_only=True)
     assert torch.equal(a["val_months"], b["val_months"])
-    assert torch.allclose(a["obj"], b["obj"], rtol=1e-10, atol=1e-13)
+    assert torch.equal(a["obj"], b["obj"])                      # bitwise
 
 
 def _copy_inputs(src: str, dst: str) -> None:
@@ -186,7 +197,7 @@ def _copy_inputs(src: str, dst: str) -> None:
             shutil.copy(p, os.path.join(dst, n))
 
 
-@pytest.mark.parametrize("world,start", [(2, 1999), (3, 1999), (6, 2008)])
+@pytest.mark.parametrize("world,start", [(2, 1999), (3, 1999), (8, 1999), (6, 2008)])
 def test_pipeline_sharded_matches_single(world, start, small_data, tmp_path):
     """The main pipeline from pfml-input to pfml-best-hps on ``world`` gloo ranks - S4 built
     per rank on its hp-year blocks + validation halo (no denom all-gather), betas sharded,
@@ -211,12 +222,9 @@ def test_pipeline_sharded_matches_single(world, start, small_data, tmp_path):
         a = pd.read_csv(os.path.join(d1, name))
         b = pd.read_csv(os.path.join(d2, name))
         assert list(a.columns) == list(b.columns) and len(a) == len(b), name
-        for c in a.columns:
-            if a[c].dtype.kind in "fc":
-                assert np.allclose(a[c].to_numpy(), b[c].to_numpy(), rtol=1e-10, atol=1e-13,
-                                   equal_nan=True), (name, c)
-            else:
-                assert (a[c].astype(str) == b[c].astype(str)).all(), (name, c)
+        # bitwise: the CSV texts are identical (canonical window-sum order on every world)
+        with open(os.path.join(d1, name)) as fa, open(os.path.join(d2, name)) as fb:
+            assert fa.read() == fb.read(), name
     # per-rank done markers of the sharded stages
     for st in ("pfml-input", "pfml-search-coef"):
         for r in range(world):

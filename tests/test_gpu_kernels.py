@@ -227,7 +227,7 @@ def test_ridge_variants_agree(gpu, variant, monkeypatch):
     assert rel < 1e-8, rel
 
 
-@pytest.mark.parametrize("mode", ["single", "multi"])
+@pytest.mark.parametrize("mode", ["single", "multi", "fused"])
 def test_band_reduction_modes(gpu, mode, monkeypatch):
     """One-workgroup-per-cell and multi-workgroup band reductions both reproduce the LU-solve
     oracle, with cells of different n (65 .. 513) in one launch."""
@@ -244,6 +244,30 @@ def test_band_reduction_modes(gpu, mode, monkeypatch):
     out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
     rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
     assert rel < 1e-8, rel
+
+
+@pytest.mark.parametrize("n_obs", [700, 90])
+def test_band_fused_bitwise_single(gpu, n_obs, monkeypatch):
+    """The fused band reduction (one pass over the trailing matrix per panel, full symmetric
+    storage, upper tiles in the mirror's operation order) gives bitwise the betas of the
+    one-workgroup kernel on exactly symmetric window sums, for every n of the grid (and a
+    ragged n), full-rank and rank-deficient (n_obs = 90 < n: lambda = 0 repaired)."""
+    from pfml.ops.ridge import ridge_grid
+    P = 513
+    SD = _spd_stack(3, P, n_obs=n_obs, seed=71)
+    SD = 0.5 * (SD + SD.transpose(1, 2))           # exactly symmetric, like the window sums
+    Sr = _rand(3, P, seed=72)
+    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
+    src = np.array([0, 1, 2, 1, 0, 2, 2, 1])
+    nn = np.array([513, 513, 65, 257, 129, 100, 513, 17])
+    sc = np.full(len(src), 1.5e-3)
+    out = {}
+    for mode in ("single", "fused"):
+        monkeypatch.setenv("PFML_BAND_MODE", mode)
+        out[mode] = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
+    a, b = out["single"], out["fused"]
+    same = (a == b) | (torch.isnan(a) & torch.isnan(b))
+    assert bool(same.all()), float((a - b).abs().max())
 
 
 @pytest.mark.parametrize("hybrid", ["0", "3"])

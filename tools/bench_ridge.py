@@ -51,6 +51,8 @@ def timing(n=513, ncells=1):
     extra = {"solve_fwd_cyc": int(allb[ncells * 8]), "solve_bwd_cyc": int(allb[ncells * 8 + 1])}
     if os.environ.get("PFML_RIDGE_VARIANT", "band")[:1] in ("f", "t"):
         names = ["col_k", "householder", "sweep", "xy", "p_w_z", "trailing", "panel_end", "-"]
+    elif os.environ.get("PFML_BAND_MODE", "")[:1] == "f":
+        names = ["-", "strip", "qr", "U", "pass", "P_z_W", "final", "-"]
     else:
         names = ["load", "qr", "G_T", "U", "X", "P4_z_W", "trailing", "-"]
     tot = max(1, int(t.sum()))
@@ -64,8 +66,9 @@ if __name__ == "__main__":
         print(json.dumps(timing(), indent=1))
         sys.exit(0)
     out = {}
+    ncs = [int(x) for x in os.environ.get("PFML_BENCH_CELLS", "1,8,32,106,212").split(",")]
     for n in (513, 257):
-        for nc in (1, 8, 32, 106, 212):
+        for nc in ncs:
             out[f"n{n}_cells{nc}_ms"] = round(run(nc, n), 3)
             print(n, nc, out[f"n{n}_cells{nc}_ms"], flush=True)
     print(json.dumps(out))

@@ -1,0 +1,45 @@
+#!/bin/bash
+# round-3 GPU session script: MODE selects the steps (comma list), TAG the output dir.
+#   suite  : pytest -m gpu + smoke + headline bench
+#   peak   : fp64 MFMA / VALU roofline anchor (tools/micro/mfma_f64_peak)
+#   bench  : headline bench only
+#   ridge  : ridge-grid A/B (tools/bench_ridge.py) with PFML_BAND_MODE variants
+set -o pipefail
+TAG=${1:-r03}
+MODE=${2:-suite}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p $OUT
+cd $ROOT
+for step in ${MODE//,/ }; do
+  case $step in
+    peak)
+      timeout -k 10 120 ./tools/micro/mfma_f64_peak > $OUT/mfma_peak.json 2>&1
+      rc=$?; cat $OUT/mfma_peak.json; [ $rc -ne 0 ] && exit $rc ;;
+    suite)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+      rc=$?; tail -2 $OUT/pytest_gpu.log
+      if [ $rc -ne 0 ]; then grep -E "^E |FAILED" $OUT/pytest_gpu.log | head -20; exit $rc; fi
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+      rc=$?; tail -1 $OUT/smoke.log; [ $rc -ne 0 ] && exit $rc ;;
+    bench)
+      timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
+      rc=$?; grep '^{' $OUT/bench.json | cut -c1-400; if [ $rc -ne 0 ]; then tail -5 $OUT/bench.err; exit $rc; fi ;;
+    ridge)
+      # band-reduction A/B: per-phase cycles of one n = 513 cell and the grid vs #cells
+      for m in single fused; do
+        PFML_BAND_MODE=$m timeout -k 10 120 python tools/bench_ridge.py --timing > $OUT/ridge_timing_$m.json 2>&1
+        rc=$?; cat $OUT/ridge_timing_$m.json; [ $rc -ne 0 ] && exit $rc
+        PFML_BAND_MODE=$m PFML_BENCH_CELLS=1,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/ridge_cells_$m.log 2>&1
+        rc=$?; tail -1 $OUT/ridge_cells_$m.log; [ $rc -ne 0 ] && exit $rc
+      done ;;
+    fusedtest)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 120 --timeout-method thread -k "band_fused or band_reduction_modes" > $OUT/pytest_fused.log 2>&1
+      rc=$?; tail -3 $OUT/pytest_fused.log
+      if [ $rc -ne 0 ]; then grep -E "^E |FAILED" $OUT/pytest_fused.log | head -20; exit $rc; fi ;;
+    benchfused)
+      PFML_BAND_MODE=fused timeout -k 10 300 python bench.py --no-inputs > $OUT/bench_fused.json 2> $OUT/bench_fused.err
+      rc=$?; grep '^{' $OUT/bench_fused.json | cut -c1-300; if [ $rc -ne 0 ]; then tail -5 $OUT/bench_fused.err; exit $rc; fi ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
