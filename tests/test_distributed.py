@@ -229,3 +229,38 @@ def test_pipeline_sharded_matches_single(world, start, small_data, tmp_path):
     for st in ("pfml-input", "pfml-search-coef"):
         for r in range(world):
             assert os.path.exists(os.path.join(d2, "art", st, f"_DONE.rank{r}.json"))
+
+
+@pytest.mark.parametrize("fault", ["pfml-search-coef", "pfml-best-hps"])
+def test_pipeline_fault_injection_two_ranks(fault, small_data, tmp_path):
+    """Failure recovery on 2 ranks: a poisoned S5 coefficient cell on EVERY rank is
+    repaired locally before the utilities are gathered (no rank raises, none waits in the
+    gather), and a poisoned S9 w_start makes every rank rerun the chained recursion on the CPU
+    with its collectives staged for the backend.  The 2-rank outputs equal the 1-rank outputs
+    of the same fault bitwise, and the clean run's to 1e-10."""
+    import pandas as pd
+    from pfml.parallel import dist as pdist
+    from pfml.pipeline import Pipeline
+    dates = ["pf.dates.start_year=1999", "pf.dates.end_yr=2012", "pf.dates.split_years=3"]
+    base = small_data.override(dates + [f"run.fault_inject={fault}"])
+    clean = small_data.override(dates)
+    dirs = {k: str(tmp_path / k) for k in ("clean", "w1", "w2")}
+    for d in dirs.values():
+        _copy_inputs(small_data.run.data_dir, d)
+    for k, c in (("clean", clean), ("w1", base)):
+        pdist.set_env(None)
+        Pipeline(c.override([f"run.data_dir={dirs[k]}",
+                             f"run.artifact_dir={os.path.join(dirs[k], 'art')}"]),
+                 device="cpu").run(_PIPE_STAGES)
+    pdist.set_env(None)
+    _PIPE_CFG[:] = [base]
+    _run(2, "pipeline", dirs["w2"])
+    for name in ("validation.csv", "weights.csv", "pf.csv", "pf_summary.csv"):
+        with open(os.path.join(dirs["w1"], name)) as fa, open(os.path.join(dirs["w2"], name)) as fb:
+            assert fa.read() == fb.read(), name
+        a = pd.read_csv(os.path.join(dirs["clean"], name))
+        b = pd.read_csv(os.path.join(dirs["w2"], name))
+        for c in a.columns:
+            if a[c].dtype.kind in "fc":
+                assert np.allclose(a[c].to_numpy(), b[c].to_numpy(), rtol=1e-10, atol=1e-13,
+                                   equal_nan=True), (name, c)
