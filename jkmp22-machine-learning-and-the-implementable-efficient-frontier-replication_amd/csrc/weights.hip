@@ -96,3 +96,47 @@ extern "C" hipError_t pfml_weights_chain(const double* mt, int64_t ldm, int64_t 
                        sm, a, wa, grow, nmap, hit, sv, ws0, m, B, N, Wst, Wopt, ws_out);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------
+// Aim portfolios (PFML_aim_fun.py:138-163, K18): w_aim = s_t beta for every OOS month in ONE
+// launch instead of a per-month library GEMV from a Python loop.  Job j (one month): S_j =
+// rows [0, nrow_j) of a row-major [*, ld_j] signal block at sptr_j (the S4 signal views, no
+// copy), beta_j = coef row j (nk_j = p + 1 entries), out[off_j + r].  One wave per output row:
+// lane l sums k = l, l + 64, ... in order, then a fixed butterfly - the same order for a row
+// wherever its month sits in the launch (aims are bitwise independent of the sharding).
+namespace {
+struct AimJob {
+  const double* s;
+  int64_t ld;
+  int64_t off;
+  int nrow;
+  int nk;
+};
+
+__global__ __launch_bounds__(256) void aim_gemv_kernel(const AimJob* __restrict__ jobs,
+                                                       const double* __restrict__ coef,
+                                                       int64_t ldc, double* __restrict__ out) {
+  const AimJob jb = jobs[blockIdx.y];
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= jb.nrow) return;
+  const double* srow = jb.s + (int64_t)r * jb.ld;
+  const double* c = coef + (int64_t)blockIdx.y * ldc;
+  double acc = 0.0;
+  for (int k = lane; k < jb.nk; k += 64) acc = fma(srow[k], c[k], acc);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) out[jb.off + r] = acc;
+}
+}  // namespace
+
+extern "C" int pfml_aim_job_size() { return (int)sizeof(AimJob); }
+
+// jobs: device AimJob[njobs]; coef: [njobs, ldc]; rows per job <= max_rows.
+extern "C" hipError_t pfml_aim_gemv(const void* jobs, int njobs, int max_rows, const double* coef,
+                                    int64_t ldc, double* out, hipStream_t st) {
+  if (njobs <= 0 || max_rows <= 0) return hipSuccess;
+  hipLaunchKernelGGL(aim_gemv_kernel, dim3((max_rows + 3) / 4, njobs), dim3(256), 0, st,
+                     static_cast<const AimJob*>(jobs), coef, ldc, out);
+  return hipGetLastError();
+}

@@ -99,6 +99,10 @@ class PfmlInputs:
     signal_t: list                       # per g: per month [n_d, P] tensors (device)
     rff_w: np.ndarray                    # [G, k, P/2]
     ids: list                            # per month: ids
+    # m_tilde and a = lambda^-1/2 of the months asked for with ``keep_m`` (S9 reuses them:
+    # PFML_best_hps.py:185-190 recomputes exactly S4's m_t): {"months", "mt" [K, N, N],
+    # "a" [K, N], "n" [K]} in the padded universe width N of the plan
+    m_keep: dict | None = None
 
 
 def _rff_weights(cfg: Config, k: int) -> np.ndarray:
@@ -195,6 +199,14 @@ class S4Plan:
     sig_rows: list
     sig_ids: list
     R: int
+
+
+def universe_npad(chars: pd.DataFrame, months: np.ndarray) -> int:
+    """The padded universe width S4 uses for the month grid ``months`` (dates_m2): S9 pads its
+    m_t recompute to the same width, so a recomputed m_tilde is bitwise S4's."""
+    panel = Panel.from_chars(chars, [])
+    nmax = max((len(panel.valid_rows(int(d))) for d in months), default=1)
+    return _even(max(nmax, 2))
 
 
 def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.DataFrame,
@@ -357,8 +369,10 @@ def _vol_device(plan: S4Plan) -> torch.Tensor:
     return vol
 
 
-def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False) -> "PfmlInputs":
-    """The S4 arithmetic for every month of the plan (device or CPU fp64 oracle)."""
+def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
+             keep_m: np.ndarray | None = None) -> "PfmlInputs":
+    """The S4 arithmetic for every month of the plan (device or CPU fp64 oracle).  ``keep_m``:
+    months whose m_tilde / a are kept for S9 (``PfmlInputs.m_keep``)."""
     pf = cfg.pf_set
     gamma, mu = float(pf["gamma_rel"]), float(pf["mu"])
     lb = int(pf["lb_hor"])
@@ -384,6 +398,15 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False) -> "PfmlInpu
     sing = torch.zeros(max((len(b.months) for b in plan.batches), default=0),
                        dtype=torch.int32, device=dev)          # singular const flags (batch)
     nsing_t = torch.zeros((), dtype=torch.int64, device=dev)  # running count, on device
+    m_keep = None
+    if keep_m is not None:
+        km = np.asarray([m for m in plan.months if int(m) in set(int(x) for x in keep_m)],
+                        np.int64)
+        kpos = {int(m): i for i, m in enumerate(km)}
+        m_keep = {"months": km, "mt": torch.empty((len(km), N, N), dtype=torch.float64,
+                                                   device=dev),
+                  "a": torch.empty((len(km), N), dtype=torch.float64, device=dev),
+                  "n": np.zeros(len(km), np.int64)}
     b0 = 0
     for bt in plan.batches:
         B = len(bt.months)
@@ -407,6 +430,15 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False) -> "PfmlInpu
         # m = diag(a) m_tilde diag(1/a) (Lemma 1); a and 1/a are folded into the Horner GEMMs
         mt, a = la.m_tilde(Sigma, bt.lam, bt.w, bt.rf, mu, gamma, cfg.run.iterations,
                            mask=bt.mask)
+        if m_keep is not None:
+            sel = [(bi, kpos[int(d)]) for bi, d in enumerate(bt.months) if int(d) in kpos]
+            if sel:
+                src = torch.as_tensor([x[0] for x in sel], device=dev)
+                dst = torch.as_tensor([x[1] for x in sel], device=dev)
+                m_keep["mt"][dst] = mt[src]
+                m_keep["a"][dst] = a[src]
+                for bi, k in sel:
+                    m_keep["n"][k] = int(bt.ns[bi])
         # (24) Horner chain over [S_theta | I | R], one fused GEMM launch per step:
         #   T_theta = [S_theta | I] + diag(a) m_tilde diag(D_theta / a) T_{theta+1}
         # The lag-1 chain of omega_l1 (PFML_Input_Data.py:425-450: gtm_agg_l1, same m_t) is
@@ -501,17 +533,17 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False) -> "PfmlInpu
         log.warning(f"PFML inputs: {nsing} month(s) with a numerically singular sum of agg")
     reals = PfmlReals(months=plan.months, r_tilde=r_out, denom=d_out, risk=risk_out, tc=tc_out)
     return PfmlInputs(reals=reals, months=plan.months, signal_rows=plan.sig_rows,
-                      signal_t=signal_t, rff_w=plan.W, ids=plan.sig_ids)
+                      signal_t=signal_t, rff_w=plan.W, ids=plan.sig_ids, m_keep=m_keep)
 
 
 def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.DataFrame,
                  risk_free: pd.DataFrame, device, months: np.ndarray | None = None,
                  keep_risk_tc: bool = False, batch: int | None = None,
-                 plan: S4Plan | None = None) -> PfmlInputs:
+                 plan: S4Plan | None = None, keep_m: np.ndarray | None = None) -> PfmlInputs:
     """S4 for ``months`` (default dates_m2): ``make_s4_plan`` + ``run_plan``."""
     if plan is None:
         plan = make_s4_plan(cfg, chars, barra, wealth, risk_free, device, months, batch)
-    return run_plan(plan, cfg, keep_risk_tc)
+    return run_plan(plan, cfg, keep_risk_tc, keep_m=keep_m)
 
 
 def to_reference_order(x: torch.Tensor, p_max: int, dims: tuple = (-1,)) -> torch.Tensor:

@@ -31,6 +31,10 @@ _P, _I, _L = nat.C.c_void_p, nat.C.c_int, nat.C.c_int64
 nat.register_hip("pfml_weights_chain", [_P, _L, _L, _P, _P, _P, _P, _P, _L, _P, _I, _I, _P, _P,
                                         _P, _P])
 nat.register_hip("pfml_weights_chain_max_n", [])
+nat.register_hip("pfml_aim_gemv", [_P, _I, _I, _P, _L, _P, _P])
+nat.register_hip("pfml_aim_job_size", [])
+AIM_JOB = np.dtype([("s", "<u8"), ("ld", "<i8"), ("off", "<i8"), ("nrow", "<i4"),
+                    ("nk", "<i4")])
 
 log = get_logger("portfolio")
 
@@ -48,16 +52,17 @@ def aim_portfolios(cfg: Config, validation: pd.DataFrame, beta_years: np.ndarray
                    signal_ids: list, oos_months: np.ndarray) -> dict:
     """{g: {d: {'aim_pf': DataFrame(id, eom, w_aim), 'coef': ndarray}}} (internal order).
 
-    w_aim = s_t beta (K18) for every month on the device, one host copy at the end."""
+    w_aim = s_t beta (K18) for every (g, month): on the device ONE launch over all of them
+    (csrc/weights.hip aim_gemv_kernel reads the S4 signal views in place; coefficients
+    gathered by one index op), one host copy at the end; on the CPU one product per month."""
     G = beta.shape[0]
     p_vec = cfg.p_vec
-    out = {}
     mpos = {int(m): i for i, m in enumerate(signal_months)}
     byear = np.asarray(beta_years)
+    meta = []                                     # (g, d, i, p, l, year index, p index)
     for g in range(G):
         opt = _opt_hps(validation, g)
         sel = {int(y): (int(p), int(l)) for y, p, l in zip(opt["hp_end"], opt["p"], opt["l"])}
-        ws, coefs, meta = [], [], []
         for d in oos_months:
             oos_year = int(month_end(int(d) + 1).year[0])
             if oos_year - 1 not in sel:
@@ -66,23 +71,44 @@ def aim_portfolios(cfg: Config, validation: pd.DataFrame, beta_years: np.ndarray
             hit = np.nonzero(byear == oos_year)[0]
             if len(hit) == 0:
                 raise KeyError(f"coefficients of hp year {oos_year} are not on this rank")
-            coef = beta[g, int(hit[0]), p_vec.index(p), l, : p + 1]
-            i = mpos[int(d)]
-            s = signal_t[g][i][:, : p + 1]
-            ws.append(s @ coef.to(s.device))
-            coefs.append(coef)
-            meta.append((int(d), i, p, l))
-        if ws:
-            w_all = torch.cat(ws).cpu().numpy()
-            c_all = [c.cpu().numpy() for c in coefs]
-        res, o = {}, 0
-        for k, (d, i, p, l) in enumerate(meta):
-            n = len(signal_ids[i])
-            res[d] = {"aim_pf": pd.DataFrame({"id": signal_ids[i], "eom": month_end(d)[0],
-                                              "w_aim": w_all[o:o + n]}),
-                      "coef": c_all[k], "p": p, "l": l}
-            o += n
-        out[g] = res
+            meta.append((g, int(d), mpos[int(d)], p, l, int(hit[0]), p_vec.index(p)))
+    J = len(meta)
+    out: dict = {g: {} for g in range(G)}
+    if J == 0:
+        return out
+    gi = torch.as_tensor([m[0] for m in meta], device=beta.device)
+    yi = torch.as_tensor([m[5] for m in meta], device=beta.device)
+    pi = torch.as_tensor([m[6] for m in meta], device=beta.device)
+    li = torch.as_tensor([m[4] for m in meta], device=beta.device)
+    coefs = beta[gi, yi, pi, li].contiguous()          # [J, P], zero beyond p + 1
+    sig = [signal_t[m[0]][m[2]] for m in meta]
+    nrows = np.asarray([int(x.shape[0]) for x in sig], np.int64)
+    offs = np.concatenate([[0], np.cumsum(nrows)[:-1]])
+    if nat.is_device(beta) and all(x.is_cuda and x.stride(-1) == 1 for x in sig):
+        from ..ops.ridge import upload
+        if nat.hip_lib().pfml_aim_job_size() != AIM_JOB.itemsize:
+            raise RuntimeError("AimJob layout mismatch between python and libpfml_hip")
+        jobs = np.zeros(J, AIM_JOB)
+        jobs["s"] = [x.data_ptr() for x in sig]
+        jobs["ld"] = [x.stride(0) for x in sig]
+        jobs["off"] = offs
+        jobs["nrow"] = nrows
+        jobs["nk"] = [m[3] + 1 for m in meta]
+        (dj,) = upload([jobs], beta.device)
+        w = torch.empty(int(nrows.sum()), dtype=torch.float64, device=beta.device)
+        nat.check(nat.hip_lib().pfml_aim_gemv(dj.data_ptr(), J, int(nrows.max()),
+                                              coefs.data_ptr(), coefs.shape[1], w.data_ptr(),
+                                              nat.stream_of(beta)), "pfml_aim_gemv")
+        w_all = w.cpu().numpy()
+    else:
+        w_all = torch.cat([s_[:, : m[3] + 1] @ coefs[k, : m[3] + 1].to(s_.device)
+                           for k, (s_, m) in enumerate(zip(sig, meta))]).cpu().numpy()
+    c_all = coefs.cpu().numpy()
+    for k, (g, d, i, p, l, _, _) in enumerate(meta):
+        o, n = int(offs[k]), int(nrows[k])
+        out[g][d] = {"aim_pf": pd.DataFrame({"id": signal_ids[i], "eom": month_end(d)[0],
+                                             "w_aim": w_all[o:o + n]}),
+                     "coef": c_all[k, : p + 1].copy(), "p": p, "l": l}
     return out
 
 
@@ -227,15 +253,20 @@ def _weights_plan(cfg: Config, chars: pd.DataFrame, wealth: pd.DataFrame, aims: 
 
 def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.DataFrame,
                  risk_free: pd.DataFrame, aims: pd.DataFrame, oos_months: np.ndarray,
-                 device) -> pd.DataFrame | None:
+                 device, mine_months: np.ndarray | None = None,
+                 m_cache: dict | None = None, n_pad: int = 0) -> pd.DataFrame | None:
     """Weight recursion (17) (PFML_best_hps.py:168-218) -> weights.csv frame (rank 0).
 
-    The OOS months are split contiguously over ranks.  Each rank computes m_t of ITS months as
-    batched device m_func (K19; m = diag(a) m_tilde diag(1/a), never formed), then runs its
-    part of the sequential chain on the device - w_opt = w_aim + m (w_start - w_aim), the
-    drift w_start(t+1) = w_opt (1 + tr_ld1) / (1 + mu_ld1) gathered through the id map, new
-    names 0 - with no host round trip per month.  The chain crosses ranks as ONE N-vector
-    hand-off (point-to-point, rank r -> r+1); the per-row weights are gathered at the end."""
+    Each rank takes the OOS months it owns (``mine_months``: the S4 month ownership of
+    search.owned_month_rows - contiguous in time, ranks in time order; default a contiguous
+    split) and needs m_t of them: from ``m_cache`` (S4's m_tilde and a of exactly these
+    months, PfmlInputs.m_keep - the reference recomputes the same m_t here,
+    PFML_best_hps.py:185-190) or else as batched device m_func (K19; m = diag(a) m_tilde
+    diag(1/a), never formed).  It then runs its part of the sequential chain on the device -
+    w_opt = w_aim + m (w_start - w_aim), the drift w_start(t+1) = w_opt (1 + tr_ld1) /
+    (1 + mu_ld1) gathered through the id map, new names 0 - with no host round trip per month.
+    The chain crosses ranks as ONE N-vector hand-off (point-to-point, rank r -> r+1); the
+    per-row weights are gathered at the end."""
     from ..ops.ridge import _HostClock
     from ..parallel import collectives as coll
     from ..parallel.dist import env as dist_env
@@ -250,11 +281,16 @@ def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
     data, months, starts, stops = pl["data"], pl["months"], pl["starts"], pl["stops"]
     B = len(months)
     ns = stops - starts
-    N = int(ns.max()) if B else 1
+    # n_pad: S4's padded universe width (pfml_inputs.universe_npad) - a recomputed m_t then
+    # has S4's shapes and is bitwise the cached one
+    N = max(int(ns.max()) if B else 1, int(n_pad))
     K = barra.X.shape[1]
     wvals = _month_values(wealth, "wealth", months)
     rfvals = _month_values(risk_free, "rf", months)
-    mine = np.asarray(list(coll.contiguous_split(B, env.world_size, env.rank)), np.int64)
+    if mine_months is not None:
+        mine = np.nonzero(np.isin(months, np.asarray(mine_months, np.int64)))[0].astype(np.int64)
+    else:
+        mine = np.asarray(list(coll.contiguous_split(B, env.world_size, env.rank)), np.int64)
     f64 = dict(dtype=torch.float64, device=dev)
     lam_col = data["lambda"].to_numpy(np.float64) if tc_on else None
     tr1 = data["tr_ld1"].to_numpy(np.float64)
@@ -271,15 +307,31 @@ def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         col = np.arange(int(n_t.sum())) - np.repeat(np.cumsum(n_t) - n_t, n_t)
         return starts[tt][bi] + col, bi, col
 
-    # ---- batched m_t of this rank's months (K19) --------------------------------------
+    # ---- m_t of this rank's months: S4's (cache) or batched m_func (K19) --------------
     Bm = len(mine)
-    mt_all = torch.zeros((Bm, N, N), **f64)
-    a_all = torch.ones((Bm, N), **f64)
-    chunk = int(cfg.run.month_batch)
-    if chunk <= 0:
-        from .pfml_inputs import auto_month_batch
-        chunk = auto_month_batch(N, 0, dev)
-    for c0 in range(0, Bm, chunk):
+    kpos = None
+    if m_cache is not None and Bm:
+        cm_ = np.asarray(m_cache["months"], np.int64)
+        p_ = np.searchsorted(cm_, months[mine])
+        ok = (len(cm_) > 0 and bool(np.all(p_ < len(cm_)))
+              and bool(np.all(cm_[np.minimum(p_, len(cm_) - 1)] == months[mine]))
+              and m_cache["mt"].shape[-1] >= N and m_cache["mt"].device == dev)
+        if ok and np.array_equal(np.asarray(m_cache["n"])[p_], ns[mine]):
+            kpos = torch.as_tensor(p_, device=dev)
+    if kpos is not None:
+        mt_all = m_cache["mt"].index_select(0, kpos)[:, :N, :N]   # ld = the S4 width
+        a_all = m_cache["a"].index_select(0, kpos)[:, :N].contiguous()
+        chunk, Bm_run = 1, 0
+        log.info(f"S9: m_t of {Bm} month(s) reused from S4")
+    else:
+        mt_all = torch.zeros((Bm, N, N), **f64)
+        a_all = torch.ones((Bm, N), **f64)
+        chunk = int(cfg.run.month_batch)
+        if chunk <= 0:
+            from .pfml_inputs import auto_month_batch
+            chunk = auto_month_batch(N, 0, dev)
+        Bm_run = Bm
+    for c0 in range(0, Bm_run, chunk):
         cm = mine[c0:c0 + chunk]
         Bc = len(cm)
         rows, bi, col = rows_of(cm)
@@ -294,8 +346,9 @@ def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         lam[bi, col] = lam_col[rows] if tc_on else 1e-16
         Xd, ivd = torch.as_tensor(Xl, **f64), torch.as_tensor(iv, **f64)
         Sig = torch.empty((Bc, N, N), **f64)
-        gemm_fused(torch.bmm(Xd, torch.as_tensor(Fb, **f64)), Xd, Sig, trans_b=True,
-                   diag_col0=0, diag_vec=ivd)
+        XF = torch.empty((Bc, N, K), **f64)
+        gemm_fused(Xd, torch.as_tensor(Fb, **f64), XF)          # in-house GEMM, no rocBLAS
+        gemm_fused(XF, Xd, Sig, trans_b=True, diag_col0=0, diag_vec=ivd)
         mt, a = la.m_tilde(Sig, torch.as_tensor(lam, **f64), torch.as_tensor(wvals[cm], **f64),
                            torch.as_tensor(rfvals[cm], **f64), mu, gamma, cfg.run.iterations,
                            mask=torch.as_tensor(mask, **f64))
@@ -323,12 +376,13 @@ def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         hit[has_next[b1], c1] = q >= 0
     nmap_t, hit_t = torch.as_tensor(nmap, device=dev), torch.as_tensor(hit, **f64)
     ws0 = torch.zeros(N, **f64)
-    if Bm and mine[0] == 0:
+    if env.is_dist:
+        ws0 = coll.recv_prev(ws0)                 # rank 0: zeros; a rank owning no month
+    if Bm and mine[0] == 0:                       # passes the vector on unchanged
         g0 = np.arange(starts[0], stops[0])
         me = data["me"].to_numpy(np.float64)[g0]
+        ws0 = torch.zeros(N, **f64)
         ws0[: len(g0)] = torch.as_tensor(me / me.sum(), **f64)    # value-weighted start
-    elif env.is_dist:
-        ws0 = coll.recv_prev(ws0)
     Wst = torch.zeros((Bm, N), **f64)
     Wopt = torch.zeros((Bm, N), **f64)
     ws = ws0
@@ -337,7 +391,8 @@ def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         ws = torch.empty(N, **f64)
         if Bm:
             nat.check(nat.hip_lib().pfml_weights_chain(
-                mt_all.data_ptr(), N, N * N, a_all.data_ptr(), wa.data_ptr(),
+                mt_all.data_ptr(), mt_all.stride(1), mt_all.stride(0), a_all.data_ptr(),
+                wa.data_ptr(),
                 grow.contiguous().data_ptr(), nmap_t.data_ptr(), hit_t.data_ptr(), N,
                 ws0.contiguous().data_ptr(), Bm, N, Wst.data_ptr(), Wopt.data_ptr(),
                 ws.data_ptr(), nat.stream_of(mt_all)), "pfml_weights_chain")

@@ -158,6 +158,27 @@ def local_month_rows(all_months: np.ndarray, years: np.ndarray, world: int,
     return np.unique(np.concatenate(rows)).astype(np.int64)
 
 
+def owned_month_rows(all_months: np.ndarray, years: np.ndarray, world: int,
+                     rank: int) -> np.ndarray:
+    """Global rows OWNED by ``rank``: its burn-in pieces and hp-year blocks, and (owner of the
+    last hp year) the months after the last block - every month has exactly one owner, and in
+    time order
+    the owners never decrease, so a time-sequential chain (the S9 recursion) can run over
+    the owned months rank after rank with one hand-off each."""
+    all_months = np.asarray(all_months, np.int64)
+    plan = make_plan(all_months, np.asarray(years))
+    lay = win_layout(plan, len(years), world)
+    rows = [np.arange(a, b) for k, (a, b) in enumerate(lay.burn)
+            if chunk_owner(k, lay.C, world) == rank]
+    for y in rank_years(len(years), world, rank):
+        rows.append(np.arange(int(plan.seg_start[y]), int(plan.seg_stop[y])))
+    # the months after the last block go to the owner of the last year (its halo holds them)
+    if len(years) and len(rank_years(len(years), world, rank)) and \
+            rank_years(len(years), world, rank)[-1] == len(years) - 1:
+        rows.append(np.arange(int(plan.seg_stop[-1]), len(all_months)))
+    return np.unique(np.concatenate(rows)).astype(np.int64) if rows else np.zeros(0, np.int64)
+
+
 def s4_month_counts(all_months: np.ndarray, years: np.ndarray, world: int) -> list:
     """S4 months per rank (load balance report)."""
     return [len(local_month_rows(all_months, years, world, r)) for r in range(world)]

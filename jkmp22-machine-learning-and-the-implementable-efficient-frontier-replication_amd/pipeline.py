@@ -173,9 +173,14 @@ class Pipeline:
             log.info(f"[pfml-input] rank {self.env.rank}: shard up to date (resume)")
             self._ensure_reals()
             return
+        # S9 reuses S4's m_tilde of the OOS months this rank owns (PFML_best_hps.py:185-190
+        # recomputes exactly these m_t)
+        own_oos = self._owned_oos()
+        keep = None if own_oos is None else np.intersect1d(own_oos, months)
         res = pin.build_inputs(self.cfg, st["chars"], st["barra"], st["wealth"],
-                               st["risk_free"], self.device, months=months)
+                               st["risk_free"], self.device, months=months, keep_m=keep)
         self._guard_inputs(res, months)
+        st["m_oos"] = res.m_keep
         R = res.reals
         R = search.PfmlReals(months=months, r_tilde=R.r_tilde, denom=R.denom, all_months=m2)
         st["reals"] = R
@@ -192,6 +197,21 @@ class Pipeline:
                 payload[f"sig{g}"] = (torch.cat(res.signal_t[g]) if res.signal_t[g] else
                                       torch.zeros((0, R.P), dtype=torch.float64))
             self.store.save_tensors("pfml-input", f"reals.rank{self.env.rank}", payload)
+
+    def _owned_oos(self) -> np.ndarray | None:
+        """OOS months this rank owns (search.owned_month_rows): S9's shard of the chain.  None
+        (S9 falls back to a contiguous split and recomputes m_t) if the owners of the OOS
+        months are not non-decreasing in time - the chain runs rank after rank."""
+        g = self.state["grids"]
+        m2, oos = g["m2"], g["oos"]
+        W = self.env.world_size
+        owner = np.full(len(oos), -1, np.int64)
+        for r in range(W):
+            own = m2[search.owned_month_rows(m2, self.cfg.hp_years, W, r)]
+            owner[np.isin(oos, own)] = r
+        if (owner < 0).any() or (np.diff(owner) < 0).any():
+            return None
+        return oos[owner == self.env.rank]
 
     def _guard_inputs(self, res, months) -> None:
         """Failure detection: months whose summands are not finite are recomputed
@@ -362,8 +382,11 @@ class Pipeline:
             self._pfml_hps()
         best, chosen, aims = portfolio.best_hps(st["hps"], oos)
         # m_t sharded over ranks, the recursion chained across them (rank 0 gets the frame)
+        npad = pin.universe_npad(st["chars"], st["grids"]["m2"])
         w = portfolio.pfml_weights(self.cfg, st["chars"], st["barra"], st["wealth"],
-                                   st["risk_free"], aims, oos, self.device)
+                                   st["risk_free"], aims, oos, self.device,
+                                   mine_months=self._owned_oos(), m_cache=st.get("m_oos"),
+                                   n_pad=npad)
         # failure detection: the chained w_start is finite by construction (value
         # weights, drift, 0 for new names); a non-finite one means a fault in the device chain
         # -> the recursion is recomputed on the CPU (a collective decision: every rank reruns)
@@ -379,7 +402,8 @@ class Pipeline:
                         "the CPU")
             COUNTERS.add("pfml_best_hps.recomputed", 1)
             w = portfolio.pfml_weights(self.cfg, st["chars"], st["barra"], st["wealth"],
-                                       st["risk_free"], aims, oos, torch.device("cpu"))
+                                       st["risk_free"], aims, oos, torch.device("cpu"),
+                                       mine_months=self._owned_oos(), n_pad=npad)
             if self.env.is_main and not np.isfinite(w["w_start"].to_numpy()).all():
                 raise FloatingPointError("w_start stays non-finite on the CPU recursion")
         if not self.env.is_main:
