@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
 """Freeze S4-S9 golden outputs by running the REFERENCE's own stage scripts.
 
-Dev-time only (needs /root/reference).  A small synthetic dataset (tests' 50-stock panel,
-taken through this engine's L0-L3 stages) is written in the reference's file layout
-(``<path>/Data/JKP_US_SP500.db:Factors_processed``, ``wealth_processed.csv``,
-``FF_RF_monthly.csv``, ``rff_w.csv`` and ``Barra_Cov.pkl`` in the reference's dict-of-DataFrames
-format), then the reference scripts PFML_Input_Data.py, PFML_Search_Coef.py,
-PFML_hp_reals.py, PFML_aim_fun.py, PFML_hps.py and PFML_best_hps.py are exec'd verbatim in
-one shared namespace, exactly as Main.py does (Main.py:16-22), with three harness-only edits:
+OFFLINE, MANUAL, DEV-TIME TOOL (needs /root/reference; exec()s the untrusted reference
+scripts in-process - never run by a test, by build() or on the GPU box).  The tests' 50-stock
+synthetic raw files go through this engine's L0 (ETL + S&P 500 subset, the reference's file
+layout), then ALL EIGHT reference stage scripts of Main.py - Prepare_Data.py, Estimate
+Covariance Matrix.py, PFML_Input_Data.py, PFML_Search_Coef.py, PFML_hp_reals.py,
+PFML_aim_fun.py, PFML_hps.py and PFML_best_hps.py - are exec'd verbatim in one shared
+namespace, exactly as Main.py does (Main.py:16-22): the S4-S9 golden is fed by the
+reference's OWN L2/L3 outputs (Factors_processed, wealth_processed.csv, Barra_Cov.pkl written
+by the reference in this run).  Harness-only edits: those of tools/make_golden_l2l3.py for the
+two L2/L3 scripts (small-panel settings, Factor Details CSV twin, numba stub), and for S4-S9:
 
 * ``get_settings`` is wrapped to apply the small-config overrides (p_vec = [8, 16], hp years
   1999-2012, 3 split years, test_end 2012-12-31) that the engine's test runs with;
@@ -18,11 +21,13 @@ one shared namespace, exactly as Main.py does (Main.py:16-22), with three harnes
   and statsmodels are not installed here; statsmodels' ECDF is only used by the reference's
   dead ``ecdf_transform``, so a stub module satisfies the import).
 
-The reference's outputs (pickles written by the reference code in this run, CSVs) are reduced
-to small fixtures under tests/golden/ref_pipeline/: S4 summands of a few months, ridge
-coefficients of a few (year, p, lambda) cells, a fixed sample of validation.csv rows plus every
-December rank-1 row, and the full weights.csv / pf.csv / pf_summary.csv.  A checksum of the
-engine-produced inputs is stored so the test detects an input drift.
+The reference's outputs are reduced to small fixtures under tests/golden/ref_pipeline/: S4
+summands of a few months, ridge coefficients of a few (year, p, lambda) cells, a fixed sample
+of validation.csv rows plus every December rank-1 row, and the full weights.csv / pf.csv /
+pf_summary.csv - all taken from the scripts' in-memory objects or their CSVs (nothing the
+reference writes is unpickled here).  A fingerprint of the reference's L2/L3 outputs is
+stored; the test checks the engine's own L2/L3 outputs against it (rtol 1e-9), so the chain
+L2 -> S9 is anchored to the reference end to end.
 
     python tools/make_golden_pipeline.py [/root/reference]
 """
@@ -44,6 +49,7 @@ OUT = os.path.join(ROOT, "tests", "golden", "ref_pipeline")
 
 OVERRIDES = ["pf_ml.p_vec=[8,16]", "pf.dates.start_year=1999", "pf.dates.end_yr=2012",
              "pf.dates.split_years=3"]
+L2L3 = ["Prepare_Data.py", "Estimate Covariance Matrix.py"]
 SCRIPTS = ["PFML_Input_Data.py", "PFML_Search_Coef.py", "PFML_hp_reals.py", "PFML_aim_fun.py",
            "PFML_hps.py", "PFML_best_hps.py"]
 
@@ -81,6 +87,31 @@ def input_fingerprint(data_dir: str) -> dict:
     out = {}
     for name, a in (("chars", chars.select_dtypes("number").to_numpy(np.float64)), ("X", b.X),
                     ("F", b.F), ("ivol", b.ivol), ("ids", b.ids.astype(np.float64))):
+        a = np.asarray(a, np.float64).ravel()
+        nan = np.isnan(a)
+        v = a[~nan]
+        w = np.random.default_rng(5).uniform(0.5, 1.5, v.size)
+        out[name] = [float(a.size), float(nan.sum()), float(v.sum()), float(np.abs(v).sum()),
+                     float((v * v).sum()), float(v @ w)]
+    return out
+
+
+def reference_fingerprint(data_dir: str, barra: dict) -> dict:
+    """input_fingerprint of the REFERENCE's L2/L3 outputs: Factors_processed read back from
+    its SQLite table with the engine's reader, the Barra arrays from the reference's in-memory
+    ``barra_cov`` (months ascending, ids ascending within a month - the engine's layout)."""
+    from pfml.config import get_features
+    from pfml.data import io
+    chars = io.read_processed_chars(data_dir, get_features())
+    dates = sorted(barra.keys())
+    arrs = {"chars": chars.select_dtypes("number").to_numpy(np.float64),
+            "X": np.concatenate([barra[d]["fct_load"].to_numpy(np.float64) for d in dates]),
+            "F": np.stack([barra[d]["fct_cov"].to_numpy(np.float64) for d in dates]),
+            "ivol": np.concatenate([barra[d]["ivol_vec"].to_numpy(np.float64) for d in dates]),
+            "ids": np.concatenate([np.asarray(barra[d]["fct_load"].index, np.float64)
+                                   for d in dates])}
+    out = {}
+    for name, a in arrs.items():
         a = np.asarray(a, np.float64).ravel()
         nan = np.isnan(a)
         v = a[~nan]
@@ -143,6 +174,11 @@ def patched_settings(gf, cfg) -> None:
 
     def get_settings():
         s, p = orig()
+        for sec, keys in (("screens", ("start", "end")),):
+            for k in keys:
+                s[sec][k] = pd.Timestamp(cfg.settings[sec][k])
+        for k in ("obs", "hl_cor", "hl_var"):
+            s["cov_set"][k] = cfg.settings["cov_set"][k]
         s["pf_ml"]["p_vec"] = list(cfg.p_vec)
         s["pf"]["dates"]["start_year"] = int(cfg.settings["pf"]["dates"]["start_year"])
         s["pf"]["dates"]["end_yr"] = int(cfg.settings["pf"]["dates"]["end_yr"])
@@ -155,6 +191,8 @@ def patched_settings(gf, cfg) -> None:
 
 def script_source(name: str) -> str:
     src = open(os.path.join(REF, name), encoding="utf-8").read()
+    if name in L2L3:
+        return src
     if name == "PFML_aim_fun.py":
         line = "settings['split']['test_end'] = pd.to_datetime('2023-12-31')"
         assert line in src
@@ -170,12 +208,14 @@ def script_source(name: str) -> str:
 
 def main():
     from pfml.config import get_features
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from make_golden_l2l3 import install_stubs as l2l3_stubs, raw_inputs
     tmp = tempfile.mkdtemp(prefix="pfml_ref_")
     data = os.path.join(tmp, "Data")
     os.makedirs(data)
-    cfg = engine_inputs(data)
+    cfg = raw_inputs(data).override(OVERRIDES)          # synthetic raw files + engine L0
     small_rff_w(data, len(get_features()), cfg.p_max // 2)
-    write_reference_barra(data, os.path.join(data, "Barra_Cov.pkl"))
+    l2l3_stubs()
     install_stubs()
     sys.path.insert(0, REF)
     cwd = os.getcwd()
@@ -183,14 +223,22 @@ def main():
     import General_functions as gf
     patched_settings(gf, cfg)
     ns = {"__name__": "__main__", "path": tmp + "/"}
-    for s in SCRIPTS:
+    captured = {}                    # what the scripts pickle.dump, by file name (in memory)
+    dump = pickle.dump
+
+    def capture_dump(obj, f, *a, **k):
+        captured[os.path.basename(getattr(f, "name", ""))] = obj
+        return dump(obj, f, *a, **k)
+
+    pickle.dump = capture_dump
+    for s in L2L3 + SCRIPTS:                             # Main.py's eight scripts, in order
         print(f"=== reference {s}", flush=True)
         exec(compile(script_source(s), os.path.join(REF, s), "exec"), ns)
     os.chdir(cwd)
 
     os.makedirs(OUT, exist_ok=True)
-    with open(os.path.join(data, "pfml_input_0.pkl"), "rb") as f:      # written above
-        pin = pickle.load(f)
+    pickle.dump = dump
+    pin = captured["pfml_input_0.pkl"]                   # in memory: nothing is unpickled
     reals = pin[list(pin.keys())[0]]["reals"]
     dates = sorted(reals.keys())
     pick = [dates[0], dates[len(dates) // 2], dates[-1]]
@@ -200,8 +248,7 @@ def main():
         months=np.array([str(pd.Timestamp(d).date()) for d in pick]), feat=np.array(feat),
         **{f"{k}_{i}": np.asarray(reals[d][k], dtype=np.float64)
            for i, d in enumerate(pick) for k in ("r_tilde", "denom", "risk", "tc")})
-    with open(os.path.join(data, "coef_dict_0.pkl"), "rb") as f:
-        cd = pickle.load(f)
+    cd = captured["coef_dict_0.pkl"]
     cd = cd[list(cd.keys())[0]]
     years = sorted(cd.keys())
     cells = {}
@@ -221,8 +268,8 @@ def main():
     for n in ("weights.csv", "pf.csv", "pf_summary.csv"):
         shutil.copy(os.path.join(data, n), os.path.join(OUT, n))
     meta = {"overrides": OVERRIDES, "validation_rows": int(len(val)),
-            "input_fingerprint": input_fingerprint(data), "rff_w_seed": 11,
-            "reference_scripts": SCRIPTS}
+            "input_fingerprint": reference_fingerprint(data, captured["Barra_Cov.pkl"]),
+            "rff_w_seed": 11, "reference_scripts": L2L3 + SCRIPTS}
     with open(os.path.join(OUT, "meta.json"), "w") as f:
         json.dump(meta, f, indent=1)
     print("golden written to", OUT, meta)
