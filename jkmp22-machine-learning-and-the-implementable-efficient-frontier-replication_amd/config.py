@@ -161,6 +161,14 @@ class RunOptions:
     # compat_mode=True reproduces the reference quirks: Q1 (g ignored when the
     # RFF weight matrix is supplied), Q2 (validation rows accumulate across g), Q3
     # (pf.csv eom_ret == eom).  False gives the corrected behaviour.
+    # Intentional deviation in both modes (Q19): a Barra factor with zero variance over the
+    # EWMA window (no stock exposed to it, e.g. an empty FF12 industry) gets correlation 0,
+    # where the reference's weighted_cor_wt (General_functions.py:827, cov / outer(sd, sd))
+    # gives 0/0 = NaN when the variance is exactly 0 - which would make F, and through
+    # X F X' every Sigma_t of that month, NaN.  (In practice the reference's pinv fallback
+    # leaves ~1e-16 coefficient noise there, so its variance is ~1e-32, not 0, and its F
+    # entries ~1e-32: the engine's exact 0 differs from that by far below every tolerance.)
+    # Outputs differ only where the reference's would be NaN.
     compat_mode: bool = True
     # fp64 (production) | fp32 | bf16 | fp8: the S4 covariance (K1), RFF (K13) and risk GEMMs
     # in reduced precision (fp32 sgemm, or bf16 / fp8 MFMA with fp32 accumulation); solves

@@ -607,7 +607,10 @@ __device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n,
   if (t < BB * BB) Tglob[t] = Ts[t / BB][t % BB];
 }
 
-template <bool qr_fast>
+// DBG (phase-timing experiments only, PFML_BAND_DBG with --timing; results are garbage):
+// 1 no A stores in the trailing update, 2 no trailing MFMAs, 4 no trailing A loads,
+// 8 no LDS transpose (lower stores straight from the accumulators, no mirror)
+template <bool qr_fast, int DBG = 0>
 __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
     const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
     const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work,
@@ -631,26 +634,34 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
 
   const RidgeCellDesc cd = cells[blockIdx.x];
   const int n = cd.n;
-  const int t = threadIdx.x, lane = t & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int c16 = lane & 15, g4 = lane >> 4;
-  const int cq = t & 15, rg = t >> 4;            // (row group of 32, column) thread map
+  // leading dimension padded to 16 doubles (128 B): every tile row of the trailing update and
+  // of X = A22 U is one whole cache line (lda = n split most of them over two)
+  const int lda = band_npad(n);
+  const int t_ = threadIdx.x, lane_ = t_ & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t_ >> 6);
   BandWork bw(work + cd.work, n, L);
   double* A = bw.A;
   const double* S = SD + cd.src;
   const double sc = cd.scale;
   for (int i = wid; i < n; i += NWR) {
     const double* srow = S + (int64_t)i * ldS;
-    double* arow = A + (int64_t)i * n;
-    for (int j = lane; j < n; j += 64) arow[j] = srow[j] * sc;
+    double* arow = A + (int64_t)i * lda;
+    for (int j = lane_; j < n; j += 64) arow[j] = srow[j] * sc;
   }
-  for (int i = t; i < n; i += NTR) zs[i] = Sr[cd.rsrc + i] * sc;
+  for (int i = t_; i < n; i += NTR) zs[i] = Sr[cd.rsrc + i] * sc;
   __syncthreads();
 
   if (tim != nullptr && threadIdx.x == 0) tlast = (long long)__builtin_amdgcn_s_memtime();
   for (int k0 = 0; k0 + BB < n; k0 += BB) {
     const int r0 = k0 + BB, m = n - r0, p = k0 / BB;
-    band_panel_factor(A, n, k0, r0, m, Vs, Ws, &red[0][0], Ts, taus, bw.T + (int64_t)p * BB * BB,
+    // lane indices laundered per panel (as in band_fused_kernel): otherwise every
+    // lane-dependent offset of the phases is hoisted out of the panel loop and kept live
+    // across the register-hungry QR
+    int t = t_, lane = lane_;
+    asm volatile("" : "+v"(t), "+v"(lane));
+    const int c16 = lane & 15, g4 = lane >> 4;
+    const int cq = t & 15, rg = t >> 4;          // (row group of 32, column) thread map
+    band_panel_factor(A, lda, k0, r0, m, Vs, Ws, &red[0][0], Ts, taus, bw.T + (int64_t)p * BB * BB,
                       qr_fast);
     BAND_TMARK(1)
     // ---- U = V T -> Ws  (MFMA, all 32 row blocks so rows >= m read back as zero)
@@ -672,10 +683,10 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) X[q] = double4_t{0.0, 0.0, 0.0, 0.0};
     switch (nq) {
-      case 1: band_x_accum<1>(A, n, r0, m, wid, c16, g4, Ws, X); break;
-      case 2: band_x_accum<2>(A, n, r0, m, wid, c16, g4, Ws, X); break;
-      case 3: band_x_accum<3>(A, n, r0, m, wid, c16, g4, Ws, X); break;
-      case 4: band_x_accum<4>(A, n, r0, m, wid, c16, g4, Ws, X); break;
+      case 1: band_x_accum<1>(A, lda, r0, m, wid, c16, g4, Ws, X); break;
+      case 2: band_x_accum<2>(A, lda, r0, m, wid, c16, g4, Ws, X); break;
+      case 3: band_x_accum<3>(A, lda, r0, m, wid, c16, g4, Ws, X); break;
+      case 4: band_x_accum<4>(A, lda, r0, m, wid, c16, g4, Ws, X); break;
       default: break;
     }
     BAND_TMARK(4)
@@ -756,66 +767,160 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
     }
     __syncthreads();
     BAND_TMARK(5)
-    // ---- P6: A22 -= V W^T + W V^T on the LOWER block triangle (K = 32 MFMA per 16x16 tile,
-    //      TBR tiles per pass); each off-diagonal tile is also stored transposed, so A stays
-    //      bitwise symmetric at half the MFMA work.  The A tiles of a wave's NEXT pass are
-    //      loaded before this pass's MFMAs, so a wave exposes one memory latency instead of
-    //      one per pass (passes touch disjoint lower tiles; mirrored stores land in the upper
-    //      triangle, which no pass reads).
+    // ---- P6: A22 -= V W^T + W V^T on the LOWER block triangle (K = 32 MFMA per 16x16 tile);
+    //      each off-diagonal tile is also stored transposed, so A stays bitwise symmetric at
+    //      half the MFMA work.  Wave w owns whole block rows I (snake order over groups of
+    //      2 NWR rows: w, 2 NWR - 1 - w, ... - equal tile counts per wave) and walks each row
+    //      TBR tiles at a time: the TBR tiles' operands are read before the chunk's 8 TBR
+    //      MFMAs, which run as TBR independent accumulator chains, and the next chunk's A tiles
+    //      are loaded before this chunk's MFMAs.  No branch surrounds a memory instruction
+    //      (masked loads read a clamped in-range element, masked stores go to a
+    //      per-lane dummy slot in the unused fused-path scratch), so the waitcnt pass knows the
+    //      chunk's store count and waits only for the prefetched loads, never for the stores'
+    //      write-back.
+    //      The per-tile arithmetic (operands and MFMA order) is unchanged, so A is bitwise the
+    //      same.  Chunks touch disjoint lower tiles; mirrored stores land in the upper
+    //      triangle, which no chunk reads.
     {
-      const int ntt = nI * (nI + 1) / 2;
+      double* __restrict__ dummy = bw.F + lane;   // sink of masked stores
+      auto row_of = [&](int rr) {                 // rr-th block row of this wave (may be >= nI)
+        return 2 * NWR * (rr >> 1) + ((rr & 1) ? (2 * NWR - 1 - wid) : wid);
+      };
+      auto sptr = [&](int i, int j, bool ok) {    // &A22[i][j], or the sink if !ok
+        return ok ? A + (int64_t)(r0 + i) * lda + r0 + j : dummy;
+      };
       double4_t nxt[TBR];
-      int ni0[TBR], nj0[TBR];
-      auto fetch = [&](int tb) {
+      auto fetch = [&](int I, int J0) {
 #pragma unroll
         for (int u = 0; u < TBR; ++u) {
-          const int tile = min(tb + u, ntt - 1);
-          // fp32 root (8 tile + 1 < 2^24 is exact; the two fix-ups below absorb any rounding)
-          int I = (int)((__builtin_sqrtf(8.0f * (float)tile + 1.0f) - 1.0f) * 0.5f);
-          if (I * (I + 1) / 2 > tile) --I;
-          if ((I + 1) * (I + 2) / 2 <= tile) ++I;
-          ni0[u] = (tb + u < ntt) ? I * 16 : BMP;      // BMP: beyond every row, a no-op tile
-          nj0[u] = (tile - I * (I + 1) / 2) * 16;
+          const int J = J0 + u;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int i = ni0[u] + g4 + 4 * r, jj = nj0[u] + c16;
-            nxt[u][r] = (i < m && jj < m) ? A[(int64_t)(r0 + i) * n + r0 + jj] : 0.0;
+            const int i = 16 * I + g4 + 4 * r, jj = 16 * J + c16;
+            // (masked elements: any finite value; they only meet their own accumulator entry,
+            // which is never stored)
+            nxt[u][r] = (DBG & 4) ? (double)(i + jj)
+                                  : A[(int64_t)(r0 + min(i, m - 1)) * lda + r0 + min(jj, m - 1)];
           }
         }
       };
-      int tb = wid * TBR;
-      if (tb < ntt) fetch(tb);
-      for (; tb < ntt; tb += NWR * TBR) {
-        double4_t acc[TBR];
-        int ci0[TBR], cj0[TBR];
-#pragma unroll
-        for (int u = 0; u < TBR; ++u) {
-          acc[u] = nxt[u];
-          ci0[u] = ni0[u];
-          cj0[u] = nj0[u];
+      int rr = 0, I = row_of(0), J0 = 0;
+      while (rr < 4 && I >= nI) I = row_of(++rr);
+      if (rr >= 4) I = nI;
+      // advance (I, J0): next chunk of the row, else the next of the wave's rows below nI (the
+      // candidates are not monotone in rr, so every one is tested); I = nI ends the walk
+      auto advance = [&]() {
+        J0 += TBR;
+        if (J0 > I) {
+          J0 = 0;
+          do I = row_of(++rr);
+          while (rr < 4 && I >= nI);
+          if (rr >= 4) I = nI;
         }
-        if (tb + NWR * TBR < ntt) fetch(tb + NWR * TBR);
+      };
+      fetch(I, 0);
+      double* tw = &red[0][0] + wid * (BB * BB);  // wave-private transpose image
+      // the chunk's tiles move nxt -> acc at the END of the previous chunk (after its stores):
+      // at the loop head no load is pending, so the waitcnt pass never merges the first
+      // entry's load-only queue with the loop's load + store queue (which forced a full
+      // vmcnt(0) drain of the stores)
+      double4_t acc[TBR];
+#pragma unroll
+      for (int u = 0; u < TBR; ++u) acc[u] = nxt[u];
+      // (a use here makes the first chunk's loads complete before the loop: otherwise they
+      // are still pending at the loop head, and the wait merged from that entry edge drains
+      // the previous chunk's stores on every iteration)
+#pragma unroll
+      for (int u = 0; u < TBR; ++u) asm volatile("" ::"v"(acc[u]));
+      int ci = I, cj = J0;
+      advance();
+      while (ci < nI) {
+        // this chunk: tiles (ci, cj .. cj + TBR - 1), J <= ci
+        fetch(I, J0);                             // (I = nI: every lane masked)
+        double aV[4], aW[4], bW[TBR][4], bV[TBR][4];
+        const int ia = 16 * ci + c16;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          aV[s] = -Vs[ia][4 * s + g4];
+          aW[s] = -Ws[ia][4 * s + g4];
+        }
 #pragma unroll
         for (int u = 0; u < TBR; ++u) {
-          const int ia = min(ci0[u], BMP - 16) + c16, jb = cj0[u] + c16;
+          const int jb = 16 * min(cj + u, ci) + c16;
 #pragma unroll
-          for (int s = 0; s < 8; ++s) {
-            const int kk = 4 * (s & 3) + g4;
-            const double av = (s < 4) ? Vs[ia][kk] : Ws[ia][kk];
-            const double bv = (s < 4) ? Ws[jb][kk] : Vs[jb][kk];
-            acc[u] = mfma_f64_16x16x4(-av, bv, acc[u]);
+          for (int s = 0; s < 4; ++s) {
+            bW[u][s] = Ws[jb][4 * s + g4];
+            bV[u][s] = Vs[jb][4 * s + g4];
           }
         }
+        if constexpr (!(DBG & 2)) {
 #pragma unroll
-        for (int u = 0; u < TBR; ++u)
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int u = 0; u < TBR; ++u) acc[u] = mfma_f64_16x16x4(aV[s], bW[u][s], acc[u]);
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int u = 0; u < TBR; ++u) acc[u] = mfma_f64_16x16x4(aW[s], bV[u][s], acc[u]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < TBR; ++u) acc[u][0] += aV[u] * bW[u][0] + aW[u] * bV[u][3];
+        }
+#pragma unroll
+        for (int u = 0; u < TBR; ++u) {
+          const int J = cj + u;
+          const bool live = J <= ci;
+          if constexpr ((DBG & 1) != 0) {
+            continue;
+          } else if constexpr ((DBG & 8) != 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int i = 16 * ci + g4 + 4 * r, jj = 16 * J + c16;
+              *sptr(i, jj, live && i < m && jj < m) = acc[u][r];
+            }
+            continue;
+          }
+          // the tile goes through the wave-private 16 x 16 LDS image (XOR-swizzled,
+          // conflict-free both ways; `red` is free in this phase): the mirror (upper) tile is
+          // stored row-contiguous, and both stores take their data from LDS reads, not from
+          // the accumulators - a store whose data registers the next chunk's MFMAs overwrite
+          // would make the waitcnt pass drain it first
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int i = ci0[u] + g4 + 4 * r, jj = cj0[u] + c16;
-            if (i < m && jj < m) {
-              A[(int64_t)(r0 + i) * n + r0 + jj] = acc[u][r];
-              if (ci0[u] != cj0[u]) A[(int64_t)(r0 + jj) * n + r0 + i] = acc[u][r];
-            }
+            const int row = g4 + 4 * r;
+            tw[row * BB + (c16 ^ (row & ~1))] = acc[u][r];
           }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = g4 + 4 * r;
+            const double v = tw[row * BB + (c16 ^ (row & ~1))];
+            const int i = 16 * ci + row, jj = 16 * J + c16;
+            *sptr(i, jj, live && i < m && jj < m) = v;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int col = g4 + 4 * r;                    // mirror row = tile column
+            const double v = tw[c16 * BB + (col ^ (c16 & ~1))];
+            const int mi = 16 * J + col, mj = 16 * ci + c16;
+            *sptr(mi, mj, live && J != ci && mi < m && mj < m) = v;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        // accumulators kept live to here: the stores' address / data temporaries must not
+        // reuse their registers (the next chunk's MFMAs write them, and the waitcnt pass
+        // would drain the stores before those MFMAs)
+#pragma unroll
+        for (int u = 0; u < TBR; ++u) asm volatile("" ::"v"(acc[u]));
+#pragma unroll
+        for (int u = 0; u < TBR; ++u) acc[u] = nxt[u];
+        ci = I;
+        cj = J0;
+        advance();
       }
     }
     __syncthreads();
@@ -825,11 +930,11 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
   if (tim != nullptr && threadIdx.x == 0)
     for (int q = 0; q < 8; ++q) tim[(int64_t)blockIdx.x * 8 + q] = tacc[q];
 #undef BAND_TMARK
-  for (int i = t; i < n; i += NTR) bw.z[i] = zs[i];
+  for (int i = t_; i < n; i += NTR) bw.z[i] = zs[i];
   // ---- row-major lower band: LB[r][s] = B[r][r-16+s]  (s = 16: diagonal)
-  for (int e = t; e < n * LS; e += NTR) {
+  for (int e = t_; e < n * LS; e += NTR) {
     const int r = e / LS, c = r - BB + e % LS;
-    bw.LB[e] = (c >= 0) ? A[(int64_t)r * n + c] : 0.0;
+    bw.LB[e] = (c >= 0) ? A[(int64_t)r * lda + c] : 0.0;
   }
 }
 
@@ -935,12 +1040,24 @@ __global__ __launch_bounds__(NTR) void band_fused_kernel(
         aops(Vq, p, cV);
         aops(Wq, p, cW);
       }
-      for (int it = wid; it < nb - p; it += NWR) {
-        const int I = p + it;
-        double4_t c;
-        const int64_t o = toff(I, p);
+      constexpr int FS = (BNMAX / BB + NWR - 1) / NWR;   // strip tiles per wave (<= 5)
+      double4_t cs[FS];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) c[r] = A[o + (int64_t)4 * r * lda];
+      for (int u = 0; u < FS; ++u) {                       // every load in flight at once
+        const int it = wid + NWR * u;
+        if (it < nb - p) {
+          const int64_t o = toff(p + it, p);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cs[u][r] = A[o + (int64_t)4 * r * lda];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < FS; ++u) {
+        const int it = wid + NWR * u;
+        if (it >= nb - p) continue;
+        const int I = p + it;
+        double4_t c = cs[u];
+        const int64_t o = toff(I, p);
         if (p > 0) {
           double rV[4], rW[4];
           aops(Vq, I, rV);
@@ -964,8 +1081,17 @@ __global__ __launch_bounds__(NTR) void band_fused_kernel(
     __syncthreads();
     FUSED_TMARK(1)
     // ---- B: QR of the panel (rows r0 .., from Vs) -> V_p (Vs), T_p, R / V into A
-    band_panel_factor(A, lda, k0, r0, m, Vs, Us, &red[0][0], Ts, taus,
-                      bw.T + (int64_t)p * BB * BB, false, nullptr, Vs);
+    {
+      long long tk[2] = {0, 0};
+      band_panel_factor(A, lda, k0, r0, m, Vs, Us, &red[0][0], Ts, taus,
+                        bw.T + (int64_t)p * BB * BB, false,
+                        (TIMED && threadIdx.x == 0) ? tk : nullptr, Vs);
+      if (TIMED && threadIdx.x == 0) {    // slot 0: column loop + V stores, 7: G and T
+        const long long now = (long long)__builtin_amdgcn_s_memtime();
+        tacc[0] += tk[1] - tk[0];
+        tacc[7] += now - tk[1];
+      }
+    }
     FUSED_TMARK(2)
     asm volatile("" : "+v"(c16), "+v"(g4), "+v"(cq), "+v"(rg), "+v"(t), "+v"(lane));
     // ---- C: U = V T -> Us (all 32 row blocks: rows >= m read back as zero)
@@ -997,24 +1123,39 @@ __global__ __launch_bounds__(NTR) void band_fused_kernel(
             aops(Wq, J0 + NWR * (jg + j), cW[j]);
           }
         }
-        for (int I = p + 1; I < nb; ++I) {
-          double rV[4], rW[4], ub[4];
+        // software pipeline: the tiles and row operands of row block I + 1 are loaded
+        // before the MFMAs of row block I (one memory latency per pass, not one per tile)
+        double4_t cn[FJ];
+        double rVn[4], rWn[4];
+        auto fetch = [&](int I) {
           if (p > 0) {
-            aops(Vq, I, rV);
-            aops(Wq, I, rW);
+            aops(Vq, I, rVn);
+            aops(Wq, I, rWn);
           }
-          const int il = 16 * (I - p - 1);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) ub[r] = Us[il + 4 * r + g4][c16];
-          double4_t c[FJ];
 #pragma unroll
           for (int j = 0; j < FJ; ++j) {
             if (jg + j < nj) {
               const double* __restrict__ tp = A + toff(I, J0 + NWR * (jg + j));
 #pragma unroll
-              for (int r = 0; r < 4; ++r) c[j][r] = tp[4 * r * lda];
+              for (int r = 0; r < 4; ++r) cn[j][r] = tp[4 * r * lda];
             }
           }
+        };
+        fetch(p + 1);
+        for (int I = p + 1; I < nb; ++I) {
+          double rV[4], rW[4], ub[4];
+          double4_t c[FJ];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            rV[q] = rVn[q];
+            rW[q] = rWn[q];
+          }
+#pragma unroll
+          for (int j = 0; j < FJ; ++j) c[j] = cn[j];
+          if (I + 1 < nb) fetch(I + 1);
+          const int il = 16 * (I - p - 1);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ub[r] = Us[il + 4 * r + g4][c16];
 #pragma unroll
           for (int j = 0; j < FJ; ++j) {
             if (jg + j < nj) {
@@ -1806,7 +1947,7 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
       Y[q][r] = (lok && i < n) ? yc[i] : 0.0;
     }
   // va[q][r] = V_p[16 b - r0 + 4 r + g4][c16] for the live blocks b = wid + 8 q of panel p
-  const int lda = fused ? band_npad(n) : n;       // A's leading dimension (fused: padded)
+  const int lda = fused ? band_npad(n) : n;       // A's leading dimension (padded: the one-WG kernels)
   const int lo_a = g4 * lda + c16;
   double vn[NBW][4], tn[4];
   auto fetch = [&](int p) {
@@ -1934,7 +2075,24 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
       hipLaunchKernelGGL(band_fused_kernel<false>, dim3(ncells), dim3(NTR), 0, st, SD, ldS, Sr, cd,
                          L, work, tim);
   } else if (single) {
-    if (qr_fast)
+    const char* denv = getenv("PFML_BAND_DBG");
+    const int dbg = (tim != nullptr && denv) ? atoi(denv) : 0;
+    if (dbg == 1)
+      hipLaunchKernelGGL((ridge_band_reduce_kernel<false, 1>), dim3(ncells), dim3(NTR), 0, st, SD,
+                         ldS, Sr, cd, L, work, tim);
+    else if (dbg == 2)
+      hipLaunchKernelGGL((ridge_band_reduce_kernel<false, 2>), dim3(ncells), dim3(NTR), 0, st, SD,
+                         ldS, Sr, cd, L, work, tim);
+    else if (dbg == 4)
+      hipLaunchKernelGGL((ridge_band_reduce_kernel<false, 4>), dim3(ncells), dim3(NTR), 0, st, SD,
+                         ldS, Sr, cd, L, work, tim);
+    else if (dbg == 8)
+      hipLaunchKernelGGL((ridge_band_reduce_kernel<false, 8>), dim3(ncells), dim3(NTR), 0, st, SD,
+                         ldS, Sr, cd, L, work, tim);
+    else if (dbg == 7)
+      hipLaunchKernelGGL((ridge_band_reduce_kernel<false, 7>), dim3(ncells), dim3(NTR), 0, st, SD,
+                         ldS, Sr, cd, L, work, tim);
+    else if (qr_fast)
       hipLaunchKernelGGL(ridge_band_reduce_kernel<true>, dim3(ncells), dim3(NTR), 0, st, SD, ldS,
                          Sr, cd, L, work, tim);
     else
@@ -1972,6 +2130,6 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   }
   const int nch = (L + LC - 1) / LC;
   hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3(ncells * nch), dim3(NTB), 0, st, cd,
-                     ncells, L, work, beta_out, ldo, fused ? 1 : 0);
+                     ncells, L, work, beta_out, ldo, (fused || single) ? 1 : 0);
   return hipGetLastError();
 }

@@ -1,15 +1,12 @@
 """fp64 batched GEMM with fused diagonal scalings.
 
 ``gemm(A, B)`` computes ``alpha * diag(rs) @ op(A) @ op(B) @ diag(cs) + beta * C`` for 2-D or
-3-D (batched) fp64 tensors.  On CPU it is the torch fp64 oracle.  On a HIP device:
-
-* a product with a fused diagonal scaling runs ``pfml_dgemm`` (csrc/gemm_f64.hip,
-  v_mfma_f64_16x16x4_f64, scales in the epilogue);
-* a plain product (no scaling) is a library GEMM and goes to rocBLAS through torch
-  (``baddbmm``), which sustains 40-66 TF/s fp64 on the S4 shapes against 19-40 TF/s for the
-  hand-written tile (tools/bench_gemm.py, profiles/r01_gemm_own_vs_rocblas.json).
-
-``backend="own"`` (or PFML_GEMM=own) forces the hand-written kernel, ``"blas"`` rocBLAS.
+3-D (batched) fp64 tensors.  On CPU it is the torch fp64 oracle.  On a HIP device every
+product runs ``pfml_dgemm`` (csrc/gemm_f64.hip, v_mfma_f64_16x16x4_f64, scales in the
+epilogue): 54 TF/s plain and 51.5 TF/s with the fused Horner epilogue on the S4 shapes, against
+56-61 TF/s for rocBLAS (profiles/r02_gemm_own_vs_rocblas.txt) - the engine has no library GEMM
+on its paths.  ``backend="blas"`` (or PFML_GEMM=blas) routes an unscaled product to rocBLAS
+through torch, as an explicit A/B only.
 """
 from __future__ import annotations
 
@@ -82,9 +79,9 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, trans_a: bool = False, trans_b: bo
     cs3 = None if col_scale is None else (col_scale.unsqueeze(0) if col_scale.dim() == 1 else col_scale)
 
     if backend == "auto":
-        backend = os.environ.get("PFML_GEMM", "auto")
-    if (nat.is_device(A) and backend != "own" and rs3 is None and cs3 is None
-            and C3.stride(-1) == 1 and (backend == "blas" or A.dtype == torch.float64)):
+        backend = os.environ.get("PFML_GEMM", "own")
+    if (nat.is_device(A) and backend == "blas" and rs3 is None and cs3 is None
+            and C3.stride(-1) == 1):
         _blas_gemm(A3, B3, trans_a, trans_b, float(alpha), float(beta), C3)
     elif nat.is_device(A):
         if A.dtype != torch.float64:

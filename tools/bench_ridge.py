@@ -52,7 +52,7 @@ def timing(n=513, ncells=1):
     if os.environ.get("PFML_RIDGE_VARIANT", "band")[:1] in ("f", "t"):
         names = ["col_k", "householder", "sweep", "xy", "p_w_z", "trailing", "panel_end", "-"]
     elif os.environ.get("PFML_BAND_MODE", "")[:1] == "f":
-        names = ["-", "strip", "qr", "U", "pass", "P_z_W", "final", "-"]
+        names = ["qr_columns", "strip", "qr_total", "U", "pass", "P_z_W", "final", "qr_G_T"]
     else:
         names = ["load", "qr", "G_T", "U", "X", "P4_z_W", "trailing", "-"]
     tot = max(1, int(t.sum()))

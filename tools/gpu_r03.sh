@@ -15,13 +15,13 @@ for step in ${MODE//,/ }; do
   case $step in
     peak)
       timeout -k 10 120 ./tools/micro/mfma_f64_peak > $OUT/mfma_peak.json 2>&1
-      rc=$?; cat $OUT/mfma_peak.json; [ $rc -ne 0 ] && exit $rc ;;
+      rc=$?; cat $OUT/mfma_peak.json; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     suite)
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
       rc=$?; tail -2 $OUT/pytest_gpu.log
       if [ $rc -ne 0 ]; then grep -E "^E |FAILED" $OUT/pytest_gpu.log | head -20; exit $rc; fi
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
-      rc=$?; tail -1 $OUT/smoke.log; [ $rc -ne 0 ] && exit $rc ;;
+      rc=$?; tail -1 $OUT/smoke.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     bench)
       timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
       rc=$?; grep '^{' $OUT/bench.json | cut -c1-400; if [ $rc -ne 0 ]; then tail -5 $OUT/bench.err; exit $rc; fi ;;
@@ -29,9 +29,15 @@ for step in ${MODE//,/ }; do
       # band-reduction A/B: per-phase cycles of one n = 513 cell and the grid vs #cells
       for m in single fused; do
         PFML_BAND_MODE=$m timeout -k 10 120 python tools/bench_ridge.py --timing > $OUT/ridge_timing_$m.json 2>&1
-        rc=$?; cat $OUT/ridge_timing_$m.json; [ $rc -ne 0 ] && exit $rc
+        rc=$?; cat $OUT/ridge_timing_$m.json; if [ $rc -ne 0 ]; then exit $rc; fi
         PFML_BAND_MODE=$m PFML_BENCH_CELLS=1,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/ridge_cells_$m.log 2>&1
-        rc=$?; tail -1 $OUT/ridge_cells_$m.log; [ $rc -ne 0 ] && exit $rc
+        rc=$?; tail -1 $OUT/ridge_cells_$m.log; if [ $rc -ne 0 ]; then exit $rc; fi
+      done ;;
+    ridgedbg)
+      # trailing-update bottleneck probe: per-phase cycles with parts of P6 compiled out
+      for d in 0 1 2 4 8 7; do
+        PFML_BAND_MODE=single PFML_BAND_DBG=$d timeout -k 10 120 python tools/bench_ridge.py --timing > $OUT/ridge_dbg_$d.json 2>&1
+        rc=$?; echo "dbg $d: $(grep trailing $OUT/ridge_dbg_$d.json)"; if [ $rc -ne 0 ]; then exit $rc; fi
       done ;;
     fusedtest)
       timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 120 --timeout-method thread -k "band_fused or band_reduction_modes" > $OUT/pytest_fused.log 2>&1
