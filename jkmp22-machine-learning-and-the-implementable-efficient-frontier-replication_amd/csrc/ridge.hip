@@ -921,7 +921,9 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
 extern "C" int64_t pfml_ridge_work_doubles(int n, int L) {
   const int64_t tri = (int64_t)n * n + 5LL * n * L + 4LL * n + 32LL * n;
   const int64_t band = pfml_ridge_band_work_doubles(n, L);
-  return tri > band ? tri : band;
+  // rounded to 32 doubles: every cell's workspace (and so its band matrix, whose rows the
+  // band kernels store 16 bytes at a time) starts 256-byte aligned
+  return ((tri > band ? tri : band) + 31) / 32 * 32;
 }
 
 static long long* g_ridge_timing = nullptr;

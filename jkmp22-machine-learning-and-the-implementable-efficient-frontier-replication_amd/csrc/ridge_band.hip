@@ -498,6 +498,9 @@ __device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n,
   static_for<0, BB>([&](auto J) {
     constexpr int j = decltype(J)::value;
     const int par = j & 1;
+    // (tk: per-column sub-phases of thread 0's wave, accumulated in tk[2..4]: own work before
+    // the barrier, barrier wait, reductions + pivot chain + update after it)
+    const long long tc0 = tk ? (long long)__builtin_amdgcn_s_memtime() : 0;
     double x[16];
     double s1p[4] = {0.0, 0.0, 0.0, 0.0};
     // Only row group q = 0 (rows < 32) meets the diagonal; groups of four row groups at or
@@ -517,7 +520,17 @@ __device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n,
     const double s1 = rowgroup_sum((s1p[0] + s1p[1]) + (s1p[2] + s1p[3]));
     if (lane < 16) redf[par * 256 + wid * 16 + lane] = s1;
     if (rg == j) redf[512 + par * 16 + cq] = a[0];       // row j (q = 0)
+    long long tc1 = 0;
+    if (tk) {
+      tc1 = (long long)__builtin_amdgcn_s_memtime();
+      tk[2] += tc1 - tc0;
+    }
     __syncthreads();
+    if (tk) {
+      const long long tc2 = (long long)__builtin_amdgcn_s_memtime();
+      tk[3] += tc2 - tc1;
+      tk[5] = tc2;
+    }
     double xn2 = 0.0, dc = 0.0;
 #pragma unroll
     for (int w = 0; w < NWR; ++w) {
@@ -541,6 +554,12 @@ __device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n,
       scal = copysign(rcp_f64(fabs(alpha) + nrm), alpha);
     }
     const double wc = tau * (vjc + scal * dc);
+    // rows >= 32 (q > 0, below every diagonal): one FMA and one multiply per element with
+    // lane factors fixed per column instead of two selects - columns cq > j get
+    // a - v wc (wcl = wc, sl = 1), column j becomes v = a scal (its x IS its own a: wcl = 0,
+    // sl = scal), finished columns cq < j stay (wcl = 0, sl = 1)
+    const double wcl = (cq > j) ? wc : 0.0;
+    const double sl = (cq == j) ? scal : 1.0;
 #pragma unroll
     for (int q4 = 0; q4 < 16; q4 += 4) {
       if (q4 > 0 && 32 * q4 >= m) continue;
@@ -550,14 +569,15 @@ __device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n,
         if (q == 0) {
           const double v = (i > j) ? x[q] * scal : ((i == j && i < m) ? 1.0 : 0.0);
           const double diag = (i > j) ? v : ((i == j) ? beta : a[q]);
-          a[q] = (cq > j) ? a[q] - v * wc : ((cq == j) ? diag : a[q]);
+          a[q] = (cq > j) ? fma(-v, wc, a[q]) : ((cq == j) ? diag : a[q]);
         } else {
           const double v = x[q] * scal;
-          a[q] = (cq > j) ? a[q] - v * wc : ((cq == j) ? v : a[q]);
+          a[q] = fma(-v, wcl, a[q]) * sl;
         }
       }
     }
     if (t == 0) taus[j] = tau;
+    if (tk) tk[4] += (long long)__builtin_amdgcn_s_memtime() - tk[5];
   });
   // explicit V -> Vs (MFMA operand); V (strictly lower) and R (upper) -> A's panel columns
 #pragma unroll
@@ -661,8 +681,19 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
     asm volatile("" : "+v"(t), "+v"(lane));
     const int c16 = lane & 15, g4 = lane >> 4;
     const int cq = t & 15, rg = t >> 4;          // (row group of 32, column) thread map
-    band_panel_factor(A, lda, k0, r0, m, Vs, Ws, &red[0][0], Ts, taus, bw.T + (int64_t)p * BB * BB,
-                      qr_fast);
+    {
+      // (timing: slots 0 / 2 / 7 = the column loop's own work / barrier wait / pivot chain +
+      // update, accumulated over the panels by thread 0)
+      long long tk[6] = {0, 0, 0, 0, 0, 0};
+      band_panel_factor(A, lda, k0, r0, m, Vs, Ws, &red[0][0], Ts, taus,
+                        bw.T + (int64_t)p * BB * BB, qr_fast,
+                        (tim != nullptr && threadIdx.x == 0) ? tk : nullptr);
+      if (tim != nullptr && threadIdx.x == 0) {
+        tacc[0] += tk[2];
+        tacc[2] += tk[3];
+        tacc[7] += tk[4];
+      }
+    }
     BAND_TMARK(1)
     // ---- U = V T -> Ws  (MFMA, all 32 row blocks so rows >= m read back as zero)
 #pragma unroll
@@ -715,28 +746,30 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
       if (lane < 16) red2[wid][lane] = s;
     }
     __syncthreads();
-    // z <- Q_p^T z = z - V (T^T (V^T z))
+    // z <- Q_p^T z = z - V (T^T (V^T z)).  Lane c16 forms zv[c16] and zt[c16] only (8 + 16
+    // LDS reads instead of every thread reading all 8 x 16 partials and the 136 T entries);
+    // the other entries reach it by row_newbcast DPP.  Same operations in the same order as
+    // band_fused_kernel, so the bits are unchanged.
     {
-      double zv[BB];
+      double zvl = 0.0;
 #pragma unroll
-      for (int a = 0; a < BB; ++a) {
-        double s = 0.0;
-#pragma unroll
-        for (int w = 0; w < NWR; ++w) s += red2[w][a];
-        zv[a] = s;
-      }
-      double zt[BB];
-#pragma unroll
-      for (int c = 0; c < BB; ++c) {
-        double s = 0.0;
-#pragma unroll
-        for (int a = 0; a <= c; ++a) s += Ts[a][c] * zv[a];
-        zt[c] = s;
-      }
+      for (int w = 0; w < NWR; ++w) zvl += red2[w][c16];
+      double ztl = 0.0;
+      static_for<0, BB>([&](auto A_) {
+        constexpr int a = decltype(A_)::value;
+        const double za = row_bcast<a>(zvl);
+        const double ns = fma(Ts[a][c16], za, ztl);
+        ztl = (a <= c16) ? ns : ztl;
+      });
+      double zt[BB];                     // broadcast before the row loop (all lanes active)
+      static_for<0, BB>([&](auto C_) {
+        constexpr int c = decltype(C_)::value;
+        zt[c] = row_bcast<c>(ztl);
+      });
       for (int i = t; i < m; i += NTR) {
         double s = 0.0;
 #pragma unroll
-        for (int c = 0; c < BB; ++c) s += Vs[i][c] * zt[c];
+        for (int c = 0; c < BB; ++c) s = fma(Vs[i][c], zt[c], s);
         zs[r0 + i] -= s;
       }
     }
@@ -783,6 +816,7 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
     //      triangle, which no chunk reads.
     {
       double* __restrict__ dummy = bw.F + lane;   // sink of masked stores
+      double2* __restrict__ dummy2 = reinterpret_cast<double2*>(bw.F) + lane;
       auto row_of = [&](int rr) {                 // rr-th block row of this wave (may be >= nI)
         return 2 * NWR * (rr >> 1) + ((rr & 1) ? (2 * NWR - 1 - wid) : wid);
       };
@@ -880,11 +914,15 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
             }
             continue;
           }
-          // the tile goes through the wave-private 16 x 16 LDS image (XOR-swizzled,
-          // conflict-free both ways; `red` is free in this phase): the mirror (upper) tile is
-          // stored row-contiguous, and both stores take their data from LDS reads, not from
-          // the accumulators - a store whose data registers the next chunk's MFMAs overwrite
-          // would make the waitcnt pass drain it first
+          // the tile goes through the wave-private 16 x 16 LDS image (XOR-swizzled on even
+          // column offsets, so column pairs stay adjacent; `red` is free in this phase) and
+          // leaves as 16-byte stores: lane l writes columns 2 (l & 7), +1 of row l >> 3 (+8),
+          // two dwordx4 stores per 16 x 16 tile and two for its mirror (upper) tile, where
+          // lane-per-element stores took eight dwordx2.  The data comes from LDS reads, not
+          // from the accumulators: a store whose data registers the next chunk's MFMAs
+          // overwrite would make the waitcnt pass drain it first.  Elements past m (rows or
+          // columns >= n) are written like the rest: the padding of the npad x npad matrix is
+          // never read (every load is clamped below m).
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = g4 + 4 * r;
@@ -893,19 +931,29 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          {
+            const int pr = lane >> 3, pc = 2 * (lane & 7);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = g4 + 4 * r;
-            const double v = tw[row * BB + (c16 ^ (row & ~1))];
-            const int i = 16 * ci + row, jj = 16 * J + c16;
-            *sptr(i, jj, live && i < m && jj < m) = v;
-          }
+            for (int h = 0; h < 2; ++h) {
+              const int row = pr + 8 * h;
+              const double2 v = *reinterpret_cast<const double2*>(&tw[row * BB + (pc ^ (row & ~1))]);
+              double2* dst = live ? reinterpret_cast<double2*>(
+                                        A + (int64_t)(r0 + 16 * ci + row) * lda + r0 + 16 * J + pc)
+                                  : dummy2;
+              *dst = v;
+            }
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int col = g4 + 4 * r;                    // mirror row = tile column
-            const double v = tw[c16 * BB + (col ^ (c16 & ~1))];
-            const int mi = 16 * J + col, mj = 16 * ci + c16;
-            *sptr(mi, mj, live && J != ci && mi < m && mj < m) = v;
+            for (int h = 0; h < 2; ++h) {
+              const int col = pr + 8 * h;                    // mirror row = tile column
+              double2 v;
+              v.x = tw[pc * BB + (col ^ (pc & ~1))];
+              v.y = tw[(pc + 1) * BB + (col ^ ((pc + 1) & ~1))];
+              double2* dst = (live && J != ci)
+                                 ? reinterpret_cast<double2*>(
+                                       A + (int64_t)(r0 + 16 * J + col) * lda + r0 + 16 * ci + pc)
+                                 : dummy2;
+              *dst = v;
+            }
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
@@ -1082,7 +1130,7 @@ __global__ __launch_bounds__(NTR) void band_fused_kernel(
     FUSED_TMARK(1)
     // ---- B: QR of the panel (rows r0 .., from Vs) -> V_p (Vs), T_p, R / V into A
     {
-      long long tk[2] = {0, 0};
+      long long tk[6] = {0, 0, 0, 0, 0, 0};
       band_panel_factor(A, lda, k0, r0, m, Vs, Us, &red[0][0], Ts, taus,
                         bw.T + (int64_t)p * BB * BB, false,
                         (TIMED && threadIdx.x == 0) ? tk : nullptr, Vs);

@@ -54,7 +54,8 @@ def timing(n=513, ncells=1):
     elif os.environ.get("PFML_BAND_MODE", "")[:1] == "f":
         names = ["qr_columns", "strip", "qr_total", "U", "pass", "P_z_W", "final", "qr_G_T"]
     else:
-        names = ["load", "qr", "G_T", "U", "X", "P4_z_W", "trailing", "-"]
+        names = ["qrcol_own", "qr", "qrcol_barrier", "U", "X", "P4_z_W", "trailing",
+                 "qrcol_chain_update"]   # qrcol_*: inside "qr" (thread 0 wave)
     tot = max(1, int(t.sum()))
     out = {nm: f"{int(v)} cyc ({100.0 * v / tot:.1f}%)" for nm, v in zip(names, t)}
     out.update(extra)

@@ -39,6 +39,12 @@ for step in ${MODE//,/ }; do
         PFML_BAND_MODE=single PFML_BAND_DBG=$d timeout -k 10 120 python tools/bench_ridge.py --timing > $OUT/ridge_dbg_$d.json 2>&1
         rc=$?; echo "dbg $d: $(grep trailing $OUT/ridge_dbg_$d.json)"; if [ $rc -ne 0 ]; then exit $rc; fi
       done ;;
+    ridgecqr)
+      # CholeskyQR2 panel factorisation (PFML_BAND_QR=cqr) in the single kernel
+      PFML_BAND_MODE=single PFML_BAND_QR=cqr timeout -k 10 120 python tools/bench_ridge.py --timing > $OUT/ridge_timing_cqr.json 2>&1
+      rc=$?; cat $OUT/ridge_timing_cqr.json; if [ $rc -ne 0 ]; then exit $rc; fi
+      PFML_BAND_MODE=single PFML_BAND_QR=cqr PFML_BENCH_CELLS=1,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/ridge_cells_cqr.log 2>&1
+      rc=$?; tail -1 $OUT/ridge_cells_cqr.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     fusedtest)
       timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 120 --timeout-method thread -k "band_fused or band_reduction_modes" > $OUT/pytest_fused.log 2>&1
       rc=$?; tail -3 $OUT/pytest_fused.log
