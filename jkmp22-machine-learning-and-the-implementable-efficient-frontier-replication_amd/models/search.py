@@ -298,6 +298,17 @@ def _search_setup(months: np.ndarray, years: np.ndarray, p_vec, G: int, T: int, 
                cell_scale=np.asarray(cell_scale), v_yi=v_yi, v_m=v_m, nVr=nVr,
                jc=np.asarray(jc), jm=np.asarray(jm), jn=np.asarray(jn), dev_idx=None,
                lvec=torch.as_tensor(l_vec, dtype=torch.float64, device=dev))
+    # every index the window-sum kernels turn into an address, checked on the host
+    sta, spa = np.asarray(st, np.int64), np.asarray(sp, np.int64)
+    if nseg and (sta.min() < 0 or spa.max() > T or (spa < sta).any() or nseg > 128):
+        raise ValueError(f"rank {rank}: window segments out of range (T={T}, nseg={nseg})")
+    nlc = len(chunk_seg)
+    if nlc and (cs.min() < 0 or ce.max() > nseg or (ce < cs).any()):
+        raise ValueError(f"rank {rank}: chunk segment ranges out of range")
+    nslot = int(sum(counts))
+    for arr in (tot_slots[0], tot_slots[1]):
+        if len(arr) and (arr.min() < 0 or arr.max() >= nslot):
+            raise ValueError(f"rank {rank}: chunk total slots out of range")
     if nseg and dev is not None and dev.type == "cuda":
         from ..ops.ridge import upload
         out["dev_idx"] = upload([np.asarray(st, np.int32), np.asarray(sp, np.int32),

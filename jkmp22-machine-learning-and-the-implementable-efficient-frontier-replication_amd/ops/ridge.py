@@ -535,6 +535,28 @@ def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell,
     return plan
 
 
+def check_launch_bounds(S: int, P: int, T: int, cell_src, cell_n, job_cell, job_month,
+                        job_n) -> None:
+    """Host-side guard before any ridge / utilities kernel sees the plan: every index the
+    descriptors turn into a device address must be in range (a bad plan would otherwise be a
+    GPU memory fault, not an exception)."""
+    nc = len(cell_src)
+    bad = []
+    if nc and (int(np.min(cell_src)) < 0 or int(np.max(cell_src)) >= S):
+        bad.append(f"cell_src outside [0, {S})")
+    if nc and (int(np.min(cell_n)) < 1 or int(np.max(cell_n)) > P):
+        bad.append(f"cell_n outside [1, {P}]")
+    if len(job_cell):
+        if int(np.min(job_cell)) < 0 or int(np.max(job_cell)) >= nc:
+            bad.append(f"job_cell outside [0, {nc})")
+        if int(np.min(job_month)) < 0 or int(np.max(job_month)) >= T:
+            bad.append(f"job_month outside [0, {T})")
+        if int(np.min(job_n)) < 1 or int(np.max(job_n)) > P:
+            bad.append(f"job_n outside [1, {P}]")
+    if bad:
+        raise ValueError("ridge_utilities: invalid launch plan: " + "; ".join(bad))
+
+
 def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_scale,
                     lvec: torch.Tensor, D: torch.Tensor, R: torch.Tensor, job_cell, job_month,
                     job_n, ready: dict | None = None) -> tuple[torch.Tensor, torch.Tensor]:
@@ -567,6 +589,7 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
         ready = None
     th = _HostClock()
     S, P, _ = SD.shape
+    check_launch_bounds(S, P, D.shape[0], cell_src, cell_n, job_cell, job_month, job_n)
     L = int(lvec.numel())
     nc = len(cell_src)
     dev = SD.device

@@ -52,6 +52,15 @@ for step in ${MODE//,/ }; do
     benchfused)
       PFML_BAND_MODE=fused timeout -k 10 300 python bench.py --no-inputs > $OUT/bench_fused.json 2> $OUT/bench_fused.err
       rc=$?; grep '^{' $OUT/bench_fused.json | cut -c1-300; if [ $rc -ne 0 ]; then tail -5 $OUT/bench_fused.err; exit $rc; fi ;;
+    timeline)
+      # kernel timeline of the last full 1-GPU grid step
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/prof1 -o run -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-inputs > $OUT/prof1.log 2>&1)
+      rc=$?; if [ $rc -ne 0 ]; then tail -3 $OUT/prof1.log; exit $rc; fi
+      python tools/rocprof_timeline.py $(find $OUT/prof1 -name "*.db" | head -1) --last 40 > $OUT/timeline1.txt 2>&1
+      tail -32 $OUT/timeline1.txt ;;
+    shard)
+      PFML_SHARD_GRAPH=1 timeout -k 10 300 python tools/bench_shard.py 1,2,4,8 > $OUT/shard.json 2> $OUT/shard.err
+      rc=$?; cat $OUT/shard.json; if [ $rc -ne 0 ]; then tail -3 $OUT/shard.err; exit $rc; fi ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
