@@ -129,8 +129,10 @@ def graphed(fn, dev):
         torch.cuda.synchronize(dev)
         return g.replay
     except Exception as e:                         # noqa: BLE001 - fall back to eager launches
+        import traceback
         print(f"[bench] graph capture failed, eager launches: {type(e).__name__}: {e}",
               file=sys.stderr)
+        traceback.print_exc()
         return None
 
 

@@ -241,12 +241,15 @@ __device__ __forceinline__ bool tile_upper(int I, int J, int i, int j, int r, in
   return i < P && j < P && (I != J || c >= r);
 }
 
-// tot slot[lc] (upper triangle) = left fold of segments [cs[lc], ce[lc]) from 0
+// tot slot[lc] (upper triangle) = left fold of segments [cs[lc], ce[lc]) from 0; one
+// workgroup per (tile, g, chunk): the chunks are independent, so the launch has nlc times
+// the workgroups of a per-tile loop over them (that form was latency-bound: 306 workgroups
+// walking 61 segment tiles one after another, 127 us for 128 MB).  Same per-element order.
 __global__ __launch_bounds__(256) void wsum_chunk_totals_kernel(
     int P, int nseg, int skip, const double* __restrict__ out, const double* __restrict__ scratch,
     int nlc, const int* __restrict__ cs, const int* __restrict__ ce, const int* __restrict__ slot,
     double* __restrict__ tot, int64_t tstride) {
-  const int g = blockIdx.y;
+  const int g = blockIdx.y, lc = blockIdx.z;
   int tile = blockIdx.x;
   const int nt = (P + 31) / 32;
   int I = 0;
@@ -254,35 +257,52 @@ __global__ __launch_bounds__(256) void wsum_chunk_totals_kernel(
   const int J = I + tile;
   const int64_t PP = (int64_t)P * P;
   const int t = threadIdx.x, c = t & 31, r0 = t >> 5;
-  for (int lc = 0; lc < nlc; ++lc) {
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int s = cs[lc]; s < ce[lc]; ++s) {
-      const double* o = seg_slot(const_cast<double*>(out), const_cast<double*>(scratch), g, s,
-                                 nseg, skip, PP);
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  const int s0 = cs[lc], s1 = ce[lc];
+  // all of a segment's loads in flight before the adds; the next segment's issued first
+  double nx[4];
+  auto fetch = [&](int s) {
+    const double* o = seg_slot(const_cast<double*>(out), const_cast<double*>(scratch), g, s,
+                               nseg, skip, PP);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
-        if (tile_upper(I, J, i, j, r, c, P)) acc[q] += o[(int64_t)i * P + j];
-      }
+    for (int q = 0; q < 4; ++q) {
+      const int i = min(I * 32 + r0 + 8 * q, P - 1), j = min(J * 32 + c, P - 1);
+      nx[q] = o[(int64_t)i * P + j];
     }
-    double* d = tot + (int64_t)slot[lc] * tstride + (int64_t)g * PP;
+  };
+  if (s0 < s1) fetch(s0);
+  for (int s = s0; s < s1; ++s) {
+    double cur[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cur[q] = nx[q];
+    if (s + 1 < s1) fetch(s + 1);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
-      if (tile_upper(I, J, i, j, r, c, P)) d[(int64_t)i * P + j] = acc[q];
+      if (tile_upper(I, J, i, j, r, c, P)) acc[q] += cur[q];
     }
+  }
+  double* d = tot + (int64_t)slot[lc] * tstride + (int64_t)g * PP;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
+    if (tile_upper(I, J, i, j, r, c, P)) d[(int64_t)i * P + j] = acc[q];
   }
 }
 
 // windows: E = fold(tot[sb[k]]), P_0 = E; chunk c with local year segments [ys[c], ye[c]):
 // acc = P_c, acc += seg s, out[s - skip] = acc (full, mirrored); P_{c+1} = P_c + tot[sy[c]].
-// Chunks past the last local one are not visited.
+// One workgroup per (tile, g, chunk ch <= clast): it forms P_ch itself by the same left fold
+// (E, then + tot[sy[0]], ..., + tot[sy[ch - 1]]), so every chunk's windows run in parallel
+// and the bits are those of the sequential walk.
 __global__ __launch_bounds__(256) void wsum_chunk_prefix_kernel(
     int P, int nseg, int skip, double* __restrict__ out, double* __restrict__ scratch, int C,
     const int* __restrict__ sb, const int* __restrict__ sy, const int* __restrict__ ys,
     const int* __restrict__ ye, const double* __restrict__ tot, int64_t tstride, int clast) {
   __shared__ double Ts[32][33];
-  const int g = blockIdx.y;
+  const int g = blockIdx.y, ch = blockIdx.z;
+  const int s0 = ys[ch], s1 = ye[ch];
+  if (s0 >= s1) return;                         // no local windows in this chunk
   int tile = blockIdx.x;
   const int nt = (P + 31) / 32;
   int I = 0;
@@ -291,48 +311,54 @@ __global__ __launch_bounds__(256) void wsum_chunk_prefix_kernel(
   const int64_t PP = (int64_t)P * P;
   const int t = threadIdx.x, c = t & 31, r0 = t >> 5;
   const double* tg = tot + (int64_t)g * PP;     // slot k at tg + k * tstride
-  double pc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int k = 0; k < C; ++k) {
-    const double* o = tg + (int64_t)sb[k] * tstride;
+  // the C + ch prefix tiles, loaded together, then added in the canonical order
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  const int nk = C + ch;
+  for (int k0 = 0; k0 < nk; k0 += 8) {
+    double v[8][4];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = min(k0 + u, nk - 1);
+      const double* o = tg + (int64_t)(k < C ? sb[k] : sy[k - C]) * tstride;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = min(I * 32 + r0 + 8 * q, P - 1), j = min(J * 32 + c, P - 1);
+        v[u][q] = o[(int64_t)i * P + j];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (k0 + u < nk) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
+          if (tile_upper(I, J, i, j, r, c, P)) acc[q] += v[u][q];
+        }
+      }
+    }
+  }
+  for (int s = s0; s < s1; ++s) {
+    const double* o = seg_slot(out, scratch, g, s, nseg, skip, PP);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
-      if (tile_upper(I, J, i, j, r, c, P)) pc[q] += o[(int64_t)i * P + j];
+      const double v = tile_upper(I, J, i, j, r, c, P) ? o[(int64_t)i * P + j] : 0.0;
+      acc[q] += v;
+      Ts[r][c] = acc[q];
     }
-  }
-  for (int ch = 0; ch <= clast; ++ch) {
-    double acc[4] = {pc[0], pc[1], pc[2], pc[3]};
-    for (int s = ys[ch]; s < ye[ch]; ++s) {
-      const double* o = seg_slot(out, scratch, g, s, nseg, skip, PP);
+    __syncthreads();
+    if (s >= skip) {
+      double* w = seg_slot(out, scratch, g, s, nseg, skip, PP);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
-        const double v = tile_upper(I, J, i, j, r, c, P) ? o[(int64_t)i * P + j] : 0.0;
-        acc[q] += v;
-        Ts[r][c] = acc[q];
-      }
-      __syncthreads();
-      if (s >= skip) {
-        double* w = seg_slot(out, scratch, g, s, nseg, skip, PP);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int r = r0 + 8 * q;
-          const int i = I * 32 + r, j = J * 32 + c;
-          if (i < P && j < P) w[(int64_t)i * P + j] = (I != J || c >= r) ? Ts[r][c] : Ts[c][r];
-          const int i2 = J * 32 + r, j2 = I * 32 + c;
-          if (I != J && i2 < P && j2 < P) w[(int64_t)i2 * P + j2] = Ts[c][r];
-        }
-      }
-      __syncthreads();
-    }
-    if (ch < clast) {
-      const double* o = tg + (int64_t)sy[ch] * tstride;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
-        if (tile_upper(I, J, i, j, r, c, P)) pc[q] += o[(int64_t)i * P + j];
+        const int r = r0 + 8 * q;
+        const int i = I * 32 + r, j = J * 32 + c;
+        if (i < P && j < P) w[(int64_t)i * P + j] = (I != J || c >= r) ? Ts[r][c] : Ts[c][r];
+        const int i2 = J * 32 + r, j2 = I * 32 + c;
+        if (I != J && i2 < P && j2 < P) w[(int64_t)i2 * P + j2] = Ts[c][r];
       }
     }
+    __syncthreads();
   }
 }
 
@@ -401,7 +427,7 @@ extern "C" hipError_t pfml_wsum_chunk_totals(const double* X, int P, int T, int 
                      seg_stop, nseg, skip, out, scratch);
   if (nlc > 0) {
     const int nt = (P + 31) / 32;
-    hipLaunchKernelGGL(wsum_chunk_totals_kernel, dim3(nt * (nt + 1) / 2, G), dim3(256), 0, st, P,
+    hipLaunchKernelGGL(wsum_chunk_totals_kernel, dim3(nt * (nt + 1) / 2, G, nlc), dim3(256), 0, st, P,
                        nseg, skip, out, scratch, nlc, idx, idx + nlc, idx + 2 * nlc, tot,
                        tstride);
   }
@@ -415,7 +441,7 @@ extern "C" hipError_t pfml_wsum_chunk_prefix(int P, int G, int nseg, int skip, d
                                              hipStream_t st) {
   if (nseg <= 0 || P <= 0 || G <= 0 || clast < 0) return hipSuccess;
   const int nt = (P + 31) / 32;
-  hipLaunchKernelGGL(wsum_chunk_prefix_kernel, dim3(nt * (nt + 1) / 2, G), dim3(256), 0, st, P,
+  hipLaunchKernelGGL(wsum_chunk_prefix_kernel, dim3(nt * (nt + 1) / 2, G, clast + 1), dim3(256), 0, st, P,
                      nseg, skip, out, scratch, C, cidx, cidx + C, cidx + 2 * C, cidx + 3 * C, tot,
                      tstride, clast);
   return hipGetLastError();

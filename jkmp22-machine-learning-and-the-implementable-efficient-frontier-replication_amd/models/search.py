@@ -329,10 +329,24 @@ def window_sums(reals: "PfmlReals", su: dict) -> tuple[torch.Tensor, torch.Tenso
     from ..ops.ridge import chunk_totals, chunk_windows
     X, R = reals.denom, reals.r_tilde.contiguous()
     totD, totR, scratch = chunk_totals(X, R, su)
-    if dist_env().is_dist:
+    env = dist_env()
+    if env.is_dist:
         # [nlc, G, ...] chunk-major: one known-size all-gather of every rank's chunk totals
         totD = coll.all_gather_known(totD, [c for c in su["counts"]])
         totR = coll.all_gather_known(totR, [c for c in su["counts"]])
+    elif env.world_size > 1:
+        # one-process rehearsal of a rank of a W-rank run (tools/bench_shard.py: collectives
+        # are no-ops): the gathered layout with this rank's totals in its own slots and zeros
+        # for the other ranks' - the kernels see the real shapes; the sums lack the other
+        # ranks' chunks, so only the timing is meaningful
+        off = int(sum(su["counts"][:env.rank]))
+        fullD = torch.zeros((int(sum(su["counts"])),) + tuple(totD.shape[1:]), dtype=totD.dtype,
+                            device=totD.device)
+        fullR = torch.zeros((int(sum(su["counts"])),) + tuple(totR.shape[1:]), dtype=totR.dtype,
+                            device=totR.device)
+        fullD[off:off + totD.shape[0]] = totD
+        fullR[off:off + totR.shape[0]] = totR
+        totD, totR = fullD, fullR
     return chunk_windows(X, R, su, totD, totR, scratch)
 
 

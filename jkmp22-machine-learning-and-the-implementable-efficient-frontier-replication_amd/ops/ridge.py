@@ -184,6 +184,12 @@ def chunk_windows(X: torch.Tensor, R: torch.Tensor, su: dict, totD: torch.Tensor
     nseg, skip, nYl, clast = su["nseg"], su["skip"], su["nYl"], su["clast"]
     C = su["layout"].C
     out = bufs["out"]
+    nslot = int(sum(su["counts"]))
+    if totD.shape[0] != nslot or totR.shape[0] != nslot:
+        # the slot map addresses the GATHERED totals of every rank (a local-only buffer here
+        # would be read out of bounds by the device kernels)
+        raise ValueError(f"chunk_windows: {totD.shape[0]} chunk totals, the canonical layout "
+                         f"has {nslot} slots (all-gather missing?)")
     Sr = torch.empty((G, nYl, P), dtype=X.dtype, device=X.device)
     if nat.is_device(X):
         st, sp, idx, cidx = su["dev_idx"]

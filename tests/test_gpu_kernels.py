@@ -136,7 +136,45 @@ def test_ridge_grid_production_size(gpu):
     ref = ridge_grid(SD, Sr, src, nn, sc, lv)
     out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
     rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
-    assert rel < 1e-8, rel
+    assert rel < 1e-10, rel
+
+
+def test_ridge_grid_production_rank_deficient(gpu):
+    """Production size (n = 513, 257) with a RANK-DEFICIENT, indefinite window sum (400
+    observations, rank 401 < 513): every lambda > 0 matches the fp64 pivoted LU (torch.linalg.solve) to 1e-10;
+    at lambda = 0 the system is singular, the banded Cholesky fails and the device repairs it
+    by the pivoted banded LU (PFML_Search_Coef.py:131-133 semantics).  A singular system has
+    no unique solution to compare, so the lambda = 0 betas are held to np.linalg.solve's own
+    guarantee instead: backward stability, |(Dbar) b - rbar| <= 1e-12 (|Dbar| |b| + |rbar|),
+    with rbar in the range of Dbar (a consistent system)."""
+    from pfml.ops import ridge as rg
+    P = 513
+    X = _rand(1, 400, P, seed=23)
+    SD = X.transpose(1, 2) @ X / 400
+    # one null direction turned negative: Dbar' = Dbar - 0.7 v v' stays singular (112 zero
+    # eigenvalues) and is indefinite, so the banded Cholesky MUST fail at lambda = 0 (and
+    # for lambda < 0.7) and every such system goes through the device repair
+    e, V = torch.linalg.eigh(SD[0])
+    SD[0] = SD[0] - 0.7 * torch.outer(V[:, 0], V[:, 0])
+    SD[0] = 0.5 * (SD[0] + SD[0].T)
+    w = _rand(1, P, seed=24)
+    Sr = (SD @ w.unsqueeze(-1)).squeeze(-1)            # consistent at lambda = 0
+    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
+    src, nn, sc = np.array([0, 0]), np.array([513, 257]), np.array([1.0, 1.0])
+    ref = rg.ridge_grid(SD, Sr, src, nn, sc, lv)
+    out = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
+    assert rg.repairs_done() >= 1                        # the n = 513 lambda = 0 system
+    rel = ((out[:, 1:] - ref[:, 1:]).norm(dim=-1) / ref[:, 1:].norm(dim=-1)).max().item()
+    assert rel < 1e-10, rel
+    # n = 257 (leading block): lambda = 0 is regular here -> plain comparison
+    r257 = ((out[1, 0] - ref[1, 0]).norm() / ref[1, 0].norm()).item()
+    assert r257 < 1e-10, r257
+    b = out[0, 0, :P]
+    assert torch.isfinite(b).all()
+    D0, r0 = SD[0], Sr[0]
+    res = (D0 @ b - r0).norm().item()
+    scale = (torch.linalg.matrix_norm(D0, ord=2) * b.norm() + r0.norm()).item()
+    assert res <= 1e-12 * scale, (res, scale)
 
 
 def test_quadform_utilities(gpu):
@@ -224,7 +262,45 @@ def test_ridge_variants_agree(gpu, variant, monkeypatch):
     ref = ridge_grid(SD, Sr, src, nn, sc, lv)
     out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
     rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
-    assert rel < 1e-8, rel
+    assert rel < 1e-10, rel
+
+
+def test_ridge_grid_production_rank_deficient(gpu):
+    """Production size (n = 513, 257) with a RANK-DEFICIENT, indefinite window sum (400
+    observations, rank 401 < 513): every lambda > 0 matches the fp64 pivoted LU (torch.linalg.solve) to 1e-10;
+    at lambda = 0 the system is singular, the banded Cholesky fails and the device repairs it
+    by the pivoted banded LU (PFML_Search_Coef.py:131-133 semantics).  A singular system has
+    no unique solution to compare, so the lambda = 0 betas are held to np.linalg.solve's own
+    guarantee instead: backward stability, |(Dbar) b - rbar| <= 1e-12 (|Dbar| |b| + |rbar|),
+    with rbar in the range of Dbar (a consistent system)."""
+    from pfml.ops import ridge as rg
+    P = 513
+    X = _rand(1, 400, P, seed=23)
+    SD = X.transpose(1, 2) @ X / 400
+    # one null direction turned negative: Dbar' = Dbar - 0.7 v v' stays singular (112 zero
+    # eigenvalues) and is indefinite, so the banded Cholesky MUST fail at lambda = 0 (and
+    # for lambda < 0.7) and every such system goes through the device repair
+    e, V = torch.linalg.eigh(SD[0])
+    SD[0] = SD[0] - 0.7 * torch.outer(V[:, 0], V[:, 0])
+    SD[0] = 0.5 * (SD[0] + SD[0].T)
+    w = _rand(1, P, seed=24)
+    Sr = (SD @ w.unsqueeze(-1)).squeeze(-1)            # consistent at lambda = 0
+    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
+    src, nn, sc = np.array([0, 0]), np.array([513, 257]), np.array([1.0, 1.0])
+    ref = rg.ridge_grid(SD, Sr, src, nn, sc, lv)
+    out = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
+    assert rg.repairs_done() >= 1                        # the n = 513 lambda = 0 system
+    rel = ((out[:, 1:] - ref[:, 1:]).norm(dim=-1) / ref[:, 1:].norm(dim=-1)).max().item()
+    assert rel < 1e-10, rel
+    # n = 257 (leading block): lambda = 0 is regular here -> plain comparison
+    r257 = ((out[1, 0] - ref[1, 0]).norm() / ref[1, 0].norm()).item()
+    assert r257 < 1e-10, r257
+    b = out[0, 0, :P]
+    assert torch.isfinite(b).all()
+    D0, r0 = SD[0], Sr[0]
+    res = (D0 @ b - r0).norm().item()
+    scale = (torch.linalg.matrix_norm(D0, ord=2) * b.norm() + r0.norm()).item()
+    assert res <= 1e-12 * scale, (res, scale)
 
 
 @pytest.mark.parametrize("mode", ["single", "multi", "fused"])
@@ -243,7 +319,45 @@ def test_band_reduction_modes(gpu, mode, monkeypatch):
     ref = ridge_grid(SD, Sr, src, nn, sc, lv)
     out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
     rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
-    assert rel < 1e-8, rel
+    assert rel < 1e-10, rel
+
+
+def test_ridge_grid_production_rank_deficient(gpu):
+    """Production size (n = 513, 257) with a RANK-DEFICIENT, indefinite window sum (400
+    observations, rank 401 < 513): every lambda > 0 matches the fp64 pivoted LU (torch.linalg.solve) to 1e-10;
+    at lambda = 0 the system is singular, the banded Cholesky fails and the device repairs it
+    by the pivoted banded LU (PFML_Search_Coef.py:131-133 semantics).  A singular system has
+    no unique solution to compare, so the lambda = 0 betas are held to np.linalg.solve's own
+    guarantee instead: backward stability, |(Dbar) b - rbar| <= 1e-12 (|Dbar| |b| + |rbar|),
+    with rbar in the range of Dbar (a consistent system)."""
+    from pfml.ops import ridge as rg
+    P = 513
+    X = _rand(1, 400, P, seed=23)
+    SD = X.transpose(1, 2) @ X / 400
+    # one null direction turned negative: Dbar' = Dbar - 0.7 v v' stays singular (112 zero
+    # eigenvalues) and is indefinite, so the banded Cholesky MUST fail at lambda = 0 (and
+    # for lambda < 0.7) and every such system goes through the device repair
+    e, V = torch.linalg.eigh(SD[0])
+    SD[0] = SD[0] - 0.7 * torch.outer(V[:, 0], V[:, 0])
+    SD[0] = 0.5 * (SD[0] + SD[0].T)
+    w = _rand(1, P, seed=24)
+    Sr = (SD @ w.unsqueeze(-1)).squeeze(-1)            # consistent at lambda = 0
+    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
+    src, nn, sc = np.array([0, 0]), np.array([513, 257]), np.array([1.0, 1.0])
+    ref = rg.ridge_grid(SD, Sr, src, nn, sc, lv)
+    out = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
+    assert rg.repairs_done() >= 1                        # the n = 513 lambda = 0 system
+    rel = ((out[:, 1:] - ref[:, 1:]).norm(dim=-1) / ref[:, 1:].norm(dim=-1)).max().item()
+    assert rel < 1e-10, rel
+    # n = 257 (leading block): lambda = 0 is regular here -> plain comparison
+    r257 = ((out[1, 0] - ref[1, 0]).norm() / ref[1, 0].norm()).item()
+    assert r257 < 1e-10, r257
+    b = out[0, 0, :P]
+    assert torch.isfinite(b).all()
+    D0, r0 = SD[0], Sr[0]
+    res = (D0 @ b - r0).norm().item()
+    scale = (torch.linalg.matrix_norm(D0, ord=2) * b.norm() + r0.norm()).item()
+    assert res <= 1e-12 * scale, (res, scale)
 
 
 @pytest.mark.parametrize("n_obs", [700, 90])
@@ -321,7 +435,45 @@ def test_band_panel_qr(gpu, qr, mode, n_obs, monkeypatch):
     ref = ridge_grid(SD, Sr, src, nn, sc, lv)
     out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
     rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
-    assert rel < 1e-8, rel
+    assert rel < 1e-10, rel
+
+
+def test_ridge_grid_production_rank_deficient(gpu):
+    """Production size (n = 513, 257) with a RANK-DEFICIENT, indefinite window sum (400
+    observations, rank 401 < 513): every lambda > 0 matches the fp64 pivoted LU (torch.linalg.solve) to 1e-10;
+    at lambda = 0 the system is singular, the banded Cholesky fails and the device repairs it
+    by the pivoted banded LU (PFML_Search_Coef.py:131-133 semantics).  A singular system has
+    no unique solution to compare, so the lambda = 0 betas are held to np.linalg.solve's own
+    guarantee instead: backward stability, |(Dbar) b - rbar| <= 1e-12 (|Dbar| |b| + |rbar|),
+    with rbar in the range of Dbar (a consistent system)."""
+    from pfml.ops import ridge as rg
+    P = 513
+    X = _rand(1, 400, P, seed=23)
+    SD = X.transpose(1, 2) @ X / 400
+    # one null direction turned negative: Dbar' = Dbar - 0.7 v v' stays singular (112 zero
+    # eigenvalues) and is indefinite, so the banded Cholesky MUST fail at lambda = 0 (and
+    # for lambda < 0.7) and every such system goes through the device repair
+    e, V = torch.linalg.eigh(SD[0])
+    SD[0] = SD[0] - 0.7 * torch.outer(V[:, 0], V[:, 0])
+    SD[0] = 0.5 * (SD[0] + SD[0].T)
+    w = _rand(1, P, seed=24)
+    Sr = (SD @ w.unsqueeze(-1)).squeeze(-1)            # consistent at lambda = 0
+    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
+    src, nn, sc = np.array([0, 0]), np.array([513, 257]), np.array([1.0, 1.0])
+    ref = rg.ridge_grid(SD, Sr, src, nn, sc, lv)
+    out = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
+    assert rg.repairs_done() >= 1                        # the n = 513 lambda = 0 system
+    rel = ((out[:, 1:] - ref[:, 1:]).norm(dim=-1) / ref[:, 1:].norm(dim=-1)).max().item()
+    assert rel < 1e-10, rel
+    # n = 257 (leading block): lambda = 0 is regular here -> plain comparison
+    r257 = ((out[1, 0] - ref[1, 0]).norm() / ref[1, 0].norm()).item()
+    assert r257 < 1e-10, r257
+    b = out[0, 0, :P]
+    assert torch.isfinite(b).all()
+    D0, r0 = SD[0], Sr[0]
+    res = (D0 @ b - r0).norm().item()
+    scale = (torch.linalg.matrix_norm(D0, ord=2) * b.norm() + r0.norm()).item()
+    assert res <= 1e-12 * scale, (res, scale)
 
 
 @pytest.mark.parametrize("fmt", ["bf16", "fp8"])
@@ -544,3 +696,63 @@ def test_validation_rank_ties_zeros_infs(gpu):
         _, _, r0 = validation_scores(obj, 1, compat)
         _, _, r1 = validation_scores(obj.to(gpu), 1, compat)
         assert torch.equal(r0.nan_to_num(-1), r1.cpu().nan_to_num(-1))
+
+
+def _chunked_windows_all_ranks(X, R, months, years, W, dev):
+    """Window sums of every rank of a W-rank run, the all-gather emulated in one process:
+    each rank's chunk totals (its local months only), concatenated in canonical slot order,
+    then each rank's windows.  Returns {global hp-year index: (SD, Sr)}."""
+    from pfml.models.search import _search_setup, local_month_rows
+    from pfml.ops.ridge import chunk_totals, chunk_windows
+    G, T, P, _ = X.shape
+    lv = np.array([0.0, 1.0])
+    sus, tots = [], []
+    for r in range(W):
+        rows = local_month_rows(months, years, W, r)
+        Xr = X[:, rows].contiguous().to(dev)
+        Rr = R[:, rows].contiguous().to(dev)
+        su = _search_setup(months, years, [16], G, len(rows), W, r,
+                           torch.device(dev) if dev != "cpu" else None, lv, rows)
+        totD, totR, bufs = chunk_totals(Xr, Rr, su)
+        sus.append((su, Xr, Rr, bufs))
+        tots.append((totD, totR))
+    allD = torch.cat([t[0] for t in tots])
+    allR = torch.cat([t[1] for t in tots])
+    out = {}
+    for su, Xr, Rr, bufs in sus:
+        SD, Sr = chunk_windows(Xr, Rr, su, allD, allR, bufs)
+        for k, y in enumerate(su["yl"]):
+            out[int(y)] = (SD[:, k].cpu(), Sr[:, k].cpu())
+    return out
+
+
+def test_chunked_window_sums_world_bitwise(gpu):
+    """Canonical chunked window sums (csrc/segsum.hip chunk kernels): on the device every
+    hp-year window is BITWISE the same for a 1, 2, 3 and 4-rank sharding, and matches the
+    CPU folds to rounding."""
+    from pfml.models.search import make_plan
+    from pfml.utils.dates import mi_from_ym
+    G, P = 2, 37
+    months = np.arange(mi_from_ym(1990, 0), mi_from_ym(2012, 11) + 1, dtype=np.int64)
+    years = np.arange(1998, 2012)
+    T = len(months)
+    X = _rand(G, T, P, P, seed=91)
+    X = X + X.transpose(-1, -2)
+    R = _rand(G, T, P, seed=92)
+    ref = _chunked_windows_all_ranks(X, R, months, years, 1, gpu)
+    cpu = _chunked_windows_all_ranks(X, R, months, years, 1, "cpu")
+    assert sorted(ref) == list(range(len(years)))
+    for y in ref:
+        assert torch.allclose(ref[y][0], cpu[y][0], rtol=1e-12, atol=1e-11)
+        assert torch.allclose(ref[y][1], cpu[y][1], rtol=1e-12, atol=1e-11)
+        assert torch.equal(ref[y][0], ref[y][0].transpose(-1, -2))
+    plan = make_plan(months, years)
+    last = int(plan.seg_stop[len(years) - 1])
+    full = X[:, :last].sum(1)
+    assert torch.allclose(ref[len(years) - 1][0], full, rtol=1e-12, atol=1e-11)
+    for W in (2, 3, 4):
+        got = _chunked_windows_all_ranks(X, R, months, years, W, gpu)
+        assert sorted(got) == sorted(ref)
+        for y in ref:
+            assert torch.equal(got[y][0], ref[y][0]), (W, y)
+            assert torch.equal(got[y][1], ref[y][1]), (W, y)

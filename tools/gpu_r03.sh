@@ -61,6 +61,19 @@ for step in ${MODE//,/ }; do
     shard)
       PFML_SHARD_GRAPH=1 timeout -k 10 300 python tools/bench_shard.py 1,2,4,8 > $OUT/shard.json 2> $OUT/shard.err
       rc=$?; cat $OUT/shard.json; if [ $rc -ne 0 ]; then tail -3 $OUT/shard.err; exit $rc; fi ;;
+    shardserial)
+      # fault hunt: serialised launches, so a memory fault surfaces at the launching call
+      AMD_SERIALIZE_KERNEL=3 PFML_SHARD_GRAPH=1 timeout -k 10 300 python tools/bench_shard.py 1,2,4,8 2 > $OUT/shard_serial.json 2> $OUT/shard_serial.err
+      rc=$?; cat $OUT/shard_serial.json; if [ $rc -ne 0 ]; then grep -v "^frame" $OUT/shard_serial.err | tail -25; exit $rc; fi ;;
+    ktest)
+      # targeted GPU tests: PFML_KTEST = pytest -k expression
+      timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "${PFML_KTEST}" > $OUT/pytest_k.log 2>&1
+      rc=$?; tail -3 $OUT/pytest_k.log
+      if [ $rc -ne 0 ]; then grep -E "^E |FAILED" $OUT/pytest_k.log | head -20; exit $rc; fi ;;
+    diag)
+      # staged fault hunt: PFML_DIAG = options of tools/diag_shard.py (setdev, env)
+      timeout -k 10 300 python tools/diag_shard.py ${PFML_DIAG} > $OUT/diag_${PFML_DIAG// /_}.log 2>&1
+      rc=$?; grep -v "^frame" $OUT/diag_${PFML_DIAG// /_}.log | tail -30; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
