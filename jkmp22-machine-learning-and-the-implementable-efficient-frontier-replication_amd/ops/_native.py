@@ -34,7 +34,7 @@ def _declare_hip(lib):
     lib.pfml_ridge_work_doubles.restype = L
     lib.pfml_ridge_cell_desc_size.restype = I
     lib.pfml_ridge_band_nmax.restype = I
-    lib.pfml_quadform.argtypes = [P, L, P, P, L, P, I, P, I, I, P, P, P]
+    lib.pfml_quadform.argtypes = [P, L, P, P, L, P, I, P, I, I, I, P, P, P]
     lib.pfml_quadform.restype = I
     lib.pfml_quadform_job_desc_size.restype = I
     lib.pfml_quadform_rows_per_tile.restype = I

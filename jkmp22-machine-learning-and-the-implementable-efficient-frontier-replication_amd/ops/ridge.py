@@ -501,7 +501,8 @@ def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell,
     grid's shape (cells, jobs, P, L), so repeated grid searches (every step of a run, every
     benchmark step) reuse the uploaded device copies and skip all host planning.  Each group's
     cells / jobs write straight into the full beta / obj arrays (global out offsets)."""
-    key = (P, L, str(dev), split, cell_src.tobytes(), cell_n.tobytes(), cell_scale.tobytes(),
+    key = (P, L, str(dev), split, os.environ.get("PFML_QUAD_MM", "1"),
+           cell_src.tobytes(), cell_n.tobytes(), cell_scale.tobytes(),
            job_cell.tobytes(), job_month.tobytes(), job_n.tobytes(),
            None if big_key is None else big_key.tobytes())
     hit = _UTIL_PLANS.get(key)
@@ -669,16 +670,43 @@ def quad_plan(P: int, L: int, Pb: int, job_cell, job_month, job_n, job_out=None)
                      else np.asarray(job_out, np.int64)) * L
     desc["n"] = job_n.astype(np.int32)
     desc["ptile0"] = pt0
-    # tiles longest-first (row tile 0 of every job, then row tile 1, ...): the triangular K
-    # loop of row tile rt is ~(n - 64 rt) long, so the launch ends on the short tiles;
-    # entry = job << 5 | rt (the kernel writes partial slot ptile0 + rt)
     if nj and int(ntile.max()) > 32:
         raise ValueError("quad_plan: more than 32 row tiles per job (n > 32 * rows)")
-    jj = np.repeat(np.arange(nj, dtype=np.int64), ntile)
-    rt = np.arange(len(jj), dtype=np.int64) - np.repeat(pt0.astype(np.int64), ntile)
-    order = np.lexsort((jj, rt))
-    tile_job = ((jj[order] << 5) | rt[order]).astype(np.int32)
-    return {"desc": desc, "tile_job": tile_job, "nj": nj}
+    # a tile covers `mm` jobs of ONE cell (same beta, same n: its validation months), so the
+    # staged beta K-tiles feed mm D tiles; an odd job out gets -1 in the spare entries
+    # (2 months per tile: measured 5.90 vs 5.78 ms per grid step on MI355X - fewer resident
+    # workgroups cost more than the halved beta traffic saves - so 1 is the default)
+    mm = 2 if os.environ.get("PFML_QUAD_MM", "1") == "2" else 1
+    jc = np.asarray(job_cell, np.int64)
+    # jobs grouped by (cell, n), stable: a tile's jobs share beta AND the row / K extent
+    by_cell = np.lexsort((np.arange(nj), job_n, jc))
+    key = jc * 65536 + job_n.astype(np.int64)
+    groups = []
+    i = 0
+    while i < nj:
+        c = key[by_cell[i]]
+        k = i
+        while k < nj and key[by_cell[k]] == c and k - i < mm:
+            k += 1
+        groups.append(by_cell[i:k])
+        i = k
+    ng = len(groups)
+    gj = np.full((ng, mm), -1, dtype=np.int64)
+    for gi, grp in enumerate(groups):
+        gj[gi, :len(grp)] = grp
+    gnt = ntile[gj[:, 0]] if ng else np.zeros(0, np.int64)
+    # tiles longest-first (row tile 0 of every group, then row tile 1, ...): the triangular K
+    # loop of row tile rt is ~(n - 64 rt) long, so the launch ends on the short tiles;
+    # entry = job << 5 | rt (the kernel writes partial slot ptile0 + rt of each live job)
+    gg = np.repeat(np.arange(ng, dtype=np.int64), gnt)
+    g0 = np.concatenate([[0], np.cumsum(gnt)[:-1]]).astype(np.int64) if ng else np.zeros(0, np.int64)
+    rt = np.arange(len(gg), dtype=np.int64) - np.repeat(g0, gnt)
+    order = np.lexsort((gg, rt))
+    gg, rt = gg[order], rt[order]
+    jobs_t = gj[gg]                                      # [ntiles, mm]
+    tile_job = np.where(jobs_t >= 0, (jobs_t << 5) | rt[:, None], -1).astype(np.int32).reshape(-1)
+    return {"desc": desc, "tile_job": tile_job, "nj": nj, "ntiles": len(gg),
+            "nslots": int(ntile.sum()), "mm": mm}
 
 
 def quad_launch(plan: dict, d_desc: torch.Tensor, d_tj: torch.Tensor, D: torch.Tensor,
@@ -687,10 +715,11 @@ def quad_launch(plan: dict, d_desc: torch.Tensor, d_tj: torch.Tensor, D: torch.T
         return
     P = D.shape[-1]
     L, Pb = beta.shape[1], beta.shape[2]
-    nt = len(plan["tile_job"])
-    partial = torch.empty((nt, L), dtype=torch.float64, device=D.device)
+    nt = plan["ntiles"]
+    partial = torch.empty((plan["nslots"], L), dtype=torch.float64, device=D.device)
     nat.check(nat.hip_lib().pfml_quadform(D.data_ptr(), P, R.data_ptr(), beta.data_ptr(), Pb,
-                                          d_desc.data_ptr(), plan["nj"], d_tj.data_ptr(), nt, L,
+                                          d_desc.data_ptr(), plan["nj"], d_tj.data_ptr(), nt,
+                                          plan["mm"], L,
                                           partial.data_ptr(), obj.data_ptr(),
                                           nat.stream_of(D)), "pfml_quadform")
 

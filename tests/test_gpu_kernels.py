@@ -756,3 +756,24 @@ def test_chunked_window_sums_world_bitwise(gpu):
         for y in ref:
             assert torch.equal(got[y][0], ref[y][0]), (W, y)
             assert torch.equal(got[y][1], ref[y][1]), (W, y)
+
+
+def test_quadform_two_months_bitwise(gpu, monkeypatch):
+    """Two validation months per workgroup (shared beta tiles) give BITWISE the utilities of
+    one month per workgroup (same per-month MFMA order), incl. an odd job out and n < 64."""
+    from pfml.ops.ridge import quadform_utilities
+    P, L = 130, 101
+    D = _spd_stack(7, P, n_obs=150, seed=95) / 150
+    R = _rand(7, P, seed=96)
+    beta = _rand(3, L, P, seed=97)
+    jc = np.array([0, 0, 0, 1, 1, 2, 2, 2, 2])
+    jm = np.array([0, 1, 2, 3, 4, 5, 6, 0, 1])
+    jn = np.array([130, 130, 130, 65, 65, 33, 33, 33, 33])
+    args = (D.to(gpu), R.to(gpu), beta.to(gpu), jc, jm, jn)
+    monkeypatch.setenv("PFML_QUAD_MM", "1")
+    one = quadform_utilities(*args).cpu()
+    monkeypatch.setenv("PFML_QUAD_MM", "2")
+    two = quadform_utilities(*args).cpu()
+    assert torch.equal(one, two)
+    ref = quadform_utilities(D, R, beta, jc, jm, jn)
+    assert torch.allclose(two, ref, rtol=1e-11, atol=1e-11)

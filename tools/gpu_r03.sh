@@ -16,6 +16,9 @@ for step in ${MODE//,/ }; do
     peak)
       timeout -k 10 120 ./tools/micro/mfma_f64_peak > $OUT/mfma_peak.json 2>&1
       rc=$?; cat $OUT/mfma_peak.json; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    dgemm)
+      timeout -k 10 200 python tools/micro/dgemm_rate.py > $OUT/dgemm_rate.json 2>&1
+      rc=$?; tail -4 $OUT/dgemm_rate.json; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     suite)
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
       rc=$?; tail -2 $OUT/pytest_gpu.log

@@ -129,6 +129,47 @@ __global__ __launch_bounds__(256) void mfma_ops_loop(double* out, WaveRec* rec, 
   }
 }
 
+// VGPR-form MFMA through inline asm ("+v": the accumulators stay in VGPRs for the whole
+// loop).  The builtin variants above were compiled to the AGPR form with every accumulator
+// copied VGPR -> AGPR before and AGPR -> VGPR after each MFMA group (8 v_accvgpr moves per
+// MFMA, llvm-objdump of this file): they measured those moves (~104 cycles / MFMA), not the
+// MFMA pipe.  This loop has no other instruction between the MFMAs.
+template <int NACC>
+__global__ __launch_bounds__(256) void mfma_vgpr_loop(double* out, WaveRec* rec, int iters) {
+  double4_t acc[NACC];
+  double av[NACC], bv[NACC];
+#pragma unroll
+  for (int q = 0; q < NACC; ++q) {
+    acc[q] = double4_t{0.25, -0.5, 0.125, 1.0};
+    av[q] = 1.0 + ((threadIdx.x + 7 * q) * 2654435761u % 1000) * 1e-4;
+    bv[q] = -1.0 + ((blockIdx.x + 3 * q) * 40503u % 977) * 1e-4;
+  }
+  const long long t0 = (long long)__builtin_amdgcn_s_memtime();
+  const long long r0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int q = 0; q < NACC; ++q)
+      asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(acc[q]) : "v"(av[q]), "v"(bv[q]));
+  }
+  const long long t1 = (long long)__builtin_amdgcn_s_memtime();
+  const long long r1 = (long long)__builtin_amdgcn_s_memrealtime();
+  asm volatile("s_nop 15" ::: "memory");
+  double s = 0;
+#pragma unroll
+  for (int q = 0; q < NACC; ++q) s += acc[q][0] + acc[q][1] + acc[q][2] + acc[q][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+  if ((threadIdx.x & 63) == 0) {
+    WaveRec w;
+    w.hwid = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    w.xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    w.t0 = t0;
+    w.t1 = t1;
+    w.r0 = r0;
+    w.r1 = r1;
+    rec[blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64] = w;
+  }
+}
+
 __global__ __launch_bounds__(256) void fma_loop(double* out, int iters) {
   double x0 = threadIdx.x, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4, x5 = x0 + 5, x6 = x0 + 6, x7 = x0 + 7;
   const double m = 0.999999, c = 1e-7;
@@ -209,23 +250,21 @@ int main() {
            name, wps, simd.size(), maxw, med, cpm.front(), ghz, simd_tf, ev_tf);
   };
   for (int wps : {1, 2, 4}) {
-    run(mfma_loop<4>, 4, wps, "mfma_acc4");
-    run(mfma_loop<8>, 8, wps, "mfma_acc8");
-    run(mfma_loop<16>, 16, wps, "mfma_acc16");
-    run(mfma_agpr_loop<4>, 4, wps, "mfma_agpr_acc4");
-    run(mfma_agpr_loop<8>, 8, wps, "mfma_agpr_acc8");
-    run(mfma_ops_loop<4>, 4, wps, "mfma_ops_acc4");
-    run(mfma_ops_loop<8>, 8, wps, "mfma_ops_acc8");
+    run(mfma_vgpr_loop<4>, 4, wps, "mfma_vgpr_acc4");
+    run(mfma_vgpr_loop<8>, 8, wps, "mfma_vgpr_acc8");
+    run(mfma_vgpr_loop<16>, 16, wps, "mfma_vgpr_acc16");
   }
+  // the builtin forms (AGPR shuffles around every MFMA group, see mfma_vgpr_loop): kept as the
+  // record of what rounds 1-2 measured
+  run(mfma_loop<8>, 8, 4, "builtin_acc8");
+  run(mfma_ops_loop<8>, 8, 4, "builtin_ops_acc8");
   // partial chip (1/8 and 1/2 of the CUs busy): is the full-chip rate a pipe limit or a
   // chip-level power / current limit?
   for (int frac : {8, 2}) {
     ncu_run = ncu / frac;
     char nm[64];
-    snprintf(nm, sizeof(nm), "part%d_ops_acc8", frac);
-    run(mfma_ops_loop<8>, 8, 4, nm);
-    snprintf(nm, sizeof(nm), "part%d_acc8", frac);
-    run(mfma_loop<8>, 8, 4, nm);
+    snprintf(nm, sizeof(nm), "part%d_vgpr_acc8", frac);
+    run(mfma_vgpr_loop<8>, 8, 4, nm);
   }
   ncu_run = ncu;
   const int blocks = maxblocks;
