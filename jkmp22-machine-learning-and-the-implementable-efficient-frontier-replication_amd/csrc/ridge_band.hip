@@ -2108,6 +2108,7 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   const bool fused = band_mode == 3 || (band_mode == 0 && mode && mode[0] == 'f');
   const bool single = band_mode == 1 || (band_mode == 0 && mode && mode[0] == 's') ||
                       (tim != nullptr && band_mode == 0 && !env_multi);
+
   // panel QR: column-by-column Householder (default), or PFML_BAND_QR=cqr: CholeskyQR2 +
   // Householder reconstruction with a per-panel fallback to Householder.  Measured on MI355X
   // the CholeskyQR2 form is 6-10 % slower per reduction (profiles/r01_band_qr_ab.json): its

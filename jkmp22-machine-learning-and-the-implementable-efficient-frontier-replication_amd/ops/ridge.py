@@ -445,6 +445,9 @@ def _side_stream(dev: torch.device, k: int = 0) -> torch.cuda.Stream:
 
 
 BAND_SINGLE, BAND_MULTI, BAND_FUSED = 1, 2, 3
+# One workgroup per cell: the plain kernel (a look-ahead form with panel p+1's QR inside
+# panel p's trailing update measured slower: profiles/r03_band_lookahead_single_wg_ab.json).
+ONE_WG_DEFAULT = BAND_SINGLE
 # Above this many largest-n cells per launch the one-workgroup-per-cell reduction (throughput
 # form, big cells on their own stream) beats the multi-workgroup one (latency form); measured
 # on MI355X, tools/bench_band.py, and in the strong-scaling rehearsal: 53 big cells per rank
@@ -477,7 +480,7 @@ def band_policy(cell_n: np.ndarray) -> tuple[int, bool]:
     import os
     cell_n = np.asarray(cell_n)
     nbig = int((cell_n == cell_n.max()).sum()) if len(cell_n) else 0
-    mode = BAND_MULTI if nbig <= BAND_MULTI_MAX_CELLS else BAND_SINGLE
+    mode = BAND_MULTI if nbig <= BAND_MULTI_MAX_CELLS else ONE_WG_DEFAULT
     env = os.environ.get("PFML_BAND_MODE", "")[:1]
     if env == "s":
         mode = BAND_SINGLE
@@ -517,7 +520,7 @@ def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell,
     elif split and nhy:
         # the first nhy big cells (in cell order) -> multi-workgroup group
         hy = big & (np.cumsum(big) <= nhy)
-        parts = ((big & ~hy, BAND_SINGLE), (hy, BAND_MULTI), (~big, BAND_SINGLE))
+        parts = ((big & ~hy, ONE_WG_DEFAULT), (hy, BAND_MULTI), (~big, ONE_WG_DEFAULT))
     elif split:
         # big cells in the launch's mode; the small ones too (one workgroup per cell: the
         # split form is only taken with the single or the fused reduction)
