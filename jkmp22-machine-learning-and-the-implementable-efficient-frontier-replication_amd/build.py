@@ -84,7 +84,10 @@ def build_runtime(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIBDIR, exist_ok=True)
     cxx = os.environ.get("CXX", "g++")
     tmp = RT_LIB + ".tmp"
-    _run([cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-o", tmp, *srcs], verbose)
+    # runtime/sqlite_io.cpp links the system SQLite (no header in the image: the C-API
+    # prototypes are declared in the source)
+    _run([cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-fopenmp", "-o", tmp, *srcs,
+          "-l:libsqlite3.so.0"], verbose)
     os.replace(tmp, RT_LIB)
     return RT_LIB
 

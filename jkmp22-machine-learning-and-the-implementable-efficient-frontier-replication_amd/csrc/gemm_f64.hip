@@ -220,7 +220,10 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(
       for (int r = 0; r < 4; ++r) {
         const int gi = bm + wm * (BM / 2) + i * 16 + PFML_F64_CROW(lane, r);
         const int gj = bn + wn * (BN / 2) + j * 16 + li;
-        if (ep.sincos) {
+        // (128 x 128 tiles never take the sincos epilogue - the host routes it to 64 x 64 -
+        // so that kernel has no libm call, whose clobbers put its 64-double accumulator
+        // array in scratch: 544 B/lane and 25 TF/s at n = 8192 before)
+        if (BM * BN < 128 * 128 && ep.sincos) {
           if (gi < M && gj < N) {
             double sn, cs;
             sincos(ep.alpha * acc[i][j][r], &sn, &cs);
@@ -323,6 +326,7 @@ extern "C" hipError_t pfml_dgemm_ex(int ta, int tb, int M, int N, int K, int bat
     // better; 128 x 128 for large matrices (tools/bench_gemm2.py, profiles/r02_gemm_*.json)
     cfg = (M >= 1024 && N >= 1024) ? 1 : 3;
   }
+  if (cfg == 1 && h->sincos) cfg = 3;    // the 128 x 128 kernel has no sincos epilogue
   if (cfg == 1)
     return launch_w<128, 128>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, ep, st);
   if (cfg == 2)

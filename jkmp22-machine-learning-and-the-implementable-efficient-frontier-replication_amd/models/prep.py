@@ -248,58 +248,83 @@ def prepare_data(cfg: Config, write: bool = True) -> dict:
     lag["eom"] = lag["eom"] + pd.offsets.MonthEnd(1)
     ld = ld.merge(lag, on=["id", "eom"], how="left")[["id", "eom", "tr_ld0", "eom_ret",
                                                       "ret_ld1", "tr_ld1"]]
-    chars = chars.merge(ld, on=["id", "eom"], how="left")
+    # left merges onto the ~130-column panel as key lookups + column assignments (a merge
+    # would copy the whole panel; the left-join semantics - every chars row kept, in order,
+    # NaN where (id, eom) has no lead row - are the same; (id, eom) is unique in ld)
+    key_c = chars["id"].to_numpy(np.int64) * 100000 + month_index(chars["eom"]).astype(np.int64)
+    key_l = ld["id"].to_numpy(np.int64) * 100000 + month_index(ld["eom"]).astype(np.int64)
+    pos = pd.Index(key_l).get_indexer(key_c)
+    hit = pos >= 0
+    for c in ("tr_ld0", "eom_ret", "ret_ld1", "tr_ld1"):
+        v = ld[c].to_numpy()[np.where(hit, pos, 0)]
+        if c == "eom_ret":
+            chars[c] = pd.Series(v, index=chars.index).where(hit)
+        else:
+            chars[c] = np.where(hit, v, np.nan)
     log.info("Leading Returns Complete")
 
     wealth = wealth_func(pf["wealth"], s["split"]["test_end"], market, risk_free)
     ws = wealth[["eom", "mu_ld1"]].rename(columns={"mu_ld1": "mu_ld0"}).copy()
     ws["eom"] = ws["eom"] + pd.offsets.MonthEnd(1)
-    chars = chars.merge(ws, on="eom", how="left")
+    wpos = pd.Index(ws["eom"]).get_indexer(chars["eom"])
+    chars["mu_ld0"] = np.where(wpos >= 0, ws["mu_ld0"].to_numpy()[np.where(wpos >= 0, wpos, 0)],
+                               np.nan)
     log.info("Wealth Evolution Complete.")
 
-    # ---- screens (Prepare_Data.py:268-309) ----------------------------------------------
+    # ---- screens (Prepare_Data.py:268-309): one keep-mask, the panel filtered once --------
     sc = s["screens"]
-    if sc["nyse_stocks"]:
-        log.info(f"   NYSE stock screen excludes {(chars['crsp_exchcd'] != 1).mean() * 100:.2f}% of the observations")
-        chars = chars[chars["crsp_exchcd"] == 1]
-    n_start, me_start = len(chars), chars["me"].dropna().sum()
+    keep = np.ones(len(chars), dtype=bool)
 
     def screen(mask_keep, label):
-        nonlocal chars
-        log.info(f"   {label} excludes {(~mask_keep).mean() * 100:.2f}% of the observations")
-        chars = chars[mask_keep]
+        m = np.asarray(mask_keep, dtype=bool)
+        log.info(f"   {label} excludes {(~m[keep]).mean() * 100:.2f}% of the observations")
+        keep[:] = keep & m
 
+    if sc["nyse_stocks"]:
+        screen(chars["crsp_exchcd"].to_numpy() == 1, "NYSE stock screen")
+    n_start = int(keep.sum())
+    me = chars["me"].to_numpy(np.float64)
+    me_start = np.nansum(me[keep])
     screen((chars["eom"] >= sc["start"]) & (chars["eom"] <= sc["end"]), "Date screen")
     screen(chars["me"].notna(), "Non-missing me")
     screen(chars["tr_ld1"].notna() & chars["tr_ld0"].notna(), "Valid return req")
     screen(chars["dolvol"].notna() & (chars["dolvol"] > 0), "Non-missing/non-zero dolvol")
     screen(chars["sic"].notna(), "Valid SIC code")
-    avail = chars[features].notna().sum(axis=1)
+    avail = (~np.isnan(chars[features].to_numpy(np.float64))).sum(axis=1)
     min_feat = np.floor(len(features) * sc["feat_pct"])
     screen(avail >= min_feat, f"At least {sc['feat_pct'] * 100}% of feature")
-    log.info(f"In total, the final dataset has {round(len(chars) / n_start * 100, 2)}% of the "
-             f"observations and {round(chars['me'].sum() / me_start * 100, 2)}% of the market cap "
+    log.info(f"In total, the final dataset has {round(int(keep.sum()) / n_start * 100, 2)}% of the "
+             f"observations and {round(np.nansum(me[keep]) / me_start * 100, 2)}% of the market cap "
              f"in the post {sc['start']} data")
+    # the panel in (id, eom) order, filtered: ONE reorder copy (the reference sorts by
+    # (eom, id) for the ranks and back by (id, eom) for the lookback; the ranks below are
+    # computed through a permutation instead)
+    idx = np.nonzero(keep)[0]
+    o = np.lexsort((month_index(chars["eom"].iloc[idx]), chars["id"].to_numpy(np.int64)[idx]))
+    chars = chars.take(idx[o]).reset_index(drop=True)
 
     # ---- percentile ranks + imputation (Prepare_Data.py:324-374) ----------------------
-    chars = chars.sort_values(["eom", "id"], kind="stable").reset_index(drop=True)
     if s["feat_prank"]:
-        seg = rt.group_starts(month_index(chars["eom"]))
-        X = chars[features].to_numpy(np.float64)
+        mi_rows = month_index(chars["eom"]).astype(np.int64)
+        pe = np.lexsort((chars["id"].to_numpy(np.int64), mi_rows))      # (eom, id) order
+        seg = rt.group_starts(mi_rows[pe])
+        X = chars[features].to_numpy(np.float64)[pe]
         R = rt.pct_rank(X, seg)
         R[X == 0.0] = 0.0                                  # quirk Q15: exact zeros stay 0
-        chars[features] = R
+        if s["feat_impute"]:
+            R[np.isnan(R)] = 0.5
+        Rb = np.empty_like(R)
+        Rb[pe] = R
+        chars[features] = Rb
         log.info("Feature Rank Complete.")
-    if s["feat_impute"]:
-        if s["feat_prank"]:
-            chars[features] = chars[features].fillna(0.5)
-        else:
-            chars[features] = chars.groupby("eom")[features].transform(lambda x: x.fillna(x.median()))
+        if s["feat_impute"]:
+            log.info("Feature Imputation Complete.")
+    elif s["feat_impute"]:
+        chars[features] = chars.groupby("eom")[features].transform(lambda x: x.fillna(x.median()))
         log.info("Feature Imputation Complete.")
     chars["ff12"] = categorize_sic(chars["sic"].to_numpy()).astype(str)
 
     # ---- lookback validity, size screen, addition/deletion (Prepare_Data.py:412-453) ---
-    chars = chars.sort_values(["id", "eom"], kind="stable").reset_index(drop=True)
     lb = pf["lb_hor"] + 1
     gs = rt.group_starts(chars["id"].to_numpy(np.int64))
     mi = month_index(chars["eom"]).astype(np.float64)
@@ -319,7 +344,7 @@ def prepare_data(cfg: Config, write: bool = True) -> dict:
     if write:
         io.write_csv(wealth, dd, "wealth_processed.csv")
         io.write_csv(labels, dd, "cluster_labels_processed.csv")
-        out = chars.copy()
+        out = chars.copy(deep=False)                   # (column replacement only)
         out["eom"] = out["eom"].dt.strftime("%Y-%m-%d")
         out["eom_ret"] = out["eom_ret"].dt.strftime("%Y-%m-%d")
         io.sql_write(io.path(dd, "JKP_US_SP500.db"), "Factors_processed", out)

@@ -25,6 +25,27 @@ def declare(lib) -> None:
     lib.pfml_group_starts.restype = L
     lib.pfml_group_shift.argtypes = [P, P, L, L, P]
     lib.pfml_group_shift.restype = None
+    # runtime/sqlite_io.cpp (columnar SQLite I/O)
+    lib.pfml_sql_query.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_longlong),
+                                   C.POINTER(C.c_int), C.c_char_p, I]
+    lib.pfml_sql_query.restype = P
+    lib.pfml_sql_col_name.argtypes = [P, I]
+    lib.pfml_sql_col_name.restype = C.c_char_p
+    lib.pfml_sql_col_kind.argtypes = [P, I]
+    lib.pfml_sql_col_kind.restype = I
+    lib.pfml_sql_col_f64.argtypes = [P, I, P]
+    lib.pfml_sql_col_f64.restype = None
+    lib.pfml_sql_col_i64.argtypes = [P, I, P]
+    lib.pfml_sql_col_i64.restype = None
+    lib.pfml_sql_col_text_bytes.argtypes = [P, I]
+    lib.pfml_sql_col_text_bytes.restype = C.c_longlong
+    lib.pfml_sql_col_text.argtypes = [P, I, P, P, P]
+    lib.pfml_sql_col_text.restype = None
+    lib.pfml_sql_free.argtypes = [P]
+    lib.pfml_sql_free.restype = None
+    lib.pfml_sql_write.argtypes = [C.c_char_p, C.c_char_p, I, I, P, P, P, P, P, P, C.c_longlong,
+                                   C.c_char_p, I]
+    lib.pfml_sql_write.restype = I
 
 
 def _lib():

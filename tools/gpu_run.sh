@@ -1,9 +1,15 @@
 #!/bin/bash
-# round-3 GPU session script: MODE selects the steps (comma list), TAG the output dir.
-#   suite  : pytest -m gpu + smoke + headline bench
-#   peak   : fp64 MFMA / VALU roofline anchor (tools/micro/mfma_f64_peak)
-#   bench  : headline bench only
-#   ridge  : ridge-grid A/B (tools/bench_ridge.py) with PFML_BAND_MODE variants
+# GPU session driver (run through gpurun): bash tools/gpu_run.sh TAG step1,step2,...
+# Every step writes under gpurun_out/TAG, runs under its own time limit and stops the chain on
+# failure.  Steps:
+#   suite      pytest -m gpu + smoke()          bench     headline bench (one JSON line)
+#   timeline   kernel timeline of one grid step shard     one-GPU per-rank strong-scaling rehearsal
+#   peak       fp64 MFMA / VALU roofline anchor dgemm     library vs in-house DGEMM rate
+#   ridge      band reduction A/B per phase     ktest     pytest -m gpu -k "$PFML_KTEST"
+#   e2e        production-shape `main` end to end (synthetic raw data, S0 stages, 8 stages)
+#   s4         S4+S5+S6 bench + S4 kernel stats stress    3000-stock S4 stress (BASELINE config 4)
+#   prec       bf16 / fp8 S4 GEMMs (BASELINE config 5)  pmc     PMC counters of one grid step
+#   multiproc  2 and 4 ranks sharing the GPU (gloo), utilities vs 1 rank
 set -o pipefail
 TAG=${1:-r03}
 MODE=${2:-suite}
@@ -77,6 +83,38 @@ for step in ${MODE//,/ }; do
       # staged fault hunt: PFML_DIAG = options of tools/diag_shard.py (setdev, env)
       timeout -k 10 300 python tools/diag_shard.py ${PFML_DIAG} > $OUT/diag_${PFML_DIAG// /_}.log 2>&1
       rc=$?; grep -v "^frame" $OUT/diag_${PFML_DIAG// /_}.log | tail -30; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    e2e)
+      # production-shape end-to-end run of `main` (SURVEY §7 north star): synthetic raw data of
+      # the production shape (500 stocks, 1952-2023), the two S0 stages, then the 8 stages of
+      # Main.py on the GPU; per-stage JSONL metrics
+      D=/tmp/pfml_e2e_data; AD=/tmp/pfml_e2e_art
+      rm -rf $D $AD
+      timeout -k 10 400 python -u -m pfml synth-data --data-dir $D > $OUT/e2e_synth.log 2>&1
+      rc=$?; tail -1 $OUT/e2e_synth.log | cut -c1-200; if [ $rc -ne 0 ]; then exit $rc; fi
+      PFML_METRICS=$OUT/e2e_metrics.jsonl timeout -k 10 600 python -u -m pfml stages get-additional-data,sp500-subset --data-dir $D --artifact-dir $AD --device cuda > $OUT/e2e_s0.log 2>&1
+      rc=$?; tail -2 $OUT/e2e_s0.log | cut -c1-200; if [ $rc -ne 0 ]; then exit $rc; fi
+      PFML_METRICS=$OUT/e2e_metrics.jsonl timeout -k 10 900 python -u -m pfml main --data-dir $D --artifact-dir $AD --device cuda > $OUT/e2e_main.log 2>&1
+      rc=$?; tail -3 $OUT/e2e_main.log | cut -c1-300; cat $OUT/e2e_metrics.jsonl | cut -c1-200; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    s4)
+      timeout -k 10 600 python bench.py --with-inputs --steps 1 --warmup 1 > $OUT/bench_s4.json 2> $OUT/bench_s4.err
+      rc=$?; grep '^{' $OUT/bench_s4.json | cut -c1-300; if [ $rc -ne 0 ]; then tail -3 $OUT/bench_s4.err; exit $rc; fi
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_s4 -o run -- python3 $ROOT/bench.py --with-inputs --steps 1 --warmup 0 > $OUT/prof_s4.log 2>&1)
+      rc=$?; if [ $rc -ne 0 ]; then tail -3 $OUT/prof_s4.log; exit $rc; fi
+      python tools/rocprof_summary.py $(find $OUT/prof_s4 -name "*.db" | head -1) --top 14 > $OUT/kernels_s4.txt 2>&1
+      cat $OUT/kernels_s4.txt ;;
+    stress)
+      timeout -k 10 900 python -u bench.py --s4-stress 48 --stocks 3000 --warmup 1 > $OUT/stress3000.json 2> $OUT/stress3000.err
+      rc=$?; cat $OUT/stress3000.json; tail -2 $OUT/stress3000.err; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    prec)
+      for pr in bf16 fp8; do
+        timeout -k 10 600 python bench.py --with-inputs --steps 1 --warmup 1 --precision $pr > $OUT/bench_s4_$pr.json 2> $OUT/bench_s4_$pr.err
+        rc=$?; grep '^{' $OUT/bench_s4_$pr.json | cut -c1-300; if [ $rc -ne 0 ]; then tail -3 $OUT/bench_s4_$pr.err; exit $rc; fi
+      done ;;
+    pmc)
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_ANY --output-format csv -d $OUT/pmc -o run -- python3 $ROOT/bench.py --steps 1 --warmup 0 --no-inputs > $OUT/pmc.log 2>&1)
+      rc=$?; python tools/pmc_summary.py $OUT/pmc --top 10 > $OUT/pmc.txt 2>&1; cat $OUT/pmc.txt; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    multiproc)
+      timeout -k 10 300 bash tools/gpu_multiproc.sh $TAG ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
