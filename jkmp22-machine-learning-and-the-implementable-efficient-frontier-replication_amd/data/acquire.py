@@ -57,22 +57,24 @@ def get_additional_data(cfg: Config, start="1952-01-01", end="2024-12-31") -> in
     n = 0
     with sqlite3.connect(db) as con:
         con.execute("DROP TABLE IF EXISTS crsp_daily_excess")
-        for a, b in _chunks(pd.Timestamp(start), pd.Timestamp(end)):
-            log.info(f"Processing chunk: {a.date()} to {b.date()}")
-            ch = pd.read_sql_query(
-                f"SELECT * FROM crsp_daily WHERE date BETWEEN '{a.date()}' AND '{b.date()}'",
-                con, parse_dates=["date"]).dropna()
-            if ch.empty:
-                continue
-            ch["ret"] = pd.to_numeric(ch["ret"], errors="coerce")
-            ch = ch.dropna(subset=["ret"]).merge(rf, on="date", how="left").dropna(subset=["RF"])
-            ch["permno"] = ch["permno"].astype(np.int64)
-            ch["ret_excess"] = (ch["ret"] - ch["RF"]).astype(np.float32)
-            ch["ret"] = ch["ret"].astype(np.float32)
-            ch["date"] = ch["date"].dt.strftime("%Y-%m-%d")
-            ch[["permno", "date", "ret", "primaryexch", "ret_excess"]].to_sql(
-                "crsp_daily_excess", con, if_exists="append", index=False)
-            n += len(ch)
+    # chunked as the reference (bounded memory); reads and appends through the columnar
+    # SQLite I/O (data/io.py, runtime/sqlite_io.cpp)
+    for a, b in _chunks(pd.Timestamp(start), pd.Timestamp(end)):
+        log.info(f"Processing chunk: {a.date()} to {b.date()}")
+        ch = io.sql_read(db, f"SELECT * FROM crsp_daily WHERE date BETWEEN '{a.date()}' AND "
+                             f"'{b.date()}'", parse_dates=["date"]).dropna()
+        if ch.empty:
+            continue
+        ch["ret"] = pd.to_numeric(ch["ret"], errors="coerce")
+        ch = ch.dropna(subset=["ret"]).merge(rf, on="date", how="left").dropna(subset=["RF"])
+        ch["permno"] = ch["permno"].astype(np.int64)
+        ch["ret_excess"] = (ch["ret"] - ch["RF"]).astype(np.float32)
+        ch["ret"] = ch["ret"].astype(np.float32)
+        ch["date"] = ch["date"].dt.strftime("%Y-%m-%d")
+        io.sql_write(db, "crsp_daily_excess",
+                     ch[["permno", "date", "ret", "primaryexch", "ret_excess"]], if_exists="append")
+        n += len(ch)
+    with sqlite3.connect(db) as con:
         con.execute("DROP TABLE IF EXISTS d_ret_ex")
         con.execute("ALTER TABLE crsp_daily_excess RENAME TO d_ret_ex")
     log.info("Processing complete.")
@@ -92,32 +94,30 @@ def sp500_subset(cfg: Config, start="1952-01-01", end="2024-12-31") -> dict:
             with sqlite3.connect(p) as con:
                 con.execute("DROP TABLE IF EXISTS Factors")
                 con.execute("DROP TABLE IF EXISTS d_ret_ex")
-    with sqlite3.connect(io.path(dd, "JKP_US.db")) as src:
-        for a, b in _chunks(pd.Timestamp(start), pd.Timestamp(end)):
-            ch = pd.read_sql_query(
-                f"SELECT * FROM Factors WHERE eom BETWEEN '{a.date()}' AND '{b.date()}'", src,
-                parse_dates=["eom"])
-            if ch.empty:
-                continue
-            sub = cons[["permno", "eom"]].merge(ch, left_on=["permno", "eom"],
-                                                right_on=["id", "eom"], how="inner")
-            sub = sub.drop(columns=["permno"])
-            sub["eom"] = sub["eom"].dt.strftime("%Y-%m-%d")
-            io.sql_write(outs["factors"], "Factors", sub, if_exists="append")
-            counts["factors"] += len(sub)
+    src = io.path(dd, "JKP_US.db")
+    for a, b in _chunks(pd.Timestamp(start), pd.Timestamp(end)):
+        ch = io.sql_read(src, f"SELECT * FROM Factors WHERE eom BETWEEN '{a.date()}' AND "
+                              f"'{b.date()}'", parse_dates=["eom"])
+        if ch.empty:
+            continue
+        sub = cons[["permno", "eom"]].merge(ch, left_on=["permno", "eom"],
+                                            right_on=["id", "eom"], how="inner")
+        sub = sub.drop(columns=["permno"])
+        sub["eom"] = sub["eom"].dt.strftime("%Y-%m-%d")
+        io.sql_write(outs["factors"], "Factors", sub, if_exists="append")
+        counts["factors"] += len(sub)
     log.info("Processing JKP_SP500 complete.")
-    with sqlite3.connect(io.path(dd, "crsp_daily.db")) as src:
-        for a, b in _chunks(pd.Timestamp(start), pd.Timestamp(end)):
-            ch = pd.read_sql_query(
-                f"SELECT * FROM d_ret_ex WHERE date BETWEEN '{a.date()}' AND '{b.date()}'", src,
-                parse_dates=["date"])
-            if ch.empty:
-                continue
-            ch["eom"] = ch["date"] + pd.offsets.MonthEnd(0)
-            sub = cons[["permno", "eom"]].merge(ch, on=["eom", "permno"], how="inner")
-            sub = sub.drop(columns=["eom"])
-            sub["date"] = sub["date"].dt.strftime("%Y-%m-%d")
-            io.sql_write(outs["daily"], "d_ret_ex", sub, if_exists="append")
-            counts["daily"] += len(sub)
+    src = io.path(dd, "crsp_daily.db")
+    for a, b in _chunks(pd.Timestamp(start), pd.Timestamp(end)):
+        ch = io.sql_read(src, f"SELECT * FROM d_ret_ex WHERE date BETWEEN '{a.date()}' AND "
+                              f"'{b.date()}'", parse_dates=["date"])
+        if ch.empty:
+            continue
+        ch["eom"] = ch["date"] + pd.offsets.MonthEnd(0)
+        sub = cons[["permno", "eom"]].merge(ch, on=["eom", "permno"], how="inner")
+        sub = sub.drop(columns=["eom"])
+        sub["date"] = sub["date"].dt.strftime("%Y-%m-%d")
+        io.sql_write(outs["daily"], "d_ret_ex", sub, if_exists="append")
+        counts["daily"] += len(sub)
     log.info("Processing crsp_daily_SP500 complete.")
     return counts

@@ -27,6 +27,33 @@ def path(data_dir: str, name: str) -> str:
     return os.path.join(data_dir, name)
 
 
+# wall seconds spent in this module's file I/O (SQLite, CSV); the stage runner reports the
+# per-stage delta next to the stage time (pipeline.run -> metrics "io_seconds")
+IO_SECONDS = [0.0]
+
+
+def _io_timed(fn):
+    import functools
+    import time
+
+    @functools.wraps(fn)
+    def wrap(*a, **k):
+        depth = _io_timed.depth
+        _io_timed.depth += 1
+        t0 = time.perf_counter()
+        try:
+            return fn(*a, **k)
+        finally:
+            _io_timed.depth -= 1
+            if depth == 0:                       # outermost I/O call only
+                IO_SECONDS[0] += time.perf_counter() - t0
+    return wrap
+
+
+_io_timed.depth = 0
+
+
+@_io_timed
 def read_risk_free(data_dir: str) -> pd.DataFrame:
     """FF monthly RF (percent) -> [eom, rf] (Prepare_Data.py:62-71)."""
     rf = pd.read_csv(path(data_dir, "FF_RF_monthly.csv"), usecols=["yyyymm", "RF"])
@@ -34,6 +61,7 @@ def read_risk_free(data_dir: str) -> pd.DataFrame:
     return pd.DataFrame({"eom": eom, "rf": rf["RF"] / 100.0})
 
 
+@_io_timed
 def read_market(data_dir: str) -> pd.DataFrame:
     """US value-weighted market excess return -> [eom_ret, mkt_vw_exc] (Prepare_Data.py:82-89)."""
     m = pd.read_csv(path(data_dir, "market_returns.csv"), dtype={"eom": str})
@@ -42,6 +70,7 @@ def read_market(data_dir: str) -> pd.DataFrame:
                          "mkt_vw_exc": m["mkt_vw_exc"].values})
 
 
+@_io_timed
 def read_factor_details(data_dir: str) -> pd.DataFrame:
     x = path(data_dir, "Factor Details.xlsx")
     if os.path.exists(x):
@@ -52,6 +81,7 @@ def read_factor_details(data_dir: str) -> pd.DataFrame:
     return pd.read_csv(path(data_dir, "Factor Details.csv"))
 
 
+@_io_timed
 def read_rff_w(data_dir: str) -> np.ndarray:
     """RFF weight matrix, k x p_max/2, stored with an unnamed index column."""
     w = pd.read_csv(path(data_dir, "rff_w.csv"))
@@ -118,6 +148,7 @@ def _native_read(db: str, query: str, parse_dates) -> pd.DataFrame | None:
     return df
 
 
+@_io_timed
 def sql_read(db: str, query: str, **kw) -> pd.DataFrame:
     """pandas.read_sql_query semantics; the columnar native reader when available (about 20x
     faster on the 430k x 130 Factors tables), pandas otherwise / for other keywords."""
@@ -197,6 +228,7 @@ def _native_write(db: str, table: str, df: pd.DataFrame, if_exists: str) -> bool
     return True
 
 
+@_io_timed
 def sql_write(db: str, table: str, df: pd.DataFrame, if_exists: str = "replace") -> None:
     """DataFrame.to_sql(index=False) semantics; the native column writer when available."""
     if os.environ.get("PFML_SQL_NATIVE", "1") != "0" and _native_write(db, table, df, if_exists):
@@ -210,6 +242,7 @@ PROCESSED_COLUMNS = ["id", "eom", "sic", "ff49", "size_grp", "me", "crsp_exchcd"
                      "ff12", "valid"]
 
 
+@_io_timed
 def read_processed_chars(data_dir: str, features: list[str]) -> pd.DataFrame:
     """Factors_processed as loaded by the later stages (e.g. PFML_Input_Data.py:53-79)."""
     q = "SELECT " + ", ".join(PROCESSED_COLUMNS + features) + " FROM Factors_processed"
@@ -218,6 +251,7 @@ def read_processed_chars(data_dir: str, features: list[str]) -> pd.DataFrame:
     return chars
 
 
+@_io_timed
 def write_csv(df: pd.DataFrame, data_dir: str, name: str) -> str:
     cols = CSV_COLUMNS.get(name)
     if cols is not None:

@@ -103,8 +103,10 @@ class Pipeline:
                 log.info(f"[{st}] up to date (resume)")
                 continue
             t0 = time.time()
+            io0 = io.IO_SECONDS[0]
             with self.timer(st):
                 getattr(self, "_" + st.replace("-", "_"))()
+            io_s = io.IO_SECONDS[0] - io0
             if self.checkpoint:
                 if st in _SHARDED:
                     self.store.mark_done(st, self._rank_key(st), rank=self.env.rank,
@@ -112,8 +114,9 @@ class Pipeline:
                 elif self.env.is_main:
                     self.store.mark_done(st, self._keys[st], seconds=time.time() - t0)
             pdist.barrier()
-            metric(stage=st, seconds=round(time.time() - t0, 3), rank=self.env.rank,
-                   world_size=self.env.world_size, fallbacks=COUNTERS.as_dict())
+            metric(stage=st, seconds=round(time.time() - t0, 3), io_seconds=round(io_s, 3),
+                   rank=self.env.rank, world_size=self.env.world_size,
+                   fallbacks=COUNTERS.as_dict())
             log.info(f"[{st}] done in {time.time() - t0:.2f}s")
         return self.state
 
