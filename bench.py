@@ -136,6 +136,24 @@ def graphed(fn, dev):
         return None
 
 
+def segmented(fn, dev):
+    """Segment-wise graph capture of a multi-rank step (collectives eager in between);
+    None (eager launches) when the capture fails - the same decision on every rank."""
+    from pfml.parallel.graphs import SegmentedGraph
+    ok, rep, err = 1.0, None, None
+    try:
+        rep = SegmentedGraph(dev).capture(fn)
+    except Exception as e:                         # noqa: BLE001
+        ok, err = 0.0, e
+    # every rank must take the same path (the replay's collectives pair up across ranks)
+    if coll.all_reduce_max(1.0 - ok, device=dev) > 0.0:
+        if err is not None:
+            print(f"[bench] segmented graph capture failed, eager launches: "
+                  f"{type(err).__name__}: {err}", file=sys.stderr)
+        return None
+    return rep
+
+
 def timed(fn, steps: int, warmup: int, dev) -> float:
     """ms per step: W untimed steps, then K steps bracketed by barrier + synchronize, max over
     ranks."""
@@ -262,8 +280,9 @@ def main():
     ap.add_argument("--device", default="auto")
     ap.add_argument("--profile", action="store_true")
     ap.add_argument("--graph", action=argparse.BooleanOptionalAction, default=True,
-                    help="replay the step as a captured HIP graph (one rank, grid step without "
-                         "S4; falls back to eager launches if the capture fails)")
+                    help="replay the grid step (without S4) as a captured HIP graph - one rank: "
+                         "one graph; several ranks: graph segments between the eager "
+                         "collectives; falls back to eager launches if the capture fails")
     ap.add_argument("--with-inputs", action="store_true",
                     help="time S4 (PFML input construction for every month) + S5 + S6 as the step")
     ap.add_argument("--rank-deficient", type=int, default=0, metavar="NT",
@@ -320,8 +339,13 @@ def main():
         box["res"], box["scores"] = one_step(reals, cfg, engine)
 
     use_graph = False
-    if args.graph and dev.type == "cuda" and not env.is_dist and engine is None:
-        rep = graphed(step, dev)
+    if args.graph and dev.type == "cuda" and engine is None:
+        if env.is_dist:
+            # one process per GPU: the compute between the collectives replays as graph
+            # segments, the collectives run eagerly between them (parallel/graphs.py)
+            rep = segmented(step, dev)
+        else:
+            rep = graphed(step, dev)
         if rep is not None:
             use_graph = True
             ms = timed(rep, args.steps, args.warmup, dev)

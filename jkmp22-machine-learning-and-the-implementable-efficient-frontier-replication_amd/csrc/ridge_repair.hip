@@ -139,6 +139,16 @@ __global__ __launch_bounds__(RT) void ridge_lu_repair_kernel(
 
 extern "C" int pfml_ridge_repair_wg() { return REPAIR_WG; }
 
+// workgroups of one repair launch: never more than the systems it can be handed (cap)
+static int repair_wgs(int cap) { return cap < REPAIR_WG ? (cap > 0 ? cap : 1) : REPAIR_WG; }
+
+// scratch doubles of a launch with list capacity `cap`: one nmax x (nmax + 1) system per
+// workgroup (64 x 1025 x 1026 doubles = 540 MB at nmax = 1025 only when >= 64 systems can
+// fail; a launch of few cells sizes it by its own capacity)
+extern "C" int64_t pfml_ridge_repair_work_doubles_cap(int nmax, int cap) {
+  return (int64_t)repair_wgs(cap) * nmax * (nmax + 1);
+}
+
 extern "C" int64_t pfml_ridge_repair_work_doubles(int nmax) {
   return (int64_t)REPAIR_WG * nmax * (nmax + 1);
 }
@@ -154,7 +164,7 @@ extern "C" hipError_t pfml_ridge_repair(const double* SD, int64_t ldS, const dou
   const int tot = ncells * L;
   hipLaunchKernelGGL(ridge_flag_kernel, dim3((tot + 255) / 256), dim3(256), 0, st, cd, ncells, L,
                      beta, ldo, list, count, cap);
-  hipLaunchKernelGGL(ridge_lu_repair_kernel, dim3(REPAIR_WG), dim3(RT), 0, st, SD, ldS, Sr, cd,
+  hipLaunchKernelGGL(ridge_lu_repair_kernel, dim3(repair_wgs(cap)), dim3(RT), 0, st, SD, ldS, Sr, cd,
                      lvec, L, beta, ldo, list, count, cap, work, nmax);
   return hipGetLastError();
 }

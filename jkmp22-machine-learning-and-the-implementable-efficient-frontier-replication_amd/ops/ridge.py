@@ -304,6 +304,8 @@ nat.register_hip("pfml_ridge_repair", [C.c_void_p, C.c_int64, C.c_void_p, C.c_vo
                                        C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int64,
                                        C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p])
 nat.register_hip("pfml_ridge_repair_work_doubles", [C.c_int], C.c_int64)
+nat.register_hip("pfml_ridge_repair_work_doubles_cap", [C.c_int, C.c_int], C.c_int64)
+_REPAIR_WORK: dict = {}
 
 # device repair counts of the most recent ridge launches (int32 device scalars; read them
 # only when reporting - reading forces a sync)
@@ -321,8 +323,15 @@ def repair_launch(plan: dict, d_desc: torch.Tensor, SD: torch.Tensor, Sr: torch.
     count = torch.zeros(1, dtype=torch.int32, device=SD.device)
     cap = plan["nc"] * L
     lst = torch.empty(cap, dtype=torch.int32, device=SD.device)
-    work = torch.empty(lib.pfml_ridge_repair_work_doubles(plan["nmax"]), dtype=torch.float64,
-                       device=SD.device)
+    # scratch sized by the launch's own capacity and kept per (device, size): allocated once,
+    # not per launch (540 MB per tridiagonal-path launch at n = 1025)
+    nwd = int(lib.pfml_ridge_repair_work_doubles_cap(plan["nmax"], cap))
+    wkey = (str(SD.device), nat.stream_of(SD), nwd)     # (per stream: no sharing across streams)
+    work = _REPAIR_WORK.get(wkey)
+    if work is None:
+        if len(_REPAIR_WORK) > 4:
+            _REPAIR_WORK.clear()
+        work = _REPAIR_WORK[wkey] = torch.empty(nwd, dtype=torch.float64, device=SD.device)
     nat.check(lib.pfml_ridge_repair(SD.data_ptr(), P, Sr.data_ptr(), d_desc.data_ptr(),
                                     plan["nc"], plan["nmax"], lv.data_ptr(), L, beta.data_ptr(),
                                     beta.shape[-1], lst.data_ptr(), count.data_ptr(), cap,

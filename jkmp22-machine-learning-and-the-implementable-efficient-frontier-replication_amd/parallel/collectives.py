@@ -58,12 +58,31 @@ def all_gather_varlen(x: torch.Tensor) -> torch.Tensor:
     return torch.cat(parts, 0)
 
 
+# Segmented HIP-graph capture (parallel/graphs.py): while a step is being captured, the
+# collectives below end the current graph segment, run eagerly into a static output and
+# start the next segment; a replay then alternates segment graphs and these collectives.
+_CAPTURE = None
+
+
+def set_capture(cap) -> None:
+    global _CAPTURE
+    _CAPTURE = cap
+
+
 def all_gather_known(x: torch.Tensor, counts) -> torch.Tensor:
     """all_gather_varlen when every rank's first-dim size is already known everywhere (e.g.
     from a plan all ranks share): ONE collective, no size exchange and no host round trip."""
     e = env()
     if not e.is_dist:
         return x
+    if _CAPTURE is not None:
+        return _CAPTURE.collective(_all_gather_known_into, x, counts)
+    return _all_gather_known_into(None, x, counts)
+
+
+def _all_gather_known_into(out: torch.Tensor | None, x: torch.Tensor, counts) -> torch.Tensor:
+    """all_gather_known; with ``out`` the result is copied into that (static) tensor."""
+    e = env()
     counts = [int(c) for c in counts]
     if len(counts) != e.world_size or x.shape[0] != counts[e.rank]:
         raise ValueError(f"all_gather_known: rank {e.rank} holds {x.shape[0]} rows, "
@@ -76,7 +95,11 @@ def all_gather_known(x: torch.Tensor, counts) -> torch.Tensor:
         pad = torch.zeros((m, *x.shape[1:]), dtype=x.dtype, device=x.device)
         pad[: x.shape[0]] = x
     g = all_gather_cat(pad)
-    return torch.cat([g[r * m: r * m + counts[r]] for r in range(e.world_size)], 0)
+    res = torch.cat([g[r * m: r * m + counts[r]] for r in range(e.world_size)], 0)
+    if out is None:
+        return res
+    out.copy_(res)
+    return out
 
 
 def exclusive_prefix_sum(total: torch.Tensor) -> torch.Tensor:
