@@ -20,6 +20,7 @@ import pandas as pd
 import torch
 
 from ..config import Config
+from ..data import io
 from ..ops import linalg as la
 from ..ops import _native as nat
 from ..ops.gemm import gemm_fused
@@ -460,6 +461,7 @@ def pf_summary(pf: pd.DataFrame, gamma: float) -> pd.DataFrame:
         "obj": (r.mean() - 0.5 * r.var(ddof=1) * gamma - tc.mean()) * 12}])
 
 
+@io._io_timed                                             # (figure files: stage I/O time)
 def plots(pf: pd.DataFrame, best: pd.DataFrame, gamma: float, out_dir: str) -> list[str]:
     """Cumulative performance and chosen hyper-parameters (PFML_best_hps.py:281-291,361-422)."""
     try:

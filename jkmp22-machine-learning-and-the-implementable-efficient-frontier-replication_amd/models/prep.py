@@ -357,6 +357,7 @@ def universe_counts(chars: pd.DataFrame) -> pd.DataFrame:
     return v.groupby("eom").size().reset_index(name="N")
 
 
+@io._io_timed                                             # (figure files: stage I/O time)
 def universe_plot(chars: pd.DataFrame, out_dir: str) -> list[str]:
     """The investable-universe figure of Prepare_Data.py:464-471 (valid stocks per eom, a
     scatter with a zero line) as a PNG, plus its data as universe_counts.csv."""

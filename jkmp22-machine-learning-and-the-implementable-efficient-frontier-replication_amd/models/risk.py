@@ -58,6 +58,7 @@ class BarraCov:
         a, b = self.offsets[p], self.offsets[p + 1]
         return self.ids[a:b], self.X[a:b], self.F[p], self.ivol[a:b]
 
+    @io._io_timed                                         # (file output: stage I/O time)
     def save(self, path: str) -> None:
         os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
         np.savez(path, months=self.months, offsets=self.offsets, ids=self.ids, X=self.X,

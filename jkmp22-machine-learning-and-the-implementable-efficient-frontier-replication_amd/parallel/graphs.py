@@ -35,7 +35,11 @@ class SegmentedGraph:
         self._cur = g
 
     def _end(self) -> None:
-        self._cur.capture_end()
+        import warnings
+        with warnings.catch_warnings():
+            # back-to-back collectives leave an empty segment in between (harmless)
+            warnings.filterwarnings("ignore", message="The CUDA Graph is empty")
+            self._cur.capture_end()
         self.graphs.append(self._cur)
         self._cur = None
 
