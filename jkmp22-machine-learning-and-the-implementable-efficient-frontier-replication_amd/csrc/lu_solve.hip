@@ -18,9 +18,18 @@
 
 namespace {
 
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+
 // Block width NB and the panel rows PMAX held in LDS: NB = 32 for n <= 512 (half the passes
 // over the augmented rows of NB = 16; the 512 x 33 panel is 135 KB of LDS), NB = 16 up to
-// n = 1024.  The trailing update is bandwidth-bound (each pass reads and writes the live
+// n = 1024; longer panels (n <= 3072, the 3000-stock stress) are pivoted in registers
+// (lu_pivot_reg_kernel).  The trailing update is bandwidth-bound (each pass reads and writes the live
 // part of every row), so the pass count sets its time.
 
 // live column v (0 .. nlive-1) -> physical column
@@ -85,6 +94,144 @@ __global__ __launch_bounds__(256) void lu_pivot_kernel(const double* __restrict_
     }
     __syncthreads();
   }
+}
+
+// Pivot search for tall panels (n - k0 > 1024 rows, up to R * 1024): the panel lives in
+// REGISTERS of a 1024-thread workgroup - thread t holds rows t, t + 1024, ... (R rows x NB
+// columns; the last RL row sets in a thread-private LDS slot when R rows would spill) -
+// instead of a shared LDS panel (a 3000 x 16 panel is 384 KB).  One barrier per column: before it
+// each wave posts its best candidate row (value, index, the row's NB entries) and thread j
+// posts the current row j, so after it every thread knows the pivot row's values and the
+// owners of rows j and p swap in registers (double-buffered posts: the next column writes the
+// other buffer).  Same pivot choice (first index of the maximum |a|) and the same elimination
+// arithmetic as lu_pivot_kernel, so both forms pick the same pivots.
+template <int NB, int R, int RL>
+__global__ __launch_bounds__(1024) void lu_pivot_reg_kernel(const double* __restrict__ M, int n,
+                                                            int64_t ldm, int64_t sM, int a0,
+                                                            int k0, int nb,
+                                                            int* __restrict__ piv,
+                                                            int* __restrict__ status) {
+  constexpr int NT = 1024, NW = NT / 64, RR = R - RL;
+  __shared__ double cand[2][NW][NB];
+  __shared__ double cval[2][NW];
+  __shared__ int cidx[2][NW];
+  __shared__ double rowj[2][NB];
+  __shared__ double al[RL > 0 ? RL : 1][NB][NT];   // the last RL row sets (thread-private)
+  const int b = blockIdx.x;
+  const double* Mb = M + (int64_t)b * sM;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int rows = n - k0;
+  double a[RR][NB];
+  // element (row set r, column c) of this thread: registers for r < RR, LDS for the rest
+  auto el = [&](auto RI, int c) -> double& {
+    constexpr int r = decltype(RI)::value;
+    if constexpr (r < RR) return a[r][c];
+    else return al[r - RR][c][t];
+  };
+  static_for<0, R>([&](auto RI) {
+    constexpr int r = decltype(RI)::value;
+    const int i = t + r * NT;
+    const double* src = Mb + (int64_t)(k0 + min(i, rows - 1)) * ldm + a0 + k0;
+#pragma unroll
+    for (int c = 0; c < NB; ++c) el(RI, c) = (i < rows && c < nb) ? src[min(c, nb - 1)] : 0.0;
+  });
+  static_for<0, NB>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    if (j >= nb) return;                            // (uniform: nb is a kernel argument)
+    const int buf = j & 1;
+    // own candidate: first row of the largest |a[.][j]| among rows i >= j
+    double best = -1.0;
+    int bi = 0x7fffffff;
+    static_for<0, R>([&](auto RI) {
+      constexpr int r = decltype(RI)::value;
+      const int i = t + r * NT;
+      const double v = fabs(el(RI, j));
+      if (i >= j && i < rows && v > best) { best = v; bi = i; }
+    });
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double ov = __shfl_xor(best, off, 64);
+      const int oi = __shfl_xor(bi, off, 64);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    if (lane == 0) { cval[buf][w] = best; cidx[buf][w] = bi; }
+    if (bi != 0x7fffffff && (bi % NT) == t) {      // the wave's winner posts its row
+      static_for<0, R>([&](auto RI) {
+        constexpr int r = decltype(RI)::value;
+        if (r == bi / NT) {
+#pragma unroll
+          for (int c = 0; c < NB; ++c) cand[buf][w][c] = el(RI, c);
+        }
+      });
+    }
+    if (t == j) {                                   // current row j (rows < 32: set 0)
+#pragma unroll
+      for (int c = 0; c < NB; ++c) rowj[buf][c] = a[0][c];
+    }
+    __syncthreads();
+    double bv = cval[buf][0];
+    int bx = cidx[buf][0], bw = 0;
+#pragma unroll
+    for (int q = 1; q < NW; ++q) {
+      const double v = cval[buf][q];
+      const int x = cidx[buf][q];
+      if (v > bv || (v == bv && x < bx)) { bv = v; bx = x; bw = q; }
+    }
+    if (t == 0) {
+      piv[(int64_t)b * NB + j] = k0 + bx;
+      if (!(bv > 0.0) || !isfinite(bv)) status[b] = 1;
+    }
+    const double* prow = cand[buf][bw];             // pivot row, read from LDS where used
+    // swap: row j <- pivot row, row p <- old row j
+    if (bx != j && (bx % NT) == t) {
+      static_for<0, R>([&](auto RI) {
+        constexpr int r = decltype(RI)::value;
+        if (r == bx / NT) {
+#pragma unroll
+          for (int c = 0; c < NB; ++c) el(RI, c) = rowj[buf][c];
+        }
+      });
+    }
+    if (t == j) {
+#pragma unroll
+      for (int c = 0; c < NB; ++c) a[0][c] = prow[c];
+    }
+    const double pv = prow[j];
+    static_for<0, R>([&](auto RI) {
+      constexpr int r = decltype(RI)::value;
+      const int i = t + r * NT;
+      if (i > j && i < rows) {
+        const double l = el(RI, j) / pv;
+#pragma unroll
+        for (int c = j + 1; c < NB; ++c) el(RI, c) -= l * prow[c];
+      }
+    });
+  });
+}
+
+// pivot search of block k0 by the LDS form (rows <= PMAX) or the register form (longer panels)
+template <int NB, int PMAX>
+hipError_t lu_pivot_launch(const double* M, int n, int64_t ldm, int64_t sM, int a0, int k0,
+                           int nb, int* piv, int* status, int batch, hipStream_t st) {
+  const int rows = n - k0;
+  if (rows <= PMAX) {
+    hipLaunchKernelGGL((lu_pivot_kernel<NB, PMAX>), dim3(batch), dim3(256), 0, st, M, n, ldm,
+                       sM, a0, k0, nb, piv, status);
+    return hipSuccess;
+  }
+  if constexpr (NB == 16) {          // (NB = 32 panels would not fit the register budget)
+    if (rows <= 2048) {
+      hipLaunchKernelGGL((lu_pivot_reg_kernel<NB, 2, 0>), dim3(batch), dim3(1024), 0, st, M, n,
+                         ldm, sM, a0, k0, nb, piv, status);
+      return hipSuccess;
+    }
+    if (rows <= 3072) {
+      hipLaunchKernelGGL((lu_pivot_reg_kernel<NB, 3, 1>), dim3(batch), dim3(1024), 0, st, M, n,
+                         ldm, sM, a0, k0, nb, piv, status);
+      return hipSuccess;
+    }
+  }
+  return hipErrorInvalidValue;
 }
 
 // apply the NB sequential row swaps of block k0 to every live column (+ block k's own A cols)
@@ -277,8 +424,8 @@ hipError_t lu_solve_nb(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
   int* piv = reinterpret_cast<int*>(Cbuf + (int64_t)batch * n * NB);
   for (int k0 = 0; k0 < n; k0 += NB) {
     const int nb = (n - k0 < NB) ? (n - k0) : NB;
-    hipLaunchKernelGGL((lu_pivot_kernel<NB, PMAX>), dim3(batch), dim3(256), 0, st, M, n, ldm, sM,
-                       a0, k0, nb, piv, status);
+    hipError_t e = lu_pivot_launch<NB, PMAX>(M, n, ldm, sM, a0, k0, nb, piv, status, batch, st);
+    if (e != hipSuccess) return e;
     const int nswap = (n - k0) + m;           // A cols >= k0 and all B cols
     hipLaunchKernelGGL((lu_swap_kernel<NB>), dim3((nswap + 255) / 256, batch), dim3(256), 0, st,
                        M, ldm, sM, nswap, a0 + k0, n - k0, b0, k0, nb, piv);
@@ -300,7 +447,7 @@ hipError_t lu_solve_nb(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
 }
 
 // ---------------------------------------------------------------------------------------
-// Two-level form (n <= 512): 128-wide outer panels.  The 32-wide inner steps above run on the
+// Two-level form (n <= 3072): 128-wide outer panels.  The 32-wide (n > 512: 16-wide) inner steps above run on the
 // panel's own A columns plus a 128-column block Z of M (the inner update touches <= 256
 // columns instead of all n + m), and Z accumulates the panel's Gauss-Jordan transform:
 // the unit vector of each pivot row is placed in Z when its inner block is reached (after
@@ -349,9 +496,9 @@ extern "C" hipError_t pfml_dgemm(int ta, int tb, int M, int N, int K, int batch,
 
 namespace {
 
+template <int NB, int PMAX>
 hipError_t lu_solve_2level(double* M, int n, int m, int64_t ldm, int64_t sM, int a0, int b0,
                            int z0, int batch, double* work, int* status, hipStream_t st) {
-  constexpr int NB = 32;
   double* Pbuf = work;
   double* Rbuf = Pbuf + (int64_t)batch * NB * NB;
   double* Cbuf = Rbuf + (int64_t)batch * NB * (2 * LU_KB);
@@ -365,8 +512,8 @@ hipError_t lu_solve_2level(double* M, int n, int m, int64_t ldm, int64_t sM, int
     for (int k0 = K0; k0 < aend; k0 += NB) {
       const int nb = (aend - k0 < NB) ? (aend - k0) : NB;
       int* pv = piv + (int64_t)((k0 - K0) / NB) * batch * NB;
-      hipLaunchKernelGGL((lu_pivot_kernel<NB, 512>), dim3(batch), dim3(256), 0, st, M, n, ldm, sM,
-                         a0, k0, nb, pv, status);
+      hipError_t e = lu_pivot_launch<NB, PMAX>(M, n, ldm, sM, a0, k0, nb, pv, status, batch, st);
+      if (e != hipSuccess) return e;
       // live set of the inner step: A columns k0 .. aend (swap) / right of the block, and Z
       const int nswap = (aend - k0) + kb;
       hipLaunchKernelGGL((lu_swap_kernel<NB>), dim3((nswap + 255) / 256, batch), dim3(256), 0, st,
@@ -434,22 +581,27 @@ extern "C" int64_t pfml_lu_solve_work_doubles(int n, int m, int batch) {
 }
 
 // Solve A X = B in place for `batch` augmented systems (see header); X overwrites B.
-extern "C" int pfml_lu_solve_max_n() { return 1024; }
+extern "C" int pfml_lu_solve_max_n() { return 3072; }
 
 extern "C" hipError_t pfml_lu_solve(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
                                     int b0, int batch, double* work, int* status,
                                     hipStream_t st) {
   if (n <= 0 || batch <= 0) return hipSuccess;
   if (n <= 512) return lu_solve_nb<32, 512>(M, n, m, ldm, sM, a0, b0, batch, work, status, st);
-  if (n <= 1024) return lu_solve_nb<16, 1024>(M, n, m, ldm, sM, a0, b0, batch, work, status, st);
+  if (n <= 3072) return lu_solve_nb<16, 1024>(M, n, m, ldm, sM, a0, b0, batch, work, status, st);
   return hipErrorInvalidValue;
 }
 
 // Two-level solve; M must hold LU_KB free columns at z0 (scratch for the panel transform).
+extern "C" int pfml_lu_solve2_max_n() { return 3072; }
+
 extern "C" hipError_t pfml_lu_solve2(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
                                      int b0, int z0, int batch, double* work, int* status,
                                      hipStream_t st) {
   if (n <= 0 || batch <= 0) return hipSuccess;
-  if (n > 512) return hipErrorInvalidValue;
-  return lu_solve_2level(M, n, m, ldm, sM, a0, b0, z0, batch, work, status, st);
+  if (n <= 512)
+    return lu_solve_2level<32, 512>(M, n, m, ldm, sM, a0, b0, z0, batch, work, status, st);
+  if (n <= 3072)
+    return lu_solve_2level<16, 1024>(M, n, m, ldm, sM, a0, b0, z0, batch, work, status, st);
+  return hipErrorInvalidValue;
 }

@@ -214,11 +214,12 @@ def solve_augmented(M: torch.Tensor, n: int, m: int, a0: int, b0: int,
     """In-place solve of augmented systems: rows of M [B, n, W] hold A at columns a0..a0+n and
     B at b0..b0+m; on return the B columns hold X = A^-1 B (returned as a view).
 
-    Device: csrc/lu_solve.hip (blocked Gauss-Jordan with partial pivoting, the pivot panel in
-    LDS; 32-wide blocks up to n = 512, 16-wide up to 1024); larger systems (the 3000-stock
-    stress) take the library (rocSOLVER) LU through torch.  ``z0``: M holds LU_PANEL_COLS free
-    scratch columns there, and n <= 512 takes the two-level form (128-wide panels whose
-    transform reaches the other columns through K = 128 GEMMs).  With ``status`` (a [B] int32
+    Device: csrc/lu_solve.hip (blocked Gauss-Jordan with partial pivoting; 32-wide blocks up to
+    n = 512, 16-wide up to 3072 - the pivot panel in LDS up to 1024 rows, in the registers of a
+    1024-thread workgroup beyond, which covers the 3000-stock stress); larger systems take the
+    library (rocSOLVER) LU through torch.  ``z0``: M holds LU_PANEL_COLS free scratch columns
+    there, and the two-level form runs (128-wide panels whose transform reaches the other
+    columns through K = 128 GEMMs).  With ``status`` (a [B] int32
     device tensor) singular systems are only flagged there (no host sync; the caller checks
     once), otherwise they are counted here."""
     if nat.is_device(M) and n <= _lu_max_n():
@@ -230,7 +231,7 @@ def solve_augmented(M: torch.Tensor, n: int, m: int, a0: int, b0: int,
                            device=M.device)
         st = status if status is not None else torch.zeros(Bt, dtype=torch.int32,
                                                            device=M.device)
-        if z0 is not None and n <= 512:
+        if z0 is not None:
             if z0 + LU_PANEL_COLS > W:
                 raise ValueError("solve_augmented: z0 needs LU_PANEL_COLS scratch columns")
             nat.check(lib.pfml_lu_solve2(M.data_ptr(), n, m, W, nn * W, a0, b0, z0, Bt,

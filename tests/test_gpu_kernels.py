@@ -213,7 +213,7 @@ def test_grid_search_gpu_matches_cpu(gpu):
 
 
 @pytest.mark.parametrize("n,m,b", [(17, 5, 2), (64, 10, 2), (100, 37, 3), (490, 1028, 2),
-                                   (512, 20, 1), (513, 1026, 2)])
+                                   (512, 20, 1), (513, 1026, 2), (1500, 40, 2), (2900, 70, 2)])
 def test_lu_solve_augmented(gpu, n, m, b):
     from pfml.ops.linalg import solve
     A = _rand(b, n, n, seed=n) + n ** 0.5 * torch.eye(n, dtype=torch.float64)
@@ -226,11 +226,13 @@ def test_lu_solve_augmented(gpu, n, m, b):
 
 
 @pytest.mark.parametrize("n,m,b", [(490, 1026, 3), (512, 300, 2), (130, 70, 4), (100, 514, 2),
-                                   (257, 33, 3)])
+                                   (257, 33, 3), (700, 130, 2), (1100, 260, 2), (2100, 100, 2),
+                                   (2900, 1026, 2)])
 def test_lu_solve_two_level(gpu, n, m, b):
     """Two-level solve (128-wide panels, transform block Z in scratch columns, K = 128 GEMM
     updates) on the S4 layout [B | A | scratch] vs torch.linalg.solve; pivoting forced in
-    the first and in a later panel."""
+    the first and in a later panel.  n > 1024: the pivot panels of > 1024 rows are searched
+    in registers (lu_pivot_reg_kernel, 2 and 3 row sets) - the 3000-stock stress sizes."""
     from pfml.ops.linalg import LU_PANEL_COLS, solve_augmented
     A = _rand(b, n, n, seed=n + 1) + 0.5 * n ** 0.5 * torch.eye(n, dtype=torch.float64)
     A[:, 0, 0] = 1e-8
@@ -245,7 +247,7 @@ def test_lu_solve_two_level(gpu, n, m, b):
     got = solve_augmented(Md, n, m, a0=m, b0=0, status=st, z0=m + n).cpu()
     assert int(st.sum()) == 0
     rel = ((got - ref).norm() / ref.norm()).item()
-    assert rel < 1e-11, rel
+    assert rel < (1e-11 if n <= 512 else 1e-10), rel     # (rounding grows with n)
 
 
 @pytest.mark.parametrize("variant", ["unblocked", "blocked", "fast"])

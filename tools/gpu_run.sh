@@ -8,7 +8,7 @@
 #   ridge      band reduction A/B per phase     ktest     pytest -m gpu -k "$PFML_KTEST"
 #   e2e        production-shape `main` end to end (synthetic raw data, S0 stages, 8 stages)
 #   s4         S4+S5+S6 bench + S4 kernel stats stress    3000-stock S4 stress (BASELINE config 4)
-#   prec       bf16 / fp8 S4 GEMMs (BASELINE config 5)  pmc     PMC counters of one grid step
+#   stressprof kernel stats of the stress    prec bf16 / fp8 S4 GEMMs (BASELINE config 5)  pmc     PMC counters of one grid step
 #   multiproc  2 and 4 ranks sharing the GPU (gloo), utilities vs 1 rank
 set -o pipefail
 TAG=${1:-r03}
@@ -101,10 +101,16 @@ for step in ${MODE//,/ }; do
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_s4 -o run -- python3 $ROOT/bench.py --with-inputs --steps 1 --warmup 0 > $OUT/prof_s4.log 2>&1)
       rc=$?; if [ $rc -ne 0 ]; then tail -3 $OUT/prof_s4.log; exit $rc; fi
       python tools/rocprof_summary.py $(find $OUT/prof_s4 -name "*.db" | head -1) --top 14 > $OUT/kernels_s4.txt 2>&1
-      cat $OUT/kernels_s4.txt ;;
+      rm -rf $OUT/prof_s4; cat $OUT/kernels_s4.txt ;;
     stress)
       timeout -k 10 900 python -u bench.py --s4-stress 48 --stocks 3000 --warmup 1 > $OUT/stress3000.json 2> $OUT/stress3000.err
       rc=$?; cat $OUT/stress3000.json; tail -2 $OUT/stress3000.err; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    stressprof)
+      # kernel stats of the 3000-stock stress (12 months)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_stress -o run -- python3 $ROOT/bench.py --s4-stress 12 --stocks 3000 --warmup 0 > $OUT/prof_stress.log 2>&1)
+      rc=$?; if [ $rc -ne 0 ]; then tail -3 $OUT/prof_stress.log; exit $rc; fi
+      python tools/rocprof_summary.py $(find $OUT/prof_stress -name "*.db" | head -1) --top 20 > $OUT/kernels_stress.txt 2>&1
+      rm -rf $OUT/prof_stress; cat $OUT/kernels_stress.txt ;;
     prec)
       for pr in bf16 fp8; do
         timeout -k 10 600 python bench.py --with-inputs --steps 1 --warmup 1 --precision $pr > $OUT/bench_s4_$pr.json 2> $OUT/bench_s4_$pr.err
