@@ -175,7 +175,13 @@ def size_screen(chars: pd.DataFrame, type_: str) -> None:
 
 def addition_deletion(chars: pd.DataFrame, addition_n: int, deletion_n: int) -> pd.DataFrame:
     """addition_deletion_fun (General_functions.py:550-699) with native per-id kernels."""
-    chars = chars.sort_values(["id", "eom"], kind="stable").reset_index(drop=True)
+    ids = chars["id"].to_numpy(np.int64)
+    o = np.lexsort((month_index(chars["eom"]), ids))
+    if (np.diff(o) > 0).all():                         # already (id, eom) ordered (prepare_data)
+        chars = chars.copy(deep=False)
+    else:
+        chars = chars.take(o)
+    chars.index = pd.RangeIndex(len(chars))
     vt = (chars["valid_data"].to_numpy(bool) & chars["valid_size"].fillna(False).to_numpy(bool))
     gs = rt.group_starts(chars["id"].to_numpy(np.int64))
     add_cnt = rt.rolling_sum(vt.astype(np.float64), gs, addition_n)
@@ -201,7 +207,8 @@ def addition_deletion(chars: pd.DataFrame, addition_n: int, deletion_n: int) -> 
     log.info(f"Turnover wo addition/deletion rule: {round(agg['raw'].mean() * 100, 2)}%")
     log.info(f"Turnover w  addition/deletion rule: {round(agg['adj'].mean() * 100, 2)}%")
     chars["valid"] = valid
-    return chars.drop(columns=["valid_data", "valid_size"])
+    del chars["valid_data"], chars["valid_size"]
+    return chars
 
 
 def prepare_data(cfg: Config, write: bool = True) -> dict:
@@ -226,14 +233,21 @@ def prepare_data(cfg: Config, write: bool = True) -> dict:
 
     q = ("SELECT id, eom, sic, ff49, size_grp, me, crsp_exchcd, ret_exc, " + ", ".join(features)
          + " FROM Factors")
-    chars = io.sql_read(io.path(dd, "JKP_US_SP500.db"), q, parse_dates={"eom"})
+    raw = io.sql_read(io.path(dd, "JKP_US_SP500.db"), q, parse_dates={"eom"})
+    # the panel assembled from its columns in one go: replacing ~130 columns one by one
+    # leaves one pandas block per column (PerformanceWarning: highly fragmented) and every
+    # later take / filter pays per block
+    cols = {c: raw[c] for c in raw.columns}
     for f in features:
-        chars[f] = pd.to_numeric(chars[f], errors="coerce")
-    chars["id"] = chars["id"].astype("int64")
-    chars["sic"] = pd.to_numeric(chars["sic"], errors="coerce")
-    chars["dolvol"] = chars["dolvol_126d"]
-    chars["lambda"] = 2.0 / chars["dolvol"] * s["pi"]
-    chars["rvol_m"] = chars["rvol_252d"] * (21 ** 0.5)
+        if cols[f].dtype != np.float64:
+            cols[f] = pd.to_numeric(cols[f], errors="coerce")
+    cols["id"] = cols["id"].astype("int64")
+    cols["sic"] = pd.to_numeric(cols["sic"], errors="coerce")
+    cols["dolvol"] = cols["dolvol_126d"]
+    cols["lambda"] = 2.0 / cols["dolvol"] * s["pi"]
+    cols["rvol_m"] = cols["rvol_252d"] * (21 ** 0.5)
+    chars = pd.DataFrame(cols)
+    del raw, cols
     log.info("Chars Data Complete")
 
     # ---- lead / total returns (Prepare_Data.py:194-233) -------------------------------
@@ -255,20 +269,23 @@ def prepare_data(cfg: Config, write: bool = True) -> dict:
     key_l = ld["id"].to_numpy(np.int64) * 100000 + month_index(ld["eom"]).astype(np.int64)
     pos = pd.Index(key_l).get_indexer(key_c)
     hit = pos >= 0
+    add = {}
     for c in ("tr_ld0", "eom_ret", "ret_ld1", "tr_ld1"):
         v = ld[c].to_numpy()[np.where(hit, pos, 0)]
         if c == "eom_ret":
-            chars[c] = pd.Series(v, index=chars.index).where(hit)
+            add[c] = pd.Series(v, index=chars.index).where(hit)
         else:
-            chars[c] = np.where(hit, v, np.nan)
+            add[c] = np.where(hit, v, np.nan)
     log.info("Leading Returns Complete")
 
     wealth = wealth_func(pf["wealth"], s["split"]["test_end"], market, risk_free)
     ws = wealth[["eom", "mu_ld1"]].rename(columns={"mu_ld1": "mu_ld0"}).copy()
     ws["eom"] = ws["eom"] + pd.offsets.MonthEnd(1)
     wpos = pd.Index(ws["eom"]).get_indexer(chars["eom"])
-    chars["mu_ld0"] = np.where(wpos >= 0, ws["mu_ld0"].to_numpy()[np.where(wpos >= 0, wpos, 0)],
-                               np.nan)
+    add["mu_ld0"] = np.where(wpos >= 0, ws["mu_ld0"].to_numpy()[np.where(wpos >= 0, wpos, 0)],
+                             np.nan)
+    chars = pd.concat([chars.drop(columns=[c for c in add if c in chars.columns]),
+                       pd.DataFrame(add, index=chars.index)], axis=1)
     log.info("Wealth Evolution Complete.")
 
     # ---- screens (Prepare_Data.py:268-309): one keep-mask, the panel filtered once --------
@@ -301,21 +318,19 @@ def prepare_data(cfg: Config, write: bool = True) -> dict:
     # computed through a permutation instead)
     idx = np.nonzero(keep)[0]
     o = np.lexsort((month_index(chars["eom"].iloc[idx]), chars["id"].to_numpy(np.int64)[idx]))
-    chars = chars.take(idx[o]).reset_index(drop=True)
+    chars = chars.take(idx[o])
+    chars.index = pd.RangeIndex(len(chars))            # (reset_index would copy the panel again)
 
     # ---- percentile ranks + imputation (Prepare_Data.py:324-374) ----------------------
     if s["feat_prank"]:
         mi_rows = month_index(chars["eom"]).astype(np.int64)
         pe = np.lexsort((chars["id"].to_numpy(np.int64), mi_rows))      # (eom, id) order
         seg = rt.group_starts(mi_rows[pe])
-        X = chars[features].to_numpy(np.float64)[pe]
-        R = rt.pct_rank(X, seg)
-        R[X == 0.0] = 0.0                                  # quirk Q15: exact zeros stay 0
-        if s["feat_impute"]:
-            R[np.isnan(R)] = 0.5
-        Rb = np.empty_like(R)
-        Rb[pe] = R
-        chars[features] = Rb
+        # ranks within each month through the permutation, written back in panel order;
+        # quirk Q15: exact zeros stay 0; imputation: NaN ranks -> 0.5
+        Rb = rt.pct_rank_rows(chars[features].to_numpy(np.float64), pe, seg, zero_keep=True,
+                              impute=0.5 if s["feat_impute"] else None)
+        chars.loc[:, features] = Rb                    # in place: no per-column blocks
         log.info("Feature Rank Complete.")
         if s["feat_impute"]:
             log.info("Feature Imputation Complete.")

@@ -19,6 +19,8 @@ def declare(lib) -> None:
     lib.pfml_rolling_sum.restype = None
     lib.pfml_pct_rank.argtypes = [P, L, L, P, L, P]
     lib.pfml_pct_rank.restype = None
+    lib.pfml_pct_rank_rows.argtypes = [P, L, L, P, P, L, I, D, P]
+    lib.pfml_pct_rank_rows.restype = None
     lib.pfml_ewma_vol.argtypes = [P, P, L, D, I, P]
     lib.pfml_ewma_vol.restype = None
     lib.pfml_group_starts.argtypes = [P, L, P]
@@ -92,6 +94,22 @@ def pct_rank(x: np.ndarray, segments) -> np.ndarray:
     _lib().pfml_pct_rank(Xc.ctypes.data, Xc.shape[0], Xc.shape[1], seg.ctypes.data,
                          len(seg) - 1, out.ctypes.data)
     return out[:, 0].copy() if squeeze else np.ascontiguousarray(out)
+
+
+def pct_rank_rows(X: np.ndarray, perm, segments, zero_keep: bool = False,
+                  impute: float | None = None) -> np.ndarray:
+    """Percentile ranks of the row-major panel X [nrows, ncol] within the segments of the row
+    permutation ``perm`` (segment s = rows perm[segments[s]:segments[s + 1]]), written in X's
+    own row order; NaN preserved (or set to ``impute``), exact zeros ranked 0 with
+    ``zero_keep``."""
+    Xc = np.ascontiguousarray(X, dtype=np.float64)
+    pm = _c(perm, np.int64)
+    seg = _c(segments, np.int64)
+    out = np.empty_like(Xc)
+    _lib().pfml_pct_rank_rows(Xc.ctypes.data, Xc.shape[0], Xc.shape[1], pm.ctypes.data,
+                              seg.ctypes.data, len(seg) - 1, int(zero_keep),
+                              float("nan") if impute is None else float(impute), out.ctypes.data)
+    return out
 
 
 def ewma_vol(x, groups, lam: float, start: int) -> np.ndarray:

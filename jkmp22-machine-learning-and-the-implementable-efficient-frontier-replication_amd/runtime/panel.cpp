@@ -91,6 +91,62 @@ void pfml_pct_rank(const double* x, int64_t nrows, int64_t ncol, const int64_t* 
   }
 }
 
+// Percentile ranks of a row-major panel X [nrows, ncol] within segments of a row permutation
+// (Prepare_Data.py:324-374: groupby(eom).rank(pct=True) per feature): segment s holds the rows
+// perm[ss[s] .. ss[s+1]).  One task per segment gathers its rows once (contiguous row reads),
+// ranks every column (average ties / non-NaN count) and writes out[row][c] in the original row
+// order - no transposes or reordered copies of the panel.  zero_keep: exact zeros rank 0 (quirk
+// Q15); impute (not NaN): NaN ranks take that value.
+void pfml_pct_rank_rows(const double* X, int64_t nrows, int64_t ncol, const int64_t* perm,
+                        const int64_t* ss, int64_t nseg, int zero_keep, double impute,
+                        double* out) {
+  (void)nrows;
+  const double nan = std::numeric_limits<double>::quiet_NaN();
+  const bool imp = !std::isnan(impute);
+#pragma omp parallel
+  {
+    std::vector<double> buf;                       // [ncol][m] column-major segment copy
+    std::vector<double> res;
+    std::vector<int32_t> idx;
+#pragma omp for schedule(dynamic, 4)
+    for (int64_t s = 0; s < nseg; ++s) {
+      const int64_t a = ss[s], m = ss[s + 1] - a;
+      if (m <= 0) continue;
+      buf.resize((size_t)(m * ncol));
+      res.resize((size_t)(m * ncol));
+      for (int64_t i = 0; i < m; ++i) {
+        const double* row = X + perm[a + i] * ncol;
+        for (int64_t c = 0; c < ncol; ++c) buf[c * m + i] = row[c];
+      }
+      for (int64_t c = 0; c < ncol; ++c) {
+        const double* col = buf.data() + c * m;
+        double* rc = res.data() + c * m;
+        idx.clear();
+        for (int64_t i = 0; i < m; ++i) {
+          if (std::isnan(col[i])) rc[i] = imp ? impute : nan;
+          else idx.push_back((int32_t)i);
+        }
+        std::stable_sort(idx.begin(), idx.end(),
+                         [col](int32_t p, int32_t q) { return col[p] < col[q]; });
+        const double n = (double)idx.size();
+        size_t k = 0;
+        while (k < idx.size()) {
+          size_t e = k + 1;
+          while (e < idx.size() && col[idx[e]] == col[idx[k]]) ++e;
+          const double avg = 0.5 * ((double)(k + 1) + (double)e);   // mean of ranks k+1..e
+          const double r = (zero_keep && col[idx[k]] == 0.0) ? 0.0 : avg / n;
+          for (size_t q = k; q < e; ++q) rc[idx[q]] = r;
+          k = e;
+        }
+      }
+      for (int64_t i = 0; i < m; ++i) {
+        double* orow = out + perm[a + i] * ncol;
+        for (int64_t c = 0; c < ncol; ++c) orow[c] = res[c * m + i];
+      }
+    }
+  }
+}
+
 // Zero-mean EWMA volatility (numba ewma_vol, Estimate Covariance Matrix.py:345-386):
 // var[start] = sum(x[:start]^2 over non-NaN) / (count - 1); then
 // var[i] = lam var[i-1] + (1-lam) x[i-1]^2, carrying var forward over NaN x[i-1].

@@ -286,3 +286,26 @@ def test_universe_plot_and_counts(small_data):
     ref = chars.loc[chars["valid"].astype(bool)].groupby("eom").size()
     assert vc["N"].tolist() == ref.tolist()
     assert vc["N"].sum() == int(chars["valid"].sum())
+
+
+def test_pct_rank_rows_matches_pandas():
+    """Native segmented percentile ranks of a row-major panel (runtime/panel.cpp
+    pfml_pct_rank_rows) == pandas groupby(eom).rank(pct=True) per column, with exact zeros at
+    0 (quirk Q15) and NaN imputed to 0.5 (Prepare_Data.py:324-374)."""
+    from pfml import runtime as rt
+    rng = np.random.default_rng(3)
+    n, k = 4000, 6
+    X = rng.integers(-3, 4, size=(n, k)).astype(float) + rng.random((n, k)) * (rng.random((n, k)) < 0.5)
+    X[rng.random(X.shape) < 0.1] = np.nan
+    month = rng.integers(0, 30, n)
+    ids = rng.permutation(n)
+    pe = np.lexsort((ids, month))
+    seg = rt.group_starts(month[pe])
+    got = rt.pct_rank_rows(X, pe, seg, zero_keep=True, impute=0.5)
+    df = pd.DataFrame(X)
+    ref = df.groupby(month).rank(pct=True).to_numpy()
+    ref[X == 0.0] = 0.0
+    ref[np.isnan(ref)] = 0.5
+    assert np.allclose(got, ref, rtol=0, atol=1e-15)
+    raw = rt.pct_rank_rows(X, pe, seg)
+    assert np.array_equal(np.isnan(raw), np.isnan(X))

@@ -25,6 +25,7 @@ def timeit(fn, reps=5):
 def main():
     dev = torch.device("cuda", 0)
     shapes = [  # (batch, M, N, K, trans_a, horner_fusion)
+        (122, 490, 2006, 490, False, True),     # Horner step with the lag-1 block R (GP + 2N)
         (256, 496, 1522, 496, False, True),     # Horner step, 2 distinct g (GP = 1026)
         (256, 496, 1010, 496, False, True),     # Horner step, compat (GP = 514)
         (256, 496, 496, 496, False, False),     # x^2, DB products, inverse * Omega

@@ -22,6 +22,9 @@ for step in ${MODE//,/ }; do
     peak)
       timeout -k 10 120 ./tools/micro/mfma_f64_peak > $OUT/mfma_peak.json 2>&1
       rc=$?; cat $OUT/mfma_peak.json; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    gemm2)
+      timeout -k 10 400 python tools/bench_gemm2.py > $OUT/gemm2.log 2>&1
+      rc=$?; tail -1 $OUT/gemm2.log | cut -c1-3000; if [ $rc -ne 0 ]; then tail -5 $OUT/gemm2.log; exit $rc; fi ;;
     dgemm)
       timeout -k 10 200 python tools/micro/dgemm_rate.py > $OUT/dgemm_rate.json 2>&1
       rc=$?; tail -4 $OUT/dgemm_rate.json; if [ $rc -ne 0 ]; then exit $rc; fi ;;
