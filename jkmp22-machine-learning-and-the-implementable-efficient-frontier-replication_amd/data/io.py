@@ -118,15 +118,22 @@ def _native_read(db: str, query: str, parse_dates) -> pd.DataFrame | None:
         kinds = [lib.pfml_sql_col_kind(h, c) for c in range(ncol.value)]
         if any(k < 0 for k in kinds):
             return None
+        names = [lib.pfml_sql_col_name(h, c).decode() for c in range(ncol.value)]
+        # the float64 columns land in the rows of ONE [nf, n] array, which becomes the frame's
+        # single float block without a copy (a dict of columns gives one block per column:
+        # a "highly fragmented" frame whose every take / filter pays per column)
+        fcols = [c for c, k in enumerate(kinds) if k == 2]
+        F = np.empty((len(fcols), n), dtype=np.float64)
+        for j, c in enumerate(fcols):
+            lib.pfml_sql_col_f64(h, c, F[j].ctypes.data)
         cols = {}
         for c, k in enumerate(kinds):
-            name = lib.pfml_sql_col_name(h, c).decode()
+            name = names[c]
+            if k == 2:
+                continue
             if k == 1:
                 a = np.empty(n, dtype=np.int64)
                 lib.pfml_sql_col_i64(h, c, a.ctypes.data)
-            elif k == 2:
-                a = np.empty(n, dtype=np.float64)
-                lib.pfml_sql_col_f64(h, c, a.ctypes.data)
             elif k == 3:
                 nb = int(lib.pfml_sql_col_text_bytes(h, c))
                 buf = np.empty(max(nb, 1), dtype=np.uint8)
@@ -141,7 +148,10 @@ def _native_read(db: str, query: str, parse_dates) -> pd.DataFrame | None:
             cols[name] = a
     finally:
         lib.pfml_sql_free(h)
-    df = pd.DataFrame(cols, copy=False)
+    df = pd.DataFrame(F.T, columns=[names[c] for c in fcols], copy=False)
+    for c, name in enumerate(names):                   # the other columns at their positions
+        if kinds[c] != 2:
+            df.insert(c, name, cols[name])
     for c in (parse_dates or ()):
         if c in df.columns:
             df[c] = pd.to_datetime(df[c])

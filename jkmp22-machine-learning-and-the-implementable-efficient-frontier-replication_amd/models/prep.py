@@ -233,21 +233,23 @@ def prepare_data(cfg: Config, write: bool = True) -> dict:
 
     q = ("SELECT id, eom, sic, ff49, size_grp, me, crsp_exchcd, ret_exc, " + ", ".join(features)
          + " FROM Factors")
-    raw = io.sql_read(io.path(dd, "JKP_US_SP500.db"), q, parse_dates={"eom"})
-    # the panel assembled from its columns in one go: replacing ~130 columns one by one
-    # leaves one pandas block per column (PerformanceWarning: highly fragmented) and every
-    # later take / filter pays per block
-    cols = {c: raw[c] for c in raw.columns}
-    for f in features:
-        if cols[f].dtype != np.float64:
-            cols[f] = pd.to_numeric(cols[f], errors="coerce")
-    cols["id"] = cols["id"].astype("int64")
-    cols["sic"] = pd.to_numeric(cols["sic"], errors="coerce")
-    cols["dolvol"] = cols["dolvol_126d"]
-    cols["lambda"] = 2.0 / cols["dolvol"] * s["pi"]
-    cols["rvol_m"] = cols["rvol_252d"] * (21 ** 0.5)
-    chars = pd.DataFrame(cols)
-    del raw, cols
+    chars = io.sql_read(io.path(dd, "JKP_US_SP500.db"), q, parse_dates={"eom"})
+    # only columns that need a conversion are replaced, and all of them in one go: replacing
+    # ~130 columns one by one leaves one pandas block per column (PerformanceWarning: highly
+    # fragmented) and every later take / filter pays per block
+    conv = {f: pd.to_numeric(chars[f], errors="coerce") for f in features + ["sic"]
+            if chars[f].dtype != np.float64}
+    if chars["id"].dtype != np.int64:
+        conv["id"] = chars["id"].astype("int64")
+    if len(conv) > 8:
+        chars = pd.concat([chars.drop(columns=list(conv)), pd.DataFrame(conv)],
+                          axis=1)[list(chars.columns)]
+    else:                                   # a few new blocks (sic, id): no full-panel copy
+        for c, v in conv.items():
+            chars[c] = v
+    chars["dolvol"] = chars["dolvol_126d"]
+    chars["lambda"] = 2.0 / chars["dolvol"] * s["pi"]
+    chars["rvol_m"] = chars["rvol_252d"] * (21 ** 0.5)
     log.info("Chars Data Complete")
 
     # ---- lead / total returns (Prepare_Data.py:194-233) -------------------------------
@@ -284,8 +286,8 @@ def prepare_data(cfg: Config, write: bool = True) -> dict:
     wpos = pd.Index(ws["eom"]).get_indexer(chars["eom"])
     add["mu_ld0"] = np.where(wpos >= 0, ws["mu_ld0"].to_numpy()[np.where(wpos >= 0, wpos, 0)],
                              np.nan)
-    chars = pd.concat([chars.drop(columns=[c for c in add if c in chars.columns]),
-                       pd.DataFrame(add, index=chars.index)], axis=1)
+    for c, v in add.items():                # (five new columns: a few blocks, no panel copy)
+        chars[c] = v
     log.info("Wealth Evolution Complete.")
 
     # ---- screens (Prepare_Data.py:268-309): one keep-mask, the panel filtered once --------

@@ -404,7 +404,7 @@ def estimate_cov_frames_pandas(chars: pd.DataFrame, daily: pd.DataFrame, labels:
 
     # ---- daily merge with previous month's exposures (:168-183) ----------------------
     daily = daily[daily["date"] >= cm["eom"].min()]
-    daily["eom_ret"] = daily["date"] + pd.offsets.MonthEnd(0)
+    daily = daily.assign(eom_ret=daily["date"] + pd.offsets.MonthEnd(0))
     dm = cm.merge(daily[["id", "date", "ret_exc", "eom_ret"]], how="inner", on=["id", "eom_ret"])
     dm = dm.dropna()
     dm = dm.sort_values(["date", "id"], kind="stable").reset_index(drop=True)
