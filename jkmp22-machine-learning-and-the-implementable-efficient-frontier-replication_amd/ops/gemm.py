@@ -215,6 +215,10 @@ def _vec3(v, batch):
     return v2, (0 if (v2.shape[0] == 1 and batch > 1) else v2.stride(0))
 
 
+# A/B switch for the auto tile choice (0 auto, 1: 128x128, 2: 128x64, 3: 64x64), read once
+_TILE_DEFAULT = int(os.environ.get("PFML_GEMM_TILE", "0"))
+
+
 def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: bool = False,
                trans_b: bool = False, alpha: float = 1.0, beta: float = 0.0,
                row_scale: torch.Tensor | None = None, col_scale: torch.Tensor | None = None,
@@ -261,7 +265,8 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
                   nat.ptr(E3), 0 if E3 is None else E3.stride(1),
                   0 if E3 is None else _bstride(E3, batch), int(addend_cols or 0),
                   int(diag_col0 or 0), float(diag_value), nat.ptr(dv), sdv,
-                  int(diag_col0 is not None), nat.ptr(es), ses, int(sincos), int(tile_cfg))
+                  int(diag_col0 is not None), nat.ptr(es), ses, int(sincos),
+                  int(tile_cfg or _TILE_DEFAULT))
         nat.check(nat.hip_lib().pfml_dgemm_ex(
             int(trans_a), int(trans_b), M, N, K, batch,
             A3.data_ptr(), A3.stride(1), _bstride(A3, batch),

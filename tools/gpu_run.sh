@@ -22,6 +22,13 @@ for step in ${MODE//,/ }; do
     peak)
       timeout -k 10 120 ./tools/micro/mfma_f64_peak > $OUT/mfma_peak.json 2>&1
       rc=$?; cat $OUT/mfma_peak.json; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    s4tile)
+      # S4 with the 128 x 128 GEMM tile forced vs the auto choice (A / B / A)
+      for tc in 0 1 0 1; do
+        PFML_GEMM_TILE=$tc timeout -k 10 400 python bench.py --with-inputs --steps 1 --warmup 1 > $OUT/bench_s4_tile$tc.json 2> $OUT/bench_s4_tile$tc.err
+        rc=$?; echo "tile $tc: $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_s4_tile$tc.json)"
+        if [ $rc -ne 0 ]; then tail -3 $OUT/bench_s4_tile$tc.err; exit $rc; fi
+      done ;;
     gemm2)
       timeout -k 10 400 python tools/bench_gemm2.py > $OUT/gemm2.log 2>&1
       rc=$?; tail -1 $OUT/gemm2.log | cut -c1-3000; if [ $rc -ne 0 ]; then tail -5 $OUT/gemm2.log; exit $rc; fi ;;
