@@ -149,9 +149,16 @@ def _native_read(db: str, query: str, parse_dates) -> pd.DataFrame | None:
     finally:
         lib.pfml_sql_free(h)
     df = pd.DataFrame(F.T, columns=[names[c] for c in fcols], copy=False)
-    for c, name in enumerate(names):                   # the other columns at their positions
-        if kinds[c] != 2:
-            df.insert(c, name, cols[name])
+    import warnings
+    with warnings.catch_warnings():                    # (blocks merged once, below)
+        warnings.simplefilter("ignore", pd.errors.PerformanceWarning)
+        for c, name in enumerate(names):               # the other columns at their positions
+            if kinds[c] != 2:
+                df.insert(c, name, cols[name])
+    if len(names) - len(fcols) > 16:
+        # many int / text columns: merge their one-column blocks (the float block is alone
+        # in its dtype and stays as it is)
+        df._consolidate_inplace()
     for c in (parse_dates or ()):
         if c in df.columns:
             df[c] = pd.to_datetime(df[c])

@@ -309,7 +309,9 @@ def prepare_data(cfg: Config, write: bool = True) -> dict:
     screen(chars["tr_ld1"].notna() & chars["tr_ld0"].notna(), "Valid return req")
     screen(chars["dolvol"].notna() & (chars["dolvol"] > 0), "Non-missing/non-zero dolvol")
     screen(chars["sic"].notna(), "Valid SIC code")
-    avail = (~np.isnan(chars[features].to_numpy(np.float64))).sum(axis=1)
+    avail = np.zeros(len(chars), dtype=np.int64)       # column views: no panel copy
+    for f in features:
+        avail += ~np.isnan(chars[f].to_numpy(np.float64))
     min_feat = np.floor(len(features) * sc["feat_pct"])
     screen(avail >= min_feat, f"At least {sc['feat_pct'] * 100}% of feature")
     log.info(f"In total, the final dataset has {round(int(keep.sum()) / n_start * 100, 2)}% of the "

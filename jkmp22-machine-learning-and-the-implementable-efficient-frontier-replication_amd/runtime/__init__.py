@@ -19,7 +19,7 @@ def declare(lib) -> None:
     lib.pfml_rolling_sum.restype = None
     lib.pfml_pct_rank.argtypes = [P, L, L, P, L, P]
     lib.pfml_pct_rank.restype = None
-    lib.pfml_pct_rank_rows.argtypes = [P, L, L, P, P, L, I, D, P]
+    lib.pfml_pct_rank_rows.argtypes = [P, L, L, L, L, P, P, L, I, D, P, L, L]
     lib.pfml_pct_rank_rows.restype = None
     lib.pfml_ewma_vol.argtypes = [P, P, L, D, I, P]
     lib.pfml_ewma_vol.restype = None
@@ -102,13 +102,18 @@ def pct_rank_rows(X: np.ndarray, perm, segments, zero_keep: bool = False,
     permutation ``perm`` (segment s = rows perm[segments[s]:segments[s + 1]]), written in X's
     own row order; NaN preserved (or set to ``impute``), exact zeros ranked 0 with
     ``zero_keep``."""
-    Xc = np.ascontiguousarray(X, dtype=np.float64)
+    Xc = np.asarray(X, dtype=np.float64)
+    if Xc.ndim != 2 or not (Xc.flags.c_contiguous or Xc.flags.f_contiguous):
+        Xc = np.ascontiguousarray(Xc)
     pm = _c(perm, np.int64)
     seg = _c(segments, np.int64)
-    out = np.empty_like(Xc)
-    _lib().pfml_pct_rank_rows(Xc.ctypes.data, Xc.shape[0], Xc.shape[1], pm.ctypes.data,
-                              seg.ctypes.data, len(seg) - 1, int(zero_keep),
-                              float("nan") if impute is None else float(impute), out.ctypes.data)
+    out = np.empty_like(Xc)                  # same layout as X (C or Fortran order): no copies
+    xs = [st // 8 for st in Xc.strides]
+    os_ = [st // 8 for st in out.strides]
+    _lib().pfml_pct_rank_rows(Xc.ctypes.data, Xc.shape[0], Xc.shape[1], xs[0], xs[1],
+                              pm.ctypes.data, seg.ctypes.data, len(seg) - 1, int(zero_keep),
+                              float("nan") if impute is None else float(impute), out.ctypes.data,
+                              os_[0], os_[1])
     return out
 
 

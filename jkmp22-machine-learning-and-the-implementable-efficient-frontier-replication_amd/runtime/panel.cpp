@@ -97,9 +97,10 @@ void pfml_pct_rank(const double* x, int64_t nrows, int64_t ncol, const int64_t* 
 // ranks every column (average ties / non-NaN count) and writes out[row][c] in the original row
 // order - no transposes or reordered copies of the panel.  zero_keep: exact zeros rank 0 (quirk
 // Q15); impute (not NaN): NaN ranks take that value.
-void pfml_pct_rank_rows(const double* X, int64_t nrows, int64_t ncol, const int64_t* perm,
-                        const int64_t* ss, int64_t nseg, int zero_keep, double impute,
-                        double* out) {
+// Element (r, c) of X / out at r * rs + c * cs (row- or column-major, no reordered copy).
+void pfml_pct_rank_rows(const double* X, int64_t nrows, int64_t ncol, int64_t xrs, int64_t xcs,
+                        const int64_t* perm, const int64_t* ss, int64_t nseg, int zero_keep,
+                        double impute, double* out, int64_t ors, int64_t ocs) {
   (void)nrows;
   const double nan = std::numeric_limits<double>::quiet_NaN();
   const bool imp = !std::isnan(impute);
@@ -115,8 +116,8 @@ void pfml_pct_rank_rows(const double* X, int64_t nrows, int64_t ncol, const int6
       buf.resize((size_t)(m * ncol));
       res.resize((size_t)(m * ncol));
       for (int64_t i = 0; i < m; ++i) {
-        const double* row = X + perm[a + i] * ncol;
-        for (int64_t c = 0; c < ncol; ++c) buf[c * m + i] = row[c];
+        const double* row = X + perm[a + i] * xrs;
+        for (int64_t c = 0; c < ncol; ++c) buf[c * m + i] = row[c * xcs];
       }
       for (int64_t c = 0; c < ncol; ++c) {
         const double* col = buf.data() + c * m;
@@ -140,8 +141,8 @@ void pfml_pct_rank_rows(const double* X, int64_t nrows, int64_t ncol, const int6
         }
       }
       for (int64_t i = 0; i < m; ++i) {
-        double* orow = out + perm[a + i] * ncol;
-        for (int64_t c = 0; c < ncol; ++c) orow[c] = res[c * m + i];
+        double* orow = out + perm[a + i] * ors;
+        for (int64_t c = 0; c < ncol; ++c) orow[c * ocs] = res[c * m + i];
       }
     }
   }
