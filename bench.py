@@ -414,6 +414,7 @@ def main():
                 "global_batch": n_solves,
                 "seq_len": args.months,
                 "parallelism": f"dp{env.world_size}",
+                "dist_backend": env.backend if env.is_dist else "none",
                 "utilities_per_step": n_util,
                 "device": torch.cuda.get_device_name(dev) if dev.type == "cuda" else "cpu",
                 "setup_s": round(t_setup, 2),

@@ -22,10 +22,14 @@ class DistEnv:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: str = "none"
+    # PFML_DIST_FORCE=1: the distributed code path (process group, collectives, segmented
+    # graphs) even at world size 1 - on a one-GPU box this is how RCCL itself is exercised
+    force: bool = False
 
     @property
     def is_dist(self) -> bool:
-        return self.world_size > 1 and dist.is_available() and dist.is_initialized()
+        return ((self.world_size > 1 or self.force) and dist.is_available()
+                and dist.is_initialized())
 
     @property
     def is_main(self) -> bool:
@@ -52,7 +56,9 @@ def init(device: str = "auto", timeout_s: int = 600) -> DistEnv:
     else:
         dev = torch.device("cpu")
     backend = "none"
-    if ws > 1:
+    force = ws == 1 and os.environ.get("PFML_DIST_FORCE", "0") == "1"
+    if ws > 1 or force:
+        os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = "nccl" if dev.type == "cuda" else "gloo"
         # PFML_DIST_BACKEND=gloo with GPUs: ranks may share a device (a rehearsal of the
@@ -64,7 +70,8 @@ def init(device: str = "auto", timeout_s: int = 600) -> DistEnv:
                 kw["device_id"] = dev
             dist.init_process_group(backend=backend, rank=rank, world_size=ws,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
-    _ENV = DistEnv(rank=rank, world_size=ws, local_rank=lrank, device=dev, backend=backend)
+    _ENV = DistEnv(rank=rank, world_size=ws, local_rank=lrank, device=dev, backend=backend,
+                   force=force)
     return _ENV
 
 

@@ -264,3 +264,21 @@ def test_pipeline_fault_injection_two_ranks(fault, small_data, tmp_path):
             if a[c].dtype.kind in "fc":
                 assert np.allclose(a[c].to_numpy(), b[c].to_numpy(), rtol=1e-10, atol=1e-13,
                                    equal_nan=True), (name, c)
+
+
+def test_collectives_check_gloo_two_ranks():
+    """tools/rccl_check.py (every collective, host-staged reduce, p2p hand-off) under
+    torch.distributed.run with 2 gloo ranks on CPU; the GPU suite runs it over RCCL."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    envv = dict(os.environ, PFML_CHECK_DEVICE="cpu")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", "29581", os.path.join(root, "tools", "rccl_check.py")],
+                       capture_output=True, text=True, timeout=240, env=envv, cwd=root)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and lines, r.stdout[-2000:] + r.stderr[-3000:]
+    rec = json.loads(lines[-1])
+    assert rec["backend"] == "gloo" and rec["world_size"] == 2 and rec["all_ok"], rec

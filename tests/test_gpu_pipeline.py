@@ -205,3 +205,23 @@ def test_grid_step_hip_graph_replay_matches_eager(gpu):
     assert torch.equal(box["res"].obj, ref_obj)
     for s, r in zip(box["sc"], ref_rank):
         assert torch.equal(torch.nan_to_num(s[2], nan=-1.0), torch.nan_to_num(r, nan=-1.0))
+
+
+@pytest.mark.gpu
+def test_rccl_collectives_world1(gpu):
+    """Every collective of parallel/collectives.py through a real RCCL process group
+    (tools/rccl_check.py under torch.distributed.run; PFML_DIST_FORCE=1 takes the distributed
+    path at world size 1, the one configuration RCCL can run on a one-GPU box)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    envv = dict(os.environ, PFML_DIST_FORCE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
+                        "--master-port", "29547", os.path.join(root, "tools", "rccl_check.py")],
+                       capture_output=True, text=True, timeout=240, env=envv, cwd=root)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0 and lines, r.stdout[-2000:] + r.stderr[-3000:]
+    rec = json.loads(lines[-1])
+    assert rec["backend"] == "nccl" and rec["all_ok"], rec

@@ -29,6 +29,13 @@ for step in ${MODE//,/ }; do
         rc=$?; echo "tile $tc: $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_s4_tile$tc.json)"
         if [ $rc -ne 0 ]; then tail -3 $OUT/bench_s4_tile$tc.err; exit $rc; fi
       done ;;
+    rccl1)
+      # RCCL itself on a one-GPU box: the collectives check and the bench's distributed path
+      # (graph segments between RCCL collectives) as a forced world of one rank
+      PFML_DIST_FORCE=1 timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29561 tools/rccl_check.py > $OUT/rccl_check.log 2>&1
+      rc=$?; grep '^{' $OUT/rccl_check.log; if [ $rc -ne 0 ]; then tail -20 $OUT/rccl_check.log; exit $rc; fi
+      PFML_DIST_FORCE=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29562 bench.py --no-inputs > $OUT/bench_rccl1.json 2> $OUT/bench_rccl1.err
+      rc=$?; grep '^{' $OUT/bench_rccl1.json | cut -c1-200; grep -o '"dist_backend": "[a-z]*"\|"hip_graph": [a-z]*' $OUT/bench_rccl1.json; if [ $rc -ne 0 ]; then tail -5 $OUT/bench_rccl1.err; exit $rc; fi ;;
     gemm2)
       timeout -k 10 400 python tools/bench_gemm2.py > $OUT/gemm2.log 2>&1
       rc=$?; tail -1 $OUT/gemm2.log | cut -c1-3000; if [ $rc -ne 0 ]; then tail -5 $OUT/gemm2.log; exit $rc; fi ;;
