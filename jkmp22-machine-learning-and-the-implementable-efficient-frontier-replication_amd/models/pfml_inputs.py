@@ -35,6 +35,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import os
+
 import numpy as np
 import pandas as pd
 import torch
@@ -139,6 +141,7 @@ def auto_month_batch(n_stocks: int, gp: int, device, cap: int = 256) -> int:
     13-month signal window (13 N GP), five Horner buffers of N x (GP + N) plus two N x N blocks, ~8 N x N matrices of
     m_func / Sigma and the (25) scratch.  A device batch takes up to 60 % of free HBM (288 GB on
     MI355X: 256 months at N = 500, ~60 at N = 3000), a host batch 25 % of available RAM."""
+    cap = int(os.environ.get("PFML_S4_BATCH_CAP", cap))      # (A/B switch)
     per = 8.0 * (13.0 * n_stocks * gp + 6.0 * n_stocks * (gp + n_stocks) + 11.0 * n_stocks ** 2
                  + 2.0 * gp * gp)
     dev = torch.device(device)

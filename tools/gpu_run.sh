@@ -36,6 +36,13 @@ for step in ${MODE//,/ }; do
       rc=$?; grep '^{' $OUT/rccl_check.log; if [ $rc -ne 0 ]; then tail -20 $OUT/rccl_check.log; exit $rc; fi
       PFML_DIST_FORCE=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29562 bench.py --no-inputs > $OUT/bench_rccl1.json 2> $OUT/bench_rccl1.err
       rc=$?; grep '^{' $OUT/bench_rccl1.json | cut -c1-200; grep -o '"dist_backend": "[a-z]*"\|"hip_graph": [a-z]*' $OUT/bench_rccl1.json; if [ $rc -ne 0 ]; then tail -5 $OUT/bench_rccl1.err; exit $rc; fi ;;
+    s4cap)
+      # S4 months per batch: the default cap (256) vs all 731 months in one batch (A / B / A / B)
+      for cap in 256 1024 256 1024; do
+        PFML_S4_BATCH_CAP=$cap timeout -k 10 400 python bench.py --with-inputs --steps 1 --warmup 1 > $OUT/bench_s4_cap$cap.json 2> $OUT/bench_s4_cap$cap.err
+        rc=$?; echo "cap $cap: $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_s4_cap$cap.json) $(grep -o 'months per batch[^"]*' $OUT/bench_s4_cap$cap.err | head -1)"
+        if [ $rc -ne 0 ]; then tail -3 $OUT/bench_s4_cap$cap.err; exit $rc; fi
+      done ;;
     gemm2)
       timeout -k 10 400 python tools/bench_gemm2.py > $OUT/gemm2.log 2>&1
       rc=$?; tail -1 $OUT/gemm2.log | cut -c1-3000; if [ $rc -ne 0 ]; then tail -5 $OUT/gemm2.log; exit $rc; fi ;;
