@@ -208,20 +208,28 @@ def test_grid_step_hip_graph_replay_matches_eager(gpu):
 
 
 @pytest.mark.gpu
-def test_rccl_collectives_world1(gpu):
-    """Every collective of parallel/collectives.py through a real RCCL process group
-    (tools/rccl_check.py under torch.distributed.run; PFML_DIST_FORCE=1 takes the distributed
-    path at world size 1, the one configuration RCCL can run on a one-GPU box)."""
-    import json
-    import subprocess
+def test_rccl_collectives_world1(gpu, monkeypatch):
+    """Every collective of parallel/collectives.py through a real RCCL process group, in this
+    process: PFML_DIST_FORCE=1 takes the distributed path at world size 1, the one
+    configuration RCCL can run on a one-GPU box (tools/rccl_check.py; the driver step
+    `tools/gpu_run.sh rccl1` also runs bench.py that way under torch.distributed.run)."""
+    import socket
     import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    envv = dict(os.environ, PFML_DIST_FORCE="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                        "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
-                        "--master-port", "29547", os.path.join(root, "tools", "rccl_check.py")],
-                       capture_output=True, text=True, timeout=240, env=envv, cwd=root)
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert r.returncode == 0 and lines, r.stdout[-2000:] + r.stderr[-3000:]
-    rec = json.loads(lines[-1])
-    assert rec["backend"] == "nccl" and rec["all_ok"], rec
+    from pfml.parallel import dist as pdist
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "tools"))
+    import rccl_check
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    for k, v in {"PFML_DIST_FORCE": "1", "WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0",
+                 "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                 "PFML_CHECK_DEVICE": "cuda"}.items():
+        monkeypatch.setenv(k, v)
+    pdist.set_env(None)
+    try:
+        rec = rccl_check.run_checks()
+    finally:
+        pdist.shutdown()
+        pdist.set_env(None)
+    assert rec["backend"] == "nccl" and rec["forced"] and rec["all_ok"], rec

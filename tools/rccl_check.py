@@ -18,7 +18,8 @@ from pfml.parallel import collectives as coll  # noqa: E402
 from pfml.parallel import dist as pdist  # noqa: E402
 
 
-def main():
+def run_checks() -> dict:
+    """The checks on the process group of pdist.init (rank 0's record; every rank returns)."""
     want = os.environ.get("PFML_CHECK_DEVICE", "cuda")        # (cpu: gloo dry run of the logic)
     env = pdist.init(want)
     assert env.is_dist and env.backend == ("nccl" if want == "cuda" else "gloo"), env
@@ -51,12 +52,17 @@ def main():
     pdist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
-    if env.is_main:
-        print(json.dumps({"backend": env.backend, "world_size": W, "forced": env.force,
-                          "rccl": str(torch.cuda.nccl.version()) if dev.type == "cuda" else None,
-                          "checks": ok, "all_ok": all(ok.values())}), flush=True)
+    return {"backend": env.backend, "world_size": W, "forced": env.force,
+            "rccl": str(torch.cuda.nccl.version()) if dev.type == "cuda" else None,
+            "checks": ok, "all_ok": all(ok.values()), "main": env.is_main}
+
+
+def main():
+    rec = run_checks()
+    if rec.pop("main"):
+        print(json.dumps(rec), flush=True)
     pdist.shutdown()
-    return 0 if all(ok.values()) else 1
+    return 0 if rec["all_ok"] else 1
 
 
 if __name__ == "__main__":
