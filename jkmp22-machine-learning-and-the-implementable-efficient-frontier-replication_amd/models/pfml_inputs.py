@@ -136,11 +136,12 @@ def vol_scales(panel: Panel, barra: BarraCov, months: np.ndarray) -> np.ndarray:
     return s.fillna(med).to_numpy()
 
 
-def auto_month_batch(n_stocks: int, gp: int, device, cap: int = 256) -> int:
+def auto_month_batch(n_stocks: int, gp: int, device, cap: int = 1024) -> int:
     """Months per S4 batch from the memory one month's working set needs (fp64): the
     13-month signal window (13 N GP), five Horner buffers of N x (GP + N) plus two N x N blocks, ~8 N x N matrices of
     m_func / Sigma and the (25) scratch.  A device batch takes up to 60 % of free HBM (288 GB on
-    MI355X: 256 months at N = 500, ~60 at N = 3000), a host batch 25 % of available RAM."""
+    MI355X: all 731 months at N = 500 in one batch - 23 ms faster than 256-month batches,
+    profiles/r03_s4_batch_cap_ab.json - ~100 at N = 3000), a host batch 25 % of available RAM."""
     cap = int(os.environ.get("PFML_S4_BATCH_CAP", cap))      # (A/B switch)
     per = 8.0 * (13.0 * n_stocks * gp + 6.0 * n_stocks * (gp + n_stocks) + 11.0 * n_stocks ** 2
                  + 2.0 * gp * gp)
