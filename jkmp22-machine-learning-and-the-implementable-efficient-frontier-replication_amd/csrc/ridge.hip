@@ -915,7 +915,8 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
                                              const double* lvec, int L, double* work,
                                              double* beta_out, int64_t ldo, int band_mode,
                                              long long* tim, int* lu_list, int* lu_count,
-                                             int lu_cap, hipStream_t st);
+                                             int lu_cap, const int* wgmap, int nwg,
+                                             unsigned* syncw, hipStream_t st);
 
 // Workspace per cell: enough for whichever path the launcher picks (band path: ridge_band.hip).
 extern "C" int64_t pfml_ridge_work_doubles(int n, int L) {
@@ -939,9 +940,11 @@ extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const doubl
                                       const void* cells, int ncells, int nmax,
                                       const double* lvec, int L, double* work, double* beta_out,
                                       int64_t ldo, int band_mode, int* lu_list, int* lu_count,
-                                      int lu_cap, hipStream_t st) {
+                                      int lu_cap, const int* wgmap, int nwg, unsigned* syncw,
+                                      hipStream_t st) {
   if (ncells <= 0) return hipSuccess;
   if (L > 128 || nmax > NMAX) return hipErrorInvalidValue;
+  if (band_mode == 4 && nmax > pfml_ridge_band_nmax()) return hipErrorInvalidValue;
   const CellDesc* cd = static_cast<const CellDesc*>(cells);
   // PFML_RIDGE_VARIANT: band (default) | tridiag-fast | unblocked | blocked
   const char* var = getenv("PFML_RIDGE_VARIANT");
@@ -952,7 +955,7 @@ extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const doubl
       nmax <= pfml_ridge_band_nmax())
     return pfml_ridge_band_launch(SD, ldS, Sr, cells, ncells, nmax, lvec, L, work, beta_out,
                                   ldo, band_mode, g_ridge_timing, lu_list, lu_count, lu_cap,
-                                  st);
+                                  wgmap, nwg, syncw, st);
   if (force_unblocked || (getenv("PFML_RIDGE_UNBLOCKED") != nullptr))
     hipLaunchKernelGGL(ridge_tridiag_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr, cd, L,
                        work);

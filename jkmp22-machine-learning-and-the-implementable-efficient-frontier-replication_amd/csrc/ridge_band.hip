@@ -317,14 +317,16 @@ __device__ __forceinline__ void cqr_apply(double (*Vs)[LS], const double (&x)[BB
 __device__ __forceinline__ bool band_panel_cqr(double* __restrict__ A, int n, int k0, int r0,
                                                int m, double (*Vs)[LS], double* redf,
                                                double (*Ts)[LS], double* __restrict__ Tglob,
-                                               long long* tk) {
+                                               long long* tk, const double (*Pn)[LS]) {
   if (m < BB) return false;
   const int t = threadIdx.x, lane = t & 63;
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
   const int c16 = lane & 15, g4 = lane >> 4;
   // ---- P = rows k0..k0+15, columns r0.. of the symmetric A, transposed into Vs (32 lanes
-  //      per row: 256 B contiguous per load); rows >= m are zero
-  {
+  //      per row: 256 B contiguous per load); rows >= m are zero.  With Pn (== Vs: the
+  //      panel already in LDS, rows >= m zero) nothing moves; on a rejection the Householder
+  //      fallback re-reads the panel, so Pn is not overwritten before the accept tests.
+  if (Pn == nullptr) {
     const int c = t >> 5, il = t & 31;
     const double* src = A + (int64_t)(k0 + c) * n + r0;
     double a[16];
@@ -463,13 +465,46 @@ __device__ __forceinline__ bool band_panel_cqr(double* __restrict__ A, int n, in
 // (dlarft) -> Ts and Tglob.  Ends with a barrier.  `redf` needs 2 x 256 + 32 doubles.
 // `n` is A's leading dimension.  `Pn` (fused path): the panel is read from this LDS image
 // (Pn[i][c] = panel row i, column c; it may alias Vs) instead of A's mirror row.
+__device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int k0, int r0,
+                                              int m, double (*Vs)[LS], double (*Gs)[LS],
+                                              double* redf, double (*Ts)[LS], double* taus,
+                                              double* __restrict__ Tglob, long long* tk,
+                                              const double (*Pn)[LS]);
+
+// The Householder form as a call of its own: the CholeskyQR2 path's fallback, so that the two
+// forms do not share one register allocation (inlined together they spilled 344 B per lane)
+__device__ __noinline__ void band_panel_hh_call(double* __restrict__ A, int n, int k0, int r0,
+                                                int m, double (*Vs)[LS], double (*Gs)[LS],
+                                                double* redf, double (*Ts)[LS], double* taus,
+                                                double* __restrict__ Tglob, long long* tk,
+                                                const double (*Pn)[LS]) {
+  band_panel_hh(A, n, k0, r0, m, Vs, Gs, redf, Ts, taus, Tglob, tk, Pn);
+}
+
 __device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n, int k0, int r0,
                                                   int m, double (*Vs)[LS], double (*Gs)[LS],
                                                   double* redf, double (*Ts)[LS], double* taus,
                                                   double* __restrict__ Tglob, bool qr_fast,
                                                   long long* tk = nullptr,
-                                                  const double (*Pn)[LS] = nullptr) {
-  if (qr_fast && band_panel_cqr(A, n, k0, r0, m, Vs, redf, Ts, Tglob, tk)) return;
+                                                  const double (*Pn)[LS] = nullptr,
+                                                  const double (*Pcopy)[LS] = nullptr) {
+  // qr_fast with the panel in LDS: Pn must be Vs (factored in place) and Pcopy an untouched
+  // copy of it for the Householder fallback (not Gs's rows 0..15, which that fallback writes
+  // only after it has read the panel)
+  if (qr_fast) {
+    if (band_panel_cqr(A, n, k0, r0, m, Vs, redf, Ts, Tglob, tk, Pn)) return;
+    band_panel_hh_call(A, n, k0, r0, m, Vs, Gs, redf, Ts, taus, Tglob, tk,
+                       Pn != nullptr ? Pcopy : nullptr);
+    return;
+  }
+  band_panel_hh(A, n, k0, r0, m, Vs, Gs, redf, Ts, taus, Tglob, tk, Pn);
+}
+
+__device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int k0, int r0,
+                                              int m, double (*Vs)[LS], double (*Gs)[LS],
+                                              double* redf, double (*Ts)[LS], double* taus,
+                                              double* __restrict__ Tglob, long long* tk,
+                                              const double (*Pn)[LS]) {
   const int t = threadIdx.x, lane = t & 63;
   const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
   const int cq = t & 15, rg = t >> 4;
@@ -986,6 +1021,543 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
   for (int e = t_; e < n * LS; e += NTR) {
     const int r = e / LS, c = r - BB + e % LS;
     bw.LB[e] = (c >= 0) ? A[(int64_t)r * lda + c] : 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// kernel 1, cooperative form (band_mode 4, the production form): K workgroups per cell in
+// ONE launch, K chosen per cell by the host (ops/ridge.py::coop_plan) so that a launch fills
+// the chip whether it holds 106 big cells (one GPU) or 13 (one rank of eight).  The results
+// are BITWISE independent of K: every value has one producer whose arithmetic does not
+// depend on which workgroup runs it, and every cross-block sum runs over per-block partials in
+// a fixed block order.  So a 1-GPU and an N-GPU grid search pick the same hyper-parameters
+// (PFML_hp_reals.py:118-122 dense rank, PFML_best_hps.py:275 first rank).
+//
+// Work units are 16-row blocks of the trailing matrix A22 (lower-triangle semantics; every
+// off-diagonal tile is mirrored, as in ridge_band_reduce_kernel).  Per panel p:
+//
+//   B  every WG   U = V_p T_p (LDS), X_I = A22 U for the blocks I = gb (mod K) it owns in the
+//                 X phase (gb = global block), partials V_I' X_I and V_I' z_I per block
+//   C  every WG   P = sum_I V_I' X_I and V'z in block order, M = T' P, z_I -= V_I T' V'z,
+//                 W_I = X_I - V_I M / 2 for its X blocks
+//   D  QR WG      look-ahead: the tiles (I, 0) of A22 ARE panel p+1; it applies update p to
+//                 them in registers and factors panel p+1 (band_panel_factor) while
+//      others     apply A22 -= V W' + W V' to their update blocks, tiles (I, J), 1 <= J <= I
+//                 (tile (0, 0): the diagonal band block)
+//
+// With K = 1 the one workgroup runs D's update first, then the look-ahead panel: the same
+// operations in the same order.  Hand-offs between the workgroups of a cell
+// (cdna_hip_programming.md Guideline 16): every handed-off byte is stored write-through (sc1:
+// 8- and 16-byte buffer stores through descriptors on the cell's workspace), every storing
+// wave drains (s_waitcnt vmcnt(0)) before the workgroup barrier behind which one lane adds to
+// the cell's arrival counter; consumers poll that counter relaxed and read the small payloads
+// (V, T, W, partials, z) with sc1 loads; the matrix reads of the X phase follow one agent-scope
+// acquire per panel.  Spins are bounded: a timeout sets the cell's error word, every later
+// wait of the workgroup returns at once and the launch drains (the host reads the word in
+// tests; results are then garbage, never a hang).
+// ---------------------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int COOP_SYNC = 32;               // u32 words of sync state per cell (128 B)
+constexpr unsigned COOP_SPIN_MAX = 1u << 22;
+
+// hand-off scratch of one cell (in BandWork's F region: 2 npad x 16 + 256 + 33 x 272 doubles)
+struct CoopWork {
+  double *Vg, *Wg, *Tg, *Pg, *Pzg;
+  __device__ CoopWork(double* f, int npad) {
+    Vg = f;                                  // V_p rows 0..m-1 (published by the QR WG)
+    Wg = Vg + (int64_t)npad * BB;            // W_p rows (every WG its X blocks)
+    Tg = Wg + (int64_t)npad * BB;            // T_p
+    Pg = Tg + BB * BB;                       // per block V_I' X_I  [33][256]
+    Pzg = Pg + (BNMAX / BB) * BB * BB;       // per block V_I' z_I  [33][16]
+  }
+};
+
+struct CoopSync {
+  gu32* ctr;
+  gu32* err;
+  int K;
+  unsigned epoch;
+  // Every thread of the workgroup calls it; returns with the cell's K workgroups past the
+  // same point.  acquire: one agent-scope acquire behind the poll (plain loads of other
+  // workgroups' matrix tiles follow).
+  __device__ __forceinline__ void sync(bool acquire, int* err_s) {
+    ++epoch;
+    if (K == 1) {
+      __syncthreads();
+      return;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its sc1 stores are out
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = (unsigned)K * epoch;
+      unsigned spins = 0;
+      bool bad = *err_s != 0;
+      while (!bad && __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins >= COOP_SPIN_MAX) {
+          bad = true;
+          *err_s = 1;
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      if (acquire) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+  }
+};
+
+// X_I += A22[k][I cols] U[k][:] for the NQ blocks blk[] of this wave (band_x_accum with an
+// explicit block list).
+template <int NQ>
+__device__ __forceinline__ void coop_x_accum(const double* __restrict__ A, int lda, int r0,
+                                             int m, const int (&blk)[4], int c16, int g4,
+                                             const double (*__restrict__ Us)[LS],
+                                             double4_t (&X)[4]) {
+  int col[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) col[q] = min(blk[q] * 16 + c16, m - 1);
+  for (int k = 0; k < m; k += 32) {
+    double a[8][NQ], b[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double* arow = A + (int64_t)(r0 + min(k + 4 * u + g4, m - 1)) * lda + r0;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) a[u][q] = arow[col[q]];
+      b[u] = Us[k + 4 * u + g4][c16];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) X[q] = mfma_f64_16x16x4(a[u][q], b[u], X[q]);
+  }
+}
+
+template <bool TIMED>
+__global__ __launch_bounds__(NTR) void band_coop_kernel(
+    const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
+    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work,
+    const int* __restrict__ wgmap, unsigned* __restrict__ syncw, long long* __restrict__ tim) {
+  __shared__ double Vs[BMP][LS];       // V_p (rows >= m zero); the QR WG: panel p+1, V_{p+1}
+  __shared__ double Ws[BMP][LS];       // U = V T, then W
+  __shared__ double red[NWR][BB * BB]; // QR scratch, canonical sums, update transposes
+  __shared__ double Ts[BB][LS];
+  __shared__ double taus[BB];
+  __shared__ double zts[BB];
+  __shared__ int err_s;
+
+  const int code = wgmap[blockIdx.x];
+  const int cell = code >> 8, w = (code >> 4) & 15, K = (code & 15) + 1;
+  const RidgeCellDesc cd = cells[cell];
+  const int n = cd.n;
+  const int lda = band_npad(n), nb = lda / BB;
+  const int npan = (n - 1) / BB;                 // panels: k0 = 16 p with k0 + 16 < n
+  const int t_ = threadIdx.x, lane_ = t_ & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(t_ >> 6);
+  BandWork bw(work + cd.work, n, L);
+  CoopWork cw(bw.F, lda);
+  double* __restrict__ A = bw.A;
+  CoopSync cs{(gu32*)(syncw + (int64_t)cell * COOP_SYNC),
+              (gu32*)(syncw + (int64_t)cell * COOP_SYNC + 1), K, 0u};
+  const bool qwg = (w == 0);
+  const int Ku = K > 1 ? K - 1 : 1;            // update workgroups: all but the QR one
+  const int wu = K > 1 ? w - 1 : 0;            // (-1: the QR workgroup when K > 1)
+  // 16-byte write-through stores of the matrix tiles through a buffer descriptor on A (a
+  // masked store gets an offset past the range and is dropped by the range check)
+  const unsigned abytes = (unsigned)lda * (unsigned)lda * 8u;
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc(A, 0, (int)abytes, 0x00020000);
+  auto st2 = [&](unsigned off, bool ok, double x, double y) {
+    const double2 v = make_double2(x, y);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsA,
+                                           ok ? off : abytes, 0, 16);
+  };
+  // the hand-off words (V, T, W, partials, z) through a descriptor on the cell's workspace:
+  // write-through (sc1) 8-byte buffer stores and sc1 buffer loads (not atomics: a loop's loads
+  // are all in flight before the first wait)
+  const auto rsW = __builtin_amdgcn_make_buffer_rsrc(A, 0, 0x7ffffff0, 0x00020000);
+  auto ldw = [&](const double* p) -> double {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                          rsW, (unsigned)((p - A) * 8), 0, 16));
+  };
+  auto stw = [&](double* p, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), rsW,
+                                          (unsigned)((p - A) * 8), 0, 16);
+  };
+  long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long tlast = 0;
+#define COOP_TMARK(ph)                                                   \
+  if (TIMED && threadIdx.x == 0) {                                       \
+    const long long now = (long long)__builtin_amdgcn_s_memtime();       \
+    tacc[ph] += now - tlast;                                             \
+    tlast = now;                                                         \
+  }
+  if (t_ == 0) err_s = 0;
+
+  // ---- A = S * scale (both triangles, zero padding), z = r * scale: row blocks gb = w (mod K)
+  {
+    const double* S = SD + cd.src;
+    const double sc = cd.scale;
+    for (int gb = w; gb < nb; gb += K) {
+      for (int e = t_; e < BB * (lda / 2); e += NTR) {
+        const int i = 16 * gb + e / (lda / 2), j = 2 * (e % (lda / 2));
+        const double* srow = S + (int64_t)min(i, n - 1) * ldS;
+        const double x = (i < n && j < n) ? srow[j] * sc : 0.0;
+        const double y = (i < n && j + 1 < n) ? srow[j + 1] * sc : 0.0;
+        st2((unsigned)((i * lda + j) * 8), true, x, y);
+      }
+      if (t_ < BB && 16 * gb + t_ < n) stw(bw.z + 16 * gb + t_, Sr[cd.rsrc + 16 * gb + t_] * sc);
+    }
+  }
+  cs.sync(true, &err_s);
+  if (TIMED && threadIdx.x == 0) tlast = (long long)__builtin_amdgcn_s_memtime();
+
+  // ---- panel 0 (the QR workgroup): column block 0, rows 16.., then publish V_0, T_0
+  auto publish_vt = [&](int mp) {
+    for (int e = t_; e < mp * BB; e += NTR) stw(cw.Vg + e, Vs[e / BB][e % BB]);
+    if (t_ < BB * BB) stw(cw.Tg + t_, Ts[t_ / BB][t_ % BB]);
+  };
+  if (npan > 0 && qwg) {
+    const int m0 = n - BB;
+    for (int e = t_; e < BMP * BB; e += NTR) {
+      const int i = e / BB, c = e % BB;
+      Vs[i][c] = (i < m0) ? A[(int64_t)(BB + i) * lda + c] : 0.0;
+    }
+    __syncthreads();
+    band_panel_factor(A, lda, 0, BB, m0, Vs, Ws, &red[0][0], Ts, taus, bw.T, false, nullptr, Vs);
+    if (K > 1) publish_vt(m0);
+  }
+  if (npan > 0) cs.sync(false, &err_s);
+  COOP_TMARK(0)
+
+  for (int p = 0; p < npan; ++p) {
+    const int k0 = p * BB, r0 = k0 + BB, m = n - r0;
+    const int nI = (m + 15) >> 4;
+    int t = t_, lane = lane_;
+    asm volatile("" : "+v"(t), "+v"(lane));
+    const int c16 = lane & 15, g4 = lane >> 4;
+    // ---- B: V_p, T_p (the other workgroups load the published copy), U = V T -> Ws
+    if (!qwg) {
+      double v[BMP * BB / NTR];
+#pragma unroll
+      for (int u = 0; u < BMP * BB / NTR; ++u) v[u] = ldw(cw.Vg + min(t + NTR * u, m * BB - 1));
+      const double tv = ldw(cw.Tg + (t & (BB * BB - 1)));
+#pragma unroll
+      for (int u = 0; u < BMP * BB / NTR; ++u) {
+        const int e = t + NTR * u, i = e / BB;
+        Vs[i][e % BB] = (i < m) ? v[u] : 0.0;
+      }
+      if (t < BB * BB) Ts[t / BB][t % BB] = tv;
+      __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < BMP / 16 / NWR; ++q) {
+      const int i0 = (wid + NWR * q) * 16;
+      double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vs[i0 + c16][4 * r + g4], Ts[4 * r + g4][c16], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Ws[i0 + g4 + 4 * r][c16] = acc[r];
+    }
+    __syncthreads();
+    COOP_TMARK(1)
+    // X blocks of this workgroup: I = first + (wid + 8 q) K
+    const int first = ((w - (p + 1)) % K + K) % K;
+    int blk[4];
+    int nq = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      blk[q] = first + (wid + NWR * q) * K;
+      nq += (blk[q] < nI) ? 1 : 0;
+    }
+    double4_t X[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) X[q] = double4_t{0.0, 0.0, 0.0, 0.0};
+    switch (nq) {
+      case 1: coop_x_accum<1>(A, lda, r0, m, blk, c16, g4, Ws, X); break;
+      case 2: coop_x_accum<2>(A, lda, r0, m, blk, c16, g4, Ws, X); break;
+      case 3: coop_x_accum<3>(A, lda, r0, m, blk, c16, g4, Ws, X); break;
+      case 4: coop_x_accum<4>(A, lda, r0, m, blk, c16, g4, Ws, X); break;
+      default: break;
+    }
+    // per-block partials V_I' X_I and V_I' z_I (z as column 0 of the B operand)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q < nq) {
+        const int i0 = 16 * blk[q];
+        double4_t Pp = {0.0, 0.0, 0.0, 0.0}, Pz = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i0 + 4 * r + g4;
+          const double va = Vs[row][c16];
+          Pp = mfma_f64_16x16x4(va, X[q][r], Pp);
+          const double zl = ldw(bw.z + r0 + min(row, m - 1));
+          const double zb = (c16 == 0 && row < m) ? zl : 0.0;
+          Pz = mfma_f64_16x16x4(va, zb, Pz);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          stw(cw.Pg + (int64_t)blk[q] * (BB * BB) + (g4 + 4 * r) * BB + c16, Pp[r]);
+          if (c16 == 0) stw(cw.Pzg + blk[q] * BB + g4 + 4 * r, Pz[r]);
+        }
+      }
+    }
+    COOP_TMARK(2)
+    cs.sync(false, &err_s);
+    COOP_TMARK(3)
+    // ---- C: canonical sums (block order), M = T' P, z and W of the X blocks
+    if (t < BB * BB + BB) {
+      // (all nI partials in flight, then summed in block order)
+      const bool isP = t < BB * BB;
+      const double* base = isP ? cw.Pg + t : cw.Pzg + (t - BB * BB);
+      const int stride = isP ? BB * BB : BB;
+      constexpr int NB = BNMAX / BB;
+      double v[NB];
+#pragma unroll
+      for (int I = 0; I < NB; ++I) v[I] = ldw(base + min(I, nI - 1) * stride);
+      double s = 0.0;
+#pragma unroll
+      for (int I = 0; I < NB; ++I) s = (I < nI) ? s + v[I] : s;
+      if (isP) red[0][t] = s;
+      else red[1][t - BB * BB] = s;
+    }
+    __syncthreads();
+    if (t < BB) {
+      double s = 0.0;
+      for (int a = 0; a <= t; ++a) s = fma(Ts[a][t], red[1][a], s);
+      zts[t] = s;
+    }
+    double4_t Mm = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      Mm = mfma_f64_16x16x4(Ts[4 * r + g4][c16], red[0][(4 * r + g4) * BB + c16], Mm);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (q < nq) {
+        const int i0 = 16 * blk[q];
+        if (lane < BB && i0 + lane < m) {
+          const int i = i0 + lane;
+          double s = 0.0;
+#pragma unroll
+          for (int c = 0; c < BB; ++c) s = fma(Vs[i][c], zts[c], s);
+          stw(bw.z + r0 + i, ldw(bw.z + r0 + i) - s);
+        }
+        double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vs[i0 + c16][4 * r + g4], Mm[r], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + g4 + 4 * r;
+          stw(cw.Wg + i * BB + c16, (i < m) ? X[q][r] - 0.5 * acc[r] : 0.0);
+        }
+      }
+    }
+    COOP_TMARK(4)
+    cs.sync(false, &err_s);
+    COOP_TMARK(3)
+    // ---- D: W -> Ws; update (update workgroups) / look-ahead panel p+1 (QR workgroup)
+    {
+      double v[BMP * BB / NTR];
+#pragma unroll
+      for (int u = 0; u < BMP * BB / NTR; ++u) v[u] = ldw(cw.Wg + min(t + NTR * u, nI * BB * BB - 1));
+#pragma unroll
+      for (int u = 0; u < BMP * BB / NTR; ++u) {
+        const int e = t + NTR * u;
+        if (e < nI * BB * BB) Ws[e / BB][e % BB] = v[u];
+      }
+    }
+    __syncthreads();
+    auto update = [&]() {
+      // rows I = first_u + pos Ku (pos: snake over the waves), tiles J = (I ? 1 : 0) .. I,
+      // TBR tiles per chunk, next chunk's tiles loaded before this chunk's MFMAs (the
+      // one-workgroup kernel's trailing loop; stores through the buffer descriptor)
+      const int first_u = ((wu - (p + 1)) % Ku + Ku) % Ku;
+      auto row_of = [&](int rr) {
+        const int pos = 2 * NWR * (rr >> 1) + ((rr & 1) ? (2 * NWR - 1 - wid) : wid);
+        return first_u + pos * Ku;
+      };
+      double4_t nxt[TBR];
+      auto fetch = [&](int I, int J0) {
+#pragma unroll
+        for (int u = 0; u < TBR; ++u) {
+          const int J = J0 + u;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = 16 * I + g4 + 4 * r, jj = 16 * J + c16;
+            nxt[u][r] = A[(int64_t)(r0 + min(i, m - 1)) * lda + r0 + min(jj, m - 1)];
+          }
+        }
+      };
+      int rr = 0, I = row_of(0);
+      while (rr < 4 && I >= nI) I = row_of(++rr);
+      if (rr >= 4) I = nI;
+      int J0 = (I == 0) ? 0 : 1;
+      auto advance = [&]() {
+        J0 += TBR;
+        if (J0 > I) {
+          do I = row_of(++rr);
+          while (rr < 4 && I >= nI);
+          if (rr >= 4) I = nI;
+          J0 = (I == 0) ? 0 : 1;
+        }
+      };
+      fetch(I, J0);
+      double* tw = &red[0][0] + wid * (BB * BB);
+      double4_t acc[TBR];
+#pragma unroll
+      for (int u = 0; u < TBR; ++u) acc[u] = nxt[u];
+#pragma unroll
+      for (int u = 0; u < TBR; ++u) asm volatile("" ::"v"(acc[u]));
+      int ci = I, cj = J0;
+      advance();
+      while (ci < nI) {
+        fetch(I, J0);
+        double aV[4], aW[4], bW[TBR][4], bV[TBR][4];
+        const int ia = 16 * ci + c16;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          aV[s] = -Vs[ia][4 * s + g4];
+          aW[s] = -Ws[ia][4 * s + g4];
+        }
+#pragma unroll
+        for (int u = 0; u < TBR; ++u) {
+          const int jb = 16 * min(cj + u, ci) + c16;
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            bW[u][s] = Ws[jb][4 * s + g4];
+            bV[u][s] = Vs[jb][4 * s + g4];
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int u = 0; u < TBR; ++u) acc[u] = mfma_f64_16x16x4(aV[s], bW[u][s], acc[u]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int u = 0; u < TBR; ++u) acc[u] = mfma_f64_16x16x4(aW[s], bV[u][s], acc[u]);
+#pragma unroll
+        for (int u = 0; u < TBR; ++u) {
+          const int J = cj + u;
+          const bool live = J <= ci;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = g4 + 4 * r;
+            tw[row * BB + (c16 ^ (row & ~1))] = acc[u][r];
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          {
+            const int pr = lane >> 3, pc = 2 * (lane & 7);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int row = pr + 8 * h;
+              const double2 v = *reinterpret_cast<const double2*>(&tw[row * BB + (pc ^ (row & ~1))]);
+              st2((unsigned)(((r0 + 16 * ci + row) * lda + r0 + 16 * J + pc) * 8), live, v.x, v.y);
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int col = pr + 8 * h;
+              const double x = tw[pc * BB + (col ^ (pc & ~1))];
+              const double y = tw[(pc + 1) * BB + (col ^ ((pc + 1) & ~1))];
+              st2((unsigned)(((r0 + 16 * J + col) * lda + r0 + 16 * ci + pc) * 8),
+                  live && J != ci, x, y);
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+#pragma unroll
+        for (int u = 0; u < TBR; ++u) asm volatile("" ::"v"(acc[u]));
+#pragma unroll
+        for (int u = 0; u < TBR; ++u) acc[u] = nxt[u];
+        ci = I;
+        cj = J0;
+        advance();
+      }
+    };
+    auto lookahead = [&]() {
+      // panel p+1 = tiles (I, 0), I >= 1, of A22 after update p (computed here, never stored
+      // by the update), into Vs rows 16 (I - 1) .., then its QR (V_{p+1} -> Vs, T -> Ts)
+      const int m1 = m - BB;
+      double bW0[4], bV0[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bW0[s] = Ws[c16][4 * s + g4];
+        bV0[s] = Vs[c16][4 * s + g4];
+      }
+      double4_t pt[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int I = 1 + wid + NWR * q;
+        if (I < nI) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            pt[q][r] = A[(int64_t)(r0 + min(16 * I + g4 + 4 * r, m - 1)) * lda + r0 + c16];
+          double aV[4], aW[4];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            aV[s] = -Vs[16 * I + c16][4 * s + g4];
+            aW[s] = -Ws[16 * I + c16][4 * s + g4];
+          }
+#pragma unroll
+          for (int s = 0; s < 4; ++s) pt[q] = mfma_f64_16x16x4(aV[s], bW0[s], pt[q]);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) pt[q] = mfma_f64_16x16x4(aW[s], bV0[s], pt[q]);
+        }
+      }
+      __syncthreads();                             // every V_p / W_p read is done
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int I = 1 + wid + NWR * q;
+        if (I < nI) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = 16 * I + g4 + 4 * r;     // A22 row; panel row i - 16
+            Vs[i - BB][c16] = (i < m) ? pt[q][r] : 0.0;
+          }
+        }
+      }
+      for (int e = t + 16 * (nI - 1) * BB; e < BMP * BB; e += NTR) Vs[e / BB][e % BB] = 0.0;
+      __syncthreads();
+      band_panel_factor(A, lda, k0 + BB, r0 + BB, m1, Vs, Ws, &red[0][0], Ts, taus,
+                        bw.T + (int64_t)(p + 1) * BB * BB, false, nullptr, Vs);
+      if (K > 1) publish_vt(m1);
+    };
+    if (K == 1) {
+      update();
+      COOP_TMARK(5)
+      __syncthreads();
+      if (p + 1 < npan) lookahead();
+      COOP_TMARK(6)
+    } else if (qwg) {
+      if (p + 1 < npan) lookahead();
+      COOP_TMARK(6)
+    } else {
+      update();
+      COOP_TMARK(5)
+    }
+    cs.sync(true, &err_s);
+    COOP_TMARK(7)
+  }
+  if (TIMED && threadIdx.x == 0 && w < 2)
+    for (int q = 0; q < 8; ++q) tim[(int64_t)cell * 16 + w * 8 + q] = tacc[q];
+#undef COOP_TMARK
+  // ---- row-major lower band (the QR workgroup: it wrote the R blocks itself)
+  if (qwg) {
+    for (int e = t_; e < n * LS; e += NTR) {
+      const int r = e / LS, c = r - BB + e % LS;
+      bw.LB[e] = (c >= 0) ? A[(int64_t)r * lda + c] : 0.0;
+    }
   }
 }
 
@@ -2089,20 +2661,115 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
 extern "C" int64_t pfml_ridge_band_work_doubles(int n, int L) {
   const int64_t np = (n + BB - 1) / BB;
   const int64_t npad = band_npad(n);
+  // F region: the fused path's 5 npad x 16 scratch or the cooperative hand-off scratch
+  // (CoopWork), whichever is larger
+  const int64_t fused = 5LL * npad * BB;
+  const int64_t coop = 2LL * npad * BB + BB * BB + (int64_t)(BNMAX / BB) * (BB * BB + BB);
   return npad * npad + (int64_t)n * LS + n + np * BB * BB + (int64_t)L * n +
          (int64_t)L * n * LS + 3LL * BMP * BB + (int64_t)(BMP / MK_XR) * (BB * BB + BB) +
-         5LL * npad * BB;
+         (fused > coop ? fused : coop);
 }
 
 extern "C" int pfml_ridge_band_nmax() { return BNMAX; }
+
+namespace {
+// Panel-QR micro-benchmark (tools/bench_qr.py): every workgroup factors its own m x 16 panel
+// (row-major in P) `reps` times with band_panel_factor, the band kernels' hot serial step, in
+// the layout of the band kernels: A (lda = m + 16) holds the panel as its rows 0..15, columns
+// 16.. (the symmetric mirror the CholeskyQR2 path reads), the Householder path reads the LDS
+// image.  Cycles per factorisation (thread 0's s_memtime) -> cyc[block]; V -> Vout, T -> Tout;
+// R / V as band_panel_factor stores them land in A's columns 0..15, rows 16...
+template <int VARIANT>
+__global__ __launch_bounds__(NTR) void band_qr_bench_kernel(const double* __restrict__ P, int m,
+                                                            int reps,
+                                                            double* __restrict__ Aout,
+                                                            double* __restrict__ Vout,
+                                                            double* __restrict__ Tout,
+                                                            long long* __restrict__ cyc) {
+  __shared__ double Vs[BMP][LS];
+  __shared__ double Pc[BMP][LS];       // untouched panel copy (the CholeskyQR2 fallback's input)
+  __shared__ double Gs[BB][LS];
+  __shared__ double red[NWR][BB * BB];
+  __shared__ double Ts[BB][LS];
+  __shared__ double taus[BB];
+  const int t = threadIdx.x;
+  const int lda = m + BB;
+  const double* Pb = P + (int64_t)blockIdx.x * m * BB;
+  double* Ab = Aout + (int64_t)blockIdx.x * lda * lda;
+  // cyc[block * 8 + ...]: total, load, column loop (incl. V stores), G + T, and the column
+  // loop's own work / barrier wait / pivot chain + update (thread 0; Householder form only)
+  long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int rep = 0; rep < reps; ++rep) {
+    for (int e = t; e < BMP * BB; e += NTR) {
+      const int i = e / BB, c = e % BB;
+      const double v = (i < m) ? Pb[e] : 0.0;
+      Vs[i][c] = v;
+      Pc[i][c] = v;
+      if (i < m) Ab[(int64_t)c * lda + BB + i] = v;
+    }
+    __threadfence_block();
+    __syncthreads();
+    long long tk[6] = {0, 0, 0, 0, 0, 0};
+    const long long t0 = (long long)__builtin_amdgcn_s_memtime();
+    band_panel_factor(Ab, lda, 0, BB, m, Vs, Gs, &red[0][0], Ts, taus,
+                      Tout + (int64_t)blockIdx.x * BB * BB, VARIANT >= 1,
+                      (VARIANT == 0 && t == 0) ? tk : nullptr, VARIANT == 1 ? nullptr : Vs,
+                      VARIANT == 2 ? Pc : nullptr);
+    __syncthreads();
+    const long long t1 = (long long)__builtin_amdgcn_s_memtime();
+    acc[0] += t1 - t0;
+    if (VARIANT == 0) {
+      acc[1] += tk[0] - t0;
+      acc[2] += tk[1] - tk[0];
+      acc[3] += t1 - tk[1];
+      acc[4] += tk[2];
+      acc[5] += tk[3];
+      acc[6] += tk[4];
+    }
+  }
+  for (int e = t; e < m * BB; e += NTR) Vout[(int64_t)blockIdx.x * m * BB + e] = Vs[e / BB][e % BB];
+  if (t == 0)
+    for (int q = 0; q < 8; ++q) cyc[(int64_t)blockIdx.x * 8 + q] = acc[q] / (reps > 0 ? reps : 1);
+}
+}  // namespace
+
+extern "C" hipError_t pfml_band_qr_bench(const double* P, int m, int nblocks, int reps,
+                                         int variant, double* Aout, double* Vout, double* Tout,
+                                         long long* cyc, hipStream_t st) {
+  if (m < 1 || m > BMP) return hipErrorInvalidValue;
+  if (variant == 2)       // CholeskyQR2 on the LDS panel (the cooperative kernel's form)
+    hipLaunchKernelGGL(band_qr_bench_kernel<2>, dim3(nblocks), dim3(NTR), 0, st, P, m, reps, Aout,
+                       Vout, Tout, cyc);
+  else if (variant == 1)  // CholeskyQR2 reading the panel from A
+    hipLaunchKernelGGL(band_qr_bench_kernel<1>, dim3(nblocks), dim3(NTR), 0, st, P, m, reps, Aout,
+                       Vout, Tout, cyc);
+  else
+    hipLaunchKernelGGL(band_qr_bench_kernel<0>, dim3(nblocks), dim3(NTR), 0, st, P, m, reps, Aout,
+                       Vout, Tout, cyc);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, const double* Sr,
                                              const void* cells, int ncells, int nmax,
                                              const double* lvec, int L, double* work,
                                              double* beta_out, int64_t ldo, int band_mode,
                                              long long* tim, int* lu_list, int* lu_count,
-                                             int lu_cap, hipStream_t st) {
+                                             int lu_cap, const int* wgmap, int nwg,
+                                             unsigned* syncw, hipStream_t st) {
   const RidgeCellDesc* cd = static_cast<const RidgeCellDesc*>(cells);
+  if (band_mode == 4) {
+    // cooperative reduction: nwg workgroups (wgmap: cell << 8 | w << 4 | K - 1), the cells'
+    // sync words zeroed on the stream first (a memset node under graph capture)
+    if (wgmap == nullptr || syncw == nullptr || nwg <= 0) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(syncw, 0, (size_t)ncells * COOP_SYNC * sizeof(unsigned), st);
+    if (e != hipSuccess) return e;
+    if (tim != nullptr)
+      hipLaunchKernelGGL(band_coop_kernel<true>, dim3(nwg), dim3(NTR), 0, st, SD, ldS, Sr, cd, L,
+                         work, wgmap, syncw, tim);
+    else
+      hipLaunchKernelGGL(band_coop_kernel<false>, dim3(nwg), dim3(NTR), 0, st, SD, ldS, Sr, cd, L,
+                         work, wgmap, syncw, tim);
+  }
   // band_mode 1 (or PFML_BAND_MODE=single, or phase timing): one workgroup per cell for the
   // whole reduction; 2 / default: the multi-workgroup form, three launches per panel.
   const char* mode = getenv("PFML_BAND_MODE");
@@ -2120,7 +2787,9 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   // barrier-separated Householder columns they replace.
   const char* qenv = getenv("PFML_BAND_QR");
   const int qr_fast = (qenv && qenv[0] == 'c') ? 1 : 0;
-  if (fused) {
+  if (band_mode == 4) {
+    // (launched above)
+  } else if (fused) {
     if (tim != nullptr)
       hipLaunchKernelGGL(band_fused_kernel<true>, dim3(ncells), dim3(NTR), 0, st, SD, ldS, Sr, cd,
                          L, work, tim);
@@ -2179,8 +2848,11 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
     }
     hipLaunchKernelGGL(band_mk_extract_kernel, dim3(ncells), dim3(256), 0, st, cd, L, work);
   }
+  // (timing: the cooperative kernel fills 16 slots per cell, the solve's two go after them)
   hipLaunchKernelGGL(ridge_band_solve_kernel, dim3(ncells * ((L + 15) / 16)), dim3(NTS), 0, st,
-                     cd, lvec, L, work, tim, ncells, lu_count);
+                     cd, lvec, L, work,
+                     (band_mode == 4 && tim != nullptr) ? tim + (int64_t)ncells * 8 : tim, ncells,
+                     lu_count);
   if (lu_count != nullptr) {   // non-SPD lambdas: pivoted banded LU (count zeroed by kernel 2)
     hipLaunchKernelGGL(band_lu_flag_kernel, dim3((ncells * L + 255) / 256), dim3(256), 0, st, cd,
                        ncells, L, work, lu_list, lu_count, lu_cap);
@@ -2189,6 +2861,6 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   }
   const int nch = (L + LC - 1) / LC;
   hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3(ncells * nch), dim3(NTB), 0, st, cd,
-                     ncells, L, work, beta_out, ldo, (fused || single) ? 1 : 0);
+                     ncells, L, work, beta_out, ldo, (fused || single || band_mode == 4) ? 1 : 0);
   return hipGetLastError();
 }

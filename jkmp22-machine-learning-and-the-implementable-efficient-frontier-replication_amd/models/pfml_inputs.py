@@ -403,14 +403,20 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
                        dtype=torch.int32, device=dev)          # singular const flags (batch)
     nsing_t = torch.zeros((), dtype=torch.int64, device=dev)  # running count, on device
     m_keep = None
-    if keep_m is not None:
+    # (only an fp64 Sigma is kept: S9's weight recursion is specified in fp64 whatever the S4
+    # GEMM precision, config.py run.precision; other precisions leave S9 its own fp64 m_t)
+    if keep_m is not None and prec == "fp64":
         km = np.asarray([m for m in plan.months if int(m) in set(int(x) for x in keep_m)],
                         np.int64)
         kpos = {int(m): i for i, m in enumerate(km)}
+        mpos = {int(m): i for i, m in enumerate(plan.months)}
         m_keep = {"months": km, "mt": torch.empty((len(km), N, N), dtype=torch.float64,
                                                    device=dev),
                   "a": torch.empty((len(km), N), dtype=torch.float64, device=dev),
-                  "n": np.zeros(len(km), np.int64)}
+                  "n": np.zeros(len(km), np.int64),
+                  # the ids (in row order) behind each kept m_tilde: S9 reuses a month's m_t
+                  # only for exactly this universe
+                  "ids": [np.asarray(plan.sig_ids[mpos[int(m)]], np.int64) for m in km]}
     b0 = 0
     for bt in plan.batches:
         B = len(bt.months)

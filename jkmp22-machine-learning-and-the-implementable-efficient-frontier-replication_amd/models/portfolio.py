@@ -252,6 +252,35 @@ def _weights_plan(cfg: Config, chars: pd.DataFrame, wealth: pd.DataFrame, aims: 
                 w_aim=w_aim, nxt=nxt, trow=trow, mu=_month_values(wealth, "mu_ld1", months))
 
 
+def _same_device(a: torch.device, b) -> bool:
+    b = torch.device(b)
+    return a.type == b.type and (b.index is None or a.index == b.index)
+
+
+def m_cache_positions(m_cache: dict | None, months: np.ndarray, ns: np.ndarray, ids: list,
+                      N: int, dev) -> torch.Tensor | None:
+    """Rows of S4's kept m_tilde (PfmlInputs.m_keep) for S9's months, or None when the cache
+    cannot stand in for S9's own m_func: a month missing, a different device or width, or a
+    different universe (row count, or the ids and their order, month by month - a count match
+    alone could pair another universe's m_t with this month's rows)."""
+    if m_cache is None or not len(months):
+        return None
+    cm_ = np.asarray(m_cache["months"], np.int64)
+    if not len(cm_):
+        return None
+    p_ = np.searchsorted(cm_, months)
+    ok = (bool(np.all(p_ < len(cm_)))
+          and bool(np.all(cm_[np.minimum(p_, len(cm_) - 1)] == months))
+          and m_cache["mt"].shape[-1] >= N and _same_device(m_cache["mt"].device, dev))
+    if not ok or not np.array_equal(np.asarray(m_cache["n"])[p_], ns):
+        return None
+    cids = m_cache.get("ids")
+    if cids is None or not all(np.array_equal(cids[int(p)], np.asarray(i, np.int64))
+                               for p, i in zip(p_, ids)):
+        return None
+    return torch.as_tensor(p_, device=m_cache["mt"].device)
+
+
 def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.DataFrame,
                  risk_free: pd.DataFrame, aims: pd.DataFrame, oos_months: np.ndarray,
                  device, mine_months: np.ndarray | None = None,
@@ -310,15 +339,8 @@ def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
 
     # ---- m_t of this rank's months: S4's (cache) or batched m_func (K19) --------------
     Bm = len(mine)
-    kpos = None
-    if m_cache is not None and Bm:
-        cm_ = np.asarray(m_cache["months"], np.int64)
-        p_ = np.searchsorted(cm_, months[mine])
-        ok = (len(cm_) > 0 and bool(np.all(p_ < len(cm_)))
-              and bool(np.all(cm_[np.minimum(p_, len(cm_) - 1)] == months[mine]))
-              and m_cache["mt"].shape[-1] >= N and m_cache["mt"].device == dev)
-        if ok and np.array_equal(np.asarray(m_cache["n"])[p_], ns[mine]):
-            kpos = torch.as_tensor(p_, device=dev)
+    kpos = m_cache_positions(m_cache, months[mine], ns[mine],
+                             [ids_all[starts[t]:stops[t]] for t in mine], N, dev)
     if kpos is not None:
         mt_all = m_cache["mt"].index_select(0, kpos)[:, :N, :N]   # ld = the S4 width
         a_all = m_cache["a"].index_select(0, kpos)[:, :N].contiguous()

@@ -454,8 +454,10 @@ def estimate_cov_frames_pandas(chars: pd.DataFrame, daily: pd.DataFrame, labels:
     ids_l, X_l, iv_l, off = [], [], [], [0]
     for mi in calc_mi:
         cd = cm[cm["mi"] == mi].merge(srm, on=["id", "mi"], how="left")
-        med = cd.groupby("size_grp")["res_vol"].transform(lambda x: x.median(skipna=True))
-        if med.isna().any():
+        # (an all-NaN size group has no median: NaN, filled by the overall median below -
+        # groupby's own median gives it without numpy's empty-slice warning)
+        med = cd.groupby("size_grp")["res_vol"].transform("median")
+        if med.isna().any() and cd["res_vol"].notna().any():
             med = med.fillna(cd["res_vol"].median(skipna=True))
         cd["res_vol"] = cd["res_vol"].fillna(med)
         cd = cd.sort_values("id", kind="stable")

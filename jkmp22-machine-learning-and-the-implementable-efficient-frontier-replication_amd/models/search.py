@@ -266,10 +266,7 @@ def _search_setup(months: np.ndarray, years: np.ndarray, p_vec, G: int, T: int, 
     cs = np.asarray([x[2] for x in chunk_seg], np.int32)
     ce = np.asarray([x[3] for x in chunk_seg], np.int32)
     slot = np.arange(len(chunk_seg), dtype=np.int32)          # local totals: local order
-    if world == 1:
-        tot_slots = (np.asarray(sb, np.int32), np.asarray(sy, np.int32))
-    else:
-        tot_slots = (np.asarray(sb, np.int32), np.asarray(sy, np.int32))
+    tot_slots = (np.asarray(sb, np.int32), np.asarray(sy, np.int32))
     pv = np.asarray(p_vec, dtype=np.int64)
     gg, yy, pp = np.meshgrid(np.arange(G), np.arange(nYl), np.arange(nP), indexing="ij")
     cell_src = (gg * nYl + yy).reshape(-1)                 # cell order [g][year][p]
@@ -373,7 +370,6 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
     # ---- 1. window sums over this rank's chunks (canonical order; one all-gather) -----
     range_push("search.window_sums")
     SD, Sr = window_sums(reals, su)
-    ready = None
     range_pop()
 
     # ---- 2. ridge grid + 3. utilities for every (cell, validation month) -------------
@@ -385,8 +381,7 @@ def grid_search(reals: PfmlReals, cfg: Config, *, gather: bool = True) -> GridRe
     beta, obj = ridge_utilities(SD.reshape(G * nYl, P, P), Sr.reshape(G * nYl, P),
                                 su["cell_src"], su["cell_n"], su["cell_scale"], lvec,
                                 reals.denom.reshape(G * T, P, P),
-                                reals.r_tilde.reshape(G * T, P), su["jc"], su["jm"], su["jn"],
-                                ready=ready)
+                                reals.r_tilde.reshape(G * T, P), su["jc"], su["jm"], su["jn"])
     beta = beta.view(G, nYl, nP, L, P)
     obj = obj.view(su["nVr"], G, nP, L)
     range_pop()

@@ -278,8 +278,65 @@ def _work_doubles(n_arr: np.ndarray, L: int) -> np.ndarray:
     return out
 
 
-def ridge_plan(P: int, L: int, cell_src, cell_n, cell_scale) -> dict:
-    """Host-side descriptors of one ridge-grid launch (CELL_DTYPE, big cells first)."""
+COOP_KMAX = 16          # workgroups per cell of the cooperative band reduction (wgmap: 4 bits)
+COOP_SYNC_WORDS = 32    # csrc/ridge_band.hip COOP_SYNC: int32 sync words per cell
+
+
+def coop_k(cell_n: np.ndarray, ncu: int) -> np.ndarray:
+    """Workgroups per cell of the cooperative band reduction (band_mode 4).
+
+    The largest-n cells of a launch share the chip's CUs (at most COOP_KMAX each, at least 1)
+    when they are the p = 512 cells (n > 256: 32 panels, the grid step's critical chain); every
+    other cell gets one workgroup (its chain is shorter than the big cells' and it shares the
+    CUs with them from a second stream).  The betas do not depend on this choice (bitwise: see
+    band_coop_kernel), only the time does.  PFML_COOP_K=k forces k for the largest cells."""
+    n = np.asarray(cell_n)
+    k = np.ones(len(n), dtype=np.int64)
+    if not len(n):
+        return k
+    big = n == n.max()
+    v = os.environ.get("PFML_COOP_K")
+    if v:
+        kb = int(v)
+    elif int(n.max()) > 256:
+        kb = ncu // int(big.sum())
+    else:
+        kb = 1
+    k[big] = min(max(kb, 1), COOP_KMAX)
+    return k
+
+
+def coop_wgmap(k: np.ndarray) -> np.ndarray:
+    """Block -> (cell, rank, K) codes ``cell << 8 | w << 4 | K - 1`` for cells in plan order.
+    Runs of up to 8 cells with the same K are interleaved (block b and b + 8 hold ranks w and
+    w + 1 of one cell: the same XCD under the observed round-robin placement - speed only)."""
+    codes = []
+    c = 0
+    nc = len(k)
+    while c < nc:
+        g = 1
+        while c + g < nc and g < 8 and k[c + g] == k[c]:
+            g += 1
+        for w in range(int(k[c])):
+            for j in range(g):
+                codes.append(((c + j) << 8) | (w << 4) | (int(k[c]) - 1))
+        c += g
+    return np.asarray(codes, dtype=np.int32)
+
+
+_NCU: dict = {}
+
+
+def num_cus(dev) -> int:
+    key = str(dev)
+    if key not in _NCU:
+        _NCU[key] = int(torch.cuda.get_device_properties(dev).multi_processor_count)
+    return _NCU[key]
+
+
+def ridge_plan(P: int, L: int, cell_src, cell_n, cell_scale, ncu: int = 256) -> dict:
+    """Host-side descriptors of one ridge-grid launch (CELL_DTYPE, big cells first) and the
+    workgroup map of the cooperative reduction (``ncu``: the device's CUs)."""
     lib = nat.hip_lib()
     if lib.pfml_ridge_cell_desc_size() != CELL_DTYPE.itemsize:
         raise RuntimeError("CellDesc layout mismatch between python and libpfml_hip")
@@ -297,7 +354,9 @@ def ridge_plan(P: int, L: int, cell_src, cell_n, cell_scale) -> dict:
     desc = desc[order]
     wsz = wsz[order]
     desc["work"] = np.concatenate([[0], np.cumsum(wsz)[:-1]])
-    return {"desc": desc, "work": int(wsz.sum()), "nmax": int(cell_n.max()), "nc": nc}
+    wgmap = coop_wgmap(coop_k(desc["n"], ncu))
+    return {"desc": desc, "work": int(wsz.sum()), "nmax": int(cell_n.max()), "nc": nc,
+            "wgmap": wgmap}
 
 
 nat.register_hip("pfml_ridge_repair", [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int,
@@ -327,10 +386,11 @@ def repair_launch(plan: dict, d_desc: torch.Tensor, SD: torch.Tensor, Sr: torch.
     # not per launch (540 MB per tridiagonal-path launch at n = 1025)
     nwd = int(lib.pfml_ridge_repair_work_doubles_cap(plan["nmax"], cap))
     wkey = (str(SD.device), nat.stream_of(SD), nwd)     # (per stream: no sharing across streams)
+    # never evicted: a HIP graph that captured a launch keeps this buffer's raw pointer (it is
+    # not in the graph's private pool), so freeing it would hand the graph's scratch to other
+    # tensors; one buffer per (device, stream, size) key stays bounded
     work = _REPAIR_WORK.get(wkey)
     if work is None:
-        if len(_REPAIR_WORK) > 4:
-            _REPAIR_WORK.clear()
         work = _REPAIR_WORK[wkey] = torch.empty(nwd, dtype=torch.float64, device=SD.device)
     nat.check(lib.pfml_ridge_repair(SD.data_ptr(), P, Sr.data_ptr(), d_desc.data_ptr(),
                                     plan["nc"], plan["nmax"], lv.data_ptr(), L, beta.data_ptr(),
@@ -356,10 +416,12 @@ def band_path(plan: dict) -> bool:
 
 def ridge_launch(plan: dict, d_desc: torch.Tensor, SD: torch.Tensor, Sr: torch.Tensor,
                  lv: torch.Tensor, beta: torch.Tensor, band_mode: int = 0,
-                 repair: bool = True) -> torch.Tensor | None:
+                 repair: bool = True, d_wgmap: torch.Tensor | None = None
+                 ) -> torch.Tensor | None:
     """Queue one ridge-grid launch; returns the device count of non-SPD systems re-solved by
     the band path's pivoted banded LU (kernel 2b of ridge_band.hip), None when the launch has
-    no in-band repair (``repair=False`` or the tridiagonal path)."""
+    no in-band repair (``repair=False`` or the tridiagonal path).  ``d_wgmap``: the device
+    copy of plan["wgmap"] (band_mode 4, the cooperative reduction)."""
     P = SD.shape[-1]
     L = int(lv.numel())
     work = torch.empty(plan["work"], dtype=torch.float64, device=SD.device)
@@ -367,15 +429,39 @@ def ridge_launch(plan: dict, d_desc: torch.Tensor, SD: torch.Tensor, Sr: torch.T
     if repair and band_path(plan):
         count = torch.empty(1, dtype=torch.int32, device=SD.device)   # zeroed by the solve
         lst = torch.empty(plan["nc"] * L, dtype=torch.int32, device=SD.device)
+    coop = int(band_mode) == BAND_COOP and band_path(plan)
+    if coop and d_wgmap is None:
+        raise ValueError("ridge_launch: the cooperative reduction needs the device wgmap")
+    sync = (torch.empty(plan["nc"] * COOP_SYNC_WORDS, dtype=torch.int32, device=SD.device)
+            if coop else None)
+    LAST_COOP_SYNC[:] = [sync] if coop else []
     nat.check(nat.hip_lib().pfml_ridge_grid(SD.data_ptr(), P, Sr.data_ptr(), d_desc.data_ptr(),
                                             plan["nc"], plan["nmax"], lv.data_ptr(), L,
                                             work.data_ptr(), beta.data_ptr(), beta.shape[-1],
-                                            int(band_mode),
+                                            int(band_mode) if (coop or band_mode != BAND_COOP)
+                                            else 0,
                                             lst.data_ptr() if lst is not None else None,
                                             count.data_ptr() if count is not None else None,
-                                            plan["nc"] * L, nat.stream_of(SD)),
+                                            plan["nc"] * L,
+                                            d_wgmap.data_ptr() if coop else None,
+                                            len(plan["wgmap"]) if coop else 0,
+                                            sync.data_ptr() if coop else None,
+                                            nat.stream_of(SD)),
               "pfml_ridge_grid")
     return count
+
+
+# sync words of the most recent cooperative launch (tests read the error word: index 1 of
+# every cell's COOP_SYNC_WORDS)
+LAST_COOP_SYNC: list = []
+
+
+def coop_errors() -> int:
+    """Number of cells of the last cooperative launch whose spin-wait timed out (host sync)."""
+    if not LAST_COOP_SYNC:
+        return 0
+    s = LAST_COOP_SYNC[0].view(-1, COOP_SYNC_WORDS)
+    return int((s[:, 1] != 0).sum().item())
 
 
 def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n: np.ndarray,
@@ -395,11 +481,14 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
     if nc == 0:
         return beta
     if nat.is_device(SD):
-        plan = ridge_plan(P, L, cell_src, cell_n, cell_scale)
-        (d_desc,) = upload([plan["desc"]], SD.device)
+        if band_mode == 0:
+            band_mode = band_policy(np.asarray(cell_n))[0]
+        plan = ridge_plan(P, L, cell_src, cell_n, cell_scale, ncu=num_cus(SD.device))
+        d_desc, d_wg = upload([plan["desc"], plan["wgmap"]], SD.device)
         lv = lvec.to(device=SD.device, dtype=torch.float64).contiguous()
         SDc, Src = SD.contiguous(), Sr.contiguous()
-        count = ridge_launch(plan, d_desc, SDc, Src, lv, beta, band_mode, repair=repair)
+        count = ridge_launch(plan, d_desc, SDc, Src, lv, beta, band_mode, repair=repair,
+                             d_wgmap=d_wg)
         if repair:
             LAST_REPAIRS[:] = [count if count is not None
                                else repair_launch(plan, d_desc, SDc, Src, lv, beta)]
@@ -453,7 +542,7 @@ def _side_stream(dev: torch.device, k: int = 0) -> torch.cuda.Stream:
     return _SIDE[key]
 
 
-BAND_SINGLE, BAND_MULTI, BAND_FUSED = 1, 2, 3
+BAND_SINGLE, BAND_MULTI, BAND_FUSED, BAND_COOP = 1, 2, 3, 4
 # One workgroup per cell: the plain kernel (a look-ahead form with panel p+1's QR inside
 # panel p's trailing update measured slower: profiles/r03_band_lookahead_single_wg_ab.json).
 ONE_WG_DEFAULT = BAND_SINGLE
@@ -488,8 +577,7 @@ def band_policy(cell_n: np.ndarray) -> tuple[int, bool]:
     PFML_RIDGE_STREAMS=1|2 override."""
     import os
     cell_n = np.asarray(cell_n)
-    nbig = int((cell_n == cell_n.max()).sum()) if len(cell_n) else 0
-    mode = BAND_MULTI if nbig <= BAND_MULTI_MAX_CELLS else ONE_WG_DEFAULT
+    mode = BAND_COOP
     env = os.environ.get("PFML_BAND_MODE", "")[:1]
     if env == "s":
         mode = BAND_SINGLE
@@ -497,7 +585,7 @@ def band_policy(cell_n: np.ndarray) -> tuple[int, bool]:
         mode = BAND_MULTI
     elif env == "f":
         mode = BAND_FUSED
-    two = mode in (BAND_SINGLE, BAND_FUSED)
+    two = mode in (BAND_SINGLE, BAND_FUSED, BAND_COOP)
     v = os.environ.get("PFML_RIDGE_STREAMS")
     if v:
         two = v.strip() == "2"
@@ -508,31 +596,27 @@ _UTIL_PLANS: dict = {}
 
 
 def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell, job_month,
-                    job_n, split: bool = True, big_key: np.ndarray | None = None) -> dict:
+                    job_n, split: bool = True) -> dict:
     """Launch plan of ridge_utilities on a device, cached: the descriptors depend only on the
     grid's shape (cells, jobs, P, L), so repeated grid searches (every step of a run, every
     benchmark step) reuse the uploaded device copies and skip all host planning.  Each group's
     cells / jobs write straight into the full beta / obj arrays (global out offsets)."""
     key = (P, L, str(dev), split, os.environ.get("PFML_QUAD_MM", "1"),
+           os.environ.get("PFML_COOP_K", ""),
            cell_src.tobytes(), cell_n.tobytes(), cell_scale.tobytes(),
-           job_cell.tobytes(), job_month.tobytes(), job_n.tobytes(),
-           None if big_key is None else big_key.tobytes())
+           job_cell.tobytes(), job_month.tobytes(), job_n.tobytes())
     hit = _UTIL_PLANS.get(key)
     if hit is not None:
         return hit
     big = cell_n == cell_n.max()
     nhy = _hybrid_cells(int(big.sum())) if split else 0
-    if split and big_key is not None:
-        # one big-cell group per key (pipelined window sums), then the small cells
-        parts = tuple((big & (big_key == k), None) for k in np.unique(big_key[big]))
-        parts += ((~big, None),)
-    elif split and nhy:
+    if split and nhy:
         # the first nhy big cells (in cell order) -> multi-workgroup group
         hy = big & (np.cumsum(big) <= nhy)
         parts = ((big & ~hy, ONE_WG_DEFAULT), (hy, BAND_MULTI), (~big, ONE_WG_DEFAULT))
     elif split:
-        # big cells in the launch's mode; the small ones too (one workgroup per cell: the
-        # split form is only taken with the single or the fused reduction)
+        # the largest cells (their own cooperative launch: the chip's CUs shared among them)
+        # and the rest (one workgroup each), each group on a stream of its own
         parts = ((big, None), (~big, None))
     else:
         parts = ((np.ones(len(cell_n), dtype=bool), None),)
@@ -540,12 +624,12 @@ def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell,
     for grp, gmode in parts:
         cells = np.nonzero(grp)[0]
         jobs = np.nonzero(grp[job_cell])[0]
-        rp = ridge_plan(P, L, cell_src[cells], cell_n[cells], cell_scale[cells])
+        rp = ridge_plan(P, L, cell_src[cells], cell_n[cells], cell_scale[cells], ncu=num_cus(dev))
         # ridge_plan orders cells big-first and numbers outputs 0..: map to global rows
         rp["desc"]["out"] = cells[rp["desc"]["out"] // (L * P)].astype(np.int64) * L * P
         qp = quad_plan(P, L, P, job_cell[jobs], job_month[jobs], job_n[jobs], job_out=jobs)
         groups.append((cells, jobs, rp, qp, gmode))
-        arrays += [rp["desc"], qp["desc"], qp["tile_job"]]
+        arrays += [rp["desc"], qp["desc"], qp["tile_job"], rp["wgmap"]]
     dv = upload(arrays, dev)                     # all descriptors, one async copy
     plan = {"groups": groups, "dv": dv}
     if len(_UTIL_PLANS) > 64:
@@ -578,22 +662,14 @@ def check_launch_bounds(S: int, P: int, T: int, cell_src, cell_n, job_cell, job_
 
 def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_scale,
                     lvec: torch.Tensor, D: torch.Tensor, R: torch.Tensor, job_cell, job_month,
-                    job_n, ready: dict | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+                    job_n) -> tuple[torch.Tensor, torch.Tensor]:
     """(beta, obj) = (ridge_grid(...), quadform_utilities(D, R, beta, jobs)).
 
-    On a device with many big cells (one GPU holds the grid) the cells split into the
-    largest-n group and the rest; each group's ridge -> utilities chain is issued on its own
-    HIP stream, the big group first, so the small cells' whole chain runs on the CUs the big
-    cells' one-workgroup-per-cell band reductions leave idle.  With few (multi-GPU shards) one
-    chain in one stream.  Either way beta / obj rows are written in place from cached launch
-    plans, and the non-SPD systems are re-solved on the device inside each group's ridge
-    launch (pivoted banded LU; no host sync, counts in ``LAST_REPAIRS``).
-
-    ``ready`` (grid_search's pipelined window sums): {"key": per-cell group key (the cell's
-    g), "streams": per key the stream that produced its sums, "events": per key the extra
-    events it waits for, "all": events after which every input is complete}.  The big cells
-    then split by key into one chain per key, issued on that key's stream so it starts as soon
-    as its own sums are done; the small cells wait for "all" on a side stream.
+    On a device the cells split into the largest-n group and the rest; each group's ridge ->
+    utilities chain is issued on its own HIP stream, the big group first, so the small cells'
+    chain runs on the CUs the big cells' reduction leaves idle.  beta / obj rows are written in
+    place from cached launch plans, and the non-SPD systems are re-solved on the device inside
+    each group's ridge launch (pivoted banded LU; no host sync, counts in ``LAST_REPAIRS``).
     """
     cell_src, cell_n = np.asarray(cell_src), np.asarray(cell_n)
     cell_scale = np.asarray(cell_scale, dtype=np.float64)
@@ -604,8 +680,6 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
         beta = ridge_grid(SD, Sr, cell_src, cell_n, cell_scale, lvec, band_mode=mode)
         return beta, quadform_utilities(D, R, beta, job_cell, job_month, job_n)
     split = two and len(np.unique(cell_n)) >= 2
-    if not split:
-        ready = None
     th = _HostClock()
     S, P, _ = SD.shape
     check_launch_bounds(S, P, D.shape[0], cell_src, cell_n, job_cell, job_month, job_n)
@@ -613,8 +687,7 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     nc = len(cell_src)
     dev = SD.device
     plan = _utilities_plan(P, L, dev, cell_src, cell_n, cell_scale, job_cell, job_month, job_n,
-                           split=split,
-                           big_key=None if ready is None else np.asarray(ready["key"]))
+                           split=split)
     th("plans")
     # every [L, P] block is written whole by the ridge grid (zero padding past n included), so
     # no fill on the stream the big cells' chain forks from
@@ -626,32 +699,18 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     dv = plan["dv"]
     ng = len(plan["groups"])
     # big cells' factorisations issued first, on side streams; the small cells on `cur`
-    if ready is None:
-        streams = [_side_stream(dev, k) for k in range(ng - 1)] + [cur]
-        for st in streams[:-1]:
-            st.wait_stream(cur)
-    else:
-        # group k < ng - 1 holds the big cells of key k (in key order) and runs on the stream
-        # that produced key k's sums (stream order = the dependency, and no more streams than
-        # hardware queues: two streams sharing a queue serialise); the small cells wait for
-        # everything on one more side stream
-        streams = list(ready["streams"]) + [_side_stream(dev, 0)]
-        for k, st in enumerate(streams[:-1]):
-            for ev in ready["events"][k]:
-                st.wait_event(ev)
-        for ev in ready["all"]:
-            streams[-1].wait_event(ev)
+    streams = [_side_stream(dev, k) for k in range(ng - 1)] + [cur]
+    for st in streams[:-1]:
+        st.wait_stream(cur)
     counts = []
-    order = list(range(ng))
-    if ready is not None and os.environ.get("PFML_PIPE_ORDER", "small_first") == "small_first":
-        order = [ng - 1] + order[:-1]            # (graph branch layout: see grid_search)
-    for gi in order:
+    for gi in range(ng):
         stream = streams[gi]
         _, _, rp, qp, gmode = plan["groups"][gi]
         with torch.cuda.stream(stream):
-            cnt = ridge_launch(rp, dv[3 * gi], SD, Sr, lv, beta, mode if gmode is None else gmode)
-            counts.append(cnt if cnt is not None else repair_launch(rp, dv[3 * gi], SD, Sr, lv, beta))
-            quad_launch(qp, dv[3 * gi + 1], dv[3 * gi + 2], D, R, beta, obj)
+            cnt = ridge_launch(rp, dv[4 * gi], SD, Sr, lv, beta, mode if gmode is None else gmode,
+                               d_wgmap=dv[4 * gi + 3])
+            counts.append(cnt if cnt is not None else repair_launch(rp, dv[4 * gi], SD, Sr, lv, beta))
+            quad_launch(qp, dv[4 * gi + 1], dv[4 * gi + 2], D, R, beta, obj)
     th("launch")
     for st in streams:
         if st == cur:

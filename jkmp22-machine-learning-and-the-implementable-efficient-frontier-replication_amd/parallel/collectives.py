@@ -178,9 +178,11 @@ def send_next(x: torch.Tensor) -> None:
 
 
 def recv_prev(like: torch.Tensor) -> torch.Tensor:
-    """Receive the tensor ``send_next`` of rank - 1 sent (shape / dtype of ``like``)."""
+    """Receive the tensor ``send_next`` of rank - 1 sent (shape / dtype of ``like``); rank 0
+    (and a non-distributed run) gets zeros, so a chain never starts from uninitialised
+    memory."""
     e = env()
-    out = torch.empty_like(like)
+    out = torch.zeros_like(like)
     if e.is_dist and e.rank > 0:
         if _staged(out):
             h = torch.empty_like(out, device=_comm_device(out))

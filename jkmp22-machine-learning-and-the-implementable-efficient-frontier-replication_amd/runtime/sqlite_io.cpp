@@ -154,6 +154,34 @@ std::string plain_scan_table(const std::string& sql) {
     if (!(std::isalnum((unsigned char)ch) || ch == '_')) return "";
   for (const char* kw : {" WHERE ", " JOIN ", " GROUP ", " ORDER ", " LIMIT ", " UNION "})
     if (u.find(kw) != std::string::npos) return "";
+  // the select list must be `*` or plain column names (optionally "quoted"): DISTINCT,
+  // aggregates and expressions (count(*), max(eom), a + b) give per-part rows that do not
+  // concatenate to the query's result, so they run on one connection
+  const std::string list = sql.substr(7, f - 7);
+  size_t s0 = list.find_first_not_of(' ');
+  if (s0 == std::string::npos) return "";
+  const std::string lt = list.substr(s0, list.find_last_not_of(' ') - s0 + 1);
+  if (lt == "*") return t;
+  std::string ul(lt);
+  for (auto& ch : ul) ch = (char)std::toupper((unsigned char)ch);
+  if (ul.compare(0, 9, "DISTINCT ") == 0 || ul.compare(0, 4, "ALL ") == 0) return "";
+  size_t p = 0;
+  while (p <= lt.size()) {
+    size_t q = lt.find(',', p);
+    if (q == std::string::npos) q = lt.size();
+    std::string tok = lt.substr(p, q - p);
+    const size_t a0 = tok.find_first_not_of(' '), a1 = tok.find_last_not_of(' ');
+    if (a0 == std::string::npos) return "";
+    tok = tok.substr(a0, a1 - a0 + 1);
+    if (tok.size() >= 2 && tok.front() == '"' && tok.back() == '"') {
+      for (size_t k = 1; k + 1 < tok.size(); ++k)
+        if (tok[k] == '"') return "";
+    } else {
+      for (char ch : tok)
+        if (!(std::isalnum((unsigned char)ch) || ch == '_')) return "";
+    }
+    p = q + 1;
+  }
   return t;
 }
 

@@ -267,44 +267,6 @@ def test_ridge_variants_agree(gpu, variant, monkeypatch):
     assert rel < 1e-10, rel
 
 
-def test_ridge_grid_production_rank_deficient(gpu):
-    """Production size (n = 513, 257) with a RANK-DEFICIENT, indefinite window sum (400
-    observations, rank 401 < 513): every lambda > 0 matches the fp64 pivoted LU (torch.linalg.solve) to 1e-10;
-    at lambda = 0 the system is singular, the banded Cholesky fails and the device repairs it
-    by the pivoted banded LU (PFML_Search_Coef.py:131-133 semantics).  A singular system has
-    no unique solution to compare, so the lambda = 0 betas are held to np.linalg.solve's own
-    guarantee instead: backward stability, |(Dbar) b - rbar| <= 1e-12 (|Dbar| |b| + |rbar|),
-    with rbar in the range of Dbar (a consistent system)."""
-    from pfml.ops import ridge as rg
-    P = 513
-    X = _rand(1, 400, P, seed=23)
-    SD = X.transpose(1, 2) @ X / 400
-    # one null direction turned negative: Dbar' = Dbar - 0.7 v v' stays singular (112 zero
-    # eigenvalues) and is indefinite, so the banded Cholesky MUST fail at lambda = 0 (and
-    # for lambda < 0.7) and every such system goes through the device repair
-    e, V = torch.linalg.eigh(SD[0])
-    SD[0] = SD[0] - 0.7 * torch.outer(V[:, 0], V[:, 0])
-    SD[0] = 0.5 * (SD[0] + SD[0].T)
-    w = _rand(1, P, seed=24)
-    Sr = (SD @ w.unsqueeze(-1)).squeeze(-1)            # consistent at lambda = 0
-    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
-    src, nn, sc = np.array([0, 0]), np.array([513, 257]), np.array([1.0, 1.0])
-    ref = rg.ridge_grid(SD, Sr, src, nn, sc, lv)
-    out = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
-    assert rg.repairs_done() >= 1                        # the n = 513 lambda = 0 system
-    rel = ((out[:, 1:] - ref[:, 1:]).norm(dim=-1) / ref[:, 1:].norm(dim=-1)).max().item()
-    assert rel < 1e-10, rel
-    # n = 257 (leading block): lambda = 0 is regular here -> plain comparison
-    r257 = ((out[1, 0] - ref[1, 0]).norm() / ref[1, 0].norm()).item()
-    assert r257 < 1e-10, r257
-    b = out[0, 0, :P]
-    assert torch.isfinite(b).all()
-    D0, r0 = SD[0], Sr[0]
-    res = (D0 @ b - r0).norm().item()
-    scale = (torch.linalg.matrix_norm(D0, ord=2) * b.norm() + r0.norm()).item()
-    assert res <= 1e-12 * scale, (res, scale)
-
-
 @pytest.mark.parametrize("mode", ["single", "multi", "fused"])
 def test_band_reduction_modes(gpu, mode, monkeypatch):
     """One-workgroup-per-cell and multi-workgroup band reductions both reproduce the LU-solve
@@ -322,44 +284,6 @@ def test_band_reduction_modes(gpu, mode, monkeypatch):
     out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
     rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
     assert rel < 1e-10, rel
-
-
-def test_ridge_grid_production_rank_deficient(gpu):
-    """Production size (n = 513, 257) with a RANK-DEFICIENT, indefinite window sum (400
-    observations, rank 401 < 513): every lambda > 0 matches the fp64 pivoted LU (torch.linalg.solve) to 1e-10;
-    at lambda = 0 the system is singular, the banded Cholesky fails and the device repairs it
-    by the pivoted banded LU (PFML_Search_Coef.py:131-133 semantics).  A singular system has
-    no unique solution to compare, so the lambda = 0 betas are held to np.linalg.solve's own
-    guarantee instead: backward stability, |(Dbar) b - rbar| <= 1e-12 (|Dbar| |b| + |rbar|),
-    with rbar in the range of Dbar (a consistent system)."""
-    from pfml.ops import ridge as rg
-    P = 513
-    X = _rand(1, 400, P, seed=23)
-    SD = X.transpose(1, 2) @ X / 400
-    # one null direction turned negative: Dbar' = Dbar - 0.7 v v' stays singular (112 zero
-    # eigenvalues) and is indefinite, so the banded Cholesky MUST fail at lambda = 0 (and
-    # for lambda < 0.7) and every such system goes through the device repair
-    e, V = torch.linalg.eigh(SD[0])
-    SD[0] = SD[0] - 0.7 * torch.outer(V[:, 0], V[:, 0])
-    SD[0] = 0.5 * (SD[0] + SD[0].T)
-    w = _rand(1, P, seed=24)
-    Sr = (SD @ w.unsqueeze(-1)).squeeze(-1)            # consistent at lambda = 0
-    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
-    src, nn, sc = np.array([0, 0]), np.array([513, 257]), np.array([1.0, 1.0])
-    ref = rg.ridge_grid(SD, Sr, src, nn, sc, lv)
-    out = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
-    assert rg.repairs_done() >= 1                        # the n = 513 lambda = 0 system
-    rel = ((out[:, 1:] - ref[:, 1:]).norm(dim=-1) / ref[:, 1:].norm(dim=-1)).max().item()
-    assert rel < 1e-10, rel
-    # n = 257 (leading block): lambda = 0 is regular here -> plain comparison
-    r257 = ((out[1, 0] - ref[1, 0]).norm() / ref[1, 0].norm()).item()
-    assert r257 < 1e-10, r257
-    b = out[0, 0, :P]
-    assert torch.isfinite(b).all()
-    D0, r0 = SD[0], Sr[0]
-    res = (D0 @ b - r0).norm().item()
-    scale = (torch.linalg.matrix_norm(D0, ord=2) * b.norm() + r0.norm()).item()
-    assert res <= 1e-12 * scale, (res, scale)
 
 
 @pytest.mark.parametrize("n_obs", [700, 90])
@@ -386,6 +310,66 @@ def test_band_fused_bitwise_single(gpu, n_obs, monkeypatch):
         b = out[mode]
         same = (a == b) | (torch.isnan(a) & torch.isnan(b))
         assert bool(same.all()), (mode, float((a - b).abs().max()))
+
+
+@pytest.mark.parametrize("n_obs", [700, 90])
+def test_band_coop_matches_lu_and_bitwise_across_k(gpu, n_obs, monkeypatch):
+    """Cooperative band reduction (K workgroups per cell, the production form): for every n
+    of the grid (513, 257, 129, 65) plus ragged ones (100, 17), full-rank (n_obs = 700) and
+    rank-deficient (n_obs = 90: lambda = 0 repaired on the device), the betas are BITWISE
+    equal for K = 1, 2, 3, 8 and 16 workgroups per cell - so the K a 1-GPU and an 8-GPU run
+    choose (ops/ridge.py::coop_k) cannot change a hyper-parameter pick - and match the
+    LU-solve oracle (np.linalg.solve per lambda, PFML_Search_Coef.py:131-133)."""
+    from pfml.ops import ridge as rg
+    P = 513
+    SD = _spd_stack(3, P, n_obs=n_obs, seed=171)
+    SD = 0.5 * (SD + SD.transpose(1, 2))           # exactly symmetric, like the window sums
+    Sr = _rand(3, P, seed=172)
+    if n_obs > P:
+        lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
+    else:
+        lv = torch.tensor([0.0] + list(np.exp(np.linspace(-2, 10, 40))), dtype=torch.float64)
+    for ncell in (513, 257, 129, 100, 65, 17):
+        src = np.array([0, 1, 2])
+        nn = np.full(3, ncell)
+        sc = np.full(3, 1.5e-3)
+        out = {}
+        for k in ("1", "2", "3", "8", "16"):
+            monkeypatch.setenv("PFML_COOP_K", k)
+            out[k] = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu),
+                                   band_mode=rg.BAND_COOP).cpu()
+            assert rg.coop_errors() == 0, (ncell, k)
+        a = out["1"]
+        for k, b in out.items():
+            same = (a == b) | (torch.isnan(a) & torch.isnan(b))
+            assert bool(same.all()), (ncell, k, float((a - b).abs().max()))
+        ref = rg.ridge_grid(SD, Sr, src, nn, sc, lv)
+        ok = slice(1, None) if n_obs <= ncell else slice(None)   # singular at lambda = 0
+        rel = ((a[:, ok] - ref[:, ok]).norm(dim=-1) / ref[:, ok].norm(dim=-1)).max().item()
+        assert rel < 1e-10, (ncell, rel)
+
+
+def test_band_coop_mixed_launch_bitwise(gpu, monkeypatch):
+    """Cells of different n in ONE cooperative launch (largest cells K > 1, the rest K = 1)
+    give bitwise the betas of each cell launched alone at K = 1."""
+    from pfml.ops import ridge as rg
+    P = 513
+    SD = _spd_stack(3, P, n_obs=700, seed=173)
+    SD = 0.5 * (SD + SD.transpose(1, 2))
+    Sr = _rand(3, P, seed=174)
+    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
+    src = np.array([0, 1, 2, 1, 0, 2, 2, 1])
+    nn = np.array([513, 513, 65, 257, 129, 100, 513, 17])
+    sc = np.full(len(src), 1.5e-3)
+    monkeypatch.setenv("PFML_COOP_K", "4")
+    mixed = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu),
+                          band_mode=rg.BAND_COOP).cpu()
+    assert rg.coop_errors() == 0
+    monkeypatch.setenv("PFML_COOP_K", "1")
+    for c in range(len(src)):
+        one = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src[c:c + 1], nn[c:c + 1], sc[c:c + 1],
+                            lv.to(gpu), band_mode=rg.BAND_COOP).cpu()
+        assert torch.equal(one[0], mixed[c]), c
 
 
 @pytest.mark.parametrize("hybrid", ["0", "3"])
@@ -440,44 +424,6 @@ def test_band_panel_qr(gpu, qr, mode, n_obs, monkeypatch):
     out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
     rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
     assert rel < 1e-10, rel
-
-
-def test_ridge_grid_production_rank_deficient(gpu):
-    """Production size (n = 513, 257) with a RANK-DEFICIENT, indefinite window sum (400
-    observations, rank 401 < 513): every lambda > 0 matches the fp64 pivoted LU (torch.linalg.solve) to 1e-10;
-    at lambda = 0 the system is singular, the banded Cholesky fails and the device repairs it
-    by the pivoted banded LU (PFML_Search_Coef.py:131-133 semantics).  A singular system has
-    no unique solution to compare, so the lambda = 0 betas are held to np.linalg.solve's own
-    guarantee instead: backward stability, |(Dbar) b - rbar| <= 1e-12 (|Dbar| |b| + |rbar|),
-    with rbar in the range of Dbar (a consistent system)."""
-    from pfml.ops import ridge as rg
-    P = 513
-    X = _rand(1, 400, P, seed=23)
-    SD = X.transpose(1, 2) @ X / 400
-    # one null direction turned negative: Dbar' = Dbar - 0.7 v v' stays singular (112 zero
-    # eigenvalues) and is indefinite, so the banded Cholesky MUST fail at lambda = 0 (and
-    # for lambda < 0.7) and every such system goes through the device repair
-    e, V = torch.linalg.eigh(SD[0])
-    SD[0] = SD[0] - 0.7 * torch.outer(V[:, 0], V[:, 0])
-    SD[0] = 0.5 * (SD[0] + SD[0].T)
-    w = _rand(1, P, seed=24)
-    Sr = (SD @ w.unsqueeze(-1)).squeeze(-1)            # consistent at lambda = 0
-    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
-    src, nn, sc = np.array([0, 0]), np.array([513, 257]), np.array([1.0, 1.0])
-    ref = rg.ridge_grid(SD, Sr, src, nn, sc, lv)
-    out = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
-    assert rg.repairs_done() >= 1                        # the n = 513 lambda = 0 system
-    rel = ((out[:, 1:] - ref[:, 1:]).norm(dim=-1) / ref[:, 1:].norm(dim=-1)).max().item()
-    assert rel < 1e-10, rel
-    # n = 257 (leading block): lambda = 0 is regular here -> plain comparison
-    r257 = ((out[1, 0] - ref[1, 0]).norm() / ref[1, 0].norm()).item()
-    assert r257 < 1e-10, r257
-    b = out[0, 0, :P]
-    assert torch.isfinite(b).all()
-    D0, r0 = SD[0], Sr[0]
-    res = (D0 @ b - r0).norm().item()
-    scale = (torch.linalg.matrix_norm(D0, ord=2) * b.norm() + r0.norm()).item()
-    assert res <= 1e-12 * scale, (res, scale)
 
 
 @pytest.mark.parametrize("fmt", ["bf16", "fp8"])
@@ -598,46 +544,6 @@ def test_grid_search_bitwise_deterministic(gpu):
     for b, o, k in runs[1:]:
         assert torch.equal(b, runs[0][0]) and torch.equal(o, runs[0][1])
         assert torch.equal(k, runs[0][2])
-
-
-def test_grid_search_pipelined_sums_bitwise(gpu, monkeypatch):
-    """Per-g pipelined window sums (g's big cells start while g + 1's sums stream; 3 ridge
-    groups on their own streams) give the same betas / utilities bit for bit as the one-pass
-    sums + 2 groups, eager and under HIP-graph capture."""
-    from pfml.config import Config
-    from pfml.models.search import PfmlReals, grid_search
-    from pfml.utils.dates import mi_from_ym
-    monkeypatch.setenv("PFML_BAND_MODE", "single")
-    monkeypatch.setenv("PFML_RIDGE_STREAMS", "2")
-    cfg = Config.default().override(["pf_ml.p_vec=[16,64]", "pf.dates.start_year=2001",
-                                     "pf.dates.end_yr=2006"])
-    G, P = 2, 65
-    months = np.arange(mi_from_ym(1994, 3), mi_from_ym(2006, 11) + 1)
-    T = len(months)
-    X = _rand(G * T, 80, P, seed=93).to(gpu)
-    D = (X.transpose(1, 2) @ X / 80).view(G, T, P, P).contiguous()
-    r = (0.1 * _rand(G, T, P, seed=94)).to(gpu)
-    reals = PfmlReals(months, r, D)
-    out = {}
-    for pipe in ("0", "1"):
-        monkeypatch.setenv("PFML_PIPE_SUMS", pipe)
-        res = grid_search(reals, cfg)
-        out[pipe] = (res.beta.cpu(), res.obj.cpu())
-        if pipe == "1":                               # captured replay of the pipelined form
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                grid_search(reals, cfg)
-            torch.cuda.current_stream().wait_stream(s)
-            torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                res_g = grid_search(reals, cfg)
-            g.replay()
-            torch.cuda.synchronize()
-            out["graph"] = (res_g.beta.cpu(), res_g.obj.cpu())
-    for k in ("1", "graph"):
-        assert torch.equal(out[k][0], out["0"][0]) and torch.equal(out[k][1], out["0"][1]), k
 
 
 @pytest.mark.parametrize("P", [65, 513])

@@ -157,6 +157,36 @@ def test_pfml_inputs_match_reference_order_oracle(small_data):
         assert torch.equal(out.reals.denom[0, i], out.reals.denom[1, i])
 
 
+def test_s9_m_cache_fp64_only_and_universe_guard(small_data):
+    """S4 keeps m_tilde for S9 only when its Sigma is fp64 (S9's recursion is specified in
+    fp64 whatever run.precision says), and S9 reuses a kept month only for exactly its
+    universe: same row count AND the same ids in the same order."""
+    from pfml.models.pfml_inputs import build_inputs
+    from pfml.models.portfolio import m_cache_positions
+    from pfml.utils.dates import pfml_date_grids
+    cfg = small_data
+    chars, barra, wealth, rf = _load(cfg)
+    grids = pfml_date_grids(int(barra.months.min()), 11, cfg.settings["split"]["test_end"],
+                            1971, 10)
+    months = grids["m2"][[3, 9]]
+    res = build_inputs(cfg, chars, barra, wealth, rf, "cpu", months=months, keep_m=months)
+    mk = res.m_keep
+    assert mk is not None and list(mk["months"]) == list(months)
+    assert len(mk["ids"]) == 2 and all(len(i) == n for i, n in zip(mk["ids"], mk["n"]))
+    low = cfg.override(["run.precision=fp32"])
+    assert build_inputs(low, chars, barra, wealth, rf, "cpu", months=months,
+                        keep_m=months).m_keep is None
+    N = int(mk["mt"].shape[-1])
+    ids = [np.asarray(i) for i in mk["ids"]]
+    pos = m_cache_positions(mk, months, np.asarray(mk["n"]), ids, N, "cpu")
+    assert pos is not None and pos.tolist() == [0, 1]
+    swapped = [ids[0], ids[1][::-1].copy()]                 # same count, other row order
+    assert m_cache_positions(mk, months, np.asarray(mk["n"]), swapped, N, "cpu") is None
+    other = [ids[0], ids[1] + 1]                             # same count, other universe
+    assert m_cache_positions(mk, months, np.asarray(mk["n"]), other, N, "cpu") is None
+    assert m_cache_positions(mk, months[:1], np.asarray(mk["n"])[:1], ids[:1], N, "cpu").tolist() == [0]
+
+
 def test_m_func_matches_sqrtm_reference():
     from oracle import m_func_ref
     from pfml.ops.linalg import m_func

@@ -80,3 +80,24 @@ def test_native_parallel_scan_equals_pandas(native, tmp_path, monkeypatch):
     monkeypatch.setenv("PFML_SQL_NATIVE", "0")
     ref = native.sql_read(db, "SELECT id, eom, x, y, grp, flag FROM Big", parse_dates=["eom"])
     pd.testing.assert_frame_equal(got, ref)
+
+
+def test_native_aggregates_and_distinct_on_big_table(native, tmp_path, monkeypatch):
+    """Queries over a > 64k-row table that are NOT plain column scans (DISTINCT, aggregates,
+    expressions) run on one connection: one result, as pandas gives it."""
+    db = str(tmp_path / "agg.db")
+    df = _frame(n=70_001, seed=4)
+    with sqlite3.connect(db) as con:
+        df.to_sql("Big", con, index=False)
+    for q in ("SELECT DISTINCT grp FROM Big", "SELECT count(*) FROM Big",
+              "SELECT max(eom) FROM Big", "SELECT id + 1 AS k FROM Big",
+              'SELECT "id", x FROM Big'):
+        got = native.sql_read(db, q)
+        monkeypatch.setenv("PFML_SQL_NATIVE", "0")
+        ref = native.sql_read(db, q)
+        monkeypatch.delenv("PFML_SQL_NATIVE")
+        if "DISTINCT" in q:
+            got = got.sort_values("grp", na_position="first").reset_index(drop=True)
+            ref = ref.sort_values("grp", na_position="first").reset_index(drop=True)
+        pd.testing.assert_frame_equal(got, ref, check_dtype=False)
+        assert len(got) == len(ref), q

@@ -41,6 +41,27 @@ def timing(n=513, ncells=1):
     fast tridiagonalisation) for one cell."""
     from pfml.ops import _native as nat
     dev = torch.device("cuda", 0)
+    mode = os.environ.get("PFML_BAND_MODE", "coop")[:1]
+    if mode not in ("s", "m", "f"):
+        # cooperative kernel: 8 phase slots for workgroup 0 (the QR one) and 1 of cell 0
+        ncells = int(os.environ.get("PFML_TIMING_CELLS", "1"))
+        buf = torch.zeros(ncells * 16 + 16, dtype=torch.int64, device=dev)
+        nat.hip_lib().pfml_ridge_set_timing(buf.data_ptr())
+        run(ncells, n, reps=1)
+        torch.cuda.synchronize()
+        nat.hip_lib().pfml_ridge_set_timing(None)
+        allb = buf.cpu().numpy()
+        names = ["init_panel0", "U", "X_partials", "sync_wait", "C_sums_W", "update",
+                 "lookahead_qr", "end_sync"]
+        out = {"K": os.environ.get("PFML_COOP_K", "auto"), "cells": ncells}
+        for w in (0, 1):
+            t = allb[w * 8:(w + 1) * 8]
+            tot = max(1, int(t.sum()))
+            out[f"wg{w}"] = {nm: f"{int(v)} cyc ({100.0 * v / tot:.1f}%)" for nm, v in zip(names, t)}
+            out[f"wg{w}_total_cyc"] = tot
+        out.update({"solve_fwd_cyc": int(allb[ncells * 16]),
+                    "solve_bwd_cyc": int(allb[ncells * 16 + 1])})
+        return out
     buf = torch.zeros(ncells * 8 + 16, dtype=torch.int64, device=dev)
     nat.hip_lib().pfml_ridge_set_timing(buf.data_ptr())
     run(ncells, n, reps=1)

@@ -58,6 +58,31 @@ for step in ${MODE//,/ }; do
     bench)
       timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
       rc=$?; grep '^{' $OUT/bench.json | cut -c1-400; if [ $rc -ne 0 ]; then tail -5 $OUT/bench.err; exit $rc; fi ;;
+    qr)
+      # panel QR in isolation (band_panel_factor): cycles per panel, Householder vs CholeskyQR2
+      timeout -k 10 200 python tools/bench_qr.py 497 241 > $OUT/qr_bench.jsonl 2> $OUT/qr_bench.err
+      rc=$?; cat $OUT/qr_bench.jsonl; if [ $rc -ne 0 ]; then tail -5 $OUT/qr_bench.err; exit $rc; fi ;;
+    cooptime)
+      for k in 1 2; do
+        PFML_COOP_K=$k timeout -k 10 120 python tools/bench_ridge.py --timing > $OUT/coop_timing_k$k.json 2>&1
+        rc=$?; grep -E '"(X_partials|C_sums_W|update|lookahead_qr|U|sync_wait|end_sync)"|total' $OUT/coop_timing_k$k.json; if [ $rc -ne 0 ]; then cat $OUT/coop_timing_k$k.json; exit $rc; fi
+      done
+      PFML_BENCH_CELLS=1,13,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/coop_cells.log 2>&1
+      rc=$?; tail -1 $OUT/coop_cells.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    coop)
+      # cooperative band reduction: tests (oracle + bitwise across K), per-phase timing of
+      # one n = 513 cell at K = 1 / 2 / 4, wall time vs #cells (auto K), and vs single
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 300 --timeout-method thread -k "coop" > $OUT/pytest_coop.log 2>&1
+      rc=$?; tail -3 $OUT/pytest_coop.log
+      if [ $rc -ne 0 ]; then grep -E "^E |FAILED" $OUT/pytest_coop.log | head -20; exit $rc; fi
+      for k in 1 2 4; do
+        PFML_COOP_K=$k timeout -k 10 120 python tools/bench_ridge.py --timing > $OUT/coop_timing_k$k.json 2>&1
+        rc=$?; cat $OUT/coop_timing_k$k.json; if [ $rc -ne 0 ]; then exit $rc; fi
+      done
+      PFML_BENCH_CELLS=1,13,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/coop_cells.log 2>&1
+      rc=$?; tail -1 $OUT/coop_cells.log; if [ $rc -ne 0 ]; then exit $rc; fi
+      PFML_BAND_MODE=single PFML_BENCH_CELLS=1,13,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/single_cells.log 2>&1
+      rc=$?; tail -1 $OUT/single_cells.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     ridge)
       # band-reduction A/B: per-phase cycles of one n = 513 cell and the grid vs #cells
       for m in single fused; do
