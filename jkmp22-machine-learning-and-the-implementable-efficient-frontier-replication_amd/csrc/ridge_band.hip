@@ -530,6 +530,7 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
   // ---- P2: Householder QR of the m x 16 panel in REGISTERS: column j reaches the 16 lanes
   //      of a row group by a row_newbcast DPP move; one barrier per column (cross-wave sums,
   //      ping-pong buffers).
+  double tau_r[BB];
   static_for<0, BB>([&](auto J) {
     constexpr int j = decltype(J)::value;
     const int par = j & 1;
@@ -588,7 +589,13 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
       tau = fma(fabs(alpha), rn, 1.0);
       scal = copysign(rcp_f64(fabs(alpha) + nrm), alpha);
     }
-    const double wc = tau * (vjc + scal * dc);
+    // v_c' v_j for a finished column c = cq < j: v_c[j] + scal_j sum_{i > j} v_c[i] a_j[i]
+    // (a finished column holds v_c below its diagonal), i.e. the same vjc + scal dc that
+    // scales the update of the columns cq > j: the dlarft dots G = V'V come free
+    const double gcj = vjc + scal * dc;
+    const double wc = tau * gcj;
+    if (t < j) Gs[t][j] = gcj;                   // (t < 16: row group 0, cq = t)
+    tau_r[j] = tau;
     // rows >= 32 (q > 0, below every diagonal): one FMA and one multiply per element with
     // lane factors fixed per column instead of two selects - columns cq > j get
     // a - v wc (wcl = wc, sl = 1), column j becomes v = a scal (its x IS its own a: wcl = 0,
@@ -623,39 +630,18 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
   }
   __syncthreads();
   if (tk) tk[1] = (long long)__builtin_amdgcn_s_memtime();
-  // ---- G = V^T V (dlarft dots) on MFMA: wave w sums rows [64 w, 64 w + 64)
+  // ---- T of the compact WY form: T^-1 = diag(1 / tau) + striu(V'V) (Puglisi; Joffrain,
+  //      Low, Quintana-Orti, van de Geijn, "Accumulating Householder transformations,
+  //      revisited", 2006), inverted in registers by every wave (lane c16: column c16 of U,
+  //      1 / U_kk = tau_k - a zero tau gives a zero row and column of T, as dlarft does)
   {
-    double4_t g = {0.0, 0.0, 0.0, 0.0};
+    double uc[BB], tc[BB];
 #pragma unroll
-    for (int k = 0; k < 64; k += 4) {
-      const double v = Vs[wid * 64 + k + g4][c16];
-      g = mfma_f64_16x16x4(v, v, g);
-    }
+    for (int i = 0; i < BB; ++i) uc[i] = (i < c16) ? Gs[i][c16] : 0.0;
+    triu_inv16(uc, tau_r, tc, c16);
+    if (wid == 0 && g4 == 0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) redf[wid * 256 + PFML_F64_CROW(lane, r) * BB + c16] = g[r];
-  }
-  __syncthreads();
-  if (t < BB * BB) {
-    double g = 0.0;
-#pragma unroll
-    for (int w = 0; w < NWR; ++w) g += redf[w * 256 + t];
-    Gs[t / BB][t % BB] = g;
-  }
-  __syncthreads();
-  // ---- T (dlarft, forward columnwise): T[j][j] = tau_j,
-  //      T[0:j, j] = -tau_j T[0:j, 0:j] G[0:j, j]   (one wave, lane = row)
-  if (wid == 0) {                    // lane = row i: T[i][0:j] stays in registers
-    double trow[BB];
-    static_for<0, BB>([&](auto J) {
-      constexpr int j = decltype(J)::value;
-      double s = 0.0;
-#pragma unroll
-      for (int k = 0; k < j; ++k) s += trow[k] * Gs[k][j];   // G[k][j]: LDS broadcast
-      trow[j] = (lane < j) ? -taus[j] * s : (lane == j ? taus[j] : 0.0);
-    });
-    if (lane < BB) {
-#pragma unroll
-      for (int j = 0; j < BB; ++j) Ts[lane][j] = trow[j];
+      for (int i = 0; i < BB; ++i) Ts[i][c16] = tc[i];
     }
   }
   __syncthreads();
@@ -1485,6 +1471,18 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
         advance();
       }
     };
+    // the old tiles (I, 0) of the look-ahead panel, loaded before the update's stores are
+    // issued (a load behind write-through stores waits for them: one vmcnt counter)
+    double4_t pt[4];
+    auto lookahead_load = [&]() {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int I = 1 + wid + NWR * q;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          pt[q][r] = A[(int64_t)(r0 + min(16 * min(I, nI - 1) + g4 + 4 * r, m - 1)) * lda + r0 + c16];
+      }
+    };
     auto lookahead = [&]() {
       // panel p+1 = tiles (I, 0), I >= 1, of A22 after update p (computed here, never stored
       // by the update), into Vs rows 16 (I - 1) .., then its QR (V_{p+1} -> Vs, T -> Ts)
@@ -1495,14 +1493,10 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
         bW0[s] = Ws[c16][4 * s + g4];
         bV0[s] = Vs[c16][4 * s + g4];
       }
-      double4_t pt[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int I = 1 + wid + NWR * q;
         if (I < nI) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            pt[q][r] = A[(int64_t)(r0 + min(16 * I + g4 + 4 * r, m - 1)) * lda + r0 + c16];
           double aV[4], aW[4];
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
@@ -1534,13 +1528,17 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
       if (K > 1) publish_vt(m1);
     };
     if (K == 1) {
+      if (p + 1 < npan) lookahead_load();
       update();
       COOP_TMARK(5)
       __syncthreads();
       if (p + 1 < npan) lookahead();
       COOP_TMARK(6)
     } else if (qwg) {
-      if (p + 1 < npan) lookahead();
+      if (p + 1 < npan) {
+        lookahead_load();
+        lookahead();
+      }
       COOP_TMARK(6)
     } else {
       update();

@@ -206,7 +206,8 @@ constexpr int COV_ROWS = 64;
 __global__ __launch_bounds__(256) void ewma_factor_cov_kernel(
     const double* __restrict__ fr, int K, const int64_t* __restrict__ ends, int obs,
     const double* __restrict__ w_cor, const double* __restrict__ w_var, double scale,
-    double* __restrict__ F, double* __restrict__ cor_out, double* __restrict__ var_out) {
+    double* __restrict__ F, double* __restrict__ cor_out, double* __restrict__ var_out,
+    int nan_cor) {
   __shared__ double Xs[COV_ROWS][ZS];
   __shared__ double sw[2][COV_ROWS];
   __shared__ double mu[2][KP];
@@ -301,11 +302,13 @@ __global__ __launch_bounds__(256) void ewma_factor_cov_kernel(
   for (int q = t; q < K * K; q += 256) {
     const int i = q / K, j = q % K;
     // a factor with no exposure in the window (an industry without members: its daily OLS
-    // coefficient is the pinv's zero) has variance 0; its correlations are taken as 0 so F
-    // carries 0 there (the reference's pinv leaves ~1e-16 noise, i.e. F ~ 1e-32) instead of
-    // a NaN that would poison every Sigma of the month
+    // coefficient is the pinv's zero) has variance 0.  nan_cor (compat mode): cov / (sd sd')
+    // as weighted_cor_wt divides (General_functions.py:827), 0 / 0 = NaN off the diagonal,
+    // which poisons that month's Sigma as it does the reference's; corrected mode: those
+    // correlations are 0, so F carries 0 there (the reference's pinv mostly leaves ~1e-16
+    // noise instead of an exact zero, i.e. F ~ 1e-32)
     const double dn = sqrt(C[0][i][i]) * sqrt(C[0][j][j]);
-    const double cor = (i == j) ? 1.0 : (dn > 0.0 ? C[0][i][j] / dn : 0.0);
+    const double cor = (i == j) ? 1.0 : ((nan_cor || dn > 0.0) ? C[0][i][j] / dn : 0.0);
     const double sdi = sqrt(C[1][i][i]), sdj = sqrt(C[1][j][j]);
     const int64_t o = (int64_t)bi * K * K + q;
     F[o] = sdi * cor * sdj * scale;
@@ -393,11 +396,11 @@ extern "C" hipError_t pfml_daily_ols(const double* X, const double* y, const int
 extern "C" hipError_t pfml_ewma_factor_cov(const double* fr, int K, const int64_t* ends, int nb,
                                            int obs, const double* w_cor, const double* w_var,
                                            double scale, double* F, double* cor_out,
-                                           double* var_out, hipStream_t st) {
+                                           double* var_out, int nan_cor, hipStream_t st) {
   if (K < 1 || K > KP) return hipErrorInvalidValue;
   if (nb <= 0) return hipSuccess;
   hipLaunchKernelGGL(ewma_factor_cov_kernel, dim3(nb), dim3(256), 0, st, fr, K, ends, obs, w_cor,
-                     w_var, scale, F, cor_out, var_out);
+                     w_var, scale, F, cor_out, var_out, nan_cor);
   return hipGetLastError();
 }
 

@@ -132,9 +132,14 @@ def generate(spec: SyntheticSpec | None = None, features: list[str] | None = Non
     size_q = pd.Series(me).groupby(t_of_row).rank(pct=True).to_numpy()
     size_grp = np.select([size_q > 0.8, size_q > 0.5, size_q > 0.2, size_q > 0.05],
                          ["mega", "large", "small", "micro"], "nano")
+    # JKP's `date`: the month's last business day (the column 0_SP500_Subset.py:52-55 filters
+    # the Factors chunks on)
+    mdt = pd.DatetimeIndex(months[t_of_row])
+    last_bday = mdt - pd.to_timedelta(np.maximum(mdt.weekday.to_numpy() - 4, 0), unit="D")
     head = pd.DataFrame({
         "id": ids[firm_of_row],
         "eom": months[t_of_row].strftime("%Y-%m-%d"),
+        "date": last_bday.strftime("%Y-%m-%d"),
         "sic": sic_row,
         "ff49": rng.integers(1, 50, n_firms)[firm_of_row],
         "size_grp": size_grp,
@@ -185,7 +190,10 @@ def generate(spec: SyntheticSpec | None = None, features: list[str] | None = Non
         d_idx = np.repeat(mstart[t_of_row] - np.cumsum(np.r_[0, cnt[:-1]]), cnt) + np.arange(cnt.sum())
         dret = beta[d_firm] * mkt_d[d_idx] + ivol[d_firm] / np.sqrt(21) * rng.standard_normal(len(d_idx))
         dret = dret + rf_d[d_idx] / 100.0
-        crsp_daily = pd.DataFrame({"permno": ids[d_firm], "date": days[d_idx].strftime("%Y-%m-%d"),
+        # dates as pandas holds them after read_sql_query(parse_dates) of the WRDS pull: to_sql
+        # stores "YYYY-MM-DD 00:00:00" text (0_Get_Additional_Data.py:65-79), the form the
+        # reference's chunked BETWEEN reads compare as strings
+        crsp_daily = pd.DataFrame({"permno": ids[d_firm], "date": days[d_idx],
                                    "ret": dret.astype(np.float32),
                                    "primaryexch": np.array(["N", "A", "Q"])[d_firm % 3]})
         out["crsp_daily"] = crsp_daily
@@ -223,6 +231,16 @@ def small_spec(**kw) -> SyntheticSpec:
     return SyntheticSpec(**base)
 
 
+def l0_spec(**kw) -> SyntheticSpec:
+    """The L0 golden's panel: few names but the reference's whole 1952-2024 window, so every
+    5-year chunk of the reference's L0 loops holds rows (0_SP500_Subset.py:109-111 merges an
+    empty chunk's object-typed keys with int64 ones and raises)."""
+    base = dict(n_stocks=12, start="1952-01-31", end="2024-12-31", mean_life_months=240,
+                seed=7)
+    base.update(kw)
+    return SyntheticSpec(**base)
+
+
 def settings_for_small(cfg, spec: SyntheticSpec):
     """Shrink the date-dependent settings so a short synthetic panel exercises every stage."""
     s = cfg.settings
@@ -235,7 +253,7 @@ def settings_for_small(cfg, spec: SyntheticSpec):
     return cfg
 
 
-__all__ = ["SyntheticSpec", "generate", "write_raw", "small_spec", "settings_for_small",
+__all__ = ["SyntheticSpec", "generate", "write_raw", "small_spec", "l0_spec", "settings_for_small",
            "get_settings"]
 
 

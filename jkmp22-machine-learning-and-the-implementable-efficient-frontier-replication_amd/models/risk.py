@@ -115,10 +115,12 @@ def cluster_ranks(chars: pd.DataFrame, labels: pd.DataFrame, features: list[str]
     return clusters, R
 
 
-def weighted_cov(X: torch.Tensor, w: torch.Tensor, cor: bool) -> torch.Tensor:
+def weighted_cov(X: torch.Tensor, w: torch.Tensor, cor: bool,
+                 nan_cor: bool = False) -> torch.Tensor:
     """Batched R cov.wt(..., method='unbiased') [and cor=TRUE] (General_functions.py:745-835).
 
-    X: [B, T, K], w: [B, T] (zero weight = padding)."""
+    X: [B, T, K], w: [B, T] (zero weight = padding).  A zero-variance column's correlations:
+    0 (default) or, with ``nan_cor`` (compat mode), 0 / 0 = NaN as weighted_cor_wt divides."""
     wn = w / w.sum(1, keepdim=True)
     mu = (wn.unsqueeze(-1) * X).sum(1, keepdim=True)
     Xw = (X - mu) * wn.sqrt().unsqueeze(-1)
@@ -127,8 +129,11 @@ def weighted_cov(X: torch.Tensor, w: torch.Tensor, cor: bool) -> torch.Tensor:
         return cov
     sd = torch.sqrt(torch.diagonal(cov, dim1=1, dim2=2))
     den = sd.unsqueeze(-1) * sd.unsqueeze(-2)
-    # zero-variance factor (no exposure in the window): correlations 0, as csrc/risk.hip
-    c = torch.where(den > 0, cov / torch.where(den > 0, den, 1.0), torch.zeros_like(cov))
+    if nan_cor:
+        c = cov / den
+    else:
+        # zero-variance factor (no exposure in the window): correlations 0, as csrc/risk.hip
+        c = torch.where(den > 0, cov / torch.where(den > 0, den, 1.0), torch.zeros_like(cov))
     idx = torch.arange(c.shape[-1])
     c[:, idx, idx] = 1.0
     return c
@@ -170,7 +175,9 @@ def _load_risk_inputs(cfg: Config):
 def estimate_cov(cfg: Config, device: str = "cpu", write: bool = True) -> BarraCov:
     """S3 (Estimate Covariance Matrix.py): load, ``estimate_cov_frames``, write Barra_Cov."""
     chars, daily, labels = _load_risk_inputs(cfg)
-    barra = estimate_cov_frames(chars, daily, labels, cfg.settings["cov_set"], device)
+    # compat mode: a zero-variance factor's NaN correlations as the reference computes them
+    barra = estimate_cov_frames(chars, daily, labels, cfg.settings["cov_set"], device,
+                                nan_cor=bool(cfg.run.compat_mode))
     log.info(f"Barra covariance for {len(barra.months)} months, K = {len(barra.factors)} "
              f"factors.")
     if write:
@@ -215,7 +222,7 @@ def _seg_median(v: torch.Tensor, g: torch.Tensor, G: int) -> torch.Tensor:
 
 
 def estimate_cov_frames(chars: pd.DataFrame, daily: pd.DataFrame, labels: pd.DataFrame,
-                        cs: dict, device: str = "cpu") -> BarraCov:
+                        cs: dict, device: str = "cpu", nan_cor: bool = True) -> BarraCov:
     """The Barra model from in-memory frames, batched end to end (no per-day / per-month
     Python loop, no groupby lambda, no frame merges over the daily panel):
 
@@ -312,7 +319,8 @@ def estimate_cov_frames(chars: pd.DataFrame, daily: pd.DataFrame, labels: pd.Dat
     calc = np.unique(eoms[eoms >= np.datetime64(min_date.date())])
     calc_mi = month_index(calc)
     end_idx = np.searchsorted(day_dt, calc, side="right")
-    Fm = ewma_factor_cov(coef, end_idx, obs, w_cor, w_var, scale=21.0).cpu().numpy()
+    Fm = ewma_factor_cov(coef, end_idx, obs, w_cor, w_var, scale=21.0,
+                         nan_cor=nan_cor).cpu().numpy()
     th("s3.ewma_factor_cov")
 
     # ---- idiosyncratic EWMA vol (:345-442), on the device ---------------------------------
@@ -381,7 +389,7 @@ def estimate_cov_frames(chars: pd.DataFrame, daily: pd.DataFrame, labels: pd.Dat
 
 
 def estimate_cov_frames_pandas(chars: pd.DataFrame, daily: pd.DataFrame, labels: pd.DataFrame,
-                               cs: dict, device: str = "cpu") -> BarraCov:
+                               cs: dict, device: str = "cpu", nan_cor: bool = True) -> BarraCov:
     """The round-1 pandas-bound form of ``estimate_cov_frames`` (groupby-lambda z-score,
     frame merges over the daily panel, one loop iteration per calc month): the test oracle
     and the host baseline of tools/bench_s3.py."""
@@ -429,7 +437,8 @@ def estimate_cov_frames_pandas(chars: pd.DataFrame, daily: pd.DataFrame, labels:
     dev = torch.device(device)
     from ..ops.risk_kernels import ewma_factor_cov, ewma_vol as _ewma_vol
     fr = torch.as_tensor(coef, dtype=torch.float64, device=dev)
-    Fm = ewma_factor_cov(fr, end_idx, obs, w_cor, w_var, scale=21.0).cpu().numpy()
+    Fm = ewma_factor_cov(fr, end_idx, obs, w_cor, w_var, scale=21.0,
+                         nan_cor=nan_cor).cpu().numpy()
 
     # ---- idiosyncratic EWMA vol (:345-442) -----------------------------------------
     sr = pd.DataFrame({"id": dm["id"].to_numpy(np.int64), "date": dnum, "residual": resid})

@@ -24,7 +24,7 @@ from ..utils.log import COUNTERS
 
 _P, _I, _L, _D = C.c_void_p, C.c_int, C.c_int64, C.c_double
 nat.register_hip("pfml_daily_ols", [_P, _P, _P, _I, _I, _P, _P, _P, _P])
-nat.register_hip("pfml_ewma_factor_cov", [_P, _I, _P, _I, _I, _P, _P, _D, _P, _P, _P, _P])
+nat.register_hip("pfml_ewma_factor_cov", [_P, _I, _P, _I, _I, _P, _P, _D, _P, _P, _P, _I, _P])
 nat.register_hip("pfml_ewma_vol", [_P, _P, _L, _D, _I, _P, _P])
 nat.register_hip("pfml_risk_max_factors", [])
 
@@ -76,9 +76,11 @@ def _daily_ols_torch(X, y, offsets):
 
 
 def ewma_factor_cov(fr: torch.Tensor, ends, obs: int, w_cor, w_var, scale: float = 21.0,
-                    return_parts: bool = False):
+                    return_parts: bool = False, nan_cor: bool = True):
     """F[b] = sd_b cor_b sd_b * scale for the window fr[ends[b]-t_b : ends[b]], t_b = min(obs,
-    ends[b]), with weights w_*[obs - t_b:] (cor: hl_cor, sd: hl_var).  fr: [days, K]."""
+    ends[b]), with weights w_*[obs - t_b:] (cor: hl_cor, sd: hl_var).  fr: [days, K].
+    ``nan_cor`` (compat mode): a zero-variance factor's correlations are 0 / 0 = NaN, as the
+    reference's weighted_cor_wt gives them (General_functions.py:827); else 0."""
     dev = fr.device
     ends_np = np.asarray(ends, dtype=np.int64)
     B, K = len(ends_np), fr.shape[1]
@@ -92,14 +94,15 @@ def ewma_factor_cov(fr: torch.Tensor, ends, obs: int, w_cor, w_var, scale: float
         var = torch.empty_like(F) if return_parts else None
         nat.check(nat.hip_lib().pfml_ewma_factor_cov(
             frc.data_ptr(), K, e.data_ptr(), B, int(obs), wc.data_ptr(), wv.data_ptr(),
-            float(scale), F.data_ptr(), nat.ptr(cor), nat.ptr(var), nat.stream_of(frc)),
+            float(scale), F.data_ptr(), nat.ptr(cor), nat.ptr(var), int(bool(nan_cor)),
+            nat.stream_of(frc)),
             "pfml_ewma_factor_cov")
         return (F, cor, var) if return_parts else F
     Fs, cs, vs = [], [], []
     for b in range(B):
         t = min(int(obs), int(ends_np[b]))
         Xw = fr[ends_np[b] - t: ends_np[b]].double()
-        c = weighted_cov_torch(Xw, wc[obs - t:], cor=True)
+        c = weighted_cov_torch(Xw, wc[obs - t:], cor=True, nan_cor=nan_cor)
         v = weighted_cov_torch(Xw, wv[obs - t:], cor=False)
         sd = torch.sqrt(torch.diagonal(v))
         Fs.append(sd.unsqueeze(-1) * c * sd.unsqueeze(0) * scale)
@@ -111,8 +114,10 @@ def ewma_factor_cov(fr: torch.Tensor, ends, obs: int, w_cor, w_var, scale: float
     return F
 
 
-def weighted_cov_torch(X: torch.Tensor, w: torch.Tensor, cor: bool) -> torch.Tensor:
-    """R cov.wt(center=TRUE, method='unbiased'[, cor=TRUE]) of X [T, K] (oracle)."""
+def weighted_cov_torch(X: torch.Tensor, w: torch.Tensor, cor: bool,
+                       nan_cor: bool = True) -> torch.Tensor:
+    """R cov.wt(center=TRUE, method='unbiased'[, cor=TRUE]) of X [T, K] (oracle).  cor with a
+    zero-variance column: NaN off the diagonal (``nan_cor``, the reference's division) or 0."""
     wn = w / w.sum()
     mu = (wn.unsqueeze(-1) * X).sum(0, keepdim=True)
     Xw = (X - mu) * wn.sqrt().unsqueeze(-1)
@@ -120,7 +125,11 @@ def weighted_cov_torch(X: torch.Tensor, w: torch.Tensor, cor: bool) -> torch.Ten
     if not cor:
         return cov
     sd = torch.sqrt(torch.diagonal(cov))
-    c = cov / (sd.unsqueeze(-1) * sd.unsqueeze(0))
+    den = sd.unsqueeze(-1) * sd.unsqueeze(0)
+    if nan_cor:
+        c = cov / den
+    else:
+        c = torch.where(den > 0, cov / torch.where(den > 0, den, 1.0), torch.zeros_like(cov))
     c.fill_diagonal_(1.0)
     return c
 

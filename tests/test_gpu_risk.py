@@ -113,3 +113,12 @@ def test_estimate_cov_device_matches_pandas_form(gpu, small_data):
     assert np.array_equal(np.isnan(a.F), np.isnan(b.F))
     assert np.allclose(a.F, b.F, rtol=1e-9, atol=1e-12 * np.nanmax(np.abs(b.F)), equal_nan=True)
     assert np.allclose(a.ivol, b.ivol, rtol=1e-9, atol=1e-10 * np.abs(b.ivol).max())
+
+
+def test_factor_cov_zero_variance_modes_gpu(gpu):
+    """A factor with no exposure (an all-zero return column: zero variance) on the device:
+    compat mode gives the reference's weighted_cor_wt NaN correlations (General_functions.py:827:
+    cov / outer(sd, sd), diagonal 1), so F is NaN in that row / column off the diagonal;
+    corrected mode gives 0 there.  Every other entry matches the CPU oracle in both modes."""
+    from zero_var_check import check_zero_variance_modes
+    check_zero_variance_modes(gpu)

@@ -339,3 +339,10 @@ def test_pct_rank_rows_matches_pandas():
     assert np.allclose(got, ref, rtol=0, atol=1e-15)
     raw = rt.pct_rank_rows(X, pe, seg)
     assert np.array_equal(np.isnan(raw), np.isnan(X))
+
+
+def test_factor_cov_zero_variance_modes_cpu():
+    """CPU form of test_gpu_risk.py::test_factor_cov_zero_variance_modes_gpu: compat NaN
+    correlations for a zero-variance factor (the reference's division), corrected 0."""
+    from zero_var_check import check_zero_variance_modes
+    check_zero_variance_modes("cpu")

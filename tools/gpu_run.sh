@@ -69,6 +69,14 @@ for step in ${MODE//,/ }; do
       done
       PFML_BENCH_CELLS=1,13,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/coop_cells.log 2>&1
       rc=$?; tail -1 $OUT/coop_cells.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    benchk)
+      # headline bench with the cooperative reduction at auto K and at K = 1 (every cell one WG)
+      for k in auto 1; do
+        if [ $k = auto ]; then unset PFML_COOP_K; else export PFML_COOP_K=$k; fi
+        timeout -k 10 300 python bench.py --no-inputs > $OUT/bench_k$k.json 2> $OUT/bench_k$k.err
+        rc=$?; echo "K=$k: $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_k$k.json)"; if [ $rc -ne 0 ]; then tail -5 $OUT/bench_k$k.err; exit $rc; fi
+      done
+      unset PFML_COOP_K ;;
     coop)
       # cooperative band reduction: tests (oracle + bitwise across K), per-phase timing of
       # one n = 513 cell at K = 1 / 2 / 4, wall time vs #cells (auto K), and vs single
