@@ -4,7 +4,12 @@ W-rank run (its hp-year shard; collectives are no-ops) and report the slowest ra
 
 This is the compute part of `bench.py --gpus W` (the driver runs the real multi-GPU bench);
 it shows whether the per-rank work shrinks as 1/W or hits a latency floor.  PFML_SHARD_GRAPH=1
-replays each rank's step as a captured HIP graph."""
+replays each rank's step as a captured HIP graph.  ``--with-inputs``: each rank's S4 (its own
+PFML months) and its S4 + S5 + S6 step instead (the whole-node projection of the full
+grid-search wall-clock).
+
+    python tools/bench_shard.py [1,2,4,8] [steps]
+    python tools/bench_shard.py --with-inputs [1,2,4,8] [steps]"""
 import json
 import os
 import sys
@@ -18,7 +23,72 @@ from pfml.config import Config  # noqa: E402
 from pfml.parallel import dist as pdist  # noqa: E402
 
 
+def with_inputs(worlds, steps: int) -> dict:
+    """Per-rank S4 (this rank's PFML months: local_month_rows, burn-in pieces + hp-year
+    blocks + a one-block halo) and its S4 + S5 + S6 step, every rank of each W in turn on
+    this one GPU (PFML_Input_Data.py:318-491 sharded by month blocks; collectives no-ops)."""
+    from pfml.data.synthetic import engine_inputs
+    from pfml.models.pfml_inputs import make_s4_plan, run_plan
+    from pfml.models.search import local_month_rows
+    from pfml.utils.dates import pfml_date_grids
+    dev = torch.device("cuda", 0)
+    cfg = Config.default()
+    cfg.run.compat_mode = False                  # as bench.py: distinct RFF draw per g
+    chars, barra, wealth, rf = engine_inputs(n_stocks=500)
+    g = pfml_date_grids(int(barra.months.min()), 11, cfg.settings["split"]["test_end"],
+                        int(cfg.settings["pf"]["dates"]["start_year"]),
+                        int(cfg.settings["pf"]["dates"]["split_years"]))
+    months = g["m2"]
+    out = {"months_total": int(len(months))}
+    for W in worlds:
+        s4, grid, nm = [], [], []
+        for r in range(W):
+            env = pdist.DistEnv(rank=r, world_size=W, device=dev)
+            pdist.set_env(env)
+            rows = local_month_rows(months, cfg.hp_years, W, r)
+            plan = make_s4_plan(cfg, chars, barra, wealth, rf, dev, months[rows])
+            eng = (plan, months)
+            run_plan(plan, cfg)                                   # warm-up
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(steps):
+                run_plan(plan, cfg)
+            torch.cuda.synchronize()
+            t_s4 = 1e3 * (time.perf_counter() - t) / steps
+            bench.one_step(None, cfg, eng)                        # warm-up (plans, caches)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            for _ in range(steps):
+                bench.one_step(None, cfg, eng)
+            torch.cuda.synchronize()
+            t_all = 1e3 * (time.perf_counter() - t) / steps
+            s4.append(round(t_s4, 1))
+            grid.append(round(t_all - t_s4, 1))
+            nm.append(int(len(rows)))
+            del plan, eng
+            torch.cuda.empty_cache()
+            print(f"W={W} rank={r}: {len(rows)} months, S4 {t_s4:.1f} ms, "
+                  f"S5+S6 {t_all - t_s4:.1f} ms", file=sys.stderr, flush=True)
+        out[f"w{W}_s4_ms"] = s4
+        out[f"w{W}_s5s6_ms"] = grid
+        out[f"w{W}_months"] = nm
+        out[f"w{W}_s4_max_ms"] = max(s4)
+        out[f"w{W}_s4_max_over_min"] = round(max(s4) / max(min(s4), 1e-9), 3)
+        out[f"w{W}_total_max_ms"] = round(max(a + b for a, b in zip(s4, grid)), 1)
+    if "w1_s4_max_ms" in out:
+        for W in worlds:
+            out[f"w{W}_s4_max_vs_ideal"] = round(out[f"w{W}_s4_max_ms"] * W / out["w1_s4_max_ms"], 3)
+    pdist.set_env(None)
+    return out
+
+
 def main():
+    if "--with-inputs" in sys.argv:
+        args = [a for a in sys.argv[1:] if a != "--with-inputs"]
+        worlds = [int(w) for w in (args[0] if args else "1,2,4,8").split(",")]
+        steps = int(args[1]) if len(args) > 1 else 2
+        print(json.dumps(with_inputs(worlds, steps)))
+        return
     worlds = [int(w) for w in (sys.argv[1] if len(sys.argv) > 1 else "1,2,4,8").split(",")]
     steps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     only = [int(r) for r in sys.argv[3].split(",")] if len(sys.argv) > 3 else None

@@ -124,6 +124,10 @@ for step in ${MODE//,/ }; do
       rc=$?; if [ $rc -ne 0 ]; then tail -3 $OUT/prof1.log; exit $rc; fi
       python tools/rocprof_timeline.py $(find $OUT/prof1 -name "*.db" | head -1) --last 40 > $OUT/timeline1.txt 2>&1
       tail -32 $OUT/timeline1.txt ;;
+    shards4)
+      # per-rank S4 + S5 + S6 of W = 1, 2, 4, 8 rank shards on this GPU (whole-node projection)
+      timeout -k 10 900 python tools/bench_shard.py --with-inputs 1,2,4,8 2 > $OUT/shard_s4.json 2> $OUT/shard_s4.err
+      rc=$?; cat $OUT/shard_s4.json; if [ $rc -ne 0 ]; then tail -5 $OUT/shard_s4.err; exit $rc; fi ;;
     shard)
       PFML_SHARD_GRAPH=1 timeout -k 10 300 python tools/bench_shard.py 1,2,4,8 > $OUT/shard.json 2> $OUT/shard.err
       rc=$?; cat $OUT/shard.json; if [ $rc -ne 0 ]; then tail -3 $OUT/shard.err; exit $rc; fi ;;
