@@ -528,16 +528,20 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
   }
   if (tk) tk[0] = (long long)__builtin_amdgcn_s_memtime();
   // ---- P2: Householder QR of the m x 16 panel in REGISTERS: column j reaches the 16 lanes
-  //      of a row group by a row_newbcast DPP move; one barrier per column (cross-wave sums,
-  //      ping-pong buffers).
+  //      of a row group by row_newbcast DPP, fused into the FMA that consumes it
+  //      (v_fmac_f64_dpp); one barrier per column (cross-wave sums, ping-pong buffers).
+  //      A finished column keeps its Householder vector UNSCALED below the diagonal (u = the
+  //      column at its own step; v = scal u): its scal is applied once, when V is written, and
+  //      the dlarft dots of later steps carry it as one factor - so every element costs two
+  //      fp64 operations per step (its share of the dots and its update), not five.
   double tau_r[BB];
+  double myscal = 0.0;                           // scal of this lane's column once finished
   static_for<0, BB>([&](auto J) {
     constexpr int j = decltype(J)::value;
     const int par = j & 1;
     // (tk: per-column sub-phases of thread 0's wave, accumulated in tk[2..4]: own work before
     // the barrier, barrier wait, reductions + pivot chain + update after it)
     const long long tc0 = tk ? (long long)__builtin_amdgcn_s_memtime() : 0;
-    double x[16];
     double s1p[4] = {0.0, 0.0, 0.0, 0.0};
     // Only row group q = 0 (rows < 32) meets the diagonal; groups of four row groups at or
     // beyond m are all-zero and skipped (one wave-uniform branch per four).  Four partial
@@ -548,8 +552,8 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
 #pragma unroll
       for (int q = q4; q < q4 + 4; ++q) {
         const int i = rg + 32 * q;
-        x[q] = row_bcast<j>(a[q]);
-        s1p[q & 3] += (q > 0 || i > j) ? x[q] * a[q] : 0.0;
+        const double mq = (q > 0 || i > j) ? a[q] : 0.0;       // rows below the diagonal
+        fmac_bcast<j, true>(s1p[q & 3], a[q], mq);             // += x_j[i] a_cq[i]
       }
     }
     // sum over the wave's 4 row groups (lanes l, l^16, l^32, l^48): VALU lane swaps
@@ -589,19 +593,18 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
       tau = fma(fabs(alpha), rn, 1.0);
       scal = copysign(rcp_f64(fabs(alpha) + nrm), alpha);
     }
-    // v_c' v_j for a finished column c = cq < j: v_c[j] + scal_j sum_{i > j} v_c[i] a_j[i]
-    // (a finished column holds v_c below its diagonal), i.e. the same vjc + scal dc that
-    // scales the update of the columns cq > j: the dlarft dots G = V'V come free
+    // v_j' a_cq = a_cq[j] + scal sum_{i > j} x_j[i] a_cq[i] = vjc + scal dc: for cq > j the
+    // update coefficient wc = tau (...), for a finished column cq < j (unscaled u_cq, factor
+    // myscal) the dlarft dot G[cq][j] = v_cq' v_j = myscal (...): G = V'V comes free
     const double gcj = vjc + scal * dc;
     const double wc = tau * gcj;
-    if (t < j) Gs[t][j] = gcj;                   // (t < 16: row group 0, cq = t)
+    if (t < j) Gs[t][j] = myscal * gcj;          // (t < 16: row group 0, cq = t)
     tau_r[j] = tau;
-    // rows >= 32 (q > 0, below every diagonal): one FMA and one multiply per element with
-    // lane factors fixed per column instead of two selects - columns cq > j get
-    // a - v wc (wcl = wc, sl = 1), column j becomes v = a scal (its x IS its own a: wcl = 0,
-    // sl = scal), finished columns cq < j stay (wcl = 0, sl = 1)
-    const double wcl = (cq > j) ? wc : 0.0;
-    const double sl = (cq == j) ? scal : 1.0;
+    const bool upd = cq > j, own = cq == j;
+    if (own) myscal = scal;
+    // columns cq > j: a[i] -= v_j[i] wc = scal x_j[i] wc below the diagonal, a[j] -= wc on
+    // it; column j: beta on the diagonal, u = x below it (scaled later); cq < j: unchanged
+    const double nsw = upd ? -(scal * wc) : 0.0;
 #pragma unroll
     for (int q4 = 0; q4 < 16; q4 += 4) {
       if (q4 > 0 && 32 * q4 >= m) continue;
@@ -609,12 +612,11 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
       for (int q = q4; q < q4 + 4; ++q) {
         const int i = rg + 32 * q;
         if (q == 0) {
-          const double v = (i > j) ? x[q] * scal : ((i == j && i < m) ? 1.0 : 0.0);
-          const double diag = (i > j) ? v : ((i == j) ? beta : a[q]);
-          a[q] = (cq > j) ? fma(-v, wc, a[q]) : ((cq == j) ? diag : a[q]);
+          const double ns0 = (i > j) ? nsw : 0.0;
+          fmac_bcast<j, true>(a[0], a[0], ns0);
+          if (i == j) a[0] = upd ? a[0] - wc : (own ? beta : a[0]);
         } else {
-          const double v = x[q] * scal;
-          a[q] = fma(-v, wcl, a[q]) * sl;
+          fmac_bcast<j, true>(a[q], a[q], nsw);
         }
       }
     }
@@ -625,8 +627,9 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int i = rg + 32 * q;
-    Vs[i][cq] = (i > cq) ? a[q] : ((i == cq && i < m) ? 1.0 : 0.0);
-    if (i < m) A[(int64_t)(r0 + i) * n + k0 + cq] = a[q];
+    const double v = a[q] * myscal;
+    Vs[i][cq] = (i > cq) ? v : ((i == cq && i < m) ? 1.0 : 0.0);
+    if (i < m) A[(int64_t)(r0 + i) * n + k0 + cq] = (i > cq) ? v : a[q];
   }
   __syncthreads();
   if (tk) tk[1] = (long long)__builtin_amdgcn_s_memtime();
