@@ -221,6 +221,24 @@ def _seg_median(v: torch.Tensor, g: torch.Tensor, G: int) -> torch.Tensor:
     return torch.where(cnt > 0, med, torch.full_like(med, float("nan")))
 
 
+def _zero_exposureless(Fm: np.ndarray, coef: torch.Tensor, end_idx, obs: int) -> None:
+    """Compat NaN correlations only where the reference has them.
+
+    A factor without exposure on every day of a window comes out of the pinv fallback
+    (Estimate Covariance Matrix.py:228-229) as exactly 0 in the device Jacobi pinv, but as
+    LAPACK rounding noise (|c| ~ 1e-17) in the reference's numpy.linalg.pinv, so the
+    reference's weighted_cor_wt divides noise by noise: finite correlations and F entries
+    ~1e-34.  Such a factor's F row / column is set to 0 here (equal to the reference's to any
+    tolerance); a factor with exposure and exactly constant returns keeps its NaN."""
+    nz = (coef != 0).to(torch.int64).cumsum(0).cpu().numpy()
+    nz = np.vstack([np.zeros((1, nz.shape[1]), np.int64), nz])
+    e = np.asarray(end_idx, np.int64)
+    cnt = nz[e] - nz[np.maximum(e - obs, 0)]                  # nonzero coefficient days
+    for b, k in zip(*np.nonzero(cnt == 0)):
+        Fm[b, k, :] = 0.0
+        Fm[b, :, k] = 0.0
+
+
 def estimate_cov_frames(chars: pd.DataFrame, daily: pd.DataFrame, labels: pd.DataFrame,
                         cs: dict, device: str = "cpu", nan_cor: bool = True) -> BarraCov:
     """The Barra model from in-memory frames, batched end to end (no per-day / per-month
@@ -321,6 +339,8 @@ def estimate_cov_frames(chars: pd.DataFrame, daily: pd.DataFrame, labels: pd.Dat
     end_idx = np.searchsorted(day_dt, calc, side="right")
     Fm = ewma_factor_cov(coef, end_idx, obs, w_cor, w_var, scale=21.0,
                          nan_cor=nan_cor).cpu().numpy()
+    if nan_cor:
+        _zero_exposureless(Fm, coef, end_idx, obs)
     th("s3.ewma_factor_cov")
 
     # ---- idiosyncratic EWMA vol (:345-442), on the device ---------------------------------
@@ -439,6 +459,8 @@ def estimate_cov_frames_pandas(chars: pd.DataFrame, daily: pd.DataFrame, labels:
     fr = torch.as_tensor(coef, dtype=torch.float64, device=dev)
     Fm = ewma_factor_cov(fr, end_idx, obs, w_cor, w_var, scale=21.0,
                          nan_cor=nan_cor).cpu().numpy()
+    if nan_cor:
+        _zero_exposureless(Fm, fr, end_idx, obs)
 
     # ---- idiosyncratic EWMA vol (:345-442) -----------------------------------------
     sr = pd.DataFrame({"id": dm["id"].to_numpy(np.int64), "date": dnum, "residual": resid})

@@ -346,3 +346,27 @@ def test_factor_cov_zero_variance_modes_cpu():
     correlations for a zero-variance factor (the reference's division), corrected 0."""
     from zero_var_check import check_zero_variance_modes
     check_zero_variance_modes("cpu")
+
+
+def test_exposureless_factor_keeps_finite_cov_in_compat():
+    """S3 compat: a factor with exactly-zero coefficients over a window (the device pinv's
+    answer for a factor without exposure; the reference's LAPACK pinv leaves 1e-17 noise, so
+    its correlations are finite) gets a zero F row / column, while an exposed factor with
+    exactly constant returns keeps the reference's NaN correlations."""
+    import torch
+    from pfml.models.risk import _zero_exposureless
+    from pfml.ops.risk_kernels import ewma_factor_cov
+    g = torch.Generator().manual_seed(5)
+    days, K, obs = 400, 5, 300
+    fr = torch.randn(days, K, generator=g, dtype=torch.float64) * 0.01
+    fr[:350, 1] = 0.0                       # no exposure until day 350
+    fr[:, 3] = 0.002                        # exposed, exactly constant
+    ends = np.array([340, 400])
+    tr = np.arange(obs, 0, -1, dtype=np.float64)
+    w = 0.99 ** tr
+    Fm = ewma_factor_cov(fr, ends, obs, w, w, scale=21.0, nan_cor=True).numpy()
+    assert np.isnan(Fm[0, 1, 0]) and np.isnan(Fm[0, 3, 0])
+    _zero_exposureless(Fm, fr, ends, obs)
+    assert (Fm[0, 1, :] == 0).all() and (Fm[0, :, 1] == 0).all()
+    assert np.isnan(Fm[0, 3, 0]) and np.isnan(Fm[1, 3, 0])
+    assert np.isfinite(Fm[1, 1, [0, 2, 4]]).all()           # exposed in window 2
