@@ -154,7 +154,15 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(
   const int tiles = tiles_m * tiles_n;
   const int b = wg / tiles;
   const int tile = wg - b * tiles;
-  const int bm = (tile % tiles_m) * BM, bn = (tile / tiles_m) * BN;
+  // grouped order: bands of GM tile rows walked column by column, so the tiles an XCD runs at
+  // once form a GM x (its share / GM) block that reuses GM A row panels and as many B column
+  // panels from its L2 (column-major over all tile rows re-streamed the whole of A per tile
+  // column once tiles_m > 8)
+  constexpr int GM = 8;
+  const int band = tile / (GM * tiles_n);
+  const int gm = min(GM, tiles_m - band * GM);
+  const int in = tile - band * GM * tiles_n;
+  const int bm = (band * GM + in % gm) * BM, bn = (in / gm) * BN;
   A += (int64_t)b * sA;
   B += (int64_t)b * sB;
   C += (int64_t)b * sC;

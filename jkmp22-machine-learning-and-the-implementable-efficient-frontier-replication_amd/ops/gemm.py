@@ -16,6 +16,7 @@ import os
 import torch
 
 from . import _native as nat
+from ..utils import work as _work
 
 _P, _I, _L, _D = C.c_void_p, C.c_int, C.c_int64, C.c_double
 
@@ -55,6 +56,30 @@ def _blas_gemm(A3, B3, trans_a, trans_b, alpha, beta, C3) -> None:
         torch.bmm(a, b, out=C3) if alpha == 1.0 else C3.copy_(torch.bmm(a, b).mul_(alpha))
     else:
         C3.baddbmm_(a, b, beta=beta, alpha=alpha)
+
+
+def _ledger(ta, tb, M, N, K, batch, A3, B3, C3, ks=None, sks=0, sincos=False, cfg=0,
+            extra_bytes=0):
+    """Work-ledger entry of one pfml_dgemm_ex launch under the kernel name its dispatch picks
+    (the tile / vector-width / k-scale choice of csrc/gemm_f64.hip, mirrored)."""
+    cfg = 0 if cfg < 0 else (cfg or _TILE_DEFAULT)          # -1: pfml_dgemm (always auto)
+    if cfg == 0:
+        cfg = 1 if (M >= 1024 and N >= 1024) else 3
+    if cfg == 1 and sincos:
+        cfg = 3
+    bm, bn = {1: (128, 128), 2: (128, 64)}.get(cfg, (64, 64))
+    lda, ldb = A3.stride(1), B3.stride(1)
+    sa, sb = _bstride(A3, batch), _bstride(B3, batch)
+    a_cont, b_cont = (M if ta else K), (K if tb else N)
+    vec = (a_cont % 2 == 0 and b_cont % 2 == 0 and lda % 2 == 0 and ldb % 2 == 0
+           and sa % 2 == 0 and sb % 2 == 0 and A3.data_ptr() % 16 == 0
+           and B3.data_ptr() % 16 == 0
+           and (ks is None or (ks.data_ptr() % 16 == 0 and sks % 2 == 0)))
+    b = lambda v: "true" if v else "false"                                  # noqa: E731
+    name = f"dgemm_kernel<{b(ta)}, {b(tb)}, {bm}, {bn}, {2 if vec else 1}, {b(ks is not None)}>"
+    na = M * K * (A3.shape[0] if sa else 1)
+    nb = K * N * (B3.shape[0] if sb else 1)
+    _work.add(name, 2.0 * batch * M * N * K, 8.0 * (na + nb + batch * M * N) + extra_bytes)
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, *, trans_a: bool = False, trans_b: bool = False,
@@ -99,6 +124,9 @@ def gemm(A: torch.Tensor, B: torch.Tensor, *, trans_a: bool = False, trans_b: bo
                 B3 = B3.contiguous()
         if C3.stride(-1) != 1:
             raise ValueError("gemm output must have unit inner stride")
+        if _work.on():
+            _ledger(trans_a, trans_b, M, N, K, batch, A3, B3, C3, cfg=-1,
+                    extra_bytes=8.0 * batch * M * N if beta != 0.0 else 0)
         lib = nat.hip_lib()
         err = lib.pfml_dgemm(
             int(trans_a), int(trans_b), M, N, K, batch, float(alpha),
@@ -267,6 +295,11 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
                   int(diag_col0 or 0), float(diag_value), nat.ptr(dv), sdv,
                   int(diag_col0 is not None), nat.ptr(es), ses, int(sincos),
                   int(tile_cfg or _TILE_DEFAULT))
+        if _work.on():
+            _ledger(trans_a, trans_b, M, N, K, batch, A3, B3, C3, ks=ks, sks=sks,
+                    sincos=sincos, cfg=tile_cfg,
+                    extra_bytes=8.0 * batch * M * ((N if beta != 0.0 else 0)
+                                                   + (addend_cols or 0 if E3 is not None else 0)))
         nat.check(nat.hip_lib().pfml_dgemm_ex(
             int(trans_a), int(trans_b), M, N, K, batch,
             A3.data_ptr(), A3.stride(1), _bstride(A3, batch),

@@ -17,6 +17,7 @@ import torch
 
 from . import _native as nat
 from .gemm import gemm, gemm_fused
+from ..utils import work as _work
 from ..utils.log import COUNTERS
 
 
@@ -128,6 +129,7 @@ def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor,
 
     def rec(r0, nn, depth, A):
         if nn <= _REC_LEAF:
+            _work.add("spd_leafinv_kernel", 2.0 * B * nn ** 3, 16.0 * B * nn * nn)
             nat.check(lib.pfml_spd_leafinv_to(A.data_ptr(), A.stride(1), A.stride(0),
                                               X.data_ptr(), ld, sX, B, r0, nn,
                                               status.data_ptr(), st), "pfml_spd_leafinv_to")
@@ -209,6 +211,48 @@ nat.register_hip("pfml_lu_solve2", [C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c
                                     C.c_void_p])
 
 
+def _lu_ledger(M, n, m, ldm, sM, a0, b0, z0, batch) -> None:
+    """Work-ledger entries of one pfml_lu_solve / pfml_lu_solve2 call (csrc/lu_solve.hip loop
+    structure): the rank-nb Gauss-Jordan updates, the panel pivoting and, in the two-level
+    form, the K = 128 panel-transform GEMMs under the dgemm kernel name they launch."""
+    nb = 32 if n <= 512 else 16
+    upd, piv = f"lu_update_kernel<{nb}>", f"lu_pivot_kernel<{nb}, {512 if n <= 512 else 1024}>"
+    if z0 is None:
+        for k0 in range(0, n, nb):
+            b = min(nb, n - k0)
+            nlive = n - (k0 + b) + m
+            _work.add(upd, 2.0 * batch * n * nlive * b, 8.0 * batch * 2 * n * nlive)
+            _work.add(piv, 2.0 * batch * (n - k0) * b * b, 8.0 * batch * (n - k0) * b)
+        return
+    kbw = LU_PANEL_COLS
+    for K0 in range(0, n, kbw):
+        kb = min(kbw, n - K0)
+        aend = K0 + kb
+        for k0 in range(K0, aend, nb):
+            b = min(nb, aend - k0)
+            nlive = aend - (k0 + b) + kb
+            _work.add(upd, 2.0 * batch * n * nlive * b, 8.0 * batch * 2 * n * nlive)
+            _work.add(piv, 2.0 * batch * (n - k0) * b * b, 8.0 * batch * (n - k0) * b)
+        nAr = n - aend
+        nrest = nAr + m
+        if nrest <= 0:
+            continue
+        for off, wdt in ((0, nAr), (nAr, m)):
+            if wdt <= 0:
+                continue
+            # pfml_dgemm(0, 0, rows, wdt, kb): A = Z rows (ld ldm), B = RK + off (ld nrest)
+            vec = (kb % 2 == 0 and wdt % 2 == 0 and ldm % 2 == 0 and nrest % 2 == 0
+                   and sM % 2 == 0 and (kb * nrest) % 2 == 0 and z0 % 2 == 0 and off % 2 == 0
+                   and M.data_ptr() % 16 == 0)
+            for rows in (K0, kb, n - aend):
+                if rows <= 0:
+                    continue
+                big = rows >= 1024 and wdt >= 1024
+                t = "128, 128" if big else "64, 64"
+                _work.add(f"dgemm_kernel<false, false, {t}, {2 if vec else 1}, false>",
+                         2.0 * batch * rows * wdt * kb, 8.0 * batch * (rows * kb + 2 * rows * wdt))
+
+
 def solve_augmented(M: torch.Tensor, n: int, m: int, a0: int, b0: int,
                     status: torch.Tensor | None = None, z0: int | None = None) -> torch.Tensor:
     """In-place solve of augmented systems: rows of M [B, n, W] hold A at columns a0..a0+n and
@@ -231,6 +275,8 @@ def solve_augmented(M: torch.Tensor, n: int, m: int, a0: int, b0: int,
                            device=M.device)
         st = status if status is not None else torch.zeros(Bt, dtype=torch.int32,
                                                            device=M.device)
+        if _work.on():
+            _lu_ledger(M, n, m, W, nn * W, a0, b0, z0, Bt)
         if z0 is not None:
             if z0 + LU_PANEL_COLS > W:
                 raise ValueError("solve_augmented: z0 needs LU_PANEL_COLS scratch columns")
@@ -346,6 +392,8 @@ def mf_sym(mode: int, X: torch.Tensor, Y: torch.Tensor | None, out: torch.Tensor
             raise ValueError("mf_sym: a and mask need the same batch stride")
         if mask is not None and a is None:
             sv = mask.stride(0)
+        _work.add("mfunc_sym_kernel", 6.0 * B * N * N,
+                 8.0 * B * N * N * (2 + (Y is not None)))
         args = _MfArgs(mode, B, N, N, N * N, X.data_ptr(), nat.ptr(Y), out.data_ptr(),
                        nat.ptr(svec), nat.ptr(cvec), nat.ptr(a), nat.ptr(mask), sv, float(d))
         nat.check(nat.hip_lib().pfml_mfunc_sym(C.byref(args), nat.stream_of(X)), "pfml_mfunc_sym")
@@ -374,9 +422,11 @@ def _db_mu(M: torch.Tensor, Minv: torch.Tensor, unscaled: bool, out: torch.Tenso
     B, N, _ = M.shape
     if nat.is_device(M):
         lib = nat.hip_lib()
-        work = torch.empty(lib.pfml_db_mu_work_doubles(B), dtype=torch.float64, device=M.device)
+        if not unscaled:                         # (unscaled steps launch no norm pass)
+            _work.add("db_norm_partial_kernel", 4.0 * B * N * N, 16.0 * B * N * N)
+        wbuf = torch.empty(lib.pfml_db_mu_work_doubles(B), dtype=torch.float64, device=M.device)
         nat.check(lib.pfml_db_mu(M.data_ptr(), Minv.data_ptr(), B, N, N, N * N, int(unscaled),
-                                 out.data_ptr(), work.data_ptr(), nat.stream_of(M)), "pfml_db_mu")
+                                 out.data_ptr(), wbuf.data_ptr(), nat.stream_of(M)), "pfml_db_mu")
         return
     if unscaled:
         out.fill_(1.0)

@@ -11,6 +11,7 @@ import ctypes as C
 import torch
 
 from . import _native as nat
+from ..utils import work as _work
 from .gemm import gemm_fused, gemm_prec
 
 nat.register_hip("pfml_rff_sincos", [C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_int64,
@@ -76,6 +77,7 @@ def standardize_signals(F: torch.Tensor, idx: torch.Tensor, mask: torch.Tensor,
             n_real = mask.sum(1).to(torch.int32)
         n_real = n_real.to(torch.int32).contiguous()
         rows = idx.to(torch.int64).contiguous()
+        _work.add("standardize", 6.0 * B * TH * N * P, 8.0 * B * TH * N * (P + Pw))
         nat.check(nat.hip_lib().pfml_standardize(
             F.data_ptr(), P, F.stride(0), rows.data_ptr(), n_real.data_ptr(), B, TH, N,
             vol.data_ptr(), out.data_ptr(), out.stride(2), out.stride(1), Pw,

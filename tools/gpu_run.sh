@@ -49,6 +49,18 @@ for step in ${MODE//,/ }; do
     dgemm)
       timeout -k 10 200 python tools/micro/dgemm_rate.py > $OUT/dgemm_rate.json 2>&1
       rc=$?; tail -4 $OUT/dgemm_rate.json; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    s4roof)
+      # S4 roofline: one-batch S4 (+ grid step) under a kernel trace with the work ledger on
+      (cd /tmp && export TMPDIR=/tmp PFML_WORK_LEDGER=$OUT/work_ledger.json && timeout -k 10 600 rocprofv3 --kernel-trace -d $OUT/prof_s4r -o run -- python3 $ROOT/bench.py --with-inputs --steps 1 --warmup 0 > $OUT/prof_s4r.log 2>&1)
+      rc=$?; tail -1 $OUT/prof_s4r.log | cut -c1-300; if [ $rc -ne 0 ]; then tail -5 $OUT/prof_s4r.log; exit $rc; fi
+      python tools/roofline_s4.py $(find $OUT/prof_s4r -name "*.db" | head -1) $OUT/work_ledger.json > $OUT/roofline_s4.md 2>&1
+      rc=$?; cat $OUT/roofline_s4.md | head -30; python tools/rocprof_summary.py $(find $OUT/prof_s4r -name "*.db" | head -1) --top 40 > $OUT/kernels_s4r.txt 2>&1; rm -rf $OUT/prof_s4r; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    dgemmpmc)
+      # in-house DGEMM on the Horner shape / large squares: TF/s, then one PMC pass
+      timeout -k 10 200 python tools/micro/dgemm_shapes.py 5 > $OUT/dgemm_shapes.log 2>&1
+      rc=$?; tail -1 $OUT/dgemm_shapes.log; if [ $rc -ne 0 ]; then tail -5 $OUT/dgemm_shapes.log; exit $rc; fi
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/dgemm_pmc -o run -- python3 $ROOT/tools/micro/dgemm_shapes.py 2 > $OUT/dgemm_pmc.log 2>&1)
+      rc=$?; python tools/pmc_summary.py $OUT/dgemm_pmc --top 8 > $OUT/dgemm_pmc.txt 2>&1; cat $OUT/dgemm_pmc.txt; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     suite)
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
       rc=$?; tail -2 $OUT/pytest_gpu.log
@@ -118,6 +130,12 @@ for step in ${MODE//,/ }; do
     benchfused)
       PFML_BAND_MODE=fused timeout -k 10 300 python bench.py --no-inputs > $OUT/bench_fused.json 2> $OUT/bench_fused.err
       rc=$?; grep '^{' $OUT/bench_fused.json | cut -c1-300; if [ $rc -ne 0 ]; then tail -5 $OUT/bench_fused.err; exit $rc; fi ;;
+    abband)
+      # headline bench: the one-WG-per-cell reduction (single) vs the cooperative one, A/B/A/B
+      for m in single coop single coop; do
+        PFML_BAND_MODE=$m timeout -k 10 200 python bench.py > $OUT/bench_$m.json 2> $OUT/bench_$m.err
+        rc=$?; echo "$m: $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_$m.json)"; if [ $rc -ne 0 ]; then tail -5 $OUT/bench_$m.err; exit $rc; fi
+      done ;;
     timeline)
       # kernel timeline of the last full 1-GPU grid step
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/prof1 -o run -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-inputs > $OUT/prof1.log 2>&1)
