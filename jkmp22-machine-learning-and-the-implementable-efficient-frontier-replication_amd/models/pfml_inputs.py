@@ -464,7 +464,9 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
         eye = torch.eye(N, dtype=torch.float64, device=dev)
         Tb[0][:, :, :GP] = S[:, lb]
         Tb[0][:, :, GP:Wd] = eye
-        gemm_fused(mt, eye, Tb[0][:, :, Wd:], row_scale=a, k_scale=(Dg[:, lb] * ainv))  # R_11
+        # R_11 = diag(a) m_tilde diag(D_11 / a): elementwise, in the rounding order the fused
+        # GEMM against the identity produced ((m_tilde * k-scale) * row scale)
+        torch.mul(mt * (Dg[:, lb] * ainv).unsqueeze(-2), a.unsqueeze(-1), out=Tb[0][:, :, Wd:])
         cur = 0
         for th in range(lb - 1, 0, -1):
             gemm_fused(mt, Tb[cur], Tb[cur ^ 1], row_scale=a, k_scale=(Dg[:, th] * ainv),
@@ -478,11 +480,11 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
         T0, U0 = T0f[:, :, :Wd], U0f[:, :, :Wd]
         gemm_fused(mt, T1[:, :, :Wd], T0, row_scale=a, k_scale=(Dg[:, 0] * ainv),
                    addend=S[:, 0], addend_cols=GP, diag_col0=GP, diag_value=1.0)
-        SI = torch.empty((B, N, Wd), dtype=torch.float64, device=dev)
-        SI[:, :, :GP] = S[:, lb + 1]
-        SI[:, :, GP:] = eye
-        gemm_fused(T1[:, :, Wd:], SI, U0, addend=T1[:, :, :Wd], addend_cols=Wd)   # T_1 + Q [S_12|I]
-        del Tb, T1, SI
+        # U_0 = T_1 + Q [S_12 | I]: the S_12 block on the GEMM, the identity block as Q + T_1
+        gemm_fused(T1[:, :, Wd:], S[:, lb + 1], U0[:, :, :GP], addend=T1[:, :, :GP],
+                   addend_cols=GP)
+        torch.add(T1[:, :, Wd:], T1[:, :, GP:Wd], out=U0[:, :, GP:])
+        del Tb, T1
         sig0 = S[:, 0].clone()                                      # signal_t blocks
         del S
         # omega = const^-1 Omega, solved in place on the augmented [Omega | const] rows (K7)

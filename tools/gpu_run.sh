@@ -199,7 +199,7 @@ for step in ${MODE//,/ }; do
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_ANY --output-format csv -d $OUT/pmc -o run -- python3 $ROOT/bench.py --steps 1 --warmup 0 --no-inputs > $OUT/pmc.log 2>&1)
       rc=$?; python tools/pmc_summary.py $OUT/pmc --top 10 > $OUT/pmc.txt 2>&1; cat $OUT/pmc.txt; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     multiproc)
-      timeout -k 10 300 bash tools/gpu_multiproc.sh $TAG ;;
+      timeout -k 10 900 bash tools/gpu_multiproc.sh $TAG ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
