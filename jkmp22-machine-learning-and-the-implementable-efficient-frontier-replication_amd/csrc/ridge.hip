@@ -7,17 +7,13 @@
 //
 //     beta_l = Q (T + l I)^-1 Q^T rbar
 //
+// Used for 528 < n <= 1024 (p up to 1023; the band path, ridge_band.hip, takes n <= 528).
 // One 1024-thread workgroup owns one (g, year, p) cell.
 //
-// Phase A (tridiagonalisation).  The n x n working copy lives in global memory (L2-resident:
-//   2.1 MB at n = 513) in FULL symmetric storage.  Each Householder step makes ONE fused
-//   read+write sweep of the trailing matrix that applies the previous step's rank-2 update
-//   and, in the same sweep, accumulates the next step's symmetric mat-vec (textbook sytd2
-//   needs two sweeps).  The sweep is column-oriented: lane l of a wave owns column i and walks
-//   rows j, so A[j][i] loads are coalesced across lanes and, because A is symmetric, the
-//   mat-vec sum  p_i = sum_j A[j][i] v_j  accumulates inside the lane with no cross-lane
-//   reduction; 8-way unrolled rows keep 8 loads per lane in flight.  The rank-2 update term is
-//   evaluated as (v_j w_i + w_j v_i) with contraction off so A stays bitwise symmetric.
+// Phase A (tridiagonalisation, blocked as LAPACK dlatrd: ridge_tridiag_blocked_kernel).  The
+//   n x n working copy lives in global memory (L2-resident) in FULL symmetric storage; within
+//   a panel of PB reflectors the sweeps read the panel-start matrix, corrected on the fly, and
+//   the trailing matrix gets one rank-2PB update per panel.
 // Phase B (lambda sweep).  One thread per lambda runs Gaussian elimination with partial
 //   pivoting on T + l I (as LAPACK dgtsv), so l = 0 on a singular-ish Dbar behaves like the
 //   reference's pivoted LU; the back-substitution prefetches its operands 8 rows ahead.
@@ -30,7 +26,7 @@
 
 namespace {
 
-constexpr int NMAX = 1024;      // largest p+1 supported (p_max = 512 -> 513)
+constexpr int NMAX = 1024;      // largest n = p + 1 supported
 constexpr int NT = 1024;        // threads per workgroup
 constexpr int NW = NT / 64;
 constexpr int YREG = 33;        // rows of Y per lane in the register back-transform (n <= 528)
@@ -38,168 +34,6 @@ constexpr int RMAX = 528;       // reflector row length staged by the back-trans
 constexpr int KB = 4;           // reflectors per staging block
 
 typedef RidgeCellDesc CellDesc;
-
-__device__ __forceinline__ double rank2(double a, double vj, double wi, double wj, double vi) {
-#pragma clang fp contract(off)
-  const double s = vj * wi + wj * vi;
-  return a - s;
-}
-
-__global__ __launch_bounds__(NT) void ridge_tridiag_kernel(
-    const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
-    const CellDesc* __restrict__ cells, int L, double* __restrict__ work) {
-  __shared__ double v[NMAX], vp[NMAX], wp[NMAX], pk[NMAX], z[NMAX];
-  __shared__ double dd[NMAX], ee[NMAX], tau[NMAX];
-  __shared__ double part[NT];                 // sweep partials / back-transform partials
-  __shared__ double red[NW * 2];
-
-  const CellDesc cd = cells[blockIdx.x];
-  const int n = cd.n;
-  const int t = threadIdx.x, lane = t & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  double* A = work + cd.work;                 // n x n, ld n
-  double* Y = A + (int64_t)n * n;             // n x L  ([i][l])
-  double* Ua = Y + (int64_t)n * L;            // pivoted-LU of T + lI, per lambda, [i][l]
-  double* Ub = Ua + (int64_t)n * L;
-  double* Uc = Ub + (int64_t)n * L;
-  double* Uy = Uc + (int64_t)n * L;
-  const double* S = SD + cd.src;
-  const double sc = cd.scale;
-
-  // ---- load scaled copy + rhs ---------------------------------------------------------
-  for (int i = wid; i < n; i += NW) {
-    const double* srow = S + (int64_t)i * ldS;
-    double* arow = A + (int64_t)i * n;
-    for (int j = lane; j < n; j += 64) arow[j] = srow[j] * sc;
-  }
-  for (int i = t; i < n; i += NT) {
-    z[i] = Sr[cd.rsrc + i] * sc;
-    vp[i] = 0.0;
-    wp[i] = 0.0;
-    v[i] = 0.0;
-  }
-  __syncthreads();
-
-  auto bsum2 = [&](double a, double b, double& ra, double& rb) {
-    a = wave_sum(a);
-    b = wave_sum(b);
-    if (lane == 0) { red[wid] = a; red[NW + wid] = b; }
-    __syncthreads();
-    double sa = 0.0, sb = 0.0;
-#pragma unroll
-    for (int q = 0; q < NW; ++q) { sa += red[q]; sb += red[NW + q]; }
-    ra = sa;
-    rb = sb;
-    __syncthreads();
-  };
-
-  // ================================ Phase A ============================================
-  for (int k = 0; k + 2 < n; ++k) {
-    // (1) row k (== column k) with the previous rank-2 update applied: c_i, i >= k
-    const double vpk = vp[k], wpk = wp[k];
-    const double* rowk = A + (int64_t)k * n;
-    for (int i = k + t; i < n; i += NT) pk[i] = rank2(rowk[i], vpk, wp[i], wpk, vp[i]);
-    __syncthreads();
-    // (2) Householder vector from x = c[k+1:]
-    double x2 = 0.0;
-    for (int i = k + 2 + t; i < n; i += NT) x2 += pk[i] * pk[i];
-    double xnorm2, dummy;
-    bsum2(x2, 0.0, xnorm2, dummy);
-    const double alpha = pk[k + 1];
-    double tk, ek, scal;
-    if (xnorm2 == 0.0) {
-      tk = 0.0; ek = alpha; scal = 0.0;
-    } else {
-      const double bet = -copysign(sqrt(alpha * alpha + xnorm2), alpha);
-      tk = (bet - alpha) / bet;
-      scal = 1.0 / (alpha - bet);
-      ek = bet;
-    }
-    if (t == 0) { dd[k] = pk[k]; ee[k] = ek; tau[k] = tk; }
-    double* rowk_w = A + (int64_t)k * n;
-    for (int i = k + 1 + t; i < n; i += NT) {
-      const double vi = (i == k + 1) ? 1.0 : pk[i] * scal;
-      v[i] = vi;
-      rowk_w[i] = vi;                           // row k now stores reflector k
-    }
-    __syncthreads();
-    // (3) fused column-oriented sweep over rows/cols r0..n-1
-    const int r0 = k + 1, m = n - r0;
-    const int ncb = (m + 63) >> 6;
-    const int nrg = NW / ncb;
-    {
-      const int cb = wid % ncb, rg = wid / ncb;
-      if (rg < nrg) {
-        const int c = cb * 64 + lane;
-        const int i = r0 + c;
-        const int rows_per = (m + nrg - 1) / nrg;
-        const int j0 = r0 + rg * rows_per;
-        const int j1 = min(n, j0 + rows_per);
-        double acc = 0.0;
-        if (i < n) {
-          const double vpi = vp[i], wpi = wp[i];
-          double* col = A + i;
-          int j = j0;
-          for (; j + 8 <= j1; j += 8) {
-            double a[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) a[u] = col[(int64_t)(j + u) * n];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              a[u] = rank2(a[u], vp[j + u], wpi, wp[j + u], vpi);
-              col[(int64_t)(j + u) * n] = a[u];
-              acc += a[u] * v[j + u];
-            }
-          }
-          for (; j < j1; ++j) {
-            double a = rank2(col[(int64_t)j * n], vp[j], wpi, wp[j], vpi);
-            col[(int64_t)j * n] = a;
-            acc += a * v[j];
-          }
-        }
-        part[rg * (ncb * 64) + c] = acc;
-      }
-    }
-    __syncthreads();
-    for (int c = t; c < m; c += NT) {
-      double s = 0.0;
-      for (int q = 0; q < nrg; ++q) s += part[q * (ncb * 64) + c];
-      pk[r0 + c] = tk * s;
-    }
-    __syncthreads();
-    // (4) w = p - (tau/2)(p.v) v ;  z <- H_k z
-    double pv = 0.0, vz = 0.0;
-    for (int i = r0 + t; i < n; i += NT) { pv += pk[i] * v[i]; vz += v[i] * z[i]; }
-    double spv, svz;
-    bsum2(pv, vz, spv, svz);
-    const double half = 0.5 * tk * spv;
-    for (int i = r0 + t; i < n; i += NT) {
-      wp[i] = pk[i] - half * v[i];
-      vp[i] = v[i];
-      z[i] -= tk * svz * v[i];
-    }
-    __syncthreads();
-  }
-  // trailing 2 x 2 (or smaller) block
-  if (t == 0) {
-    if (n >= 2) {
-      const int a = n - 2, b = n - 1;
-      dd[a] = rank2(A[(int64_t)a * n + a], vp[a], wp[a], wp[a], vp[a]);
-      ee[a] = rank2(A[(int64_t)a * n + b], vp[a], wp[b], wp[a], vp[b]);
-      dd[b] = rank2(A[(int64_t)b * n + b], vp[b], wp[b], wp[b], vp[b]);
-    } else {
-      dd[0] = A[0];
-    }
-  }
-  __syncthreads();
-
-  // export the tridiagonal factor and Q^T r for the lambda sweep / back-transform kernels
-  double* dg = Uy + (int64_t)n * L;
-  double* eg = dg + n;
-  double* tg = eg + n;
-  double* zg = tg + n;
-  for (int i = t; i < n; i += NT) { dg[i] = dd[i]; eg[i] = ee[i]; tg[i] = tau[i]; zg[i] = z[i]; }
-}
 
 // Phase A, blocked variant (LAPACK dlatrd structure, panels of PB reflectors).  Within a panel
 // the sweeps are READ-ONLY against the panel-start matrix A0, corrected on the fly by the
@@ -417,294 +251,6 @@ __global__ __launch_bounds__(NT) void ridge_tridiag_blocked_kernel(
   for (int i = t; i < n; i += NT) { dg[i] = dd[i]; eg[i] = ee[i]; tg[i] = tau[i]; zg[i] = z[i]; }
 }
 
-// Phase A, fast path for n <= NV (p_max <= 512): same blocked algorithm with PF = 8
-// reflectors per panel and EVERYTHING except A itself in LDS (V/W panel, vectors), so the
-// only global round trips per reflector are the sweep itself and one row of A0 (prefetched a
-// step ahead inside a panel).  The read-only sweep is software-pipelined: the next 16 rows of
-// the lane's column are in flight while the current 16 are consumed.
-constexpr int NV = 513;       // fast path: n <= 513 keeps every sweep within 8 column blocks
-constexpr int PF = 8;
-constexpr int SW = 16;         // sweep rows per load batch
-constexpr int NBUF = 4;        // batches in the sweep's load ring (NBUF-1 in flight)
-constexpr int TB = 4;          // trailing-update tiles per wave per pass
-constexpr int VPAD = NBUF * SW;   // zero tail of v read by the last (ring-padded) partition
-constexpr int NTF = 512;       // fast path: 8 waves, up to 256 VGPRs per lane
-constexpr int NWF = NTF / 64;
-
-__global__ __launch_bounds__(NTF) void ridge_tridiag_fast_kernel(
-    const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
-    const CellDesc* __restrict__ cells, int L, double* __restrict__ work,
-    long long* __restrict__ tim) {
-  // optional per-phase cycle accounting (tools/bench_ridge.py --timing): thread 0 only
-  long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  long long tlast = 0;
-#define PFML_TMARK(ph)                                                   \
-  if (tim != nullptr && threadIdx.x == 0) {                              \
-    const long long now = (long long)__builtin_amdgcn_s_memtime();       \
-    tacc[ph] += now - tlast;                                             \
-    tlast = now;                                                         \
-  }
-  __shared__ double VWs[NV + 16][2 * PF + 1];     // rows >= n stay zero
-  __shared__ double v[NV + VPAD], pk[NV], z[NV], dd[NV], ee[NV], tau[NV];
-  __shared__ double part[NTF];
-  __shared__ double red[NWF * 2];
-  __shared__ double red32[NTF / 16][2 * PF + 1];
-  __shared__ double xy[2 * PF], vwk[2 * PF];
-
-  const CellDesc cd = cells[blockIdx.x];
-  const int n = cd.n;
-  const int t = threadIdx.x, lane = t & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  double* A = work + cd.work;
-  double* Y = A + (int64_t)n * n;
-  double* Uy = Y + 4LL * n * L;
-  double* dg = Uy + (int64_t)n * L;
-  double* eg = dg + n;
-  double* tg = eg + n;
-  double* zg = tg + n;
-  const double* S = SD + cd.src;
-  const double sc = cd.scale;
-
-  for (int i = wid; i < n; i += NWF) {
-    const double* srow = S + (int64_t)i * ldS;
-    double* arow = A + (int64_t)i * n;
-    for (int j = lane; j < n; j += 64) arow[j] = srow[j] * sc;
-  }
-  for (int i = t; i < n; i += NTF) z[i] = Sr[cd.rsrc + i] * sc;
-  for (int i = n + t; i < NV + VPAD; i += NTF) v[i] = 0.0;
-  for (int e = t; e < (NV + 16 - n) * (2 * PF + 1); e += NTF) (&VWs[n][0])[e] = 0.0;
-  __syncthreads();
-
-  auto bsum2 = [&](double a, double b, double& ra, double& rb) {
-    a = wave_sum(a);
-    b = wave_sum(b);
-    if (lane == 0) { red[wid] = a; red[NWF + wid] = b; }
-    __syncthreads();
-    double sa = 0.0, sb = 0.0;
-#pragma unroll
-    for (int q = 0; q < NWF; ++q) { sa += red[q]; sb += red[NWF + q]; }
-    ra = sa;
-    rb = sb;
-    __syncthreads();
-  };
-
-  const int kend = n - 2;
-  if (tim != nullptr && threadIdx.x == 0) tlast = (long long)__builtin_amdgcn_s_memtime();
-  for (int k0 = 0; k0 < kend; k0 += PF) {
-    const int nbp = min(PF, kend - k0);
-    constexpr int RP = (NV + NTF - 1) / NTF;     // row elements per thread
-    double rcur[RP];                              // row k0 of A0, i = k0 + t + h*NTF
-#pragma unroll
-    for (int h = 0; h < RP; ++h) {
-      const int i = k0 + t + h * NTF;
-      rcur[h] = (i < n) ? A[(int64_t)k0 * n + i] : 0.0;
-    }
-    for (int j = 0; j < nbp; ++j) {
-      const int k = k0 + j;
-      // prefetch row k+1 of A0 (unchanged inside the panel) for the next step
-      double rnext[RP];
-#pragma unroll
-      for (int h = 0; h < RP; ++h) {
-        const int i = k + 1 + t + h * NTF;
-        rnext[h] = (j + 1 < nbp && i < n) ? A[(int64_t)(k + 1) * n + i] : 0.0;
-      }
-      // (1) column k, panel-corrected
-      if (t < 2 * PF) vwk[t] = (t % PF < j) ? VWs[k][t] : 0.0;
-      __syncthreads();
-#pragma unroll
-      for (int h = 0; h < RP; ++h) {
-        const int i = k + t + h * NTF;
-        if (i < n) {
-          double c = rcur[h];
-          for (int q = 0; q < j; ++q) c -= VWs[i][q] * vwk[PF + q] + VWs[i][PF + q] * vwk[q];
-          pk[i] = c;
-        }
-      }
-      __syncthreads();
-      PFML_TMARK(0)
-      // (2) Householder vector
-      double x2 = 0.0;
-      for (int i = k + 2 + t; i < n; i += NTF) x2 += pk[i] * pk[i];
-      double xnorm2, dummy;
-      bsum2(x2, 0.0, xnorm2, dummy);
-      const double alpha = pk[k + 1];
-      double tk, ek, scal;
-      if (xnorm2 == 0.0) {
-        tk = 0.0; ek = alpha; scal = 0.0;
-      } else {
-        const double bet = -copysign(sqrt(alpha * alpha + xnorm2), alpha);
-        tk = (bet - alpha) / bet;
-        scal = 1.0 / (alpha - bet);
-        ek = bet;
-      }
-      if (t == 0) { dd[k] = pk[k]; ee[k] = ek; tau[k] = tk; }
-      for (int i = k + 1 + t; i < n; i += NTF) {
-        const double vi = (i == k + 1) ? 1.0 : pk[i] * scal;
-        v[i] = vi;
-        A[(int64_t)k * n + i] = vi;                // reflector k for the back-transform
-        VWs[i][j] = vi;
-      }
-      __syncthreads();
-      PFML_TMARK(1)
-      // (3) pipelined read-only sweep + correction dots
-      const int r0 = k + 1, m = n - r0;
-      const int ncb = (m + 63) >> 6;
-      const int nrg = NWF / ncb;
-      {
-        const int cb = wid % ncb, rg = wid / ncb;
-        if (rg < nrg) {
-          const int c = cb * 64 + lane;
-          const int i = r0 + c;
-          // row partitions are whole rings (NBUF*SW rows) so no batch straddles two partitions
-          constexpr int RING = NBUF * SW;
-          const int rows_per = ((m + nrg - 1) / nrg + RING - 1) / RING * RING;
-          const int j0 = r0 + rg * rows_per;
-          const int nit = max(0, min(rows_per, n - j0) + RING - 1) / RING;
-          double acc0 = 0.0, acc1 = 0.0;
-          // raw buffer loads: the lane's column offset lives in ONE VGPR, the wave-uniform row
-          // offset in an SGPR (soffset), so in-flight rows cost only their data registers.
-          // Rows past the partition (ring padding, the ring's last prefetches) are clamped to
-          // its last row, which is cache-hot and finite; their weights come from the zero tail
-          // of v (or are never consumed).  Columns past n only feed part[c >= m], never read.
-          const int vo = i * 8;
-          const int rlim = min(n, j0 + nit * RING) - 1;
-          const __amdgpu_buffer_rsrc_t rs =
-              __builtin_amdgcn_make_buffer_rsrc(A, (short)0, n * n * 8, 0x00020000);
-          auto ldrow = [&](int row) -> double {
-            const int so = __builtin_amdgcn_readfirstlane(min(row, rlim) * n * 8);
-            return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0));
-          };
-          // NBUF-stage ring of SW-row batches with no branches inside the loop body, so the
-          // waitcnt pass keeps (NBUF-1)*SW loads in flight while one batch is consumed.
-          double a[NBUF][SW];
-          if (nit > 0) {
-#pragma unroll
-            for (int s = 0; s < NBUF - 1; ++s)
-#pragma unroll
-              for (int u = 0; u < SW; ++u) a[s][u] = ldrow(j0 + s * SW + u);
-          }
-          for (int it = 0; it < nit; ++it) {
-#pragma unroll
-            for (int s = 0; s < NBUF; ++s) {
-              const int l0 = j0 + (it * NBUF + s) * SW;
-              const int lp = l0 + (NBUF - 1) * SW;
-#pragma unroll
-              for (int u = 0; u < SW; ++u) a[(s + NBUF - 1) % NBUF][u] = ldrow(lp + u);
-#pragma unroll
-              for (int u = 0; u < SW; u += 2) {
-                acc0 += a[s][u] * v[l0 + u];
-                acc1 += a[s][u + 1] * v[l0 + u + 1];
-              }
-            }
-          }
-          part[rg * (ncb * 64) + c] = acc0 + acc1;
-        }
-      }
-      {
-        const int q = t & 15, pr = t >> 4;        // NTF/16 row partitions x 16 (V|W) columns
-        double s = 0.0;
-        if ((q & (PF - 1)) < j)
-          for (int i = r0 + pr; i < n; i += NTF / 16) s += VWs[i][q] * v[i];
-        red32[pr][q] = s;
-      }
-      __syncthreads();
-      PFML_TMARK(2)
-      if (t < 2 * PF) {
-        double s = 0.0;
-#pragma unroll 8
-        for (int pr = 0; pr < NTF / 16; ++pr) s += red32[pr][t];
-        xy[t] = s;                                 // xy[0..PF) = V'v, xy[PF..) = W'v
-      }
-      __syncthreads();
-      PFML_TMARK(3)
-      // (4) p, w, z
-      double pv = 0.0, vz = 0.0;
-      for (int c = t; c < m; c += NTF) {
-        double s = 0.0;
-        for (int qq = 0; qq < nrg; ++qq) s += part[qq * (ncb * 64) + c];
-        const int i = r0 + c;
-        for (int q = 0; q < j; ++q) s -= VWs[i][q] * xy[PF + q] + VWs[i][PF + q] * xy[q];
-        s *= tk;
-        pk[i] = s;
-        pv += s * v[i];
-        vz += v[i] * z[i];
-      }
-      double spv, svz;
-      bsum2(pv, vz, spv, svz);
-      const double half = 0.5 * tk * spv;
-      for (int i = r0 + t; i < n; i += NTF) {
-        VWs[i][PF + j] = pk[i] - half * v[i];
-        z[i] -= tk * svz * v[i];
-      }
-      __syncthreads();
-      PFML_TMARK(4)
-#pragma unroll
-      for (int h = 0; h < RP; ++h) rcur[h] = rnext[h];
-    }
-    PFML_TMARK(6)
-    // (5) rank-2*nbp trailing update (rows, cols >= k0 + nbp), fp64 MFMA, VW from LDS
-    const int r0 = k0 + nbp, m = n - r0;
-    if (m > 0) {
-      const int nt = (m + 15) >> 4;
-      const int g4 = lane >> 4, c16 = lane & 15;
-      // TB tiles per wave per pass: all 4*TB loads are issued before the first MFMA so the
-      // pass costs one memory latency, not TB.  (Plain global stores: raw buffer stores here
-      // were not seen by the next panel's loads.)
-      const int ntt = nt * nt;
-      for (int tb = wid * TB; tb < ntt; tb += NWF * TB) {
-        double4_t acc[TB];
-        int off[TB][4];
-#pragma unroll
-        for (int u = 0; u < TB; ++u) {
-          const int tile = min(tb + u, ntt - 1);
-          const bool tv = tb + u < ntt;
-          const int i0 = r0 + (tile / nt) * 16, j0 = r0 + (tile % nt) * 16;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int i = i0 + PFML_F64_CROW(lane, r), jj = j0 + c16;
-            off[u][r] = (tv && i < n && jj < n) ? i * n + jj : -1;
-            acc[u][r] = (off[u][r] >= 0) ? A[off[u][r]] : 0.0;
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < TB; ++u) {
-          const int tile = min(tb + u, ntt - 1);
-          const int ia = r0 + (tile / nt) * 16 + c16, jb = r0 + (tile % nt) * 16 + c16;
-#pragma unroll
-          for (int q0 = 0; q0 < 2 * PF; q0 += 4) {
-            const int q = q0 + g4;
-            const bool qv = (q & (PF - 1)) < nbp;
-            const double ua = qv ? -VWs[ia][q] : 0.0;
-            const double zb = qv ? VWs[jb][q < PF ? PF + q : q - PF] : 0.0;
-            acc[u] = mfma_f64_16x16x4(ua, zb, acc[u]);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < TB; ++u)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (off[u][r] >= 0) A[off[u][r]] = acc[u][r];
-      }
-    }
-    __syncthreads();
-    PFML_TMARK(5)
-  }
-  if (t == 0) {
-    if (n >= 2) {
-      dd[n - 2] = A[(int64_t)(n - 2) * n + n - 2];
-      ee[n - 2] = A[(int64_t)(n - 1) * n + n - 2];
-      dd[n - 1] = A[(int64_t)(n - 1) * n + n - 1];
-    } else {
-      dd[0] = A[0];
-    }
-  }
-  __syncthreads();
-  for (int i = t; i < n; i += NTF) { dg[i] = dd[i]; eg[i] = ee[i]; tg[i] = tau[i]; zg[i] = z[i]; }
-  if (tim != nullptr && threadIdx.x == 0)
-    for (int q = 0; q < 8; ++q) tim[(int64_t)blockIdx.x * 8 + q] = tacc[q];
-#undef PFML_TMARK
-}
-
 // Phase B: one thread per (cell, lambda) over the whole GPU.
 __global__ __launch_bounds__(256) void ridge_trisolve_kernel(
     const CellDesc* __restrict__ cells, int ncells, const double* __restrict__ lvec, int L,
@@ -911,9 +457,8 @@ __global__ __launch_bounds__(NT) void ridge_backtransform_kernel(
 extern "C" int64_t pfml_ridge_band_work_doubles(int n, int L);
 extern "C" int pfml_ridge_band_nmax();
 extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, const double* Sr,
-                                             const void* cells, int ncells, int nmax,
-                                             const double* lvec, int L, double* work,
-                                             double* beta_out, int64_t ldo, int band_mode,
+                                             const void* cells, int ncells, const double* lvec,
+                                             int L, double* work, double* beta_out, int64_t ldo,
                                              long long* tim, int* lu_list, int* lu_count,
                                              int lu_cap, const int* wgmap, int nwg,
                                              unsigned* syncw, hipStream_t st);
@@ -928,43 +473,28 @@ extern "C" int64_t pfml_ridge_work_doubles(int n, int L) {
 }
 
 static long long* g_ridge_timing = nullptr;
-// Debug: per-cell phase cycle counters of the fast tridiagonalisation (8 per cell).
+// Debug: per-cell phase cycle counters of the band reduction (tools/bench_ridge.py --timing).
 extern "C" void pfml_ridge_set_timing(long long* buf) { g_ridge_timing = buf; }
 
-// band_mode: 0 = PFML_BAND_MODE / default, 1 = one workgroup per cell, 2 = multi-workgroup.
-// lu_list / lu_count / lu_cap (band path only; count zeroed on the stream by the banded solve,
-// nullptr = off): the
-// in-band pivoted-LU repair of non-SPD lambdas; the tridiagonal path leaves its NaN markers
-// to the dense repair (ridge_repair.hip).
+// n <= 528: the band path (ridge_band.hip: cooperative reduction, banded Cholesky, in-band
+// pivoted-LU repair of non-SPD lambdas through lu_list / lu_count / lu_cap, nullptr = off);
+// 528 < n <= 1024: the blocked tridiagonal path below, whose NaN markers go to the dense
+// repair (ridge_repair.hip).
 extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const double* Sr,
                                       const void* cells, int ncells, int nmax,
                                       const double* lvec, int L, double* work, double* beta_out,
-                                      int64_t ldo, int band_mode, int* lu_list, int* lu_count,
-                                      int lu_cap, const int* wgmap, int nwg, unsigned* syncw,
+                                      int64_t ldo, int* lu_list, int* lu_count, int lu_cap,
+                                      const int* wgmap, int nwg, unsigned* syncw,
                                       hipStream_t st) {
   if (ncells <= 0) return hipSuccess;
   if (L > 128 || nmax > NMAX) return hipErrorInvalidValue;
-  if (band_mode == 4 && nmax > pfml_ridge_band_nmax()) return hipErrorInvalidValue;
   const CellDesc* cd = static_cast<const CellDesc*>(cells);
-  // PFML_RIDGE_VARIANT: band (default) | tridiag-fast | unblocked | blocked
-  const char* var = getenv("PFML_RIDGE_VARIANT");
-  const bool force_unblocked = var && var[0] == 'u';
-  const bool force_blocked = var && var[0] == 'b' && var[1] == 'l';
-  const bool force_fast = var && (var[0] == 'f' || var[0] == 't');
-  if (!force_unblocked && !force_blocked && !force_fast && !getenv("PFML_RIDGE_UNBLOCKED") &&
-      nmax <= pfml_ridge_band_nmax())
-    return pfml_ridge_band_launch(SD, ldS, Sr, cells, ncells, nmax, lvec, L, work, beta_out,
-                                  ldo, band_mode, g_ridge_timing, lu_list, lu_count, lu_cap,
-                                  wgmap, nwg, syncw, st);
-  if (force_unblocked || (getenv("PFML_RIDGE_UNBLOCKED") != nullptr))
-    hipLaunchKernelGGL(ridge_tridiag_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr, cd, L,
-                       work);
-  else if (force_blocked || nmax > NV)
-    hipLaunchKernelGGL(ridge_tridiag_blocked_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr,
-                       cd, L, work);
-  else
-    hipLaunchKernelGGL(ridge_tridiag_fast_kernel, dim3(ncells), dim3(NTF), 0, st, SD, ldS, Sr, cd,
-                       L, work, g_ridge_timing);
+  if (nmax <= pfml_ridge_band_nmax())
+    return pfml_ridge_band_launch(SD, ldS, Sr, cells, ncells, lvec, L, work, beta_out, ldo,
+                                  g_ridge_timing, lu_list, lu_count, lu_cap, wgmap, nwg, syncw,
+                                  st);
+  hipLaunchKernelGGL(ridge_tridiag_blocked_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr,
+                     cd, L, work);
   const int64_t nth = (int64_t)ncells * L;
   hipLaunchKernelGGL(ridge_trisolve_kernel, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0,
                      st, cd, ncells, lvec, L, work);

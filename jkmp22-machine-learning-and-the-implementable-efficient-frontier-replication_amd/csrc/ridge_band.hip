@@ -16,9 +16,8 @@
 // per lambda, register window with DPP broadcasts, O(n BB^2)), and beta = Q y is a blocked-WY back-transform
 // (MFMA, Y chunk of 16 lambdas resident in registers).
 //
-//   kernel 1  band_mk_{panel,x,trail}_kernel three launches per panel, many workgroups per
-//                                            cell (ridge_band_reduce_kernel: one 512-thread
-//                                            workgroup per cell, PFML_BAND_MODE=single)
+//   kernel 1  band_coop_kernel               K workgroups per cell (1..16, chosen per launch),
+//                                            bitwise independent of K
 //   kernel 2  ridge_band_solve_kernel        4 lambdas per wave (16-lane DPP rows)
 //   kernel 3  ridge_band_backtransform_kernel one 512-thread workgroup per (cell, 16 lambdas)
 //
@@ -43,13 +42,12 @@ constexpr int NTB = 512;            // back-transform kernel: 8 waves
 constexpr int NWB = NTB / 64;
 constexpr int LC = 16;              // lambdas per back-transform workgroup
 
-// Per-cell workspace layout (doubles).  A has room for the padded npad x npad matrix of the
-// fused path (npad = n rounded up to 16); the single / multi-workgroup paths use its first
-// n x n doubles with leading dimension n.
+// Per-cell workspace layout (doubles).  A has room for the padded npad x npad matrix
+// (npad = n rounded up to 16).
 __host__ __device__ __forceinline__ int band_npad(int n) { return (n + BB - 1) & ~(BB - 1); }
 
 struct BandWork {
-  double *A, *LB, *z, *T, *Yt, *Lf, *Vg, *Ug, *Xg, *Pg, *Pzg, *F;
+  double *A, *LB, *z, *T, *Yt, *Lf, *F;
   __device__ BandWork(double* w, int n, int L) {
     const int np = (n + BB - 1) / BB;
     const int npad = band_npad(n);
@@ -59,25 +57,8 @@ struct BandWork {
     T = z + n;                               // np x 16 x 16 compact-WY T_p
     Yt = T + (int64_t)np * BB * BB;          // L x n   solutions y_l, then beta_l
     Lf = Yt + (int64_t)L * n;                // L x n x LS banded Cholesky factors
-    Vg = Lf + (int64_t)L * n * LS;           // multi-workgroup path: panel V   (BMP x 16)
-    Ug = Vg + BMP * BB;                      //                        U = V T  (BMP x 16)
-    Xg = Ug + BMP * BB;                      //                        X = A U  (BMP x 16)
-    Pg = Xg + BMP * BB;                      //                        V_I^T X_I partials
-    Pzg = Pg + (BMP / 64) * BB * BB;         //                        V_I^T z_I partials
-    F = Pzg + (BMP / 64) * BB;               // fused path: V, W (x2 by panel parity), X
+    F = Lf + (int64_t)L * n * LS;            // cooperative hand-off scratch (CoopWork)
   }
-};
-
-// Fused-path scratch: V and W of a panel (double-buffered by panel parity) and X of the
-// current panel, row-major [npad][16] with ABSOLUTE row indices (rows < r0 unused).
-struct FusedWork {
-  double* f;
-  int64_t s;                                 // npad * 16
-  __device__ FusedWork(double* f_, int npad) : f(f_), s((int64_t)npad * BB) {}
-  // (arithmetic selection: an indexed pointer array would live in scratch)
-  __device__ double* V(int par) const { return f + (par & 1) * s; }
-  __device__ double* W(int par) const { return f + (2 + (par & 1)) * s; }
-  __device__ double* X() const { return f + 4 * s; }
 };
 
 // DPP helpers (gfx950: row_newbcast broadcasts one lane of each 16-lane row).
@@ -163,109 +144,6 @@ __device__ __forceinline__ double rowgroup_sum(double v) {
 // ---------------------------------------------------------------------------------------
 // kernel 1: band reduction of one cell.
 // ---------------------------------------------------------------------------------------
-template <int NQ>
-__device__ __forceinline__ void band_x_accum(const double* __restrict__ A, int n, int r0, int m,
-                                             int wid, int c16, int g4,
-                                             const double (*__restrict__ Ws)[LS],
-                                             double4_t (&X)[4]) {
-  // X_I += A22[I rows][k] U[k][:]  for the NQ row blocks I = wid + 8q of this wave.  A22 is
-  // read through its symmetry (row r0+k, columns of block I: 128 B contiguous per row).
-  int col[NQ];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) col[q] = min((wid + NWR * q) * 16 + c16, m - 1);
-  // whole 32-row chunks: rows past m are clamped (valid memory) and meet U rows that are
-  // zero, so the ragged end costs no extra, serially exposed, load latencies
-  for (int k = 0; k < m; k += 32) {
-    double a[8][NQ], b[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const double* arow = A + (int64_t)(r0 + min(k + 4 * u + g4, m - 1)) * n + r0;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) a[u][q] = arow[col[q]];
-      b[u] = Ws[k + 4 * u + g4][c16];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) X[q] = mfma_f64_16x16x4(a[u][q], b[u], X[q]);
-  }
-}
-
-// ---- CholeskyQR2 panel factorisation with Householder reconstruction --------------------
-//
-// The column-by-column Householder QR below needs one barrier and a dependent rsq/rcp chain
-// per column (16 per panel, ~60 % of a panel's time at the multi-GPU shard sizes).  When the
-// panel is well conditioned it is factored instead as
-//
-//   P = Q1 R1, Q1 = P R1^-1  (G = P^T P on MFMA, 16x16 Cholesky in registers)   twice
-//   [S; 0] - Q = V U~        (LU without pivoting of the 16x16 top block, S_kk = sign of the
-//                             running pivot so |pivot| >= 1; Ballard et al., "Reconstructing
-//                             Householder vectors from TSQR")
-//   V2 = -Q2 U~^-1,  T = U~ S V1^-T,  R_house = S R2 R1
-//
-// which gives the same compact-WY (V unit lower trapezoidal, T upper) and band block as
-// dgeqrt up to the column signs, in five barriers (opt-in, PFML_BAND_QR=cqr: see the
-// launcher for the measured cost).  Every wave repeats the 16x16 work in
-// registers (lane c16 holds column c16, the 4 row groups redundantly; cross-lane values by
-// row_newbcast DPP), so no barrier distributes the small factors, and the accept/reject tests
-// come out identical in every wave.  A panel is rejected (-> the Householder path) when it
-// has fewer rows than columns, a first-pass pivot loses more than 10 digits relative to its
-// column norm, or the second-pass Gram is more than 1e-2 from the identity (the
-// CholeskyQR2 stability bound kappa(P) < ~1e7).
-template <int R>
-__device__ __forceinline__ double pick4(const double (&x)[BB], int g4) {   // x[4R + g4]
-  return g4 == 0 ? x[4 * R] : (g4 == 1 ? x[4 * R + 1] : (g4 == 2 ? x[4 * R + 2] : x[4 * R + 3]));
-}
-
-// G = P^T P of the BMP x 16 panel in Vs: per-wave MFMA partials -> redf, barrier, then every
-// wave sums the partials of column c16 (lanes g4 take waves g4, g4 + 4; row-group sum).
-__device__ __forceinline__ void cqr_gram(const double (*Vs)[LS], double* redf, int m, int wid,
-                                         int lane, double (&g)[BB]) {
-  const int c16 = lane & 15, g4 = lane >> 4;
-  double4_t acc = {0.0, 0.0, 0.0, 0.0};
-  if (wid * 64 < m) {
-#pragma unroll
-    for (int k = 0; k < 64; k += 4) {
-      const double v = Vs[wid * 64 + k + g4][c16];
-      acc = mfma_f64_16x16x4(v, v, acc);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) redf[wid * 256 + PFML_F64_CROW(lane, r) * BB + c16] = acc[r];
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < BB; ++i)
-    g[i] = rowgroup_sum(redf[g4 * 256 + i * BB + c16] + redf[(g4 + 4) * 256 + i * BB + c16]);
-}
-
-// The 16x16 factor routines below accumulate with fmac_bcast<SEL, true> (one volatile
-// v_fmac_f64_dpp behind its own s_nop): as plain expressions the compiler hoists every
-// broadcast of a constant factor entry to the top of the unrolled substitution and spills
-// them, and no ordering of the builtins prevents that.
-
-// Upper Cholesky G = R^T R (lane c16 holds G[:, c16]): rc[i] = R[i][c16], di[i] = 1 / R[i][i].
-// False on a non-positive (or NaN) pivot; a near-dependence that still passes shows up as a
-// second-pass Gram far from the identity.
-__device__ __forceinline__ bool chol16(double (&g)[BB], double (&rc)[BB], double (&di)[BB],
-                                       int c16) {
-  bool ok = true;
-  static_for<0, BB>([&](auto K) {
-    constexpr int k = decltype(K)::value;
-    const double d = row_bcast<k>(g[k]);
-    ok = ok && (d > 0.0);
-    const double rinv = rsqrt_f64(ok ? d : 1.0);
-    const double rk = (c16 >= k) ? g[k] * rinv : 0.0;
-    const double nrk = -rk;
-    rc[k] = rk;
-    di[k] = rinv;
-    static_for<k + 1, BB>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      fmac_bcast<i, true>(g[i], rk, nrk);          // G[i][c16] -= R[k][i] R[k][c16]
-    });
-  });
-  return ok;
-}
-
 // X = U^-1 for upper U given by columns (lane c16: uc[i] = U[i][c16]) and di[i] = 1 / U[i][i];
 // x[i] = X[i][c16].  Only entries above the diagonal of uc are read.
 __device__ __forceinline__ void triu_inv16(const double (&uc)[BB], const double (&di)[BB],
@@ -286,220 +164,14 @@ __device__ __forceinline__ void triu_inv16(const double (&uc)[BB], const double 
   });
 }
 
-// Vs[rows] <- sign * Vs[rows] X for the row blocks [16 b0, m) this wave owns (X by columns,
-// in place: a wave reads a block's 16 rows before it writes them).  When `Aout` is set the
-// result rows also go to the panel columns of A (rows i < m).
-__device__ __forceinline__ void cqr_apply(double (*Vs)[LS], const double (&x)[BB], int m, int wid,
-                                          int lane, int b0, double sign, double* Aout = nullptr,
-                                          int n = 0) {
-  const int c16 = lane & 15, g4 = lane >> 4;
-  double b[4];
-  b[0] = pick4<0>(x, g4);
-  b[1] = pick4<1>(x, g4);
-  b[2] = pick4<2>(x, g4);
-  b[3] = pick4<3>(x, g4);
-#pragma unroll
-  for (int q = 0; q < BMP / 16 / NWR; ++q) {
-    const int blk = wid + NWR * q, i0 = blk * 16;
-    if (blk < b0 || i0 >= m) continue;
-    double4_t acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vs[i0 + c16][4 * r + g4], b[r], acc);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = i0 + PFML_F64_CROW(lane, r);
-      Vs[i][c16] = sign * acc[r];
-      if (Aout != nullptr && i < m) Aout[(int64_t)i * n + c16] = sign * acc[r];
-    }
-  }
-}
-
-__device__ __forceinline__ bool band_panel_cqr(double* __restrict__ A, int n, int k0, int r0,
-                                               int m, double (*Vs)[LS], double* redf,
-                                               double (*Ts)[LS], double* __restrict__ Tglob,
-                                               long long* tk, const double (*Pn)[LS]) {
-  if (m < BB) return false;
-  const int t = threadIdx.x, lane = t & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int c16 = lane & 15, g4 = lane >> 4;
-  // ---- P = rows k0..k0+15, columns r0.. of the symmetric A, transposed into Vs (32 lanes
-  //      per row: 256 B contiguous per load); rows >= m are zero.  With Pn (== Vs: the
-  //      panel already in LDS, rows >= m zero) nothing moves; on a rejection the Householder
-  //      fallback re-reads the panel, so Pn is not overwritten before the accept tests.
-  if (Pn == nullptr) {
-    const int c = t >> 5, il = t & 31;
-    const double* src = A + (int64_t)(k0 + c) * n + r0;
-    double a[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int i = il + 32 * q;
-      a[q] = (i < m) ? src[i] : 0.0;
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) Vs[il + 32 * q][c] = a[q];
-  }
-  __syncthreads();
-  if (tk) tk[0] = (long long)__builtin_amdgcn_s_memtime();
-  // ---- pass 1: G = P^T P, R1, Q1 = P R1^-1
-  double g[BB], rc1[BB], di[BB], x[BB];
-  cqr_gram(Vs, redf, m, wid, lane, g);
-  if (!chol16(g, rc1, di, c16)) {
-    __syncthreads();   // every wave is past its redf reads before the fallback reuses redf
-    return false;
-  }
-  triu_inv16(rc1, di, x, c16);
-  cqr_apply(Vs, x, m, wid, lane, 0, 1.0);
-  __syncthreads();
-  // ---- pass 2: G2 = Q1^T Q1 (~ I), R2, Q = Q1 R2^-1
-  double rc2[BB];
-  cqr_gram(Vs, redf, m, wid, lane, g);
-  bool bad = false;
-#pragma unroll
-  for (int i = 0; i < BB; ++i) bad = bad || !(fabs(g[i] - (i == c16 ? 1.0 : 0.0)) < 1e-2);
-  bad = __any(bad);
-  if (bad || !chol16(g, rc2, di, c16)) {
-    __syncthreads();
-    return false;
-  }
-  triu_inv16(rc2, di, x, c16);
-  cqr_apply(Vs, x, m, wid, lane, 0, 1.0);
-  // R = R2 R1 (lane c16: rf[i] = R[i][c16])
-  double rf[BB];
-#pragma unroll
-  for (int i = 0; i < BB; ++i) rf[i] = 0.0;
-  static_for<0, BB>([&](auto K) {
-    constexpr int k = decltype(K)::value;
-    static_for<0, k + 1>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      fmac_bcast<k, true>(rf[i], rc2[i], rc1[k]);  // += R2[i][k] R1[k][c16]
-    });
-  });
-  if (wid == 0 && g4 == 0) {   // R parked in Ts until the band block is written
-#pragma unroll
-    for (int i = 0; i < BB; ++i) Ts[i][c16] = rf[i];
-  }
-  __syncthreads();
-  // ---- Householder reconstruction: LU of [S; 0] - Q (top block in registers)
-  double mm[BB];
-  unsigned neg = 0;                               // bit k set: S_kk = -1
-#pragma unroll
-  for (int i = 0; i < BB; ++i) mm[i] = -Vs[i][c16];
-  static_for<0, BB>([&](auto K) {
-    constexpr int k = decltype(K)::value;
-    const double d = row_bcast<k>(mm[k]);
-    const double s = (d >= 0.0) ? 1.0 : -1.0;
-    const double piv = d + s;                     // |piv| >= 1
-    const double pinv = rcp_f64(piv);
-    neg |= (d >= 0.0) ? 0u : (1u << k);
-    di[k] = pinv;
-    if (c16 == k) mm[k] = piv;
-    static_for<k + 1, BB>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      if (c16 == k) mm[i] *= pinv;                // L[i][k]
-    });
-    const double nuk = -mm[k];                    // -U~[k][c16]
-    static_for<k + 1, BB>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      double u = mm[i];
-      fmac_bcast<k, true>(u, mm[i], nuk);          // M[i][c16] -= L[i][k] U~[k][c16]
-      if (c16 > k) mm[i] = u;
-    });
-  });
-  // U~^-1 (x), V1^-1 (w: unit lower, forward substitution)
-  triu_inv16(mm, di, x, c16);
-  double w[BB];
-#pragma unroll
-  for (int i = 0; i < BB; ++i) w[i] = 0.0;
-  static_for<0, BB>([&](auto K) {                // right-looking forward substitution
-    constexpr int k = decltype(K)::value;
-    if (c16 == k) w[k] += 1.0;
-    const double nwk = -w[k];
-    static_for<k + 1, BB>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      fmac_bcast<k, true>(w[i], mm[i], nwk);       // W[i][c16] -= L[i][k] W[k][c16]
-    });
-  });
-  // V2 = -Q2 U~^-1 -> Vs rows >= 16 and A's panel columns
-  cqr_apply(Vs, x, m, wid, lane, 1, -1.0, A + (int64_t)r0 * n + k0, n);
-  // T = U~ S V1^-T: W^T through a wave-private LDS image (lane c16 needs row c16 of W)
-  double* wt = redf + wid * 256;
-  if (g4 == 0) {
-#pragma unroll
-    for (int i = 0; i < BB; ++i) wt[i * BB + c16] = w[i];
-  }
-  double wr[BB];                                  // (S W^T)[k][c16] = S_kk W[c16][k]
-#pragma unroll
-  for (int k = 0; k < BB; ++k) {
-    const double v = wt[c16 * BB + k];
-    wr[k] = ((neg >> k) & 1u) ? -v : v;
-  }
-  double tcol[BB];
-#pragma unroll
-  for (int i = 0; i < BB; ++i) tcol[i] = 0.0;
-  static_for<0, BB>([&](auto K) {
-    constexpr int k = decltype(K)::value;
-    static_for<0, k + 1>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      fmac_bcast<k, true>(tcol[i], mm[i], wr[k]);  // += U~[i][k] (S W^T)[k][c16]
-    });
-  });
-  __syncthreads();   // every wave has read the top block of Q
-  if (wid == 0 && g4 == 0) {
-#pragma unroll
-    for (int i = 0; i < BB; ++i) {
-      const double ri = ((neg >> i) & 1u) ? -Ts[i][c16] : Ts[i][c16];   // (S R)[i][c16]
-      Vs[i][c16] = (i > c16) ? mm[i] : (i == c16 ? 1.0 : 0.0);
-      A[(int64_t)(r0 + i) * n + k0 + c16] = (i > c16) ? mm[i] : ri;
-      Ts[i][c16] = tcol[i];
-      Tglob[i * BB + c16] = tcol[i];
-    }
-  }
-  __syncthreads();
-  if (tk) tk[1] = (long long)__builtin_amdgcn_s_memtime();
-  return true;
-}
-
 // P1 + P2 + T of one panel, by one NTR-thread workgroup: the m x 16 panel below the band
 // (columns r0.. of rows k0..k0+15 of the symmetric A) is QR-factored by Householder in
 // registers; V (unit lower trapezoid) -> Vs, V and R -> A's panel columns, the compact-WY T
 // (dlarft) -> Ts and Tglob.  Ends with a barrier.  `redf` needs 2 x 256 + 32 doubles.
-// `n` is A's leading dimension.  `Pn` (fused path): the panel is read from this LDS image
-// (Pn[i][c] = panel row i, column c; it may alias Vs) instead of A's mirror row.
-__device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int k0, int r0,
-                                              int m, double (*Vs)[LS], double (*Gs)[LS],
-                                              double* redf, double (*Ts)[LS], double* taus,
-                                              double* __restrict__ Tglob, long long* tk,
-                                              const double (*Pn)[LS]);
-
-// The Householder form as a call of its own: the CholeskyQR2 path's fallback, so that the two
-// forms do not share one register allocation (inlined together they spilled 344 B per lane)
-__device__ __noinline__ void band_panel_hh_call(double* __restrict__ A, int n, int k0, int r0,
-                                                int m, double (*Vs)[LS], double (*Gs)[LS],
-                                                double* redf, double (*Ts)[LS], double* taus,
-                                                double* __restrict__ Tglob, long long* tk,
-                                                const double (*Pn)[LS]) {
-  band_panel_hh(A, n, k0, r0, m, Vs, Gs, redf, Ts, taus, Tglob, tk, Pn);
-}
-
-__device__ __forceinline__ void band_panel_factor(double* __restrict__ A, int n, int k0, int r0,
-                                                  int m, double (*Vs)[LS], double (*Gs)[LS],
-                                                  double* redf, double (*Ts)[LS], double* taus,
-                                                  double* __restrict__ Tglob, bool qr_fast,
-                                                  long long* tk = nullptr,
-                                                  const double (*Pn)[LS] = nullptr,
-                                                  const double (*Pcopy)[LS] = nullptr) {
-  // qr_fast with the panel in LDS: Pn must be Vs (factored in place) and Pcopy an untouched
-  // copy of it for the Householder fallback (not Gs's rows 0..15, which that fallback writes
-  // only after it has read the panel)
-  if (qr_fast) {
-    if (band_panel_cqr(A, n, k0, r0, m, Vs, redf, Ts, Tglob, tk, Pn)) return;
-    band_panel_hh_call(A, n, k0, r0, m, Vs, Gs, redf, Ts, taus, Tglob, tk,
-                       Pn != nullptr ? Pcopy : nullptr);
-    return;
-  }
-  band_panel_hh(A, n, k0, r0, m, Vs, Gs, redf, Ts, taus, Tglob, tk, Pn);
-}
-
+// `n` is A's leading dimension.  `Pn`: the panel is read from this LDS image (Pn[i][c] = panel
+// row i, column c; it may alias Vs) instead of A's mirror row.
+// (A CholeskyQR2 form with Householder reconstruction measured 45-60 % slower per panel,
+// profiles/r04_qr_bench_dpp.jsonl, and was removed.)
 __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int k0, int r0,
                                               int m, double (*Vs)[LS], double (*Gs)[LS],
                                               double* redf, double (*Ts)[LS], double* taus,
@@ -651,368 +323,6 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
   if (t < BB * BB) Tglob[t] = Ts[t / BB][t % BB];
 }
 
-// DBG (phase-timing experiments only, PFML_BAND_DBG with --timing; results are garbage):
-// 1 no A stores in the trailing update, 2 no trailing MFMAs, 4 no trailing A loads,
-// 8 no LDS transpose (lower stores straight from the accumulators, no mirror)
-// TIMED = false (production): the timing pointer is a compile-time null, so the per-phase /
-// per-column cycle accounting and its stack array compile out (no scratch in the kernel).
-template <bool qr_fast, int DBG = 0, bool TIMED = (DBG != 0)>
-__global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
-    const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
-    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work,
-    long long* __restrict__ tim) {
-  if constexpr (!TIMED) tim = nullptr;
-  // optional per-phase cycle accounting (tools/bench_ridge.py --timing): thread 0 only
-  long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  long long tlast = 0;
-#define BAND_TMARK(ph)                                                   \
-  if (tim != nullptr && threadIdx.x == 0) {                              \
-    const long long now = (long long)__builtin_amdgcn_s_memtime();       \
-    tacc[ph] += now - tlast;                                             \
-    tlast = now;                                                         \
-  }
-  __shared__ double Vs[BMP][LS];       // panel: QR workspace, then V (unit lower trapezoid)
-  __shared__ double Ws[BMP][LS];       // G, then U = V T, then W
-  __shared__ double red[NWR][BB * BB]; // cross-wave partials
-  __shared__ double red2[NWR][BB];
-  __shared__ double Ts[BB][LS];
-  __shared__ double taus[BB];
-  __shared__ double zs[BNMAX];         // z = Q^T rbar, LDS-resident during the reduction
-
-  const RidgeCellDesc cd = cells[blockIdx.x];
-  const int n = cd.n;
-  // leading dimension padded to 16 doubles (128 B): every tile row of the trailing update and
-  // of X = A22 U is one whole cache line (lda = n split most of them over two)
-  const int lda = band_npad(n);
-  const int t_ = threadIdx.x, lane_ = t_ & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(t_ >> 6);
-  BandWork bw(work + cd.work, n, L);
-  double* A = bw.A;
-  const double* S = SD + cd.src;
-  const double sc = cd.scale;
-  for (int i = wid; i < n; i += NWR) {
-    const double* srow = S + (int64_t)i * ldS;
-    double* arow = A + (int64_t)i * lda;
-    for (int j = lane_; j < n; j += 64) arow[j] = srow[j] * sc;
-  }
-  for (int i = t_; i < n; i += NTR) zs[i] = Sr[cd.rsrc + i] * sc;
-  __syncthreads();
-
-  if (tim != nullptr && threadIdx.x == 0) tlast = (long long)__builtin_amdgcn_s_memtime();
-  for (int k0 = 0; k0 + BB < n; k0 += BB) {
-    const int r0 = k0 + BB, m = n - r0, p = k0 / BB;
-    // lane indices laundered per panel (as in band_fused_kernel): otherwise every
-    // lane-dependent offset of the phases is hoisted out of the panel loop and kept live
-    // across the register-hungry QR
-    int t = t_, lane = lane_;
-    asm volatile("" : "+v"(t), "+v"(lane));
-    const int c16 = lane & 15, g4 = lane >> 4;
-    const int cq = t & 15, rg = t >> 4;          // (row group of 32, column) thread map
-    {
-      // (timing: slots 0 / 2 / 7 = the column loop's own work / barrier wait / pivot chain +
-      // update, accumulated over the panels by thread 0)
-      long long tk[6] = {0, 0, 0, 0, 0, 0};
-      band_panel_factor(A, lda, k0, r0, m, Vs, Ws, &red[0][0], Ts, taus,
-                        bw.T + (int64_t)p * BB * BB, qr_fast,
-                        (tim != nullptr && threadIdx.x == 0) ? tk : nullptr);
-      if (tim != nullptr && threadIdx.x == 0) {
-        tacc[0] += tk[2];
-        tacc[2] += tk[3];
-        tacc[7] += tk[4];
-      }
-    }
-    BAND_TMARK(1)
-    // ---- U = V T -> Ws  (MFMA, all 32 row blocks so rows >= m read back as zero)
-#pragma unroll
-    for (int q = 0; q < BMP / 16 / NWR; ++q) {
-      const int i0 = (wid + NWR * q) * 16;
-      double4_t acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vs[i0 + c16][4 * r + g4], Ts[4 * r + g4][c16], acc);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Ws[i0 + g4 + 4 * r][c16] = acc[r];
-    }
-    __syncthreads();
-    BAND_TMARK(3)
-    // ---- P3: X = A22 U  (row blocks I = wid + 8q)
-    const int nI = (m + 15) >> 4;
-    const int nq = (nI > wid) ? (nI - wid + NWR - 1) / NWR : 0;
-    double4_t X[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) X[q] = double4_t{0.0, 0.0, 0.0, 0.0};
-    switch (nq) {
-      case 1: band_x_accum<1>(A, lda, r0, m, wid, c16, g4, Ws, X); break;
-      case 2: band_x_accum<2>(A, lda, r0, m, wid, c16, g4, Ws, X); break;
-      case 3: band_x_accum<3>(A, lda, r0, m, wid, c16, g4, Ws, X); break;
-      case 4: band_x_accum<4>(A, lda, r0, m, wid, c16, g4, Ws, X); break;
-      default: break;
-    }
-    BAND_TMARK(4)
-    // ---- P4: partial V^T X (MFMA: X's accumulator layout IS the B-operand layout), and
-    //          partial V^T z
-    {
-      double4_t Pp = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (q < nq) {
-          const int i0 = (wid + NWR * q) * 16;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) Pp = mfma_f64_16x16x4(Vs[i0 + 4 * r + g4][c16], X[q][r], Pp);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[wid][(g4 + 4 * r) * BB + c16] = Pp[r];
-      double s = 0.0;
-#pragma unroll
-      for (int q = 0; q < BMP / 32; ++q) {    // all loads in flight (V rows >= m are zero)
-        const int i = rg + 32 * q;
-        s += Vs[i][cq] * zs[r0 + min(i, m - 1)];
-      }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      if (lane < 16) red2[wid][lane] = s;
-    }
-    __syncthreads();
-    // z <- Q_p^T z = z - V (T^T (V^T z)).  Lane c16 forms zv[c16] and zt[c16] only (8 + 16
-    // LDS reads instead of every thread reading all 8 x 16 partials and the 136 T entries);
-    // the other entries reach it by row_newbcast DPP.  Same operations in the same order as
-    // band_fused_kernel, so the bits are unchanged.
-    {
-      double zvl = 0.0;
-#pragma unroll
-      for (int w = 0; w < NWR; ++w) zvl += red2[w][c16];
-      double ztl = 0.0;
-      static_for<0, BB>([&](auto A_) {
-        constexpr int a = decltype(A_)::value;
-        const double za = row_bcast<a>(zvl);
-        const double ns = fma(Ts[a][c16], za, ztl);
-        ztl = (a <= c16) ? ns : ztl;
-      });
-      double zt[BB];                     // broadcast before the row loop (all lanes active)
-      static_for<0, BB>([&](auto C_) {
-        constexpr int c = decltype(C_)::value;
-        zt[c] = row_bcast<c>(ztl);
-      });
-      for (int i = t; i < m; i += NTR) {
-        double s = 0.0;
-#pragma unroll
-        for (int c = 0; c < BB; ++c) s = fma(Vs[i][c], zt[c], s);
-        zs[r0 + i] -= s;
-      }
-    }
-    // M = T^T (V^T X) ; W_I = X_I - 1/2 V_I M  -> Ws
-    {
-      double4_t Mm = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        double pv = 0.0;
-#pragma unroll
-        for (int w = 0; w < NWR; ++w) pv += red[w][(4 * r + g4) * BB + c16];
-        Mm = mfma_f64_16x16x4(Ts[4 * r + g4][c16], pv, Mm);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (q < nq) {
-          const int i0 = (wid + NWR * q) * 16;
-          double4_t acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vs[i0 + c16][4 * r + g4], Mm[r], acc);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int i = i0 + g4 + 4 * r;
-            Ws[i][c16] = (i < m) ? X[q][r] - 0.5 * acc[r] : 0.0;
-          }
-        }
-      }
-    }
-    __syncthreads();
-    BAND_TMARK(5)
-    // ---- P6: A22 -= V W^T + W V^T on the LOWER block triangle (K = 32 MFMA per 16x16 tile);
-    //      each off-diagonal tile is also stored transposed, so A stays bitwise symmetric at
-    //      half the MFMA work.  Wave w owns whole block rows I (snake order over groups of
-    //      2 NWR rows: w, 2 NWR - 1 - w, ... - equal tile counts per wave) and walks each row
-    //      TBR tiles at a time: the TBR tiles' operands are read before the chunk's 8 TBR
-    //      MFMAs, which run as TBR independent accumulator chains, and the next chunk's A tiles
-    //      are loaded before this chunk's MFMAs.  No branch surrounds a memory instruction
-    //      (masked loads read a clamped in-range element, masked stores go to a
-    //      per-lane dummy slot in the unused fused-path scratch), so the waitcnt pass knows the
-    //      chunk's store count and waits only for the prefetched loads, never for the stores'
-    //      write-back.
-    //      The per-tile arithmetic (operands and MFMA order) is unchanged, so A is bitwise the
-    //      same.  Chunks touch disjoint lower tiles; mirrored stores land in the upper
-    //      triangle, which no chunk reads.
-    {
-      double* __restrict__ dummy = bw.F + lane;   // sink of masked stores
-      double2* __restrict__ dummy2 = reinterpret_cast<double2*>(bw.F) + lane;
-      auto row_of = [&](int rr) {                 // rr-th block row of this wave (may be >= nI)
-        return 2 * NWR * (rr >> 1) + ((rr & 1) ? (2 * NWR - 1 - wid) : wid);
-      };
-      auto sptr = [&](int i, int j, bool ok) {    // &A22[i][j], or the sink if !ok
-        return ok ? A + (int64_t)(r0 + i) * lda + r0 + j : dummy;
-      };
-      double4_t nxt[TBR];
-      auto fetch = [&](int I, int J0) {
-#pragma unroll
-        for (int u = 0; u < TBR; ++u) {
-          const int J = J0 + u;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int i = 16 * I + g4 + 4 * r, jj = 16 * J + c16;
-            // (masked elements: any finite value; they only meet their own accumulator entry,
-            // which is never stored)
-            nxt[u][r] = (DBG & 4) ? (double)(i + jj)
-                                  : A[(int64_t)(r0 + min(i, m - 1)) * lda + r0 + min(jj, m - 1)];
-          }
-        }
-      };
-      int rr = 0, I = row_of(0), J0 = 0;
-      while (rr < 4 && I >= nI) I = row_of(++rr);
-      if (rr >= 4) I = nI;
-      // advance (I, J0): next chunk of the row, else the next of the wave's rows below nI (the
-      // candidates are not monotone in rr, so every one is tested); I = nI ends the walk
-      auto advance = [&]() {
-        J0 += TBR;
-        if (J0 > I) {
-          J0 = 0;
-          do I = row_of(++rr);
-          while (rr < 4 && I >= nI);
-          if (rr >= 4) I = nI;
-        }
-      };
-      fetch(I, 0);
-      double* tw = &red[0][0] + wid * (BB * BB);  // wave-private transpose image
-      // the chunk's tiles move nxt -> acc at the END of the previous chunk (after its stores):
-      // at the loop head no load is pending, so the waitcnt pass never merges the first
-      // entry's load-only queue with the loop's load + store queue (which forced a full
-      // vmcnt(0) drain of the stores)
-      double4_t acc[TBR];
-#pragma unroll
-      for (int u = 0; u < TBR; ++u) acc[u] = nxt[u];
-      // (a use here makes the first chunk's loads complete before the loop: otherwise they
-      // are still pending at the loop head, and the wait merged from that entry edge drains
-      // the previous chunk's stores on every iteration)
-#pragma unroll
-      for (int u = 0; u < TBR; ++u) asm volatile("" ::"v"(acc[u]));
-      int ci = I, cj = J0;
-      advance();
-      while (ci < nI) {
-        // this chunk: tiles (ci, cj .. cj + TBR - 1), J <= ci
-        fetch(I, J0);                             // (I = nI: every lane masked)
-        double aV[4], aW[4], bW[TBR][4], bV[TBR][4];
-        const int ia = 16 * ci + c16;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          aV[s] = -Vs[ia][4 * s + g4];
-          aW[s] = -Ws[ia][4 * s + g4];
-        }
-#pragma unroll
-        for (int u = 0; u < TBR; ++u) {
-          const int jb = 16 * min(cj + u, ci) + c16;
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            bW[u][s] = Ws[jb][4 * s + g4];
-            bV[u][s] = Vs[jb][4 * s + g4];
-          }
-        }
-        if constexpr (!(DBG & 2)) {
-#pragma unroll
-          for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int u = 0; u < TBR; ++u) acc[u] = mfma_f64_16x16x4(aV[s], bW[u][s], acc[u]);
-#pragma unroll
-          for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int u = 0; u < TBR; ++u) acc[u] = mfma_f64_16x16x4(aW[s], bV[u][s], acc[u]);
-        } else {
-#pragma unroll
-          for (int u = 0; u < TBR; ++u) acc[u][0] += aV[u] * bW[u][0] + aW[u] * bV[u][3];
-        }
-#pragma unroll
-        for (int u = 0; u < TBR; ++u) {
-          const int J = cj + u;
-          const bool live = J <= ci;
-          if constexpr ((DBG & 1) != 0) {
-            continue;
-          } else if constexpr ((DBG & 8) != 0) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int i = 16 * ci + g4 + 4 * r, jj = 16 * J + c16;
-              *sptr(i, jj, live && i < m && jj < m) = acc[u][r];
-            }
-            continue;
-          }
-          // the tile goes through the wave-private 16 x 16 LDS image (XOR-swizzled on even
-          // column offsets, so column pairs stay adjacent; `red` is free in this phase) and
-          // leaves as 16-byte stores: lane l writes columns 2 (l & 7), +1 of row l >> 3 (+8),
-          // two dwordx4 stores per 16 x 16 tile and two for its mirror (upper) tile, where
-          // lane-per-element stores took eight dwordx2.  The data comes from LDS reads, not
-          // from the accumulators: a store whose data registers the next chunk's MFMAs
-          // overwrite would make the waitcnt pass drain it first.  Elements past m (rows or
-          // columns >= n) are written like the rest: the padding of the npad x npad matrix is
-          // never read (every load is clamped below m).
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int row = g4 + 4 * r;
-            tw[row * BB + (c16 ^ (row & ~1))] = acc[u][r];
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          {
-            const int pr = lane >> 3, pc = 2 * (lane & 7);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const int row = pr + 8 * h;
-              const double2 v = *reinterpret_cast<const double2*>(&tw[row * BB + (pc ^ (row & ~1))]);
-              double2* dst = live ? reinterpret_cast<double2*>(
-                                        A + (int64_t)(r0 + 16 * ci + row) * lda + r0 + 16 * J + pc)
-                                  : dummy2;
-              *dst = v;
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const int col = pr + 8 * h;                    // mirror row = tile column
-              double2 v;
-              v.x = tw[pc * BB + (col ^ (pc & ~1))];
-              v.y = tw[(pc + 1) * BB + (col ^ ((pc + 1) & ~1))];
-              double2* dst = (live && J != ci)
-                                 ? reinterpret_cast<double2*>(
-                                       A + (int64_t)(r0 + 16 * J + col) * lda + r0 + 16 * ci + pc)
-                                 : dummy2;
-              *dst = v;
-            }
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        // accumulators kept live to here: the stores' address / data temporaries must not
-        // reuse their registers (the next chunk's MFMAs write them, and the waitcnt pass
-        // would drain the stores before those MFMAs)
-#pragma unroll
-        for (int u = 0; u < TBR; ++u) asm volatile("" ::"v"(acc[u]));
-#pragma unroll
-        for (int u = 0; u < TBR; ++u) acc[u] = nxt[u];
-        ci = I;
-        cj = J0;
-        advance();
-      }
-    }
-    __syncthreads();
-    BAND_TMARK(6)
-  }
-  BAND_TMARK(7)
-  if (tim != nullptr && threadIdx.x == 0)
-    for (int q = 0; q < 8; ++q) tim[(int64_t)blockIdx.x * 8 + q] = tacc[q];
-#undef BAND_TMARK
-  for (int i = t_; i < n; i += NTR) bw.z[i] = zs[i];
-  // ---- row-major lower band: LB[r][s] = B[r][r-16+s]  (s = 16: diagonal)
-  for (int e = t_; e < n * LS; e += NTR) {
-    const int r = e / LS, c = r - BB + e % LS;
-    bw.LB[e] = (c >= 0) ? A[(int64_t)r * lda + c] : 0.0;
-  }
-}
-
 // ---------------------------------------------------------------------------------------
 // kernel 1, cooperative form (band_mode 4, the production form): K workgroups per cell in
 // ONE launch, K chosen per cell by the host (ops/ridge.py::coop_plan) so that a launch fills
@@ -1023,14 +333,14 @@ __global__ __launch_bounds__(NTR) void ridge_band_reduce_kernel(
 // (PFML_hp_reals.py:118-122 dense rank, PFML_best_hps.py:275 first rank).
 //
 // Work units are 16-row blocks of the trailing matrix A22 (lower-triangle semantics; every
-// off-diagonal tile is mirrored, as in ridge_band_reduce_kernel).  Per panel p:
+// off-diagonal tile is mirrored).  Per panel p:
 //
 //   B  every WG   U = V_p T_p (LDS), X_I = A22 U for the blocks I = gb (mod K) it owns in the
 //                 X phase (gb = global block), partials V_I' X_I and V_I' z_I per block
 //   C  every WG   P = sum_I V_I' X_I and V'z in block order, M = T' P, z_I -= V_I T' V'z,
 //                 W_I = X_I - V_I M / 2 for its X blocks
 //   D  QR WG      look-ahead: the tiles (I, 0) of A22 ARE panel p+1; it applies update p to
-//                 them in registers and factors panel p+1 (band_panel_factor) while
+//                 them in registers and factors panel p+1 (band_panel_hh) while
 //      others     apply A22 -= V W' + W V' to their update blocks, tiles (I, J), 1 <= J <= I
 //                 (tile (0, 0): the diagonal band block)
 //
@@ -1219,7 +529,7 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
       Vs[i][c] = (i < m0) ? A[(int64_t)(BB + i) * lda + c] : 0.0;
     }
     __syncthreads();
-    band_panel_factor(A, lda, 0, BB, m0, Vs, Ws, &red[0][0], Ts, taus, bw.T, false, nullptr, Vs);
+    band_panel_hh(A, lda, 0, BB, m0, Vs, Ws, &red[0][0], Ts, taus, bw.T, nullptr, Vs);
     if (K > 1) publish_vt(m0);
   }
   if (npan > 0) cs.sync(false, &err_s);
@@ -1526,8 +836,8 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
       }
       for (int e = t + 16 * (nI - 1) * BB; e < BMP * BB; e += NTR) Vs[e / BB][e % BB] = 0.0;
       __syncthreads();
-      band_panel_factor(A, lda, k0 + BB, r0 + BB, m1, Vs, Ws, &red[0][0], Ts, taus,
-                        bw.T + (int64_t)(p + 1) * BB * BB, false, nullptr, Vs);
+      band_panel_hh(A, lda, k0 + BB, r0 + BB, m1, Vs, Ws, &red[0][0], Ts, taus,
+                    bw.T + (int64_t)(p + 1) * BB * BB, nullptr, Vs);
       if (K > 1) publish_vt(m1);
     };
     if (K == 1) {
@@ -1559,661 +869,6 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
       const int r = e / LS, c = r - BB + e % LS;
       bw.LB[e] = (c >= 0) ? A[(int64_t)r * lda + c] : 0.0;
     }
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// kernel 1, fused form (band_mode 3): one workgroup per cell, ONE pass over the trailing
-// matrix per panel instead of two, bitwise equal to ridge_band_reduce_kernel.
-//
-// The one-workgroup kernel above reads the trailing matrix A22 once for X = A22 U and
-// reads + writes its lower triangle (mirrored stores) for the rank-32 update, with ~20 CU
-// barriers and three serial phases per panel.  Here the update of panel p-1 and X of panel p
-// share one pass:
-//
-//   A  strip   column block p (rows >= 16 p) gets update p-1 in registers: its diagonal tile
-//              is final (band), the rest is the panel of p, handed to the QR through LDS
-//   B  QR      Householder panel factorisation (band_panel_factor, panel from LDS)
-//   C  U       U = V_p T_p (LDS)
-//   D  pass    every trailing tile (I, J): A_IJ -= V_I W_J' + W_I V_J' (panel p-1), then
-//              X_J += A_IJ' U_I (the tile's MFMA C layout IS the A-operand layout of A_IJ', so
-//              no transpose), stored back.  Wave w owns the columns J = w (mod 8) and forms
-//              X_J completely in registers - no cross-wave reduction.
-//   E  W       V_p' X, z <- Q_p' z, M = T' V' X, W = X - V M / 2: the same arithmetic, lane
-//              map and summation order as the one-workgroup kernel (X staged through a
-//              per-cell scratch), V_p and W_p to the scratch for the next pass.
-//
-// The matrix is stored FULL (both triangles) in a zero-padded npad x npad array, so every
-// tile is a whole 16 x 16 MFMA tile and X_J needs no upper-triangle mirror reads.  An upper
-// tile (I < J) applies the two rank-16 halves in the opposite order (W_I V_J' first), which
-// makes it bitwise the transpose of tile (J, I) - exactly the value the one-workgroup kernel
-// mirrors into the upper triangle - and X accumulates over the same rows in the same order,
-// so the band, V, T and z are bitwise those of ridge_band_reduce_kernel.
-// ---------------------------------------------------------------------------------------
-constexpr int FJ = 2;                   // columns per wave per pass group (registers)
-
-template <bool TIMED>
-__global__ __launch_bounds__(NTR) void band_fused_kernel(
-    const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
-    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work,
-    long long* __restrict__ tim) {
-  // optional per-phase cycle accounting (TIMED: thread 0; tools/bench_ridge.py --timing)
-  long long tacc[TIMED ? 8 : 1] = {0};
-  long long tlast = 0;
-#define FUSED_TMARK(ph)                                                  \
-  if (TIMED && threadIdx.x == 0) {                                       \
-    const long long now = (long long)__builtin_amdgcn_s_memtime();       \
-    tacc[ph] += now - tlast;                                             \
-    tlast = now;                                                         \
-  }
-  __shared__ double Vs[BMP][LS];       // panel of p (QR input), then V_p
-  __shared__ double Us[BMP][LS];       // QR's G scratch, then U_p = V_p T_p
-  __shared__ double red[NWR][BB * BB];
-  __shared__ double red2[NWR][BB];
-  __shared__ double Ts[BB][LS];
-  __shared__ double taus[BB];
-  __shared__ double zs[BNMAX];
-
-  const RidgeCellDesc cd = cells[blockIdx.x];
-  const int n = cd.n;
-  const int nb = (n + BB - 1) / BB, npad = nb * BB, lda = npad;
-  const int npan = (n - 1) / BB;               // panels: k0 = 16 p with k0 + 16 < n
-  const int t_ = threadIdx.x, lane_ = t_ & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(t_ >> 6);
-  const int c16_ = lane_ & 15, g4_ = lane_ >> 4;
-  const int cq_ = t_ & 15, rg_ = t_ >> 4;
-  BandWork bw(work + cd.work, n, L);
-  FusedWork fw(bw.F, npad);
-  double* __restrict__ A = bw.A;
-  {
-    const double* S = SD + cd.src;
-    const double sc = cd.scale;
-    for (int i = wid; i < npad; i += NWR) {
-      const double* srow = S + (int64_t)i * ldS;
-      double* arow = A + (int64_t)i * lda;
-      for (int j = lane_; j < npad; j += 64) arow[j] = (i < n && j < n) ? srow[j] * sc : 0.0;
-    }
-    for (int i = t_; i < npad; i += NTR) zs[i] = (i < n) ? Sr[cd.rsrc + i] * sc : 0.0;
-  }
-  __syncthreads();
-  if (TIMED && threadIdx.x == 0) tlast = (long long)__builtin_amdgcn_s_memtime();
-
-  for (int p = 0; p < npan; ++p) {
-    const int k0 = p * BB, r0 = k0 + BB, m = n - r0;
-    const int mb = nb - p - 1;                  // trailing row / column blocks
-    // lane indices laundered per panel: otherwise the compiler hoists every lane-dependent LDS
-    // and global offset of the five phases out of the panel loop and keeps them live across
-    // the register-hungry QR (~70 VGPRs spilled)
-    int c16 = c16_, g4 = g4_, cq = cq_, rg = rg_, t = t_, lane = lane_;
-    asm volatile("" : "+v"(c16), "+v"(g4), "+v"(cq), "+v"(rg), "+v"(t), "+v"(lane));
-    // tile (I, J) element (16 I + g4 + 4 r, 16 J + c16): this lane's offset for r = 0
-    auto toff = [&](int I, int J) -> int64_t {
-      return (int64_t)(16 * I + g4) * lda + 16 * J + c16;
-    };
-    // A-operand chunks s of rows 16 B .. of a [npad][16] scratch: X[16 B + c16][4 s + g4]
-    auto aops = [&](const double* __restrict__ X, int B, double (&o)[4]) {
-  #pragma unroll
-      for (int s = 0; s < 4; ++s) o[s] = X[(16 * B + c16) * BB + 4 * s + g4];
-    };
-    const double* __restrict__ Vq = fw.V(p + 1);   // V, W of panel p - 1
-    const double* __restrict__ Wq = fw.W(p + 1);
-    // ---- A: strip = column block p, row blocks p .. nb-1
-    {
-      double cV[4], cW[4];
-      if (p > 0) {
-        aops(Vq, p, cV);
-        aops(Wq, p, cW);
-      }
-      constexpr int FS = (BNMAX / BB + NWR - 1) / NWR;   // strip tiles per wave (<= 5)
-      double4_t cs[FS];
-#pragma unroll
-      for (int u = 0; u < FS; ++u) {                       // every load in flight at once
-        const int it = wid + NWR * u;
-        if (it < nb - p) {
-          const int64_t o = toff(p + it, p);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) cs[u][r] = A[o + (int64_t)4 * r * lda];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < FS; ++u) {
-        const int it = wid + NWR * u;
-        if (it >= nb - p) continue;
-        const int I = p + it;
-        double4_t c = cs[u];
-        const int64_t o = toff(I, p);
-        if (p > 0) {
-          double rV[4], rW[4];
-          aops(Vq, I, rV);
-          aops(Wq, I, rW);
-#pragma unroll
-          for (int s = 0; s < 4; ++s) c = mfma_f64_16x16x4(-rV[s], cW[s], c);
-#pragma unroll
-          for (int s = 0; s < 4; ++s) c = mfma_f64_16x16x4(-rW[s], cV[s], c);
-        }
-        if (it == 0) {
-          if (p > 0) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) A[o + (int64_t)4 * r * lda] = c[r];
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) Vs[16 * (it - 1) + g4 + 4 * r][c16] = c[r];
-        }
-      }
-    }
-    __syncthreads();
-    FUSED_TMARK(1)
-    // ---- B: QR of the panel (rows r0 .., from Vs) -> V_p (Vs), T_p, R / V into A
-    {
-      long long tk[6] = {0, 0, 0, 0, 0, 0};
-      band_panel_factor(A, lda, k0, r0, m, Vs, Us, &red[0][0], Ts, taus,
-                        bw.T + (int64_t)p * BB * BB, false,
-                        (TIMED && threadIdx.x == 0) ? tk : nullptr, Vs);
-      if (TIMED && threadIdx.x == 0) {    // slot 0: column loop + V stores, 7: G and T
-        const long long now = (long long)__builtin_amdgcn_s_memtime();
-        tacc[0] += tk[1] - tk[0];
-        tacc[7] += now - tk[1];
-      }
-    }
-    FUSED_TMARK(2)
-    asm volatile("" : "+v"(c16), "+v"(g4), "+v"(cq), "+v"(rg), "+v"(t), "+v"(lane));
-    // ---- C: U = V T -> Us (all 32 row blocks: rows >= m read back as zero)
-#pragma unroll
-    for (int q = 0; q < BMP / 16 / NWR; ++q) {
-      const int i0 = (wid + NWR * q) * 16;
-      double4_t acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vs[i0 + c16][4 * r + g4], Ts[4 * r + g4][c16], acc);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Us[i0 + g4 + 4 * r][c16] = acc[r];
-    }
-    __syncthreads();
-    FUSED_TMARK(3)
-    // ---- D: fused pass over the trailing tiles; wave wid owns columns J = wid (mod 8), taken
-    //      FJ at a time (the row operands are re-read per group: L1 hits)
-    {
-      const int J0 = p + 1 + ((wid - (p + 1)) % NWR + NWR) % NWR;
-      int nj = 0;
-      for (int J = J0; J < nb; J += NWR) ++nj;
-      for (int jg = 0; jg < nj; jg += FJ) {
-        double cV[FJ][4], cW[FJ][4];
-        double4_t X[FJ];
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) {
-          X[j] = double4_t{0.0, 0.0, 0.0, 0.0};
-          if (p > 0 && jg + j < nj) {
-            aops(Vq, J0 + NWR * (jg + j), cV[j]);
-            aops(Wq, J0 + NWR * (jg + j), cW[j]);
-          }
-        }
-        // software pipeline: the tiles and row operands of row block I + 1 are loaded
-        // before the MFMAs of row block I (one memory latency per pass, not one per tile)
-        double4_t cn[FJ];
-        double rVn[4], rWn[4];
-        auto fetch = [&](int I) {
-          if (p > 0) {
-            aops(Vq, I, rVn);
-            aops(Wq, I, rWn);
-          }
-#pragma unroll
-          for (int j = 0; j < FJ; ++j) {
-            if (jg + j < nj) {
-              const double* __restrict__ tp = A + toff(I, J0 + NWR * (jg + j));
-#pragma unroll
-              for (int r = 0; r < 4; ++r) cn[j][r] = tp[4 * r * lda];
-            }
-          }
-        };
-        fetch(p + 1);
-        for (int I = p + 1; I < nb; ++I) {
-          double rV[4], rW[4], ub[4];
-          double4_t c[FJ];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            rV[q] = rVn[q];
-            rW[q] = rWn[q];
-          }
-#pragma unroll
-          for (int j = 0; j < FJ; ++j) c[j] = cn[j];
-          if (I + 1 < nb) fetch(I + 1);
-          const int il = 16 * (I - p - 1);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) ub[r] = Us[il + 4 * r + g4][c16];
-#pragma unroll
-          for (int j = 0; j < FJ; ++j) {
-            if (jg + j < nj) {
-              const int J = J0 + NWR * (jg + j);
-              if (p > 0) {
-                if (I < J) {            // upper tile: the mirror's order (bitwise transpose)
-#pragma unroll
-                  for (int s = 0; s < 4; ++s) c[j] = mfma_f64_16x16x4(-rW[s], cV[j][s], c[j]);
-#pragma unroll
-                  for (int s = 0; s < 4; ++s) c[j] = mfma_f64_16x16x4(-rV[s], cW[j][s], c[j]);
-                } else {
-#pragma unroll
-                  for (int s = 0; s < 4; ++s) c[j] = mfma_f64_16x16x4(-rV[s], cW[j][s], c[j]);
-#pragma unroll
-                  for (int s = 0; s < 4; ++s) c[j] = mfma_f64_16x16x4(-rW[s], cV[j][s], c[j]);
-                }
-                double* __restrict__ tp = A + toff(I, J);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) tp[4 * r * lda] = c[j][r];
-              }
-#pragma unroll
-              for (int r = 0; r < 4; ++r) X[j] = mfma_f64_16x16x4(c[j][r], ub[r], X[j]);
-            }
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < FJ; ++j) {
-          if (jg + j < nj) {
-            const int J = J0 + NWR * (jg + j);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) fw.X()[(16 * J + g4 + 4 * r) * BB + c16] = X[j][r];
-          }
-        }
-      }
-    }
-    __syncthreads();
-    FUSED_TMARK(4)
-    // ---- E: P = V' X (per-wave partials over blocks wid + 8 q), V' z, exactly as the
-    //      one-workgroup kernel
-    const int nI = mb;
-    const int nq = (nI > wid) ? (nI - wid + NWR - 1) / NWR : 0;
-    double4_t Xc[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      Xc[q] = double4_t{0.0, 0.0, 0.0, 0.0};
-      if (q < nq) {
-        const int i0 = (wid + NWR * q) * 16;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Xc[q][r] = fw.X()[(r0 + i0 + g4 + 4 * r) * BB + c16];
-      }
-    }
-    {
-      double4_t Pp = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (q < nq) {
-          const int i0 = (wid + NWR * q) * 16;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) Pp = mfma_f64_16x16x4(Vs[i0 + 4 * r + g4][c16], Xc[q][r], Pp);
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[wid][(g4 + 4 * r) * BB + c16] = Pp[r];
-      double s = 0.0;
-#pragma unroll
-      for (int q = 0; q < BMP / 32; ++q) {
-        const int i = rg + 32 * q;
-        s += Vs[i][cq] * zs[r0 + min(i, m - 1)];
-      }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      if (lane < 16) red2[wid][lane] = s;
-    }
-    __syncthreads();
-    {
-      double zv[BB];
-#pragma unroll
-      for (int a = 0; a < BB; ++a) {
-        double s = 0.0;
-#pragma unroll
-        for (int w = 0; w < NWR; ++w) s += red2[w][a];
-        zv[a] = s;
-      }
-      double zt[BB];
-#pragma unroll
-      for (int c = 0; c < BB; ++c) {
-        double s = 0.0;
-#pragma unroll
-        for (int a = 0; a <= c; ++a) s += Ts[a][c] * zv[a];
-        zt[c] = s;
-      }
-      for (int i = t; i < m; i += NTR) {
-        double s = 0.0;
-#pragma unroll
-        for (int c = 0; c < BB; ++c) s += Vs[i][c] * zt[c];
-        zs[r0 + i] -= s;
-      }
-    }
-    {
-      double4_t Mm = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        double pv = 0.0;
-#pragma unroll
-        for (int w = 0; w < NWR; ++w) pv += red[w][(4 * r + g4) * BB + c16];
-        Mm = mfma_f64_16x16x4(Ts[4 * r + g4][c16], pv, Mm);
-      }
-      double* __restrict__ Wn = fw.W(p);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (q < nq) {
-          const int i0 = (wid + NWR * q) * 16;
-          double4_t acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vs[i0 + c16][4 * r + g4], Mm[r], acc);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int i = i0 + g4 + 4 * r;
-            Wn[(r0 + i) * BB + c16] = (i < m) ? Xc[q][r] - 0.5 * acc[r] : 0.0;
-          }
-        }
-      }
-      double* __restrict__ Vn = fw.V(p);
-      for (int e = t; e < mb * BB * BB; e += NTR) Vn[(int64_t)r0 * BB + e] = Vs[e / BB][e % BB];
-    }
-    __syncthreads();
-    FUSED_TMARK(5)
-  }
-  const int t = t_, c16 = c16_, g4 = g4_;
-  auto toff = [&](int I, int J) -> int64_t {
-    return (int64_t)(16 * I + g4) * lda + 16 * J + c16;
-  };
-  auto aops = [&](const double* __restrict__ X, int B, double (&o)[4]) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) o[s] = X[(16 * B + c16) * BB + 4 * s + g4];
-  };
-  // the last diagonal tile (block nb - 1) gets the last panel's update
-  if (npan > 0 && wid == 0) {
-    const int p = npan, I = nb - 1;
-    const double* __restrict__ Vq = fw.V(p + 1);
-    const double* __restrict__ Wq = fw.W(p + 1);
-    double rV[4], rW[4];
-    aops(Vq, I, rV);
-    aops(Wq, I, rW);
-    double4_t c;
-    const int64_t o = toff(I, I);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) c[r] = A[o + (int64_t)4 * r * lda];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) c = mfma_f64_16x16x4(-rV[s], rW[s], c);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) c = mfma_f64_16x16x4(-rW[s], rV[s], c);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) A[o + (int64_t)4 * r * lda] = c[r];
-  }
-  __syncthreads();
-  FUSED_TMARK(6)
-  if (TIMED && threadIdx.x == 0)
-    for (int q = 0; q < 8; ++q) tim[(int64_t)blockIdx.x * 8 + q] = tacc[q];
-#undef FUSED_TMARK
-  for (int i = t; i < n; i += NTR) bw.z[i] = zs[i];
-  for (int e = t; e < n * LS; e += NTR) {
-    const int r = e / LS, c = r - BB + e % LS;
-    bw.LB[e] = (c >= 0) ? A[(int64_t)r * lda + c] : 0.0;
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// kernel 1, multi-workgroup form (default): the same band reduction with the two O(m^2)
-// phases of every panel spread over many workgroups per cell, so the reduction of ONE cell
-// is no longer bound by one CU (the single-workgroup kernel takes ~4.4 ms for one n = 513
-// cell however many CUs are idle; with few cells per GPU - the multi-GPU case - that is the
-// whole step).  Per panel p the host issues three launches over all cells:
-//
-//   (mk_init  copies the scaled window sums once)
-//   mk_panel  1 WG / cell      P1 + P2 + T (band_panel_factor), U = V T;
-//                              V and U to the cell's global panel buffers
-//   mk_x      m/64 WGs / cell  X = A22 U (16 rows per wave), partials V_I^T X_I, V_I^T z_I
-//   mk_trail  one WG per 32x32 lower tile of A22:  M = T^T sum(V_I^T X_I),
-//                              W = X - 1/2 V M for the tile's rows and columns, then
-//                              A22 -= V W^T + W V^T (MFMA), off-diagonal tiles mirrored so A
-//                              stays bitwise symmetric
-//
-// and one mk_extract launch copies the lower band out at the end.  rbar rides along as
-// z <- Q_p^T z: V_I^T z_I partials in mk_x, the update of block I's rows in tile (I, 0).  Kernel boundaries are the
-// only inter-workgroup synchronisation.
-// ---------------------------------------------------------------------------------------
-constexpr int MK_XR = 64;              // mk_x rows per workgroup (4 waves x 16)
-constexpr int MK_TS = 32;              // mk_trail tile edge (4 waves x 16 x 16)
-
-constexpr int MK_INIT_WG = 16;         // mk_init workgroups per cell
-
-// A = S * scale, z = r * scale (the working copies of the cell's window sums)
-__global__ __launch_bounds__(256) void band_mk_init_kernel(
-    const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
-    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work) {
-  const int cell = blockIdx.x / MK_INIT_WG, part = blockIdx.x % MK_INIT_WG;
-  const RidgeCellDesc cd = cells[cell];
-  const int n = cd.n;
-  BandWork bw(work + cd.work, n, L);
-  const double* S = SD + cd.src;
-  const double sc = cd.scale;
-  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int i = part * 4 + wid; i < n; i += 4 * MK_INIT_WG) {
-    const double* srow = S + (int64_t)i * ldS;
-    double* arow = bw.A + (int64_t)i * n;
-    for (int j = lane; j < n; j += 64) arow[j] = srow[j] * sc;
-  }
-  if (part == 0)
-    for (int i = threadIdx.x; i < n; i += 256) bw.z[i] = Sr[cd.rsrc + i] * sc;
-}
-
-template <bool qr_fast, bool TIMED = false>
-__global__ __launch_bounds__(NTR) void band_mk_panel_kernel(
-    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work, int p,
-    long long* __restrict__ tim) {
-  if constexpr (!TIMED) tim = nullptr;             // production: timing compiled out
-  __shared__ double Vs[BMP][LS];
-  __shared__ double Gs[BB][LS];         // dlarft dots G
-  __shared__ double red[NWR][BB * BB];
-  __shared__ double Ts[BB][LS];
-  __shared__ double taus[BB];
-  const RidgeCellDesc cd = cells[blockIdx.x];
-  const int n = cd.n;
-  const int k0 = p * BB, r0 = k0 + BB, m = n - r0;
-  if (r0 >= n) return;
-  const int t = threadIdx.x, lane = t & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int c16 = lane & 15, g4 = lane >> 4;
-  BandWork bw(work + cd.work, n, L);
-  double* A = bw.A;
-  const bool timed = tim != nullptr && t == 0;
-  long long tk[6];
-  if (timed) tk[5] = (long long)__builtin_amdgcn_s_memtime();
-  band_panel_factor(A, n, k0, r0, m, Vs, Gs, &red[0][0], Ts, taus, bw.T + (int64_t)p * BB * BB,
-                    qr_fast, timed ? tk : nullptr);
-  if (timed) tk[2] = (long long)__builtin_amdgcn_s_memtime();
-  // U = V T -> Ug, V -> Vg (all BMP rows: rows >= m are zero)
-#pragma unroll
-  for (int q = 0; q < BMP / 16 / NWR; ++q) {
-    const int i0 = (wid + NWR * q) * 16;
-    double4_t acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc = mfma_f64_16x16x4(Vs[i0 + c16][4 * r + g4], Ts[4 * r + g4][c16], acc);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bw.Ug[(i0 + g4 + 4 * r) * BB + c16] = acc[r];
-  }
-  for (int e = t; e < BMP * BB; e += NTR) bw.Vg[e] = Vs[e / BB][e % BB];
-  if (timed) tk[3] = (long long)__builtin_amdgcn_s_memtime();
-  if (timed) {   // cycles: load | QR | G,T | U,V stores | -   (accumulated over panels)
-    tk[4] = (long long)__builtin_amdgcn_s_memtime();
-    long long* o = tim + (int64_t)blockIdx.x * 8;
-    o[0] += tk[0] - tk[5];
-    o[1] += tk[1] - tk[0];
-    o[2] += tk[2] - tk[1];
-    o[3] += tk[3] - tk[2];
-    o[4] += tk[4] - tk[3];
-  }
-}
-
-__global__ __launch_bounds__(256) void band_mk_x_kernel(const RidgeCellDesc* __restrict__ cells,
-                                                        int L, double* __restrict__ work, int p,
-                                                        int nxb) {
-  __shared__ double red[4][BB * BB];
-  __shared__ double redz[4][BB];
-  const int cell = blockIdx.x / nxb, xb = blockIdx.x % nxb;
-  const RidgeCellDesc cd = cells[cell];
-  const int n = cd.n;
-  const int r0 = p * BB + BB, m = n - r0;
-  if (r0 >= n || xb * MK_XR >= m) return;
-  const int t = threadIdx.x, lane = t & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int c16 = lane & 15, g4 = lane >> 4;
-  BandWork bw(work + cd.work, n, L);
-  const double* __restrict__ A = bw.A;
-  const double* __restrict__ Ug = bw.Ug;
-  const double* __restrict__ Vg = bw.Vg;
-  const int i0 = xb * MK_XR + 16 * wid;          // this wave's 16 rows of X
-  double4_t X = {0.0, 0.0, 0.0, 0.0};
-  double4_t Pp = {0.0, 0.0, 0.0, 0.0};
-  double4_t Pz = {0.0, 0.0, 0.0, 0.0};            // V_I^T z_I in column 0 (z as B column 0)
-  if (i0 < m) {
-    // X[i][:] = sum_k A22[k][i] U[k][:]  (A symmetric: row k, 16 contiguous columns)
-    const int col = r0 + min(i0 + c16, m - 1);
-    const double* Ab = A + (int64_t)r0 * n + col;
-    for (int k = 0; k < m; k += 32) {            // rows past m: clamped, U rows zero
-      double a[8], b[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        a[u] = Ab[(int64_t)min(k + 4 * u + g4, m - 1) * n];
-        b[u] = Ug[(k + 4 * u + g4) * BB + c16];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) X = mfma_f64_16x16x4(a[u], b[u], X);
-    }
-    // rows >= m of X are duplicates of row m-1: zero them; partial V_I^T X_I
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (i0 + g4 + 4 * r >= m) X[r] = 0.0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = i0 + 4 * r + g4;
-      const double va = Vg[row * BB + c16];
-      Pp = mfma_f64_16x16x4(va, X[r], Pp);
-      Pz = mfma_f64_16x16x4(va, (c16 == 0 && row < m) ? bw.z[r0 + row] : 0.0, Pz);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bw.Xg[(i0 + g4 + 4 * r) * BB + c16] = X[r];
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) red[wid][(g4 + 4 * r) * BB + c16] = Pp[r];
-  if (c16 == 0) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) redz[wid][g4 + 4 * r] = Pz[r];
-  }
-  __syncthreads();
-  bw.Pg[xb * BB * BB + t] = red[0][t] + red[1][t] + red[2][t] + red[3][t];
-  if (t < BB) bw.Pzg[xb * BB + t] = redz[0][t] + redz[1][t] + redz[2][t] + redz[3][t];
-}
-
-__global__ __launch_bounds__(256) void band_mk_trail_kernel(const RidgeCellDesc* __restrict__ cells,
-                                                            int L, double* __restrict__ work,
-                                                            int p, int ntile) {
-  __shared__ double Ps[BB][LS];
-  __shared__ double Ms[BB][LS];
-  __shared__ double Vl[2 * MK_TS][LS];
-  __shared__ double Wl[2 * MK_TS][LS];
-  __shared__ double Zv[BB];
-  __shared__ double Zt[BB];
-  const int cell = blockIdx.x / ntile, tile = blockIdx.x % ntile;
-  int I = (int)((__builtin_sqrtf(8.0f * (float)tile + 1.0f) - 1.0f) * 0.5f);   // + fix-ups
-  if (I * (I + 1) / 2 > tile) --I;
-  if ((I + 1) * (I + 2) / 2 <= tile) ++I;
-  const int J = tile - I * (I + 1) / 2;           // lower tile (I, J), I >= J
-  const RidgeCellDesc cd = cells[cell];
-  const int n = cd.n;
-  const int r0 = p * BB + BB, m = n - r0;
-  if (r0 >= n || I * MK_TS >= m) return;
-  const int t = threadIdx.x, lane = t & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int c16 = lane & 15, g4 = lane >> 4;
-  BandWork bw(work + cd.work, n, L);
-  double* __restrict__ A = bw.A;
-  // M = T^T sum_b P_b   (tiles (I, 0) also sum the V^T z partials: z rows of block I)
-  const int nxb = (m + MK_XR - 1) / MK_XR;
-  {
-    double s = 0.0;
-    for (int b = 0; b < nxb; ++b) s += bw.Pg[b * BB * BB + t];
-    Ps[t / BB][t % BB] = s;
-    if (J == 0 && t < BB) {
-      double z = 0.0;
-      for (int b = 0; b < nxb; ++b) z += bw.Pzg[b * BB + t];
-      Zv[t] = z;
-    }
-  }
-  // V rows of the I block (local 0..31) and the J block (local 32..63)
-  for (int e = t; e < 2 * MK_TS * BB; e += 256) {
-    const int lr = e / BB, c = e % BB;
-    const int gi = (lr < MK_TS) ? I * MK_TS + lr : J * MK_TS + lr - MK_TS;
-    Vl[lr][c] = (gi < m) ? bw.Vg[gi * BB + c] : 0.0;
-  }
-  __syncthreads();
-  {
-    const double* Tp = bw.T + (int64_t)p * BB * BB;
-    const int a = t / BB, b = t % BB;
-    double s = 0.0;
-#pragma unroll
-    for (int c = 0; c < BB; ++c) s += Tp[c * BB + a] * Ps[c][b];
-    Ms[a][b] = s;
-    if (J == 0 && t < BB) {                    // zt = T^T (V^T z)
-      double z = 0.0;
-#pragma unroll
-      for (int c = 0; c < BB; ++c) z += Tp[c * BB + t] * Zv[c];
-      Zt[t] = z;
-    }
-  }
-  __syncthreads();
-  // W = X - 1/2 V M for the same 64 rows
-  for (int e = t; e < 2 * MK_TS * BB; e += 256) {
-    const int lr = e / BB, c = e % BB;
-    const int gi = (lr < MK_TS) ? I * MK_TS + lr : J * MK_TS + lr - MK_TS;
-    double s = 0.0;
-#pragma unroll
-    for (int a = 0; a < BB; ++a) s += Vl[lr][a] * Ms[a][c];
-    Wl[lr][c] = (gi < m) ? bw.Xg[gi * BB + c] - 0.5 * s : 0.0;
-  }
-  if (J == 0 && t < MK_TS) {                   // z <- Q_p^T z on the rows of block I
-    const int gi = I * MK_TS + t;
-    if (gi < m) {
-      double v = 0.0;
-#pragma unroll
-      for (int c = 0; c < BB; ++c) v += Vl[t][c] * Zt[c];
-      bw.z[r0 + gi] -= v;
-    }
-  }
-  __syncthreads();
-  // wave -> 16 x 16 sub-tile (si, sj); on a diagonal tile the upper sub-tile is the mirror
-  const int si = wid >> 1, sj = wid & 1;
-  if (I == J && sj > si) return;
-  const int gi0 = I * MK_TS + si * 16, gj0 = J * MK_TS + sj * 16;
-  const bool mirror = (I != J) || (si != sj);
-  double4_t acc;
-  int offn[4], offt[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int i = gi0 + g4 + 4 * r, j = gj0 + c16;
-    const bool ok = i < m && j < m;
-    offn[r] = ok ? (r0 + i) * n + r0 + j : -1;
-    offt[r] = (ok && mirror) ? (r0 + j) * n + r0 + i : -1;
-    acc[r] = ok ? A[offn[r]] : 0.0;
-  }
-  const int ia = si * 16 + c16, jb = MK_TS + sj * 16 + c16;
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const int kk = 4 * (s & 3) + g4;
-    const double av = (s < 4) ? Vl[ia][kk] : Wl[ia][kk];
-    const double bv = (s < 4) ? Wl[jb][kk] : Vl[jb][kk];
-    acc = mfma_f64_16x16x4(-av, bv, acc);
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    if (offn[r] >= 0) A[offn[r]] = acc[r];
-    if (offt[r] >= 0) A[offt[r]] = acc[r];
-  }
-}
-
-__global__ __launch_bounds__(256) void band_mk_extract_kernel(
-    const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work) {
-  const RidgeCellDesc cd = cells[blockIdx.x];
-  const int n = cd.n;
-  BandWork bw(work + cd.work, n, L);
-  for (int e = threadIdx.x; e < n * LS; e += 256) {
-    const int r = e / LS, c = r - BB + e % LS;
-    bw.LB[e] = (c >= 0) ? bw.A[(int64_t)r * n + c] : 0.0;
   }
 }
 
@@ -2539,7 +1194,7 @@ constexpr int NBW = (BNMAX / 16 + NWB - 1) / NWB;   // row blocks per wave
 
 __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
     const RidgeCellDesc* __restrict__ cells, int ncells, int L, double* __restrict__ work,
-    double* __restrict__ beta_out, int64_t ldo, int fused) {
+    double* __restrict__ beta_out, int64_t ldo) {
   __shared__ double red[2][NWB][BB * BB];
   __shared__ double Vw[NWB][NBW][BB][LS];         // wave-private V_b images (transpose)
   // (the chunks of a cell are adjacent in dispatch order, so they run together and share
@@ -2572,7 +1227,7 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
       Y[q][r] = (lok && i < n) ? yc[i] : 0.0;
     }
   // va[q][r] = V_p[16 b - r0 + 4 r + g4][c16] for the live blocks b = wid + 8 q of panel p
-  const int lda = fused ? band_npad(n) : n;       // A's leading dimension (padded: the one-WG kernels)
+  const int lda = band_npad(n);                   // A's leading dimension (padded)
   const int lo_a = g4 * lda + c16;
   double vn[NBW][4], tn[4];
   auto fetch = [&](int p) {
@@ -2662,25 +1317,22 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
 extern "C" int64_t pfml_ridge_band_work_doubles(int n, int L) {
   const int64_t np = (n + BB - 1) / BB;
   const int64_t npad = band_npad(n);
-  // F region: the fused path's 5 npad x 16 scratch or the cooperative hand-off scratch
-  // (CoopWork), whichever is larger
-  const int64_t fused = 5LL * npad * BB;
+  // F region: the cooperative hand-off scratch (CoopWork)
   const int64_t coop = 2LL * npad * BB + BB * BB + (int64_t)(BNMAX / BB) * (BB * BB + BB);
   return npad * npad + (int64_t)n * LS + n + np * BB * BB + (int64_t)L * n +
-         (int64_t)L * n * LS + 3LL * BMP * BB + (int64_t)(BMP / MK_XR) * (BB * BB + BB) +
-         (fused > coop ? fused : coop);
+         (int64_t)L * n * LS + coop;
 }
 
 extern "C" int pfml_ridge_band_nmax() { return BNMAX; }
 
 namespace {
 // Panel-QR micro-benchmark (tools/bench_qr.py): every workgroup factors its own m x 16 panel
-// (row-major in P) `reps` times with band_panel_factor, the band kernels' hot serial step, in
-// the layout of the band kernels: A (lda = m + 16) holds the panel as its rows 0..15, columns
-// 16.. (the symmetric mirror the CholeskyQR2 path reads), the Householder path reads the LDS
-// image.  Cycles per factorisation (thread 0's s_memtime) -> cyc[block]; V -> Vout, T -> Tout;
-// R / V as band_panel_factor stores them land in A's columns 0..15, rows 16...
-template <int VARIANT>
+// (row-major in P) `reps` times with band_panel_hh, the band reduction's hot serial step, from
+// an LDS image of the panel as the cooperative kernel holds it.  Cycles per factorisation
+// (thread 0's s_memtime) -> cyc[block * 8 + ...]: total, load, column loop (incl. V stores),
+// G + T, and the column loop's own work / barrier wait / pivot chain + update; V -> Vout,
+// T -> Tout; R / V as band_panel_hh stores them land in A's columns 0..15, rows 16.. (lda =
+// m + 16).
 __global__ __launch_bounds__(NTR) void band_qr_bench_kernel(const double* __restrict__ P, int m,
                                                             int reps,
                                                             double* __restrict__ Aout,
@@ -2688,7 +1340,6 @@ __global__ __launch_bounds__(NTR) void band_qr_bench_kernel(const double* __rest
                                                             double* __restrict__ Tout,
                                                             long long* __restrict__ cyc) {
   __shared__ double Vs[BMP][LS];
-  __shared__ double Pc[BMP][LS];       // untouched panel copy (the CholeskyQR2 fallback's input)
   __shared__ double Gs[BB][LS];
   __shared__ double red[NWR][BB * BB];
   __shared__ double Ts[BB][LS];
@@ -2697,36 +1348,26 @@ __global__ __launch_bounds__(NTR) void band_qr_bench_kernel(const double* __rest
   const int lda = m + BB;
   const double* Pb = P + (int64_t)blockIdx.x * m * BB;
   double* Ab = Aout + (int64_t)blockIdx.x * lda * lda;
-  // cyc[block * 8 + ...]: total, load, column loop (incl. V stores), G + T, and the column
-  // loop's own work / barrier wait / pivot chain + update (thread 0; Householder form only)
   long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int rep = 0; rep < reps; ++rep) {
     for (int e = t; e < BMP * BB; e += NTR) {
       const int i = e / BB, c = e % BB;
-      const double v = (i < m) ? Pb[e] : 0.0;
-      Vs[i][c] = v;
-      Pc[i][c] = v;
-      if (i < m) Ab[(int64_t)c * lda + BB + i] = v;
+      Vs[i][c] = (i < m) ? Pb[e] : 0.0;
     }
-    __threadfence_block();
     __syncthreads();
     long long tk[6] = {0, 0, 0, 0, 0, 0};
     const long long t0 = (long long)__builtin_amdgcn_s_memtime();
-    band_panel_factor(Ab, lda, 0, BB, m, Vs, Gs, &red[0][0], Ts, taus,
-                      Tout + (int64_t)blockIdx.x * BB * BB, VARIANT >= 1,
-                      (VARIANT == 0 && t == 0) ? tk : nullptr, VARIANT == 1 ? nullptr : Vs,
-                      VARIANT == 2 ? Pc : nullptr);
+    band_panel_hh(Ab, lda, 0, BB, m, Vs, Gs, &red[0][0], Ts, taus,
+                  Tout + (int64_t)blockIdx.x * BB * BB, t == 0 ? tk : nullptr, Vs);
     __syncthreads();
     const long long t1 = (long long)__builtin_amdgcn_s_memtime();
     acc[0] += t1 - t0;
-    if (VARIANT == 0) {
-      acc[1] += tk[0] - t0;
-      acc[2] += tk[1] - tk[0];
-      acc[3] += t1 - tk[1];
-      acc[4] += tk[2];
-      acc[5] += tk[3];
-      acc[6] += tk[4];
-    }
+    acc[1] += tk[0] - t0;
+    acc[2] += tk[1] - tk[0];
+    acc[3] += t1 - tk[1];
+    acc[4] += tk[2];
+    acc[5] += tk[3];
+    acc[6] += tk[4];
   }
   for (int e = t; e < m * BB; e += NTR) Vout[(int64_t)blockIdx.x * m * BB + e] = Vs[e / BB][e % BB];
   if (t == 0)
@@ -2735,124 +1376,37 @@ __global__ __launch_bounds__(NTR) void band_qr_bench_kernel(const double* __rest
 }  // namespace
 
 extern "C" hipError_t pfml_band_qr_bench(const double* P, int m, int nblocks, int reps,
-                                         int variant, double* Aout, double* Vout, double* Tout,
+                                         double* Aout, double* Vout, double* Tout,
                                          long long* cyc, hipStream_t st) {
   if (m < 1 || m > BMP) return hipErrorInvalidValue;
-  if (variant == 2)       // CholeskyQR2 on the LDS panel (the cooperative kernel's form)
-    hipLaunchKernelGGL(band_qr_bench_kernel<2>, dim3(nblocks), dim3(NTR), 0, st, P, m, reps, Aout,
-                       Vout, Tout, cyc);
-  else if (variant == 1)  // CholeskyQR2 reading the panel from A
-    hipLaunchKernelGGL(band_qr_bench_kernel<1>, dim3(nblocks), dim3(NTR), 0, st, P, m, reps, Aout,
-                       Vout, Tout, cyc);
-  else
-    hipLaunchKernelGGL(band_qr_bench_kernel<0>, dim3(nblocks), dim3(NTR), 0, st, P, m, reps, Aout,
-                       Vout, Tout, cyc);
+  hipLaunchKernelGGL(band_qr_bench_kernel, dim3(nblocks), dim3(NTR), 0, st, P, m, reps, Aout,
+                     Vout, Tout, cyc);
   return hipGetLastError();
 }
 
 extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, const double* Sr,
-                                             const void* cells, int ncells, int nmax,
-                                             const double* lvec, int L, double* work,
-                                             double* beta_out, int64_t ldo, int band_mode,
+                                             const void* cells, int ncells, const double* lvec,
+                                             int L, double* work, double* beta_out, int64_t ldo,
                                              long long* tim, int* lu_list, int* lu_count,
                                              int lu_cap, const int* wgmap, int nwg,
                                              unsigned* syncw, hipStream_t st) {
   const RidgeCellDesc* cd = static_cast<const RidgeCellDesc*>(cells);
-  if (band_mode == 4) {
-    // cooperative reduction: nwg workgroups (wgmap: cell << 8 | w << 4 | K - 1), the cells'
-    // sync words zeroed on the stream first (a memset node under graph capture)
-    if (wgmap == nullptr || syncw == nullptr || nwg <= 0) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(syncw, 0, (size_t)ncells * COOP_SYNC * sizeof(unsigned), st);
-    if (e != hipSuccess) return e;
-    if (tim != nullptr)
-      hipLaunchKernelGGL(band_coop_kernel<true>, dim3(nwg), dim3(NTR), 0, st, SD, ldS, Sr, cd, L,
-                         work, wgmap, syncw, tim);
-    else
-      hipLaunchKernelGGL(band_coop_kernel<false>, dim3(nwg), dim3(NTR), 0, st, SD, ldS, Sr, cd, L,
-                         work, wgmap, syncw, tim);
-  }
-  // band_mode 1 (or PFML_BAND_MODE=single, or phase timing): one workgroup per cell for the
-  // whole reduction; 2 / default: the multi-workgroup form, three launches per panel.
-  const char* mode = getenv("PFML_BAND_MODE");
-  // (phase timing: the single kernel unless PFML_BAND_MODE=multi)
-  const bool env_multi = mode && mode[0] == 'm';
-  // band_mode 3 (or PFML_BAND_MODE=fused): the fused one-workgroup kernel
-  const bool fused = band_mode == 3 || (band_mode == 0 && mode && mode[0] == 'f');
-  const bool single = band_mode == 1 || (band_mode == 0 && mode && mode[0] == 's') ||
-                      (tim != nullptr && band_mode == 0 && !env_multi);
-
-  // panel QR: column-by-column Householder (default), or PFML_BAND_QR=cqr: CholeskyQR2 +
-  // Householder reconstruction with a per-panel fallback to Householder.  Measured on MI355X
-  // the CholeskyQR2 form is 6-10 % slower per reduction (profiles/r01_band_qr_ab.json): its
-  // 48 sequential 16x16 pivot steps (two Cholesky, one LU) cost more latency than the 16
-  // barrier-separated Householder columns they replace.
-  const char* qenv = getenv("PFML_BAND_QR");
-  const int qr_fast = (qenv && qenv[0] == 'c') ? 1 : 0;
-  if (band_mode == 4) {
-    // (launched above)
-  } else if (fused) {
-    if (tim != nullptr)
-      hipLaunchKernelGGL(band_fused_kernel<true>, dim3(ncells), dim3(NTR), 0, st, SD, ldS, Sr, cd,
-                         L, work, tim);
-    else
-      hipLaunchKernelGGL(band_fused_kernel<false>, dim3(ncells), dim3(NTR), 0, st, SD, ldS, Sr, cd,
-                         L, work, tim);
-  } else if (single) {
-    const char* denv = getenv("PFML_BAND_DBG");
-    const int dbg = (tim != nullptr && denv) ? atoi(denv) : 0;
-    if (dbg == 1)
-      hipLaunchKernelGGL((ridge_band_reduce_kernel<false, 1>), dim3(ncells), dim3(NTR), 0, st, SD,
-                         ldS, Sr, cd, L, work, tim);
-    else if (dbg == 2)
-      hipLaunchKernelGGL((ridge_band_reduce_kernel<false, 2>), dim3(ncells), dim3(NTR), 0, st, SD,
-                         ldS, Sr, cd, L, work, tim);
-    else if (dbg == 4)
-      hipLaunchKernelGGL((ridge_band_reduce_kernel<false, 4>), dim3(ncells), dim3(NTR), 0, st, SD,
-                         ldS, Sr, cd, L, work, tim);
-    else if (dbg == 8)
-      hipLaunchKernelGGL((ridge_band_reduce_kernel<false, 8>), dim3(ncells), dim3(NTR), 0, st, SD,
-                         ldS, Sr, cd, L, work, tim);
-    else if (dbg == 7)
-      hipLaunchKernelGGL((ridge_band_reduce_kernel<false, 7>), dim3(ncells), dim3(NTR), 0, st, SD,
-                         ldS, Sr, cd, L, work, tim);
-    else if (qr_fast)
-      hipLaunchKernelGGL(ridge_band_reduce_kernel<true>, dim3(ncells), dim3(NTR), 0, st, SD, ldS,
-                         Sr, cd, L, work, tim);
-    else if (tim != nullptr)
-      hipLaunchKernelGGL((ridge_band_reduce_kernel<false, 0, true>), dim3(ncells), dim3(NTR), 0, st,
-                         SD, ldS, Sr, cd, L, work, tim);
-    else
-      hipLaunchKernelGGL(ridge_band_reduce_kernel<false>, dim3(ncells), dim3(NTR), 0, st, SD, ldS,
-                         Sr, cd, L, work, tim);
-  } else {
-    const int npan = (nmax - 1) / BB;
-    hipLaunchKernelGGL(band_mk_init_kernel, dim3(ncells * MK_INIT_WG), dim3(256), 0, st, SD, ldS,
-                       Sr, cd, L, work);
-    for (int p = 0; p < npan; ++p) {
-      const int mmax = nmax - (p + 1) * BB;
-      const int nxb = (mmax + MK_XR - 1) / MK_XR;
-      const int tt = (mmax + MK_TS - 1) / MK_TS;
-      const int ntile = tt * (tt + 1) / 2;
-      if (qr_fast)
-        hipLaunchKernelGGL(band_mk_panel_kernel<true>, dim3(ncells), dim3(NTR), 0, st, cd, L,
-                           work, p, tim);
-      else if (tim != nullptr)
-        hipLaunchKernelGGL((band_mk_panel_kernel<false, true>), dim3(ncells), dim3(NTR), 0, st, cd,
-                           L, work, p, tim);
-      else
-        hipLaunchKernelGGL(band_mk_panel_kernel<false>, dim3(ncells), dim3(NTR), 0, st, cd, L,
-                           work, p, tim);
-      hipLaunchKernelGGL(band_mk_x_kernel, dim3(ncells * nxb), dim3(256), 0, st, cd, L, work, p,
-                         nxb);
-      hipLaunchKernelGGL(band_mk_trail_kernel, dim3(ncells * ntile), dim3(256), 0, st, cd, L,
-                         work, p, ntile);
-    }
-    hipLaunchKernelGGL(band_mk_extract_kernel, dim3(ncells), dim3(256), 0, st, cd, L, work);
-  }
+  // the cooperative reduction: nwg workgroups (wgmap: cell << 8 | w << 4 | K - 1), the cells'
+  // sync words zeroed on the stream first (a memset node under graph capture)
+  if (wgmap == nullptr || syncw == nullptr || nwg <= 0)
+    return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(syncw, 0, (size_t)ncells * COOP_SYNC * sizeof(unsigned), st);
+  if (e != hipSuccess) return e;
+  if (tim != nullptr)
+    hipLaunchKernelGGL(band_coop_kernel<true>, dim3(nwg), dim3(NTR), 0, st, SD, ldS, Sr, cd, L,
+                       work, wgmap, syncw, tim);
+  else
+    hipLaunchKernelGGL(band_coop_kernel<false>, dim3(nwg), dim3(NTR), 0, st, SD, ldS, Sr, cd, L,
+                       work, wgmap, syncw, tim);
   // (timing: the cooperative kernel fills 16 slots per cell, the solve's two go after them)
   hipLaunchKernelGGL(ridge_band_solve_kernel, dim3(ncells * ((L + 15) / 16)), dim3(NTS), 0, st,
                      cd, lvec, L, work,
-                     (band_mode == 4 && tim != nullptr) ? tim + (int64_t)ncells * 8 : tim, ncells,
+                     tim != nullptr ? tim + (int64_t)ncells * 8 : tim, ncells,
                      lu_count);
   if (lu_count != nullptr) {   // non-SPD lambdas: pivoted banded LU (count zeroed by kernel 2)
     hipLaunchKernelGGL(band_lu_flag_kernel, dim3((ncells * L + 255) / 256), dim3(256), 0, st, cd,
@@ -2862,6 +1416,6 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   }
   const int nch = (L + LC - 1) / LC;
   hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3(ncells * nch), dim3(NTB), 0, st, cd,
-                     ncells, L, work, beta_out, ldo, (fused || single || band_mode == 4) ? 1 : 0);
+                     ncells, L, work, beta_out, ldo);
   return hipGetLastError();
 }

@@ -283,7 +283,7 @@ COOP_SYNC_WORDS = 32    # csrc/ridge_band.hip COOP_SYNC: int32 sync words per ce
 
 
 def coop_k(cell_n: np.ndarray, ncu: int, others: int = 0) -> np.ndarray:
-    """Workgroups per cell of the cooperative band reduction (band_mode 4).
+    """Workgroups per cell of the cooperative band reduction.
 
     The largest-n cells of a launch share the chip's CUs (at most COOP_KMAX each, at least 1)
     when they are the p = 512 cells (n > 256: 32 panels, the grid step's critical chain); every
@@ -411,47 +411,41 @@ def repairs_done() -> int:
 
 
 def band_path(plan: dict) -> bool:
-    """True when the launch takes the band path (ridge_band.hip), whose non-SPD lambdas are
-    repaired in the band domain inside the launch; the tridiagonal path (n > 528 or
-    PFML_RIDGE_VARIANT) leaves NaN markers for ``repair_launch``."""
-    import os
-    return (plan["nmax"] <= nat.hip_lib().pfml_ridge_band_nmax()
-            and not os.environ.get("PFML_RIDGE_VARIANT", "band").startswith(("u", "bl", "f", "t"))
-            and not os.environ.get("PFML_RIDGE_UNBLOCKED"))
+    """True when the launch takes the band path (ridge_band.hip, n <= 528), whose non-SPD
+    lambdas are repaired in the band domain inside the launch; the tridiagonal path
+    (ridge.hip, 528 < n <= 1024) leaves NaN markers for ``repair_launch``."""
+    return plan["nmax"] <= nat.hip_lib().pfml_ridge_band_nmax()
 
 
 def ridge_launch(plan: dict, d_desc: torch.Tensor, SD: torch.Tensor, Sr: torch.Tensor,
-                 lv: torch.Tensor, beta: torch.Tensor, band_mode: int = 0,
-                 repair: bool = True, d_wgmap: torch.Tensor | None = None
-                 ) -> torch.Tensor | None:
+                 lv: torch.Tensor, beta: torch.Tensor, repair: bool = True,
+                 d_wgmap: torch.Tensor | None = None) -> torch.Tensor | None:
     """Queue one ridge-grid launch; returns the device count of non-SPD systems re-solved by
     the band path's pivoted banded LU (kernel 2b of ridge_band.hip), None when the launch has
     no in-band repair (``repair=False`` or the tridiagonal path).  ``d_wgmap``: the device
-    copy of plan["wgmap"] (band_mode 4, the cooperative reduction)."""
+    copy of plan["wgmap"] (the cooperative band reduction's workgroup map)."""
     P = SD.shape[-1]
     L = int(lv.numel())
     work = torch.empty(plan["work"], dtype=torch.float64, device=SD.device)
     count = lst = None
-    if repair and band_path(plan):
+    band = band_path(plan)
+    if repair and band:
         count = torch.empty(1, dtype=torch.int32, device=SD.device)   # zeroed by the solve
         lst = torch.empty(plan["nc"] * L, dtype=torch.int32, device=SD.device)
-    coop = int(band_mode) == BAND_COOP and band_path(plan)
-    if coop and d_wgmap is None:
+    if band and d_wgmap is None:
         raise ValueError("ridge_launch: the cooperative reduction needs the device wgmap")
     sync = (torch.empty(plan["nc"] * COOP_SYNC_WORDS, dtype=torch.int32, device=SD.device)
-            if coop else None)
-    LAST_COOP_SYNC[:] = [sync] if coop else []
+            if band else None)
+    LAST_COOP_SYNC[:] = [sync] if band else []
     nat.check(nat.hip_lib().pfml_ridge_grid(SD.data_ptr(), P, Sr.data_ptr(), d_desc.data_ptr(),
                                             plan["nc"], plan["nmax"], lv.data_ptr(), L,
                                             work.data_ptr(), beta.data_ptr(), beta.shape[-1],
-                                            int(band_mode) if (coop or band_mode != BAND_COOP)
-                                            else 0,
                                             lst.data_ptr() if lst is not None else None,
                                             count.data_ptr() if count is not None else None,
                                             plan["nc"] * L,
-                                            d_wgmap.data_ptr() if coop else None,
-                                            len(plan["wgmap"]) if coop else 0,
-                                            sync.data_ptr() if coop else None,
+                                            d_wgmap.data_ptr() if band else None,
+                                            len(plan["wgmap"]) if band else 0,
+                                            sync.data_ptr() if band else None,
                                             nat.stream_of(SD)),
               "pfml_ridge_grid")
     return count
@@ -471,8 +465,7 @@ def coop_errors() -> int:
 
 
 def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n: np.ndarray,
-               cell_scale: np.ndarray, lvec: torch.Tensor, repair: bool = True,
-               band_mode: int = 0) -> torch.Tensor:
+               cell_scale: np.ndarray, lvec: torch.Tensor, repair: bool = True) -> torch.Tensor:
     """beta[c, l, :n_c] = solve(SD[src_c][:n,:n]*scale_c + l I, Sr[src_c][:n]*scale_c).
 
     SD: [S, P, P] running sums, Sr: [S, P]; returns [ncells, L, P] (zero beyond n_c).
@@ -487,14 +480,11 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
     if nc == 0:
         return beta
     if nat.is_device(SD):
-        if band_mode == 0:
-            band_mode = band_policy(np.asarray(cell_n))[0]
         plan = ridge_plan(P, L, cell_src, cell_n, cell_scale, ncu=num_cus(SD.device))
         d_desc, d_wg = upload([plan["desc"], plan["wgmap"]], SD.device)
         lv = lvec.to(device=SD.device, dtype=torch.float64).contiguous()
         SDc, Src = SD.contiguous(), Sr.contiguous()
-        count = ridge_launch(plan, d_desc, SDc, Src, lv, beta, band_mode, repair=repair,
-                             d_wgmap=d_wg)
+        count = ridge_launch(plan, d_desc, SDc, Src, lv, beta, repair=repair, d_wgmap=d_wg)
         if repair:
             LAST_REPAIRS[:] = [count if count is not None
                                else repair_launch(plan, d_desc, SDc, Src, lv, beta)]
@@ -548,54 +538,12 @@ def _side_stream(dev: torch.device, k: int = 0) -> torch.cuda.Stream:
     return _SIDE[key]
 
 
-BAND_SINGLE, BAND_MULTI, BAND_FUSED, BAND_COOP = 1, 2, 3, 4
-# One workgroup per cell: the plain kernel (a look-ahead form with panel p+1's QR inside
-# panel p's trailing update measured slower: profiles/r03_band_lookahead_single_wg_ab.json).
-ONE_WG_DEFAULT = BAND_SINGLE
-# Above this many largest-n cells per launch the one-workgroup-per-cell reduction (throughput
-# form, big cells on their own stream) beats the multi-workgroup one (latency form); measured
-# on MI355X, tools/bench_band.py, and in the strong-scaling rehearsal: 53 big cells per rank
-# (2 ranks) 4.51 ms single + 2 streams vs 4.65 multi, 26-27 (4 ranks) 3.64 vs 3.18
-# (tools/gpu_shard_modes2.sh, profiles/r02_shard_modes.txt).
-BAND_MULTI_MAX_CELLS = 48
-# Hybrid (one GPU holds the whole grid): this many of the largest-n cells take the
-# multi-workgroup reduction on a third stream while the rest keep one workgroup per cell, so
-# the CUs the single-workgroup cells leave idle also work on big cells.  Measured on MI355X
-# (profiles/r02_band_hybrid_ab.json): 16 / 32 / 48 hybrid cells give 7.05 / 7.54 / 7.59 ms
-# per grid step against 6.59 ms with none - the multi-workgroup cells' three launches per panel
-# contend with the one-workgroup cells - so it is off.  PFML_BAND_HYBRID overrides.
-BAND_HYBRID_CELLS = 0
-
-
-def _hybrid_cells(nbig: int) -> int:
+def two_streams() -> bool:
+    """The largest cells' ridge group and the rest on two streams (default; the small cells'
+    chain fills the CUs the big cells leave idle).  PFML_RIDGE_STREAMS=1 puts them on one."""
     import os
-    v = os.environ.get("PFML_BAND_HYBRID")
-    k = int(v) if v else BAND_HYBRID_CELLS
-    return max(0, min(k, nbig - 1))
-
-
-def band_policy(cell_n: np.ndarray) -> tuple[int, bool]:
-    """(band_mode, two_streams) for one grid launch.
-
-    Few big cells (multi-GPU shards): the multi-workgroup band reduction on one stream.  Many
-    (one GPU holds the whole grid): one workgroup per cell, the big cells on a second stream so
-    the small cells' chain fills the CUs they leave idle.  PFML_BAND_MODE=single|multi and
-    PFML_RIDGE_STREAMS=1|2 override."""
-    import os
-    cell_n = np.asarray(cell_n)
-    mode = BAND_COOP
-    env = os.environ.get("PFML_BAND_MODE", "")[:1]
-    if env == "s":
-        mode = BAND_SINGLE
-    elif env == "m":
-        mode = BAND_MULTI
-    elif env == "f":
-        mode = BAND_FUSED
-    two = mode in (BAND_SINGLE, BAND_FUSED, BAND_COOP)
     v = os.environ.get("PFML_RIDGE_STREAMS")
-    if v:
-        two = v.strip() == "2"
-    return mode, two
+    return (v.strip() == "2") if v else True
 
 
 _UTIL_PLANS: dict = {}
@@ -615,19 +563,14 @@ def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell,
     if hit is not None:
         return hit
     big = cell_n == cell_n.max()
-    nhy = _hybrid_cells(int(big.sum())) if split else 0
-    if split and nhy:
-        # the first nhy big cells (in cell order) -> multi-workgroup group
-        hy = big & (np.cumsum(big) <= nhy)
-        parts = ((big & ~hy, ONE_WG_DEFAULT), (hy, BAND_MULTI), (~big, ONE_WG_DEFAULT))
-    elif split:
+    if split:
         # the largest cells (their own cooperative launch: the chip's CUs shared among them)
         # and the rest (one workgroup each), each group on a stream of its own
-        parts = ((big, None), (~big, None))
+        parts = (big, ~big)
     else:
-        parts = ((np.ones(len(cell_n), dtype=bool), None),)
+        parts = (np.ones(len(cell_n), dtype=bool),)
     groups, arrays = [], []
-    for grp, gmode in parts:
+    for grp in parts:
         cells = np.nonzero(grp)[0]
         jobs = np.nonzero(grp[job_cell])[0]
         rp = ridge_plan(P, L, cell_src[cells], cell_n[cells], cell_scale[cells], ncu=num_cus(dev),
@@ -635,7 +578,7 @@ def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell,
         # ridge_plan orders cells big-first and numbers outputs 0..: map to global rows
         rp["desc"]["out"] = cells[rp["desc"]["out"] // (L * P)].astype(np.int64) * L * P
         qp = quad_plan(P, L, P, job_cell[jobs], job_month[jobs], job_n[jobs], job_out=jobs)
-        groups.append((cells, jobs, rp, qp, gmode))
+        groups.append((cells, jobs, rp, qp))
         arrays += [rp["desc"], qp["desc"], qp["tile_job"], rp["wgmap"]]
     dv = upload(arrays, dev)                     # all descriptors, one async copy
     plan = {"groups": groups, "dv": dv}
@@ -682,11 +625,10 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     cell_scale = np.asarray(cell_scale, dtype=np.float64)
     job_cell, job_month, job_n = (np.asarray(job_cell), np.asarray(job_month),
                                   np.asarray(job_n))
-    mode, two = band_policy(cell_n)
     if not nat.is_device(SD):
-        beta = ridge_grid(SD, Sr, cell_src, cell_n, cell_scale, lvec, band_mode=mode)
+        beta = ridge_grid(SD, Sr, cell_src, cell_n, cell_scale, lvec)
         return beta, quadform_utilities(D, R, beta, job_cell, job_month, job_n)
-    split = two and len(np.unique(cell_n)) >= 2
+    split = two_streams() and len(np.unique(cell_n)) >= 2
     th = _HostClock()
     S, P, _ = SD.shape
     check_launch_bounds(S, P, D.shape[0], cell_src, cell_n, job_cell, job_month, job_n)
@@ -712,10 +654,9 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
     counts = []
     for gi in range(ng):
         stream = streams[gi]
-        _, _, rp, qp, gmode = plan["groups"][gi]
+        _, _, rp, qp = plan["groups"][gi]
         with torch.cuda.stream(stream):
-            cnt = ridge_launch(rp, dv[4 * gi], SD, Sr, lv, beta, mode if gmode is None else gmode,
-                               d_wgmap=dv[4 * gi + 3])
+            cnt = ridge_launch(rp, dv[4 * gi], SD, Sr, lv, beta, d_wgmap=dv[4 * gi + 3])
             counts.append(cnt if cnt is not None else repair_launch(rp, dv[4 * gi], SD, Sr, lv, beta))
             quad_launch(qp, dv[4 * gi + 1], dv[4 * gi + 2], D, R, beta, obj)
     th("launch")

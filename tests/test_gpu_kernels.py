@@ -250,66 +250,58 @@ def test_lu_solve_two_level(gpu, n, m, b):
     assert rel < (1e-11 if n <= 512 else 1e-10), rel     # (rounding grows with n)
 
 
-@pytest.mark.parametrize("variant", ["unblocked", "blocked", "fast"])
-def test_ridge_variants_agree(gpu, variant, monkeypatch):
-    """The three tridiagonalisation kernels (fused sweep / dlatrd-blocked / LDS fast path)
-    all reproduce the LU-solve oracle at production size."""
-    from pfml.ops.ridge import ridge_grid
-    monkeypatch.setenv("PFML_RIDGE_VARIANT", variant)
-    P = 513
-    SD = _spd_stack(2, P, n_obs=900, seed=51)
-    Sr = _rand(2, P, seed=52)
-    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
-    src, nn, sc = np.array([0, 1, 1, 0]), np.array([513, 257, 129, 65]), np.full(4, 2e-3)
-    ref = ridge_grid(SD, Sr, src, nn, sc, lv)
-    out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
-    rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
-    assert rel < 1e-10, rel
+@pytest.mark.parametrize("n_obs", [1500, 400])
+def test_ridge_tridiagonal_large_n(gpu, n_obs):
+    """528 < n <= 1024 (p up to 1023, e.g. --set pf_ml.p_vec=[1023]) takes the blocked
+    tridiagonal path (csrc/ridge.hip) with the dense device repair (csrc/ridge_repair.hip) of
+    its non-SPD systems: the LU-solve oracle's betas, full-rank (n_obs = 1500, lambda = 0
+    included) and rank-deficient (n_obs = 400 < n: the small lambdas repaired)."""
+    from pfml.ops import ridge as rg
+    P = 1024
+    SD = _spd_stack(2, P, n_obs=n_obs, seed=151)
+    SD = 0.5 * (SD + SD.transpose(1, 2))
+    Sr = _rand(2, P, seed=152)
+    lam = np.exp(np.linspace(-10, 10, 24)) if n_obs > P else np.exp(np.linspace(-2, 10, 24))
+    lv = torch.tensor([0.0] + list(lam), dtype=torch.float64)
+    src, nn, sc = np.array([0, 1, 0]), np.array([1024, 700, 529]), np.full(3, 1e-3)
+    ref = rg.ridge_grid(SD, Sr, src, nn, sc, lv)
+    out = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
+    assert not rg.band_path({"nmax": 1024})
+    assert not torch.isnan(out).any()
+    ok = slice(None) if n_obs > P else slice(1, None)         # (singular at lambda = 0)
+    rel = ((out[:, ok] - ref[:, ok]).norm(dim=-1) / ref[:, ok].norm(dim=-1)).max().item()
+    assert rel < 1e-9, rel
 
 
-@pytest.mark.parametrize("mode", ["single", "multi", "fused"])
-def test_band_reduction_modes(gpu, mode, monkeypatch):
-    """One-workgroup-per-cell and multi-workgroup band reductions both reproduce the LU-solve
-    oracle, with cells of different n (65 .. 513) in one launch."""
-    from pfml.ops.ridge import ridge_grid
-    monkeypatch.setenv("PFML_BAND_MODE", mode)
-    P = 513
-    SD = _spd_stack(3, P, n_obs=700, seed=61)
-    Sr = _rand(3, P, seed=62)
-    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
-    src = np.array([0, 1, 2, 1, 0, 2, 2])
-    nn = np.array([513, 513, 65, 257, 129, 100, 513])
-    sc = np.full(len(src), 1.5e-3)
-    ref = ridge_grid(SD, Sr, src, nn, sc, lv)
-    out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
-    rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
-    assert rel < 1e-10, rel
-
-
-@pytest.mark.parametrize("n_obs", [700, 90])
-def test_band_fused_bitwise_single(gpu, n_obs, monkeypatch):
-    """The fused band reduction (one pass over the trailing matrix per panel, full symmetric
-    storage, upper tiles in the mirror's operation order) gives bitwise the betas of the
-    one-workgroup kernel on exactly symmetric window sums, for every n of the grid (and a
-    ragged n), full-rank and rank-deficient (n_obs = 90 < n: lambda = 0 repaired)."""
-    from pfml.ops.ridge import ridge_grid
-    P = 513
-    SD = _spd_stack(3, P, n_obs=n_obs, seed=71)
-    SD = 0.5 * (SD + SD.transpose(1, 2))           # exactly symmetric, like the window sums
-    Sr = _rand(3, P, seed=72)
-    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-10, 10, 100))), dtype=torch.float64)
-    src = np.array([0, 1, 2, 1, 0, 2, 2, 1])
-    nn = np.array([513, 513, 65, 257, 129, 100, 513, 17])
-    sc = np.full(len(src), 1.5e-3)
-    out = {}
-    for mode in ("single", "fused"):
-        monkeypatch.setenv("PFML_BAND_MODE", mode)
-        out[mode] = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
-    a = out["single"]
-    for mode in ("fused",):
-        b = out[mode]
-        same = (a == b) | (torch.isnan(a) & torch.isnan(b))
-        assert bool(same.all()), (mode, float((a - b).abs().max()))
+def test_ridge_dense_repair_tridiagonal_path(gpu):
+    """The tridiagonal path's dense device repair (csrc/ridge_repair.hip: flag + pivoted LU,
+    np.linalg.solve semantics) re-solves exactly the NaN-marked (cell, lambda) systems: betas
+    of the LU oracle there, the other systems untouched."""
+    from pfml.ops import ridge as rg
+    P = 700
+    SD = _spd_stack(2, P, n_obs=900, seed=153)
+    Sr = _rand(2, P, seed=154)
+    lv = torch.tensor([0.0] + list(np.exp(np.linspace(-6, 6, 11))), dtype=torch.float64)
+    src, nn, sc = np.array([0, 1, 1]), np.array([700, 600, 560]), np.full(3, 1e-3)
+    beta = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu), repair=False)
+    keep = beta.clone()
+    marks = [(0, 0), (1, 5), (2, 11), (2, 3)]
+    for c, l in marks:
+        beta[c, l, :nn[c]] = float("nan")
+    plan = rg.ridge_plan(P, len(lv), src, nn, sc)
+    d_desc, = rg.upload([plan["desc"]], beta.device)
+    cnt = rg.repair_launch(plan, d_desc, SD.to(gpu).contiguous(), Sr.to(gpu).contiguous(),
+                           lv.to(gpu), beta)
+    assert int(cnt.item()) == len(marks)
+    ref = rg.ridge_grid(SD, Sr, src, nn, sc, lv)
+    out = beta.cpu()
+    for c, l in marks:
+        rel = ((out[c, l] - ref[c, l]).norm() / ref[c, l].norm()).item()
+        assert rel < 1e-9, (c, l, rel)
+    untouched = torch.ones(beta.shape[:2], dtype=torch.bool)
+    for c, l in marks:
+        untouched[c, l] = False
+    assert torch.equal(out[untouched], keep.cpu()[untouched])
 
 
 @pytest.mark.parametrize("n_obs", [700, 90])
@@ -336,8 +328,7 @@ def test_band_coop_matches_lu_and_bitwise_across_k(gpu, n_obs, monkeypatch):
         out = {}
         for k in ("1", "2", "3", "8", "16"):
             monkeypatch.setenv("PFML_COOP_K", k)
-            out[k] = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu),
-                                   band_mode=rg.BAND_COOP).cpu()
+            out[k] = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
             assert rg.coop_errors() == 0, (ncell, k)
         a = out["1"]
         for k, b in out.items():
@@ -362,25 +353,24 @@ def test_band_coop_mixed_launch_bitwise(gpu, monkeypatch):
     nn = np.array([513, 513, 65, 257, 129, 100, 513, 17])
     sc = np.full(len(src), 1.5e-3)
     monkeypatch.setenv("PFML_COOP_K", "4")
-    mixed = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu),
-                          band_mode=rg.BAND_COOP).cpu()
+    mixed = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
     assert rg.coop_errors() == 0
     monkeypatch.setenv("PFML_COOP_K", "1")
     for c in range(len(src)):
         one = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src[c:c + 1], nn[c:c + 1], sc[c:c + 1],
-                            lv.to(gpu), band_mode=rg.BAND_COOP).cpu()
+                            lv.to(gpu)).cpu()
         assert torch.equal(one[0], mixed[c]), c
+    ref = rg.ridge_grid(SD, Sr, src, nn, sc, lv)
+    rel = ((mixed - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
+    assert rel < 1e-10, rel
 
 
-@pytest.mark.parametrize("hybrid", ["0", "3"])
-def test_ridge_utilities_stream_groups(gpu, hybrid, monkeypatch):
-    """ridge_utilities with the big cells split over streams (single-workgroup group, and with
-    PFML_BAND_HYBRID=3 three big cells in a multi-workgroup group on a third stream) gives the
-    CPU oracle's betas and utilities."""
+@pytest.mark.parametrize("streams", ["2", "1"])
+def test_ridge_utilities_stream_groups(gpu, streams, monkeypatch):
+    """ridge_utilities with the largest cells' chain on a side stream (default) or every cell
+    on one stream (PFML_RIDGE_STREAMS=1) gives the CPU oracle's betas and utilities."""
     from pfml.ops.ridge import ridge_utilities
-    monkeypatch.setenv("PFML_BAND_MODE", "")
-    monkeypatch.setenv("PFML_BAND_HYBRID", hybrid)
-    monkeypatch.setattr("pfml.ops.ridge.BAND_MULTI_MAX_CELLS", 2)   # force the split form
+    monkeypatch.setenv("PFML_RIDGE_STREAMS", streams)
     P = 513
     SD = _spd_stack(3, P, n_obs=700, seed=65)
     Sr = _rand(3, P, seed=66)
@@ -400,30 +390,6 @@ def test_ridge_utilities_stream_groups(gpu, hybrid, monkeypatch):
     rel = ((gb.cpu() - rb).norm(dim=-1) / rb.norm(dim=-1).clamp(min=1e-300)).max().item()
     assert rel < 1e-8, rel
     assert torch.allclose(go.cpu(), ro, rtol=1e-8, atol=1e-12 * ro.abs().max().item())
-
-
-@pytest.mark.parametrize("qr", ["cqr", "householder"])
-@pytest.mark.parametrize("mode", ["single", "multi"])
-@pytest.mark.parametrize("n_obs", [700, 90])
-def test_band_panel_qr(gpu, qr, mode, n_obs, monkeypatch):
-    """Panel QR of the band reduction: the column-by-column Householder QR (default) and the
-    opt-in CholeskyQR2 + Householder reconstruction give the LU-solve oracle's ridge solutions.  With
-    n_obs = 90 every window sum has rank 90 < n, so the trailing panels are rank-deficient and
-    the CholeskyQR2 path must hand them to the Householder fallback."""
-    from pfml.ops.ridge import ridge_grid
-    monkeypatch.setenv("PFML_BAND_MODE", mode)
-    monkeypatch.setenv("PFML_BAND_QR", qr)
-    P = 513
-    SD = _spd_stack(2, P, n_obs=n_obs, seed=63)
-    Sr = _rand(2, P, seed=64)
-    lam = np.exp(np.linspace(-10, 10, 100)) if n_obs > P else np.exp(np.linspace(-2, 10, 40))
-    lv = torch.tensor(list(lam), dtype=torch.float64)
-    src, nn = np.array([0, 1, 0, 1]), np.array([513, 513, 257, 100])
-    sc = np.full(len(src), 1.5e-3)
-    ref = ridge_grid(SD, Sr, src, nn, sc, lv)
-    out = ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
-    rel = ((out - ref).norm(dim=-1) / ref.norm(dim=-1)).max().item()
-    assert rel < 1e-10, rel
 
 
 @pytest.mark.parametrize("fmt", ["bf16", "fp8"])

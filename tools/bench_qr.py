@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
-"""Panel-QR micro-benchmark: band_panel_factor (csrc/ridge_band.hip) in isolation.
+"""Panel-QR micro-benchmark: band_panel_hh (csrc/ridge_band.hip) in isolation.
 
 Cycles per m x 16 panel factorisation (the band reduction's serial step, once per panel on
-the critical chain of every ridge cell) for the column-by-column Householder form (variant 0)
-and the CholeskyQR2 + reconstruction form (variant 1), with ``nblocks`` workgroups factoring
-at once (1: latency alone; 106: the one-GPU grid's big cells), plus the numerics of each:
-Q = I - V T V' orthogonal and Q' P = [R; 0] to fp64 rounding.
+the critical chain of every ridge cell), column-by-column Householder with the panel in LDS,
+with ``nblocks`` workgroups factoring at once (1: latency alone; 106: the one-GPU grid's big
+cells), plus the numerics: Q = I - V T V' orthogonal and Q' P = [R; 0] to fp64 rounding.
+(A CholeskyQR2 + Householder-reconstruction form measured 45-60 % slower per panel,
+profiles/r04_qr_bench_dpp.jsonl, and was removed.)
 
     python tools/bench_qr.py [m ...]            (default m = 497 241 113)
 """
@@ -20,7 +21,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from pfml.ops import _native as nat  # noqa: E402
 
-nat.register_hip("pfml_band_qr_bench", [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+nat.register_hip("pfml_band_qr_bench", [C.c_void_p, C.c_int, C.c_int, C.c_int,
                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_void_p])
 
@@ -39,7 +40,7 @@ def panels(nblocks: int, m: int, kind: str, seed: int = 0) -> torch.Tensor:
     return P
 
 
-def run(m: int, nblocks: int, variant: int, kind: str, reps: int = 20) -> dict:
+def run(m: int, nblocks: int, kind: str, reps: int = 20) -> dict:
     dev = torch.device("cuda", 0)
     P = panels(nblocks, m, kind).to(dev)
     lda = m + 16
@@ -48,7 +49,7 @@ def run(m: int, nblocks: int, variant: int, kind: str, reps: int = 20) -> dict:
     T = torch.zeros(nblocks, 16, 16, dtype=torch.float64, device=dev)
     cyc = torch.zeros(nblocks, 8, dtype=torch.int64, device=dev)
     st = torch.cuda.current_stream().cuda_stream
-    nat.check(nat.hip_lib().pfml_band_qr_bench(P.data_ptr(), m, nblocks, reps, variant,
+    nat.check(nat.hip_lib().pfml_band_qr_bench(P.data_ptr(), m, nblocks, reps,
                                                A.data_ptr(), V.data_ptr(), T.data_ptr(),
                                                cyc.data_ptr(), st), "pfml_band_qr_bench")
     torch.cuda.synchronize()
@@ -64,22 +65,18 @@ def run(m: int, nblocks: int, variant: int, kind: str, reps: int = 20) -> dict:
         ref[:16] = R
         rerr = ((QP - ref).abs().max() / Pc.abs().max()).item()
     c = cyc.float()[0].tolist()                   # block 0 (the others: cycles_max)
-    out = {"m": m, "blocks": nblocks, "variant": ["householder", "cqr2", "cqr2_lds"][variant],
-           "panel": kind, "cycles_per_panel": int(c[0]), "cycles_max": int(cyc[:, 0].max()),
-           "orth_err": orth, "qp_err": rerr}
-    if variant == 0:
-        out.update({"load": int(c[1]), "columns": int(c[2]), "g_t": int(c[3]),
-                    "col_own": int(c[4]), "col_barrier": int(c[5]), "col_chain_update": int(c[6])})
-    return out
+    return {"m": m, "blocks": nblocks, "panel": kind, "cycles_per_panel": int(c[0]),
+            "cycles_max": int(cyc[:, 0].max()), "orth_err": orth, "qp_err": rerr,
+            "load": int(c[1]), "columns": int(c[2]), "g_t": int(c[3]), "col_own": int(c[4]),
+            "col_barrier": int(c[5]), "col_chain_update": int(c[6])}
 
 
 if __name__ == "__main__":
     ms = [int(x) for x in sys.argv[1:]] or [497, 241, 113]
     out = []
     for m in ms:
-        for variant in (0, 1, 2):
-            for nb in (1, 106):
-                for kind in (("full", "deficient", "dup") if nb == 1 else ("full",)):
-                    r = run(m, nb, variant, kind)
-                    out.append(r)
-                    print(json.dumps(r), flush=True)
+        for nb in (1, 106):
+            for kind in (("full", "deficient", "dup") if nb == 1 else ("full",)):
+                r = run(m, nb, kind)
+                out.append(r)
+                print(json.dumps(r), flush=True)

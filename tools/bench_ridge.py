@@ -36,50 +36,28 @@ def run(ncells, n, reps=3):
     return (time.perf_counter() - t) / reps * 1e3
 
 
-def timing(n=513, ncells=1):
-    """Per-phase cycle split of the band reduction (or, with PFML_RIDGE_VARIANT=fast, the
-    fast tridiagonalisation) for one cell."""
+def timing(n=513):
+    """Per-phase cycle split of the cooperative band reduction: 8 phase slots for workgroup 0
+    (the QR one) and 1 of cell 0, plus the banded solve's forward / backward cycles."""
     from pfml.ops import _native as nat
     dev = torch.device("cuda", 0)
-    mode = os.environ.get("PFML_BAND_MODE", "coop")[:1]
-    if mode not in ("s", "m", "f"):
-        # cooperative kernel: 8 phase slots for workgroup 0 (the QR one) and 1 of cell 0
-        ncells = int(os.environ.get("PFML_TIMING_CELLS", "1"))
-        buf = torch.zeros(ncells * 16 + 16, dtype=torch.int64, device=dev)
-        nat.hip_lib().pfml_ridge_set_timing(buf.data_ptr())
-        run(ncells, n, reps=1)
-        torch.cuda.synchronize()
-        nat.hip_lib().pfml_ridge_set_timing(None)
-        allb = buf.cpu().numpy()
-        names = ["init_panel0", "U", "X_partials", "sync_wait", "C_sums_W", "update",
-                 "lookahead_qr", "end_sync"]
-        out = {"K": os.environ.get("PFML_COOP_K", "auto"), "cells": ncells}
-        for w in (0, 1):
-            t = allb[w * 8:(w + 1) * 8]
-            tot = max(1, int(t.sum()))
-            out[f"wg{w}"] = {nm: f"{int(v)} cyc ({100.0 * v / tot:.1f}%)" for nm, v in zip(names, t)}
-            out[f"wg{w}_total_cyc"] = tot
-        out.update({"solve_fwd_cyc": int(allb[ncells * 16]),
-                    "solve_bwd_cyc": int(allb[ncells * 16 + 1])})
-        return out
-    buf = torch.zeros(ncells * 8 + 16, dtype=torch.int64, device=dev)
+    ncells = int(os.environ.get("PFML_TIMING_CELLS", "1"))
+    buf = torch.zeros(ncells * 16 + 16, dtype=torch.int64, device=dev)
     nat.hip_lib().pfml_ridge_set_timing(buf.data_ptr())
     run(ncells, n, reps=1)
     torch.cuda.synchronize()
     nat.hip_lib().pfml_ridge_set_timing(None)
     allb = buf.cpu().numpy()
-    t = allb[:ncells * 8].reshape(ncells, 8)[0]
-    extra = {"solve_fwd_cyc": int(allb[ncells * 8]), "solve_bwd_cyc": int(allb[ncells * 8 + 1])}
-    if os.environ.get("PFML_RIDGE_VARIANT", "band")[:1] in ("f", "t"):
-        names = ["col_k", "householder", "sweep", "xy", "p_w_z", "trailing", "panel_end", "-"]
-    elif os.environ.get("PFML_BAND_MODE", "")[:1] == "f":
-        names = ["qr_columns", "strip", "qr_total", "U", "pass", "P_z_W", "final", "qr_G_T"]
-    else:
-        names = ["qrcol_own", "qr", "qrcol_barrier", "U", "X", "P4_z_W", "trailing",
-                 "qrcol_chain_update"]   # qrcol_*: inside "qr" (thread 0 wave)
-    tot = max(1, int(t.sum()))
-    out = {nm: f"{int(v)} cyc ({100.0 * v / tot:.1f}%)" for nm, v in zip(names, t)}
-    out.update(extra)
+    names = ["init_panel0", "U", "X_partials", "sync_wait", "C_sums_W", "update",
+             "lookahead_qr", "end_sync"]
+    out = {"K": os.environ.get("PFML_COOP_K", "auto"), "cells": ncells}
+    for w in (0, 1):
+        t = allb[w * 8:(w + 1) * 8]
+        tot = max(1, int(t.sum()))
+        out[f"wg{w}"] = {nm: f"{int(v)} cyc ({100.0 * v / tot:.1f}%)" for nm, v in zip(names, t)}
+        out[f"wg{w}_total_cyc"] = tot
+    out.update({"solve_fwd_cyc": int(allb[ncells * 16]),
+                "solve_bwd_cyc": int(allb[ncells * 16 + 1])})
     return out
 
 

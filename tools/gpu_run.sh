@@ -5,11 +5,15 @@
 #   suite      pytest -m gpu + smoke()          bench     headline bench (one JSON line)
 #   timeline   kernel timeline of one grid step shard     one-GPU per-rank strong-scaling rehearsal
 #   peak       fp64 MFMA / VALU roofline anchor dgemm     library vs in-house DGEMM rate
-#   ridge      band reduction A/B per phase     ktest     pytest -m gpu -k "$PFML_KTEST"
+#   coop       cooperative band reduction: tests, per-phase timing, time vs #cells
+#   cooptime   per-phase timing at K = 1 / 2       benchk    headline bench at auto K and K = 1
+#   qr         panel-QR micro-benchmark        ktest     pytest -m gpu -k "$PFML_KTEST"
 #   e2e        production-shape `main` end to end (synthetic raw data, S0 stages, 8 stages)
 #   s4         S4+S5+S6 bench + S4 kernel stats stress    3000-stock S4 stress (BASELINE config 4)
+#   s4roof     S4 roofline (kernel trace + work ledger)   dgemmpmc  in-house DGEMM TF/s + PMC
 #   stressprof kernel stats of the stress    prec bf16 / fp8 S4 GEMMs (BASELINE config 5)  pmc     PMC counters of one grid step
-#   multiproc  2 and 4 ranks sharing the GPU (gloo), utilities vs 1 rank
+#   shards4    per-rank S4 + grid step of W = 1 / 2 / 4 / 8 rank shards on this GPU
+#   multiproc  2, 4 and 8 ranks sharing the GPU (gloo), utilities bitwise vs 1 rank
 set -o pipefail
 TAG=${1:-r03}
 MODE=${2:-suite}
@@ -91,7 +95,7 @@ for step in ${MODE//,/ }; do
       unset PFML_COOP_K ;;
     coop)
       # cooperative band reduction: tests (oracle + bitwise across K), per-phase timing of
-      # one n = 513 cell at K = 1 / 2 / 4, wall time vs #cells (auto K), and vs single
+      # one n = 513 cell at K = 1 / 2 / 4, wall time vs #cells (auto K)
       timeout -k 10 600 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 300 --timeout-method thread -k "coop" > $OUT/pytest_coop.log 2>&1
       rc=$?; tail -3 $OUT/pytest_coop.log
       if [ $rc -ne 0 ]; then grep -E "^E |FAILED" $OUT/pytest_coop.log | head -20; exit $rc; fi
@@ -100,42 +104,7 @@ for step in ${MODE//,/ }; do
         rc=$?; cat $OUT/coop_timing_k$k.json; if [ $rc -ne 0 ]; then exit $rc; fi
       done
       PFML_BENCH_CELLS=1,13,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/coop_cells.log 2>&1
-      rc=$?; tail -1 $OUT/coop_cells.log; if [ $rc -ne 0 ]; then exit $rc; fi
-      PFML_BAND_MODE=single PFML_BENCH_CELLS=1,13,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/single_cells.log 2>&1
-      rc=$?; tail -1 $OUT/single_cells.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
-    ridge)
-      # band-reduction A/B: per-phase cycles of one n = 513 cell and the grid vs #cells
-      for m in single fused; do
-        PFML_BAND_MODE=$m timeout -k 10 120 python tools/bench_ridge.py --timing > $OUT/ridge_timing_$m.json 2>&1
-        rc=$?; cat $OUT/ridge_timing_$m.json; if [ $rc -ne 0 ]; then exit $rc; fi
-        PFML_BAND_MODE=$m PFML_BENCH_CELLS=1,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/ridge_cells_$m.log 2>&1
-        rc=$?; tail -1 $OUT/ridge_cells_$m.log; if [ $rc -ne 0 ]; then exit $rc; fi
-      done ;;
-    ridgedbg)
-      # trailing-update bottleneck probe: per-phase cycles with parts of P6 compiled out
-      for d in 0 1 2 4 8 7; do
-        PFML_BAND_MODE=single PFML_BAND_DBG=$d timeout -k 10 120 python tools/bench_ridge.py --timing > $OUT/ridge_dbg_$d.json 2>&1
-        rc=$?; echo "dbg $d: $(grep trailing $OUT/ridge_dbg_$d.json)"; if [ $rc -ne 0 ]; then exit $rc; fi
-      done ;;
-    ridgecqr)
-      # CholeskyQR2 panel factorisation (PFML_BAND_QR=cqr) in the single kernel
-      PFML_BAND_MODE=single PFML_BAND_QR=cqr timeout -k 10 120 python tools/bench_ridge.py --timing > $OUT/ridge_timing_cqr.json 2>&1
-      rc=$?; cat $OUT/ridge_timing_cqr.json; if [ $rc -ne 0 ]; then exit $rc; fi
-      PFML_BAND_MODE=single PFML_BAND_QR=cqr PFML_BENCH_CELLS=1,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/ridge_cells_cqr.log 2>&1
-      rc=$?; tail -1 $OUT/ridge_cells_cqr.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
-    fusedtest)
-      timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 120 --timeout-method thread -k "band_fused or band_reduction_modes" > $OUT/pytest_fused.log 2>&1
-      rc=$?; tail -3 $OUT/pytest_fused.log
-      if [ $rc -ne 0 ]; then grep -E "^E |FAILED" $OUT/pytest_fused.log | head -20; exit $rc; fi ;;
-    benchfused)
-      PFML_BAND_MODE=fused timeout -k 10 300 python bench.py --no-inputs > $OUT/bench_fused.json 2> $OUT/bench_fused.err
-      rc=$?; grep '^{' $OUT/bench_fused.json | cut -c1-300; if [ $rc -ne 0 ]; then tail -5 $OUT/bench_fused.err; exit $rc; fi ;;
-    abband)
-      # headline bench: the one-WG-per-cell reduction (single) vs the cooperative one, A/B/A/B
-      for m in single coop single coop; do
-        PFML_BAND_MODE=$m timeout -k 10 200 python bench.py > $OUT/bench_$m.json 2> $OUT/bench_$m.err
-        rc=$?; echo "$m: $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_$m.json)"; if [ $rc -ne 0 ]; then tail -5 $OUT/bench_$m.err; exit $rc; fi
-      done ;;
+      rc=$?; tail -1 $OUT/coop_cells.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     timeline)
       # kernel timeline of the last full 1-GPU grid step
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/prof1 -o run -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-inputs > $OUT/prof1.log 2>&1)
