@@ -29,8 +29,6 @@
 
 namespace {
 
-constexpr int BK = 16;
-constexpr int KS = BK + 2;       // [idx][k] row stride (doubles)
 
 struct Epi {
   double alpha, beta;
@@ -78,8 +76,9 @@ template <> struct Ld<2> {
 // load() only issues the (clamped, always valid) global loads; the bounds mask and the k-scale
 // are applied in store(), after the MFMAs of the current step, so nothing consumes a load
 // result early and the compiler keeps the whole next tile in flight across the MFMA block.
-template <int R, bool KCONTIG, int W>
+template <int R, bool KCONTIG, int W, int BK>
 struct Operand {
+  static constexpr int KS = BK + 2;                 // [idx][k] row stride (doubles)
   static constexpr int S = R + 16;
   static constexpr int SIZE = KCONTIG ? R * KS : BK * S;
   static constexpr int NV = R * BK / W / 256;       // vector loads per thread
@@ -138,17 +137,20 @@ struct Operand {
   }
 };
 
-template <bool TA, bool TB, int BM, int BN, int W, bool KSC>
+// BK: k-values staged per step; NBUF: LDS buffers (2: the next step is written to the other
+// buffer after this step's MFMAs, one barrier per step; 1: half the LDS - more resident
+// workgroups or a deeper BK at the same occupancy - for a second barrier per step).
+template <bool TA, bool TB, int BM, int BN, int W, bool KSC, int BK = 16, int NBUF = 2>
 __global__ __launch_bounds__(256, 2) void dgemm_kernel(
     int M, int N, int K, int tiles_m, int tiles_n, int nwg,
     const double* __restrict__ A, int64_t lda, int64_t sA,
     const double* __restrict__ B, int64_t ldb, int64_t sB,
     double* __restrict__ C, int64_t ldc, int64_t sC, Epi ep) {
   constexpr int TM = BM / 32, TN = BN / 32;         // 16x16 accumulators per wave (M, N)
-  using OA = Operand<BM, !TA, W>;                   // A stored M x K: contiguous along k
-  using OB = Operand<BN, TB, W>;                    // B stored N x K (TB): contiguous along k
-  __shared__ double As[2][OA::SIZE];
-  __shared__ double Bs[2][OB::SIZE];
+  using OA = Operand<BM, !TA, W, BK>;               // A stored M x K: contiguous along k
+  using OB = Operand<BN, TB, W, BK>;                // B stored N x K (TB): contiguous along k
+  __shared__ double As[NBUF][OA::SIZE];
+  __shared__ double Bs[NBUF][OB::SIZE];
 
   const int wg = xcd_remap(blockIdx.x, nwg);
   const int tiles = tiles_m * tiles_n;
@@ -188,7 +190,7 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(
   rb.template store<KSC>(Bs[0], 0, K, t);
   __syncthreads();
   for (int s = 0; s < nk; ++s) {
-    const int cur = s & 1;
+    const int cur = NBUF == 2 ? (s & 1) : 0;
     const bool more = s + 1 < nk;
     if (more) {
       ra.template load<false>(lda, (s + 1) * BK, K, nullptr, t);
@@ -208,9 +210,10 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f64_16x16x4(a[i], bb[j], acc[i][j]);
     }
+    if constexpr (NBUF == 1) __syncthreads();     // every wave is done reading the buffer
     if (more) {
-      ra.template store<false>(As[cur ^ 1], (s + 1) * BK, K, t);
-      rb.template store<KSC>(Bs[cur ^ 1], (s + 1) * BK, K, t);
+      ra.template store<false>(As[NBUF == 2 ? (cur ^ 1) : 0], (s + 1) * BK, K, t);
+      rb.template store<KSC>(Bs[NBUF == 2 ? (cur ^ 1) : 0], (s + 1) * BK, K, t);
     }
     __syncthreads();
   }
@@ -255,7 +258,7 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(
       }
 }
 
-template <int BM, int BN, int W>
+template <int BM, int BN, int W, int BK, int NBUF>
 hipError_t launch(int ta, int tb, int M, int N, int K, int batch, const double* A, int64_t lda,
                   int64_t sA, const double* B, int64_t ldb, int64_t sB, double* C, int64_t ldc,
                   int64_t sC, const Epi& ep, hipStream_t st) {
@@ -263,7 +266,8 @@ hipError_t launch(int ta, int tb, int M, int N, int K, int batch, const double* 
   const long nwg = (long)tm * tn * batch;
   if (nwg > 0x7fffffffL) return hipErrorInvalidValue;
 #define PFML_GEMM_CASE(TA_, TB_, KS_)                                                       \
-  hipLaunchKernelGGL((dgemm_kernel<TA_, TB_, BM, BN, W, KS_>), dim3((unsigned)nwg), dim3(256),  \
+  hipLaunchKernelGGL((dgemm_kernel<TA_, TB_, BM, BN, W, KS_, BK, NBUF>), dim3((unsigned)nwg),    \
+                     dim3(256),                                                                 \
                      0, st, M, N, K, tm, tn, (int)nwg, A, lda, sA, B, ldb, sB, C, ldc, sC, ep)
   const bool ksc = ep.ks != nullptr;
   if (ksc) {
@@ -283,7 +287,7 @@ hipError_t launch(int ta, int tb, int M, int N, int K, int batch, const double* 
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-template <int BM, int BN>
+template <int BM, int BN, int BK = 16, int NBUF = 2>
 hipError_t launch_w(int ta, int tb, int M, int N, int K, int batch, const double* A, int64_t lda,
                     int64_t sA, const double* B, int64_t ldb, int64_t sB, double* C,
                     int64_t ldc, int64_t sC, const Epi& ep, hipStream_t st) {
@@ -294,8 +298,10 @@ hipError_t launch_w(int ta, int tb, int M, int N, int K, int batch, const double
                    (sA % 2 == 0) && (sB % 2 == 0) && aligned16(A) && aligned16(B) &&
                    (!ep.ks || (aligned16(ep.ks) && ep.sks % 2 == 0));
   if (vec)
-    return launch<BM, BN, 2>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, ep, st);
-  return launch<BM, BN, 1>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, ep, st);
+    return launch<BM, BN, 2, BK, NBUF>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc,
+                                       sC, ep, st);
+  return launch<BM, BN, 1, BK, NBUF>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC,
+                                     ep, st);
 }
 
 }  // namespace
@@ -314,7 +320,9 @@ struct PfmlGemmEpi {
   int has_diag;
   const double* es; int64_t ses;
   int sincos;
-  int tile_cfg;      // 0 auto, 1: 128x128, 2: 128x64, 3: 64x64
+  int tile_cfg;      // 0 auto, 1: 128x128, 2: 128x64, 3: 64x64 (BK 16, two LDS buffers);
+                     // 4: 64x64 BK 32 one buffer, 5: 64x64 BK 32 two buffers (a 128x128
+                     // BK 32 form spills: 144 B per lane)
 };
 
 extern "C" int pfml_gemm_epi_size() { return (int)sizeof(PfmlGemmEpi); }
@@ -335,6 +343,12 @@ extern "C" hipError_t pfml_dgemm_ex(int ta, int tb, int M, int N, int K, int bat
     cfg = (M >= 1024 && N >= 1024) ? 1 : 3;
   }
   if (cfg == 1 && h->sincos) cfg = 3;    // the 128 x 128 kernel has no sincos epilogue
+  if (cfg == 4)
+    return launch_w<64, 64, 32, 1>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, ep,
+                                   st);
+  if (cfg == 5)
+    return launch_w<64, 64, 32, 2>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, ep,
+                                   st);
   if (cfg == 1)
     return launch_w<128, 128>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, ep, st);
   if (cfg == 2)

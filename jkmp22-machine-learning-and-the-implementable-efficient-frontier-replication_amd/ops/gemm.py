@@ -68,6 +68,7 @@ def _ledger(ta, tb, M, N, K, batch, A3, B3, C3, ks=None, sks=0, sincos=False, cf
     if cfg == 1 and sincos:
         cfg = 3
     bm, bn = {1: (128, 128), 2: (128, 64)}.get(cfg, (64, 64))
+    bk, nbuf = {4: (32, 1), 5: (32, 2)}.get(cfg, (16, 2))
     lda, ldb = A3.stride(1), B3.stride(1)
     sa, sb = _bstride(A3, batch), _bstride(B3, batch)
     a_cont, b_cont = (M if ta else K), (K if tb else N)
@@ -76,7 +77,8 @@ def _ledger(ta, tb, M, N, K, batch, A3, B3, C3, ks=None, sks=0, sincos=False, cf
            and B3.data_ptr() % 16 == 0
            and (ks is None or (ks.data_ptr() % 16 == 0 and sks % 2 == 0)))
     b = lambda v: "true" if v else "false"                                  # noqa: E731
-    name = f"dgemm_kernel<{b(ta)}, {b(tb)}, {bm}, {bn}, {2 if vec else 1}, {b(ks is not None)}>"
+    name = (f"dgemm_kernel<{b(ta)}, {b(tb)}, {bm}, {bn}, {2 if vec else 1}, "
+            f"{b(ks is not None)}, {bk}, {nbuf}>")
     na = M * K * (A3.shape[0] if sa else 1)
     nb = K * N * (B3.shape[0] if sb else 1)
     _work.add(name, 2.0 * batch * M * N * K, 8.0 * (na + nb + batch * M * N) + extra_bytes)
@@ -243,7 +245,8 @@ def _vec3(v, batch):
     return v2, (0 if (v2.shape[0] == 1 and batch > 1) else v2.stride(0))
 
 
-# A/B switch for the auto tile choice (0 auto, 1: 128x128, 2: 128x64, 3: 64x64), read once
+# A/B switch for the auto tile choice (0 auto, 1: 128x128, 2: 128x64, 3: 64x64; 4, 5: BK = 32
+# variants, csrc/gemm_f64.hip PfmlGemmEpi), read once
 _TILE_DEFAULT = int(os.environ.get("PFML_GEMM_TILE", "0"))
 
 

@@ -249,7 +249,7 @@ def _lu_ledger(M, n, m, ldm, sM, a0, b0, z0, batch) -> None:
                     continue
                 big = rows >= 1024 and wdt >= 1024
                 t = "128, 128" if big else "64, 64"
-                _work.add(f"dgemm_kernel<false, false, {t}, {2 if vec else 1}, false>",
+                _work.add(f"dgemm_kernel<false, false, {t}, {2 if vec else 1}, false, 16, 2>",
                          2.0 * batch * rows * wdt * kb, 8.0 * batch * (rows * kb + 2 * rows * wdt))
 
 

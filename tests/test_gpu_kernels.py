@@ -63,7 +63,7 @@ def test_gemm_epi_struct_matches():
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
-@pytest.mark.parametrize("cfg", [1, 2, 3])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("shape", [(2, 37, 53, 29), (3, 130, 258, 100), (2, 96, 224, 96)])
 def test_gemm_fused_matches_torch(gpu, ta, tb, cfg, shape):
     """Every fusion of csrc/gemm_f64.hip (k-scale prologue, row/col scale, beta, addend block,

@@ -23,7 +23,7 @@ SHAPES = [  # name, batch, M, N, K, horner fusion
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    cfgs = [int(c) for c in os.environ.get("PFML_DGEMM_CFGS", "1,3").split(",")]
+    cfgs = [int(c) for c in os.environ.get("PFML_DGEMM_CFGS", "1,3,4,5").split(",")]
     dev = torch.device("cuda", 0)
     out = {}
     for name, b, M, N, K, fused in SHAPES:

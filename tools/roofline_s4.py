@@ -20,12 +20,12 @@ import sys
 
 MFMA, VALU, HBM = 78.2e12, 65.7e12, 8.0e12
 ROLE = {
-    "dgemm_kernel<false, false, 64, 64, 2, true>": "Horner step of (24) (k-scaled, fused epilogue)",
-    "dgemm_kernel<false, false, 128, 128, 2, true>": "Horner step of (24), 128 x 128 tiles",
-    "dgemm_kernel<false, false, 64, 64, 2, false>": "m_func / SPD-inverse Schur GEMMs, Sigma, LU panel transforms",
-    "dgemm_kernel<false, true, 64, 64, 2, false>": "X F X' (Sigma), SPD-inverse X21 / X11 updates",
-    "dgemm_kernel<true, false, 64, 64, 2, true>": "denominator / summand Gram products (25)",
-    "dgemm_kernel<true, false, 64, 64, 2, false>": "risk / tc: omega' Sigma omega",
+    "dgemm_kernel<false, false, 64, 64, 2, true, 16, 2>": "Horner step of (24) (k-scaled, fused epilogue)",
+    "dgemm_kernel<false, false, 128, 128, 2, true, 16, 2>": "Horner step of (24), 128 x 128 tiles",
+    "dgemm_kernel<false, false, 64, 64, 2, false, 16, 2>": "m_func / SPD-inverse Schur GEMMs, Sigma, LU panel transforms",
+    "dgemm_kernel<false, true, 64, 64, 2, false, 16, 2>": "X F X' (Sigma), SPD-inverse X21 / X11 updates",
+    "dgemm_kernel<true, false, 64, 64, 2, true, 16, 2>": "denominator / summand Gram products (25)",
+    "dgemm_kernel<true, false, 64, 64, 2, false, 16, 2>": "risk / tc: omega' Sigma omega",
     "spd_leafinv_kernel": "64 x 64 SPD leaf inverses (register Gauss-Jordan)",
     "mfunc_sym_kernel": "m_func symmetric elementwise passes",
     "db_norm_partial_kernel": "Denman-Beavers scaling norms",
