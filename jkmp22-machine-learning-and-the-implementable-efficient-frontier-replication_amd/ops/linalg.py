@@ -161,7 +161,7 @@ def _spd_inverse_blocked(X: torch.Tensor, status: torch.Tensor) -> None:
     """In-place SPD inverse by 64-wide Gauss-Jordan block steps: the pivot block inverted in
     LDS (csrc/spd_inverse.hip), row panel, rank-64 trailing update and column panel on the
     fused fp64 MFMA GEMM (csrc/gemm_f64.hip).  Measured on [256, 490, 490]
-    (tools/bench_inverse.py, profiles/r02_inverse_variants.json): 4.70 ms (12.8 TF/s); the
+    (tools/bench_inverse.py, profiles/r02_inverse_variants_v2.json): 4.70 ms (12.8 TF/s); the
     fused sign-symmetric 3-launch form (PFML_SPD_INV=sym, pfml_spd_inverse_sym) 4.83 ms and
     128-wide blocks (PFML_SPD_INV=generic128) 6.0 ms - the rank-64 update pass is
     bandwidth/latency-bound in every form."""

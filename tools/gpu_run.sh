@@ -167,6 +167,13 @@ for step in ${MODE//,/ }; do
     pmc)
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_WAIT_INST_ANY --output-format csv -d $OUT/pmc -o run -- python3 $ROOT/bench.py --steps 1 --warmup 0 --no-inputs > $OUT/pmc.log 2>&1)
       rc=$?; python tools/pmc_summary.py $OUT/pmc --top 10 > $OUT/pmc.txt 2>&1; cat $OUT/pmc.txt; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    pmcmem)
+      # HBM bytes per grid-step kernel: FETCH_SIZE and WRITE_SIZE in passes of their own
+      # (3 + 2 TCC counters), with the kernel durations from the same runs
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE SQ_WAVES --output-format csv -d $OUT/pmc_fetch -o run -- python3 $ROOT/bench.py --steps 1 --warmup 0 --no-inputs > $OUT/pmc_fetch.log 2>&1)
+      rc=$?; python tools/pmc_summary.py $OUT/pmc_fetch --top 14 > $OUT/pmc_fetch.txt 2>&1; cat $OUT/pmc_fetch.txt; if [ $rc -ne 0 ]; then exit $rc; fi
+      (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE SQ_WAVES --output-format csv -d $OUT/pmc_write -o run -- python3 $ROOT/bench.py --steps 1 --warmup 0 --no-inputs > $OUT/pmc_write.log 2>&1)
+      rc=$?; python tools/pmc_summary.py $OUT/pmc_write --top 14 > $OUT/pmc_write.txt 2>&1; cat $OUT/pmc_write.txt; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     multiproc)
       timeout -k 10 900 bash tools/gpu_multiproc.sh $TAG ;;
     *) echo "unknown step $step"; exit 2 ;;

@@ -9,7 +9,7 @@ headline config (2 g x 53 years, n = 513 / 257 / 129 / 65, 101 lambdas, 12 valid
 710 months of 513 x 513 summands); the 106 big cells' reduction runs on 106 of 256 CUs, so
 its per-CU efficiency is quoted too.
 
-usage: python tools/roofline.py profiles/r03_step_timeline_v1.txt > profiles/r03_roofline.md
+usage: python tools/roofline.py profiles/r03_step_timeline_v1.txt > profiles/r03_roofline_grid_step.md
 """
 import re
 import sys
