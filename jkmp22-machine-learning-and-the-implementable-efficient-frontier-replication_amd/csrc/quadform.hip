@@ -8,6 +8,13 @@
 // on fp64 MFMA (upper block triangle only: D_t is symmetric) and folds the two reductions
 // into the epilogue, so U never leaves registers.
 //
+// Tail index: n = p + 1 with p a multiple of 64 (65 .. 513), so the last index would cost a
+// 16-wide K step of its own in every row tile and a 64-row tile of its own.  When n - 1 is a
+// multiple of BK the tiles cover indices 0 .. n-2 only (K loop included); column n-1 enters
+// each row's U in the epilogue (one rank-1 term) and row n-1's own term
+// b_{n-1} (r_{n-1} - D_{n-1,n-1} b_{n-1} / 2) is added by the reduce kernel: 1 / 5 fewer
+// tile-steps at n = 65, 2 / 15 at 129, 5 / 45 at 257, 9 / 153 at 513.
+//
 // Tile: 64 rows of D x 112 lambda columns (L <= 112) x 1 (or 2) validation months of one cell
 // per 256-thread workgroup (3 per CU); each wave owns 16 rows x 7 MFMA 16x16 accumulators per
 // month.  Every workgroup writes a deterministic per-row-tile
@@ -31,6 +38,11 @@ constexpr int BK = 16, NCOL = 112, NTILE = NCOL / 16, BM = 64, NT = 256, NW = NT
 // without bank conflicts, and a fragment read (16 rows x 2 k per 32-lane group) hits 32
 // distinct bank pairs.  (A [k][row] image made every staging store a 16-way conflict.)
 constexpr int KS = BK + 2;
+
+// indices the tiles cover (n, or n - 1 when the tail index is split off, see above)
+__host__ __device__ __forceinline__ int quad_main(int n) {
+  return (n > 1 && (n - 1) % 16 == 0) ? n - 1 : n;
+}
 
 struct JobDesc {
   int64_t d_off;     // offset of D_t (P x P, ld ldD)
@@ -72,7 +84,9 @@ __global__ __launch_bounds__(NT, MM == 1 ? 3 : 2) void quadform_kernel(
   }
   const JobDesc jd0 = jobs[jm[0]];
   const int i0 = rt * BM;
-  const int n = jd0.n;
+  const int nfull = jd0.n;
+  const int n = quad_main(nfull);                 // indices of the tiles and their K loop
+  const bool tail = n != nfull;
   const double* Dm[MM];
   const double* rm[MM];
 #pragma unroll
@@ -158,6 +172,22 @@ __global__ __launch_bounds__(NT, MM == 1 ? 3 : 2) void quadform_kernel(
   }
   __syncthreads();                            // red reuses As
 
+  // tail column n: U[i][l] += D[i][n] b_l[n] (K block above every row tile: weight 1)
+  if (tail) {
+#pragma unroll
+    for (int q = 0; q < NTILE; ++q) {
+      const int l = min(q * 16 + (lane & 15), L - 1);
+      const double bt_l = bt[(int64_t)l * ldB + n];
+#pragma unroll
+      for (int m = 0; m < MM; ++m)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int gi = min(i0 + w * 16 + PFML_F64_CROW(lane, rr), n - 1);
+          acc[m][q][rr] = fma(Dm[m][(int64_t)gi * ldD + n], bt_l, acc[m][q][rr]);
+        }
+    }
+  }
+
   // epilogue: sum over this wave's 16 rows of  beta_l[i] * (r_i - 1/2 U[i][l])
 #pragma unroll
   for (int q = 0; q < NTILE; ++q) {
@@ -197,14 +227,22 @@ __global__ __launch_bounds__(NT, MM == 1 ? 3 : 2) void quadform_kernel(
 
 __global__ void quadform_reduce_kernel(const double* __restrict__ partial,
                                        const JobDesc* __restrict__ jobs, int njobs, int L,
+                                       const double* __restrict__ D, int64_t ldD,
+                                       const double* __restrict__ R,
+                                       const double* __restrict__ Bt, int64_t ldB,
                                        double* __restrict__ obj) {
   const int j = blockIdx.x;
   const int l = threadIdx.x;
   if (j >= njobs || l >= L) return;
   const JobDesc jd = jobs[j];
-  const int nt = (jd.n + BM - 1) / BM;
+  const int n = quad_main(jd.n);
+  const int nt = (n + BM - 1) / BM;
   double s = 0.0;
   for (int q = 0; q < nt; ++q) s += partial[(int64_t)(jd.ptile0 + q) * L + l];
+  if (n != jd.n) {                              // the tail row's own term
+    const double b = Bt[jd.b_off + (int64_t)l * ldB + n];
+    s += b * (R[jd.r_off + n] - 0.5 * D[jd.d_off + (int64_t)n * ldD + n] * b);
+  }
   obj[jd.o_off + l] = s;
 }
 
@@ -212,6 +250,7 @@ __global__ void quadform_reduce_kernel(const double* __restrict__ partial,
 
 extern "C" int pfml_quadform_job_desc_size() { return (int)sizeof(JobDesc); }
 extern "C" int pfml_quadform_rows_per_tile() { return BM; }
+extern "C" int pfml_quadform_row_tiles(int n) { return (quad_main(n) + BM - 1) / BM; }
 
 // tile_job: mm (1 or 2) int32 entries per tile (see quadform_kernel).
 extern "C" hipError_t pfml_quadform(const double* D, int64_t ldD, const double* R,
@@ -228,6 +267,6 @@ extern "C" hipError_t pfml_quadform(const double* D, int64_t ldD, const double* 
     hipLaunchKernelGGL(quadform_kernel<1>, dim3(ntiles), dim3(NT), 0, st, D, ldD, R, Bt, ldB, jd,
                        tile_job, L, partial);
   hipLaunchKernelGGL(quadform_reduce_kernel, dim3(njobs), dim3(128), 0, st, partial, jd, njobs, L,
-                     obj);
+                     D, ldD, R, Bt, ldB, obj);
   return hipGetLastError();
 }

@@ -38,6 +38,8 @@ def _declare_hip(lib):
     lib.pfml_quadform.restype = I
     lib.pfml_quadform_job_desc_size.restype = I
     lib.pfml_quadform_rows_per_tile.restype = I
+    lib.pfml_quadform_row_tiles.argtypes = [I]
+    lib.pfml_quadform_row_tiles.restype = I
     lib.pfml_segsum.argtypes = [P, L, P, P, I, P, P]
     lib.pfml_segsum.restype = I
     lib.pfml_spd_inverse.argtypes = [P, I, L, L, I, P, P, P]

@@ -676,10 +676,12 @@ def quad_plan(P: int, L: int, Pb: int, job_cell, job_month, job_n, job_out=None)
     lib = nat.hip_lib()
     if lib.pfml_quadform_job_desc_size() != JOB_DTYPE.itemsize:
         raise RuntimeError("JobDesc layout mismatch between python and libpfml_hip")
-    rows = lib.pfml_quadform_rows_per_tile()
     job_n = np.asarray(job_n)
     nj = len(job_n)
-    ntile = (job_n + rows - 1) // rows
+    # row tiles per job as the kernel counts them (the tail index n - 1 split off when n - 1
+    # is a multiple of the K step: csrc/quadform.hip quad_main)
+    tiles_of = {int(v): int(lib.pfml_quadform_row_tiles(int(v))) for v in np.unique(job_n)}
+    ntile = np.array([tiles_of[int(v)] for v in job_n], dtype=np.int64)
     pt0 = np.concatenate([[0], np.cumsum(ntile)[:-1]]).astype(np.int32)
     desc = np.zeros(nj, dtype=JOB_DTYPE)
     desc["d_off"] = np.asarray(job_month, np.int64) * P * P
@@ -690,7 +692,7 @@ def quad_plan(P: int, L: int, Pb: int, job_cell, job_month, job_n, job_out=None)
     desc["n"] = job_n.astype(np.int32)
     desc["ptile0"] = pt0
     if nj and int(ntile.max()) > 32:
-        raise ValueError("quad_plan: more than 32 row tiles per job (n > 32 * rows)")
+        raise ValueError("quad_plan: more than 32 row tiles per job (n > 32 * 64)")
     # a tile covers `mm` jobs of ONE cell (same beta, same n: its validation months), so the
     # staged beta K-tiles feed mm D tiles; an odd job out gets -1 in the spare entries
     # (2 months per tile: measured 5.90 vs 5.78 ms per grid step on MI355X - fewer resident

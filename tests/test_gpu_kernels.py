@@ -178,14 +178,16 @@ def test_ridge_grid_production_rank_deficient(gpu):
 
 
 def test_quadform_utilities(gpu):
+    """Utilities vs the CPU oracle for n with a split-off tail index (n - 1 a multiple of 16:
+    129, 97, 65, 33, 17; csrc/quadform.hip quad_main) and without (130, 100, 1)."""
     from pfml.ops.ridge import quadform_utilities
     T, P, L = 5, 130, 101
     D = _spd_stack(T, P, n_obs=50, seed=31)
     R = _rand(T, P, seed=32)
     beta = _rand(4, L, P, seed=33)
-    jc = np.array([0, 1, 2, 3, 3, 0])
-    jm = np.array([0, 1, 2, 3, 4, 4])
-    jn = np.array([130, 65, 33, 17, 130, 1])
+    jc = np.array([0, 1, 2, 3, 3, 0, 1, 2, 3])
+    jm = np.array([0, 1, 2, 3, 4, 4, 0, 3, 2])
+    jn = np.array([130, 65, 33, 17, 130, 1, 129, 97, 100])
     ref = quadform_utilities(D, R, beta, jc, jm, jn)
     out = quadform_utilities(D.to(gpu), R.to(gpu), beta.to(gpu), jc, jm, jn).cpu()
     rel = ((out - ref).abs() / ref.abs().clamp_min(1e-12)).max().item()
