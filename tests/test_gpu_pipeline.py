@@ -163,17 +163,43 @@ def test_pfml_inputs_gpu_matches_cpu(gpu, small_data):
 
 
 def test_full_pipeline_gpu(gpu, small_data, tmp_path):
+    """S4-S9 on the device against the same stages on the CPU oracle path, from copies of the
+    same L0-L3 data: every validation utility (obj, cum_obj) to 1e-8, the ranks (hence the
+    chosen hyper-parameters) exactly, then weights / pf / pf_summary to 1e-8."""
+    import shutil
     from pfml.data.io import CSV_COLUMNS
     from pfml.pipeline import Pipeline
-    cfg = small_data.override([f"run.artifact_dir={tmp_path}", "pf.dates.start_year=1999",
-                               "pf.dates.end_yr=2012", "pf.dates.split_years=3"])
-    p = Pipeline(cfg, device="cuda")
-    p.run(["pfml-input", "pfml-search-coef", "pfml-hp-reals", "pfml-aim", "pfml-hps",
-           "pfml-best-hps"])
-    for name in ("validation.csv", "weights.csv", "pf.csv", "pf_summary.csv"):
-        df = pd.read_csv(os.path.join(cfg.run.data_dir, name))
+    stages = ["pfml-input", "pfml-search-coef", "pfml-hp-reals", "pfml-aim", "pfml-hps",
+              "pfml-best-hps"]
+    out = {}
+    for dev in ("cuda", "cpu"):
+        d = str(tmp_path / f"data_{dev}")
+        shutil.copytree(small_data.run.data_dir, d)
+        cfg = small_data.override([f"run.data_dir={d}", f"run.artifact_dir={tmp_path}/art_{dev}",
+                                   "pf.dates.start_year=1999", "pf.dates.end_yr=2012",
+                                   "pf.dates.split_years=3"])
+        Pipeline(cfg, device=dev).run(stages)
+        out[dev] = {n: pd.read_csv(os.path.join(d, n)) for n in
+                    ("validation.csv", "weights.csv", "pf.csv", "pf_summary.csv")}
+    for name, df in out["cuda"].items():
         assert list(df.columns) == CSV_COLUMNS[name]
-    s = pd.read_csv(os.path.join(cfg.run.data_dir, "pf_summary.csv"))
+    g, c = out["cuda"]["validation.csv"], out["cpu"]["validation.csv"]
+    key = ["g", "p", "l", "hp_end", "eom"]
+    g, c = g.sort_values(key).reset_index(drop=True), c.sort_values(key).reset_index(drop=True)
+    assert g[key].equals(c[key])
+    for col in ("obj", "cum_obj"):
+        a, b = g[col].to_numpy(), c[col].to_numpy()
+        assert np.array_equal(np.isnan(a), np.isnan(b)), col
+        ok = ~np.isnan(a)
+        assert np.allclose(a[ok], b[ok], rtol=1e-8, atol=1e-12 * np.abs(b[ok]).max()), col
+    assert np.array_equal(g["rank"].fillna(-1).to_numpy(), c["rank"].fillna(-1).to_numpy())
+    for name in ("weights.csv", "pf.csv", "pf_summary.csv"):
+        a, b = out["cuda"][name], out["cpu"][name]
+        assert a.shape == b.shape, name
+        num = [k for k in a.columns if np.issubdtype(a[k].dtype, np.number)]
+        assert np.allclose(a[num].to_numpy(float), b[num].to_numpy(float), rtol=1e-8,
+                           atol=1e-12, equal_nan=True), name
+    s = out["cuda"]["pf_summary.csv"]
     assert np.isfinite(s[["r", "sd", "sr", "obj"]].to_numpy()).all()
 
 
