@@ -219,82 +219,17 @@ extern "C" hipError_t pfml_spd_inverse(double* A, int n, int64_t lda, int64_t sA
 }
 
 // ---------------------------------------------------------------------------------------
-// Large-block variant: the NBL x NBL pivot block (NBL = 128) is inverted in LDS by one
-// 1024-thread workgroup per matrix; the row panel, the rank-NBL trailing update and the
-// column panel are then plain batched GEMMs on pfml_dgemm (host orchestration in
-// ops/linalg.py), so each block step is one MFMA-bound pass over the matrix instead of the
-// four bandwidth-bound passes of the NB = 32 kernels above.
+// Leaves of the recursive Schur-complement inverse (the production form for n >= 160, host
+// orchestration in ops/linalg.py::_spd_inverse_recursive: every off-diagonal product one
+// fused GEMM, csrc/gemm_f64.hip).  (Blocked Gauss-Jordan forms with 64- / 128-wide pivot
+// blocks and a fused sign-symmetric form measured 2.1 / 3.0 / 2.4x slower on [256, 490, 490],
+// profiles/r02_inverse_variants_v2.json, and were removed.)
 namespace {
 constexpr int NBL = 64;
 
-template <int NBT>
-__global__ __launch_bounds__(256) void spd_blockinv_kernel(const double* __restrict__ A,
-                                                            int64_t lda, int64_t sA, int k0,
-                                                            int nb, double* __restrict__ Pout,
-                                                            int* __restrict__ status) {
-  __shared__ double P[NBT][NBT + 1];
-  constexpr int EPT = NBT * NBT / 256;            // elements per thread (fixed NBT^2 frame)
-  const int b = blockIdx.x;
-  const double* Ab = A + (int64_t)b * sA + (int64_t)k0 * lda + k0;
-  const int t = threadIdx.x;
-  // element u of this thread: (i, j) = (e / NBT, e % NBT), e = t + 256 u; frame entries past
-  // nb hold the identity, so the elimination below needs no bounds tests
-  {
-    double v[EPT];
-#pragma unroll
-    for (int u = 0; u < EPT; ++u) {            // every load in flight at once
-      const int e = t + 256 * u, i = e / NBT, j = e % NBT;
-      v[u] = Ab[(int64_t)min(i, nb - 1) * lda + min(j, nb - 1)];
-    }
-#pragma unroll
-    for (int u = 0; u < EPT; ++u) {
-      const int e = t + 256 * u, i = e / NBT, j = e % NBT;
-      P[i][j] = (i < nb && j < nb) ? v[u] : (i == j ? 1.0 : 0.0);
-    }
-  }
-  __syncthreads();
-  for (int p = 0; p < nb; ++p) {
-    // P[p][p], P[i][p], P[p][j] are only rewritten after the next barrier, so reading the
-    // pivot needs no barrier of its own
-    const double piv = P[p][p];
-    if (t == 0 && (!(piv > 0.0) || !isfinite(piv))) status[b] = 1;
-    const double inv = 1.0 / piv;
-#pragma unroll
-    for (int u = 0; u < EPT; ++u) {
-      const int e = t + 256 * u, i = e / NBT, j = e % NBT;
-      if (i != p && j != p) P[i][j] -= P[i][p] * P[p][j] * inv;
-    }
-    __syncthreads();
-    if (t < NBT && t != p) {
-      P[p][t] *= inv;
-      P[t][p] *= -inv;
-    }
-    if (t == 0) P[p][p] = inv;
-    __syncthreads();
-  }
-  double* Pb = Pout + (int64_t)b * NBT * NBT;
-#pragma unroll
-  for (int u = 0; u < EPT; ++u) {
-    const int e = t + 256 * u, i = e / NBT, j = e % NBT;
-    if (i < nb && j < nb) Pb[i * NBT + j] = P[i][j];
-  }
-}
-}  // namespace
-
-extern "C" hipError_t pfml_spd_blockinv128(const double* A, int64_t lda, int64_t sA, int batch,
-                                           int k0, int nb, double* Pout, int* status,
-                                           hipStream_t st) {
-  if (batch <= 0 || nb <= 0) return hipSuccess;
-  if (nb > 128) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(spd_blockinv_kernel<128>, dim3(batch), dim3(256), 0, st, A, lda, sA, k0, nb,
-                     Pout, status);
-  return hipGetLastError();
-}
-
-namespace {
 // Register-resident 64 x 64 Gauss-Jordan inverse (no pivoting: SPD blocks), 4 pivots per
-// barrier.  The LDS form above re-reads and re-writes the whole block from LDS at every pivot
-// (LDS-bandwidth bound, ~80 us per batch of 256 blocks) and a one-pivot register form is
+// barrier.  An LDS form that re-reads and re-writes the whole block at every pivot was
+// LDS-bandwidth bound (~80 us per batch of 256 blocks) and a one-pivot register form is
 // bound by its 64 barrier + divide round trips (~50 us).  Here each of the 256 threads keeps a
 // 4 x 4 sub-block in registers; pivot block q (4 pivots) is exactly thread row / column block
 // q, so the owners publish whole register tiles to a double-buffered LDS line
@@ -418,18 +353,6 @@ __global__ __launch_bounds__(256) void spd_leafinv_kernel(const double* __restri
 }
 }  // namespace
 
-extern "C" int pfml_spd_block_size() { return NBL; }
-
-extern "C" hipError_t pfml_spd_blockinv(const double* A, int64_t lda, int64_t sA, int batch,
-                                        int k0, int nb, double* Pout, int* status,
-                                        hipStream_t st) {
-  if (batch <= 0 || nb <= 0) return hipSuccess;
-  if (nb > NBL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(spd_leafinv_kernel, dim3(batch), dim3(256), 0, st, A, lda, sA, k0, nb, Pout,
-                     (int64_t)NBL, (int64_t)NBL * NBL, status);
-  return hipGetLastError();
-}
-
 // Inverse of the nb x nb (nb <= 64) diagonal block at (k0, k0) of A written to the block at
 // (k0, k0) of P (any leading dims / batch strides; P == A: in place).
 extern "C" hipError_t pfml_spd_leafinv_to(const double* A, int64_t lda, int64_t sA, double* P,
@@ -439,216 +362,5 @@ extern "C" hipError_t pfml_spd_leafinv_to(const double* A, int64_t lda, int64_t 
   if (nb > NBL) return hipErrorInvalidValue;
   hipLaunchKernelGGL(spd_leafinv_kernel, dim3(batch), dim3(256), 0, st, A, lda, sA, k0, nb,
                      P + (int64_t)k0 * ldp + k0, ldp, sP, status);
-  return hipGetLastError();
-}
-
-// In-place inverse of the nb x nb (nb <= 64) diagonal block at (k0, k0) of each matrix.
-extern "C" hipError_t pfml_spd_leafinv_inplace(double* A, int64_t lda, int64_t sA, int batch,
-                                               int k0, int nb, int* status, hipStream_t st) {
-  if (batch <= 0 || nb <= 0) return hipSuccess;
-  if (nb > NBL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(spd_leafinv_kernel, dim3(batch), dim3(256), 0, st, A, lda, sA, k0, nb,
-                     A + (int64_t)k0 * lda + k0, lda, sA, status);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------
-// Fused symmetric block step (the production path for n >= 160).  For SPD A, blocked
-// Gauss-Jordan keeps the working matrix "sign-symmetric": with s_i = -1 on rows of blocks
-// already eliminated (i < k0) and +1 elsewhere, A_ij = s_i s_j A_ji.  So the old column
-// panel of block K is C = diag(s) W^T with W = A[K, :] (the row panel), and the new column
-// panel -C P is -diag(s) R^T with R = P W.  One step is then three launches:
-//   spd_blockinv_kernel   P = A_KK^-1                                  (LDS Gauss-Jordan)
-//   gjs_prep_kernel        W = A[K, :] (snapshot), R = P W              (MFMA, one 64-col tile)
-//   gjs_update_kernel      every 64 x 64 tile of A, one read-modify-write:
-//        i, j outside K : A_ij -= s_i sum_k W_ki R_kj                  (MFMA, rank nb)
-//        i in K, j out  : A_ij  = R_(i-k0) j
-//        i out, j in K  : A_ij  = -s_i R_(j-k0) i
-//        i, j in K      : A_ij  = P
-// instead of the seven (block inverse, three GEMMs, three copies) of the generic form.
-namespace {
-constexpr int GT = 64;          // tile = block width (NBL)
-constexpr int GK = 16;          // k chunk streamed through LDS
-constexpr int GS = GT + 16;     // [k][idx] LDS row stride (MFMA fragment reads conflict-free)
-
-// C_tile += op(X)[:, k-chunk] * Y[k-chunk, :] for a 64 x 64 tile, operands staged [k][idx]
-// in 16-deep chunks (20 KB of LDS: several workgroups per CU hide each other's latency).
-// Loads of chunk c+1 are issued before the MFMAs of chunk c; the mask / sign is applied at
-// the LDS store (after the MFMAs), so the loads stay in flight across them.
-template <typename PtrX, typename PtrY, typename MaskX, typename MaskY>
-__device__ __forceinline__ void gjs_tile_mma(double4_t (&acc)[2][2], int nk, PtrX px, PtrY py,
-                                             MaskX mx, MaskY my, double (*Xs)[GK][GS],
-                                             double (*Ys)[GK][GS]) {
-  constexpr int Q = GK * GT / 256;       // 4 elements of each operand per thread per chunk
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wm = w >> 1, wn = w & 1, li = lane & 15, lk = lane >> 4;
-  double xv[Q], yv[Q];
-  // raw loads from always-valid (clamped) addresses; nothing consumes them before the MFMAs
-  auto load = [&](int c) {
-#pragma unroll
-    for (int u = 0; u < Q; ++u) {
-      const int e = t + u * 256, k = c * GK + e / GT, i = e % GT;
-      xv[u] = *px(k, i);
-      yv[u] = *py(k, i);
-    }
-  };
-  auto store = [&](int c, int buf) {
-#pragma unroll
-    for (int u = 0; u < Q; ++u) {
-      const int e = t + u * 256, k = c * GK + e / GT, i = e % GT;
-      Xs[buf][e / GT][i] = xv[u] * mx(k, i);
-      Ys[buf][e / GT][i] = yv[u] * my(k, i);
-    }
-  };
-  load(0);
-  store(0, 0);
-  __syncthreads();
-  for (int c = 0; c < nk; ++c) {
-    const int cur = c & 1;
-    if (c + 1 < nk) load(c + 1);
-#pragma unroll
-    for (int k = 0; k < GK; k += 4) {
-      double a[2], bb[2];
-#pragma unroll
-      for (int x = 0; x < 2; ++x) a[x] = Xs[cur][k + lk][wm * 32 + x * 16 + li];
-#pragma unroll
-      for (int y = 0; y < 2; ++y) bb[y] = Ys[cur][k + lk][wn * 32 + y * 16 + li];
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int y = 0; y < 2; ++y) acc[x][y] = mfma_f64_16x16x4(a[x], bb[y], acc[x][y]);
-    }
-    if (c + 1 < nk) store(c + 1, cur ^ 1);
-    __syncthreads();
-  }
-}
-
-__global__ __launch_bounds__(256) void gjs_prep_kernel(const double* __restrict__ A, int n,
-                                                       int64_t sA, int k0, int nb,
-                                                       const double* __restrict__ Pbuf,
-                                                       double* __restrict__ Wbuf,
-                                                       double* __restrict__ Rbuf) {
-  __shared__ double Xs[2][GK][GS], Ys[2][GK][GS];
-  const int b = blockIdx.y, j0 = blockIdx.x * GT;
-  const double* Ab = A + (int64_t)b * sA;
-  const double* Pb = Pbuf + (int64_t)b * GT * GT;
-  double* Wb = Wbuf + (int64_t)b * GT * n;
-  double* Rb = Rbuf + (int64_t)b * GT * n;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wm = w >> 1, wn = w & 1, li = lane & 15;
-  // snapshot W = A[K, j0..j0+63] (row panel, coalesced)
-  for (int e = t; e < GT * GT; e += 256) {
-    const int k = e / GT, j = j0 + e % GT;
-    if (k < nb && j < n) Wb[(int64_t)k * n + j] = Ab[(int64_t)(k0 + k) * n + j];
-  }
-  double4_t acc[2][2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y) acc[x][y] = double4_t{0.0, 0.0, 0.0, 0.0};
-  // R = P W: X operand P^T[k][i] = P[i][k] (P symmetric: read P[k][i]), Y = W[k][j]
-  auto px = [&](int k, int i) { return Pb + min(k, nb - 1) * GT + min(i, nb - 1); };
-  auto py = [&](int k, int j) {
-    return Ab + (int64_t)(k0 + min(k, nb - 1)) * n + min(j0 + j, n - 1);
-  };
-  auto mx = [&](int k, int i) { return (k < nb && i < nb) ? 1.0 : 0.0; };
-  auto my = [&](int k, int j) { return (k < nb && j0 + j < n) ? 1.0 : 0.0; };
-  gjs_tile_mma(acc, (nb + GK - 1) / GK, px, py, mx, my, Xs, Ys);
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = wm * 32 + x * 16 + PFML_F64_CROW(lane, r);
-        const int j = j0 + wn * 32 + y * 16 + li;
-        if (i < nb && j < n) Rb[(int64_t)i * n + j] = acc[x][y][r];
-      }
-}
-
-__global__ __launch_bounds__(256) void gjs_update_kernel(double* __restrict__ A, int n, int64_t sA,
-                                                         int k0, int nb,
-                                                         const double* __restrict__ Pbuf,
-                                                         const double* __restrict__ Wbuf,
-                                                         const double* __restrict__ Rbuf) {
-  __shared__ double Xs[2][GK][GS], Ys[2][GK][GS];
-  const int tiles = (n + GT - 1) / GT;
-  const int b = blockIdx.y;
-  const int I0 = (blockIdx.x / tiles) * GT, J0 = (blockIdx.x % tiles) * GT;
-  double* Ab = A + (int64_t)b * sA;
-  const double* Pb = Pbuf + (int64_t)b * GT * GT;
-  const double* Wb = Wbuf + (int64_t)b * GT * n;
-  const double* Rb = Rbuf + (int64_t)b * GT * n;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int wm = w >> 1, wn = w & 1, li = lane & 15;
-  double4_t acc[2][2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y) acc[x][y] = double4_t{0.0, 0.0, 0.0, 0.0};
-  // A_ij -= s_i sum_k W_ki R_kj  (s_i = -1 on rows of eliminated blocks)
-  auto px = [&](int k, int i) { return Wb + (int64_t)min(k, nb - 1) * n + min(I0 + i, n - 1); };
-  auto py = [&](int k, int j) { return Rb + (int64_t)min(k, nb - 1) * n + min(J0 + j, n - 1); };
-  auto mx = [&](int k, int i) {
-    const int gi = I0 + i;
-    return (k < nb && gi < n) ? (gi < k0 ? -1.0 : 1.0) : 0.0;
-  };
-  auto my = [&](int k, int j) { return (k < nb && J0 + j < n) ? 1.0 : 0.0; };
-  gjs_tile_mma(acc, (nb + GK - 1) / GK, px, py, mx, my, Xs, Ys);
-  // epilogue: gather the old values first (one memory latency for the tile), then write
-  double old[2][2][4];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = min(I0 + wm * 32 + x * 16 + PFML_F64_CROW(lane, r), n - 1);
-        const int j = min(J0 + wn * 32 + y * 16 + li, n - 1);
-        old[x][y][r] = Ab[(int64_t)i * n + j];
-      }
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < 2; ++y)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = I0 + wm * 32 + x * 16 + PFML_F64_CROW(lane, r);
-        const int j = J0 + wn * 32 + y * 16 + li;
-        if (i >= n || j >= n) continue;
-        const bool ik = (i >= k0 && i < k0 + nb), jk = (j >= k0 && j < k0 + nb);
-        double v;
-        if (!ik && !jk) v = old[x][y][r] - acc[x][y][r];
-        else if (ik && !jk) v = Rb[(int64_t)(i - k0) * n + j];
-        else if (!ik && jk) v = (i < k0 ? 1.0 : -1.0) * Rb[(int64_t)(j - k0) * n + i];
-        else v = Pb[(i - k0) * GT + (j - k0)];
-        Ab[(int64_t)i * n + j] = v;
-      }
-}
-}  // namespace
-
-extern "C" int64_t pfml_spd_inverse_sym_work_doubles(int n, int batch) {
-  return (int64_t)batch * (GT * GT + 2LL * GT * n);
-}
-
-// In-place inverse of `batch` contiguous n x n SPD matrices (batch stride n*n) by the fused
-// symmetric block steps above.  status: set to 1 for a matrix that met a non-positive pivot.
-extern "C" hipError_t pfml_spd_inverse_sym(double* A, int n, int batch, double* work,
-                                           int* status, hipStream_t st) {
-  if (n <= 0 || batch <= 0) return hipSuccess;
-  const int64_t sA = (int64_t)n * n;
-  double* Pbuf = work;
-  double* Wbuf = Pbuf + (int64_t)batch * GT * GT;
-  double* Rbuf = Wbuf + (int64_t)batch * GT * n;
-  const int tiles = (n + GT - 1) / GT;
-  for (int k0 = 0; k0 < n; k0 += GT) {
-    const int nb = (n - k0 < GT) ? (n - k0) : GT;
-    hipLaunchKernelGGL(spd_blockinv_kernel<NBL>, dim3(batch), dim3(256), 0, st, A, (int64_t)n, sA,
-                       k0, nb, Pbuf, status);
-    hipLaunchKernelGGL(gjs_prep_kernel, dim3(tiles, batch), dim3(256), 0, st, A, n, sA, k0, nb,
-                       Pbuf, Wbuf, Rbuf);
-    hipLaunchKernelGGL(gjs_update_kernel, dim3(tiles * tiles, batch), dim3(256), 0, st, A, n, sA,
-                       k0, nb, Pbuf, Wbuf, Rbuf);
-  }
   return hipGetLastError();
 }

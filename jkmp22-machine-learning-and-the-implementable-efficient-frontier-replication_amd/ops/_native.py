@@ -51,9 +51,6 @@ def _declare_hip(lib):
     lib.pfml_lu_solve_work_doubles.argtypes = [I, I, I]
     lib.pfml_lu_solve_work_doubles.restype = L
     lib.pfml_lu_solve_max_n.restype = I
-    lib.pfml_spd_blockinv.argtypes = [P, L, L, I, I, I, P, P, P]
-    lib.pfml_spd_blockinv.restype = I
-    lib.pfml_spd_block_size.restype = I
     lib.pfml_ridge_set_timing.argtypes = [P]
     lib.pfml_ridge_set_timing.restype = None
     for name, argt in _EXTRA_HIP.items():

@@ -1,7 +1,9 @@
 """Batched dense linear algebra for the per-month PFML step.
 
-* ``spd_inverse``  - blocked Gauss-Jordan SPD inverse (csrc/spd_inverse.hip); matrices whose
-                     pivots are not positive fall back to a pivoted LU inverse (counted).
+* ``spd_inverse``  - SPD inverse (csrc/spd_inverse.hip): recursive Schur-complement form over
+                     64 x 64 register Gauss-Jordan leaves for n >= 160, blocked Gauss-Jordan
+                     below; matrices whose pivots are not positive fall back to a pivoted LU
+                     inverse (counted).
 * ``sqrtm_spd``    - principal square root by the scaled product-form Denman-Beavers
                      iteration (inverses + GEMMs only).  Replaces scipy.linalg.sqrtm (Schur,
                      General_functions.py:956): the argument sigma_hat^2 - 4I is symmetric PSD.
@@ -29,10 +31,8 @@ def spd_inverse_into(A: torch.Tensor, out: torch.Tensor, status: torch.Tensor) -
     """out = A^-1 for a device batch [B, n, n] of SPD matrices without modifying or copying A
     (the recursive form reads A and writes only ``out``); other forms copy A into out first.
     Non-positive pivots are flagged in ``status`` (no host sync)."""
-    import os
     B, n, _ = A.shape
-    if (nat.is_device(A) and n >= _BLOCKED_MIN_N and A.is_contiguous() and out.is_contiguous()
-            and os.environ.get("PFML_SPD_INV", SPD_INV_DEFAULT) == "recursive"):
+    if nat.is_device(A) and n >= _BLOCKED_MIN_N and A.is_contiguous() and out.is_contiguous():
         _spd_inverse_recursive(out, status, src=A)
         return out
     out.copy_(A)
@@ -43,7 +43,9 @@ def spd_inverse(A: torch.Tensor, inplace: bool = False,
                 status: torch.Tensor | None = None) -> torch.Tensor:
     """Inverse of a batch [B, n, n] of SPD matrices.
 
-    Device: blocked Gauss-Jordan (csrc/spd_inverse.hip).  With ``status`` (a [B] int32 device
+    Device: the recursive Schur-complement form for n >= 160 (GEMMs over register-resident
+    64 x 64 Gauss-Jordan leaves), blocked Gauss-Jordan below (csrc/spd_inverse.hip).  With
+    ``status`` (a [B] int32 device
     tensor) non-positive pivots are only flagged there - no host sync - and the caller repairs
     the flagged matrices once, after a whole chain of inverses (m_func); without it a flagged
     matrix is re-inverted by a pivoted LU here (one sync)."""
@@ -57,7 +59,7 @@ def spd_inverse(A: torch.Tensor, inplace: bool = False,
         lib = nat.hip_lib()
         st = status if status is not None else torch.zeros(B, dtype=torch.int32, device=X.device)
         if n >= _BLOCKED_MIN_N:
-            _spd_inverse_blocked(X, st)
+            _spd_inverse_recursive(X, st)
         else:
             work = torch.empty(lib.pfml_spd_inverse_work_doubles(n, B), dtype=torch.float64,
                                device=X.device)
@@ -78,18 +80,10 @@ def spd_inverse(A: torch.Tensor, inplace: bool = False,
 _BLOCKED_MIN_N = 160
 
 
-nat.register_hip("pfml_spd_blockinv128", [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int,
-                                          C.c_int, C.c_void_p, C.c_void_p, C.c_void_p])
-nat.register_hip("pfml_spd_inverse_sym", [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
-                                          C.c_void_p])
-nat.register_hip("pfml_spd_inverse_sym_work_doubles", [C.c_int, C.c_int], C.c_int64)
-nat.register_hip("pfml_spd_leafinv_inplace", [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int,
-                                              C.c_int, C.c_void_p, C.c_void_p])
 nat.register_hip("pfml_spd_leafinv_to", [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
                                          C.c_int64, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                          C.c_void_p])
 
-SPD_INV_DEFAULT = "recursive"
 _REC_LEAF = 64
 _REC_BUFS: dict = {}
 
@@ -155,50 +149,6 @@ def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor,
                    beta=1.0)                                                  # X11 -= X12 W'
 
     rec(0, n, 0, X if src is None else src)
-
-
-def _spd_inverse_blocked(X: torch.Tensor, status: torch.Tensor) -> None:
-    """In-place SPD inverse by 64-wide Gauss-Jordan block steps: the pivot block inverted in
-    LDS (csrc/spd_inverse.hip), row panel, rank-64 trailing update and column panel on the
-    fused fp64 MFMA GEMM (csrc/gemm_f64.hip).  Measured on [256, 490, 490]
-    (tools/bench_inverse.py, profiles/r02_inverse_variants_v2.json): 4.70 ms (12.8 TF/s); the
-    fused sign-symmetric 3-launch form (PFML_SPD_INV=sym, pfml_spd_inverse_sym) 4.83 ms and
-    128-wide blocks (PFML_SPD_INV=generic128) 6.0 ms - the rank-64 update pass is
-    bandwidth/latency-bound in every form."""
-    import os
-    lib = nat.hip_lib()
-    B, n, _ = X.shape
-    mode = os.environ.get("PFML_SPD_INV", SPD_INV_DEFAULT)
-    if mode == "recursive":
-        _spd_inverse_recursive(X, status)
-        return
-    if mode == "sym":
-        work = torch.empty(lib.pfml_spd_inverse_sym_work_doubles(n, B), dtype=torch.float64,
-                           device=X.device)
-        nat.check(lib.pfml_spd_inverse_sym(X.data_ptr(), n, B, work.data_ptr(),
-                                           status.data_ptr(), nat.stream_of(X)),
-                  "pfml_spd_inverse_sym")
-        return
-    NB = 128 if mode == "generic128" else lib.pfml_spd_block_size()
-    blockinv = lib.pfml_spd_blockinv128 if NB == 128 else lib.pfml_spd_blockinv
-    dev = X.device
-    P = torch.empty((B, NB, NB), dtype=torch.float64, device=dev)
-    Cbuf = torch.empty((B, n, NB), dtype=torch.float64, device=dev)
-    Rbuf = torch.empty((B, NB, n), dtype=torch.float64, device=dev)
-    st = nat.stream_of(X)
-    for k0 in range(0, n, NB):
-        nb = min(NB, n - k0)
-        nat.check(blockinv(X.data_ptr(), n, n * n, B, k0, nb, P.data_ptr(), status.data_ptr(),
-                           st), "pfml_spd_blockinv")
-        Pk = P[:, :nb, :nb]
-        R = Rbuf[:, :nb, :]
-        gemm_fused(Pk, X[:, k0:k0 + nb, :], R)                   # R = P A_k.
-        C = Cbuf[:, :, :nb]
-        C.copy_(X[:, :, k0:k0 + nb])                             # old column panel
-        gemm_fused(C, R, X, alpha=-1.0, beta=1.0)                # A -= C R   (rank nb)
-        X[:, k0:k0 + nb, :] = R                                  # block rows
-        gemm_fused(C, Pk, X[:, :, k0:k0 + nb], alpha=-1.0)       # block columns: -C P
-        X[:, k0:k0 + nb, k0:k0 + nb] = Pk
 
 
 def _lu_max_n() -> int:
