@@ -1194,7 +1194,7 @@ constexpr int NBW = (BNMAX / 16 + NWB - 1) / NWB;   // row blocks per wave
 
 __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
     const RidgeCellDesc* __restrict__ cells, int ncells, int L, double* __restrict__ work,
-    double* __restrict__ beta_out, int64_t ldo) {
+    double* __restrict__ beta_out, int64_t ldo, const unsigned* __restrict__ syncw) {
   __shared__ double red[2][NWB][BB * BB];
   __shared__ double Vw[NWB][NBW][BB][LS];         // wave-private V_b images (transpose)
   // (the chunks of a cell are adjacent in dispatch order, so they run together and share
@@ -1218,13 +1218,16 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
     double* __restrict__ o = beta_out + cd.out + (int64_t)l0 * ldo + n;
     for (int e = threadIdx.x; e < lc * pad; e += NTB) o[(int64_t)(e / pad) * ldo + e % pad] = 0.0;
   }
+  // a cell whose cooperative reduction timed out (its error word, CoopSync) gets NaN betas:
+  // the grid search's non-finite-cell recovery then recomputes it (never silent garbage)
+  const bool failed = syncw != nullptr && syncw[(int64_t)cell * COOP_SYNC + 1] != 0u;
   double4_t Y[NBW];
 #pragma unroll
   for (int q = 0; q < NBW; ++q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = 16 * (wid + NWB * q) + g4 + 4 * r;
-      Y[q][r] = (lok && i < n) ? yc[i] : 0.0;
+      Y[q][r] = (lok && i < n) ? (failed ? __builtin_nan("") : yc[i]) : 0.0;
     }
   // va[q][r] = V_p[16 b - r0 + 4 r + g4][c16] for the live blocks b = wid + 8 q of panel p
   const int lda = band_npad(n);                   // A's leading dimension (padded)
@@ -1416,6 +1419,6 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   }
   const int nch = (L + LC - 1) / LC;
   hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3(ncells * nch), dim3(NTB), 0, st, cd,
-                     ncells, L, work, beta_out, ldo);
+                     ncells, L, work, beta_out, ldo, syncw);
   return hipGetLastError();
 }

@@ -332,11 +332,24 @@ def coop_wgmap(k: np.ndarray) -> np.ndarray:
 _NCU: dict = {}
 
 
+def ranks_per_device() -> int:
+    """Processes of this node sharing one device (torchrun's LOCAL_WORLD_SIZE over the visible
+    devices, ranks placed LOCAL_RANK mod device_count): 1 on an N-GPU node with one rank per
+    GPU, W in the one-GPU multi-process rehearsal."""
+    lw = int(os.environ.get("LOCAL_WORLD_SIZE", "1"))
+    nd = max(1, torch.cuda.device_count())
+    return max(1, -(-lw // nd))
+
+
 def num_cus(dev) -> int:
+    """CUs this process may count on for the cooperative reduction: the device's, split among
+    the processes that share it.  A cooperative cell's K workgroups wait for each other, so
+    they must be co-resident; several processes each filling the whole chip with spinning
+    workgroups would starve each other (their cells time out)."""
     key = str(dev)
     if key not in _NCU:
         _NCU[key] = int(torch.cuda.get_device_properties(dev).multi_processor_count)
-    return _NCU[key]
+    return max(1, _NCU[key] // ranks_per_device())
 
 
 def ridge_plan(P: int, L: int, cell_src, cell_n, cell_scale, ncu: int = 256,
