@@ -56,7 +56,10 @@ struct BandWork {
     z = LB + (int64_t)n * LS;                // Q^T rbar
     T = z + n;                               // np x 16 x 16 compact-WY T_p
     Yt = T + (int64_t)np * BB * BB;          // L x n   solutions y_l, then beta_l
-    Lf = Yt + (int64_t)L * n;                // L x n x LS banded Cholesky factors
+    // banded Cholesky factors: L x n x 16 sub-diagonal entries (one 128-byte line per row,
+    // the base rounded up to 16 doubles: every row is written whole by one store
+    // instruction), then L x n inverse diagonals
+    Lf = w + ((((Yt - w) + (int64_t)L * n) + 15) & ~(int64_t)15);
     F = Lf + (int64_t)L * n * LS;            // cooperative hand-off scratch (CoopWork)
   }
 };
@@ -905,7 +908,8 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
   const int lc = lv ? l : L - 1;                 // padding rows redo the last lambda, no stores
   BandWork bw(work + cd.work, n, L);
   const double lam = lvec[lc];
-  double* Lrow = bw.Lf + (int64_t)lc * n * LS;
+  double* Lrow = bw.Lf + (int64_t)lc * n * BB;   // row j: l_{j+1..j+16, j}
+  double* Linv = bw.Lf + (int64_t)L * n * BB + (int64_t)lc * n;
   double* yl = bw.Yt + (int64_t)lc * n;
   const double* LB = bw.LB;                      // row-major band: LB[r][s] = B[r][r-16+s]
   const double* z = bw.z;
@@ -960,9 +964,8 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
       const double yj = zpiv * inv;
       const double lval = w[u] * inv;            // l_i, i = (p - u) mod 16, pivot lane: i = 16
       if (lv && j < n) {                         // uniform branch
-        double* lr = Lrow + (int64_t)j * LS;
-        lr[pl ? BB : ((p - u) & 15)] = lval;
-        lr[0] = inv;                             // same value from all 16 lanes
+        Lrow[(int64_t)j * BB + (pl ? BB - 1 : ((p - u) & 15) - 1)] = lval;
+        Linv[j] = inv;                           // same value from all 16 lanes
         yl[j] = yj;
       }
       zr -= lval * yj;
@@ -992,8 +995,8 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
       const int j = jt - v;
       const int i = (p - u) & 15;
       const bool in = j < n;
-      pli[v] = in ? Lrow[(int64_t)j * LS + (i == 0 ? BB : i)] : 0.0;
-      pinv[v] = in ? Lrow[(int64_t)j * LS] : 1.0;
+      pli[v] = in ? Lrow[(int64_t)j * BB + (i == 0 ? BB - 1 : i - 1)] : 0.0;
+      pinv[v] = in ? Linv[j] : 1.0;
       py[v] = in ? yl[j] : 0.0;
     });
     static_for<0, 8>([&](auto V) {
@@ -1322,7 +1325,7 @@ extern "C" int64_t pfml_ridge_band_work_doubles(int n, int L) {
   const int64_t npad = band_npad(n);
   // F region: the cooperative hand-off scratch (CoopWork)
   const int64_t coop = 2LL * npad * BB + BB * BB + (int64_t)(BNMAX / BB) * (BB * BB + BB);
-  return npad * npad + (int64_t)n * LS + n + np * BB * BB + (int64_t)L * n +
+  return npad * npad + (int64_t)n * LS + n + np * BB * BB + (int64_t)L * n + 15 +
          (int64_t)L * n * LS + coop;
 }
 
