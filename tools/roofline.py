@@ -7,9 +7,10 @@ Ceilings measured on MI355X (profiles/r03_mfma_f64_peak_v2.json): fp64 MFMA 78.2
 65.7 TF/s; HBM3E 8 TB/s (spec).  Flop / byte counts are the work each kernel executes for the
 headline config (2 g x 53 years, n = 513 / 257 / 129 / 65, 101 lambdas, 12 validation months,
 710 months of 513 x 513 summands); the 106 big cells' reduction runs on 106 of 256 CUs, so
-its per-CU efficiency is quoted too.
+its per-CU efficiency is quoted too.  (The reduction kernel is band_coop_kernel; its two
+launches - the big cells' and the rest - are told apart by their queues.)
 
-usage: python tools/roofline.py profiles/r03_step_timeline_v1.txt > profiles/r03_roofline_grid_step.md
+usage: python tools/roofline.py profiles/r04_step_timeline.txt > profiles/r04_roofline_grid_step.md
 """
 import re
 import sys
@@ -36,10 +37,11 @@ def bt_flops(ns):                       # blocked-WY back-transform: 4 n^2 per l
 
 
 def quad_flops(ns):                     # upper block triangle, 64-row tiles, 112 padded lambdas
-    tot = 0.0
+    tot = 0.0                           # (the tail index of n = 64k + 1 is off the tiles)
     for n in ns:
-        nt = (n + 63) // 64
-        k = sum(n - 64 * i for i in range(nt))
+        nm = n - 1 if (n > 1 and (n - 1) % 16 == 0) else n
+        nt = (nm + 63) // 64
+        k = sum(nm - 64 * i for i in range(nt))
         tot += G * Y * NV * 2.0 * 64 * 112 * k
     return tot
 
@@ -60,7 +62,7 @@ def main():
     by = {}
     for name, q, a, b, d in step:
         key = name.split("<")[0].split("(")[0]
-        if key.startswith("ridge_band_reduce"):
+        if key.startswith("band_coop_kernel"):
             key = "ridge_band_reduce_kernel"
         by.setdefault(key, []).append((q, d))
     red = by.get("ridge_band_reduce_kernel", [])
