@@ -36,8 +36,18 @@ import os
 import sys
 import time
 
+import logging
+
 import numpy as np
 import torch
+
+# the engine's stage logs go to stderr here: stdout carries the one JSON result line only
+if not logging.getLogger("pfml").handlers:
+    _h = logging.StreamHandler(sys.stderr)
+    _h.setFormatter(logging.Formatter("[%(name)s] %(message)s"))
+    logging.getLogger("pfml").addHandler(_h)
+    logging.getLogger("pfml").setLevel(os.environ.get("PFML_LOGLEVEL", "INFO"))
+    logging.getLogger("pfml").propagate = False
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
