@@ -155,6 +155,9 @@ def test_bench_contract_two_ranks_gloo(tmp_path):
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=str(tmp_path),
                        env=env)
     assert r.returncode == 0, r.stderr[-3000:]
+    # stdout: the JSON line (the engine's logs go to stderr; gloo's own connect messages,
+    # printed by its C++ layer, are the only other stdout lines)
+    assert "[pfml." not in r.stdout
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
