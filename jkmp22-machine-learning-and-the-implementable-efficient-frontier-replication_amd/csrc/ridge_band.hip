@@ -335,8 +335,10 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
 // a fixed block order.  So a 1-GPU and an N-GPU grid search pick the same hyper-parameters
 // (PFML_hp_reals.py:118-122 dense rank, PFML_best_hps.py:275 first rank).
 //
-// Work units are 16-row blocks of the trailing matrix A22 (lower-triangle semantics; every
-// off-diagonal tile is mirrored).  Per panel p:
+// Work units are 16-row blocks of the trailing matrix A22, of which only the LOWER block
+// triangle (diagonal tiles whole) is stored: the update writes no mirror tiles and the X phase
+// reads column block I above its first row from row block I (dsytrd 'L' semantics: the
+// input's upper triangle is never read).  Per panel p:
 //
 //   B  every WG   U = V_p T_p (LDS), X_I = A22 U for the blocks I = gb (mod K) it owns in the
 //                 X phase (gb = global block), partials V_I' X_I and V_I' z_I per block
@@ -423,16 +425,24 @@ __device__ __forceinline__ void coop_x_accum(const double* __restrict__ A, int l
                                              int m, const int (&blk)[4], int c16, int g4,
                                              const double (*__restrict__ Us)[LS],
                                              double4_t (&X)[4]) {
-  int col[NQ];
+  // Only the LOWER triangle of A22 is kept (the update writes no mirror tiles): element
+  // (kk, i) of column block I is A[kk][i] for rows kk at or below the block's first row and
+  // A[i][kk] above it - the same value a mirrored copy held, read from the lower triangle
+  int col[NQ], top[NQ];
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) col[q] = min(blk[q] * 16 + c16, m - 1);
+  for (int q = 0; q < NQ; ++q) {
+    col[q] = min(blk[q] * 16 + c16, m - 1);
+    top[q] = blk[q] * 16;
+  }
   for (int k = 0; k < m; k += 32) {
     double a[8][NQ], b[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const double* arow = A + (int64_t)(r0 + min(k + 4 * u + g4, m - 1)) * lda + r0;
+      const int kk = min(k + 4 * u + g4, m - 1);
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) a[u][q] = arow[col[q]];
+      for (int q = 0; q < NQ; ++q)
+        a[u][q] = (kk >= top[q]) ? A[(int64_t)(r0 + kk) * lda + r0 + col[q]]
+                                 : A[(int64_t)(r0 + col[q]) * lda + r0 + kk];
       b[u] = Us[k + 4 * u + g4][c16];
     }
 #pragma unroll
@@ -502,13 +512,15 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
   }
   if (t_ == 0) err_s = 0;
 
-  // ---- A = S * scale (both triangles, zero padding), z = r * scale: row blocks gb = w (mod K)
+  // ---- A = S * scale (the lower block triangle incl. the diagonal blocks, zero padding),
+  //      z = r * scale: row blocks gb = w (mod K)
   {
     const double* S = SD + cd.src;
     const double sc = cd.scale;
     for (int gb = w; gb < nb; gb += K) {
-      for (int e = t_; e < BB * (lda / 2); e += NTR) {
-        const int i = 16 * gb + e / (lda / 2), j = 2 * (e % (lda / 2));
+      const int wc = 8 * (gb + 1);                 // column pairs through the diagonal block
+      for (int e = t_; e < BB * wc; e += NTR) {
+        const int i = 16 * gb + e / wc, j = 2 * (e % wc);
         const double* srow = S + (int64_t)min(i, n - 1) * ldS;
         const double x = (i < n && j < n) ? srow[j] * sc : 0.0;
         const double y = (i < n && j + 1 < n) ? srow[j + 1] * sc : 0.0;
@@ -764,14 +776,6 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
               const int row = pr + 8 * h;
               const double2 v = *reinterpret_cast<const double2*>(&tw[row * BB + (pc ^ (row & ~1))]);
               st2((unsigned)(((r0 + 16 * ci + row) * lda + r0 + 16 * J + pc) * 8), live, v.x, v.y);
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const int col = pr + 8 * h;
-              const double x = tw[pc * BB + (col ^ (pc & ~1))];
-              const double y = tw[(pc + 1) * BB + (col ^ ((pc + 1) & ~1))];
-              st2((unsigned)(((r0 + 16 * J + col) * lda + r0 + 16 * ci + pc) * 8),
-                  live && J != ci, x, y);
             }
           }
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
