@@ -969,8 +969,10 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
       const double lval = w[u] * inv;            // l_i, i = (p - u) mod 16, pivot lane: i = 16
       if (lv && j < n) {                         // uniform branch
         Lrow[(int64_t)j * BB + (pl ? BB - 1 : ((p - u) & 15) - 1)] = lval;
-        Linv[j] = inv;                           // same value from all 16 lanes
-        yl[j] = yj;
+        if (p == 0) {                            // one lane per row: 16 same-address stores
+          Linv[j] = inv;                         // of a row group are not merged (measured:
+          yl[j] = yj;                            // WRITE_SIZE twice the factor's bytes)
+        }
       }
       zr -= lval * yj;
       const double nl = -lval;

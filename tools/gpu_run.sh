@@ -105,6 +105,12 @@ for step in ${MODE//,/ }; do
       done
       PFML_BENCH_CELLS=1,13,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/coop_cells.log 2>&1
       rc=$?; tail -1 $OUT/coop_cells.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    abmm)
+      # utilities: one vs two validation months per workgroup (shared beta tiles), A/B/A/B
+      for mm in 1 2 1 2; do
+        PFML_QUAD_MM=$mm timeout -k 10 200 python bench.py > $OUT/bench_mm$mm.json 2> $OUT/bench_mm$mm.err
+        rc=$?; echo "mm $mm: $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_mm$mm.json)"; if [ $rc -ne 0 ]; then tail -5 $OUT/bench_mm$mm.err; exit $rc; fi
+      done ;;
     timeline)
       # kernel timeline of the last full 1-GPU grid step
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/prof1 -o run -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-inputs > $OUT/prof1.log 2>&1)
