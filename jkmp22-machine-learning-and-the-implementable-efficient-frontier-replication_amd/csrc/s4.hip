@@ -5,8 +5,7 @@
 // are symmetric in exact arithmetic; the reference symmetrises nothing, so rounding-level
 // asymmetry is removed here once per pass instead of by extra torch passes).  Every kernel
 // processes a 32 x 32 tile (I, J) and its mirror (J, I) through LDS, so one launch reads each
-// operand once and writes the symmetric result with coalesced stores (one workgroup per tile
-// pair, see mfunc_sym_kernel):
+// operand once and writes the symmetric result with coalesced stores:
 //
 //   MF_X      x    = s a_i a_j sym(Sigma)_ij                    (Lemma 1: w^-1 L^-1/2 gS L^-1/2)
 //   MF_FIX    Aq   = x + diag(y) - sym(mt) o sigma_gr           (the fixed-point argument, Q6)
@@ -39,79 +38,53 @@ struct MfArgs {
   double d;                       // diagonal add (SHAT)
 };
 
-// One workgroup per tile PAIR (I, J), I <= J, of the upper block triangle: both tiles of each
-// operand are read once (coalesced rows), the symmetric value is formed once and written to
-// (I, J) directly and to (J, I) through an LDS transpose - every element is read once per
-// operand and written once (a workgroup per tile, each reading its mirror too, read every
-// element twice).  The values are bitwise those of the per-tile form: the mirror element's
-// sums are the same two addends (fp addition commutes) and the scalings are symmetric.
+// (A form with one workgroup per tile PAIR - every element read once per operand, the mirror
+// written through an LDS transpose - measured slower: 27.6 vs 25.7 ms per S4 run, the
+// mirror tile's second read hits L2 and the pair form halves the workgroups.)
 __global__ __launch_bounds__(256) void mfunc_sym_kernel(MfArgs p) {
-  __shared__ double xa[TS][TS + 1], xb[TS][TS + 1], ya[TS][TS + 1], yb[TS][TS + 1];
+  __shared__ double tx[TS][TS + 1], ty[TS][TS + 1];
   const int tiles = (p.N + TS - 1) / TS;
   const int b = blockIdx.y;
-  int I = 0, k = blockIdx.x;                    // pair index -> (I, J), J >= I
-  while (k >= tiles - I) { k -= tiles - I; ++I; }
-  const int J = I + k;
-  const bool diag = I == J;
-  const int I0 = I * TS, J0 = J * TS;
+  const int I0 = (blockIdx.x / tiles) * TS, J0 = (blockIdx.x % tiles) * TS;
   const int tx_ = threadIdx.x & 31, ty_ = threadIdx.x >> 5;   // 32 x 8
   const double* X = p.X + (int64_t)b * p.sX;
   const double* Y = p.Y ? p.Y + (int64_t)b * p.sX : nullptr;
   double* O = p.out + (int64_t)b * p.sX;
-  // xa[r][c] = X[I0 + r][J0 + c], xb[r][c] = X[J0 + r][I0 + c] (same for Y)
+  // mirror tile (J0.., I0..) into LDS transposed: tx[r][c] = X[J0 + c][I0 + r]
   for (int r = ty_; r < TS; r += 8) {
-    const int ia = I0 + r, ja = J0 + tx_;
-    const bool oka = ia < p.N && ja < p.N;
-    xa[r][tx_] = oka ? X[(int64_t)ia * p.ld + ja] : 0.0;
-    if (Y) ya[r][tx_] = oka ? Y[(int64_t)ia * p.ld + ja] : 0.0;
-    if (!diag) {
-      const int ib = J0 + r, jb = I0 + tx_;
-      const bool okb = ib < p.N && jb < p.N;
-      xb[r][tx_] = okb ? X[(int64_t)ib * p.ld + jb] : 0.0;
-      if (Y) yb[r][tx_] = okb ? Y[(int64_t)ib * p.ld + jb] : 0.0;
-    }
+    const int gi = J0 + r, gj = I0 + tx_;
+    const bool ok = gi < p.N && gj < p.N;
+    tx[tx_][r] = ok ? X[(int64_t)gi * p.ld + gj] : 0.0;
+    if (Y) ty[tx_][r] = ok ? Y[(int64_t)gi * p.ld + gj] : 0.0;
   }
   __syncthreads();
-  double (*mx)[TS + 1] = diag ? xa : xb;         // the mirror tile
-  double (*my)[TS + 1] = diag ? ya : yb;
   const double s = p.svec ? p.svec[b] : 0.0;
   const double c = p.cvec ? p.cvec[b] : 1.0;
   const double* av = p.a ? p.a + (int64_t)b * p.sv : nullptr;
   const double* mv = p.mask ? p.mask + (int64_t)b * p.sv : nullptr;
-  double v[TS / 8];
-#pragma unroll
-  for (int q = 0; q < TS / 8; ++q) {
-    const int r = ty_ + 8 * q;
+  for (int r = ty_; r < TS; r += 8) {
     const int i = I0 + r, j = J0 + tx_;
-    const double xs = 0.5 * (xa[r][tx_] + mx[tx_][r]);
-    const double ys = Y ? 0.5 * (ya[r][tx_] + my[tx_][r]) : 0.0;
-    double w = 0.0;
+    if (i >= p.N || j >= p.N) continue;
+    const int64_t o = (int64_t)i * p.ld + j;
+    const double xs = 0.5 * (X[o] + tx[r][tx_]);
+    const double ys = Y ? 0.5 * (Y[o] + ty[r][tx_]) : 0.0;
+    double v;
     if (p.mode == MF_X) {
-      w = s * (av[min(i, p.N - 1)] * av[min(j, p.N - 1)]) * xs;
+      v = s * (av[i] * av[j]) * xs;
     } else if (p.mode == MF_FIX) {
       const double ic2 = 1.0 / (c * c);
-      const double mm = mv[min(i, p.N - 1)] * mv[min(j, p.N - 1)];
-      w = xs * (s * (av[min(i, p.N - 1)] * av[min(j, p.N - 1)]) - ys * ic2) - ys * mm;
-      if (i == j) w += 1.0 + mm + xs * ic2;
+      const double mm = mv[i] * mv[j];
+      v = xs * (s * (av[i] * av[j]) - ys * ic2) - ys * mm;
+      if (i == j) v += 1.0 + mm + xs * ic2;
     } else if (p.mode == MF_DB) {
       const double mu2 = s * s;
-      w = 0.25 * (mu2 * xs + ys / mu2);
-      if (i == j) w += 0.5;
+      v = 0.25 * (mu2 * xs + ys / mu2);
+      if (i == j) v += 0.5;
     } else {
-      w = xs + ys;
-      if (i == j) w += p.d;
+      v = xs + ys;
+      if (i == j) v += p.d;
     }
-    v[q] = w;
-    if (i < p.N && j < p.N) O[(int64_t)i * p.ld + j] = w;
-  }
-  if (diag) return;
-  __syncthreads();                               // every mirror read of xa is done
-#pragma unroll
-  for (int q = 0; q < TS / 8; ++q) xa[ty_ + 8 * q][tx_] = v[q];
-  __syncthreads();
-  for (int r = ty_; r < TS; r += 8) {            // (J0 + r, I0 + c) = value (I0 + c, J0 + r)
-    const int i = J0 + r, j = I0 + tx_;
-    if (i < p.N && j < p.N) O[(int64_t)i * p.ld + j] = xa[tx_][r];
+    O[o] = v;
   }
 }
 
@@ -181,7 +154,7 @@ extern "C" hipError_t pfml_mfunc_sym(const PfmlMfArgs* h, hipStream_t st) {
   MfArgs p{h->mode, h->B, h->N, h->ld, h->sX, h->X, h->Y, h->out, h->svec, h->cvec, h->a,
            h->mask, h->sv, h->d};
   const int tiles = (h->N + TS - 1) / TS;
-  hipLaunchKernelGGL(mfunc_sym_kernel, dim3(tiles * (tiles + 1) / 2, h->B), dim3(256), 0, st, p);
+  hipLaunchKernelGGL(mfunc_sym_kernel, dim3(tiles * tiles, h->B), dim3(256), 0, st, p);
   return hipGetLastError();
 }
 
