@@ -84,7 +84,9 @@ for step in ${MODE//,/ }; do
         rc=$?; grep -E '"(X_partials|C_sums_W|update|lookahead_qr|U|sync_wait|end_sync)"|total' $OUT/coop_timing_k$k.json; if [ $rc -ne 0 ]; then cat $OUT/coop_timing_k$k.json; exit $rc; fi
       done
       PFML_BENCH_CELLS=1,13,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/coop_cells.log 2>&1
-      rc=$?; tail -1 $OUT/coop_cells.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+      rc=$?; tail -1 $OUT/coop_cells.log; if [ $rc -ne 0 ]; then exit $rc; fi
+      PFML_COOP_K=1 PFML_BENCH_CELLS=1,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/coop_cells_k1.log 2>&1
+      rc=$?; tail -1 $OUT/coop_cells_k1.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     benchk)
       # headline bench with the cooperative reduction at auto K and at K = 1 (every cell one WG)
       for k in auto 1; do
