@@ -422,66 +422,34 @@ struct CoopSync {
 // explicit block list).
 template <int NQ>
 __device__ __forceinline__ void coop_x_accum(const double* __restrict__ A, int lda, int r0,
-                                             int m, const int (&blk)[4], int lane,
+                                             int m, const int (&blk)[4], int c16, int g4,
                                              const double (*__restrict__ Us)[LS],
-                                             double* __restrict__ lt, double4_t (&X)[4]) {
-  // X_I += A22[k][I cols] U[k][:] for the NQ column blocks I of this wave.  Only the LOWER
-  // block triangle of A22 is stored (the update writes no mirror tiles): rows k at or below
-  // the block's first row are read as they are (128 B contiguous per row), and a 32-row
-  // chunk entirely ABOVE the block comes from row block I instead - its 16 rows x 32
-  // columns loaded with whole-line reads into the wave-private 16 x 16 LDS tile `lt`
-  // (rows rotated by the row index: conflict-free transposed reads), read back as the
-  // MFMA operand.  Same values, same order as a mirrored copy would give.
-  const int c16 = lane & 15, g4 = lane >> 4;
+                                             double4_t (&X)[4]) {
+  // Only the LOWER triangle of A22 is kept (the update writes no mirror tiles): element
+  // (kk, i) of column block I is A[kk][i] for rows kk at or below the block's first row and
+  // A[i][kk] above it - the same value a mirrored copy held, read from the lower triangle
   int col[NQ], top[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     col[q] = min(blk[q] * 16 + c16, m - 1);
     top[q] = blk[q] * 16;
   }
-  const int sr = lane >> 2, sc = (lane & 3) * 4;     // staging: row sr, columns sc .. sc + 3
   for (int k = 0; k < m; k += 32) {
-    double b[8];
+    double a[8][NQ], b[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) b[u] = Us[k + 4 * u + g4][c16];
+    for (int u = 0; u < 8; ++u) {
+      const int kk = min(k + 4 * u + g4, m - 1);
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      double a[8];                                   // (per block: 8 operands live, not 8 NQ)
-      if (k + 32 <= top[q]) {                        // wave-uniform
-        const double* srow = A + (int64_t)(r0 + min(top[q] + sr, m - 1)) * lda + r0 + k + sc;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const double2 v0 = *reinterpret_cast<const double2*>(srow + 16 * h);
-          const double2 v1 = *reinterpret_cast<const double2*>(srow + 16 * h + 2);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          lt[sr * BB + ((sc + 0 + sr) & 15)] = v0.x;
-          lt[sr * BB + ((sc + 1 + sr) & 15)] = v0.y;
-          lt[sr * BB + ((sc + 2 + sr) & 15)] = v1.x;
-          lt[sr * BB + ((sc + 3 + sr) & 15)] = v1.y;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-          for (int uu = 0; uu < 4; ++uu)
-            a[4 * h + uu] = lt[c16 * BB + ((4 * uu + g4 + c16) & 15)];
-        }
-      } else {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int kk = min(k + 4 * u + g4, m - 1);
-          a[u] = (kk >= top[q]) ? A[(int64_t)(r0 + kk) * lda + r0 + col[q]]
-                                : A[(int64_t)(r0 + col[q]) * lda + r0 + kk];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) X[q] = mfma_f64_16x16x4(a[u], b[u], X[q]);
+      for (int q = 0; q < NQ; ++q)
+        a[u][q] = (kk >= top[q]) ? A[(int64_t)(r0 + kk) * lda + r0 + col[q]]
+                                 : A[(int64_t)(r0 + col[q]) * lda + r0 + kk];
+      b[u] = Us[k + 4 * u + g4][c16];
     }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) X[q] = mfma_f64_16x16x4(a[u][q], b[u], X[q]);
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // lt free for the next user
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 template <bool TIMED>
@@ -626,10 +594,10 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
 #pragma unroll
     for (int q = 0; q < 4; ++q) X[q] = double4_t{0.0, 0.0, 0.0, 0.0};
     switch (nq) {
-      case 1: coop_x_accum<1>(A, lda, r0, m, blk, lane, Ws, &red[wid][0], X); break;
-      case 2: coop_x_accum<2>(A, lda, r0, m, blk, lane, Ws, &red[wid][0], X); break;
-      case 3: coop_x_accum<3>(A, lda, r0, m, blk, lane, Ws, &red[wid][0], X); break;
-      case 4: coop_x_accum<4>(A, lda, r0, m, blk, lane, Ws, &red[wid][0], X); break;
+      case 1: coop_x_accum<1>(A, lda, r0, m, blk, c16, g4, Ws, X); break;
+      case 2: coop_x_accum<2>(A, lda, r0, m, blk, c16, g4, Ws, X); break;
+      case 3: coop_x_accum<3>(A, lda, r0, m, blk, c16, g4, Ws, X); break;
+      case 4: coop_x_accum<4>(A, lda, r0, m, blk, c16, g4, Ws, X); break;
       default: break;
     }
     // per-block partials V_I' X_I and V_I' z_I (z as column 0 of the B operand)
