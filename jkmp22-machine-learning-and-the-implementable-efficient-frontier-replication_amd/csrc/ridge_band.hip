@@ -123,6 +123,31 @@ __device__ __forceinline__ double rcp_f64(double x) {
   return y;
 }
 
+// w[U + s] = LDS row at byte address `base` (s = 0 .. LS-1), as 17 ds_read_b64 straight into
+// the window registers ("+v": the exec-masked lanes keep their values, so no merge copies), and
+// NO wait: the caller overlaps the loads with independent work and then calls lds_row_wait<U>,
+// which waits for them and ties the same registers, so no read of w[U..U+16] can be scheduled
+// between the two.  (Written in plain C++ the compiler issued the loads into temporaries, waited
+// for them at once and merged them with 14 masked moves: the LDS latency sat on every step.)
+template <int U, int S = 0>
+__device__ __forceinline__ void lds_row_issue(double* w, unsigned base) {
+  if constexpr (S < LS) {
+    // ("memory": the stage_rows stores into LBs are only read here)
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "+v"(w[U + S]) : "v"(base), "i"(8 * S)
+                 : "memory");
+    lds_row_issue<U, S + 1>(w, base);
+  }
+}
+
+template <int U>
+__device__ __forceinline__ void lds_row_wait(double* w) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(w[U]), "+v"(w[U + 1]), "+v"(w[U + 2]), "+v"(w[U + 3]), "+v"(w[U + 4]),
+                 "+v"(w[U + 5]), "+v"(w[U + 6]), "+v"(w[U + 7]), "+v"(w[U + 8]),
+                 "+v"(w[U + 9]), "+v"(w[U + 10]), "+v"(w[U + 11]), "+v"(w[U + 12]),
+                 "+v"(w[U + 13]), "+v"(w[U + 14]), "+v"(w[U + 15]), "+v"(w[U + 16]));
+}
+
 __device__ __forceinline__ double row16_sum(double v) {
   v += dpp_mov<0xB1>(v);      // quad_perm [1,0,3,2]
   v += dpp_mov<0x4E>(v);      // quad_perm [2,3,0,1]
@@ -925,6 +950,8 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
   // block ahead (double buffer, one barrier per block) and each lane reads its row at the
   // block start, instead of a second 17-register prefetch per lane (occupancy: VGPRs).
   __shared__ double LBs[2][BB][LS];
+  // LDS byte offset of LBs (the low word of its flat address)
+  const unsigned lbs_base = (unsigned)reinterpret_cast<uintptr_t>(&LBs[0][0][0]);
   const int npad = (n + 15) & ~15;
   double w[2 * BB];
   auto stage_rows = [&](int r0s, int buf) {       // rows r0s .. r0s + 15 -> LBs[buf]
@@ -957,15 +984,17 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
       const bool pl = (p == u);                  // pivot lane: holds row j, takes row j+16
       const double piv = row_bcast<u>(w[u]);
       const double zpiv = row_bcast<u>(zr);      // (read before the pivot lane's zr changes)
-      if (pl) {                                  // exec-masked LDS reads straight into the
-#pragma unroll                                   // window (no VALU moves), in flight during
-        for (int s = 0; s < LS; ++s) w[u + s] = LBs[sb][u][s];   // the pivot's rsq chain
-        w[u + BB] += lam_in;
-        zr = znx;
-      }
+      // exec-masked LDS reads straight into the pivot lane's window, in flight during the
+      // pivot's rsq chain
+      if (pl) lds_row_issue<u>(w, lbs_base + (unsigned)(sb * BB * LS + u * LS) * 8u);
       ok = ok && (piv > 0.0);
       const double inv = rsqrt_f64(piv);
       const double yj = zpiv * inv;
+      lds_row_wait<u>(w);
+      if (pl) {
+        w[u + BB] += lam_in;
+        zr = znx;
+      }
       const double lval = w[u] * inv;            // l_i, i = (p - u) mod 16, pivot lane: i = 16
       if (lv && j < n) {                         // uniform branch
         Lrow[(int64_t)j * BB + (pl ? BB - 1 : ((p - u) & 15) - 1)] = lval;
@@ -986,40 +1015,92 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
     znx = znx2;
     __syncthreads();                               // next block's rows staged; this buffer free
   }
-  // back substitution L^T x = y, x overwrites y.  Lane (j+i) mod 16 holds x_{j+i}.  The
-  // factor columns of a 16-step block are loaded together (one memory latency per block).
+  // back substitution L^T x = y, x overwrites y.  Lane (j+i) mod 16 holds x_{j+i} (xr); every
+  // lane also holds the last two x (x1 = x_{j+1}, x2 = x_{j+2}).  Step j only waits on
+  //     x_j = ((y_j - P_j) - l_{j+2,j} x2 - l_{j+1,j} x1) / l_jj,
+  // P_j = sum_{i=3..16} l_{j+i,j} x_{j+i} being reduced over the row two steps earlier (its x
+  // are all known then), so the 16-lane sum is off the step-to-step chain (two fmas and a mul
+  // on it instead of a product, four DPP add levels, a subtract and a mul).  The factor data of
+  // a block's 16 steps come in two halves of 8, each loaded one half ahead.
   __syncthreads();
   const long long t_mid = (long long)__builtin_amdgcn_s_memtime();
-  double xr = 0.0;
-  // (two halves of 8 steps: the loads of a half in flight together, half the registers)
-  for (int jt = npad - 1; jt >= 0; jt -= 8) {
-    double pli[8], pinv[8], py[8];
-    const int uo = (jt & 15) == 15 ? 0 : 8;      // step v of this half: j & 15 = 15 - v - uo
+  struct Half {
+    double pl[8], iv[8], yv[8];
+  };
+  // step s of the block at jb: j = jb - s, u = j & 15 = 15 - s; lane p's factor entry
+  // l_{j+i,j}, i = (p - u) & 15 (0 -> 16)
+  auto load_half = [&](int jb, auto S0, Half& h) {
+    constexpr int s0 = decltype(S0)::value;
     static_for<0, 8>([&](auto V) {
       constexpr int v = decltype(V)::value;
-      const int u = 15 - v - uo;                 // j & 15 of step j = jt - v
-      const int j = jt - v;
+      constexpr int u = 15 - s0 - v;
+      const int j = jb - s0 - v;
       const int i = (p - u) & 15;
-      const bool in = j < n;
-      pli[v] = in ? Lrow[(int64_t)j * BB + (i == 0 ? BB - 1 : i - 1)] : 0.0;
-      pinv[v] = in ? Linv[j] : 1.0;
-      py[v] = in ? yl[j] : 0.0;
+      const bool in = j >= 0 && j < n;
+      h.pl[v] = in ? Lrow[(int64_t)j * BB + (i == 0 ? BB - 1 : i - 1)] : 0.0;
+      h.iv[v] = in ? Linv[j] : 1.0;
+      h.yv[v] = in ? yl[j] : 0.0;
     });
+  };
+  double xr = 0.0, x1 = 0.0, x2 = 0.0;
+  double Pq[2] = {0.0, 0.0}, L1q[2] = {0.0, 0.0}, L2q[2] = {0.0, 0.0};
+  // the row of step s + 2 (phase u' = u - 2, factor entries pl): its P from xr before step s's
+  // update, its two critical coefficients broadcast from lanes u' + 1, u' + 2
+  auto prep = [&](auto UP, double pl) {
+    constexpr int up = decltype(UP)::value & 15;
+    const int i = (p - up) & 15;
+    const double pm = (i == 1 || i == 2) ? 0.0 : pl;
+    Pq[0] = Pq[1];
+    L1q[0] = L1q[1];
+    L2q[0] = L2q[1];
+    Pq[1] = row16_sum(pm * xr);
+    L1q[1] = row_bcast<(up + 1) & 15>(pl);
+    L2q[1] = row_bcast<(up + 2) & 15>(pl);
+  };
+  auto step = [&](double yv, double iv) {
+    const double t = fma(-L2q[0], x2, yv - Pq[0]);
+    const double xj = fma(-L1q[0], x1, t) * iv;
+    x2 = x1;
+    x1 = xj;
+    return xj;
+  };
+  auto store_half = [&](int jb, int s0) {   // lanes u of the half hold their x in xr
+    const int j = jb - (15 - p);
+    if (lv && j < n && 15 - p >= s0 && 15 - p < s0 + 8) yl[j] = ok ? xr : __builtin_nan("");
+  };
+  Half A, B;
+  load_half(npad - 1, std::integral_constant<int, 0>{}, A);
+  // the first two rows' P, l (rows >= n: zero factor, so zero from xr = 0 anyway)
+  {
+    Pq[1] = 0.0;
+    L1q[1] = row_bcast<0>(A.pl[0]);   // u = 15: lanes 0, 1
+    L2q[1] = row_bcast<1>(A.pl[0]);
+    Pq[0] = Pq[1]; L1q[0] = L1q[1]; L2q[0] = L2q[1];
+    Pq[1] = 0.0;
+    L1q[1] = row_bcast<15>(A.pl[1]);  // u = 14: lanes 15, 0
+    L2q[1] = row_bcast<0>(A.pl[1]);
+  }
+  for (int jb = npad - 1; jb >= 0; jb -= 16) {
+    load_half(jb, std::integral_constant<int, 8>{}, B);
     static_for<0, 8>([&](auto V) {
       constexpr int v = decltype(V)::value;
-      const int u = 15 - v - uo;
-      const double s = row16_sum(pli[v] * xr);
-      const double xj = (py[v] - s) * pinv[v];
+      constexpr int u = 15 - v;
+      const double xj = step(A.yv[v], A.iv[v]);
+      if constexpr (v + 2 < 8) prep(std::integral_constant<int, u - 2>{}, A.pl[v + 2]);
+      else prep(std::integral_constant<int, u - 2>{}, B.pl[v - 6]);
       xr = (p == u) ? xj : xr;
-      py[v] = xj;
     });
-    if (lv) {
-      static_for<0, 8>([&](auto V) {
-        constexpr int v = decltype(V)::value;
-        const int j = jt - v;
-        if (j < n && p == 15 - v - uo) yl[j] = ok ? py[v] : __builtin_nan("");
-      });
-    }
+    store_half(jb, 0);
+    load_half(jb - 16, std::integral_constant<int, 0>{}, A);
+    static_for<0, 8>([&](auto V) {
+      constexpr int v = decltype(V)::value;
+      constexpr int u = 7 - v;
+      const double xj = step(B.yv[v], B.iv[v]);
+      if constexpr (v + 2 < 8) prep(std::integral_constant<int, u - 2 + 16>{}, B.pl[v + 2]);
+      else prep(std::integral_constant<int, u - 2 + 16>{}, A.pl[v - 6]);
+      xr = (p == u) ? xj : xr;
+    });
+    store_half(jb, 8);
   }
   if (tim != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {   // debug: wave 0 of block 0
     const long long t_end = (long long)__builtin_amdgcn_s_memtime();
