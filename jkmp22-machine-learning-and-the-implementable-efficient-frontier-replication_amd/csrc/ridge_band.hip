@@ -960,6 +960,26 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
       LBs[buf][e / LS][s] = (r < n) ? LB[(int64_t)r * LS + s] : (s == BB ? 1.0 : 0.0);
     }
   };
+  // the same in two halves: the global loads at a block's start into two registers per thread
+  // (BB * LS = 272 <= 2 NTS), the LDS stores at its end, so the loads' latency is spent under
+  // the block's 16 steps instead of in front of them
+  static_assert(BB * LS <= 2 * NTS, "two staged doubles per thread");
+  double st[2];
+  auto load_rows = [&](int r0s) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = threadIdx.x + h * NTS;
+      const int r = r0s + e / LS, s = e % LS;
+      st[h] = (e < BB * LS && r < n) ? LB[(int64_t)r * LS + s] : (s == BB ? 1.0 : 0.0);
+    }
+  };
+  auto store_rows = [&](int buf) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int e = threadIdx.x + h * NTS;
+      if (e < BB * LS) LBs[buf][e / LS][e % LS] = st[h];
+    }
+  };
   // window at j = 0: lane p holds row p, slot k <-> column k
 #pragma unroll
   for (int k = 0; k < 2 * BB; ++k)
@@ -971,12 +991,16 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
   bool ok = true;
   __syncthreads();
 
+  // every prologue load (window, z) done here: otherwise the compiler's wait for the first
+  // in-loop use of zr is a vmcnt(0) at the top of EVERY block, which also drains the block's
+  // own staging loads issued just before it
+  __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0)
   for (int j0 = 0; j0 < npad; j0 += 16) {
     const int sb = (j0 >> 4) & 1;
     // this block's entering row for lane p (row j0 + 16 + p, taken at step p), then the NEXT
     // block's rows to the other buffer
     const double lam_in = (j0 + BB + p < n) ? lam : 0.0;   // diagonal shift of the entering row
-    stage_rows(j0 + 2 * BB, sb ^ 1);
+    load_rows(j0 + 2 * BB);                        // -> LBs[sb ^ 1] at the block's end
     const double znx2 = (j0 + 2 * BB + p < n) ? z[j0 + 2 * BB + p] : 0.0;
     static_for<0, 16>([&](auto U) {
       constexpr int u = decltype(U)::value;
@@ -1013,6 +1037,7 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
 #pragma unroll
     for (int s = 0; s < BB; ++s) w[s] = w[s + BB];
     znx = znx2;
+    store_rows(sb ^ 1);
     __syncthreads();                               // next block's rows staged; this buffer free
   }
   // back substitution L^T x = y, x overwrites y.  Lane (j+i) mod 16 holds x_{j+i} (xr); every
@@ -1028,18 +1053,28 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
     double pl[8], iv[8], yv[8];
   };
   // step s of the block at jb: j = jb - s, u = j & 15 = 15 - s; lane p's factor entry
-  // l_{j+i,j}, i = (p - u) & 15 (0 -> 16)
-  auto load_half = [&](int jb, auto S0, Half& h) {
+  // l_{j+i,j}, i = (p - u) & 15 (0 -> 16).  CHECK (the first block only): rows >= n are
+  // identity rows (l = 0, 1 / l_jj = 1, y = 0).  Elsewhere every row is < n and the loads are
+  // branch-free (a row < 0, prefetched past the end, is clamped and never used): with a branch
+  // per load the compiler waited for ALL loads (the prefetch included) at the first use.
+  auto load_half = [&](int jb, auto S0, auto CHECK, Half& h) {
     constexpr int s0 = decltype(S0)::value;
     static_for<0, 8>([&](auto V) {
       constexpr int v = decltype(V)::value;
       constexpr int u = 15 - s0 - v;
       const int j = jb - s0 - v;
       const int i = (p - u) & 15;
-      const bool in = j >= 0 && j < n;
-      h.pl[v] = in ? Lrow[(int64_t)j * BB + (i == 0 ? BB - 1 : i - 1)] : 0.0;
-      h.iv[v] = in ? Linv[j] : 1.0;
-      h.yv[v] = in ? yl[j] : 0.0;
+      if constexpr (decltype(CHECK)::value) {
+        const bool in = j < n;
+        h.pl[v] = in ? Lrow[(int64_t)j * BB + (i == 0 ? BB - 1 : i - 1)] : 0.0;
+        h.iv[v] = in ? Linv[j] : 1.0;
+        h.yv[v] = in ? yl[j] : 0.0;
+      } else {
+        const int jc = max(j, 0);
+        h.pl[v] = Lrow[(int64_t)jc * BB + (i == 0 ? BB - 1 : i - 1)];
+        h.iv[v] = Linv[jc];
+        h.yv[v] = yl[jc];
+      }
     });
   };
   double xr = 0.0, x1 = 0.0, x2 = 0.0;
@@ -1068,8 +1103,10 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
     const int j = jb - (15 - p);
     if (lv && j < n && 15 - p >= s0 && 15 - p < s0 + 8) yl[j] = ok ? xr : __builtin_nan("");
   };
+  using I0 = std::integral_constant<int, 0>;
+  using I8 = std::integral_constant<int, 8>;
   Half A, B;
-  load_half(npad - 1, std::integral_constant<int, 0>{}, A);
+  load_half(npad - 1, I0{}, std::true_type{}, A);
   // the first two rows' P, l (rows >= n: zero factor, so zero from xr = 0 anyway)
   {
     Pq[1] = 0.0;
@@ -1080,8 +1117,8 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
     L1q[1] = row_bcast<15>(A.pl[1]);  // u = 14: lanes 15, 0
     L2q[1] = row_bcast<0>(A.pl[1]);
   }
-  for (int jb = npad - 1; jb >= 0; jb -= 16) {
-    load_half(jb, std::integral_constant<int, 8>{}, B);
+  auto block = [&](int jb, auto FIRST) {
+    load_half(jb, I8{}, FIRST, B);
     static_for<0, 8>([&](auto V) {
       constexpr int v = decltype(V)::value;
       constexpr int u = 15 - v;
@@ -1091,7 +1128,7 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
       xr = (p == u) ? xj : xr;
     });
     store_half(jb, 0);
-    load_half(jb - 16, std::integral_constant<int, 0>{}, A);
+    load_half(jb - 16, I0{}, std::false_type{}, A);
     static_for<0, 8>([&](auto V) {
       constexpr int v = decltype(V)::value;
       constexpr int u = 7 - v;
@@ -1101,7 +1138,9 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
       xr = (p == u) ? xj : xr;
     });
     store_half(jb, 8);
-  }
+  };
+  block(npad - 1, std::true_type{});
+  for (int jb = npad - 17; jb >= 0; jb -= 16) block(jb, std::false_type{});
   if (tim != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {   // debug: wave 0 of block 0
     const long long t_end = (long long)__builtin_amdgcn_s_memtime();
     tim[(int64_t)ncells * 8 + 0] = t_mid - t_start;
@@ -1321,23 +1360,22 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
     }
   // va[q][r] = V_p[16 b - r0 + 4 r + g4][c16] for the live blocks b = wid + 8 q of panel p
   const int lda = band_npad(n);                   // A's leading dimension (padded)
-  const int lo_a = g4 * lda + c16;
   double vn[NBW][4], tn[4];
+  // Branch-free loads (the row clamped into the panel: dead blocks and rows past m read a
+  // valid, cached element) and the unit-lower-triangular mask applied where the panel is
+  // used: with the loads under conditions and the mask right after them, the compiler waited
+  // for every V load of the prefetch as soon as it was issued.
   auto fetch = [&](int p) {
     const int k0 = p * BB, r0 = k0 + BB, m = n - r0;
     const double* Ap = A + (int64_t)r0 * lda + k0; // &V_p[0][0] (wave-uniform)
 #pragma unroll
     for (int q = 0; q < NBW; ++q) {
       const int b = wid + NWB * q;
-      const bool live = b > p && b < nb;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int ib = 16 * b - r0 + 4 * r, i = ib + g4;
-        double v = 0.0;
-        if (live && i < m && i > c16)
-          v = *reinterpret_cast<const double*>(
-              reinterpret_cast<const char*>(Ap + (int64_t)ib * lda) + (unsigned)lo_a * 8u);
-        vn[q][r] = (live && i == c16 && i < m) ? 1.0 : v;
+        const int i = 16 * b - r0 + 4 * r + g4;
+        const int ic = min(max(i, 0), m - 1);
+        vn[q][r] = Ap[(int64_t)ic * lda + c16];
       }
     }
     const double* Tp = bw.T + (int64_t)p * BB * BB;
@@ -1349,10 +1387,19 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
   for (int p = np - 1; p >= 0; --p) {
     double (*rp)[BB * BB] = red[p & 1];
     double va[NBW][4], tv[4];
+    {
+      const int m = n - (p * BB + BB);
 #pragma unroll
-    for (int q = 0; q < NBW; ++q)
+      for (int q = 0; q < NBW; ++q) {
+        const int b = wid + NWB * q;
+        const bool live = b > p && b < nb;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) va[q][r] = vn[q][r];
+        for (int r = 0; r < 4; ++r) {
+          const int i = 16 * (b - p - 1) + 4 * r + g4;
+          va[q][r] = (live && i < m && i >= c16) ? (i == c16 ? 1.0 : vn[q][r]) : 0.0;
+        }
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) tv[r] = tn[r];
     if (p > 0) fetch(p - 1);                        // next panel's V in flight from here on
