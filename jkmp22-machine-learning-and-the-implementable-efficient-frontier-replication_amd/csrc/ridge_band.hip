@@ -123,26 +123,53 @@ __device__ __forceinline__ double rcp_f64(double x) {
   return y;
 }
 
-// w[U + s] = LDS row at byte address `base` (s = 0 .. LS-1), as 17 ds_read_b64 straight into
-// the window registers ("+v": the exec-masked lanes keep their values, so no merge copies), and
-// NO wait: the caller overlaps the loads with independent work and then calls lds_row_wait<U>,
-// which waits for them and ties the same registers, so no read of w[U..U+16] can be scheduled
-// between the two.  (Written in plain C++ the compiler issued the loads into temporaries, waited
-// for them at once and merged them with 14 masked moves: the LDS latency sat on every step.)
-template <int U, int S = 0>
-__device__ __forceinline__ void lds_row_issue(double* w, unsigned base) {
-  if constexpr (S < LS) {
-    // ("memory": the stage_rows stores into LBs are only read here)
-    asm volatile("ds_read_b64 %0, %1 offset:%2" : "+v"(w[U + S]) : "v"(base), "i"(8 * S)
-                 : "memory");
-    lds_row_issue<U, S + 1>(w, base);
-  }
+// w[U + s] = LDS row at byte address `base` (s = 0 .. LS-1) in the lanes U, U+16, U+32, U+48
+// (the pivot lane of each 16-lane row): 17 ds_read_b64 straight into the window registers
+// under an exec mask set and restored INSIDE the one asm statement (no branch, and "+v": the
+// other lanes keep their values, so no merge copies), and NO wait: the caller overlaps the
+// loads with independent work and then calls lds_row_wait<U>, which waits for them and ties
+// the same registers, so no read of w[U..U+16] can be scheduled between the two.  (Written in
+// plain C++ the compiler issued the loads into temporaries, waited for them at once and merged
+// them with 14 masked moves: the LDS latency sat on every step.)
+// `pv` (the pivot, unchanged) is tied through the asm so that the rsq chain that consumes it
+// is scheduled after the loads are issued.
+template <int U>
+__device__ __forceinline__ void lds_row_issue(double* w, unsigned base, double& pv) {
+  static_assert(LS == 17, "17 loads");
+  const unsigned long long mask = 0x0001000100010001ULL << U;
+  unsigned long long saved;
+  // ("memory": the stores into the staged rows are only read here)
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_mov_b64 exec, %[mk]\n\t"
+      "ds_read_b64 %[w0], %[a] offset:0\n\t"
+      "ds_read_b64 %[w1], %[a] offset:8\n\t"
+      "ds_read_b64 %[w2], %[a] offset:16\n\t"
+      "ds_read_b64 %[w3], %[a] offset:24\n\t"
+      "ds_read_b64 %[w4], %[a] offset:32\n\t"
+      "ds_read_b64 %[w5], %[a] offset:40\n\t"
+      "ds_read_b64 %[w6], %[a] offset:48\n\t"
+      "ds_read_b64 %[w7], %[a] offset:56\n\t"
+      "ds_read_b64 %[w8], %[a] offset:64\n\t"
+      "ds_read_b64 %[w9], %[a] offset:72\n\t"
+      "ds_read_b64 %[w10], %[a] offset:80\n\t"
+      "ds_read_b64 %[w11], %[a] offset:88\n\t"
+      "ds_read_b64 %[w12], %[a] offset:96\n\t"
+      "ds_read_b64 %[w13], %[a] offset:104\n\t"
+      "ds_read_b64 %[w14], %[a] offset:112\n\t"
+      "ds_read_b64 %[w15], %[a] offset:120\n\t"
+      "ds_read_b64 %[w16], %[a] offset:128\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [sv] "=&s"(saved), [pv] "+v"(pv), [w0] "+v"(w[U + 0]), [w1] "+v"(w[U + 1]), [w2] "+v"(w[U + 2]), [w3] "+v"(w[U + 3]), [w4] "+v"(w[U + 4]), [w5] "+v"(w[U + 5]), [w6] "+v"(w[U + 6]), [w7] "+v"(w[U + 7]), [w8] "+v"(w[U + 8]), [w9] "+v"(w[U + 9]), [w10] "+v"(w[U + 10]), [w11] "+v"(w[U + 11]), [w12] "+v"(w[U + 12]), [w13] "+v"(w[U + 13]), [w14] "+v"(w[U + 14]), [w15] "+v"(w[U + 15]), [w16] "+v"(w[U + 16])
+      : [a] "v"(base), [mk] "s"(mask)
+      : "memory");
 }
 
+// (`dep`, unchanged, ties the wait after the value the caller computes under the loads)
 template <int U>
-__device__ __forceinline__ void lds_row_wait(double* w) {
+__device__ __forceinline__ void lds_row_wait(double* w, double& dep) {
   asm volatile("s_waitcnt lgkmcnt(0)"
-               : "+v"(w[U]), "+v"(w[U + 1]), "+v"(w[U + 2]), "+v"(w[U + 3]), "+v"(w[U + 4]),
+               : "+v"(dep), "+v"(w[U]), "+v"(w[U + 1]), "+v"(w[U + 2]), "+v"(w[U + 3]), "+v"(w[U + 4]),
                  "+v"(w[U + 5]), "+v"(w[U + 6]), "+v"(w[U + 7]), "+v"(w[U + 8]),
                  "+v"(w[U + 9]), "+v"(w[U + 10]), "+v"(w[U + 11]), "+v"(w[U + 12]),
                  "+v"(w[U + 13]), "+v"(w[U + 14]), "+v"(w[U + 15]), "+v"(w[U + 16]));
@@ -365,8 +392,9 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
 // reads column block I above its first row from row block I (dsytrd 'L' semantics: the
 // input's upper triangle is never read).  Per panel p:
 //
-//   B  every WG   U = V_p T_p (LDS), X_I = A22 U for the blocks I = gb (mod K) it owns in the
-//                 X phase (gb = global block), partials V_I' X_I and V_I' z_I per block
+//   B  every WG   U = V_p T_p (LDS), X_I = A22 U for the blocks I it owns in the X phase (the
+//                 QR WG the last x0(nI, K) blocks, a cost-model split; the others the rest
+//                 round-robin), partials V_I' X_I and V_I' z_I per block
 //   C  every WG   P = sum_I V_I' X_I and V'z in block order, M = T' P, z_I -= V_I T' V'z,
 //                 W_I = X_I - V_I M / 2 for its X blocks
 //   D  QR WG      look-ahead: the tiles (I, 0) of A22 ARE panel p+1; it applies update p to
@@ -445,36 +473,81 @@ struct CoopSync {
 
 // X_I += A22[k][I cols] U[k][:] for the NQ blocks blk[] of this wave (band_x_accum with an
 // explicit block list).
+// One k-chunk (NV x 8 rows of A22 from k) of the X phase for the NQ blocks of a wave, the
+// first NB of which lie entirely BELOW the chunk (their first row <= k) and the rest entirely
+// above it.  Lane (c16, g4) takes the k pair kk, kk + 1 (kk = k + 8 v + 2 g4) into two MFMAs (the
+// k order inside the 16 x 16 x 4 steps is permuted, the same for every block and every K):
+// above a block the pair is ONE 16-byte load along row i of the lower triangle (the 16 lanes of
+// a k-group read 16 rows: half the load instructions of one 8-byte load per k), below it two
+// row loads (coalesced along the block's 16 columns).  No per-element branch: with one the
+// compiler made both paths exec-masked and waited for each load's predecessor (WAW).
+template <int NQ, int NB, int NV>
+__device__ __forceinline__ void coop_x_chunk(const double* __restrict__ A, int lda, int r0, int m,
+                                             int k, const int (&col)[NQ], int c16, int g4,
+                                             const double (*__restrict__ Us)[LS],
+                                             double4_t (&X)[4]) {
+  typedef double d2v __attribute__((ext_vector_type(2)));   // 16-B aligned: one dwordx4 load
+  double a0[NV][NQ], a1[NV][NQ], b0[NV], b1[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int kk = k + 8 * v + 2 * g4;
+    static_for<0, NQ>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      if constexpr (q < NB) {
+        a0[v][q] = A[(int64_t)(r0 + min(kk, m - 1)) * lda + r0 + col[q]];
+        a1[v][q] = A[(int64_t)(r0 + min(kk + 1, m - 1)) * lda + r0 + col[q]];
+      } else {
+        const d2v x = *reinterpret_cast<const d2v*>(A + (int64_t)(r0 + col[q]) * lda + r0 + kk);
+        a0[v][q] = x.x;
+        a1[v][q] = x.y;
+      }
+    });
+    // (rows >= m of U are zero; the clamp keeps a last chunk inside Us)
+    b0[v] = Us[min(kk, BMP - 1)][c16];
+    b1[v] = Us[min(kk + 1, BMP - 1)][c16];
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      X[q] = mfma_f64_16x16x4(a0[v][q], b0[v], X[q]);
+      X[q] = mfma_f64_16x16x4(a1[v][q], b1[v], X[q]);
+    }
+}
+
+// X_I += A22[k][I cols] U[k][:] for the NQ blocks blk[] of this wave (increasing).  Only the
+// LOWER triangle of A22 is kept (the update writes no mirror tiles): element (kk, i) of column
+// block I is A[kk][i] for rows kk at or below the block's first row and A[i][kk] above it - the
+// same value a mirrored copy held.  The first rows of a wave's blocks are equal mod 32 (its
+// blocks are 8 K' apart), so 32-row chunks aligned to them (after a 16-row head when they are
+// 16 mod 32) never straddle one: each chunk is one coop_x_chunk<NQ, NB> with NB uniform.
 template <int NQ>
 __device__ __forceinline__ void coop_x_accum(const double* __restrict__ A, int lda, int r0,
                                              int m, const int (&blk)[4], int c16, int g4,
                                              const double (*__restrict__ Us)[LS],
                                              double4_t (&X)[4]) {
-  // Only the LOWER triangle of A22 is kept (the update writes no mirror tiles): element
-  // (kk, i) of column block I is A[kk][i] for rows kk at or below the block's first row and
-  // A[i][kk] above it - the same value a mirrored copy held, read from the lower triangle
   int col[NQ], top[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
     col[q] = min(blk[q] * 16 + c16, m - 1);
     top[q] = blk[q] * 16;
   }
-  for (int k = 0; k < m; k += 32) {
-    double a[8][NQ], b[8];
+  auto chunk = [&](int k, auto NV) {
+    int nb = 0;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int kk = min(k + 4 * u + g4, m - 1);
-#pragma unroll
-      for (int q = 0; q < NQ; ++q)
-        a[u][q] = (kk >= top[q]) ? A[(int64_t)(r0 + kk) * lda + r0 + col[q]]
-                                 : A[(int64_t)(r0 + col[q]) * lda + r0 + kk];
-      b[u] = Us[k + 4 * u + g4][c16];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) X[q] = mfma_f64_16x16x4(a[u][q], b[u], X[q]);
+    for (int q = 0; q < NQ; ++q) nb += (top[q] <= k) ? 1 : 0;
+    static_for<0, NQ + 1>([&](auto B) {
+      if (nb == decltype(B)::value)
+        coop_x_chunk<NQ, decltype(B)::value, decltype(NV)::value>(A, lda, r0, m, k, col, c16,
+                                                                 g4, Us, X);
+    });
+  };
+  int k = 0;
+  if (top[0] & 16) {
+    chunk(0, std::integral_constant<int, 2>{});
+    k = 16;
   }
+  for (; k < m; k += 32) chunk(k, std::integral_constant<int, 4>{});
 }
 
 template <bool TIMED>
@@ -606,14 +679,29 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
     }
     __syncthreads();
     COOP_TMARK(1)
-    // X blocks of this workgroup: I = first + (wid + 8 q) K
-    const int first = ((w - (p + 1)) % K + K) % K;
+    // X blocks of this workgroup.  The QR workgroup (w = 0) also factors the next panel and
+    // the others also apply the update, so the X blocks are split to balance the two: w = 0
+    // takes the last x0 blocks, the K - 1 others the rest round-robin, with x0 from a cost
+    // model of one panel calibrated on the MI355X phase timings (tools/bench_ridge.py
+    // --timing; cycles: X 197 per block per block row, update 174 per 16 x 16 tile, panel QR
+    // 30000 + 550 per block row) - large panels (update-heavy) give w = 0 about half the X
+    // blocks, small ones (QR-latency-bound) none.  Which workgroup computes a block does not
+    // change its arithmetic, so the betas stay bitwise independent of K.
+    int x0 = nI;
+    if (K > 1) {
+      const float fn = (float)nI;
+      const float upd = 174.0f * fn * (fn + 1.0f) * 0.5f, xs = 197.0f * fn;
+      const float qr = 30000.0f + 550.0f * fn;
+      const float xq = (upd + xs * fn - (float)(K - 1) * qr) / ((float)K * xs);
+      x0 = min(nI, max(0, (int)(xq + 0.5f)));
+    }
     int blk[4];
     int nq = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      blk[q] = first + (wid + NWR * q) * K;
-      nq += (blk[q] < nI) ? 1 : 0;
+      const int k = wid + NWR * q;
+      blk[q] = qwg ? nI - x0 + k : (w - 1) + (K - 1) * k;
+      nq += (qwg ? k < x0 : blk[q] < nI - x0) ? 1 : 0;
     }
     double4_t X[4];
 #pragma unroll
@@ -934,7 +1022,7 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
   const int p = threadIdx.x & 15;
   const int l = (blockIdx.x % nb) * 16 + (threadIdx.x >> 4);
   const bool lv = l < L;
-  const int lc = lv ? l : L - 1;                 // padding rows redo the last lambda, no stores
+  const int lc = lv ? l : L - 1;                 // padding rows redo the last lambda
   BandWork bw(work + cd.work, n, L);
   const double lam = lvec[lc];
   double* Lrow = bw.Lf + (int64_t)lc * n * BB;   // row j: l_{j+1..j+16, j}
@@ -995,38 +1083,39 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
   // in-loop use of zr is a vmcnt(0) at the top of EVERY block, which also drains the block's
   // own staging loads issued just before it
   __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0)
-  for (int j0 = 0; j0 < npad; j0 += 16) {
+  // One 16-step block.  CHECK (the last block only): rows >= n are identity rows and store
+  // nothing.  Elsewhere the stores need no condition: a padding lane (lambda >= L) redoes
+  // lambda L-1 bit for bit, so its stores repeat the same values; 1 / l_jj and y_j are kept by
+  // the pivot lane and stored once per block (16 lanes, one line) instead of per step.
+  auto fwd_block = [&](int j0, auto CHECK) {
+    constexpr bool chk = decltype(CHECK)::value;
     const int sb = (j0 >> 4) & 1;
     // this block's entering row for lane p (row j0 + 16 + p, taken at step p), then the NEXT
     // block's rows to the other buffer
     const double lam_in = (j0 + BB + p < n) ? lam : 0.0;   // diagonal shift of the entering row
     load_rows(j0 + 2 * BB);                        // -> LBs[sb ^ 1] at the block's end
     const double znx2 = (j0 + 2 * BB + p < n) ? z[j0 + 2 * BB + p] : 0.0;
+    double myinv = 0.0, myy = 0.0;
     static_for<0, 16>([&](auto U) {
       constexpr int u = decltype(U)::value;
       const int j = j0 + u;
       const bool pl = (p == u);                  // pivot lane: holds row j, takes row j+16
-      const double piv = row_bcast<u>(w[u]);
+      double piv = row_bcast<u>(w[u]);
       const double zpiv = row_bcast<u>(zr);      // (read before the pivot lane's zr changes)
-      // exec-masked LDS reads straight into the pivot lane's window, in flight during the
-      // pivot's rsq chain
-      if (pl) lds_row_issue<u>(w, lbs_base + (unsigned)(sb * BB * LS + u * LS) * 8u);
+      // LDS reads straight into the pivot lane's window, in flight during the pivot's rsq chain
+      lds_row_issue<u>(w, lbs_base + (unsigned)(sb * BB * LS + u * LS) * 8u, piv);
       ok = ok && (piv > 0.0);
-      const double inv = rsqrt_f64(piv);
+      double inv = rsqrt_f64(piv);
+      lds_row_wait<u>(w, inv);
       const double yj = zpiv * inv;
-      lds_row_wait<u>(w);
       if (pl) {
         w[u + BB] += lam_in;
         zr = znx;
+        myinv = inv;
+        myy = yj;
       }
       const double lval = w[u] * inv;            // l_i, i = (p - u) mod 16, pivot lane: i = 16
-      if (lv && j < n) {                         // uniform branch
-        Lrow[(int64_t)j * BB + (pl ? BB - 1 : ((p - u) & 15) - 1)] = lval;
-        if (p == 0) {                            // one lane per row: 16 same-address stores
-          Linv[j] = inv;                         // of a row group are not merged (measured:
-          yl[j] = yj;                            // WRITE_SIZE twice the factor's bytes)
-        }
-      }
+      if (!chk || j < n) Lrow[(int64_t)j * BB + (pl ? BB - 1 : ((p - u) & 15) - 1)] = lval;
       zr -= lval * yj;
       const double nl = -lval;
       static_for<1, LS>([&](auto K) {
@@ -1034,12 +1123,18 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
         fmac_bcast<(u + k) & 15, k == 1>(w[u + k], lval, nl);   // w -= l_k * l_i
       });
     });
+    if (!chk || j0 + p < n) {
+      Linv[j0 + p] = myinv;
+      yl[j0 + p] = myy;
+    }
 #pragma unroll
     for (int s = 0; s < BB; ++s) w[s] = w[s + BB];
     znx = znx2;
     store_rows(sb ^ 1);
     __syncthreads();                               // next block's rows staged; this buffer free
-  }
+  };
+  for (int j0 = 0; j0 < npad - 16; j0 += 16) fwd_block(j0, std::false_type{});
+  fwd_block(npad - 16, std::true_type{});
   // back substitution L^T x = y, x overwrites y.  Lane (j+i) mod 16 holds x_{j+i} (xr); every
   // lane also holds the last two x (x1 = x_{j+1}, x2 = x_{j+2}).  Step j only waits on
   //     x_j = ((y_j - P_j) - l_{j+2,j} x2 - l_{j+1,j} x1) / l_jj,

@@ -88,8 +88,9 @@ for step in ${MODE//,/ }; do
       PFML_COOP_K=1 PFML_BENCH_CELLS=1,106 timeout -k 10 300 python tools/bench_ridge.py > $OUT/coop_cells_k1.log 2>&1
       rc=$?; tail -1 $OUT/coop_cells_k1.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     benchk)
-      # headline bench with the cooperative reduction at auto K and at K = 1 (every cell one WG)
-      for k in auto 1; do
+      # headline bench with the cooperative reduction at auto K and at K = 1 (every cell one WG);
+      # PFML_BENCHK overrides the list (e.g. "1 2 1 2")
+      for k in ${PFML_BENCHK:-auto 1}; do
         if [ $k = auto ]; then unset PFML_COOP_K; else export PFML_COOP_K=$k; fi
         timeout -k 10 300 python bench.py --no-inputs > $OUT/bench_k$k.json 2> $OUT/bench_k$k.err
         rc=$?; echo "K=$k: $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_k$k.json)"; if [ $rc -ne 0 ]; then tail -5 $OUT/bench_k$k.err; exit $rc; fi
