@@ -291,8 +291,8 @@ def coop_k(cell_n: np.ndarray, ncu: int, others: int = 0) -> np.ndarray:
     CUs with them from a second stream): the big cells get the CUs the ``others`` concurrent
     one-workgroup cells leave, (ncu - others) // n_big each.  Extra workgroups per cell add
     cross-workgroup hand-offs (more CU-time per cell), so they pay only on CUs that would
-    otherwise idle: the one-GPU grid (106 big + 318 other cells) runs K = 1 (5.82 ms per step vs
-    6.28 ms at K = 2, profiles/r04_bench_coop_k1.json / _kauto.json), an 8-rank shard (about
+    otherwise idle: the one-GPU grid (106 big + 318 other cells) runs K = 1 (5.25 ms per step vs
+    5.80 ms at K = 2, profiles/r04_bench_coop_k1.json / _k2.json), an 8-rank shard (about
     13 big + 40 others) K = 16.  The betas do not depend on this choice (bitwise: see
     band_coop_kernel), only the time does.  PFML_COOP_K=k forces k for the largest cells."""
     n = np.asarray(cell_n)
