@@ -471,8 +471,6 @@ struct CoopSync {
   }
 };
 
-// X_I += A22[k][I cols] U[k][:] for the NQ blocks blk[] of this wave (band_x_accum with an
-// explicit block list).
 // One k-chunk (NV x 8 rows of A22 from k) of the X phase for the NQ blocks of a wave, the
 // first NB of which lie entirely BELOW the chunk (their first row <= k) and the rest entirely
 // above it.  Lane (c16, g4) takes the k pair kk, kk + 1 (kk = k + 8 v + 2 g4) into two MFMAs (the
@@ -713,7 +711,13 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
       case 4: coop_x_accum<4>(A, lda, r0, m, blk, c16, g4, Ws, X); break;
       default: break;
     }
-    // per-block partials V_I' X_I and V_I' z_I (z as column 0 of the B operand)
+    // per-block partials V_I' X_I and V_I' z_I (z as column 0 of the B operand).  With one
+    // workgroup per cell (K = 1) they stay on the CU: U is dead once every wave's X is done, so
+    // they go to the LDS of Ws (32 blocks x 272 doubles = exactly its 512 x 17), and W later
+    // straight to Ws - no global round trip of partials and W per panel.  (Same values, same
+    // summation order: bitwise the same betas as K > 1.)
+    double* const Pl = &Ws[0][0];
+    if (K == 1) __syncthreads();                   // every wave's reads of U are done
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (q < nq) {
@@ -730,8 +734,13 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          stw(cw.Pg + (int64_t)blk[q] * (BB * BB) + (g4 + 4 * r) * BB + c16, Pp[r]);
-          if (c16 == 0) stw(cw.Pzg + blk[q] * BB + g4 + 4 * r, Pz[r]);
+          if (K == 1) {
+            Pl[blk[q] * (BB * BB + BB) + (g4 + 4 * r) * BB + c16] = Pp[r];
+            if (c16 == 0) Pl[blk[q] * (BB * BB + BB) + BB * BB + g4 + 4 * r] = Pz[r];
+          } else {
+            stw(cw.Pg + (int64_t)blk[q] * (BB * BB) + (g4 + 4 * r) * BB + c16, Pp[r]);
+            if (c16 == 0) stw(cw.Pzg + blk[q] * BB + g4 + 4 * r, Pz[r]);
+          }
         }
       }
     }
@@ -742,12 +751,17 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
     if (t < BB * BB + BB) {
       // (all nI partials in flight, then summed in block order)
       const bool isP = t < BB * BB;
-      const double* base = isP ? cw.Pg + t : cw.Pzg + (t - BB * BB);
-      const int stride = isP ? BB * BB : BB;
       constexpr int NB = BNMAX / BB;
       double v[NB];
+      if (K == 1) {
 #pragma unroll
-      for (int I = 0; I < NB; ++I) v[I] = ldw(base + min(I, nI - 1) * stride);
+        for (int I = 0; I < NB; ++I) v[I] = Pl[min(I, nI - 1) * (BB * BB + BB) + t];
+      } else {
+        const double* base = isP ? cw.Pg + t : cw.Pzg + (t - BB * BB);
+        const int stride = isP ? BB * BB : BB;
+#pragma unroll
+        for (int I = 0; I < NB; ++I) v[I] = ldw(base + min(I, nI - 1) * stride);
+      }
       double s = 0.0;
 #pragma unroll
       for (int I = 0; I < NB; ++I) s = (I < nI) ? s + v[I] : s;
@@ -782,15 +796,18 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int i = i0 + g4 + 4 * r;
-          stw(cw.Wg + i * BB + c16, (i < m) ? X[q][r] - 0.5 * acc[r] : 0.0);
+          const double wv = (i < m) ? X[q][r] - 0.5 * acc[r] : 0.0;
+          if (K == 1) Ws[i][c16] = wv;               // (the partials were read before the
+          else stw(cw.Wg + i * BB + c16, wv);        // barriers above)
         }
       }
     }
     COOP_TMARK(4)
     cs.sync(false, &err_s);
     COOP_TMARK(3)
-    // ---- D: W -> Ws; update (update workgroups) / look-ahead panel p+1 (QR workgroup)
-    {
+    // ---- D: W -> Ws (K = 1: already there); update (update workgroups) / look-ahead panel
+    //      p+1 (QR workgroup)
+    if (K > 1) {
       double v[BMP * BB / NTR];
 #pragma unroll
       for (int u = 0; u < BMP * BB / NTR; ++u) v[u] = ldw(cw.Wg + min(t + NTR * u, nI * BB * BB - 1));
@@ -1624,7 +1641,7 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
                                              int L, double* work, double* beta_out, int64_t ldo,
                                              long long* tim, int* lu_list, int* lu_count,
                                              int lu_cap, const int* wgmap, int nwg,
-                                             unsigned* syncw, hipStream_t st) {
+                                             unsigned* syncw, hipEvent_t mid, hipStream_t st) {
   const RidgeCellDesc* cd = static_cast<const RidgeCellDesc*>(cells);
   // the cooperative reduction: nwg workgroups (wgmap: cell << 8 | w << 4 | K - 1), the cells'
   // sync words zeroed on the stream first (a memset node under graph capture)
@@ -1648,6 +1665,10 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
                        ncells, L, work, lu_list, lu_count, lu_cap);
     hipLaunchKernelGGL(ridge_band_lu_kernel, dim3(LU_WG), dim3(64), 0, st, cd, lvec, L, work,
                        lu_list, lu_count, lu_cap);
+  }
+  if (mid != nullptr) {                      // (the solves are queued: see ridge.hip)
+    e = hipEventRecord(mid, st);
+    if (e != hipSuccess) return e;
   }
   const int nch = (L + LC - 1) / LC;
   hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3(ncells * nch), dim3(NTB), 0, st, cd,
