@@ -1641,7 +1641,7 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
                                              int L, double* work, double* beta_out, int64_t ldo,
                                              long long* tim, int* lu_list, int* lu_count,
                                              int lu_cap, const int* wgmap, int nwg,
-                                             unsigned* syncw, hipEvent_t mid, hipStream_t st) {
+                                             unsigned* syncw, hipStream_t st) {
   const RidgeCellDesc* cd = static_cast<const RidgeCellDesc*>(cells);
   // the cooperative reduction: nwg workgroups (wgmap: cell << 8 | w << 4 | K - 1), the cells'
   // sync words zeroed on the stream first (a memset node under graph capture)
@@ -1665,10 +1665,6 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
                        ncells, L, work, lu_list, lu_count, lu_cap);
     hipLaunchKernelGGL(ridge_band_lu_kernel, dim3(LU_WG), dim3(64), 0, st, cd, lvec, L, work,
                        lu_list, lu_count, lu_cap);
-  }
-  if (mid != nullptr) {                      // (the solves are queued: see ridge.hip)
-    e = hipEventRecord(mid, st);
-    if (e != hipSuccess) return e;
   }
   const int nch = (L + LC - 1) / LC;
   hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3(ncells * nch), dim3(NTB), 0, st, cd,

@@ -630,7 +630,9 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
 
     On a device the cells split into the largest-n group and the rest; each group's ridge ->
     utilities chain is issued on its own HIP stream, the big group first, so the small cells'
-    chain runs on the CUs the big cells' reduction leaves idle.  beta / obj rows are written in
+    chain runs on the CUs the big cells' reduction leaves idle.  (Holding the small cells'
+    utilities back until the big cells' solves are done measured slower: 5.43 vs 5.12 ms, the
+    big back-transform then shares the chip with them, profiles/r04_quad_after_solve_ab.json.)  beta / obj rows are written in
     place from cached launch plans, and the non-SPD systems are re-solved on the device inside
     each group's ridge launch (pivoted banded LU; no host sync, counts in ``LAST_REPAIRS``).
     """
