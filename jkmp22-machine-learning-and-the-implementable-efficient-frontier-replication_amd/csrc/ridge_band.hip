@@ -94,6 +94,25 @@ __device__ __forceinline__ void fmac_bcast(double& w, double src, double m) {
                  : "+v"(w) : "v"(src), "v"(m), "i"(SEL));
 }
 
+// w -= bcast_SEL(src) * m  (the DPP source negated by the instruction's neg modifier: no
+// separate negation of src)
+template <int SEL, bool FIRST>
+__device__ __forceinline__ void fnmac_bcast(double& w, double src, double m) {
+  if constexpr (FIRST)
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(w) : "v"(src), "v"(m), "i"(SEL));
+  else
+    asm volatile("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(w) : "v"(src), "v"(m), "i"(SEL));
+}
+
+// 1/sqrt(x) with ONE Newton step on v_rsq_f64 (~2^-46 relative: the banded Cholesky's pivots,
+// far below the factorisation's own n eps backward error)
+__device__ __forceinline__ double rsqrt1_f64(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  return y * fma(-0.5 * x * y, y, 1.5);
+}
+
 template <int CTRL>
 __device__ __forceinline__ double dpp_mov(double v) {
   const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
@@ -175,6 +194,7 @@ __device__ __forceinline__ void lds_row_wait(double* w, double& dep) {
                  "+v"(w[U + 13]), "+v"(w[U + 14]), "+v"(w[U + 15]), "+v"(w[U + 16]));
 }
 
+// (64-bit DPP supports only row_newbcast, so the butterfly levels are 32-bit DPP moves)
 __device__ __forceinline__ double row16_sum(double v) {
   v += dpp_mov<0xB1>(v);      // quad_perm [1,0,3,2]
   v += dpp_mov<0x4E>(v);      // quad_perm [2,3,0,1]
@@ -1122,7 +1142,7 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
       // LDS reads straight into the pivot lane's window, in flight during the pivot's rsq chain
       lds_row_issue<u>(w, lbs_base + (unsigned)(sb * BB * LS + u * LS) * 8u, piv);
       ok = ok && (piv > 0.0);
-      double inv = rsqrt_f64(piv);
+      double inv = rsqrt1_f64(piv);
       lds_row_wait<u>(w, inv);
       const double yj = zpiv * inv;
       if (pl) {
@@ -1134,10 +1154,9 @@ __global__ __launch_bounds__(NTS, 3) void ridge_band_solve_kernel(
       const double lval = w[u] * inv;            // l_i, i = (p - u) mod 16, pivot lane: i = 16
       if (!chk || j < n) Lrow[(int64_t)j * BB + (pl ? BB - 1 : ((p - u) & 15) - 1)] = lval;
       zr -= lval * yj;
-      const double nl = -lval;
       static_for<1, LS>([&](auto K) {
         constexpr int k = decltype(K)::value;
-        fmac_bcast<(u + k) & 15, k == 1>(w[u + k], lval, nl);   // w -= l_k * l_i
+        fnmac_bcast<(u + k) & 15, k == 1>(w[u + k], lval, lval);   // w -= l_k * l_i
       });
     });
     if (!chk || j0 + p < n) {
