@@ -282,19 +282,22 @@ COOP_KMAX = 16          # workgroups per cell of the cooperative band reduction 
 COOP_SYNC_WORDS = 32    # csrc/ridge_band.hip COOP_SYNC: int32 sync words per cell
 
 
-def coop_k(cell_n: np.ndarray, ncu: int, others: int = 0) -> np.ndarray:
+COOP_BIG_SHARE = 0.42   # share of the CUs the largest cells' cooperative launch gets (coop_k)
+
+
+def coop_k(cell_n: np.ndarray, ncu: int) -> np.ndarray:
     """Workgroups per cell of the cooperative band reduction.
 
-    The largest-n cells of a launch share the chip's CUs (at most COOP_KMAX each, at least 1)
-    when they are the p = 512 cells (n > 256: 32 panels, the grid step's critical chain); every
-    other cell gets one workgroup (its chain is shorter than the big cells' and it shares the
-    CUs with them from a second stream): the big cells get the CUs the ``others`` concurrent
-    one-workgroup cells leave, (ncu - others) // n_big each.  Extra workgroups per cell add
-    cross-workgroup hand-offs (more CU-time per cell), so they pay only on CUs that would
-    otherwise idle: the one-GPU grid (106 big + 318 other cells) runs K = 1 (5.25 ms per step vs
-    5.80 ms at K = 2, profiles/r04_bench_coop_k1.json / _k2.json), an 8-rank shard (about
-    13 big + 40 others) K = 16.  The betas do not depend on this choice (bitwise: see
-    band_coop_kernel), only the time does.  PFML_COOP_K=k forces k for the largest cells."""
+    The largest-n cells of a launch are the p = 512 cells (n > 256: 32 panels, the grid step's
+    critical chain); they share about COOP_BIG_SHARE of the chip's CUs, round(0.42 ncu / n_big)
+    workgroups each (at least 1, at most COOP_KMAX), and every other cell gets one workgroup:
+    the smaller cells' whole chain (reduction, solves, back-transform, utilities) runs on the
+    rest from a second stream and must keep pace.  Measured on the one-GPU rank rehearsal
+    (tools/gpu_run.sh shardk, profiles/r04_coop_k_sweep.json): the best K is 1 / 2 / 4 / 6-8 at
+    W = 1 / 2 / 4 / 8 ranks (106 / 53 / 27 / 13 big cells per rank), i.e. ~106 of 256 CUs for the
+    big cells whatever W - giving them all the CUs the small cells leave (K = 16 at W = 8) was
+    27 % slower per rank.  The betas do not depend on K (bitwise: see band_coop_kernel), only
+    the time does.  PFML_COOP_K=k forces k for the largest cells."""
     n = np.asarray(cell_n)
     k = np.ones(len(n), dtype=np.int64)
     if not len(n):
@@ -304,7 +307,7 @@ def coop_k(cell_n: np.ndarray, ncu: int, others: int = 0) -> np.ndarray:
     if v:
         kb = int(v)
     elif int(n.max()) > 256:
-        kb = (ncu - int(others)) // int(big.sum())
+        kb = int(round(COOP_BIG_SHARE * ncu / int(big.sum())))
     else:
         kb = 1
     k[big] = min(max(kb, 1), COOP_KMAX)
@@ -352,8 +355,7 @@ def num_cus(dev) -> int:
     return max(1, _NCU[key] // ranks_per_device())
 
 
-def ridge_plan(P: int, L: int, cell_src, cell_n, cell_scale, ncu: int = 256,
-               others: int = 0) -> dict:
+def ridge_plan(P: int, L: int, cell_src, cell_n, cell_scale, ncu: int = 256) -> dict:
     """Host-side descriptors of one ridge-grid launch (CELL_DTYPE, big cells first) and the
     workgroup map of the cooperative reduction (``ncu``: the device's CUs)."""
     lib = nat.hip_lib()
@@ -373,7 +375,7 @@ def ridge_plan(P: int, L: int, cell_src, cell_n, cell_scale, ncu: int = 256,
     desc = desc[order]
     wsz = wsz[order]
     desc["work"] = np.concatenate([[0], np.cumsum(wsz)[:-1]])
-    wgmap = coop_wgmap(coop_k(desc["n"], ncu, others))
+    wgmap = coop_wgmap(coop_k(desc["n"], ncu))
     return {"desc": desc, "work": int(wsz.sum()), "nmax": int(cell_n.max()), "nc": nc,
             "wgmap": wgmap}
 
@@ -586,8 +588,7 @@ def _utilities_plan(P: int, L: int, dev, cell_src, cell_n, cell_scale, job_cell,
     for grp in parts:
         cells = np.nonzero(grp)[0]
         jobs = np.nonzero(grp[job_cell])[0]
-        rp = ridge_plan(P, L, cell_src[cells], cell_n[cells], cell_scale[cells], ncu=num_cus(dev),
-                        others=int(len(cell_n) - len(cells)))
+        rp = ridge_plan(P, L, cell_src[cells], cell_n[cells], cell_scale[cells], ncu=num_cus(dev))
         # ridge_plan orders cells big-first and numbers outputs 0..: map to global rows
         rp["desc"]["out"] = cells[rp["desc"]["out"] // (L * P)].astype(np.int64) * L * P
         qp = quad_plan(P, L, P, job_cell[jobs], job_month[jobs], job_n[jobs], job_out=jobs)

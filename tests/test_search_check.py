@@ -80,3 +80,18 @@ def test_nonfinite_cells_recomputed_on_cpu_oracle():
     assert nonfinite_cells(grid) == []
     assert torch.allclose(grid.beta, clean.beta, rtol=1e-10, atol=1e-14)
     assert torch.allclose(grid.obj, clean.obj, rtol=1e-10, atol=1e-14)
+
+
+def test_coop_k_policy_big_cells_share(monkeypatch):
+    """The cooperative band reduction's workgroups per big cell (ops/ridge.py::coop_k): the
+    p = 512 cells share ~42 % of the CUs - K = 1 / 2 / 4 / 8 for the 106 / 53 / 27 / 13 big
+    cells of a 1 / 2 / 4 / 8-rank grid (the measured optimum, profiles/r04_coop_k_sweep.json),
+    16 at most, 1 for the smaller cells; PFML_COOP_K forces the big cells' K."""
+    from pfml.ops.ridge import COOP_KMAX, coop_k
+    monkeypatch.delenv("PFML_COOP_K", raising=False)
+    for nbig, want in ((106, 1), (53, 2), (27, 4), (26, 4), (14, 8), (13, 8), (1, COOP_KMAX)):
+        k = coop_k(np.array([513] * nbig + [257, 129, 65]), 256)
+        assert (k[:nbig] == want).all() and (k[nbig:] == 1).all(), (nbig, k[:3])
+    assert (coop_k(np.array([129] * 5 + [65]), 256) == 1).all()   # no n > 256 cell: K = 1
+    monkeypatch.setenv("PFML_COOP_K", "3")
+    assert coop_k(np.array([513] * 106 + [65]), 256)[0] == 3

@@ -114,6 +114,22 @@ for step in ${MODE//,/ }; do
         PFML_QUAD_MM=$mm timeout -k 10 200 python bench.py > $OUT/bench_mm$mm.json 2> $OUT/bench_mm$mm.err
         rc=$?; echo "mm $mm: $(grep -o '"ms_per_step": [0-9.]*' $OUT/bench_mm$mm.json)"; if [ $rc -ne 0 ]; then tail -5 $OUT/bench_mm$mm.err; exit $rc; fi
       done ;;
+    shardk)
+      # W-rank rehearsal (PFML_SHARDW, default 8) with the big cells' K forced (PFML_SHARDK
+      # list, default "auto 8 4")
+      W=${PFML_SHARDW:-8}
+      for k in ${PFML_SHARDK:-auto 8 4}; do
+        if [ $k = auto ]; then unset PFML_COOP_K; else export PFML_COOP_K=$k; fi
+        PFML_SHARD_GRAPH=1 timeout -k 10 300 python tools/bench_shard.py $W > $OUT/shard${W}_k$k.json 2> $OUT/shard${W}_k$k.err
+        rc=$?; echo "W=$W K=$k: $(grep -o '"w[0-9]*_max_ms": [0-9.]*' $OUT/shard${W}_k$k.json)"; if [ $rc -ne 0 ]; then tail -3 $OUT/shard${W}_k$k.err; exit $rc; fi
+      done
+      unset PFML_COOP_K ;;
+    shardtl)
+      # kernel timeline of the last rank's grid step of a W = 8 rehearsal (graph replay)
+      (cd /tmp && export TMPDIR=/tmp PFML_SHARD_GRAPH=1 && timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/prof8 -o run -- python3 $ROOT/tools/bench_shard.py 8 3 > $OUT/prof8.log 2>&1)
+      rc=$?; if [ $rc -ne 0 ]; then tail -3 $OUT/prof8.log; exit $rc; fi
+      python tools/rocprof_timeline.py $(find $OUT/prof8 -name "*.db" | head -1) --last 40 > $OUT/timeline8.txt 2>&1
+      rm -rf $OUT/prof8; tail -34 $OUT/timeline8.txt ;;
     timeline)
       # kernel timeline of the last full 1-GPU grid step
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/prof1 -o run -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-inputs > $OUT/prof1.log 2>&1)
