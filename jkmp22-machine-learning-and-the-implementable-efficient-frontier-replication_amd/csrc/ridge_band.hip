@@ -300,7 +300,11 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
       for (int q = q4; q < q4 + 4; ++q) {
         const int i = rg + 32 * q;
         const double mq = (q > 0 || i > j) ? a[q] : 0.0;       // rows below the diagonal
-        fmac_bcast<j, true>(s1p[q & 3], a[q], mq);             // += x_j[i] a_cq[i]
+        // (DPP source a[q]: only a[0] can have been written by a plain VALU op just before -
+        // the diagonal fix-up of the last column; every other a[q] was last written by this
+        // asm sequence >= 2 instructions earlier, so only q = 0 needs the 2 wait states)
+        if (q == 0) fmac_bcast<j, true>(s1p[q & 3], a[q], mq);  // += x_j[i] a_cq[i]
+        else fmac_bcast<j, false>(s1p[q & 3], a[q], mq);
       }
     }
     // sum over the wave's 4 row groups (lanes l, l^16, l^32, l^48): VALU lane swaps
@@ -363,7 +367,7 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
           fmac_bcast<j, true>(a[0], a[0], ns0);
           if (i == j) a[0] = upd ? a[0] - wc : (own ? beta : a[0]);
         } else {
-          fmac_bcast<j, true>(a[q], a[q], nsw);
+          fmac_bcast<j, false>(a[q], a[q], nsw);
         }
       }
     }
