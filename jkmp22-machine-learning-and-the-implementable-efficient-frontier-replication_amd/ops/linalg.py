@@ -14,6 +14,7 @@
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -82,7 +83,7 @@ _BLOCKED_MIN_N = 160
 
 nat.register_hip("pfml_spd_leafinv_to", [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
                                          C.c_int64, C.c_int, C.c_int, C.c_int, C.c_void_p,
-                                         C.c_void_p])
+                                         C.c_int, C.c_void_p])
 
 _REC_LEAF = 64
 _REC_BUFS: dict = {}
@@ -126,7 +127,7 @@ def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor,
             _work.add("spd_leafinv_kernel", 2.0 * B * nn ** 3, 16.0 * B * nn * nn)
             nat.check(lib.pfml_spd_leafinv_to(A.data_ptr(), A.stride(1), A.stride(0),
                                               X.data_ptr(), ld, sX, B, r0, nn,
-                                              status.data_ptr(), st), "pfml_spd_leafinv_to")
+                                              status.data_ptr(), 0, st), "pfml_spd_leafinv_to")
             return
         h = _rec_split(nn)
         m = nn - h
@@ -149,6 +150,64 @@ def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor,
                    beta=1.0)                                                  # X11 -= X12 W'
 
     rec(0, n, 0, X if src is None else src)
+
+
+# GEMM tile config of the symmetric form's products (csrc/gemm_f64.hip tile_cfg; 0: auto);
+# PFML_SPD_SYM=0 takes the two-sided form for every m_func inverse (A/B switch)
+SYM_GEMM_CFG = int(os.environ.get("PFML_SYM_GEMM_CFG", "0"))
+SYM_INVERSE = os.environ.get("PFML_SPD_SYM", "1") != "0"
+
+
+def spd_inverse_sym(X: torch.Tensor, status: torch.Tensor) -> torch.Tensor:
+    """In-place inverse of a device batch [B, n, n] of EXACTLY symmetric SPD matrices whose
+    result is used as a symmetric matrix (m_tilde_0 and the fixed-point steps of m_func,
+    General_functions.py:957-960): the recursive Schur form with every symmetric product
+    computed on its lower block triangle only and mirrored -
+
+        X11 = A11^-1,  W = X11 A12,  S = A22 - A21 W  (lower tiles),  X22 = S^-1,
+        X12 = -W X22  (X21 = X12' written by the same launch),  X11 -= X12 W'  (lower tiles)
+
+    about n^3 flops instead of the two-sided form's ~1.67 n^3, with exactly symmetric leaves
+    and products, so the result is exactly symmetric.  Non-positive pivots flag ``status``."""
+    B, n, _ = X.shape
+    if not nat.is_device(X) or n < _BLOCKED_MIN_N or not X.is_contiguous() or not SYM_INVERSE:
+        return spd_inverse(X, inplace=True, status=status)
+    lib = nat.hip_lib()
+    st = nat.stream_of(X)
+    ld, sX = X.stride(1), X.stride(0)
+    cfg = SYM_GEMM_CFG
+
+    def buf(depth, h, m):
+        key = (X.device, B, depth, "sym")
+        w = _REC_BUFS.get(key)
+        if w is None or w.numel() < B * h * m:
+            w = torch.empty(B * h * m, dtype=torch.float64, device=X.device)
+            _REC_BUFS[key] = w
+        return w[:B * h * m].view(B, h, m)
+
+    def rec(r0, nn, depth):
+        if nn <= _REC_LEAF:
+            _work.add("spd_leafinv_kernel", 2.0 * B * nn ** 3, 16.0 * B * nn * nn)
+            nat.check(lib.pfml_spd_leafinv_to(X.data_ptr(), ld, sX, X.data_ptr(), ld, sX, B, r0,
+                                              nn, status.data_ptr(), 1, st),
+                      "pfml_spd_leafinv_to")
+            return
+        h = _rec_split(nn)
+        m = nn - h
+        a, c, e = r0, r0 + h, r0 + nn
+        rec(a, h, depth + 1)
+        W = buf(depth, h, m)
+        gemm_fused(X[:, a:c, a:c], X[:, a:c, c:e], W, tile_cfg=cfg)              # W = X11 A12
+        gemm_fused(X[:, c:e, a:c], W, X[:, c:e, c:e], alpha=-1.0, beta=1.0, sym=True,
+                   tile_cfg=cfg)                                                  # S
+        rec(c, m, depth + 1)
+        gemm_fused(W, X[:, c:e, c:e], X[:, a:c, c:e], alpha=-1.0, mirror_out=X[:, c:e, a:c],
+                   tile_cfg=cfg)                                                  # X12, X21
+        gemm_fused(X[:, a:c, c:e], W, X[:, a:c, a:c], trans_b=True, alpha=-1.0, beta=1.0,
+                   sym=True, tile_cfg=cfg)                                        # X11 -= X12 W'
+
+    rec(0, n, 0)
+    return X
 
 
 def _lu_max_n() -> int:
@@ -423,11 +482,14 @@ DB_SCALED_ITERS = 6
 
 def m_tilde(sigma: torch.Tensor, lam: torch.Tensor, w: torch.Tensor, rf: torch.Tensor,
             mu: float, gamma: float, iterations: int = 10, mask: torch.Tensor | None = None,
-            db_iters: int = DB_ITERS) -> tuple[torch.Tensor, torch.Tensor]:
+            db_iters: int = DB_ITERS, status: torch.Tensor | None = None
+            ) -> tuple[torch.Tensor, torch.Tensor]:
     """m_tilde of Lemma 1 and a = lambda^-1/2, so that m = diag(a) m_tilde diag(1/a)
     (General_functions.py:941-963).  All on the device with no host synchronisation except one
     status check at the end (matrices whose SPD inverse met a non-positive pivot anywhere in
-    the chain are recomputed by the reference-form ``m_func_reference``)."""
+    the chain are recomputed by the reference-form ``m_func_reference``).  ``status`` (a
+    zeroed [B] int32 device tensor): the flags are left there and NOT checked - no host sync
+    at all (graph capture); the caller repairs the flagged months itself."""
     B, N, _ = sigma.shape
     dt, dev = sigma.dtype, sigma.device
     if mask is None:
@@ -437,7 +499,9 @@ def m_tilde(sigma: torch.Tensor, lam: torch.Tensor, w: torch.Tensor, rf: torch.T
     s = (gamma / w).to(dt).contiguous()
     c = (1.0 + rf + mu).to(dt).contiguous()
     sigma = sigma.contiguous()
-    status = torch.zeros(B, dtype=torch.int32, device=dev) if nat.is_device(sigma) else None
+    deferred = status is not None
+    if not deferred:
+        status = torch.zeros(B, dtype=torch.int32, device=dev) if nat.is_device(sigma) else None
     x = torch.empty_like(sigma)
     mf_sym(MF_X, sigma, None, x, svec=s, a=a)                   # x = s L^-1/2 S L^-1/2
     S = torch.empty_like(sigma)
@@ -448,14 +512,16 @@ def m_tilde(sigma: torch.Tensor, lam: torch.Tensor, w: torch.Tensor, rf: torch.T
     # m_tilde_0 = (sigma_hat - root)/2 = 2 (sigma_hat + root)^-1   (cancellation-free form)
     mt = ws[2]
     mf_sym(MF_SHAT, x, root, mt, d=2.0)
-    spd_inverse(mt, inplace=True, status=status)
+    # (the 11 inverses below are of exactly symmetric arguments and only used symmetrically:
+    # the one-triangle form; the Denman-Beavers product above keeps the two-sided one)
+    spd_inverse_sym(mt, status)
     mt.mul_(2.0)
     Aq = ws[3]
     for _ in range(iterations):
         mf_sym(MF_FIX, sigma, mt, Aq, svec=s, cvec=c, a=a, mask=mask)
-        spd_inverse(Aq, inplace=True, status=status)
+        spd_inverse_sym(Aq, status)
         mt, Aq = Aq, mt
-    if status is not None:
+    if status is not None and not deferred:
         bad = torch.nonzero(status).flatten()
         if bad.numel():
             COUNTERS.add("linalg.m_func_repaired", int(bad.numel()))

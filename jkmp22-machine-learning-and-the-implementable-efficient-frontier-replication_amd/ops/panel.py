@@ -50,7 +50,7 @@ def rff_features(X: torch.Tensor, W: torch.Tensor, precision: str = "fp64",
                                                 nat.stream_of(X)), "pfml_rff_sincos")
     else:
         out = torch.zeros((R + pad_rows, width), dtype=X.dtype, device=X.device)
-        out[:R, 0] = 1.0
+        out[:R, 0].fill_(1.0)
         out[:R, 1:P:2] = torch.cos(Z)
         out[:R, 2:P:2] = torch.sin(Z)
     return out
@@ -88,7 +88,7 @@ def standardize_signals(F: torch.Tensor, idx: torch.Tensor, mask: torch.Tensor,
     m = mask.view(B, 1, N, 1)
     n = mask.sum(1).view(B, 1, 1, 1)
     mean = (S * m).sum(2, keepdim=True) / n
-    mean[..., 0] = 0.0                                          # constant is not demeaned
+    mean[..., 0].fill_(0.0)                                     # constant is not demeaned
     S = (S - mean) * m
     norm = torch.sqrt(1.0 / (S * S).sum(2, keepdim=True))
     S = S * norm

@@ -451,7 +451,11 @@ def ridge_launch(plan: dict, d_desc: torch.Tensor, SD: torch.Tensor, Sr: torch.T
         raise ValueError("ridge_launch: the cooperative reduction needs the device wgmap")
     sync = (torch.empty(plan["nc"] * COOP_SYNC_WORDS, dtype=torch.int32, device=SD.device)
             if band else None)
-    LAST_COOP_SYNC[:] = [sync] if band else []
+    if band:
+        _spin_from_env()
+        # every launch's sync words are kept until the next grid search starts (the big and the
+        # small cells' launches run on two streams: neither may hide the other's timeouts)
+        LAST_COOP_SYNC.append(sync)
     nat.check(nat.hip_lib().pfml_ridge_grid(SD.data_ptr(), P, Sr.data_ptr(), d_desc.data_ptr(),
                                             plan["nc"], plan["nmax"], lv.data_ptr(), L,
                                             work.data_ptr(), beta.data_ptr(), beta.shape[-1],
@@ -466,17 +470,40 @@ def ridge_launch(plan: dict, d_desc: torch.Tensor, SD: torch.Tensor, Sr: torch.T
     return count
 
 
-# sync words of the most recent cooperative launch (tests read the error word: index 1 of
-# every cell's COOP_SYNC_WORDS)
+# sync words of the cooperative launches since the last ``reset_coop_sync`` (one per launch;
+# the error word is index 1 of every cell's COOP_SYNC_WORDS): a timed-out cell's betas are NaN
+# (the back-transform poisons them) and the grid search's non-finite recovery recomputes them
 LAST_COOP_SYNC: list = []
+nat.register_hip("pfml_coop_set_spin_max", [C.c_uint], None)
+
+
+def reset_coop_sync() -> None:
+    LAST_COOP_SYNC.clear()
 
 
 def coop_errors() -> int:
-    """Number of cells of the last cooperative launch whose spin-wait timed out (host sync)."""
+    """Number of cells whose cooperative hand-off wait timed out, over every launch since the
+    last ``reset_coop_sync`` (one host sync)."""
     if not LAST_COOP_SYNC:
         return 0
-    s = LAST_COOP_SYNC[0].view(-1, COOP_SYNC_WORDS)
-    return int((s[:, 1] != 0).sum().item())
+    return int(sum(int((s.view(-1, COOP_SYNC_WORDS)[:, 1] != 0).sum().item())
+                   for s in LAST_COOP_SYNC))
+
+
+_SPIN_ENV: list = []
+
+
+def set_coop_spin_max(n: int) -> None:
+    """Poll bound of the cooperative reduction's waits for later launches (0: the default,
+    ~1 s).  Tests lower it to force timeouts; ``PFML_COOP_SPIN_MAX`` sets it before the first
+    launch."""
+    _SPIN_ENV[:] = [True]
+    nat.hip_lib().pfml_coop_set_spin_max(int(n))
+
+
+def _spin_from_env() -> None:
+    if not _SPIN_ENV:
+        set_coop_spin_max(int(os.environ.get("PFML_COOP_SPIN_MAX", "0") or 0))
 
 
 def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n: np.ndarray,
@@ -495,6 +522,7 @@ def ridge_grid(SD: torch.Tensor, Sr: torch.Tensor, cell_src: np.ndarray, cell_n:
     if nc == 0:
         return beta
     if nat.is_device(SD):
+        reset_coop_sync()
         plan = ridge_plan(P, L, cell_src, cell_n, cell_scale, ncu=num_cus(SD.device))
         d_desc, d_wg = upload([plan["desc"], plan["wgmap"]], SD.device)
         lv = lvec.to(device=SD.device, dtype=torch.float64).contiguous()
@@ -645,6 +673,7 @@ def ridge_utilities(SD: torch.Tensor, Sr: torch.Tensor, cell_src, cell_n, cell_s
         beta = ridge_grid(SD, Sr, cell_src, cell_n, cell_scale, lvec)
         return beta, quadform_utilities(D, R, beta, job_cell, job_month, job_n)
     split = two_streams() and len(np.unique(cell_n)) >= 2
+    reset_coop_sync()
     th = _HostClock()
     S, P, _ = SD.shape
     check_launch_bounds(S, P, D.shape[0], cell_src, cell_n, job_cell, job_month, job_n)

@@ -273,6 +273,13 @@ class Pipeline:
         if self.cfg.run.fault_inject.startswith("pfml-search-coef") and grid.beta.shape[1]:
             grid.beta[0, 0, -1, len(grid.l_vec) // 2, 0] = float("nan")
             COUNTERS.add("fault_injected")
+        if grid.beta.is_cuda:
+            from .ops.ridge import coop_errors
+            nto = coop_errors()          # cooperative hand-off timeouts: those cells are NaN
+            if nto:
+                COUNTERS.add("ridge.coop_timeouts", nto)
+                log.warning(f"{nto} cell(s) of the cooperative band reduction timed out on rank "
+                            f"{self.env.rank}: their NaN betas are recomputed below")
         bad = search.nonfinite_cells(grid)
         res = {"recomputed": 0, "singular": 0}
         if bad:

@@ -63,7 +63,7 @@ def test_gemm_epi_struct_matches():
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("shape", [(2, 37, 53, 29), (3, 130, 258, 100), (2, 96, 224, 96)])
 def test_gemm_fused_matches_torch(gpu, ta, tb, cfg, shape):
     """Every fusion of csrc/gemm_f64.hip (k-scale prologue, row/col scale, beta, addend block,
@@ -91,6 +91,59 @@ def test_gemm_fused_matches_torch(gpu, ta, tb, cfg, shape):
                      addend=E.to(gpu), addend_cols=8, diag_col0=8, diag_value=1.0,
                      tile_cfg=cfg).cpu()
     assert (out - ref).abs().max().item() / ref.abs().max().item() < 1e-13
+
+
+@pytest.mark.parametrize("cfg", [1, 3, 6, 7])
+@pytest.mark.parametrize("shape", [(3, 234, 256), (2, 130, 100), (2, 37, 29)])
+def test_gemm_sym_and_mirror(gpu, cfg, shape):
+    """Symmetric mode (only the output tiles on / below the diagonal, lower triangle mirrored:
+    an exactly symmetric result) and the transposed second output of csrc/gemm_f64.hip vs
+    the torch oracle of the same definition, for every square tile config."""
+    from pfml.ops.gemm import gemm_fused
+    b, n, K = shape
+    A, B = _rand(b, n, K, seed=1), _rand(b, K, n, seed=2)
+    C0 = _rand(b, n, n, seed=3)
+    C0 = C0 + C0.transpose(1, 2)
+    ref = gemm_fused(A, B, C0.clone(), alpha=-1.0, beta=1.0, sym=True)
+    out = gemm_fused(A.to(gpu), B.to(gpu), C0.to(gpu), alpha=-1.0, beta=1.0, sym=True,
+                     tile_cfg=cfg).cpu()
+    assert torch.equal(out, out.transpose(1, 2))                     # exactly symmetric
+    assert (out - ref).abs().max().item() / ref.abs().max().item() < 1e-13
+    Bt = _rand(b, n, K, seed=4)
+    ref = gemm_fused(A, Bt, C0.clone(), trans_b=True, alpha=-1.0, beta=1.0, sym=True)
+    out = gemm_fused(A.to(gpu), Bt.to(gpu), C0.to(gpu), trans_b=True, alpha=-1.0, beta=1.0,
+                     sym=True, tile_cfg=cfg).cpu()
+    assert torch.equal(out, out.transpose(1, 2))
+    assert (out - ref).abs().max().item() / ref.abs().max().item() < 1e-13
+    # rectangular product with its transpose written by the same launch
+    B2 = _rand(b, K, n + 6, seed=5)
+    X = torch.empty(b, n, n + 6, dtype=torch.float64, device=gpu)
+    Xt = torch.full((b, n + 6, n), float("nan"), dtype=torch.float64, device=gpu)
+    gemm_fused(A.to(gpu), B2.to(gpu), X, alpha=-1.0, mirror_out=Xt, tile_cfg=cfg)
+    ref = -(A @ B2)
+    assert (X.cpu() - ref).abs().max().item() / ref.abs().max().item() < 1e-13
+    assert torch.equal(Xt.cpu(), X.cpu().transpose(1, 2))
+
+
+@pytest.mark.parametrize("n", [490, 257, 200])
+def test_spd_inverse_sym(gpu, n):
+    """Symmetric recursive SPD inverse (one-triangle Schur products, mirrored): exactly
+    symmetric, and as close to the LU inverse as the two-sided form on a moderately
+    conditioned batch."""
+    from pfml.ops.linalg import spd_inverse, spd_inverse_sym
+    g = torch.Generator().manual_seed(n)
+    X = torch.randn(4, n + 40, n, generator=g, dtype=torch.float64)
+    A = X.transpose(1, 2) @ X / n + 1e-3 * torch.eye(n, dtype=torch.float64)
+    A = 0.5 * (A + A.transpose(1, 2))
+    ref = torch.linalg.inv(A)
+    st = torch.zeros(4, dtype=torch.int32, device=gpu)
+    out = spd_inverse_sym(A.to(gpu).contiguous(), st).cpu()
+    assert int(st.sum()) == 0
+    assert torch.equal(out, out.transpose(1, 2))
+    e_sym = ((out - ref).norm(dim=(1, 2)) / ref.norm(dim=(1, 2))).max().item()
+    two = spd_inverse(A.to(gpu)).cpu()
+    e_two = ((two - ref).norm(dim=(1, 2)) / ref.norm(dim=(1, 2))).max().item()
+    assert e_sym < 1e-11 and e_sym < 4 * e_two + 1e-14, (e_sym, e_two)
 
 
 def test_segment_sums(gpu):

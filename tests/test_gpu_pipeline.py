@@ -162,6 +162,54 @@ def test_pfml_inputs_gpu_matches_cpu(gpu, small_data):
                                   atol=1e-13)
 
 
+def test_s4_hip_graph_replay_matches_eager(gpu, small_data):
+    """S4 (run_plan with its checks deferred: no host sync) captured as ONE HIP graph replays
+    to bitwise the eager run's r_tilde / denom (PFML_Input_Data.py:318-491), and the deferred
+    checks (finish_inputs) then run once."""
+    import sys
+    from pfml.config import get_features
+    from pfml.data import io
+    from pfml.models.pfml_inputs import finish_inputs, make_s4_plan, run_plan
+    from pfml.models.risk import BarraCov
+    from pfml.utils.dates import pfml_date_grids
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    cfg = small_data
+    d = cfg.run.data_dir
+    chars = io.read_processed_chars(d, get_features())
+    barra = BarraCov.load(os.path.join(d, "Barra_Cov.npz"))
+    wealth = pd.read_csv(os.path.join(d, "wealth_processed.csv"), parse_dates=["eom"])
+    rf = io.read_risk_free(d)
+    g = pfml_date_grids(int(barra.months.min()), 11, cfg.settings["split"]["test_end"], 1971, 10)
+    plan = make_s4_plan(cfg, chars, barra, wealth, rf, gpu, months=g["m2"][:30], batch=16)
+    eager = finish_inputs(plan, cfg, run_plan(plan, cfg, defer_checks=True))
+    box = {}
+
+    def step():
+        box["out"] = run_plan(plan, cfg, defer_checks=True)
+
+    rep = bench.graphed(step, gpu)
+    assert rep is not None
+    box["out"].reals.denom.zero_()
+    rep()
+    torch.cuda.synchronize()
+    out = finish_inputs(plan, cfg, box["out"])
+    assert torch.equal(out.reals.denom, eager.reals.denom)
+    assert torch.equal(out.reals.r_tilde, eager.reals.r_tilde)
+    # the deferred repair path: months flagged on the device are re-run as one sub-batch and
+    # patched in (here nothing needs repair, so the re-run must give the same bits: a month's
+    # summands do not depend on the months batched with it)
+    again = run_plan(plan, cfg, defer_checks=True)
+    again.pending["mstat"][torch.tensor([3, 17, 29], device=gpu)] = 1
+    again.reals.denom[:, 3] = float("nan")
+    fixed = finish_inputs(plan, cfg, again)
+    assert torch.equal(fixed.reals.denom, eager.reals.denom)
+    assert torch.equal(fixed.reals.r_tilde, eager.reals.r_tilde)
+    for gg in range(len(eager.signal_t)):
+        assert torch.equal(fixed.signal_t[gg][17], eager.signal_t[gg][17])
+
+
 def test_full_pipeline_gpu(gpu, small_data, tmp_path):
     """S4-S9 on the device against the same stages on the CPU oracle path, from copies of the
     same L0-L3 data: every validation utility (obj, cum_obj) to 1e-8, the ranks (hence the

@@ -95,3 +95,45 @@ def test_coop_k_policy_big_cells_share(monkeypatch):
     assert (coop_k(np.array([129] * 5 + [65]), 256) == 1).all()   # no n > 256 cell: K = 1
     monkeypatch.setenv("PFML_COOP_K", "3")
     assert coop_k(np.array([513] * 106 + [65]), 256)[0] == 3
+
+
+@pytest.mark.gpu
+def test_coop_timeout_poisons_and_guard_recovers(gpu, monkeypatch):
+    """A cooperative hand-off that times out never yields silent garbage: with the poll bound
+    forced down to one poll (K = 2 workgroups per big cell) the timed-out cells come back as
+    NaN betas, are counted (coop_errors), and the S5 recovery (nonfinite_cells ->
+    recompute_cells, the reference's np.linalg.solve per lambda) ends with the CPU oracle's
+    betas and utilities (PFML_Search_Coef.py:131-133)."""
+    from pfml.config import Config
+    from pfml.models.search import (PfmlReals, grid_search, nonfinite_cells, recompute_cells)
+    from pfml.ops import ridge as rg
+    from pfml.utils.dates import mi_from_ym
+    cfg = Config.default().override(["pf_ml.p_vec=[32,64]", "pf.dates.start_year=2002",
+                                     "pf.dates.end_yr=2006"])
+    G, P = 2, 65
+    months = np.arange(mi_from_ym(1995, 1), mi_from_ym(2006, 11) + 1)
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(G * len(months), 90, P, generator=g, dtype=torch.float64)
+    D = (X.transpose(1, 2) @ X / 90).view(G, len(months), P, P)
+    r = 0.1 * torch.randn(G, len(months), P, generator=g, dtype=torch.float64)
+    clean = grid_search(PfmlReals(months, r, D), cfg)
+    reals = PfmlReals(months, r.to(gpu), D.to(gpu).contiguous())
+    monkeypatch.setenv("PFML_COOP_K", "2")
+    rg.set_coop_spin_max(1)
+    try:
+        grid = grid_search(reals, cfg, gather=False)
+        nto = rg.coop_errors()
+    finally:
+        rg.set_coop_spin_max(0)
+    assert nto > 0
+    bad = nonfinite_cells(grid)
+    assert len(bad) >= 1
+    res = recompute_cells(grid, reals, bad)
+    assert res["recomputed"] == len(bad) and res["singular"] == 0
+    assert nonfinite_cells(grid) == []
+    assert torch.allclose(grid.beta.cpu(), clean.beta, rtol=1e-9, atol=1e-12)
+    assert torch.allclose(grid.obj.cpu(), clean.obj, rtol=1e-9, atol=1e-12)
+    # back at the default bound: no timeouts
+    grid2 = grid_search(reals, cfg, gather=False)
+    assert rg.coop_errors() == 0
+    assert torch.allclose(grid2.beta.cpu(), clean.beta, rtol=1e-9, atol=1e-12)

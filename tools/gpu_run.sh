@@ -65,6 +65,19 @@ for step in ${MODE//,/ }; do
       rc=$?; tail -1 $OUT/dgemm_shapes.log; if [ $rc -ne 0 ]; then tail -5 $OUT/dgemm_shapes.log; exit $rc; fi
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/dgemm_pmc -o run -- python3 $ROOT/tools/micro/dgemm_shapes.py 2 > $OUT/dgemm_pmc.log 2>&1)
       rc=$?; python tools/pmc_summary.py $OUT/dgemm_pmc --top 8 > $OUT/dgemm_pmc.txt 2>&1; cat $OUT/dgemm_pmc.txt; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    gemmtest)
+      # GEMM / SPD-inverse kernel tests only (fast numerics check of a kernel change)
+      timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -k "gemm or spd_inverse or mfma" -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gemm.log 2>&1
+      rc=$?; tail -2 $OUT/pytest_gemm.log
+      if [ $rc -ne 0 ]; then grep -E "^E |FAILED" $OUT/pytest_gemm.log | head -20; exit $rc; fi ;;
+    gemmclk)
+      # Horner / DB-product GEMMs: effective clock and MFMA-pipe busy (one PMC pass)
+      (cd /tmp && export TMPDIR=/tmp && PFML_DGEMM_SHAPES=${PFML_DGEMM_SHAPES:-horner,db_prod} PFML_DGEMM_CFGS=${PFML_DGEMM_CFGS:-3,8} timeout -s KILL 180 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --output-format csv -d $OUT/gemmclk -o run -- python3 $ROOT/tools/micro/dgemm_shapes.py 3 > $OUT/gemmclk.log 2>&1)
+      rc=$?; python tools/pmc_summary.py $OUT/gemmclk --top 8 > $OUT/gemmclk.txt 2>&1; cat $OUT/gemmclk.txt
+      if [ $rc -ne 0 ]; then tail -5 $OUT/gemmclk.log; exit $rc; fi ;;
+    shapes)
+      timeout -k 10 400 python tools/micro/dgemm_shapes.py 5 > $OUT/shapes.log 2>&1
+      rc=$?; grep -v '^{' $OUT/shapes.log; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     suite)
       timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
       rc=$?; tail -2 $OUT/pytest_gpu.log
@@ -152,10 +165,6 @@ for step in ${MODE//,/ }; do
       timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "${PFML_KTEST}" > $OUT/pytest_k.log 2>&1
       rc=$?; tail -3 $OUT/pytest_k.log
       if [ $rc -ne 0 ]; then grep -E "^E |FAILED" $OUT/pytest_k.log | head -20; exit $rc; fi ;;
-    diag)
-      # staged fault hunt: PFML_DIAG = options of tools/diag_shard.py (setdev, env)
-      timeout -k 10 300 python tools/diag_shard.py ${PFML_DIAG} > $OUT/diag_${PFML_DIAG// /_}.log 2>&1
-      rc=$?; grep -v "^frame" $OUT/diag_${PFML_DIAG// /_}.log | tail -30; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     e2e)
       # production-shape end-to-end run of `main` (SURVEY §7 north star): synthetic raw data of
       # the production shape (500 stocks, 1952-2023), the two S0 stages, then the 8 stages of

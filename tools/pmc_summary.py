@@ -43,6 +43,18 @@ def main():
                     .str.replace(r"^void ", "", regex=True).str.replace(r"\(.*", "", regex=True)
                     .str.slice(0, 48))
     piv = df.pivot_table(index="kernel", columns="counter", values="value", aggfunc="sum")
+    tr = glob.glob(os.path.join(a.dir, "**", "*kernel_trace.csv"), recursive=True)
+    if tr:
+        # per-kernel time from the trace of the same run; GRBM_GUI_ACTIVE is summed over the 8
+        # XCDs (MI355X_MICROARCH.md, DVFS give-back): effective clock = it / 8 / time
+        t = pd.read_csv(tr[0])
+        t["kernel"] = (t["Kernel_Name"].str.replace("(anonymous namespace)::", "", regex=False)
+                       .str.replace(r"^void ", "", regex=True)
+                       .str.replace(r"\(.*", "", regex=True).str.slice(0, 48))
+        t["ns"] = t["End_Timestamp"] - t["Start_Timestamp"]
+        piv["time_us"] = t.groupby("kernel")["ns"].sum() / 1e3
+        if "GRBM_GUI_ACTIVE" in piv:
+            piv["clk_ghz"] = piv["GRBM_GUI_ACTIVE"] / 8.0 / (piv["time_us"] * 1e3)
     first = piv.columns[0]
     piv = piv.sort_values(first, ascending=False).head(a.top)
     pd.set_option("display.width", 250)
