@@ -48,6 +48,11 @@ struct Epi {
                                       // and below the diagonal run; v lands at (i, j), i >= j,
                                       // and is mirrored to (j, i) - exactly symmetric C
   double* Ct; int64_t ldct, sCt;      // optional transposed copy: Ct[j][i] = v (X21 = X12')
+  // gathered addend (erow != null): addend(i, j) = (E[erow[i]][j] - ecm[j]) * ecs[j], times the
+  // row scale es[i] - the standardised signal S_theta formed from the panel features where the
+  // Horner step consumes it (K11/K12 fused into K5/K6: S_theta is never stored)
+  const int64_t* erow; int64_t serow;
+  const double* ecm; const double* ecs; int64_t secm;
 };
 
 // Output tile of workgroup wg: batch entry b, first row bm / column bn.  Grouped order:
@@ -80,10 +85,30 @@ __device__ __forceinline__ void map_tile(int wg, int tiles_m, int tiles_n, bool 
   bn = (in / gm) * BN;
 }
 
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+// Buffer descriptor over [p, p + bytes) built from readfirstlane'd words: provably
+// wave-uniform, so hipcc keeps it in SGPRs instead of wrapping every buffer op in a
+// readfirstlane "waterfall" loop (cdna_hip_programming.md T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, unsigned bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const unsigned n = __builtin_amdgcn_readfirstlane(bytes);
+  void* q = (void*)(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, 0, (int)n, 0x00020000);
+}
+
 // The fused epilogue of one wave's (TM x 16) x (TN x 16) accumulator block (rows from r0,
 // columns from c0 of batch entry b's C): alpha, row / column scales, beta C, the row-scaled
 // addend block, the diagonal, then the store (symmetric: lower triangle + mirror; Ct: the
-// transposed copy).
+// transposed copy).  One 16-row slice at a time: every load of the slice (row / column
+// scales, C for beta, the addend) is issued first, from clamped always-valid addresses, then
+// the values are computed branch-free and stored through buffer descriptors, a masked
+// element's offset past the range (the store is dropped by the range check).  Per-element
+// guarded loads / stores made hipcc emit a load -> wait -> store round trip per element (32
+// L2 round trips per wave on a 128 x 64 tile: as long as the K = 128 main loop of the SPD
+// inverse's GEMMs).  Needs every C / Ct batch entry below 2 GB (checked by the host).
 template <int TM, int TN>
 __device__ __forceinline__ void store_tile(const double4_t (&acc)[TM][TN], const Epi& ep, int b,
                                            int r0, int c0, int lane, int M, int N,
@@ -94,28 +119,71 @@ __device__ __forceinline__ void store_tile(const double4_t (&acc)[TM][TN], const
   const double* dvb = ep.dv ? ep.dv + (int64_t)b * ep.sdv : nullptr;
   const double* esb = ep.es ? ep.es + (int64_t)b * ep.ses : nullptr;
   double* Ctb = ep.Ct ? ep.Ct + (int64_t)b * ep.sCt : nullptr;
+  const unsigned cbytes = (unsigned)(((int64_t)(M - 1) * ldc + N) * 8);
+  const auto rsC = uniform_rsrc(C, cbytes);
+  const unsigned tbytes = Ctb ? (unsigned)(((int64_t)(N - 1) * ep.ldct + M) * 8) : 0u;
+  const auto rsT = uniform_rsrc(Ctb ? Ctb : C, tbytes);
   const int li = lane & 15;
+  const bool has_beta = ep.beta != 0.0;
+  const bool has_e = Eb != nullptr && ep.e_cols > 0;
+  const int64_t* erb = ep.erow ? ep.erow + (int64_t)b * ep.serow : nullptr;
+  int gjc[TN], gje[TN];
+  double csv[TN], ecmv[TN], ecsv[TN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int j = 0; j < TN; ++j) {
+    gjc[j] = min(c0 + j * 16 + li, N - 1);
+    gje[j] = min(gjc[j], ep.e_cols - 1);
+    csv[j] = csb ? csb[gjc[j]] : 1.0;
+    ecmv[j] = (has_e && erb) ? ep.ecm[(int64_t)b * ep.secm + gje[j]] : 0.0;
+    ecsv[j] = (has_e && erb) ? ep.ecs[(int64_t)b * ep.secm + gje[j]] : 1.0;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int gic[4];
+    int64_t erw[4];
+    double rsv[4], esv[4], dvv[4], cv[TN][4], ev[TN][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      gic[r] = min(r0 + i * 16 + PFML_F64_CROW(lane, r), M - 1);
+      erw[r] = erb ? erb[gic[r]] : (int64_t)gic[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      rsv[r] = rsb ? rsb[gic[r]] : 1.0;
+      esv[r] = esb ? esb[gic[r]] : 1.0;
+      dvv[r] = dvb ? dvb[gic[r]] : ep.dval;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        cv[j][r] = has_beta ? C[(int64_t)gic[r] * ldc + gjc[j]] : 0.0;
+        ev[j][r] = has_e ? Eb[erw[r] * ep.lde + gje[j]] : 0.0;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int gi = r0 + i * 16 + PFML_F64_CROW(lane, r);
         const int gj = c0 + j * 16 + li;
-        if (gi < M && gj < N && (!ep.sym || gi >= gj)) {
-          double v = ep.alpha * acc[i][j][r];
-          if (rsb) v *= rsb[gi];
-          if (csb) v *= csb[gj];
-          double* cp = C + (int64_t)gi * ldc + gj;
-          if (ep.beta != 0.0) v += ep.beta * (*cp);
-          if (Eb && gj < ep.e_cols) v += (esb ? esb[gi] : 1.0) * Eb[(int64_t)gi * ep.lde + gj];
-          if (ep.has_diag && gj - ep.diag_col0 == gi) v += dvb ? dvb[gi] : ep.dval;
-          *cp = v;
-          if (ep.sym && gi > gj) C[(int64_t)gj * ldc + gi] = v;
-          if (Ctb) Ctb[(int64_t)gj * ep.ldct + gi] = v;
-        }
+        double v = ep.alpha * acc[i][j][r];
+        v *= rsv[r];
+        v *= csv[j];
+        v += has_beta ? ep.beta * cv[j][r] : 0.0;
+        v += (has_e && gj < ep.e_cols)
+                 ? esv[r] * (erb ? (ev[j][r] - ecmv[j]) * ecsv[j] : ev[j][r]) : 0.0;
+        v += (ep.has_diag && gj - ep.diag_col0 == gi) ? dvv[r] : 0.0;
+        const bool ok = gi < M && gj < N && (!ep.sym || gi >= gj);
+        const u32x2_t bits = __builtin_bit_cast(u32x2_t, v);
+        __builtin_amdgcn_raw_buffer_store_b64(
+            bits, rsC, ok ? (unsigned)(((int64_t)gi * ldc + gj) * 8) : cbytes, 0, 0);
+        if (ep.sym)
+          __builtin_amdgcn_raw_buffer_store_b64(
+              bits, rsC, (ok && gi > gj) ? (unsigned)(((int64_t)gj * ldc + gi) * 8) : cbytes, 0,
+              0);
+        if (Ctb)
+          __builtin_amdgcn_raw_buffer_store_b64(
+              bits, rsT, ok ? (unsigned)(((int64_t)gj * ep.ldct + gi) * 8) : tbytes, 0, 0);
       }
+  }
 }
 
 typedef double double2_t __attribute__((ext_vector_type(2)));
@@ -326,10 +394,11 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(
 // scaling B: one multiply per element of the sum); the K tail (k >= K) is zeroed in the A
 // fragment (the DMA reads clamped, finite addresses).
 // ---------------------------------------------------------------------------------------
-template <int R, bool KCONTIG>
+template <int R, bool KCONTIG, int NW = 4>
 struct GImg {
   static constexpr int SIZE = R * 16;              // doubles per stage
-  static constexpr int NI = R / 32;                // DMA instructions per wave per stage
+  static constexpr int NI = R / 8 / NW;            // DMA instructions per wave per stage
+  static_assert(NI >= 1 && NI * NW * 8 == R, "tile rows must split over the waves");
   // offset (doubles) of element (idx, k) inside the image
   static __device__ __forceinline__ int at(int idx, int k) {
     return KCONTIG ? idx * 16 + (((k >> 1) ^ ((idx >> 1) & 7)) << 1) + (k & 1)
@@ -356,20 +425,39 @@ __device__ __forceinline__ void glds16(const double* g, double* l) {
                                    (__attribute__((address_space(3))) void*)l, 16, 0, 0);
 }
 
-template <bool TA, bool TB, int BM, int BN, bool KSC>
-__global__ __launch_bounds__(256, 2) void dgemm_glds_kernel(
+// NS LDS stages: NS = 2 waits for the next step's DMA at the end of each step (vmcnt(0) in
+// __syncthreads); NS = 3 keeps the step after next in flight across the barrier (a counted
+// vmcnt of one stage's DMA instructions, raw s_barrier), for operands that come from HBM.
+template <int N> __device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+  else static_assert(N <= 9, "vmcnt count");
+}
+
+template <bool TA, bool TB, int BM, int BN, bool KSC, int WM = 2, int WN = 2, int NS = 2>
+__global__ __launch_bounds__(64 * WM * WN, 2) void dgemm_glds_kernel(
     int M, int N, int K, int tiles_m, int tiles_n, int nwg,
     const double* __restrict__ A, int64_t lda, int64_t sA,
     const double* __restrict__ B, int64_t ldb, int64_t sB,
     double* __restrict__ C, int64_t ldc, int64_t sC, Epi ep) {
   constexpr int BK = 16;
-  constexpr int TM = BM / 32, TN = BN / 32;
-  using IA = GImg<BM, !TA>;                        // A stored M x K: k-contiguous
-  using IB = GImg<BN, TB>;                         // B stored N x K: k-contiguous
+  constexpr int NW = WM * WN;                      // waves: WM x WN, each (BM/WM) x (BN/WN)
+  constexpr int TM = BM / 16 / WM, TN = BN / 16 / WN;
+  using IA = GImg<BM, !TA, NW>;                    // A stored M x K: k-contiguous
+  using IB = GImg<BN, TB, NW>;                     // B stored N x K: k-contiguous
   constexpr int STAGE = IA::SIZE + IB::SIZE;
+  static_assert(NS == 2 || NS == 3, "stages");
   // ONE shared array (a second __shared__ object can make hipcc wait for the DMA before
   // every LDS read: cdna_hip_programming.md §5, "Projection GEMM" item 4a)
-  __shared__ __attribute__((aligned(16))) double smem[2 * STAGE + 2 * BK];
+  __shared__ __attribute__((aligned(16))) double smem[NS * STAGE + NS * BK];
 
   const int wg = xcd_remap(blockIdx.x, nwg);
   int b, bm, bn;
@@ -380,13 +468,14 @@ __global__ __launch_bounds__(256, 2) void dgemm_glds_kernel(
   const double* ks = KSC ? ep.ks + (int64_t)b * ep.sks : nullptr;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / WN, wn = w % WN;
   const int li = lane & 15, lk = lane >> 4;
   const int nk = (K + BK - 1) / BK;
 
+  auto slot = [&](int s) { return NS == 2 ? (s & 1) : s % 3; };
   auto issue = [&](int s) {
     const int k0 = s * BK;
-    double* img = smem + (s & 1) * STAGE;
+    double* img = smem + slot(s) * STAGE;
 #pragma unroll
     for (int q = 0; q < IA::NI; ++q) {
       const int g = w * IA::NI + q;
@@ -398,7 +487,8 @@ __global__ __launch_bounds__(256, 2) void dgemm_glds_kernel(
       glds16(B + IB::src(g, lane, bn, N, k0, K, ldb), img + IA::SIZE + g * 128);
     }
     if constexpr (KSC) {
-      if (w == 0 && lane < BK / 2) glds16(ks + min(k0 + 2 * lane, K - 2), smem + 2 * STAGE + (s & 1) * BK);
+      if (w == 0 && lane < BK / 2)
+        glds16(ks + min(k0 + 2 * lane, K - 2), smem + NS * STAGE + slot(s) * BK);
     }
   };
 
@@ -408,11 +498,25 @@ __global__ __launch_bounds__(256, 2) void dgemm_glds_kernel(
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = double4_t{0.0, 0.0, 0.0, 0.0};
 
+  // DMA instructions of one stage issued by this wave (wave 0 also loads the k-scale)
+  constexpr int NIW = IA::NI + IB::NI;
   issue(0);
-  __syncthreads();
+  if constexpr (NS == 3) {
+    if (nk > 1) issue(1);
+    // stage 0 landed (this wave's DMA; the barrier: every wave's), stage 1 may still fly
+    if (nk > 1) {
+      if (KSC && w == 0) wait_vm<NIW + 1>(); else wait_vm<NIW>();
+    } else {
+      wait_vm<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  } else {
+    __syncthreads();
+  }
   for (int s = 0; s < nk; ++s) {
-    if (s + 1 < nk) issue(s + 1);
-    const double* ia = smem + (s & 1) * STAGE;
+    if (s + NS - 1 < nk) issue(s + NS - 1);
+    const double* ia = smem + slot(s) * STAGE;
     const double* ib = ia + IA::SIZE;
     const bool tail = (s + 1) * BK > K;
 #pragma unroll
@@ -420,11 +524,11 @@ __global__ __launch_bounds__(256, 2) void dgemm_glds_kernel(
       const int k = kk + lk;
       double a[TM], bb[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) a[i] = ia[IA::at(wm * (BM / 2) + i * 16 + li, k)];
+      for (int i = 0; i < TM; ++i) a[i] = ia[IA::at(wm * (BM / WM) + i * 16 + li, k)];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bb[j] = ib[IB::at(wn * (BN / 2) + j * 16 + li, k)];
+      for (int j = 0; j < TN; ++j) bb[j] = ib[IB::at(wn * (BN / WN) + j * 16 + li, k)];
       if constexpr (KSC) {
-        const double kv = smem[2 * STAGE + (s & 1) * BK + k];
+        const double kv = smem[NS * STAGE + slot(s) * BK + k];
 #pragma unroll
         for (int i = 0; i < TM; ++i) a[i] *= kv;
       }
@@ -438,12 +542,23 @@ __global__ __launch_bounds__(256, 2) void dgemm_glds_kernel(
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f64_16x16x4(a[i], bb[j], acc[i][j]);
     }
-    __syncthreads();
+    if constexpr (NS == 3) {
+      // stage s + 1 landed; stage s + 2 (issued at the top of this step) may stay in flight
+      if (s + 2 < nk) {
+        if (KSC && w == 0) wait_vm<NIW + 1>(); else wait_vm<NIW>();
+      } else {
+        wait_vm<0>();
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this step's LDS reads are done
+      __builtin_amdgcn_s_barrier();
+    } else {
+      __syncthreads();
+    }
   }
-  store_tile<TM, TN>(acc, ep, b, bm + wm * (BM / 2), bn + wn * (BN / 2), lane, M, N, C, ldc);
+  store_tile<TM, TN>(acc, ep, b, bm + wm * (BM / WM), bn + wn * (BN / WN), lane, M, N, C, ldc);
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int WM = 2, int WN = 2, int NS = 2>
 hipError_t launch_glds(int ta, int tb, int M, int N, int K, int batch, const double* A,
                        int64_t lda, int64_t sA, const double* B, int64_t ldb, int64_t sB,
                        double* C, int64_t ldc, int64_t sC, const Epi& ep, hipStream_t st) {
@@ -451,7 +566,8 @@ hipError_t launch_glds(int ta, int tb, int M, int N, int K, int batch, const dou
   const long nwg = (ep.sym ? (long)tm * (tm + 1) / 2 : (long)tm * tn) * batch;
   if (nwg > 0x7fffffffL) return hipErrorInvalidValue;
 #define PFML_GLDS_CASE(TA_, TB_, KS_)                                                        \
-  hipLaunchKernelGGL((dgemm_glds_kernel<TA_, TB_, BM, BN, KS_>), dim3((unsigned)nwg), dim3(256), \
+  hipLaunchKernelGGL((dgemm_glds_kernel<TA_, TB_, BM, BN, KS_, WM, WN, NS>), dim3((unsigned)nwg), \
+                     dim3(64 * WM * WN), \
                      0, st, M, N, K, tm, tn, (int)nwg, A, lda, sA, B, ldb, sB, C, ldc, sC, ep)
   const bool ksc = ep.ks != nullptr;
   if (ksc) {
@@ -533,6 +649,8 @@ struct PfmlGemmEpi {
   int sincos;
   int sym;
   double* Ct; int64_t ldct, sCt;
+  const int64_t* erow; int64_t serow;
+  const double* ecm; const double* ecs; int64_t secm;
   int tile_cfg;      // 0 auto, 1: 128x128, 2: 128x64, 3: 64x64 (BK 16, two LDS buffers);
                      // 4: 64x64 BK 32 one buffer, 5: 64x64 BK 32 two buffers (a 128x128
                      // BK 32 form spills: 144 B per lane)
@@ -552,9 +670,14 @@ extern "C" hipError_t pfml_dgemm_ex(int ta, int tb, int M, int N, int K, int bat
   if (M <= 0 || N <= 0 || batch <= 0) return hipSuccess;
   Epi ep{h->alpha, h->beta, h->rs, h->srs, h->cs, h->scs, h->ks, h->sks, h->E, h->lde, h->sE,
          h->e_cols, h->diag_col0, h->dval, h->dv, h->sdv, h->has_diag, h->es, h->ses,
-         h->sincos, h->sym, h->Ct, h->ldct, h->sCt};
+         h->sincos, h->sym, h->Ct, h->ldct, h->sCt, h->erow, h->serow, h->ecm, h->ecs,
+         h->secm};
   // symmetric mode: square C, square tiles, no sincos
   if (h->sym && (M != N || h->sincos)) return hipErrorInvalidValue;
+  // the epilogue's buffer stores address a batch entry of C / Ct with 32-bit byte offsets
+  if (((int64_t)(M - 1) * ldc + N) * 8 >= (int64_t)1 << 31 ||
+      (h->Ct && ((int64_t)(N - 1) * h->ldct + M) * 8 >= (int64_t)1 << 31))
+    return hipErrorInvalidValue;
   int cfg = h->tile_cfg;
   if (cfg == 0) {
     // LDS-DMA forms wherever the 16-byte chunking applies (they fall back to 64 x 64 register
@@ -564,8 +687,8 @@ extern "C" hipError_t pfml_dgemm_ex(int ta, int tb, int M, int N, int K, int bat
     cfg = (M >= 1024 && N >= 1024) ? 6 : (h->sym ? PFML_SYM_CFG : 8);
   }
   if (cfg == 1 && h->sincos) cfg = 3;    // the 128 x 128 kernel has no sincos epilogue
-  if (h->sym && (cfg == 2 || cfg == 8)) cfg = cfg == 2 ? 3 : 7;   // square tiles only
-  if (cfg >= 6 && cfg <= 8) {
+  if (h->sym && (cfg == 2 || cfg == 8 || cfg == 10)) cfg = cfg == 2 ? 3 : 7;   // square tiles
+  if (cfg >= 6 && cfg <= 11) {
     // LDS-DMA forms: 16-byte chunks along every contiguous dimension (even extents, leading
     // dimensions, batch strides, 16-B aligned bases); otherwise the register-staged form
     const int a_cont = ta ? M : K, b_cont = tb ? K : N;
@@ -580,6 +703,15 @@ extern "C" hipError_t pfml_dgemm_ex(int ta, int tb, int M, int N, int K, int bat
       if (cfg == 7)
         return launch_glds<64, 64>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC,
                                    ep, st);
+      if (cfg == 9)      // 8 waves (4 x 2) on a 128 x 128 tile
+        return launch_glds<128, 128, 4, 2>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc,
+                                           sC, ep, st);
+      if (cfg == 10)     // three LDS stages
+        return launch_glds<128, 64, 2, 2, 3>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C,
+                                             ldc, sC, ep, st);
+      if (cfg == 11)
+        return launch_glds<128, 128, 4, 2, 3>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C,
+                                              ldc, sC, ep, st);
       return launch_glds<128, 64>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, ep,
                                   st);
     }

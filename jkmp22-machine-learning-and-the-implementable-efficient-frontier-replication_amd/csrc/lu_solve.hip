@@ -37,19 +37,22 @@ __device__ __forceinline__ int live_col(int v, int nA_live, int a_first, int b0)
   return v < nA_live ? a_first + v : b0 + (v - nA_live);
 }
 
+// 1024 threads (16 waves): the panel takes 135 KB of LDS, so one workgroup per CU - the
+// row loops of the argmax and the elimination are spread over 16 waves instead of 4.
 template <int NB, int PMAX>
-__global__ __launch_bounds__(256) void lu_pivot_kernel(const double* __restrict__ M, int n,
-                                                       int64_t ldm, int64_t sM, int a0, int k0,
-                                                       int nb, int* __restrict__ piv,
-                                                       int* __restrict__ status) {
+__global__ __launch_bounds__(1024) void lu_pivot_kernel(const double* __restrict__ M, int n,
+                                                        int64_t ldm, int64_t sM, int a0, int k0,
+                                                        int nb, int* __restrict__ piv,
+                                                        int* __restrict__ status) {
+  constexpr int NT = 1024, NW = NT / 64;
   __shared__ double Pn[PMAX][NB + 1];
-  __shared__ double rv[4];
-  __shared__ int ri[4];
+  __shared__ double rv[NW];
+  __shared__ int ri[NW];
   const int b = blockIdx.x;
   const double* Mb = M + (int64_t)b * sM;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int rows = n - k0;
-  for (int e = t; e < rows * nb; e += 256) {
+  for (int e = t; e < rows * nb; e += NT) {
     const int i = e / nb, j = e % nb;
     Pn[i][j] = Mb[(int64_t)(k0 + i) * ldm + a0 + k0 + j];
   }
@@ -58,7 +61,7 @@ __global__ __launch_bounds__(256) void lu_pivot_kernel(const double* __restrict_
     // argmax |Pn[i][j]|, i in [j, rows)
     double best = -1.0;
     int bi = j;
-    for (int i = j + t; i < rows; i += 256) {
+    for (int i = j + t; i < rows; i += NT) {
       const double v = fabs(Pn[i][j]);
       if (v > best) { best = v; bi = i; }
     }
@@ -73,7 +76,7 @@ __global__ __launch_bounds__(256) void lu_pivot_kernel(const double* __restrict_
     if (t == 0) {
       double bv = rv[0];
       int bx = ri[0];
-      for (int q = 1; q < 4; ++q)
+      for (int q = 1; q < NW; ++q)
         if (rv[q] > bv || (rv[q] == bv && ri[q] < bx)) { bv = rv[q]; bx = ri[q]; }
       ri[0] = bx;
       piv[(int64_t)b * NB + j] = k0 + bx;
@@ -88,11 +91,16 @@ __global__ __launch_bounds__(256) void lu_pivot_kernel(const double* __restrict_
     }
     __syncthreads();
     const double pv = Pn[j][j];
-    for (int i = j + 1 + t; i < rows; i += 256) {
-      const double l = Pn[i][j] / pv;
-      for (int c = j + 1; c < nb; ++c) Pn[i][c] -= l * Pn[j][c];
+    // (rows x columns of the trailing panel over all 1024 threads)
+    const int nc = nb - j - 1;
+    if (nc > 0) {
+      for (int e = t; e < (rows - j - 1) * nc; e += NT) {
+        const int i = j + 1 + e / nc, c = j + 1 + e % nc;
+        Pn[i][c] -= (Pn[i][j] / pv) * Pn[j][c];
+      }
     }
     __syncthreads();
+    // the multipliers column is not stored (only the pivot order leaves the kernel)
   }
 }
 
@@ -215,7 +223,7 @@ hipError_t lu_pivot_launch(const double* M, int n, int64_t ldm, int64_t sM, int 
                            int nb, int* piv, int* status, int batch, hipStream_t st) {
   const int rows = n - k0;
   if (rows <= PMAX) {
-    hipLaunchKernelGGL((lu_pivot_kernel<NB, PMAX>), dim3(batch), dim3(256), 0, st, M, n, ldm,
+    hipLaunchKernelGGL((lu_pivot_kernel<NB, PMAX>), dim3(batch), dim3(1024), 0, st, M, n, ldm,
                        sM, a0, k0, nb, piv, status);
     return hipSuccess;
   }

@@ -55,7 +55,9 @@ __global__ __launch_bounds__(256) void standardize_kernel(const double* __restri
                                                           int TH, int N,
                                                           const double* __restrict__ vol,
                                                           double* __restrict__ out, int64_t ldo,
-                                                          int64_t so, int Pw) {
+                                                          int64_t so, int Pw,
+                                                          double* __restrict__ stats,
+                                                          int64_t lds, int write_out) {
   __shared__ double red[4][64], red2[4][64];
   __shared__ double colmean[64], colscale[64];
   const int bt = diag_tile(blockIdx.y, B, TH);   // (b, theta)
@@ -106,6 +108,11 @@ __global__ __launch_bounds__(256) void standardize_kernel(const double* __restri
   __syncthreads();
   const double mu = colmean[lane];
   const double sc = colscale[lane];
+  if (stats != nullptr && part == 0 && c < Pw) {   // (pad columns: scale 0 -> a zero addend)
+    stats[(int64_t)bt * 2 * lds + c] = c < P ? mu : 0.0;
+    stats[(int64_t)bt * 2 * lds + lds + c] = c < P ? sc : 0.0;
+  }
+  if (!write_out) return;
   double* o = out + (int64_t)bt * so;
   // scaled write: 8 rows per thread per iteration, every load issued before the first use (a
   // row-at-a-time loop waited on each gathered row's index and value in turn)
@@ -138,7 +145,8 @@ template <int RPT>
 __global__ __launch_bounds__(1024) void standardize_reg_kernel(
     const double* __restrict__ F, int P, int64_t ldf, const int64_t* __restrict__ rows,
     const int* __restrict__ n_real, int B, int TH, int N, const double* __restrict__ vol,
-    double* __restrict__ out, int64_t ldo, int64_t so, int Pw) {
+    double* __restrict__ out, int64_t ldo, int64_t so, int Pw, double* __restrict__ stats,
+    int64_t lds, int write_out) {
   constexpr int NP = 16;
   __shared__ double red[NP][64], red2[NP][64];
   __shared__ double colmean[64], colscale[64];
@@ -190,6 +198,11 @@ __global__ __launch_bounds__(1024) void standardize_reg_kernel(
   if (c >= Pw) return;
   const double mu = colmean[lane];
   const double sc = colscale[lane];
+  if (stats != nullptr && part == 0) {             // (pad columns: scale 0 -> a zero addend)
+    stats[(int64_t)bt * 2 * lds + c] = c < P ? mu : 0.0;
+    stats[(int64_t)bt * 2 * lds + lds + c] = c < P ? sc : 0.0;
+  }
+  if (!write_out) return;
   double* o = out + (int64_t)bt * so;
 #pragma unroll
   for (int u = 0; u < RPT; ++u) {
@@ -211,18 +224,25 @@ extern "C" hipError_t pfml_rff_sincos(const double* Z, int64_t R, int half, doub
   return hipGetLastError();
 }
 
+// stats (nullable): the column means and scales of every (b, theta) tile, [B*TH][2][lds]
+// (mean row, then scale row; columns P..Pw-1 zero); write_out = 0: the stats only (the
+// standardised values are then formed where they are consumed: the Horner GEMM's gathered
+// addend, csrc/gemm_f64.hip)
 extern "C" hipError_t pfml_standardize(const double* F, int P, int64_t ldf, const int64_t* rows,
                                        const int* n_real, int B, int TH, int N,
                                        const double* vol, double* out, int64_t ldo, int64_t so,
-                                       int Pw, hipStream_t st) {
+                                       int Pw, double* stats, int64_t lds, int write_out,
+                                       hipStream_t st) {
   if (B <= 0 || N <= 0) return hipSuccess;
-  if (Pw < P || ldo < Pw || ldf < P) return hipErrorInvalidValue;
+  if (Pw < P || ldf < P || (write_out && ldo < Pw) || (stats && lds < Pw) ||
+      (!write_out && !stats))
+    return hipErrorInvalidValue;
   dim3 grid((Pw + 63) / 64, (B + TH - 1) * TH);     // diagonal order (diag_tile)
   if (N <= 16 * 32)
     hipLaunchKernelGGL(standardize_reg_kernel<32>, grid, dim3(1024), 0, st, F, P, ldf, rows,
-                       n_real, B, TH, N, vol, out, ldo, so, Pw);
+                       n_real, B, TH, N, vol, out, ldo, so, Pw, stats, lds, write_out);
   else
     hipLaunchKernelGGL(standardize_kernel, grid, dim3(256), 0, st, F, P, ldf, rows, n_real, B, TH,
-                       N, vol, out, ldo, so, Pw);
+                       N, vol, out, ldo, so, Pw, stats, lds, write_out);
   return hipGetLastError();
 }

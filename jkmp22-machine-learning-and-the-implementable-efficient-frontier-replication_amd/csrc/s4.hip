@@ -36,6 +36,8 @@ struct MfArgs {
   const double* mask;             // [B, N] (FIX)
   int64_t sv;                     // batch stride of a / mask
   double d;                       // diagonal add (SHAT)
+  int flat;                       // X and Y exactly symmetric: sym() is the identity, so the
+                                  // mirror tile is not read (half the loads)
 };
 
 // (A form with one workgroup per tile PAIR - every element read once per operand, the mirror
@@ -51,13 +53,15 @@ __global__ __launch_bounds__(256) void mfunc_sym_kernel(MfArgs p) {
   const double* Y = p.Y ? p.Y + (int64_t)b * p.sX : nullptr;
   double* O = p.out + (int64_t)b * p.sX;
   // mirror tile (J0.., I0..) into LDS transposed: tx[r][c] = X[J0 + c][I0 + r]
-  for (int r = ty_; r < TS; r += 8) {
-    const int gi = J0 + r, gj = I0 + tx_;
-    const bool ok = gi < p.N && gj < p.N;
-    tx[tx_][r] = ok ? X[(int64_t)gi * p.ld + gj] : 0.0;
-    if (Y) ty[tx_][r] = ok ? Y[(int64_t)gi * p.ld + gj] : 0.0;
+  if (!p.flat) {
+    for (int r = ty_; r < TS; r += 8) {
+      const int gi = J0 + r, gj = I0 + tx_;
+      const bool ok = gi < p.N && gj < p.N;
+      tx[tx_][r] = ok ? X[(int64_t)gi * p.ld + gj] : 0.0;
+      if (Y) ty[tx_][r] = ok ? Y[(int64_t)gi * p.ld + gj] : 0.0;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   const double s = p.svec ? p.svec[b] : 0.0;
   const double c = p.cvec ? p.cvec[b] : 1.0;
   const double* av = p.a ? p.a + (int64_t)b * p.sv : nullptr;
@@ -66,8 +70,8 @@ __global__ __launch_bounds__(256) void mfunc_sym_kernel(MfArgs p) {
     const int i = I0 + r, j = J0 + tx_;
     if (i >= p.N || j >= p.N) continue;
     const int64_t o = (int64_t)i * p.ld + j;
-    const double xs = 0.5 * (X[o] + tx[r][tx_]);
-    const double ys = Y ? 0.5 * (Y[o] + ty[r][tx_]) : 0.0;
+    const double xs = p.flat ? X[o] : 0.5 * (X[o] + tx[r][tx_]);
+    const double ys = Y ? (p.flat ? Y[o] : 0.5 * (Y[o] + ty[r][tx_])) : 0.0;
     double v;
     if (p.mode == MF_X) {
       v = s * (av[i] * av[j]) * xs;
@@ -144,6 +148,7 @@ struct PfmlMfArgs {
   const double* mask;
   int64_t sv;
   double d;
+  int flat;
 };
 
 extern "C" int pfml_mf_args_size() { return (int)sizeof(PfmlMfArgs); }
@@ -152,7 +157,7 @@ extern "C" hipError_t pfml_mfunc_sym(const PfmlMfArgs* h, hipStream_t st) {
   if (h->B <= 0 || h->N <= 0) return hipSuccess;
   if (h->out == h->X || (h->Y && h->out == h->Y)) return hipErrorInvalidValue;   // tiles race
   MfArgs p{h->mode, h->B, h->N, h->ld, h->sX, h->X, h->Y, h->out, h->svec, h->cvec, h->a,
-           h->mask, h->sv, h->d};
+           h->mask, h->sv, h->d, h->flat};
   const int tiles = (h->N + TS - 1) / TS;
   hipLaunchKernelGGL(mfunc_sym_kernel, dim3(tiles * tiles, h->B), dim3(256), 0, st, p);
   return hipGetLastError();

@@ -11,7 +11,9 @@ a batched device pipeline over MONTHS (dates are independent given m_t, Sigma_t 
    semantics: mean of the two middle values), on the device;
 3. per batch of months (ragged universes padded block-diagonally):
    * signals: gather the 13 x N x P window, demean RFF columns, unit-norm every column, scale
-     rows by 1/vol (K11/K12, :357-391);
+     rows by 1/vol (K11/K12, :357-391) - stored for lags 0, 11, 12 only; lags 1..10 are
+     formed in the epilogue of the Horner step that consumes them from their column
+     statistics (a gathered addend: (F[row] - mean) * scale / vol), never stored;
    * Sigma_t = X F X' + diag(ivol) as one GEMM with a diagonal-add epilogue (K1) and
      m_tilde_t (K2/K3, Lemma 1, ops/linalg.m_tilde: fused symmetric passes + SPD inverses, no
      host sync);
@@ -45,7 +47,7 @@ from ..config import Config, get_features, interleaved_order
 from ..data import io
 from ..ops import linalg as la
 from ..ops.gemm import gemm, gemm_fused, gemm_prec
-from ..ops.panel import rff_features, standardize_signals
+from ..ops.panel import rff_features, signal_stats, standardize_signals
 from ..utils.dates import month_index, pfml_date_grids
 from ..utils.log import COUNTERS, get_logger
 from ..utils.trace import range_pop, range_push
@@ -141,12 +143,12 @@ def vol_scales(panel: Panel, barra: BarraCov, months: np.ndarray) -> np.ndarray:
 
 def auto_month_batch(n_stocks: int, gp: int, device, cap: int = 1024) -> int:
     """Months per S4 batch from the memory one month's working set needs (fp64): the
-    13-month signal window (13 N GP), five Horner buffers of N x (GP + N) plus two N x N blocks, ~8 N x N matrices of
+    three stored signal lags (3 N GP; the other ten exist only as column statistics), five Horner buffers of N x (GP + N) plus two N x N blocks, ~8 N x N matrices of
     m_func / Sigma and the (25) scratch.  A device batch takes up to 60 % of free HBM (288 GB on
     MI355X: all 731 months at N = 500 in one batch - 23 ms faster than 256-month batches,
     profiles/r03_s4_batch_cap_ab.json - ~100 at N = 3000), a host batch 25 % of available RAM."""
     cap = int(os.environ.get("PFML_S4_BATCH_CAP", cap))      # (A/B switch)
-    per = 8.0 * (13.0 * n_stocks * gp + 6.0 * n_stocks * (gp + n_stocks) + 11.0 * n_stocks ** 2
+    per = 8.0 * (3.0 * n_stocks * gp + 6.0 * n_stocks * (gp + n_stocks) + 11.0 * n_stocks ** 2
                  + 2.0 * gp * gp)
     dev = torch.device(device)
     if dev.type == "cuda":
@@ -407,6 +409,8 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
     Wdev = plan.Wd if plan.Wd is not None else [
         torch.as_tensor(plan.W[g], dtype=torch.float64, device=dev) for g in range(Gc)]
     rffs = [rff_features(plan.feats, Wdev[g], prec, width=Pp, pad_rows=1) for g in range(Gc)]
+    # the gathered addend's feature table: every g block side by side, [R + 1, Gc * Pp]
+    Fcat = torch.cat(rffs, 1) if Gc > 1 else rffs[0]
     vol = _vol_device(plan)
     range_pop()
 
@@ -441,10 +445,22 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
         B = len(bt.months)
         range_push("pfml_inputs.batch")
         # signals of every distinct g, written into one [B, 13, N, Gc*Pp] stack
-        S = torch.empty((B, lb + 2, N, GP), dtype=torch.float64, device=dev)
+        # signals (K11/K12): lags 0, 11 and 12 materialised (signal_t, T_11's S block, U_0's
+        # GEMM operand) into [B, 3, N, Gc*Pp]; lags 1..10 only as per-column means and scales -
+        # the Horner steps form (F[row] - mean) * scale / vol in their epilogue (gathered
+        # addend), so 10 of the 13 [N, Gc*Pp] signal blocks per month are never stored
+        S = torch.empty((B, 3, N, GP), dtype=torch.float64, device=dev)
+        idx3 = torch.cat([bt.idx[:, :1], bt.idx[:, lb:lb + 2]], 1)     # (no host index list)
         for g in range(Gc):
-            standardize_signals(rffs[g], bt.idx, bt.mask, vol, P=P,
+            standardize_signals(rffs[g], idx3, bt.mask, vol, P=P,
                                 out=S[..., g * Pp:(g + 1) * Pp], n_real=bt.n_real)
+        stats = torch.empty((B, lb - 1, 2, GP), dtype=torch.float64, device=dev)
+        for g in range(Gc):
+            signal_stats(rffs[g], bt.idx[:, 1:lb], bt.mask, P,
+                         out=stats[..., g * Pp:(g + 1) * Pp], n_real=bt.n_real)
+        # 1 / vol of each lag's rows (0 on padding rows: their standardised signal is 0)
+        ivol = torch.where(bt.mask.unsqueeze(1) > 0, 1.0 / vol[bt.idx[:, 1:lb]],
+                           torch.zeros((), dtype=torch.float64, device=dev))
         # Barra Sigma = X F X' + diag(ivol) (K1; pad rows: X = 0, ivol = 1 -> identity block)
         Xl = plan.bX[bt.brow]                                       # [B, N, K]
         Fb = plan.bF[bt.fpos]                                       # [B, K, K]
@@ -452,13 +468,15 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
         XF = gemm(Xl, Fb, backend="own")                             # in-house fp64 MFMA GEMM
         Sigma = torch.empty((B, N, N), dtype=torch.float64, device=dev)
         if prec == "fp64":
-            gemm_fused(XF, Xl, Sigma, trans_b=True, diag_col0=0, diag_vec=iv)
+            # symmetric mode: the lower triangle mirrored, an exactly symmetric Sigma
+            gemm_fused(XF, Xl, Sigma, trans_b=True, diag_col0=0, diag_vec=iv, sym=True)
         else:
             gemm_prec(XF, Xl, prec, trans_b=True, out=Sigma)
             Sigma.diagonal(dim1=1, dim2=2).add_(iv)
         # m = diag(a) m_tilde diag(1/a) (Lemma 1); a and 1/a are folded into the Horner GEMMs
         mt, a = la.m_tilde(Sigma, bt.lam, bt.w, bt.rf, mu, gamma, cfg.run.iterations,
-                           mask=bt.mask, status=None if mstat is None else mstat[b0:b0 + B])
+                           mask=bt.mask, status=None if mstat is None else mstat[b0:b0 + B],
+                           sigma_exact_sym=prec == "fp64")
         if m_keep is not None:
             sel = [(bi, kpos[int(d)]) for bi, d in enumerate(bt.months) if int(d) in kpos]
             if sel:
@@ -481,7 +499,7 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
         Wr = Wd + N
         Tb = [torch.empty((B, N, Wr), dtype=torch.float64, device=dev) for _ in range(2)]
         eye = torch.eye(N, dtype=torch.float64, device=dev)
-        Tb[0][:, :, :GP] = S[:, lb]
+        Tb[0][:, :, :GP] = S[:, 1]
         Tb[0][:, :, GP:Wd] = eye
         # R_11 = diag(a) m_tilde diag(D_11 / a): elementwise, in the rounding order the fused
         # GEMM against the identity produced ((m_tilde * k-scale) * row scale)
@@ -489,7 +507,9 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
         cur = 0
         for th in range(lb - 1, 0, -1):
             gemm_fused(mt, Tb[cur], Tb[cur ^ 1], row_scale=a, k_scale=(Dg[:, th] * ainv),
-                       addend=S[:, th], addend_cols=GP, diag_col0=GP, diag_value=1.0)
+                       addend=Fcat, addend_cols=GP, addend_rows=bt.idx[:, th],
+                       addend_col_shift=stats[:, th - 1, 0], addend_col_scale=stats[:, th - 1, 1],
+                       addend_row_scale=ivol[:, th - 1], diag_col0=GP, diag_value=1.0)
             cur ^= 1
         T1 = Tb[cur]
         # T0 / U0 carry LU_PANEL_COLS scratch columns for the two-level solve below
@@ -500,12 +520,12 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
         gemm_fused(mt, T1[:, :, :Wd], T0, row_scale=a, k_scale=(Dg[:, 0] * ainv),
                    addend=S[:, 0], addend_cols=GP, diag_col0=GP, diag_value=1.0)
         # U_0 = T_1 + Q [S_12 | I]: the S_12 block on the GEMM, the identity block as Q + T_1
-        gemm_fused(T1[:, :, Wd:], S[:, lb + 1], U0[:, :, :GP], addend=T1[:, :, :GP],
+        gemm_fused(T1[:, :, Wd:], S[:, 2], U0[:, :, :GP], addend=T1[:, :, :GP],
                    addend_cols=GP)
         torch.add(T1[:, :, Wd:], T1[:, :, GP:Wd], out=U0[:, :, GP:])
         del Tb, T1
         sig0 = S[:, 0].clone()                                      # signal_t blocks
-        del S
+        del S, stats, ivol
         # omega = const^-1 Omega, solved in place on the augmented [Omega | const] rows (K7)
         omega = la.solve_augmented(T0f, N, GP, a0=GP, b0=0, status=sing[:B], z0=Wd)  # [B, N, GP]
         omega_l1 = la.solve_augmented(U0f, N, GP, a0=GP, b0=0, status=sing[:B], z0=Wd)
@@ -539,18 +559,20 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
                 continue
             cs = slice(g * Pp, (g + 1) * Pp)
             og, cg, sg = omega[:, :, cs], omega_chg[:, :, cs], SO[:, :, cs]
+            # risk = gamma omega' (Sigma omega) and tc = w omega_chg' Lambda omega_chg are
+            # symmetric: the GEMM's symmetric mode computes the lower tiles and mirrors them
             if prec == "fp64":
-                gemm_fused(og, sg, Dt, trans_a=True, alpha=gamma)
+                gemm_fused(og, sg, Dt, trans_a=True, alpha=gamma, sym=True)
             else:
                 gemm_prec(og.contiguous(), sg.contiguous(), prec, trans_a=True, alpha=gamma,
                           out=Dt)
             if keep_risk_tc:
                 risk_out[g, sl] = Dt[:, :P, :P]
-                gemm_fused(cg, cg, Dk, trans_a=True, k_scale=lw)
+                gemm_fused(cg, cg, Dk, trans_a=True, k_scale=lw, sym=True)
                 tc_out[g, sl] = Dk[:, :P, :P]
                 Dt.add_(Dk)
             else:
-                gemm_fused(cg, cg, Dt, trans_a=True, k_scale=lw, beta=1.0)
+                gemm_fused(cg, cg, Dt, trans_a=True, k_scale=lw, beta=1.0, sym=True)
             d_out[g, sl] = Dt[:, :P, :P]
             r_out[g, sl] = rt_[:, g * Pp:g * Pp + P]
             for bi in range(B):

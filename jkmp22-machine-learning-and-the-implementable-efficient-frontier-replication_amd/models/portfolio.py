@@ -371,10 +371,11 @@ def pfml_weights(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         Sig = torch.empty((Bc, N, N), **f64)
         XF = torch.empty((Bc, N, K), **f64)
         gemm_fused(Xd, torch.as_tensor(Fb, **f64), XF)          # in-house GEMM, no rocBLAS
-        gemm_fused(XF, Xd, Sig, trans_b=True, diag_col0=0, diag_vec=ivd)
+        # (as in S4: the symmetric mode's exactly symmetric Sigma, so m_t is bitwise S4's)
+        gemm_fused(XF, Xd, Sig, trans_b=True, diag_col0=0, diag_vec=ivd, sym=True)
         mt, a = la.m_tilde(Sig, torch.as_tensor(lam, **f64), torch.as_tensor(wvals[cm], **f64),
                            torch.as_tensor(rfvals[cm], **f64), mu, gamma, cfg.run.iterations,
-                           mask=torch.as_tensor(mask, **f64))
+                           mask=torch.as_tensor(mask, **f64), sigma_exact_sym=True)
         mt_all[c0:c0 + Bc] = mt
         a_all[c0:c0 + Bc] = a
     th("s9.m_t")

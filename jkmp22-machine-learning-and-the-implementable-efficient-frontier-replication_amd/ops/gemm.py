@@ -27,7 +27,8 @@ class _Epi(C.Structure):
                 ("ks", _P), ("sks", _L), ("E", _P), ("lde", _L), ("sE", _L), ("e_cols", _I),
                 ("diag_col0", _I), ("dval", _D), ("dv", _P), ("sdv", _L), ("has_diag", _I),
                 ("es", _P), ("ses", _L), ("sincos", _I), ("sym", _I), ("Ct", _P), ("ldct", _L),
-                ("sCt", _L), ("tile_cfg", _I)]
+                ("sCt", _L), ("erow", _P), ("serow", _L), ("ecm", _P), ("ecs", _P),
+                ("secm", _L), ("tile_cfg", _I)]
 
 
 nat.register_hip("pfml_dgemm_ex", [_I, _I, _I, _I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _L,
@@ -69,7 +70,7 @@ def _ledger(ta, tb, M, N, K, batch, A3, B3, C3, ks=None, sks=0, sincos=False, cf
         cfg = _auto_cfg(M, N, K, sym)
     if cfg == 1 and sincos:
         cfg = 3
-    if sym and cfg in (2, 8):
+    if sym and cfg in (2, 8, 10):
         cfg = 3 if cfg == 2 else 7
     lda, ldb = A3.stride(1), B3.stride(1)
     sa, sb = _bstride(A3, batch), _bstride(B3, batch)
@@ -78,13 +79,16 @@ def _ledger(ta, tb, M, N, K, batch, A3, B3, C3, ks=None, sks=0, sincos=False, cf
            and sa % 2 == 0 and sb % 2 == 0 and A3.data_ptr() % 16 == 0
            and B3.data_ptr() % 16 == 0
            and (ks is None or (ks.data_ptr() % 16 == 0 and sks % 2 == 0)))
-    if cfg in (6, 7, 8) and not (vec and not sincos and min(M, N, K) >= 2):
+    if cfg in (6, 7, 8, 9, 10, 11) and not (vec and not sincos and min(M, N, K) >= 2):
         cfg = 3
-    bm, bn = {1: (128, 128), 2: (128, 64), 6: (128, 128), 8: (128, 64)}.get(cfg, (64, 64))
+    bm, bn = {1: (128, 128), 2: (128, 64), 6: (128, 128), 8: (128, 64), 9: (128, 128),
+              10: (128, 64), 11: (128, 128)}.get(cfg, (64, 64))
     bk, nbuf = {4: (32, 1), 5: (32, 2)}.get(cfg, (16, 2))
     b = lambda v: "true" if v else "false"                                  # noqa: E731
-    if cfg in (6, 7, 8):
-        name = f"dgemm_glds_kernel<{b(ta)}, {b(tb)}, {bm}, {bn}, {b(ks is not None)}>"
+    if cfg in (6, 7, 8, 9, 10, 11):
+        wm, wn = (4, 2) if cfg in (9, 11) else (2, 2)
+        name = (f"dgemm_glds_kernel<{b(ta)}, {b(tb)}, {bm}, {bn}, {b(ks is not None)}, "
+                f"{wm}, {wn}, {3 if cfg >= 10 else 2}>")
     else:
         name = (f"dgemm_kernel<{b(ta)}, {b(tb)}, {bm}, {bn}, {2 if vec else 1}, "
                 f"{b(ks is not None)}, {bk}, {nbuf}>")
@@ -278,7 +282,10 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
                diag_value: float = 1.0, diag_vec: torch.Tensor | None = None,
                addend_row_scale: torch.Tensor | None = None, sincos: bool = False,
                tile_cfg: int = 0, sym: bool = False,
-               mirror_out: torch.Tensor | None = None) -> torch.Tensor:
+               mirror_out: torch.Tensor | None = None,
+               addend_rows: torch.Tensor | None = None,
+               addend_col_shift: torch.Tensor | None = None,
+               addend_col_scale: torch.Tensor | None = None) -> torch.Tensor:
     """out = alpha diag(rs) op(A) diag(ks) op(B) diag(cs) + beta out
              + diag(es) addend[:, :, :addend_cols]  (on out's first addend_cols columns)
              + diag(diag_vec or diag_value) placed at out[:, i, diag_col0 + i].
@@ -287,6 +294,11 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
     computed (the output tiles on and below the diagonal) and mirrored, so out comes back
     exactly symmetric (beta / addend read at the lower positions only).  ``mirror_out``
     [.., N, M]: also receives the transpose of the result (X21 = X12' of the SPD inverse).
+
+    Gathered addend (``addend_rows`` [B, M] int64, ``addend_col_shift`` / ``addend_col_scale``
+    [B, addend_cols]): the addend row i is (addend[rows[b, i]] - shift[b]) * scale[b] (times
+    the addend row scale) - the standardised signals of the Horner steps formed from the panel
+    features on the fly.  ``addend`` is then the [R, >= addend_cols] feature table (2-D).
 
     One launch of csrc/gemm_f64.hip on a HIP device (the Horner step of (24), Sigma = X F X'
     + diag(ivol), ...); the same arithmetic in torch fp64 on CPU.  3-D batched operands
@@ -308,6 +320,10 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
         addend_cols = N
     if sym and (M != N or sincos):
         raise ValueError("gemm_fused(sym): square output, no sincos")
+    gathered = addend_rows is not None
+    if gathered and (addend is None or addend.dim() != 2 or addend_col_shift is None
+                     or addend_col_scale is None):
+        raise ValueError("gemm_fused: a gathered addend needs a 2-D table, shift and scale")
     E3 = None if addend is None else _as3(addend)
     T3 = None if mirror_out is None else _as3(mirror_out)
     if T3 is not None and (tuple(T3.shape[1:]) != (N, M) or T3.stride(-1) != 1):
@@ -323,13 +339,25 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
         ks, sks = _vec3(k_scale, batch)
         dv, sdv = _vec3(diag_vec, batch)
         es, ses = _vec3(addend_row_scale, batch)
+        er = ecm = ecs = None
+        ser = secm = 0
+        if gathered:
+            er = addend_rows if addend_rows.dim() == 2 else addend_rows.unsqueeze(0)
+            ecm = addend_col_shift if addend_col_shift.dim() == 2 else addend_col_shift.unsqueeze(0)
+            ecs = addend_col_scale if addend_col_scale.dim() == 2 else addend_col_scale.unsqueeze(0)
+            if (er.dtype != torch.int64 or er.stride(-1) != 1 or ecm.stride(-1) != 1
+                    or ecs.stride(-1) != 1 or ecm.stride(0) != ecs.stride(0)):
+                raise ValueError("gemm_fused: gathered addend layout")
+            ser = 0 if er.shape[0] == 1 else er.stride(0)
+            secm = 0 if ecm.shape[0] == 1 else ecm.stride(0)
         ep = _Epi(float(alpha), float(beta), nat.ptr(rs), srs, nat.ptr(cs), scs, nat.ptr(ks), sks,
                   nat.ptr(E3), 0 if E3 is None else E3.stride(1),
-                  0 if E3 is None else _bstride(E3, batch), int(addend_cols or 0),
+                  0 if (E3 is None or gathered) else _bstride(E3, batch), int(addend_cols or 0),
                   int(diag_col0 or 0), float(diag_value), nat.ptr(dv), sdv,
                   int(diag_col0 is not None), nat.ptr(es), ses, int(sincos), int(sym),
                   nat.ptr(T3), 0 if T3 is None else T3.stride(1),
-                  0 if T3 is None else T3.stride(0), int(tile_cfg or _TILE_DEFAULT))
+                  0 if T3 is None else T3.stride(0), nat.ptr(er), ser, nat.ptr(ecm),
+                  nat.ptr(ecs), secm, int(tile_cfg or _TILE_DEFAULT))
         if _work.on():
             _ledger(trans_a, trans_b, M, N, K, batch, A3, B3, C3, ks=ks, sks=sks,
                     sincos=sincos, cfg=tile_cfg, sym=sym,
@@ -365,7 +393,14 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
         r = r + beta * C3
     r = r.expand(batch, M, N).clone()
     if E3 is not None and addend_cols:
-        Ea = E3[:, :, :addend_cols]
+        if gathered:
+            er = addend_rows if addend_rows.dim() == 2 else addend_rows.unsqueeze(0)
+            sh = addend_col_shift if addend_col_shift.dim() == 2 else addend_col_shift.unsqueeze(0)
+            scl = addend_col_scale if addend_col_scale.dim() == 2 else addend_col_scale.unsqueeze(0)
+            Ea = (addend[:, :addend_cols][er] - sh[:, None, :addend_cols]) * \
+                scl[:, None, :addend_cols]
+        else:
+            Ea = E3[:, :, :addend_cols]
         if addend_row_scale is not None:
             esv = addend_row_scale if addend_row_scale.dim() == 2 else addend_row_scale.unsqueeze(0)
             Ea = Ea * esv.unsqueeze(-1)

@@ -156,6 +156,8 @@ def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor,
 # PFML_SPD_SYM=0 takes the two-sided form for every m_func inverse (A/B switch)
 SYM_GEMM_CFG = int(os.environ.get("PFML_SYM_GEMM_CFG", "0"))
 SYM_INVERSE = os.environ.get("PFML_SPD_SYM", "1") != "0"
+DB_SYM = os.environ.get("PFML_DB_SYM", "0") == "1"
+DB_SYMPROD = os.environ.get("PFML_DB_SYMPROD", "0") == "1"
 
 
 def spd_inverse_sym(X: torch.Tensor, status: torch.Tensor) -> torch.Tensor:
@@ -371,7 +373,7 @@ class _MfArgs(C.Structure):
     _fields_ = [("mode", C.c_int), ("B", C.c_int), ("N", C.c_int), ("ld", C.c_int64),
                 ("sX", C.c_int64), ("X", C.c_void_p), ("Y", C.c_void_p), ("out", C.c_void_p),
                 ("svec", C.c_void_p), ("cvec", C.c_void_p), ("a", C.c_void_p),
-                ("mask", C.c_void_p), ("sv", C.c_int64), ("d", C.c_double)]
+                ("mask", C.c_void_p), ("sv", C.c_int64), ("d", C.c_double), ("flat", C.c_int)]
 
 
 nat.register_hip("pfml_mfunc_sym", [C.POINTER(_MfArgs), C.c_void_p])
@@ -388,9 +390,11 @@ def _sym(x: torch.Tensor) -> torch.Tensor:
 def mf_sym(mode: int, X: torch.Tensor, Y: torch.Tensor | None, out: torch.Tensor, *,
            svec: torch.Tensor | None = None, cvec: torch.Tensor | None = None,
            a: torch.Tensor | None = None, mask: torch.Tensor | None = None,
-           d: float = 0.0) -> torch.Tensor:
+           d: float = 0.0, flat: bool = False) -> torch.Tensor:
     """One fused symmetric pass over a [B, N, N] batch (csrc/s4.hip, header for the modes);
-    the CPU branch is the torch oracle of the same formulas."""
+    the CPU branch is the torch oracle of the same formulas.  ``flat``: X and Y are known to
+    be exactly symmetric (sym() is then the identity, bit for bit): the mirror reads are
+    skipped."""
     B, N, _ = X.shape
     if nat.is_device(X):
         for t in (X, Y, out):
@@ -404,7 +408,8 @@ def mf_sym(mode: int, X: torch.Tensor, Y: torch.Tensor | None, out: torch.Tensor
         _work.add("mfunc_sym_kernel", 6.0 * B * N * N,
                  8.0 * B * N * N * (2 + (Y is not None)))
         args = _MfArgs(mode, B, N, N, N * N, X.data_ptr(), nat.ptr(Y), out.data_ptr(),
-                       nat.ptr(svec), nat.ptr(cvec), nat.ptr(a), nat.ptr(mask), sv, float(d))
+                       nat.ptr(svec), nat.ptr(cvec), nat.ptr(a), nat.ptr(mask), sv, float(d),
+                       int(flat))
         nat.check(nat.hip_lib().pfml_mfunc_sym(C.byref(args), nat.stream_of(X)), "pfml_mfunc_sym")
         return out
     xs = _sym(X)
@@ -460,12 +465,19 @@ def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tenso
     Y.copy_(S)
     mu = torch.empty(B, dtype=S.dtype, device=S.device)
     for it in range(iters):
-        spd_inverse_into(M, Mi, status)
+        if DB_SYM and nat.is_device(M) and N >= _BLOCKED_MIN_N:
+            Mi.copy_(M)                          # (experiment: one-triangle inverse in DB)
+            spd_inverse_sym(Mi, status)
+        else:
+            spd_inverse_into(M, Mi, status)
         _db_mu(M, Mi, it >= scaled_iters, mu)
         # Y' = (mu/2) Y + (1/(2 mu)) Y M^-1 ;  M' = I/2 + (mu^2 M + mu^-2 M^-1)/4
         rs = (0.5 / mu).view(B, 1).expand(B, N).contiguous()
         es = (0.5 * mu).view(B, 1).expand(B, N).contiguous()
-        gemm_fused(Y, Mi, Yn, row_scale=rs, addend=Y, addend_row_scale=es)
+        # (Y and M^-1 are commuting symmetric matrices in exact arithmetic: DB_SYMPROD takes
+        # the product's lower triangle only, mirrored - an experiment switch)
+        gemm_fused(Y, Mi, Yn, row_scale=rs, addend=Y, addend_row_scale=es,
+                   sym=DB_SYMPROD and nat.is_device(Y))
         Y, Yn = Yn, Y
         mf_sym(MF_DB, M, Mi, Yn, svec=mu)        # Yn is free here: new M into it
         M, Yn = Yn, M
@@ -482,8 +494,8 @@ DB_SCALED_ITERS = 6
 
 def m_tilde(sigma: torch.Tensor, lam: torch.Tensor, w: torch.Tensor, rf: torch.Tensor,
             mu: float, gamma: float, iterations: int = 10, mask: torch.Tensor | None = None,
-            db_iters: int = DB_ITERS, status: torch.Tensor | None = None
-            ) -> tuple[torch.Tensor, torch.Tensor]:
+            db_iters: int = DB_ITERS, status: torch.Tensor | None = None,
+            sigma_exact_sym: bool = False) -> tuple[torch.Tensor, torch.Tensor]:
     """m_tilde of Lemma 1 and a = lambda^-1/2, so that m = diag(a) m_tilde diag(1/a)
     (General_functions.py:941-963).  All on the device with no host synchronisation except one
     status check at the end (matrices whose SPD inverse met a non-positive pivot anywhere in
@@ -503,10 +515,16 @@ def m_tilde(sigma: torch.Tensor, lam: torch.Tensor, w: torch.Tensor, rf: torch.T
     if not deferred:
         status = torch.zeros(B, dtype=torch.int32, device=dev) if nat.is_device(sigma) else None
     x = torch.empty_like(sigma)
-    mf_sym(MF_X, sigma, None, x, svec=s, a=a)                   # x = s L^-1/2 S L^-1/2
+    # sigma_exact_sym: the caller built Sigma exactly symmetric (S4's X F X' in the GEMM's
+    # symmetric mode), and the one-triangle inverses keep mt exactly symmetric: the x and
+    # fixed-point passes then skip their mirror reads (same bits)
+    flat = sigma_exact_sym and nat.is_device(sigma) and SYM_INVERSE and N >= _BLOCKED_MIN_N
+    mf_sym(MF_X, sigma, None, x, svec=s, a=a, flat=flat)        # x = s L^-1/2 S L^-1/2
     S = torch.empty_like(sigma)
     four = torch.full((B, N), 4.0, dtype=dt, device=dev)
-    gemm_fused(x, x, S, addend=x, addend_row_scale=four)         # sigma_hat^2 - 4I = x^2 + 4x
+    # sigma_hat^2 - 4I = x^2 + 4x (x exactly symmetric: the GEMM's symmetric mode, half the
+    # tiles, an exactly symmetric S - and Denman-Beavers' M stays so)
+    gemm_fused(x, x, S, addend=x, addend_row_scale=four, sym=True)
     ws = [torch.empty_like(sigma) for _ in range(4)]
     root = _db_sqrt(S, db_iters, DB_SCALED_ITERS, status, ws)
     # m_tilde_0 = (sigma_hat - root)/2 = 2 (sigma_hat + root)^-1   (cancellation-free form)
@@ -518,7 +536,7 @@ def m_tilde(sigma: torch.Tensor, lam: torch.Tensor, w: torch.Tensor, rf: torch.T
     mt.mul_(2.0)
     Aq = ws[3]
     for _ in range(iterations):
-        mf_sym(MF_FIX, sigma, mt, Aq, svec=s, cvec=c, a=a, mask=mask)
+        mf_sym(MF_FIX, sigma, mt, Aq, svec=s, cvec=c, a=a, mask=mask, flat=flat)
         spd_inverse_sym(Aq, status)
         mt, Aq = Aq, mt
     if status is not None and not deferred:

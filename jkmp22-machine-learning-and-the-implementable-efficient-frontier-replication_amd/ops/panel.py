@@ -18,7 +18,8 @@ nat.register_hip("pfml_rff_sincos", [C.c_void_p, C.c_int64, C.c_int, C.c_void_p,
                                      C.c_void_p])
 nat.register_hip("pfml_standardize", [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
                                       C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
-                                      C.c_int64, C.c_int64, C.c_int, C.c_void_p])
+                                      C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_int64,
+                                      C.c_int, C.c_void_p])
 
 
 def rff_features(X: torch.Tensor, W: torch.Tensor, precision: str = "fp64",
@@ -80,7 +81,7 @@ def standardize_signals(F: torch.Tensor, idx: torch.Tensor, mask: torch.Tensor,
         _work.add("standardize", 6.0 * B * TH * N * P, 8.0 * B * TH * N * (P + Pw))
         nat.check(nat.hip_lib().pfml_standardize(
             F.data_ptr(), P, F.stride(0), rows.data_ptr(), n_real.data_ptr(), B, TH, N,
-            vol.data_ptr(), out.data_ptr(), out.stride(2), out.stride(1), Pw,
+            vol.data_ptr(), out.data_ptr(), out.stride(2), out.stride(1), Pw, None, 0, 1,
             nat.stream_of(F)), "pfml_standardize")
         return out
     F = F[:, :P]
@@ -95,4 +96,39 @@ def standardize_signals(F: torch.Tensor, idx: torch.Tensor, mask: torch.Tensor,
     v = vol[idx].unsqueeze(-1)
     out.zero_()
     out[..., :P] = S / v
+    return out
+
+
+def signal_stats(F: torch.Tensor, idx: torch.Tensor, mask: torch.Tensor, P: int,
+                 out: torch.Tensor, n_real: torch.Tensor | None = None) -> torch.Tensor:
+    """The column means and scales of ``standardize_signals`` without the standardised values:
+    out [B, TH, 2, >= Pw] (row 0 the means - 0 for the constant - row 1 the unit-norm scales;
+    columns P.. zero), so that (F[idx] - mean) * scale / vol is formed where it is consumed
+    (the Horner GEMM's gathered addend, models/pfml_inputs.py).  Same kernel, same sums."""
+    B, TH, N = idx.shape
+    Pw = out.shape[-1]
+    if nat.is_device(F):
+        if out.stride(-1) != 1 or out.stride(-2) != out.stride(1) // 2 or \
+                out.stride(1) * TH != out.stride(0) or F.stride(-1) != 1:
+            raise ValueError("signal_stats: unsupported output layout")
+        if n_real is None:
+            n_real = mask.sum(1).to(torch.int32)
+        n_real = n_real.to(torch.int32).contiguous()
+        rows = idx.to(torch.int64).contiguous()
+        _work.add("standardize", 4.0 * B * TH * N * P, 8.0 * B * TH * N * P)
+        nat.check(nat.hip_lib().pfml_standardize(
+            F.data_ptr(), P, F.stride(0), rows.data_ptr(), n_real.data_ptr(), B, TH, N,
+            F.data_ptr(), None, 0, 0, Pw, out.data_ptr(), out.stride(-2), 0,
+            nat.stream_of(F)), "pfml_standardize")
+        return out
+    S = F[:, :P][idx]                                           # [B, TH, N, P]
+    m = mask.view(B, 1, N, 1)
+    n = mask.sum(1).view(B, 1, 1, 1)
+    mean = (S * m).sum(2, keepdim=True) / n
+    mean[..., 0].fill_(0.0)
+    S = (S - mean) * m
+    norm = torch.sqrt(1.0 / (S * S).sum(2, keepdim=True))
+    out.zero_()
+    out[:, :, 0, :P] = mean[:, :, 0]
+    out[:, :, 1, :P] = norm[:, :, 0]
     return out

@@ -63,7 +63,7 @@ def test_gemm_epi_struct_matches():
 
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("shape", [(2, 37, 53, 29), (3, 130, 258, 100), (2, 96, 224, 96)])
 def test_gemm_fused_matches_torch(gpu, ta, tb, cfg, shape):
     """Every fusion of csrc/gemm_f64.hip (k-scale prologue, row/col scale, beta, addend block,
@@ -93,7 +93,28 @@ def test_gemm_fused_matches_torch(gpu, ta, tb, cfg, shape):
     assert (out - ref).abs().max().item() / ref.abs().max().item() < 1e-13
 
 
-@pytest.mark.parametrize("cfg", [1, 3, 6, 7])
+@pytest.mark.parametrize("cfg", [3, 6, 8])
+def test_gemm_gathered_addend(gpu, cfg):
+    """The gathered addend of the Horner steps (standardised signals formed in the epilogue):
+    out = rs * (A B) + es_i * (F[rows_i] - shift) * scale on the first e_cols columns, vs the
+    torch oracle, with rows repeated and out of order."""
+    from pfml.ops.gemm import gemm_fused
+    b, M, N, K, E = 3, 130, 202, 96, 150
+    A, B = _rand(b, M, K, seed=1), _rand(b, K, N, seed=2)
+    F = _rand(500, 160, seed=3)
+    rows = torch.randint(0, 500, (b, 13, M), generator=torch.Generator().manual_seed(4))
+    kw = dict(row_scale=_rand(b, M, seed=5), addend=F, addend_cols=E, addend_rows=rows[:, 7],
+              addend_col_shift=_rand(b, 2, E, seed=6)[:, 0],
+              addend_col_scale=_rand(b, 2, E, seed=6)[:, 1],
+              addend_row_scale=_rand(b, 4, M, seed=7)[:, 2], diag_col0=E, diag_value=1.0)
+    ref = gemm_fused(A, B, torch.empty(b, M, N, dtype=torch.float64), **kw)
+    kd = {k: (v.to(gpu) if isinstance(v, torch.Tensor) else v) for k, v in kw.items()}
+    out = gemm_fused(A.to(gpu), B.to(gpu), torch.empty(b, M, N, dtype=torch.float64, device=gpu),
+                     tile_cfg=cfg, **kd).cpu()
+    assert (out - ref).abs().max().item() / ref.abs().max().item() < 1e-13
+
+
+@pytest.mark.parametrize("cfg", [1, 3, 6, 7, 9, 11])
 @pytest.mark.parametrize("shape", [(3, 234, 256), (2, 130, 100), (2, 37, 29)])
 def test_gemm_sym_and_mirror(gpu, cfg, shape):
     """Symmetric mode (only the output tiles on / below the diagonal, lower triangle mirrored:

@@ -136,6 +136,18 @@ def test_rff_and_standardize(gpu):
     blk = stack[..., P + 1:].cpu()
     assert torch.allclose(blk[..., :P], ref, rtol=1e-11, atol=1e-12)
     assert not blk[..., P:].any() and bool((stack[..., :P + 1] == 7.0).all())
+    # column statistics only (the Horner steps' gathered addends), into a g block of a wider
+    # [B, TH, 2, G * (P + 1)] buffer
+    from pfml.ops.panel import signal_stats
+    st_ref = signal_stats(Fz, idx, mask, P, torch.empty(2, 13, 2, P + 1, dtype=torch.float64))
+    st = torch.full((2, 13, 2, 2 * (P + 1)), 7.0, dtype=torch.float64, device=gpu)
+    signal_stats(Fw, idx.to(gpu), mask.to(gpu), P, st[..., P + 1:])
+    assert torch.allclose(st[..., P + 1:].cpu(), st_ref, rtol=1e-12, atol=1e-13)
+    assert bool((st[..., :P + 1] == 7.0).all())
+    # (F[idx] - mean) * scale / vol reproduces the standardised signals
+    Fr = Fz[:, :P][idx]
+    rec = (Fr - st_ref[:, :, 0:1, :P]) * st_ref[:, :, 1:2, :P] / vol[idx].unsqueeze(-1)
+    assert torch.allclose(rec * mask.view(2, 1, 40, 1), ref, rtol=1e-11, atol=1e-12)
 
 
 def test_pfml_inputs_gpu_matches_cpu(gpu, small_data):

@@ -39,7 +39,7 @@ SHAPES = [  # name, batch, M, N, K, trans_a, trans_b, horner fusion
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
-    cfgs = [int(c) for c in os.environ.get("PFML_DGEMM_CFGS", "3,6,7,8").split(",")]
+    cfgs = [int(c) for c in os.environ.get("PFML_DGEMM_CFGS", "3,6,7,8,9,10,11").split(",")]
     pick = os.environ.get("PFML_DGEMM_SHAPES")
     shapes = [s for s in SHAPES if not pick or s[0] in pick.split(",")]
     dev = torch.device("cuda", 0)
@@ -75,6 +75,7 @@ def main():
             ref = torch.tril(ref) + torch.tril(ref, -1).transpose(1, 2)
         fl = 2.0 * b * M * N * K          # (sym: the full product's flops, for comparison)
         for cfg in cfgs:
+            C.fill_(float("nan"))                     # no stale result can pass the check
             gemm_fused(A, B, C, tile_cfg=cfg, **kw)
             err = float((C - ref).abs().max() / ref.abs().max())
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
