@@ -153,11 +153,12 @@ def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor,
 
 
 # GEMM tile config of the symmetric form's products (csrc/gemm_f64.hip tile_cfg; 0: auto);
-# PFML_SPD_SYM=0 takes the two-sided form for every m_func inverse (A/B switch)
+# PFML_SPD_SYM=0 takes the two-sided form for every m_func inverse, PFML_DB_SYM=0 /
+# PFML_DB_SYMPROD=0 the two-sided inverse / product inside Denman-Beavers (A/B switches)
 SYM_GEMM_CFG = int(os.environ.get("PFML_SYM_GEMM_CFG", "0"))
 SYM_INVERSE = os.environ.get("PFML_SPD_SYM", "1") != "0"
-DB_SYM = os.environ.get("PFML_DB_SYM", "0") == "1"
-DB_SYMPROD = os.environ.get("PFML_DB_SYMPROD", "0") == "1"
+DB_SYM = os.environ.get("PFML_DB_SYM", "1") != "0"
+DB_SYMPROD = os.environ.get("PFML_DB_SYMPROD", "1") != "0"
 
 
 def spd_inverse_sym(X: torch.Tensor, status: torch.Tensor) -> torch.Tensor:
@@ -455,18 +456,27 @@ def _db_mu(M: torch.Tensor, Minv: torch.Tensor, unscaled: bool, out: torch.Tenso
 
 
 def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tensor | None,
-             ws: list) -> torch.Tensor:
+             ws: list, exact_sym: bool = False) -> torch.Tensor:
     """sqrtm(S) by ``iters`` scaled product-form Denman-Beavers steps with NO host sync:
     norm scaling mu (computed on the device) for the first ``scaled_iters`` steps, then
-    quadratically convergent unscaled steps.  ws: 4 [B, N, N] work buffers."""
+    quadratically convergent unscaled steps.  ws: 4 [B, N, N] work buffers; ``exact_sym``: S is
+    exactly symmetric (bit for bit)."""
     B, N, _ = S.shape
     M, Y, Mi, Yn = ws
     M.copy_(S)
     Y.copy_(S)
     mu = torch.empty(B, dtype=S.dtype, device=S.device)
+    # S, M, M^-1 and Y are symmetric (M, Y are polynomials in S; in exact arithmetic Y and M^-1
+    # commute, so Y M^-1 is symmetric too).  sym_inv: M^-1 by the one-triangle inverse;
+    # sym_prod: Y M^-1 on its lower tiles, mirrored.  With both (and S exactly symmetric, as
+    # m_tilde builds it; after the first M update otherwise) every iterate is EXACTLY symmetric
+    # and the M update skips its mirror reads (flat).  profiles/r05_mfunc_db_accuracy.json: m
+    # vs the reference form 4e-14 (two-sided products: 3e-14); S4 -12 ms.
+    dev_sym = nat.is_device(M) and N >= _BLOCKED_MIN_N
+    sym_inv, sym_prod = DB_SYM and dev_sym, DB_SYMPROD and dev_sym
     for it in range(iters):
-        if DB_SYM and nat.is_device(M) and N >= _BLOCKED_MIN_N:
-            Mi.copy_(M)                          # (experiment: one-triangle inverse in DB)
+        if sym_inv:
+            Mi.copy_(M)
             spd_inverse_sym(Mi, status)
         else:
             spd_inverse_into(M, Mi, status)
@@ -474,12 +484,10 @@ def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tenso
         # Y' = (mu/2) Y + (1/(2 mu)) Y M^-1 ;  M' = I/2 + (mu^2 M + mu^-2 M^-1)/4
         rs = (0.5 / mu).view(B, 1).expand(B, N).contiguous()
         es = (0.5 * mu).view(B, 1).expand(B, N).contiguous()
-        # (Y and M^-1 are commuting symmetric matrices in exact arithmetic: DB_SYMPROD takes
-        # the product's lower triangle only, mirrored - an experiment switch)
-        gemm_fused(Y, Mi, Yn, row_scale=rs, addend=Y, addend_row_scale=es,
-                   sym=DB_SYMPROD and nat.is_device(Y))
+        gemm_fused(Y, Mi, Yn, row_scale=rs, addend=Y, addend_row_scale=es, sym=sym_prod)
         Y, Yn = Yn, Y
-        mf_sym(MF_DB, M, Mi, Yn, svec=mu)        # Yn is free here: new M into it
+        mf_sym(MF_DB, M, Mi, Yn, svec=mu, flat=sym_inv and (exact_sym or it > 0))
+        # (Yn was free: the new M went into it)
         M, Yn = Yn, M
     ws[0], ws[1], ws[2], ws[3] = M, Y, Mi, Yn
     return Y
@@ -526,12 +534,15 @@ def m_tilde(sigma: torch.Tensor, lam: torch.Tensor, w: torch.Tensor, rf: torch.T
     # tiles, an exactly symmetric S - and Denman-Beavers' M stays so)
     gemm_fused(x, x, S, addend=x, addend_row_scale=four, sym=True)
     ws = [torch.empty_like(sigma) for _ in range(4)]
-    root = _db_sqrt(S, db_iters, DB_SCALED_ITERS, status, ws)
+    root = _db_sqrt(S, db_iters, DB_SCALED_ITERS, status, ws, exact_sym=True)
     # m_tilde_0 = (sigma_hat - root)/2 = 2 (sigma_hat + root)^-1   (cancellation-free form)
     mt = ws[2]
-    mf_sym(MF_SHAT, x, root, mt, d=2.0)
+    # (x is exactly symmetric - MF_X symmetrises - and so is root when its last product was
+    # the one-triangle one)
+    mf_sym(MF_SHAT, x, root, mt, d=2.0, flat=DB_SYMPROD and db_iters > 0
+           and nat.is_device(x) and N >= _BLOCKED_MIN_N)
     # (the 11 inverses below are of exactly symmetric arguments and only used symmetrically:
-    # the one-triangle form; the Denman-Beavers product above keeps the two-sided one)
+    # the one-triangle form)
     spd_inverse_sym(mt, status)
     mt.mul_(2.0)
     Aq = ws[3]

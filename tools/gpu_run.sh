@@ -184,6 +184,10 @@ for step in ${MODE//,/ }; do
       rc=$?; if [ $rc -ne 0 ]; then tail -3 $OUT/prof_s4.log; exit $rc; fi
       python tools/rocprof_summary.py $(find $OUT/prof_s4 -name "*.db" | head -1) --top 14 > $OUT/kernels_s4.txt 2>&1
       rm -rf $OUT/prof_s4; cat $OUT/kernels_s4.txt ;;
+    s4b)
+      # S4+S5+S6 bench only (A/B of an env switch: PFML_* set by the caller)
+      timeout -k 10 600 python bench.py --with-inputs --steps 2 --warmup 1 > $OUT/bench_s4b.json 2> $OUT/bench_s4b.err
+      rc=$?; grep -o '"ms_per_step": [0-9.]*' $OUT/bench_s4b.json; if [ $rc -ne 0 ]; then tail -3 $OUT/bench_s4b.err; exit $rc; fi ;;
     stress)
       timeout -k 10 900 python -u bench.py --s4-stress 48 --stocks 3000 --warmup 1 > $OUT/stress3000.json 2> $OUT/stress3000.err
       rc=$?; cat $OUT/stress3000.json; tail -2 $OUT/stress3000.err; if [ $rc -ne 0 ]; then exit $rc; fi ;;
