@@ -235,24 +235,23 @@ constexpr int NBL = 64;
 // q, so the owners publish whole register tiles to a double-buffered LDS line
 // (one barrier per step, no second barrier: the buffer written at step q + 2 is rewritten
 // only after every thread has passed step q + 1's barrier, i.e. finished reading it).  Frame
-// entries past nb hold the identity, so partial blocks need no special case.  Output to any
-// (ld, batch stride): in place (Pout = the block itself) or to a packed buffer.
-__global__ __launch_bounds__(256) void spd_leafinv_kernel(const double* __restrict__ A,
-                                                          int64_t lda, int64_t sA, int k0,
-                                                          int nb, double* Pout, int64_t ldp,
-                                                          int64_t sP, int* __restrict__ status,
-                                                          int sym) {
-  __shared__ double rowb[2][4][64], colb[2][64][4];
-  const int b = blockIdx.x, t = threadIdx.x;
+// entries past nb hold the identity, so partial blocks need no special case.  ``src``: the
+// block (global or LDS, leading dimension ld); the inverse is left in a (thread (rb, cb) =
+// (t >> 4, t & 15): rows 4 rb.., columns 4 cb..).  Every thread of the block must call it.
+struct GjLds {
+  double rowb[2][4][64], colb[2][64][4];
+};
+
+__device__ __forceinline__ bool gj64(const double* src, int64_t ld, int nb, double (&a)[4][4],
+                                     GjLds& sh) {
+  const int t = threadIdx.x;
   const int rb = t >> 4, cb = t & 15;
-  const double* Ab = A + (int64_t)b * sA + (int64_t)k0 * lda + k0;
-  double a[4][4];
 #pragma unroll
   for (int u = 0; u < 4; ++u)
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int i = 4 * rb + u, j = 4 * cb + v;
-      a[u][v] = Ab[(int64_t)min(i, nb - 1) * lda + min(j, nb - 1)];
+      a[u][v] = src[(int64_t)min(i, nb - 1) * ld + min(j, nb - 1)];
     }
 #pragma unroll
   for (int u = 0; u < 4; ++u)
@@ -269,70 +268,71 @@ __global__ __launch_bounds__(256) void spd_leafinv_kernel(const double* __restri
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) rowb[buf][r][4 * cb + v] = a[r][v];
+        for (int v = 0; v < 4; ++v) sh.rowb[buf][r][4 * cb + v] = a[r][v];
     }
     if (cb == q) {
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) colb[buf][4 * rb + u][c] = a[u][c];
+        for (int c = 0; c < 4; ++c) sh.colb[buf][4 * rb + u][c] = a[u][c];
     }
     __syncthreads();
     // The 4 pivots of the block, replayed as SCALAR Gauss-Jordan steps on the thread's local
     // 8 x 8 view M = [[P, rp], [cp, a]] (P = A_KK, rp = A_K,mycols, cp = A_myrows,K): every
-    // entry sees exactly the update sequence, and the expressions, of one-pivot-at-a-time GJ,
-    // so the result is bitwise that of the LDS kernel (an explicit P^-1 block step amplifies
-    // rounding by cond(P) on ill-conditioned Denman-Beavers iterates).
+    // entry sees the update sequence of one-pivot-at-a-time GJ (an explicit P^-1 block step
+    // amplifies rounding by cond(P) on ill-conditioned Denman-Beavers iterates).  Pivot row
+    // scaled first, then one FMA per updated entry: M[r][c] -= M[r][p] (M[p][c] / piv).
     double P[4][4], rp[4][4], cp[4][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) P[r][c] = rowb[buf][r][4 * q + c];
+      for (int c = 0; c < 4; ++c) P[r][c] = sh.rowb[buf][r][4 * q + c];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) rp[r][v] = rowb[buf][r][4 * cb + v];
+      for (int v = 0; v < 4; ++v) rp[r][v] = sh.rowb[buf][r][4 * cb + v];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) cp[u][c] = colb[buf][4 * rb + u][c];
+      for (int c = 0; c < 4; ++c) cp[u][c] = sh.colb[buf][4 * rb + u][c];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const double piv = P[p][p];
       bad |= !(piv > 0.0) || !isfinite(piv);
       const double inv = 1.0 / piv;
+      // pivot row (its final values)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) rp[p][v] *= inv;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c != p) P[p][c] *= inv;
       // a (rows != p, cols != p: always, the thread's rows / cols are outside K unless it
       // owns the pivot block, whose result is then read from P / rp / cp below)
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int v = 0; v < 4; ++v) a[u][v] -= cp[u][p] * rp[p][v] * inv;
+        for (int v = 0; v < 4; ++v) a[u][v] = fma(-cp[u][p], rp[p][v], a[u][v]);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if (r != p)
 #pragma unroll
-          for (int v = 0; v < 4; ++v) rp[r][v] -= P[r][p] * rp[p][v] * inv;
+          for (int v = 0; v < 4; ++v) rp[r][v] = fma(-P[r][p], rp[p][v], rp[r][v]);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int c = 0; c < 4; ++c)
-          if (c != p) cp[u][c] -= cp[u][p] * P[p][c] * inv;
+          if (c != p) cp[u][c] = fma(-cp[u][p], P[p][c], cp[u][c]);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int c = 0; c < 4; ++c)
-          if (r != p && c != p) P[r][c] -= P[r][p] * P[p][c] * inv;
-      // pivot row / column scaling (old values of row p / column p used above)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) rp[p][v] *= inv;
+          if (r != p && c != p) P[r][c] = fma(-P[r][p], P[p][c], P[r][c]);
+      // pivot column (old values used above)
 #pragma unroll
       for (int u = 0; u < 4; ++u) cp[u][p] *= -inv;
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (c != p) {
-          P[p][c] *= inv;
-          P[c][p] *= -inv;
-        }
+      for (int r = 0; r < 4; ++r)
+        if (r != p) P[r][p] *= -inv;
       P[p][p] = inv;
     }
     const bool inr = rb == q, inc = cb == q;
@@ -342,6 +342,20 @@ __global__ __launch_bounds__(256) void spd_leafinv_kernel(const double* __restri
       for (int v = 0; v < 4; ++v)
         a[u][v] = (inr && inc) ? P[u][v] : (inr ? rp[u][v] : (inc ? cp[u][v] : a[u][v]));
   }
+  return bad;
+}
+
+// Output to any (ld, batch stride): in place (Pout = the block itself) or to a packed buffer.
+__global__ __launch_bounds__(256) void spd_leafinv_kernel(const double* __restrict__ A,
+                                                          int64_t lda, int64_t sA, int k0,
+                                                          int nb, double* Pout, int64_t ldp,
+                                                          int64_t sP, int* __restrict__ status,
+                                                          int sym) {
+  __shared__ GjLds sh;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int rb = t >> 4, cb = t & 15;
+  double a[4][4];
+  const bool bad = gj64(A + (int64_t)b * sA + (int64_t)k0 * lda + k0, lda, nb, a, sh);
   if (t == 0 && bad) status[b] = 1;
   double* Pb = Pout + (int64_t)b * sP;
 #pragma unroll
@@ -358,6 +372,220 @@ __global__ __launch_bounds__(256) void spd_leafinv_kernel(const double* __restri
       }
     }
 }
+
+// ---------------------------------------------------------------------------------------
+// One whole node of the one-triangle recursive inverse (ops/linalg.py spd_inverse_sym) for
+// 64 < nn <= 128, in ONE launch (one workgroup per matrix): the two 64-leaf Gauss-Jordan
+// inverses and the node's four products on the MFMA, with every operand in LDS -
+//
+//     X11 = A11^-1 (GJ),  W = X11 A12,  S = A22 - A21 W (lower tiles, mirrored),
+//     X22 = S^-1 (GJ),  X12 = -W X22 (X21 = X12'),  X11 -= X12 W' (lower tiles, mirrored)
+//
+// instead of 4 GEMM launches + 2 leaf launches per node (the 64-wide GEMMs ran at 5-9 TF/s:
+// tile prologue / epilogue and launch bound).  Each product walks k in steps of 4 from 0 with
+// zero padding past K and applies the same epilogue expressions as the fused GEMM
+// (csrc/gemm_f64.hip: v = -acc + C, v = -acc), and the leaves are the same gj64, so the node is
+// bitwise the launch sequence it replaces.  Input block exactly symmetric (A12 = A21' is read
+// as A21).  LDS: two 64 x 64 operand images + the GJ lines (~76 KB: two workgroups per CU);
+// X11 stays in the GJ registers between its inverse and the final update.
+constexpr int NLP = 66;                        // operand image row stride (doubles)
+
+struct NodeLds {
+  double u[64][NLP];                           // X11 -> W
+  double v[64][NLP];                           // A21 -> S -> X22 -> X12 -> X12 W'
+  GjLds gj;
+};
+
+// acc[q] (q < nt) = sum_k A(ti[q] * 16 + i, k) B(k, tj[q] * 16 + j), k < K (zero past K);
+// fa(i, k) / fb(k, j) read the LDS images (k, i, j in range: the callers clamp / mask)
+template <int NT, class FA, class FB>
+__device__ __forceinline__ void node_mm(const int (&ti)[NT], const int (&tj)[NT], int nt, int K,
+                                        FA fa, FB fb, double4_t (&acc)[NT]) {
+  const int lane = threadIdx.x & 63, li = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < NT; ++q) acc[q] = double4_t{0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < K; k0 += 4) {
+    const int k = k0 + lk;
+    const bool ok = k < K;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      if (q < nt) {
+        const double av = ok ? fa(ti[q] * 16 + li, k) : 0.0;
+        const double bv = ok ? fb(k, tj[q] * 16 + li) : 0.0;
+        acc[q] = mfma_f64_16x16x4(av, bv, acc[q]);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void spd_node_sym_kernel(double* __restrict__ X,
+                                                             int64_t ld, int64_t sX, int r0,
+                                                             int nn, int* __restrict__ status) {
+  __shared__ NodeLds L;
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int lane = t & 63, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int rb = t >> 4, cb = t & 15;
+  const int m = nn - 64;                       // 1..64
+  const int tn = (m + 15) >> 4;                // 16-wide tiles over m
+  double* Xb = X + (int64_t)b * sX + (int64_t)r0 * ld + r0;
+  double* X21 = Xb + (int64_t)64 * ld;         // rows 64.., columns 0..
+  double* X22 = X21 + 64;
+  // A21 -> v (rows >= m: zero)
+  for (int e = t; e < 64 * 64; e += 256) {
+    const int i = e >> 6, k = e & 63;
+    L.v[i][k] = i < m ? X21[(int64_t)i * ld + k] : 0.0;
+  }
+  // X11 = A11^-1 (registers), its mirrored image -> u
+  double x11[4][4];
+  bool bad = gj64(Xb, ld, 64, x11, L.gj);
+#pragma unroll
+  for (int uu = 0; uu < 4; ++uu)
+#pragma unroll
+    for (int vv = 0; vv < 4; ++vv) {
+      const int i = 4 * rb + uu, j = 4 * cb + vv;
+      if (i >= j) {
+        L.u[i][j] = x11[uu][vv];
+        L.u[j][i] = x11[uu][vv];
+      }
+    }
+  __syncthreads();
+  double4_t acc[4];
+  // W = X11 A21' (64 x m): wave w = tile row w, all tn tile columns
+  {
+    const int ti[4] = {w, w, w, w}, tj[4] = {0, 1, 2, 3};
+    node_mm<4>(ti, tj, tn, 64, [&](int i, int k) { return L.u[i][k]; },
+               [&](int k, int j) { return L.v[j][k]; }, acc);
+  }
+  __syncthreads();                             // u (X11) fully read
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < tn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = w * 16 + PFML_F64_CROW(lane, r), j = q * 16 + li;
+        L.u[i][j] = j < m ? acc[q][r] : 0.0;  // W (columns >= m: zero)
+      }
+  __syncthreads();
+  // S = A22 - A21 W: lower tiles (I >= J) of the tn x tn grid, round-robin over the waves
+  {
+    int ti[3], tj[3], nt = 0;
+    const int nl = tn * (tn + 1) / 2;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int l = w + 4 * q;
+      int I = 0;
+      while ((I + 1) * (I + 2) / 2 <= l) ++I;
+      ti[q] = l < nl ? I : 0;
+      tj[q] = l < nl ? l - I * (I + 1) / 2 : 0;
+      nt += l < nl;
+    }
+    double4_t sacc[3];
+    node_mm<3>(ti, tj, nt, 64, [&](int i, int k) { return L.v[i][k]; },
+               [&](int k, int j) { return L.u[k][j]; }, sacc);
+    double sv[3][4];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = ti[q] * 16 + PFML_F64_CROW(lane, r), j = tj[q] * 16 + li;
+        const double c = (q < nt && i < m && j < m) ? X22[(int64_t)i * ld + j] : 0.0;
+        sv[q][r] = -sacc[q][r] + c;
+      }
+    __syncthreads();                           // v (A21) fully read
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (q < nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = ti[q] * 16 + PFML_F64_CROW(lane, r), j = tj[q] * 16 + li;
+          if (i < m && j < m && i >= j) {
+            L.v[i][j] = sv[q][r];
+            L.v[j][i] = sv[q][r];
+          }
+        }
+  }
+  __syncthreads();
+  // X22 = S^-1 -> global (lower, mirrored) and v (its mirrored image, zero outside m x m)
+  double x22[4][4];
+  bad |= gj64(&L.v[0][0], NLP, m, x22, L.gj);
+  __syncthreads();                             // every thread has loaded S from v
+#pragma unroll
+  for (int uu = 0; uu < 4; ++uu)
+#pragma unroll
+    for (int vv = 0; vv < 4; ++vv) {
+      const int i = 4 * rb + uu, j = 4 * cb + vv;
+      if (i >= j) {
+        const bool in = i < m;
+        L.v[i][j] = in ? x22[uu][vv] : 0.0;
+        L.v[j][i] = in ? x22[uu][vv] : 0.0;
+        if (in) {
+          X22[(int64_t)i * ld + j] = x22[uu][vv];
+          X22[(int64_t)j * ld + i] = x22[uu][vv];
+        }
+      }
+    }
+  if (t == 0 && bad) status[b] = 1;
+  __syncthreads();
+  // X12 = -W X22 (64 x m) -> global X12 and X21 = X12'
+  {
+    const int ti[4] = {w, w, w, w}, tj[4] = {0, 1, 2, 3};
+    node_mm<4>(ti, tj, tn, m, [&](int i, int k) { return L.u[i][k]; },
+               [&](int k, int j) { return L.v[k][j]; }, acc);
+  }
+  __syncthreads();                             // v (X22) fully read
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < tn)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = w * 16 + PFML_F64_CROW(lane, r), j = q * 16 + li;
+        const double v = -acc[q][r];
+        L.v[i][j] = j < m ? v : 0.0;
+        if (j < m) {
+          Xb[(int64_t)i * ld + 64 + j] = v;
+          X21[(int64_t)j * ld + i] = v;
+        }
+      }
+  __syncthreads();
+  // D = X12 W' on the lower tiles of 64 x 64 (10 tiles), then X11 -= D (lower, mirrored)
+  {
+    int ti[3], tj[3], nt = 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int l = w + 4 * q;
+      int I = 0;
+      while ((I + 1) * (I + 2) / 2 <= l) ++I;
+      ti[q] = l < 10 ? I : 0;
+      tj[q] = l < 10 ? l - I * (I + 1) / 2 : 0;
+      nt += l < 10;
+    }
+    double4_t dacc[3];
+    node_mm<3>(ti, tj, nt, m, [&](int i, int k) { return L.v[i][k]; },
+               [&](int k, int j) { return L.u[j][k]; }, dacc);
+    __syncthreads();                           // v (X12) and u (W) fully read
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (q < nt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = ti[q] * 16 + PFML_F64_CROW(lane, r), j = tj[q] * 16 + li;
+          L.u[i][j] = dacc[q][r];
+        }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int uu = 0; uu < 4; ++uu)
+#pragma unroll
+    for (int vv = 0; vv < 4; ++vv) {
+      const int i = 4 * rb + uu, j = 4 * cb + vv;
+      if (i >= j) {
+        const double v = -L.u[i][j] + x11[uu][vv];
+        Xb[(int64_t)i * ld + j] = v;
+        Xb[(int64_t)j * ld + i] = v;
+      }
+    }
+}
 }  // namespace
 
 // Inverse of the nb x nb (nb <= 64) diagonal block at (k0, k0) of A written to the block at
@@ -370,5 +598,16 @@ extern "C" hipError_t pfml_spd_leafinv_to(const double* A, int64_t lda, int64_t 
   if (nb > NBL) return hipErrorInvalidValue;
   hipLaunchKernelGGL(spd_leafinv_kernel, dim3(batch), dim3(256), 0, st, A, lda, sA, k0, nb,
                      P + (int64_t)k0 * ldp + k0, ldp, sP, status, sym);
+  return hipGetLastError();
+}
+
+// In-place one-triangle inverse of the nn x nn diagonal block at (r0, r0) of every matrix,
+// 64 < nn <= 128 (exactly symmetric input and output), one launch (spd_node_sym_kernel).
+extern "C" hipError_t pfml_spd_node_sym(double* X, int64_t ld, int64_t sX, int batch, int r0,
+                                        int nn, int* status, hipStream_t st) {
+  if (batch <= 0) return hipSuccess;
+  if (nn <= NBL || nn > 2 * NBL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(spd_node_sym_kernel, dim3(batch), dim3(256), 0, st, X, ld, sX, r0, nn,
+                     status);
   return hipGetLastError();
 }

@@ -85,6 +85,9 @@ nat.register_hip("pfml_spd_leafinv_to", [C.c_void_p, C.c_int64, C.c_int64, C.c_v
                                          C.c_int64, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                          C.c_int, C.c_void_p])
 
+nat.register_hip("pfml_spd_node_sym", [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int,
+                                       C.c_int, C.c_void_p, C.c_void_p])
+
 _REC_LEAF = 64
 _REC_BUFS: dict = {}
 
@@ -159,6 +162,9 @@ SYM_GEMM_CFG = int(os.environ.get("PFML_SYM_GEMM_CFG", "0"))
 SYM_INVERSE = os.environ.get("PFML_SPD_SYM", "1") != "0"
 DB_SYM = os.environ.get("PFML_DB_SYM", "1") != "0"
 DB_SYMPROD = os.environ.get("PFML_DB_SYMPROD", "1") != "0"
+# nodes of 65..128 rows in one launch (csrc/spd_inverse.hip spd_node_sym_kernel: both leaves and
+# the four products in LDS, bitwise the GEMM + leaf launches it replaces); 0: those launches
+SYM_NODE = os.environ.get("PFML_SPD_NODE", "1") != "0"
 
 
 def spd_inverse_sym(X: torch.Tensor, status: torch.Tensor) -> torch.Tensor:
@@ -194,6 +200,15 @@ def spd_inverse_sym(X: torch.Tensor, status: torch.Tensor) -> torch.Tensor:
             nat.check(lib.pfml_spd_leafinv_to(X.data_ptr(), ld, sX, X.data_ptr(), ld, sX, B, r0,
                                               nn, status.data_ptr(), 1, st),
                       "pfml_spd_leafinv_to")
+            return
+        if SYM_NODE and nn <= 2 * _REC_LEAF:
+            m = nn - _REC_LEAF
+            _work.add("spd_node_sym_kernel", B * (2.0 * _REC_LEAF ** 3 + 2.0 * m ** 3
+                                                  + 3.0 * _REC_LEAF ** 2 * m
+                                                  + 3.0 * _REC_LEAF * m * m),
+                      8.0 * B * 2 * nn * nn)
+            nat.check(lib.pfml_spd_node_sym(X.data_ptr(), ld, sX, B, r0, nn, status.data_ptr(),
+                                            st), "pfml_spd_node_sym")
             return
         h = _rec_split(nn)
         m = nn - h

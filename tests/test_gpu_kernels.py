@@ -167,6 +167,32 @@ def test_spd_inverse_sym(gpu, n):
     assert e_sym < 1e-11 and e_sym < 4 * e_two + 1e-14, (e_sym, e_two)
 
 
+@pytest.mark.parametrize("n", [490, 257, 200])
+def test_spd_node_sym_bitwise(gpu, n):
+    """The one-launch 65..128-row node (csrc/spd_inverse.hip spd_node_sym_kernel) is bitwise the
+    GEMM + leaf launch sequence it replaces (490: nodes of 128 and 106 rows; 257: a 65-row node,
+    m = 1; 200: 128 and 72), including the non-positive-pivot flags."""
+    import pfml.ops.linalg as la
+    g = torch.Generator().manual_seed(n + 1)
+    X = torch.randn(6, n + 40, n, generator=g, dtype=torch.float64)
+    A = X.transpose(1, 2) @ X / n + 1e-3 * torch.eye(n, dtype=torch.float64)
+    A = 0.5 * (A + A.transpose(1, 2))
+    A[5, n - 3, n - 3] = -50.0                     # not SPD: a pivot of the last node fails
+    outs, sts = [], []
+    for node in (True, False):
+        la.SYM_NODE = node
+        try:
+            st = torch.zeros(6, dtype=torch.int32, device=gpu)
+            outs.append(la.spd_inverse_sym(A.to(gpu).contiguous(), st).cpu())
+            sts.append(st.cpu())
+        finally:
+            la.SYM_NODE = True
+    assert torch.equal(sts[0], sts[1]) and sts[0].tolist() == [0, 0, 0, 0, 0, 1]
+    assert torch.equal(outs[0][:5], outs[1][:5])
+    ref = torch.linalg.inv(A[:5])
+    assert ((outs[0][:5] - ref).norm(dim=(1, 2)) / ref.norm(dim=(1, 2))).max() < 1e-11
+
+
 def test_segment_sums(gpu):
     from pfml.ops.ridge import segment_sums
     X = _rand(40, 7, 9, seed=7)

@@ -182,7 +182,7 @@ for step in ${MODE//,/ }; do
       rc=$?; grep '^{' $OUT/bench_s4.json | cut -c1-300; if [ $rc -ne 0 ]; then tail -3 $OUT/bench_s4.err; exit $rc; fi
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_s4 -o run -- python3 $ROOT/bench.py --with-inputs --steps 1 --warmup 0 > $OUT/prof_s4.log 2>&1)
       rc=$?; if [ $rc -ne 0 ]; then tail -3 $OUT/prof_s4.log; exit $rc; fi
-      python tools/rocprof_summary.py $(find $OUT/prof_s4 -name "*.db" | head -1) --top 14 > $OUT/kernels_s4.txt 2>&1
+      python tools/rocprof_summary.py $(find $OUT/prof_s4 -name "*.db" | head -1) --top 30 > $OUT/kernels_s4.txt 2>&1
       rm -rf $OUT/prof_s4; cat $OUT/kernels_s4.txt ;;
     s4b)
       # S4+S5+S6 bench only (A/B of an env switch: PFML_* set by the caller)
