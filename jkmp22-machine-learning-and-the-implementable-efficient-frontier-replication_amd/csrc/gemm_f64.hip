@@ -53,6 +53,8 @@ struct Epi {
   // Horner step consumes it (K11/K12 fused into K5/K6: S_theta is never stored)
   const int64_t* erow; int64_t serow;
   const double* ecm; const double* ecs; int64_t secm;
+  const double* os; int64_t sos;      // output row scale, applied last (null: 1): the next
+                                      // Horner step's k-scale folded into this step's output
 };
 
 // Output tile of workgroup wg: batch entry b, first row bm / column bn.  Grouped order:
@@ -118,6 +120,7 @@ __device__ __forceinline__ void store_tile(const double4_t (&acc)[TM][TN], const
   const double* Eb = ep.E ? ep.E + (int64_t)b * ep.sE : nullptr;
   const double* dvb = ep.dv ? ep.dv + (int64_t)b * ep.sdv : nullptr;
   const double* esb = ep.es ? ep.es + (int64_t)b * ep.ses : nullptr;
+  const double* osb = ep.os ? ep.os + (int64_t)b * ep.sos : nullptr;
   double* Ctb = ep.Ct ? ep.Ct + (int64_t)b * ep.sCt : nullptr;
   const unsigned cbytes = (unsigned)(((int64_t)(M - 1) * ldc + N) * 8);
   const auto rsC = uniform_rsrc(C, cbytes);
@@ -141,7 +144,7 @@ __device__ __forceinline__ void store_tile(const double4_t (&acc)[TM][TN], const
   for (int i = 0; i < TM; ++i) {
     int gic[4];
     int64_t erw[4];
-    double rsv[4], esv[4], dvv[4], cv[TN][4], ev[TN][4];
+    double rsv[4], esv[4], dvv[4], osv[4], cv[TN][4], ev[TN][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       gic[r] = min(r0 + i * 16 + PFML_F64_CROW(lane, r), M - 1);
@@ -152,6 +155,7 @@ __device__ __forceinline__ void store_tile(const double4_t (&acc)[TM][TN], const
       rsv[r] = rsb ? rsb[gic[r]] : 1.0;
       esv[r] = esb ? esb[gic[r]] : 1.0;
       dvv[r] = dvb ? dvb[gic[r]] : ep.dval;
+      osv[r] = osb ? osb[gic[r]] : 1.0;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         cv[j][r] = has_beta ? C[(int64_t)gic[r] * ldc + gjc[j]] : 0.0;
@@ -171,6 +175,7 @@ __device__ __forceinline__ void store_tile(const double4_t (&acc)[TM][TN], const
         v += (has_e && gj < ep.e_cols)
                  ? esv[r] * (erb ? (ev[j][r] - ecmv[j]) * ecsv[j] : ev[j][r]) : 0.0;
         v += (ep.has_diag && gj - ep.diag_col0 == gi) ? dvv[r] : 0.0;
+        v *= osv[r];
         const bool ok = gi < M && gj < N && (!ep.sym || gi >= gj);
         const u32x2_t bits = __builtin_bit_cast(u32x2_t, v);
         __builtin_amdgcn_raw_buffer_store_b64(
@@ -651,6 +656,7 @@ struct PfmlGemmEpi {
   double* Ct; int64_t ldct, sCt;
   const int64_t* erow; int64_t serow;
   const double* ecm; const double* ecs; int64_t secm;
+  const double* os; int64_t sos;
   int tile_cfg;      // 0 auto, 1: 128x128, 2: 128x64, 3: 64x64 (BK 16, two LDS buffers);
                      // 4: 64x64 BK 32 one buffer, 5: 64x64 BK 32 two buffers (a 128x128
                      // BK 32 form spills: 144 B per lane)
@@ -671,7 +677,7 @@ extern "C" hipError_t pfml_dgemm_ex(int ta, int tb, int M, int N, int K, int bat
   Epi ep{h->alpha, h->beta, h->rs, h->srs, h->cs, h->scs, h->ks, h->sks, h->E, h->lde, h->sE,
          h->e_cols, h->diag_col0, h->dval, h->dv, h->sdv, h->has_diag, h->es, h->ses,
          h->sincos, h->sym, h->Ct, h->ldct, h->sCt, h->erow, h->serow, h->ecm, h->ecs,
-         h->secm};
+         h->secm, h->os, h->sos};
   // symmetric mode: square C, square tiles, no sincos
   if (h->sym && (M != N || h->sincos)) return hipErrorInvalidValue;
   // the epilogue's buffer stores address a batch entry of C / Ct with 32-bit byte offsets

@@ -496,20 +496,27 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
         # GP + N instead of 22 of GP + N (29 % fewer Horner flops at N = 490, GP = 1026).
         Dg = plan.gt[bt.idx]                                        # [B, 13, N]
         ainv = 1.0 / a
+        # k-scales D_theta / a of every step; step theta's GEMM takes T_{theta+1} with its rows
+        # already scaled by ks[theta] (written so by step theta + 1's epilogue, out_row_scale),
+        # so the ten width-(GP + 2N) main loops carry no k-scale (T_1 stays unscaled: T_0 and
+        # U_0 use it)
+        ks = Dg * ainv.unsqueeze(1)                                 # [B, 13, N]
         Wr = Wd + N
         Tb = [torch.empty((B, N, Wr), dtype=torch.float64, device=dev) for _ in range(2)]
-        eye = torch.eye(N, dtype=torch.float64, device=dev)
-        Tb[0][:, :, :GP] = S[:, 1]
-        Tb[0][:, :, GP:Wd] = eye
+        k10 = ks[:, lb - 1].unsqueeze(-1)
+        torch.mul(S[:, 1], k10, out=Tb[0][:, :, :GP])
+        Tb[0][:, :, GP:Wd] = torch.diag_embed(ks[:, lb - 1])
         # R_11 = diag(a) m_tilde diag(D_11 / a): elementwise, in the rounding order the fused
-        # GEMM against the identity produced ((m_tilde * k-scale) * row scale)
-        torch.mul(mt * (Dg[:, lb] * ainv).unsqueeze(-2), a.unsqueeze(-1), out=Tb[0][:, :, Wd:])
+        # GEMM against the identity produced ((m_tilde * k-scale) * row scale), then ks_10
+        torch.mul(mt * ks[:, lb].unsqueeze(-2), a.unsqueeze(-1), out=Tb[0][:, :, Wd:])
+        Tb[0][:, :, Wd:].mul_(k10)
         cur = 0
         for th in range(lb - 1, 0, -1):
-            gemm_fused(mt, Tb[cur], Tb[cur ^ 1], row_scale=a, k_scale=(Dg[:, th] * ainv),
+            gemm_fused(mt, Tb[cur], Tb[cur ^ 1], row_scale=a,
                        addend=Fcat, addend_cols=GP, addend_rows=bt.idx[:, th],
                        addend_col_shift=stats[:, th - 1, 0], addend_col_scale=stats[:, th - 1, 1],
-                       addend_row_scale=ivol[:, th - 1], diag_col0=GP, diag_value=1.0)
+                       addend_row_scale=ivol[:, th - 1], diag_col0=GP, diag_value=1.0,
+                       out_row_scale=ks[:, th - 1] if th > 1 else None)
             cur ^= 1
         T1 = Tb[cur]
         # T0 / U0 carry LU_PANEL_COLS scratch columns for the two-level solve below
@@ -517,7 +524,7 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
         T0f = torch.empty((B, N, Wz), dtype=torch.float64, device=dev)
         U0f = torch.empty_like(T0f)
         T0, U0 = T0f[:, :, :Wd], U0f[:, :, :Wd]
-        gemm_fused(mt, T1[:, :, :Wd], T0, row_scale=a, k_scale=(Dg[:, 0] * ainv),
+        gemm_fused(mt, T1[:, :, :Wd], T0, row_scale=a, k_scale=ks[:, 0].contiguous(),
                    addend=S[:, 0], addend_cols=GP, diag_col0=GP, diag_value=1.0)
         # U_0 = T_1 + Q [S_12 | I]: the S_12 block on the GEMM, the identity block as Q + T_1
         gemm_fused(T1[:, :, Wd:], S[:, 2], U0[:, :, :GP], addend=T1[:, :, :GP],

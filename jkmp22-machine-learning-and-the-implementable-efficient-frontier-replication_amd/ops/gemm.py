@@ -28,7 +28,7 @@ class _Epi(C.Structure):
                 ("diag_col0", _I), ("dval", _D), ("dv", _P), ("sdv", _L), ("has_diag", _I),
                 ("es", _P), ("ses", _L), ("sincos", _I), ("sym", _I), ("Ct", _P), ("ldct", _L),
                 ("sCt", _L), ("erow", _P), ("serow", _L), ("ecm", _P), ("ecs", _P),
-                ("secm", _L), ("tile_cfg", _I)]
+                ("secm", _L), ("os", _P), ("sos", _L), ("tile_cfg", _I)]
 
 
 nat.register_hip("pfml_dgemm_ex", [_I, _I, _I, _I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _L,
@@ -285,10 +285,14 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
                mirror_out: torch.Tensor | None = None,
                addend_rows: torch.Tensor | None = None,
                addend_col_shift: torch.Tensor | None = None,
-               addend_col_scale: torch.Tensor | None = None) -> torch.Tensor:
-    """out = alpha diag(rs) op(A) diag(ks) op(B) diag(cs) + beta out
+               addend_col_scale: torch.Tensor | None = None,
+               out_row_scale: torch.Tensor | None = None) -> torch.Tensor:
+    """out = diag(os) (alpha diag(rs) op(A) diag(ks) op(B) diag(cs) + beta out
              + diag(es) addend[:, :, :addend_cols]  (on out's first addend_cols columns)
-             + diag(diag_vec or diag_value) placed at out[:, i, diag_col0 + i].
+             + diag(diag_vec or diag_value) placed at out[:, i, diag_col0 + i]).
+
+    ``out_row_scale`` (os, applied last): e.g. the next Horner step's k-scale folded into this
+    step's output rows, so that step's main loop needs none.
 
     ``sym=True``: the result is known to be symmetric (square out): only its lower triangle is
     computed (the output tiles on and below the diagonal) and mirrored, so out comes back
@@ -339,6 +343,7 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
         ks, sks = _vec3(k_scale, batch)
         dv, sdv = _vec3(diag_vec, batch)
         es, ses = _vec3(addend_row_scale, batch)
+        osc, sos = _vec3(out_row_scale, batch)
         er = ecm = ecs = None
         ser = secm = 0
         if gathered:
@@ -357,7 +362,7 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
                   int(diag_col0 is not None), nat.ptr(es), ses, int(sincos), int(sym),
                   nat.ptr(T3), 0 if T3 is None else T3.stride(1),
                   0 if T3 is None else T3.stride(0), nat.ptr(er), ser, nat.ptr(ecm),
-                  nat.ptr(ecs), secm, int(tile_cfg or _TILE_DEFAULT))
+                  nat.ptr(ecs), secm, nat.ptr(osc), sos, int(tile_cfg or _TILE_DEFAULT))
         if _work.on():
             _ledger(trans_a, trans_b, M, N, K, batch, A3, B3, C3, ks=ks, sks=sks,
                     sincos=sincos, cfg=tile_cfg, sym=sym,
@@ -413,6 +418,9 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
             r[:, ii, diag_col0 + ii] += dvv[:, :n]
         else:
             r[:, ii, diag_col0 + ii] += diag_value
+    if out_row_scale is not None:
+        osv = out_row_scale if out_row_scale.dim() == 2 else out_row_scale.unsqueeze(0)
+        r = r * osv.unsqueeze(-1)
     if sym:                                     # the lower triangle, mirrored (device form)
         r = torch.tril(r) + torch.tril(r, -1).transpose(-1, -2)
     C3.copy_(r)

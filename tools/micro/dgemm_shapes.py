@@ -22,6 +22,8 @@ from pfml.ops.gemm import gemm_fused  # noqa: E402
 
 SHAPES = [  # name, batch, M, N, K, trans_a, trans_b, horner fusion
     ("horner", 256, 490, 2006, 490, False, False, True),
+    ("horner_plain", 256, 490, 2006, 490, False, False, False),
+    ("horner_ks", 256, 490, 2006, 490, False, False, "ks"),
     ("inv_W", 384, 256, 234, 256, False, False, False),
     ("inv_S", 384, 234, 234, 256, False, False, False),
     ("inv_X21", 384, 234, 256, 234, False, True, False),
@@ -32,6 +34,11 @@ SHAPES = [  # name, batch, M, N, K, trans_a, trans_b, horner fusion
     ("inv_h128", 384, 128, 128, 128, False, False, False),
     ("db_prod", 256, 490, 490, 490, False, False, False),
     ("gram_tn", 128, 514, 514, 490, True, False, False),
+    # K sweep at equal flops (per-tile prologue / epilogue vs main-loop cost)
+    ("k256", 256, 512, 2048, 256, False, False, False),
+    ("k512", 128, 512, 2048, 512, False, False, False),
+    ("k1024", 64, 512, 2048, 1024, False, False, False),
+    ("k4096", 16, 512, 2048, 4096, False, False, False),
     ("square8192", 1, 8192, 8192, 8192, False, False, False),
     ("square2048", 4, 2048, 2048, 2048, False, False, False),
 ]
@@ -55,6 +62,8 @@ def main():
         mode, fused = (fused if isinstance(fused, str) else ""), fused is True
         if mode == "sym":
             kw.update(sym=True)
+        elif mode == "ks":
+            kw.update(k_scale=torch.rand((b, K), generator=g, dtype=torch.float64, device=dev) + 0.5)
         elif mode == "mirror":
             kw.update(mirror_out=torch.empty((b, N, M), dtype=torch.float64, device=dev))
         if fused:
@@ -69,6 +78,8 @@ def main():
             ref = torch.bmm(opa * kw["k_scale"].unsqueeze(1), opb) * kw["row_scale"].unsqueeze(-1)
             ref[:, :, :N - 2 * M] += kw["addend"]
             ref[:, :, N - 2 * M:N - M] += torch.eye(M, dtype=torch.float64, device=dev)
+        elif mode == "ks":
+            ref = torch.bmm(opa * kw["k_scale"].unsqueeze(1), opb)
         else:
             ref = torch.bmm(opa, opb)
         if mode == "sym":
