@@ -419,7 +419,7 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
     risk_out = torch.zeros_like(d_out) if keep_risk_tc else None
     tc_out = torch.zeros_like(d_out) if keep_risk_tc else None
     signal_t = [[None] * T for _ in range(G)]
-    sing = torch.zeros(max((len(b.months) for b in plan.batches), default=0),
+    sing = torch.zeros(2 * max((len(b.months) for b in plan.batches), default=0),
                        dtype=torch.int32, device=dev)          # singular const flags (batch)
     nsing_t = torch.zeros((), dtype=torch.int64, device=dev)  # running count, on device
     # m_func repair flags of every month (device runs; checked once, by finish_inputs)
@@ -521,8 +521,9 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
         T1 = Tb[cur]
         # T0 / U0 carry LU_PANEL_COLS scratch columns for the two-level solve below
         Wz = Wd + la.LU_PANEL_COLS
-        T0f = torch.empty((B, N, Wz), dtype=torch.float64, device=dev)
-        U0f = torch.empty_like(T0f)
+        # (T_0 and U_0 side by side: their two solves below are ONE batched launch sequence)
+        TU0 = torch.empty((2, B, N, Wz), dtype=torch.float64, device=dev)
+        T0f, U0f = TU0[0], TU0[1]
         T0, U0 = T0f[:, :, :Wd], U0f[:, :, :Wd]
         gemm_fused(mt, T1[:, :, :Wd], T0, row_scale=a, k_scale=ks[:, 0].contiguous(),
                    addend=S[:, 0], addend_cols=GP, diag_col0=GP, diag_value=1.0)
@@ -534,10 +535,11 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
         sig0 = S[:, 0].clone()                                      # signal_t blocks
         del S, stats, ivol
         # omega = const^-1 Omega, solved in place on the augmented [Omega | const] rows (K7)
-        omega = la.solve_augmented(T0f, N, GP, a0=GP, b0=0, status=sing[:B], z0=Wd)  # [B, N, GP]
-        omega_l1 = la.solve_augmented(U0f, N, GP, a0=GP, b0=0, status=sing[:B], z0=Wd)
+        om2 = la.solve_augmented(TU0.view(2 * B, N, Wz), N, GP, a0=GP, b0=0,
+                                 status=sing[:2 * B], z0=Wd)                  # [2B, N, GP]
+        omega, omega_l1 = om2[:B], om2[B:]
         omega_chg = torch.addcmul(omega, Dg[:, 0].unsqueeze(-1), omega_l1, value=-1.0)
-        nsing_t += sing[:B].sum()
+        nsing_t += torch.maximum(sing[:B], sing[B:2 * B]).sum()
         sing.zero_()
         # (25): r_tilde = omega' r, risk = gamma omega' Sigma omega (Sigma in low-rank form:
         # X (F (X' omega)) + ivol o omega), tc = w omega_chg' Lambda omega_chg, denom
