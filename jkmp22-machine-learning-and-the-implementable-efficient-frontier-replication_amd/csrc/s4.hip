@@ -20,6 +20,8 @@
 
 namespace {
 
+typedef double double2_t __attribute__((ext_vector_type(2)));
+
 constexpr int TS = 32;
 
 enum Mode { MF_X = 0, MF_FIX = 1, MF_DB = 2, MF_SHAT = 3 };
@@ -92,6 +94,78 @@ __global__ __launch_bounds__(256) void mfunc_sym_kernel(MfArgs p) {
   }
 }
 
+// The flat passes (X and Y exactly symmetric: no mirror tile) as a row stream: one wave per
+// row, 16-byte loads / stores of column pairs, the row's a_i / mask_i wave-uniform.  Same
+// expressions as mfunc_sym_kernel (bitwise), ~1.4x its rate: the 32 x 32 tile form spends a
+// 256-thread workgroup on 1024 elements with 8-byte accesses.  Needs even ld and 16-byte
+// aligned operands (host checks).
+constexpr int FLAT_ROWS = 16;                      // rows per workgroup (4 per wave)
+
+__device__ __forceinline__ double mf_value(const MfArgs& p, int i, int j, double xs, double ys,
+                                           double s, double c, double ai, double aj, double mi,
+                                           double mj) {
+  double v;
+  if (p.mode == MF_X) {
+    v = s * (ai * aj) * xs;
+  } else if (p.mode == MF_FIX) {
+    const double ic2 = 1.0 / (c * c);
+    const double mm = mi * mj;
+    v = xs * (s * (ai * aj) - ys * ic2) - ys * mm;
+    if (i == j) v += 1.0 + mm + xs * ic2;
+  } else if (p.mode == MF_DB) {
+    const double mu2 = s * s;
+    v = 0.25 * (mu2 * xs + ys / mu2);
+    if (i == j) v += 0.5;
+  } else {
+    v = xs + ys;
+    if (i == j) v += p.d;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(256) void mfunc_flat_kernel(MfArgs p) {
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const double* X = p.X + (int64_t)b * p.sX;
+  const double* Y = p.Y ? p.Y + (int64_t)b * p.sX : nullptr;
+  double* O = p.out + (int64_t)b * p.sX;
+  const double s = p.svec ? p.svec[b] : 0.0;
+  const double c = p.cvec ? p.cvec[b] : 1.0;
+  const double* av = p.a ? p.a + (int64_t)b * p.sv : nullptr;
+  const double* mv = p.mask ? p.mask + (int64_t)b * p.sv : nullptr;
+  const int np = (p.N + 1) >> 1;                   // column pairs (the last may be half)
+  const int r1 = min(p.N, (int)(blockIdx.x + 1) * FLAT_ROWS);
+  for (int i = blockIdx.x * FLAT_ROWS + w; i < r1; i += 4) {
+    const double ai = av ? av[i] : 0.0, mi = mv ? mv[i] : 0.0;
+    const double2_t* xr = reinterpret_cast<const double2_t*>(X + (int64_t)i * p.ld);
+    const double2_t* yr = Y ? reinterpret_cast<const double2_t*>(Y + (int64_t)i * p.ld) : nullptr;
+    double* orow = O + (int64_t)i * p.ld;
+    for (int q = lane; q < np; q += 64) {
+      const int j = 2 * q;
+      const bool two = j + 1 < p.N;
+      double2_t xv, yv = {0.0, 0.0}, aj = {0.0, 0.0}, mj = {0.0, 0.0};
+      if (two) {
+        xv = xr[q];
+        if (yr) yv = yr[q];
+        if (av) aj = reinterpret_cast<const double2_t*>(av)[q];
+        if (mv) mj = reinterpret_cast<const double2_t*>(mv)[q];
+      } else {
+        xv = double2_t{X[(int64_t)i * p.ld + j], 0.0};
+        if (yr) yv.x = Y[(int64_t)i * p.ld + j];
+        if (av) aj.x = av[j];
+        if (mv) mj.x = mv[j];
+      }
+      const double v0 = mf_value(p, i, j, xv.x, yv.x, s, c, ai, aj.x, mi, mj.x);
+      if (two) {
+        const double v1 = mf_value(p, i, j + 1, xv.y, yv.y, s, c, ai, aj.y, mi, mj.y);
+        reinterpret_cast<double2_t*>(orow)[q] = double2_t{v0, v1};
+      } else {
+        orow[j] = v0;
+      }
+    }
+  }
+}
+
 // Per-batch Frobenius norms of two [B, N, N] matrices -> DB scaling mu = (|Minv| / |M|)^(1/4)
 // (1 once the iteration runs unscaled).  Two phases: MU_SPLIT workgroups per matrix reduce
 // row slabs with 16-byte loads into partial sums, the last phase (one wave per matrix) adds
@@ -158,6 +232,15 @@ extern "C" hipError_t pfml_mfunc_sym(const PfmlMfArgs* h, hipStream_t st) {
   if (h->out == h->X || (h->Y && h->out == h->Y)) return hipErrorInvalidValue;   // tiles race
   MfArgs p{h->mode, h->B, h->N, h->ld, h->sX, h->X, h->Y, h->out, h->svec, h->cvec, h->a,
            h->mask, h->sv, h->d, h->flat};
+  const auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  const bool vec = h->ld % 2 == 0 && h->sX % 2 == 0 && (h->sv % 2 == 0 || (!h->a && !h->mask)) &&
+                   al16(h->X) && (!h->Y || al16(h->Y)) && al16(h->out) &&
+                   (!h->a || al16(h->a)) && (!h->mask || al16(h->mask));
+  if (h->flat && vec) {
+    hipLaunchKernelGGL(mfunc_flat_kernel, dim3((h->N + FLAT_ROWS - 1) / FLAT_ROWS, h->B),
+                       dim3(256), 0, st, p);
+    return hipGetLastError();
+  }
   const int tiles = (h->N + TS - 1) / TS;
   hipLaunchKernelGGL(mfunc_sym_kernel, dim3(tiles * tiles, h->B), dim3(256), 0, st, p);
   return hipGetLastError();

@@ -65,6 +65,23 @@ def test_mf_sym_modes(gpu, mode, N):
     assert torch.equal(got, got.transpose(1, 2))                  # exactly symmetric
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("N", [490, 64])
+def test_mf_flat_stream_bitwise(gpu, mode, N):
+    """The flat passes' row-stream kernel (exactly symmetric inputs, csrc/s4.hip
+    mfunc_flat_kernel) give bitwise the tiled symmetrising kernel's result."""
+    from pfml.ops.linalg import mf_sym
+    B = 3
+    X, Y = _rand(B, N, N, seed=11), _rand(B, N, N, seed=12)
+    X, Y = (X + X.transpose(1, 2)).to(gpu), (Y + Y.transpose(1, 2)).to(gpu)
+    kw = dict(svec=_rand(B, seed=3).abs() + 0.5, cvec=_rand(B, seed=4).abs() + 1.0,
+              a=_rand(B, N, seed=5).abs() + 0.1, mask=(torch.rand(B, N) > 0.2).double(), d=1.5)
+    kd = {k: (v.to(gpu) if isinstance(v, torch.Tensor) else v) for k, v in kw.items()}
+    flat = mf_sym(mode, X, Y, torch.empty_like(X), flat=True, **kd)
+    tiled = mf_sym(mode, X, Y, torch.empty_like(X), flat=False, **kd)
+    assert torch.equal(flat, tiled)
+
+
 def test_db_sqrt_device_matches_eigh(gpu):
     """Fixed-count, sync-free Denman-Beavers (device mu scaling) vs an eigh square root."""
     from pfml.ops.linalg import DB_ITERS, DB_SCALED_ITERS, _db_sqrt
