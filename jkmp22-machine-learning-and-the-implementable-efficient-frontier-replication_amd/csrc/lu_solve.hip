@@ -222,6 +222,19 @@ template <int NB, int PMAX>
 hipError_t lu_pivot_launch(const double* M, int n, int64_t ldm, int64_t sM, int a0, int k0,
                            int nb, int* piv, int* status, int batch, hipStream_t st) {
   const int rows = n - k0;
+#ifndef PFML_LU_PIVOT_LDS
+  // 32-wide panels of up to 1024 rows in registers (one row per thread): one barrier per
+  // column and ~8 KB of LDS, so two workgroups share a CU - the LDS form's 135 KB panel
+  // allowed one, and its elimination spent an integer division per element (same pivots,
+  // same arithmetic)
+  if constexpr (NB == 32) {
+    if (rows <= 1024) {
+      hipLaunchKernelGGL((lu_pivot_reg_kernel<NB, 1, 0>), dim3(batch), dim3(1024), 0, st, M, n,
+                         ldm, sM, a0, k0, nb, piv, status);
+      return hipSuccess;
+    }
+  }
+#endif
   if (rows <= PMAX) {
     hipLaunchKernelGGL((lu_pivot_kernel<NB, PMAX>), dim3(batch), dim3(1024), 0, st, M, n, ldm,
                        sM, a0, k0, nb, piv, status);
