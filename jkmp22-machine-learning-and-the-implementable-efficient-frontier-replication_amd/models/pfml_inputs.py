@@ -37,6 +37,7 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import contextlib
 import os
 
 import numpy as np
@@ -161,6 +162,26 @@ def auto_month_batch(n_stocks: int, gp: int, device, cap: int = 1024) -> int:
         except Exception:                                   # pragma: no cover
             budget = 4e9
     return int(max(1, min(cap, budget // per)))
+
+
+# S4 month batches run on this many streams (PFML_S4_STREAMS; make_s4_plan then splits the
+# months into at least that many batches): one batch's latency-bound kernels (SPD inverse
+# nodes, LU pivot panels, leaves, the elementwise passes) overlap another's MFMA GEMMs.
+# S4+S5+S6 on one MI355X (A/B on one box): 1 stream 357.6, 2: 345.5, 3: 341.4, 4: 340.8 ms
+# (profiles/r05_s4_streams_ab.json; 4 hardware queues per process).  1: one stream.
+S4_STREAMS = int(os.environ.get("PFML_S4_STREAMS", "3"))
+_STREAMS: dict = {}
+
+
+def _s4_streams(dev, n_batches: int):
+    """The side streams of a multi-batch device run (created once per device), or None."""
+    if dev.type != "cuda" or S4_STREAMS <= 1 or n_batches <= 1:
+        return None
+    key = (str(dev), S4_STREAMS)
+    if key not in _STREAMS:
+        _STREAMS[key] = [torch.cuda.Stream(device=dev) for _ in range(S4_STREAMS)]
+        la.CONCURRENT_STREAMS.update(st_.cuda_stream for st_ in _STREAMS[key])
+    return _STREAMS[key]
 
 
 def _even(n: int) -> int:
@@ -293,6 +314,8 @@ def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
     bsz = batch or cfg.run.month_batch
     if not bsz or bsz <= 0:
         bsz = auto_month_batch(Npad, Gc * Pp, dev)
+        if torch.device(dev).type == "cuda" and S4_STREAMS > 1 and T > 1:
+            bsz = min(bsz, -(-T // S4_STREAMS))              # one batch per stream at least
         log.info(f"PFML inputs: {bsz} months per batch (N <= {nmax})")
     batches, sig_rows, sig_ids = [], [], []
     for b0 in range(0, T, bsz):
@@ -419,9 +442,11 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
     risk_out = torch.zeros_like(d_out) if keep_risk_tc else None
     tc_out = torch.zeros_like(d_out) if keep_risk_tc else None
     signal_t = [[None] * T for _ in range(G)]
-    sing = torch.zeros(2 * max((len(b.months) for b in plan.batches), default=0),
-                       dtype=torch.int32, device=dev)          # singular const flags (batch)
-    nsing_t = torch.zeros((), dtype=torch.int64, device=dev)  # running count, on device
+    # singular const flags (batch) and the running count (on device), one of each per stream
+    nst = max(1, len(_s4_streams(dev, len(plan.batches)) or []))
+    sing_all = torch.zeros((nst, 2 * max((len(b.months) for b in plan.batches), default=0)),
+                           dtype=torch.int32, device=dev)
+    nsing_all = torch.zeros(nst, dtype=torch.int64, device=dev)
     # m_func repair flags of every month (device runs; checked once, by finish_inputs)
     mstat = (torch.zeros(T, dtype=torch.int32, device=dev)
              if dev.type == "cuda" and not inline_repair else None)
@@ -441,154 +466,166 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
                   # only for exactly this universe
                   "ids": [np.asarray(plan.sig_ids[mpos[int(m)]], np.int64) for m in km]}
     b0 = 0
-    for bt in plan.batches:
+    streams = _s4_streams(dev, len(plan.batches))
+    if streams:                     # side streams fork from (and below join) the caller's
+        for st_ in streams:
+            st_.wait_stream(torch.cuda.current_stream(dev))
+    for kb, bt in enumerate(plan.batches):
         B = len(bt.months)
-        range_push("pfml_inputs.batch")
-        # signals of every distinct g, written into one [B, 13, N, Gc*Pp] stack
-        # signals (K11/K12): lags 0, 11 and 12 materialised (signal_t, T_11's S block, U_0's
-        # GEMM operand) into [B, 3, N, Gc*Pp]; lags 1..10 only as per-column means and scales -
-        # the Horner steps form (F[row] - mean) * scale / vol in their epilogue (gathered
-        # addend), so 10 of the 13 [N, Gc*Pp] signal blocks per month are never stored
-        S = torch.empty((B, 3, N, GP), dtype=torch.float64, device=dev)
-        idx3 = torch.cat([bt.idx[:, :1], bt.idx[:, lb:lb + 2]], 1)     # (no host index list)
-        for g in range(Gc):
-            standardize_signals(rffs[g], idx3, bt.mask, vol, P=P,
-                                out=S[..., g * Pp:(g + 1) * Pp], n_real=bt.n_real)
-        stats = torch.empty((B, lb - 1, 2, GP), dtype=torch.float64, device=dev)
-        for g in range(Gc):
-            signal_stats(rffs[g], bt.idx[:, 1:lb], bt.mask, P,
-                         out=stats[..., g * Pp:(g + 1) * Pp], n_real=bt.n_real)
-        # 1 / vol of each lag's rows (0 on padding rows: their standardised signal is 0)
-        ivol = torch.where(bt.mask.unsqueeze(1) > 0, 1.0 / vol[bt.idx[:, 1:lb]],
-                           torch.zeros((), dtype=torch.float64, device=dev))
-        # Barra Sigma = X F X' + diag(ivol) (K1; pad rows: X = 0, ivol = 1 -> identity block)
-        Xl = plan.bX[bt.brow]                                       # [B, N, K]
-        Fb = plan.bF[bt.fpos]                                       # [B, K, K]
-        iv = plan.biv[bt.brow]                                      # [B, N]
-        XF = gemm(Xl, Fb, backend="own")                             # in-house fp64 MFMA GEMM
-        Sigma = torch.empty((B, N, N), dtype=torch.float64, device=dev)
-        if prec == "fp64":
-            # symmetric mode: the lower triangle mirrored, an exactly symmetric Sigma
-            gemm_fused(XF, Xl, Sigma, trans_b=True, diag_col0=0, diag_vec=iv, sym=True)
-        else:
-            gemm_prec(XF, Xl, prec, trans_b=True, out=Sigma)
-            Sigma.diagonal(dim1=1, dim2=2).add_(iv)
-        # m = diag(a) m_tilde diag(1/a) (Lemma 1); a and 1/a are folded into the Horner GEMMs
-        mt, a = la.m_tilde(Sigma, bt.lam, bt.w, bt.rf, mu, gamma, cfg.run.iterations,
-                           mask=bt.mask, status=None if mstat is None else mstat[b0:b0 + B],
-                           sigma_exact_sym=prec == "fp64")
-        if m_keep is not None:
-            sel = [(bi, kpos[int(d)]) for bi, d in enumerate(bt.months) if int(d) in kpos]
-            if sel:
-                src = torch.as_tensor([x[0] for x in sel], device=dev)
-                dst = torch.as_tensor([x[1] for x in sel], device=dev)
-                m_keep["mt"][dst] = mt[src]
-                m_keep["a"][dst] = a[src]
-                for bi, k in sel:
-                    m_keep["n"][k] = int(bt.ns[bi])
-        # (24) Horner chain over [S_theta | I | R], one fused GEMM launch per step:
-        #   T_theta = [S_theta | I] + diag(a) m_tilde diag(D_theta / a) T_{theta+1}
-        # The lag-1 chain of omega_l1 (PFML_Input_Data.py:425-450: gtm_agg_l1, same m_t) is
-        #   U_0 = sum_{j=1..12} (prod_{tau=1..j-1} m D_tau) [S_j | I] = T_1 + Q [S_12 | I],
-        #   Q = m D_1 m D_2 ... m D_11,
-        # and Q rides along the T steps theta = 10..1 as an N-column block R (R_11 = m D_11,
-        # R_theta = m D_theta R_{theta+1}, no addend): 10 steps of width GP + 2N plus two of
-        # GP + N instead of 22 of GP + N (29 % fewer Horner flops at N = 490, GP = 1026).
-        Dg = plan.gt[bt.idx]                                        # [B, 13, N]
-        ainv = 1.0 / a
-        # k-scales D_theta / a of every step; step theta's GEMM takes T_{theta+1} with its rows
-        # already scaled by ks[theta] (written so by step theta + 1's epilogue, out_row_scale),
-        # so the ten width-(GP + 2N) main loops carry no k-scale (T_1 stays unscaled: T_0 and
-        # U_0 use it)
-        ks = Dg * ainv.unsqueeze(1)                                 # [B, 13, N]
-        Wr = Wd + N
-        Tb = [torch.empty((B, N, Wr), dtype=torch.float64, device=dev) for _ in range(2)]
-        k10 = ks[:, lb - 1].unsqueeze(-1)
-        torch.mul(S[:, 1], k10, out=Tb[0][:, :, :GP])
-        Tb[0][:, :, GP:Wd] = torch.diag_embed(ks[:, lb - 1])
-        # R_11 = diag(a) m_tilde diag(D_11 / a): elementwise, in the rounding order the fused
-        # GEMM against the identity produced ((m_tilde * k-scale) * row scale), then ks_10
-        torch.mul(mt * ks[:, lb].unsqueeze(-2), a.unsqueeze(-1), out=Tb[0][:, :, Wd:])
-        Tb[0][:, :, Wd:].mul_(k10)
-        cur = 0
-        for th in range(lb - 1, 0, -1):
-            gemm_fused(mt, Tb[cur], Tb[cur ^ 1], row_scale=a,
-                       addend=Fcat, addend_cols=GP, addend_rows=bt.idx[:, th],
-                       addend_col_shift=stats[:, th - 1, 0], addend_col_scale=stats[:, th - 1, 1],
-                       addend_row_scale=ivol[:, th - 1], diag_col0=GP, diag_value=1.0,
-                       out_row_scale=ks[:, th - 1] if th > 1 else None)
-            cur ^= 1
-        T1 = Tb[cur]
-        # T0 / U0 carry LU_PANEL_COLS scratch columns for the two-level solve below
-        Wz = Wd + la.LU_PANEL_COLS
-        # (T_0 and U_0 side by side: their two solves below are ONE batched launch sequence)
-        TU0 = torch.empty((2, B, N, Wz), dtype=torch.float64, device=dev)
-        T0f, U0f = TU0[0], TU0[1]
-        T0, U0 = T0f[:, :, :Wd], U0f[:, :, :Wd]
-        gemm_fused(mt, T1[:, :, :Wd], T0, row_scale=a, k_scale=ks[:, 0].contiguous(),
-                   addend=S[:, 0], addend_cols=GP, diag_col0=GP, diag_value=1.0)
-        # U_0 = T_1 + Q [S_12 | I]: the S_12 block on the GEMM, the identity block as Q + T_1
-        gemm_fused(T1[:, :, Wd:], S[:, 2], U0[:, :, :GP], addend=T1[:, :, :GP],
-                   addend_cols=GP)
-        torch.add(T1[:, :, Wd:], T1[:, :, GP:Wd], out=U0[:, :, GP:])
-        del Tb, T1
-        sig0 = S[:, 0].clone()                                      # signal_t blocks
-        del S, stats, ivol
-        # omega = const^-1 Omega, solved in place on the augmented [Omega | const] rows (K7)
-        om2 = la.solve_augmented(TU0.view(2 * B, N, Wz), N, GP, a0=GP, b0=0,
-                                 status=sing[:2 * B], z0=Wd)                  # [2B, N, GP]
-        omega, omega_l1 = om2[:B], om2[B:]
-        omega_chg = torch.addcmul(omega, Dg[:, 0].unsqueeze(-1), omega_l1, value=-1.0)
-        nsing_t += torch.maximum(sing[:B], sing[B:2 * B]).sum()
-        sing.zero_()
-        # (25): r_tilde = omega' r, risk = gamma omega' Sigma omega (Sigma in low-rank form:
-        # X (F (X' omega)) + ivol o omega), tc = w omega_chg' Lambda omega_chg, denom
-        omega = omega.contiguous()
-        omega_chg = omega_chg.contiguous()
-        rt_ = gemm(omega, bt.r.unsqueeze(-1).contiguous(), trans_a=True,
-                   backend="own").squeeze(-1)                                # [B, GP]
-        XtO = torch.empty((B, Xl.shape[2], GP), dtype=torch.float64, device=dev)
-        gemm_fused(Xl, omega, XtO, trans_a=True)
-        FXO = gemm(Fb, XtO, backend="own")
-        SO = torch.empty_like(omega)
-        gemm_fused(Xl, FXO, SO, addend=omega, addend_row_scale=iv)
-        lw = (bt.lam * bt.w.view(B, 1)).contiguous()
-        Dt = torch.empty((B, Pp, Pp), dtype=torch.float64, device=dev)
-        Dk = torch.empty_like(Dt) if keep_risk_tc else None
-        for g in range(G):
-            sl = slice(b0, b0 + B)
-            if g >= Gc:                                  # shared block (quirk Q1)
-                d_out[g, sl] = d_out[0, sl]
-                r_out[g, sl] = r_out[0, sl]
-                if keep_risk_tc:
-                    risk_out[g, sl] = risk_out[0, sl]
-                    tc_out[g, sl] = tc_out[0, sl]
-                for bi in range(B):
-                    signal_t[g][b0 + bi] = signal_t[0][b0 + bi]
-                continue
-            cs = slice(g * Pp, (g + 1) * Pp)
-            og, cg, sg = omega[:, :, cs], omega_chg[:, :, cs], SO[:, :, cs]
-            # risk = gamma omega' (Sigma omega) and tc = w omega_chg' Lambda omega_chg are
-            # symmetric: the GEMM's symmetric mode computes the lower tiles and mirrors them
+        sing = sing_all[kb % len(sing_all)]
+        nsing_t = nsing_all[kb % len(nsing_all)]
+        ctx = torch.cuda.stream(streams[kb % len(streams)]) if streams else contextlib.nullcontext()
+        with ctx:
+            range_push("pfml_inputs.batch")
+            # signals of every distinct g, written into one [B, 13, N, Gc*Pp] stack
+            # signals (K11/K12): lags 0, 11 and 12 materialised (signal_t, T_11's S block, U_0's
+            # GEMM operand) into [B, 3, N, Gc*Pp]; lags 1..10 only as per-column means and scales -
+            # the Horner steps form (F[row] - mean) * scale / vol in their epilogue (gathered
+            # addend), so 10 of the 13 [N, Gc*Pp] signal blocks per month are never stored
+            S = torch.empty((B, 3, N, GP), dtype=torch.float64, device=dev)
+            idx3 = torch.cat([bt.idx[:, :1], bt.idx[:, lb:lb + 2]], 1)     # (no host index list)
+            for g in range(Gc):
+                standardize_signals(rffs[g], idx3, bt.mask, vol, P=P,
+                                    out=S[..., g * Pp:(g + 1) * Pp], n_real=bt.n_real)
+            stats = torch.empty((B, lb - 1, 2, GP), dtype=torch.float64, device=dev)
+            for g in range(Gc):
+                signal_stats(rffs[g], bt.idx[:, 1:lb], bt.mask, P,
+                             out=stats[..., g * Pp:(g + 1) * Pp], n_real=bt.n_real)
+            # 1 / vol of each lag's rows (0 on padding rows: their standardised signal is 0)
+            ivol = torch.where(bt.mask.unsqueeze(1) > 0, 1.0 / vol[bt.idx[:, 1:lb]],
+                               torch.zeros((), dtype=torch.float64, device=dev))
+            # Barra Sigma = X F X' + diag(ivol) (K1; pad rows: X = 0, ivol = 1 -> identity block)
+            Xl = plan.bX[bt.brow]                                       # [B, N, K]
+            Fb = plan.bF[bt.fpos]                                       # [B, K, K]
+            iv = plan.biv[bt.brow]                                      # [B, N]
+            XF = gemm(Xl, Fb, backend="own")                             # in-house fp64 MFMA GEMM
+            Sigma = torch.empty((B, N, N), dtype=torch.float64, device=dev)
             if prec == "fp64":
-                gemm_fused(og, sg, Dt, trans_a=True, alpha=gamma, sym=True)
+                # symmetric mode: the lower triangle mirrored, an exactly symmetric Sigma
+                gemm_fused(XF, Xl, Sigma, trans_b=True, diag_col0=0, diag_vec=iv, sym=True)
             else:
-                gemm_prec(og.contiguous(), sg.contiguous(), prec, trans_a=True, alpha=gamma,
-                          out=Dt)
-            if keep_risk_tc:
-                risk_out[g, sl] = Dt[:, :P, :P]
-                gemm_fused(cg, cg, Dk, trans_a=True, k_scale=lw, sym=True)
-                tc_out[g, sl] = Dk[:, :P, :P]
-                Dt.add_(Dk)
-            else:
-                gemm_fused(cg, cg, Dt, trans_a=True, k_scale=lw, beta=1.0, sym=True)
-            d_out[g, sl] = Dt[:, :P, :P]
-            r_out[g, sl] = rt_[:, g * Pp:g * Pp + P]
-            for bi in range(B):
-                signal_t[g][b0 + bi] = sig0[bi, : int(bt.ns[bi]), g * Pp:g * Pp + P]
-        range_pop()
+                gemm_prec(XF, Xl, prec, trans_b=True, out=Sigma)
+                Sigma.diagonal(dim1=1, dim2=2).add_(iv)
+            # m = diag(a) m_tilde diag(1/a) (Lemma 1); a and 1/a are folded into the Horner GEMMs
+            mt, a = la.m_tilde(Sigma, bt.lam, bt.w, bt.rf, mu, gamma, cfg.run.iterations,
+                               mask=bt.mask, status=None if mstat is None else mstat[b0:b0 + B],
+                               sigma_exact_sym=prec == "fp64")
+            if m_keep is not None:
+                sel = [(bi, kpos[int(d)]) for bi, d in enumerate(bt.months) if int(d) in kpos]
+                if sel:
+                    src = torch.as_tensor([x[0] for x in sel], device=dev)
+                    dst = torch.as_tensor([x[1] for x in sel], device=dev)
+                    m_keep["mt"][dst] = mt[src]
+                    m_keep["a"][dst] = a[src]
+                    for bi, k in sel:
+                        m_keep["n"][k] = int(bt.ns[bi])
+            # (24) Horner chain over [S_theta | I | R], one fused GEMM launch per step:
+            #   T_theta = [S_theta | I] + diag(a) m_tilde diag(D_theta / a) T_{theta+1}
+            # The lag-1 chain of omega_l1 (PFML_Input_Data.py:425-450: gtm_agg_l1, same m_t) is
+            #   U_0 = sum_{j=1..12} (prod_{tau=1..j-1} m D_tau) [S_j | I] = T_1 + Q [S_12 | I],
+            #   Q = m D_1 m D_2 ... m D_11,
+            # and Q rides along the T steps theta = 10..1 as an N-column block R (R_11 = m D_11,
+            # R_theta = m D_theta R_{theta+1}, no addend): 10 steps of width GP + 2N plus two of
+            # GP + N instead of 22 of GP + N (29 % fewer Horner flops at N = 490, GP = 1026).
+            Dg = plan.gt[bt.idx]                                        # [B, 13, N]
+            ainv = 1.0 / a
+            # k-scales D_theta / a of every step; step theta's GEMM takes T_{theta+1} with its rows
+            # already scaled by ks[theta] (written so by step theta + 1's epilogue, out_row_scale),
+            # so the ten width-(GP + 2N) main loops carry no k-scale (T_1 stays unscaled: T_0 and
+            # U_0 use it)
+            ks = Dg * ainv.unsqueeze(1)                                 # [B, 13, N]
+            Wr = Wd + N
+            Tb = [torch.empty((B, N, Wr), dtype=torch.float64, device=dev) for _ in range(2)]
+            k10 = ks[:, lb - 1].unsqueeze(-1)
+            torch.mul(S[:, 1], k10, out=Tb[0][:, :, :GP])
+            Tb[0][:, :, GP:Wd] = torch.diag_embed(ks[:, lb - 1])
+            # R_11 = diag(a) m_tilde diag(D_11 / a): elementwise, in the rounding order the fused
+            # GEMM against the identity produced ((m_tilde * k-scale) * row scale), then ks_10
+            torch.mul(mt * ks[:, lb].unsqueeze(-2), a.unsqueeze(-1), out=Tb[0][:, :, Wd:])
+            Tb[0][:, :, Wd:].mul_(k10)
+            cur = 0
+            for th in range(lb - 1, 0, -1):
+                gemm_fused(mt, Tb[cur], Tb[cur ^ 1], row_scale=a,
+                           addend=Fcat, addend_cols=GP, addend_rows=bt.idx[:, th],
+                           addend_col_shift=stats[:, th - 1, 0], addend_col_scale=stats[:, th - 1, 1],
+                           addend_row_scale=ivol[:, th - 1], diag_col0=GP, diag_value=1.0,
+                           out_row_scale=ks[:, th - 1] if th > 1 else None)
+                cur ^= 1
+            T1 = Tb[cur]
+            # T0 / U0 carry LU_PANEL_COLS scratch columns for the two-level solve below
+            Wz = Wd + la.LU_PANEL_COLS
+            # (T_0 and U_0 side by side: their two solves below are ONE batched launch sequence)
+            TU0 = torch.empty((2, B, N, Wz), dtype=torch.float64, device=dev)
+            T0f, U0f = TU0[0], TU0[1]
+            T0, U0 = T0f[:, :, :Wd], U0f[:, :, :Wd]
+            gemm_fused(mt, T1[:, :, :Wd], T0, row_scale=a, k_scale=ks[:, 0].contiguous(),
+                       addend=S[:, 0], addend_cols=GP, diag_col0=GP, diag_value=1.0)
+            # U_0 = T_1 + Q [S_12 | I]: the S_12 block on the GEMM, the identity block as Q + T_1
+            gemm_fused(T1[:, :, Wd:], S[:, 2], U0[:, :, :GP], addend=T1[:, :, :GP],
+                       addend_cols=GP)
+            torch.add(T1[:, :, Wd:], T1[:, :, GP:Wd], out=U0[:, :, GP:])
+            del Tb, T1
+            sig0 = S[:, 0].clone()                                      # signal_t blocks
+            del S, stats, ivol
+            # omega = const^-1 Omega, solved in place on the augmented [Omega | const] rows (K7)
+            om2 = la.solve_augmented(TU0.view(2 * B, N, Wz), N, GP, a0=GP, b0=0,
+                                     status=sing[:2 * B], z0=Wd)                  # [2B, N, GP]
+            omega, omega_l1 = om2[:B], om2[B:]
+            omega_chg = torch.addcmul(omega, Dg[:, 0].unsqueeze(-1), omega_l1, value=-1.0)
+            nsing_t += torch.maximum(sing[:B], sing[B:2 * B]).sum()
+            sing.zero_()
+            # (25): r_tilde = omega' r, risk = gamma omega' Sigma omega (Sigma in low-rank form:
+            # X (F (X' omega)) + ivol o omega), tc = w omega_chg' Lambda omega_chg, denom
+            omega = omega.contiguous()
+            omega_chg = omega_chg.contiguous()
+            rt_ = gemm(omega, bt.r.unsqueeze(-1).contiguous(), trans_a=True,
+                       backend="own").squeeze(-1)                                # [B, GP]
+            XtO = torch.empty((B, Xl.shape[2], GP), dtype=torch.float64, device=dev)
+            gemm_fused(Xl, omega, XtO, trans_a=True)
+            FXO = gemm(Fb, XtO, backend="own")
+            SO = torch.empty_like(omega)
+            gemm_fused(Xl, FXO, SO, addend=omega, addend_row_scale=iv)
+            lw = (bt.lam * bt.w.view(B, 1)).contiguous()
+            Dt = torch.empty((B, Pp, Pp), dtype=torch.float64, device=dev)
+            Dk = torch.empty_like(Dt) if keep_risk_tc else None
+            for g in range(G):
+                sl = slice(b0, b0 + B)
+                if g >= Gc:                                  # shared block (quirk Q1)
+                    d_out[g, sl] = d_out[0, sl]
+                    r_out[g, sl] = r_out[0, sl]
+                    if keep_risk_tc:
+                        risk_out[g, sl] = risk_out[0, sl]
+                        tc_out[g, sl] = tc_out[0, sl]
+                    for bi in range(B):
+                        signal_t[g][b0 + bi] = signal_t[0][b0 + bi]
+                    continue
+                cs = slice(g * Pp, (g + 1) * Pp)
+                og, cg, sg = omega[:, :, cs], omega_chg[:, :, cs], SO[:, :, cs]
+                # risk = gamma omega' (Sigma omega) and tc = w omega_chg' Lambda omega_chg are
+                # symmetric: the GEMM's symmetric mode computes the lower tiles and mirrors them
+                if prec == "fp64":
+                    gemm_fused(og, sg, Dt, trans_a=True, alpha=gamma, sym=True)
+                else:
+                    gemm_prec(og.contiguous(), sg.contiguous(), prec, trans_a=True, alpha=gamma,
+                              out=Dt)
+                if keep_risk_tc:
+                    risk_out[g, sl] = Dt[:, :P, :P]
+                    gemm_fused(cg, cg, Dk, trans_a=True, k_scale=lw, sym=True)
+                    tc_out[g, sl] = Dk[:, :P, :P]
+                    Dt.add_(Dk)
+                else:
+                    gemm_fused(cg, cg, Dt, trans_a=True, k_scale=lw, beta=1.0, sym=True)
+                d_out[g, sl] = Dt[:, :P, :P]
+                r_out[g, sl] = rt_[:, g * Pp:g * Pp + P]
+                for bi in range(B):
+                    signal_t[g][b0 + bi] = sig0[bi, : int(bt.ns[bi]), g * Pp:g * Pp + P]
+            range_pop()
         b0 += B
         log.info(f"PFML inputs: months {b0}/{T}")
+    if streams:
+        for st_ in streams:
+            torch.cuda.current_stream(dev).wait_stream(st_)
+    nsing_t = nsing_all.sum()
     reals = PfmlReals(months=plan.months, r_tilde=r_out, denom=d_out, risk=risk_out, tc=tc_out)
     out = PfmlInputs(reals=reals, months=plan.months, signal_rows=plan.sig_rows,
                      signal_t=signal_t, rff_w=plan.W, ids=plan.sig_ids, m_keep=m_keep,

@@ -90,6 +90,15 @@ nat.register_hip("pfml_spd_node_sym", [C.c_void_p, C.c_int64, C.c_int64, C.c_int
 
 _REC_LEAF = 64
 _REC_BUFS: dict = {}
+# streams that run recursive inverses concurrently with others (the multi-stream S4 batches,
+# models/pfml_inputs.py): their scratch buffers are their own; every other stream shares one
+# set (so a graph capture reuses the eager run's buffers)
+CONCURRENT_STREAMS: set = set()
+
+
+def _buf_tag(X: torch.Tensor) -> int:
+    h = nat.stream_of(X)
+    return h if h in CONCURRENT_STREAMS else 0
 
 
 def _rec_split(n: int) -> int:
@@ -118,7 +127,7 @@ def _spd_inverse_recursive(X: torch.Tensor, status: torch.Tensor,
     ld, sX = X.stride(1), X.stride(0)
 
     def buf(depth, h, m):
-        key = (X.device, B, depth)
+        key = (X.device, B, depth, _buf_tag(X))
         w = _REC_BUFS.get(key)
         if w is None or w.numel() < B * h * m:
             w = torch.empty(B * h * m, dtype=torch.float64, device=X.device)
@@ -187,7 +196,7 @@ def spd_inverse_sym(X: torch.Tensor, status: torch.Tensor) -> torch.Tensor:
     cfg = SYM_GEMM_CFG
 
     def buf(depth, h, m):
-        key = (X.device, B, depth, "sym")
+        key = (X.device, B, depth, "sym", _buf_tag(X))
         w = _REC_BUFS.get(key)
         if w is None or w.numel() < B * h * m:
             w = torch.empty(B * h * m, dtype=torch.float64, device=X.device)

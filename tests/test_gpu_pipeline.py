@@ -191,6 +191,47 @@ def test_pfml_inputs_gpu_matches_cpu(gpu, small_data):
                                   atol=1e-13)
 
 
+def test_s4_two_streams_bitwise(gpu, small_data, monkeypatch):
+    """S4 month batches on two streams (PFML_S4_STREAMS=2: each batch's latency-bound kernels
+    overlap the other's GEMMs) give bitwise the one-stream summands, eager and as a replayed
+    HIP graph (the side streams fork from and join the capture stream)."""
+    import sys
+    from pfml.config import get_features
+    from pfml.data import io
+    from pfml.models import pfml_inputs as PI
+    from pfml.models.risk import BarraCov
+    from pfml.utils.dates import pfml_date_grids
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    cfg = small_data
+    d = cfg.run.data_dir
+    chars = io.read_processed_chars(d, get_features())
+    barra = BarraCov.load(os.path.join(d, "Barra_Cov.npz"))
+    wealth = pd.read_csv(os.path.join(d, "wealth_processed.csv"), parse_dates=["eom"])
+    rf = io.read_risk_free(d)
+    g = pfml_date_grids(int(barra.months.min()), 11, cfg.settings["split"]["test_end"], 1971, 10)
+    plan = PI.make_s4_plan(cfg, chars, barra, wealth, rf, gpu, months=g["m2"][:30], batch=12)
+    assert len(plan.batches) == 3
+    one = PI.finish_inputs(plan, cfg, PI.run_plan(plan, cfg, defer_checks=True))
+    monkeypatch.setattr(PI, "S4_STREAMS", 2)
+    two = PI.finish_inputs(plan, cfg, PI.run_plan(plan, cfg, defer_checks=True))
+    assert torch.equal(two.reals.denom, one.reals.denom)
+    assert torch.equal(two.reals.r_tilde, one.reals.r_tilde)
+    box = {}
+
+    def step():
+        box["out"] = PI.run_plan(plan, cfg, defer_checks=True)
+
+    rep = bench.graphed(step, gpu)
+    assert rep is not None
+    box["out"].reals.denom.zero_()
+    rep()
+    torch.cuda.synchronize()
+    out = PI.finish_inputs(plan, cfg, box["out"])
+    assert torch.equal(out.reals.denom, one.reals.denom)
+
+
 def test_s4_hip_graph_replay_matches_eager(gpu, small_data):
     """S4 (run_plan with its checks deferred: no host sync) captured as ONE HIP graph replays
     to bitwise the eager run's r_tilde / denom (PFML_Input_Data.py:318-491), and the deferred

@@ -6,7 +6,7 @@ This is the compute part of `bench.py --gpus W` (the driver runs the real multi-
 it shows whether the per-rank work shrinks as 1/W or hits a latency floor.  PFML_SHARD_GRAPH=1
 replays each rank's step as a captured HIP graph.  ``--with-inputs``: each rank's S4 (its own
 PFML months) and its S4 + S5 + S6 step instead (the whole-node projection of the full
-grid-search wall-clock).
+grid-search wall-clock), both replayed as HIP graphs (PFML_SHARD_GRAPH=0: eager launches).
 
     python tools/bench_shard.py [1,2,4,8] [steps]
     python tools/bench_shard.py --with-inputs [1,2,4,8] [steps]"""
@@ -39,6 +39,8 @@ def with_inputs(worlds, steps: int) -> dict:
                         int(cfg.settings["pf"]["dates"]["start_year"]),
                         int(cfg.settings["pf"]["dates"]["split_years"]))
     months = g["m2"]
+    graph = os.environ.get("PFML_SHARD_GRAPH", "1") != "0"
+    hip_graph = graph
     out = {"months_total": int(len(months))}
     for W in worlds:
         s4, grid, nm = [], [], []
@@ -48,20 +50,34 @@ def with_inputs(worlds, steps: int) -> dict:
             rows = local_month_rows(months, cfg.hp_years, W, r)
             plan = make_s4_plan(cfg, chars, barra, wealth, rf, dev, months[rows])
             eng = (plan, months)
-            run_plan(plan, cfg)                                   # warm-up
+            # both timed forms replay as captured HIP graphs (S4's checks deferred: no host
+            # sync inside), as bench.py --with-inputs does; eager launches if capture fails
+            f_s4 = lambda: run_plan(plan, cfg, defer_checks=True)          # noqa: E731
+            rep = bench.graphed(f_s4, dev) if graph else None
+            hip_graph &= rep is not None
+            rep = rep or f_s4
+            rep()                                                 # warm-up
             torch.cuda.synchronize()
             t = time.perf_counter()
             for _ in range(steps):
-                run_plan(plan, cfg)
+                rep()
             torch.cuda.synchronize()
             t_s4 = 1e3 * (time.perf_counter() - t) / steps
-            bench.one_step(None, cfg, eng)                        # warm-up (plans, caches)
+            del rep
+            torch.cuda.empty_cache()
+            f_all = lambda: bench.one_step(None, cfg, eng)                 # noqa: E731
+            rep = bench.graphed(f_all, dev) if graph else None
+            hip_graph &= rep is not None
+            rep = rep or f_all
+            rep()                                                 # warm-up (plans, caches)
             torch.cuda.synchronize()
             t = time.perf_counter()
             for _ in range(steps):
-                bench.one_step(None, cfg, eng)
+                rep()
             torch.cuda.synchronize()
             t_all = 1e3 * (time.perf_counter() - t) / steps
+            del rep
+            bench.LAST_S4.clear()
             s4.append(round(t_s4, 1))
             grid.append(round(t_all - t_s4, 1))
             nm.append(int(len(rows)))
@@ -79,6 +95,7 @@ def with_inputs(worlds, steps: int) -> dict:
         for W in worlds:
             out[f"w{W}_s4_max_vs_ideal"] = round(out[f"w{W}_s4_max_ms"] * W / out["w1_s4_max_ms"], 3)
     pdist.set_env(None)
+    out["hip_graph"] = bool(hip_graph)
     return out
 
 
