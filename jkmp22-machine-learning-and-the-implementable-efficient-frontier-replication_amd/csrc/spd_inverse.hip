@@ -390,6 +390,15 @@ __global__ __launch_bounds__(256) void spd_leafinv_kernel(const double* __restri
 // X11 stays in the GJ registers between its inverse and the final update.
 constexpr int NLP = 66;                        // operand image row stride (doubles)
 
+// phase timestamps of workgroup 0 (a build with -DPFML_NODE_TIMING; pfml_node_timing reads
+// them): where one node's latency goes, for the small-batch (per-rank) S4
+#ifdef PFML_NODE_TIMING
+__device__ unsigned long long g_node_ts[16];
+#define NODE_TS(k) do { if (blockIdx.x == 0 && threadIdx.x == 0) g_node_ts[k] = clock64(); } while (0)
+#else
+#define NODE_TS(k) do { } while (0)
+#endif
+
 struct NodeLds {
   double u[64][NLP];                           // X11 -> W
   double v[64][NLP];                           // A21 -> S -> X22 -> X12 -> X12 W'
@@ -422,6 +431,7 @@ __global__ __launch_bounds__(256, 2) void spd_node_sym_kernel(double* __restrict
                                                              int64_t ld, int64_t sX, int r0,
                                                              int nn, int* __restrict__ status) {
   __shared__ NodeLds L;
+  NODE_TS(0);
   const int b = blockIdx.x, t = threadIdx.x;
   const int lane = t & 63, li = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -438,7 +448,9 @@ __global__ __launch_bounds__(256, 2) void spd_node_sym_kernel(double* __restrict
   }
   // X11 = A11^-1 (registers), its mirrored image -> u
   double x11[4][4];
+  NODE_TS(1);
   bool bad = gj64(Xb, ld, 64, x11, L.gj);
+  NODE_TS(2);
 #pragma unroll
   for (int uu = 0; uu < 4; ++uu)
 #pragma unroll
@@ -467,6 +479,7 @@ __global__ __launch_bounds__(256, 2) void spd_node_sym_kernel(double* __restrict
         L.u[i][j] = j < m ? acc[q][r] : 0.0;  // W (columns >= m: zero)
       }
   __syncthreads();
+  NODE_TS(3);
   // S = A22 - A21 W: lower tiles (I >= J) of the tn x tn grid, round-robin over the waves
   {
     int ti[3], tj[3], nt = 0;
@@ -506,9 +519,11 @@ __global__ __launch_bounds__(256, 2) void spd_node_sym_kernel(double* __restrict
         }
   }
   __syncthreads();
+  NODE_TS(4);
   // X22 = S^-1 -> global (lower, mirrored) and v (its mirrored image, zero outside m x m)
   double x22[4][4];
   bad |= gj64(&L.v[0][0], NLP, m, x22, L.gj);
+  NODE_TS(5);
   __syncthreads();                             // every thread has loaded S from v
 #pragma unroll
   for (int uu = 0; uu < 4; ++uu)
@@ -527,6 +542,7 @@ __global__ __launch_bounds__(256, 2) void spd_node_sym_kernel(double* __restrict
     }
   if (t == 0 && bad) status[b] = 1;
   __syncthreads();
+  NODE_TS(6);
   // X12 = -W X22 (64 x m) -> global X12 and X21 = X12'
   {
     const int ti[4] = {w, w, w, w}, tj[4] = {0, 1, 2, 3};
@@ -548,6 +564,7 @@ __global__ __launch_bounds__(256, 2) void spd_node_sym_kernel(double* __restrict
         }
       }
   __syncthreads();
+  NODE_TS(7);
   // D = X12 W' on the lower tiles of 64 x 64 (10 tiles), then X11 -= D (lower, mirrored)
   {
     int ti[3], tj[3], nt = 0;
@@ -574,6 +591,7 @@ __global__ __launch_bounds__(256, 2) void spd_node_sym_kernel(double* __restrict
         }
   }
   __syncthreads();
+  NODE_TS(8);
 #pragma unroll
   for (int uu = 0; uu < 4; ++uu)
 #pragma unroll
@@ -585,6 +603,7 @@ __global__ __launch_bounds__(256, 2) void spd_node_sym_kernel(double* __restrict
         Xb[(int64_t)j * ld + i] = v;
       }
     }
+  NODE_TS(9);
 }
 }  // namespace
 
@@ -610,4 +629,15 @@ extern "C" hipError_t pfml_spd_node_sym(double* X, int64_t ld, int64_t sX, int b
   hipLaunchKernelGGL(spd_node_sym_kernel, dim3(batch), dim3(256), 0, st, X, ld, sX, r0, nn,
                      status);
   return hipGetLastError();
+}
+
+// the phase timestamps of the last node launch's workgroup 0 (16 values; zeros without
+// -DPFML_NODE_TIMING)
+extern "C" hipError_t pfml_node_timing(unsigned long long* out) {
+#ifdef PFML_NODE_TIMING
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_node_ts), 16 * sizeof(unsigned long long));
+#else
+  for (int i = 0; i < 16; ++i) out[i] = 0;
+  return hipSuccess;
+#endif
 }

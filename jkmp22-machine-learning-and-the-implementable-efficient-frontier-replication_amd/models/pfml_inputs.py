@@ -228,9 +228,12 @@ class S4Plan:
     batches: list
     sig_rows: list
     sig_ids: list
-    R: int
+    R: int                      # rows of feats (the pad row is R)
     Wd: list | None = None      # device copies of W per distinct signal block (no upload in
                                 # run_plan: its launches can be captured in a HIP graph)
+    vol_real: torch.Tensor | None = None   # [Mv, nv] slot holds a real panel row (the vol
+                                # month's median runs over all of them, whether this plan
+                                # keeps a row or not)
 
 
 def universe_npad(chars: pd.DataFrame, months: np.ndarray) -> int:
@@ -360,17 +363,37 @@ def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
     K = barra.X.shape[1]
     bX = np.concatenate([barra.X, np.zeros((1, K))])
     biv = np.r_[barra.ivol, 1.0]
+    # compaction: only the panel rows this plan's months reference (their lookback rows) keep
+    # an RFF feature row, a vol slot and a growth factor - a rank's S4 then scales with its own
+    # months instead of paying the RFF GEMM of the whole panel (per-row arithmetic: the same
+    # bits); vol months still take their medians over every row of the month
+    used = np.unique(np.concatenate([b.idx.cpu().numpy().ravel() for b in batches]
+                                    + [np.zeros(0, np.int64)]))
+    used = used[used < R]
+    Rc = len(used)
+
+    def remap(a):
+        pos = np.searchsorted(used, a)
+        hit = (a < R) & (pos < Rc) & (used[np.minimum(pos, max(Rc - 1, 0))] == a) if Rc else \
+            np.zeros(a.shape, bool)
+        return np.where(hit, pos, Rc).astype(np.int64)
+
+    for b in batches:
+        b.idx = torch.as_tensor(remap(b.idx.cpu().numpy()), dtype=torch.int64, device=dev)
+    vol_real = vol_rows < R
+    vol_rows = remap(vol_rows)
     return S4Plan(
         months=months, G=G, Gc=Gc, P=P, Pp=Pp, N=Npad, W=W, same_w=same_w,
-        feats=torch.as_tensor(panel.feats, dtype=torch.float64, device=dev),
-        gt=torch.as_tensor(np.r_[gt_all, 1.0], dtype=torch.float64, device=dev),
+        feats=torch.as_tensor(panel.feats[used], dtype=torch.float64, device=dev),
+        gt=torch.as_tensor(np.r_[gt_all[used], 1.0], dtype=torch.float64, device=dev),
         vol_rows=torch.as_tensor(vol_rows, device=dev),
+        vol_real=torch.as_tensor(vol_real, device=dev),
         vol_brow=torch.as_tensor(vol_brow, device=dev),
         vol_fpos=torch.as_tensor(np.asarray(vf, np.int64), device=dev),
         bX=torch.as_tensor(bX, dtype=torch.float64, device=dev),
         biv=torch.as_tensor(biv, dtype=torch.float64, device=dev),
         bF=torch.as_tensor(barra.F, dtype=torch.float64, device=dev),
-        batches=batches, sig_rows=sig_rows, sig_ids=sig_ids, R=R,
+        batches=batches, sig_rows=sig_rows, sig_ids=sig_ids, R=Rc,
         Wd=[torch.as_tensor(W[g], dtype=torch.float64, device=dev) for g in range(Gc)])
 
 
@@ -388,7 +411,7 @@ def _vol_device(plan: S4Plan) -> torch.Tensor:
         Fm = plan.bF[plan.vol_fpos]                               # one F per vol month
         d = (gemm(Xr, Fm, backend="own") * Xr).sum(-1) + plan.biv[brc]
         v = torch.where(ok, d.sqrt(), torch.full_like(d, float("nan")))
-        real = plan.vol_rows < plan.R
+        real = plan.vol_real if plan.vol_real is not None else plan.vol_rows < plan.R
         v = torch.where(real, v, torch.full_like(v, float("nan")))
         # pandas median: mean of the two middle values of the non-NaN entries (torch's
         # nanmedian returns the lower one); NaN sorts last

@@ -42,6 +42,8 @@ def main():
         la.spd_inverse_sym(X, st)
     e1.record()
     torch.cuda.synchronize()
+    err = float((torch.bmm(X[:4], A[:4]) - torch.eye(n, device=dev, dtype=torch.float64))
+                .abs().max())
     e2, e3 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e2.record()
     for _ in range(reps):
@@ -49,8 +51,6 @@ def main():
     e3.record()
     torch.cuda.synchronize()
     total = (e0.elapsed_time(e1) - e2.elapsed_time(e3)) / reps
-    err = float((torch.bmm(X[:4], A[:4]) - torch.eye(n, device=dev, dtype=torch.float64))
-                .abs().max())
     # per-GEMM timing (synchronised launches)
     groups = defaultdict(lambda: [0, 0.0, 0.0])
     real = la.gemm_fused
