@@ -242,6 +242,17 @@ struct GjLds {
   double rowb[2][4][64], colb[2][64][4];
 };
 
+// 1 / x as v_rcp_f64 + two Newton steps (correctly rounded on every x measured by
+// tools/micro/rsq_acc.hip, as the IEEE divide): a 5-instruction dependent chain in place of
+// the divide's ~10 (div_scale, rcp, Newton, div_fmas, div_fixup) on every pivot - the pivot
+// chain is what bounds a Gauss-Jordan step (profiles/r05_spd_node_phase_cycles.jsonl)
+__device__ __forceinline__ double gj_rcp(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+#pragma unroll
+  for (int it = 0; it < 2; ++it) y = fma(y, fma(-x, y, 1.0), y);
+  return y;
+}
+
 __device__ __forceinline__ bool gj64(const double* src, int64_t ld, int nb, double (&a)[4][4],
                                      GjLds& sh) {
   const int t = threadIdx.x;
@@ -299,7 +310,7 @@ __device__ __forceinline__ bool gj64(const double* src, int64_t ld, int nb, doub
     for (int p = 0; p < 4; ++p) {
       const double piv = P[p][p];
       bad |= !(piv > 0.0) || !isfinite(piv);
-      const double inv = 1.0 / piv;
+      const double inv = gj_rcp(piv);
       // pivot row (its final values)
 #pragma unroll
       for (int v = 0; v < 4; ++v) rp[p][v] *= inv;
