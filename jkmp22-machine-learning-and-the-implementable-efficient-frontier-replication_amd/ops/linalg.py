@@ -430,8 +430,10 @@ def mf_sym(mode: int, X: torch.Tensor, Y: torch.Tensor | None, out: torch.Tensor
             raise ValueError("mf_sym: a and mask need the same batch stride")
         if mask is not None and a is None:
             sv = mask.stride(0)
-        _work.add("mfunc_sym_kernel", 6.0 * B * N * N,
-                 8.0 * B * N * N * (2 + (Y is not None)))
+        # (the flat form streams each operand once; the tiled form reads the mirror tile too,
+        # mostly from L2: the same minimum bytes)
+        _work.add("mfunc_flat_kernel" if flat else "mfunc_sym_kernel", 6.0 * B * N * N,
+                  8.0 * B * N * N * (2 + (Y is not None)))
         args = _MfArgs(mode, B, N, N, N * N, X.data_ptr(), nat.ptr(Y), out.data_ptr(),
                        nat.ptr(svec), nat.ptr(cvec), nat.ptr(a), nat.ptr(mask), sv, float(d),
                        int(flat))

@@ -54,8 +54,9 @@ for step in ${MODE//,/ }; do
       timeout -k 10 200 python tools/micro/dgemm_rate.py > $OUT/dgemm_rate.json 2>&1
       rc=$?; tail -4 $OUT/dgemm_rate.json; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     s4roof)
-      # S4 roofline: one-batch S4 (+ grid step) under a kernel trace with the work ledger on
-      (cd /tmp && export TMPDIR=/tmp PFML_WORK_LEDGER=$OUT/work_ledger.json && timeout -k 10 600 rocprofv3 --kernel-trace -d $OUT/prof_s4r -o run -- python3 $ROOT/bench.py --with-inputs --steps 1 --warmup 0 > $OUT/prof_s4r.log 2>&1)
+      # S4 roofline: ONE eager S4 of all 731 months on one stream (per-kernel times do not
+      # overlap; the work ledger counts the same launches) under a kernel trace
+      (cd /tmp && export TMPDIR=/tmp PFML_S4_STREAMS=1 PFML_WORK_LEDGER=$OUT/work_ledger.json && timeout -k 10 600 rocprofv3 --kernel-trace -d $OUT/prof_s4r -o run -- python3 $ROOT/bench.py --s4-stress 731 --stocks 500 --warmup 0 > $OUT/prof_s4r.log 2>&1)
       rc=$?; tail -1 $OUT/prof_s4r.log | cut -c1-300; if [ $rc -ne 0 ]; then tail -5 $OUT/prof_s4r.log; exit $rc; fi
       python tools/roofline_s4.py $(find $OUT/prof_s4r -name "*.db" | head -1) $OUT/work_ledger.json > $OUT/roofline_s4.md 2>&1
       rc=$?; cat $OUT/roofline_s4.md | head -30; python tools/rocprof_summary.py $(find $OUT/prof_s4r -name "*.db" | head -1) --top 40 > $OUT/kernels_s4r.txt 2>&1; rm -rf $OUT/prof_s4r; if [ $rc -ne 0 ]; then exit $rc; fi ;;

@@ -5,9 +5,11 @@ rocprofv3 kernel trace (rocpd .db) joined with the run's work ledger (PFML_WORK_
 pfml/utils/work.py: flops and minimum bytes per kernel name, counted by the host wrappers with
 the same dispatch rules as the kernels).
 
-    PFML_WORK_LEDGER=ledger.json rocprofv3 --kernel-trace -d prof -o run -- \\
-        python3 bench.py --with-inputs --steps 1 --warmup 0
-    python tools/roofline_s4.py prof/.../run_results.db ledger.json > profiles/r04_roofline_s4.md
+    PFML_S4_STREAMS=1 PFML_WORK_LEDGER=ledger.json rocprofv3 --kernel-trace -d prof -o run -- \\
+        python3 bench.py --s4-stress 731 --warmup 0      (ONE eager S4 on one stream: per-kernel
+                                                          times do not overlap, the ledger
+                                                          counts the same launches)
+    python tools/roofline_s4.py prof/.../run_results.db ledger.json > profiles/r05_roofline_s4.md
 
 Ledger keys are full kernel names (``dgemm_kernel<false, false, 64, 64, 2, true>``) or name
 prefixes (``standardize`` covers standardize_kernel / standardize_reg_kernel<32>).  Kernels the
@@ -20,16 +22,20 @@ import sys
 
 MFMA, VALU, HBM = 78.2e12, 65.7e12, 8.0e12
 ROLE = {
-    "dgemm_kernel<false, false, 64, 64, 2, true, 16, 2>": "Horner step of (24) (k-scaled, fused epilogue)",
-    "dgemm_kernel<false, false, 128, 128, 2, true, 16, 2>": "Horner step of (24), 128 x 128 tiles",
-    "dgemm_kernel<false, false, 64, 64, 2, false, 16, 2>": "m_func / SPD-inverse Schur GEMMs, Sigma, LU panel transforms",
-    "dgemm_kernel<false, true, 64, 64, 2, false, 16, 2>": "X F X' (Sigma), SPD-inverse X21 / X11 updates",
-    "dgemm_kernel<true, false, 64, 64, 2, true, 16, 2>": "denominator / summand Gram products (25)",
-    "dgemm_kernel<true, false, 64, 64, 2, false, 16, 2>": "risk / tc: omega' Sigma omega",
+    "dgemm_glds_kernel<false, false, 128, 64, false, 2, 2, 2>": "Horner steps of (24) (row-scaled, gathered addend, output row scale); SPD-inverse W / X12 and DB products",
+    "dgemm_glds_kernel<false, false, 128, 64, true, 2, 2, 2>": "T_0 step of (24) (k-scaled)",
+    "dgemm_glds_kernel<false, false, 64, 64, false, 2, 2, 2>": "symmetric-mode products: S = A22 - A21 W, Y M^-1, x^2 + 4x, Sigma",
+    "dgemm_glds_kernel<false, true, 64, 64, false, 2, 2, 2>": "symmetric-mode X11 -= X12 W'",
+    "dgemm_glds_kernel<true, false, 64, 64, true, 2, 2, 2>": "tc = w omega_chg' Lambda omega_chg (k-scaled, symmetric)",
+    "dgemm_glds_kernel<true, false, 64, 64, false, 2, 2, 2>": "risk = gamma omega' Sigma omega (symmetric), X' omega",
+    "dgemm_kernel<false, false, 64, 64, 1, false, 16, 2>": "odd-width operands (RFF / 1-column products)",
+    "spd_node_sym_kernel": "SPD-inverse nodes of 65..128 rows (two 64-leaf Gauss-Jordan + four MFMA products)",
     "spd_leafinv_kernel": "64 x 64 SPD leaf inverses (register Gauss-Jordan)",
-    "mfunc_sym_kernel": "m_func symmetric elementwise passes",
+    "mfunc_flat_kernel": "m_func elementwise passes, row stream (exactly symmetric operands)",
+    "mfunc_sym_kernel": "m_func elementwise passes, tiled (symmetrising)",
     "db_norm_partial_kernel": "Denman-Beavers scaling norms",
-    "standardize": "signal gather + standardise + 1/vol",
+    "standardize": "signal gather + standardise + 1/vol (lags 0, 11, 12) and column statistics (lags 1-10)",
+    "lu_update_kernel<32>": "LU solve of [const | Omega] (K7): trailing update",
 }
 
 
