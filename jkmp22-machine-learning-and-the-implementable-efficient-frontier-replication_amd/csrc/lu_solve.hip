@@ -113,13 +113,14 @@ __global__ __launch_bounds__(1024) void lu_pivot_kernel(const double* __restrict
 // owners of rows j and p swap in registers (double-buffered posts: the next column writes the
 // other buffer).  Same pivot choice (first index of the maximum |a|) and the same elimination
 // arithmetic as lu_pivot_kernel, so both forms pick the same pivots.
-template <int NB, int R, int RL>
-__global__ __launch_bounds__(1024) void lu_pivot_reg_kernel(const double* __restrict__ M, int n,
-                                                            int64_t ldm, int64_t sM, int a0,
-                                                            int k0, int nb,
-                                                            int* __restrict__ piv,
-                                                            int* __restrict__ status) {
-  constexpr int NT = 1024, NW = NT / 64, RR = R - RL;
+template <int NB, int R, int RL, int NTT = 1024>
+__global__ __launch_bounds__(NTT) void lu_pivot_reg_kernel(const double* __restrict__ M, int n,
+                                                           int64_t ldm, int64_t sM, int a0,
+                                                           int k0, int nb,
+                                                           int* __restrict__ piv,
+                                                           int* __restrict__ status) {
+  constexpr int NT = NTT, NW = NT / 64, RR = R - RL;
+  static_assert(NT > NB, "thread j posts row j");
   __shared__ double cand[2][NW][NB];
   __shared__ double cval[2][NW];
   __shared__ int cidx[2][NW];
@@ -227,7 +228,19 @@ hipError_t lu_pivot_launch(const double* M, int n, int64_t ldm, int64_t sM, int 
   // column and ~8 KB of LDS, so two workgroups share a CU - the LDS form's 135 KB panel
   // allowed one, and its elimination spent an integer division per element (same pivots,
   // same arithmetic)
+  // (the workgroup shrinks with the panel: 256 / 512 threads for panels of <= 256 / 512 rows,
+  // so more matrices' panels run per CU - the panel's rows, not the threads, are the work)
   if constexpr (NB == 32) {
+    if (rows <= 256) {
+      hipLaunchKernelGGL((lu_pivot_reg_kernel<NB, 1, 0, 256>), dim3(batch), dim3(256), 0, st, M,
+                         n, ldm, sM, a0, k0, nb, piv, status);
+      return hipSuccess;
+    }
+    if (rows <= 512) {
+      hipLaunchKernelGGL((lu_pivot_reg_kernel<NB, 1, 0, 512>), dim3(batch), dim3(512), 0, st, M,
+                         n, ldm, sM, a0, k0, nb, piv, status);
+      return hipSuccess;
+    }
     if (rows <= 1024) {
       hipLaunchKernelGGL((lu_pivot_reg_kernel<NB, 1, 0>), dim3(batch), dim3(1024), 0, st, M, n,
                          ldm, sM, a0, k0, nb, piv, status);
