@@ -454,9 +454,11 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
     range_push("pfml_inputs.rff")
     Wdev = plan.Wd if plan.Wd is not None else [
         torch.as_tensor(plan.W[g], dtype=torch.float64, device=dev) for g in range(Gc)]
-    rffs = [rff_features(plan.feats, Wdev[g], prec, width=Pp, pad_rows=1) for g in range(Gc)]
-    # the gathered addend's feature table: every g block side by side, [R + 1, Gc * Pp]
-    Fcat = torch.cat(rffs, 1) if Gc > 1 else rffs[0]
+    # the gathered addend's feature table: every g block side by side, [R + 1, Gc * Pp], each
+    # block written in place by its RFF launch (no concatenation pass)
+    Fcat = torch.empty((plan.feats.shape[0] + 1, Gc * Pp), dtype=torch.float64, device=dev)
+    rffs = [rff_features(plan.feats, Wdev[g], prec, width=Pp, pad_rows=1,
+                         out=Fcat[:, g * Pp:(g + 1) * Pp]) for g in range(Gc)]
     vol = _vol_device(plan)
     range_pop()
 
@@ -599,8 +601,8 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
             sing.zero_()
             # (25): r_tilde = omega' r, risk = gamma omega' Sigma omega (Sigma in low-rank form:
             # X (F (X' omega)) + ivol o omega), tc = w omega_chg' Lambda omega_chg, denom
-            omega = omega.contiguous()
-            omega_chg = omega_chg.contiguous()
+            # (omega stays a row-strided view of the solve buffer: every consumer takes the
+            # row stride; omega_chg is a fresh tensor)
             rt_ = gemm(omega, bt.r.unsqueeze(-1).contiguous(), trans_a=True,
                        backend="own").squeeze(-1)                                # [B, GP]
             XtO = torch.empty((B, Xl.shape[2], GP), dtype=torch.float64, device=dev)

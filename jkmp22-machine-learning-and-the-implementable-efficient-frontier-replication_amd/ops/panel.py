@@ -23,34 +23,49 @@ nat.register_hip("pfml_standardize", [C.c_void_p, C.c_int, C.c_int64, C.c_void_p
 
 
 def rff_features(X: torch.Tensor, W: torch.Tensor, precision: str = "fp64",
-                 width: int | None = None, pad_rows: int = 0) -> torch.Tensor:
+                 width: int | None = None, pad_rows: int = 0,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
     """[R, k] x [k, P/2] -> [R + pad_rows, width] rows [1, cos z1, sin z1, cos z2, sin z2, ...,
     0 ...] (P = 2 (P/2) + 1 real columns; ``width`` >= P pads with zero columns, ``pad_rows``
     appends all-zero rows).  fp64 on a device: ONE launch of the fused GEMM whose epilogue
     writes cos / sin of each accumulator straight into the interleaved row (X W never
     stored); ``precision`` fp32 / bf16 / fp8 (experimental configs): the lowered GEMM, then the
-    sincos kernel."""
+    sincos kernel.  ``out``: a [R + pad_rows, width] (column block) view to write into."""
     R, half = X.shape[0], W.shape[1]
     P = 2 * half + 1
     width = width or P
+    if out is not None and (tuple(out.shape) != (R + pad_rows, width) or out.stride(-1) != 1):
+        raise ValueError("rff_features: out must be a [R + pad_rows, width] row-major view")
     if nat.is_device(X) and precision == "fp64":
-        out = torch.empty((R + pad_rows, width), dtype=X.dtype, device=X.device)
+        if out is None:
+            out = torch.empty((R + pad_rows, width), dtype=X.dtype, device=X.device)
         if pad_rows:
             out[R:].zero_()
         if width > P:
             out[:R, P:].zero_()
-        gemm_fused(X.contiguous(), W.contiguous(), out[:R], sincos=True)
+        Xc, Wc = X.contiguous(), W.contiguous()
+        # row chunks: the GEMM's epilogue addresses one output with 32-bit byte offsets (< 2 GB)
+        ch = max(1, ((1 << 31) // 8 - out.shape[1]) // out.stride(0) - 1)
+        for r0 in range(0, R, ch):
+            gemm_fused(Xc[r0:r0 + ch], Wc, out[r0:min(R, r0 + ch)], sincos=True)
         return out
     Z = gemm_prec(X, W, precision)
     if nat.is_device(X):
-        out = torch.empty((R + pad_rows, width), dtype=X.dtype, device=X.device)
+        if out is None:
+            out = torch.empty((R + pad_rows, width), dtype=X.dtype, device=X.device)
         if pad_rows:
             out[R:].zero_()
+        if width > P:
+            out[:R, P:].zero_()
         Zc = Z.contiguous()
-        nat.check(nat.hip_lib().pfml_rff_sincos(Zc.data_ptr(), R, half, out.data_ptr(), width,
-                                                nat.stream_of(X)), "pfml_rff_sincos")
+        nat.check(nat.hip_lib().pfml_rff_sincos(Zc.data_ptr(), R, half, out.data_ptr(),
+                                                out.stride(0), nat.stream_of(X)),
+                  "pfml_rff_sincos")
     else:
-        out = torch.zeros((R + pad_rows, width), dtype=X.dtype, device=X.device)
+        if out is None:
+            out = torch.zeros((R + pad_rows, width), dtype=X.dtype, device=X.device)
+        else:
+            out.zero_()
         out[:R, 0].fill_(1.0)
         out[:R, 1:P:2] = torch.cos(Z)
         out[:R, 2:P:2] = torch.sin(Z)
