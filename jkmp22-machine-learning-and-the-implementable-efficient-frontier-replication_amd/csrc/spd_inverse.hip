@@ -438,7 +438,9 @@ __device__ __forceinline__ void node_mm(const int (&ti)[NT], const int (&tj)[NT]
   }
 }
 
-__global__ __launch_bounds__(256, 2) void spd_node_sym_kernel(double* __restrict__ X,
+// Src: the input (the same layout as X; == X in place): A11, A21, A22 are read from it, every
+// result is written to X (out of place: no copy of the input first)
+__global__ __launch_bounds__(256, 2) void spd_node_sym_kernel(const double* Src, double* X,
                                                              int64_t ld, int64_t sX, int r0,
                                                              int nn, int* __restrict__ status) {
   __shared__ NodeLds L;
@@ -452,15 +454,18 @@ __global__ __launch_bounds__(256, 2) void spd_node_sym_kernel(double* __restrict
   double* Xb = X + (int64_t)b * sX + (int64_t)r0 * ld + r0;
   double* X21 = Xb + (int64_t)64 * ld;         // rows 64.., columns 0..
   double* X22 = X21 + 64;
+  const double* Ab = Src + (int64_t)b * sX + (int64_t)r0 * ld + r0;
+  const double* A21 = Ab + (int64_t)64 * ld;
+  const double* A22 = A21 + 64;
   // A21 -> v (rows >= m: zero)
   for (int e = t; e < 64 * 64; e += 256) {
     const int i = e >> 6, k = e & 63;
-    L.v[i][k] = i < m ? X21[(int64_t)i * ld + k] : 0.0;
+    L.v[i][k] = i < m ? A21[(int64_t)i * ld + k] : 0.0;
   }
   // X11 = A11^-1 (registers), its mirrored image -> u
   double x11[4][4];
   NODE_TS(1);
-  bool bad = gj64(Xb, ld, 64, x11, L.gj);
+  bool bad = gj64(Ab, ld, 64, x11, L.gj);
   NODE_TS(2);
 #pragma unroll
   for (int uu = 0; uu < 4; ++uu)
@@ -513,7 +518,7 @@ __global__ __launch_bounds__(256, 2) void spd_node_sym_kernel(double* __restrict
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = ti[q] * 16 + PFML_F64_CROW(lane, r), j = tj[q] * 16 + li;
-        const double c = (q < nt && i < m && j < m) ? X22[(int64_t)i * ld + j] : 0.0;
+        const double c = (q < nt && i < m && j < m) ? A22[(int64_t)i * ld + j] : 0.0;
         sv[q][r] = -sacc[q][r] + c;
       }
     __syncthreads();                           // v (A21) fully read
@@ -631,13 +636,15 @@ extern "C" hipError_t pfml_spd_leafinv_to(const double* A, int64_t lda, int64_t 
   return hipGetLastError();
 }
 
-// In-place one-triangle inverse of the nn x nn diagonal block at (r0, r0) of every matrix,
-// 64 < nn <= 128 (exactly symmetric input and output), one launch (spd_node_sym_kernel).
-extern "C" hipError_t pfml_spd_node_sym(double* X, int64_t ld, int64_t sX, int batch, int r0,
-                                        int nn, int* status, hipStream_t st) {
+// One-triangle inverse of the nn x nn diagonal block at (r0, r0) of every matrix of Src into
+// the same block of X (Src == X: in place), 64 < nn <= 128 (exactly symmetric input and
+// output), one launch (spd_node_sym_kernel).
+extern "C" hipError_t pfml_spd_node_sym(const double* Src, double* X, int64_t ld, int64_t sX,
+                                        int batch, int r0, int nn, int* status,
+                                        hipStream_t st) {
   if (batch <= 0) return hipSuccess;
   if (nn <= NBL || nn > 2 * NBL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(spd_node_sym_kernel, dim3(batch), dim3(256), 0, st, X, ld, sX, r0, nn,
+  hipLaunchKernelGGL(spd_node_sym_kernel, dim3(batch), dim3(256), 0, st, Src, X, ld, sX, r0, nn,
                      status);
   return hipGetLastError();
 }

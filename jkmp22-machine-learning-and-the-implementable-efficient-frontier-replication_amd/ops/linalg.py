@@ -85,8 +85,8 @@ nat.register_hip("pfml_spd_leafinv_to", [C.c_void_p, C.c_int64, C.c_int64, C.c_v
                                          C.c_int64, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                          C.c_int, C.c_void_p])
 
-nat.register_hip("pfml_spd_node_sym", [C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int,
-                                       C.c_int, C.c_void_p, C.c_void_p])
+nat.register_hip("pfml_spd_node_sym", [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int,
+                                       C.c_int, C.c_int, C.c_void_p, C.c_void_p])
 
 _REC_LEAF = 64
 _REC_BUFS: dict = {}
@@ -176,7 +176,8 @@ DB_SYMPROD = os.environ.get("PFML_DB_SYMPROD", "1") != "0"
 SYM_NODE = os.environ.get("PFML_SPD_NODE", "1") != "0"
 
 
-def spd_inverse_sym(X: torch.Tensor, status: torch.Tensor) -> torch.Tensor:
+def spd_inverse_sym(X: torch.Tensor, status: torch.Tensor,
+                    src: torch.Tensor | None = None) -> torch.Tensor:
     """In-place inverse of a device batch [B, n, n] of EXACTLY symmetric SPD matrices whose
     result is used as a symmetric matrix (m_tilde_0 and the fixed-point steps of m_func,
     General_functions.py:957-960): the recursive Schur form with every symmetric product
@@ -186,9 +187,17 @@ def spd_inverse_sym(X: torch.Tensor, status: torch.Tensor) -> torch.Tensor:
         X12 = -W X22  (X21 = X12' written by the same launch),  X11 -= X12 W'  (lower tiles)
 
     about n^3 flops instead of the two-sided form's ~1.67 n^3, with exactly symmetric leaves
-    and products, so the result is exactly symmetric.  Non-positive pivots flag ``status``."""
+    and products, so the result is exactly symmetric.  Non-positive pivots flag ``status``.
+    ``src`` (same shape, contiguous): the input, only read - the inverse goes to X without a
+    copy of the input first (the input blocks along the recursion's left spine and the A12 /
+    A21 / A22 blocks of its nodes are read from src; A22 enters the Schur GEMM as its addend,
+    the same arithmetic as the in-place beta)."""
     B, n, _ = X.shape
+    if src is not None and (src.shape != X.shape or not src.is_contiguous()):
+        raise ValueError("spd_inverse_sym: src must be contiguous and shaped like X")
     if not nat.is_device(X) or n < _BLOCKED_MIN_N or not X.is_contiguous() or not SYM_INVERSE:
+        if src is not None:
+            X.copy_(src)
         return spd_inverse(X, inplace=True, status=status)
     lib = nat.hip_lib()
     st = nat.stream_of(X)
@@ -203,10 +212,11 @@ def spd_inverse_sym(X: torch.Tensor, status: torch.Tensor) -> torch.Tensor:
             _REC_BUFS[key] = w
         return w[:B * h * m].view(B, h, m)
 
-    def rec(r0, nn, depth):
+    def rec(r0, nn, depth, A):
+        # A: where this block's input lives (src along the left spine, else X itself)
         if nn <= _REC_LEAF:
             _work.add("spd_leafinv_kernel", 2.0 * B * nn ** 3, 16.0 * B * nn * nn)
-            nat.check(lib.pfml_spd_leafinv_to(X.data_ptr(), ld, sX, X.data_ptr(), ld, sX, B, r0,
+            nat.check(lib.pfml_spd_leafinv_to(A.data_ptr(), ld, sX, X.data_ptr(), ld, sX, B, r0,
                                               nn, status.data_ptr(), 1, st),
                       "pfml_spd_leafinv_to")
             return
@@ -216,24 +226,28 @@ def spd_inverse_sym(X: torch.Tensor, status: torch.Tensor) -> torch.Tensor:
                                                   + 3.0 * _REC_LEAF ** 2 * m
                                                   + 3.0 * _REC_LEAF * m * m),
                       8.0 * B * 2 * nn * nn)
-            nat.check(lib.pfml_spd_node_sym(X.data_ptr(), ld, sX, B, r0, nn, status.data_ptr(),
-                                            st), "pfml_spd_node_sym")
+            nat.check(lib.pfml_spd_node_sym(A.data_ptr(), X.data_ptr(), ld, sX, B, r0, nn,
+                                            status.data_ptr(), st), "pfml_spd_node_sym")
             return
         h = _rec_split(nn)
         m = nn - h
         a, c, e = r0, r0 + h, r0 + nn
-        rec(a, h, depth + 1)
+        rec(a, h, depth + 1, A)
         W = buf(depth, h, m)
-        gemm_fused(X[:, a:c, a:c], X[:, a:c, c:e], W, tile_cfg=cfg)              # W = X11 A12
-        gemm_fused(X[:, c:e, a:c], W, X[:, c:e, c:e], alpha=-1.0, beta=1.0, sym=True,
-                   tile_cfg=cfg)                                                  # S
-        rec(c, m, depth + 1)
+        gemm_fused(X[:, a:c, a:c], A[:, a:c, c:e], W, tile_cfg=cfg)              # W = X11 A12
+        if A is X:
+            gemm_fused(X[:, c:e, a:c], W, X[:, c:e, c:e], alpha=-1.0, beta=1.0, sym=True,
+                       tile_cfg=cfg)                                              # S
+        else:
+            gemm_fused(A[:, c:e, a:c], W, X[:, c:e, c:e], alpha=-1.0, addend=A[:, c:e, c:e],
+                       sym=True, tile_cfg=cfg)                                    # S
+        rec(c, m, depth + 1, X)
         gemm_fused(W, X[:, c:e, c:e], X[:, a:c, c:e], alpha=-1.0, mirror_out=X[:, c:e, a:c],
                    tile_cfg=cfg)                                                  # X12, X21
         gemm_fused(X[:, a:c, c:e], W, X[:, a:c, a:c], trans_b=True, alpha=-1.0, beta=1.0,
                    sym=True, tile_cfg=cfg)                                        # X11 -= X12 W'
 
-    rec(0, n, 0)
+    rec(0, n, 0, X if src is None else src)
     return X
 
 
@@ -502,8 +516,7 @@ def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tenso
     sym_inv, sym_prod = DB_SYM and dev_sym, DB_SYMPROD and dev_sym
     for it in range(iters):
         if sym_inv:
-            Mi.copy_(M)
-            spd_inverse_sym(Mi, status)
+            spd_inverse_sym(Mi, status, src=M)
         else:
             spd_inverse_into(M, Mi, status)
         _db_mu(M, Mi, it >= scaled_iters, mu)

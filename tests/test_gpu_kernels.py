@@ -193,6 +193,27 @@ def test_spd_node_sym_bitwise(gpu, n):
     assert ((outs[0][:5] - ref).norm(dim=(1, 2)) / ref.norm(dim=(1, 2))).max() < 1e-11
 
 
+@pytest.mark.parametrize("n", [490, 257, 200])
+def test_spd_inverse_sym_out_of_place_bitwise(gpu, n):
+    """spd_inverse_sym(X, st, src=A) (input only read, no copy) is bitwise the in-place
+    inverse of a copy of A, flags included, and leaves A untouched."""
+    from pfml.ops.linalg import spd_inverse_sym
+    g = torch.Generator().manual_seed(n + 7)
+    X = torch.randn(5, n + 40, n, generator=g, dtype=torch.float64)
+    A = X.transpose(1, 2) @ X / n + 1e-3 * torch.eye(n, dtype=torch.float64)
+    A = 0.5 * (A + A.transpose(1, 2))
+    A[4, 3, 3] = -20.0                             # not SPD: the first leaf's pivot fails
+    Ad = A.to(gpu).contiguous()
+    keep = Ad.clone()
+    st1 = torch.zeros(5, dtype=torch.int32, device=gpu)
+    st2 = torch.zeros(5, dtype=torch.int32, device=gpu)
+    inplace = spd_inverse_sym(Ad.clone(), st1)
+    out = spd_inverse_sym(torch.empty_like(Ad), st2, src=Ad)
+    assert torch.equal(Ad, keep)
+    assert torch.equal(st1, st2) and st1.tolist() == [0, 0, 0, 0, 1]
+    assert torch.equal(out[:4], inplace[:4])
+
+
 def test_segment_sums(gpu):
     from pfml.ops.ridge import segment_sums
     X = _rand(40, 7, 9, seed=7)
