@@ -95,10 +95,11 @@ __global__ __launch_bounds__(256) void mfunc_sym_kernel(MfArgs p) {
 }
 
 // The flat passes (X and Y exactly symmetric: no mirror tile) as a row stream: one wave per
-// row, 16-byte loads / stores of column pairs, the row's a_i / mask_i wave-uniform.  Same
+// row, 16-byte loads / stores of column pairs (all of a row's loads issued before its first
+// store), the row's a_i / mask_i wave-uniform, the column vectors loaded once per wave.  Same
 // expressions as mfunc_sym_kernel (bitwise), ~1.4x its rate: the 32 x 32 tile form spends a
-// 256-thread workgroup on 1024 elements with 8-byte accesses.  Needs even ld and 16-byte
-// aligned operands (host checks).
+// 256-thread workgroup on 1024 elements with 8-byte accesses.  Needs even N <= 512, even ld and
+// 16-byte aligned operands (host checks; otherwise the tiled form runs).
 constexpr int FLAT_ROWS = 16;                      // rows per workgroup (4 per wave)
 
 __device__ __forceinline__ double mf_value(const MfArgs& p, int i, int j, double xs, double ys,
@@ -123,6 +124,9 @@ __device__ __forceinline__ double mf_value(const MfArgs& p, int i, int j, double
   return v;
 }
 
+// (even N: every lane handles whole column pairs; N <= 64 * 2 * QM per wave pass)
+constexpr int FLAT_QM = 4;                         // column-pair chunks per lane (N <= 512)
+
 __global__ __launch_bounds__(256) void mfunc_flat_kernel(MfArgs p) {
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -133,34 +137,38 @@ __global__ __launch_bounds__(256) void mfunc_flat_kernel(MfArgs p) {
   const double c = p.cvec ? p.cvec[b] : 1.0;
   const double* av = p.a ? p.a + (int64_t)b * p.sv : nullptr;
   const double* mv = p.mask ? p.mask + (int64_t)b * p.sv : nullptr;
-  const int np = (p.N + 1) >> 1;                   // column pairs (the last may be half)
+  const int np = p.N >> 1;                         // column pairs
   const int r1 = min(p.N, (int)(blockIdx.x + 1) * FLAT_ROWS);
+  // the column vectors of this lane's pairs, once per wave (the same for every row)
+  double2_t aj[FLAT_QM], mj[FLAT_QM];
+#pragma unroll
+  for (int k = 0; k < FLAT_QM; ++k) {
+    const int q = min(lane + 64 * k, np - 1);
+    aj[k] = av ? reinterpret_cast<const double2_t*>(av)[q] : double2_t{0.0, 0.0};
+    mj[k] = mv ? reinterpret_cast<const double2_t*>(mv)[q] : double2_t{0.0, 0.0};
+  }
   for (int i = blockIdx.x * FLAT_ROWS + w; i < r1; i += 4) {
     const double ai = av ? av[i] : 0.0, mi = mv ? mv[i] : 0.0;
     const double2_t* xr = reinterpret_cast<const double2_t*>(X + (int64_t)i * p.ld);
     const double2_t* yr = Y ? reinterpret_cast<const double2_t*>(Y + (int64_t)i * p.ld) : nullptr;
-    double* orow = O + (int64_t)i * p.ld;
-    for (int q = lane; q < np; q += 64) {
-      const int j = 2 * q;
-      const bool two = j + 1 < p.N;
-      double2_t xv, yv = {0.0, 0.0}, aj = {0.0, 0.0}, mj = {0.0, 0.0};
-      if (two) {
-        xv = xr[q];
-        if (yr) yv = yr[q];
-        if (av) aj = reinterpret_cast<const double2_t*>(av)[q];
-        if (mv) mj = reinterpret_cast<const double2_t*>(mv)[q];
-      } else {
-        xv = double2_t{X[(int64_t)i * p.ld + j], 0.0};
-        if (yr) yv.x = Y[(int64_t)i * p.ld + j];
-        if (av) aj.x = av[j];
-        if (mv) mj.x = mv[j];
-      }
-      const double v0 = mf_value(p, i, j, xv.x, yv.x, s, c, ai, aj.x, mi, mj.x);
-      if (two) {
-        const double v1 = mf_value(p, i, j + 1, xv.y, yv.y, s, c, ai, aj.y, mi, mj.y);
-        reinterpret_cast<double2_t*>(orow)[q] = double2_t{v0, v1};
-      } else {
-        orow[j] = v0;
+    double2_t* orow = reinterpret_cast<double2_t*>(O + (int64_t)i * p.ld);
+    // every load of the row first (clamped addresses), then the values and the stores
+    double2_t xv[FLAT_QM], yv[FLAT_QM];
+#pragma unroll
+    for (int k = 0; k < FLAT_QM; ++k) {
+      const int q = min(lane + 64 * k, np - 1);
+      xv[k] = xr[q];
+      yv[k] = yr ? yr[q] : double2_t{0.0, 0.0};
+    }
+#pragma unroll
+    for (int k = 0; k < FLAT_QM; ++k) {
+      const int q = lane + 64 * k;
+      if (q < np) {
+        const int j = 2 * q;
+        const double v0 = mf_value(p, i, j, xv[k].x, yv[k].x, s, c, ai, aj[k].x, mi, mj[k].x);
+        const double v1 = mf_value(p, i, j + 1, xv[k].y, yv[k].y, s, c, ai, aj[k].y, mi,
+                                   mj[k].y);
+        orow[q] = double2_t{v0, v1};
       }
     }
   }
@@ -233,7 +241,8 @@ extern "C" hipError_t pfml_mfunc_sym(const PfmlMfArgs* h, hipStream_t st) {
   MfArgs p{h->mode, h->B, h->N, h->ld, h->sX, h->X, h->Y, h->out, h->svec, h->cvec, h->a,
            h->mask, h->sv, h->d, h->flat};
   const auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
-  const bool vec = h->ld % 2 == 0 && h->sX % 2 == 0 && (h->sv % 2 == 0 || (!h->a && !h->mask)) &&
+  const bool vec = h->N % 2 == 0 && h->N <= 128 * FLAT_QM && h->ld % 2 == 0 && h->sX % 2 == 0 &&
+                   (h->sv % 2 == 0 || (!h->a && !h->mask)) &&
                    al16(h->X) && (!h->Y || al16(h->Y)) && al16(h->out) &&
                    (!h->a || al16(h->a)) && (!h->mask || al16(h->mask));
   if (h->flat && vec) {
