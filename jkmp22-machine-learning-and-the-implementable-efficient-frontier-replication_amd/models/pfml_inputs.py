@@ -360,9 +360,20 @@ def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
             n_real=tt(ns, torch.int32), brow=tt(brow, torch.int64), fpos=tt(fpos, torch.int64),
             lam=tt(lam), r=tt(rr), w=tt([wmap[int(d)] for d in bm]),
             rf=tt([rfmap[int(d)] for d in bm])))
+    # even inner dimensions (a zero factor / a zero feature column - exact zeros in every sum):
+    # the GEMMs on them (X F, X' omega, the RFF product) then take the 16-byte-load kernels
     K = barra.X.shape[1]
-    bX = np.concatenate([barra.X, np.zeros((1, K))])
+    Kp = _even(K)
+    bX = np.zeros((barra.X.shape[0] + 1, Kp))
+    bX[:-1, :K] = barra.X
+    bF = np.zeros((barra.F.shape[0], Kp, Kp))
+    bF[:, :K, :K] = barra.F
     biv = np.r_[barra.ivol, 1.0]
+    kf = panel.feats.shape[1]
+    kfp = _even(kf)
+    Wp = [np.zeros((kfp, W[g].shape[1])) for g in range(Gc)]
+    for g in range(Gc):
+        Wp[g][:kf] = W[g]
     # compaction: only the panel rows this plan's months reference (their lookback rows) keep
     # an RFF feature row, a vol slot and a growth factor - a rank's S4 then scales with its own
     # months instead of paying the RFF GEMM of the whole panel (per-row arithmetic: the same
@@ -382,9 +393,11 @@ def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         b.idx = torch.as_tensor(remap(b.idx.cpu().numpy()), dtype=torch.int64, device=dev)
     vol_real = vol_rows < R
     vol_rows = remap(vol_rows)
+    feats_p = np.zeros((Rc, kfp))
+    feats_p[:, :kf] = panel.feats[used]
     return S4Plan(
         months=months, G=G, Gc=Gc, P=P, Pp=Pp, N=Npad, W=W, same_w=same_w,
-        feats=torch.as_tensor(panel.feats[used], dtype=torch.float64, device=dev),
+        feats=torch.as_tensor(feats_p, dtype=torch.float64, device=dev),
         gt=torch.as_tensor(np.r_[gt_all[used], 1.0], dtype=torch.float64, device=dev),
         vol_rows=torch.as_tensor(vol_rows, device=dev),
         vol_real=torch.as_tensor(vol_real, device=dev),
@@ -392,9 +405,9 @@ def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         vol_fpos=torch.as_tensor(np.asarray(vf, np.int64), device=dev),
         bX=torch.as_tensor(bX, dtype=torch.float64, device=dev),
         biv=torch.as_tensor(biv, dtype=torch.float64, device=dev),
-        bF=torch.as_tensor(barra.F, dtype=torch.float64, device=dev),
+        bF=torch.as_tensor(bF, dtype=torch.float64, device=dev),
         batches=batches, sig_rows=sig_rows, sig_ids=sig_ids, R=Rc,
-        Wd=[torch.as_tensor(W[g], dtype=torch.float64, device=dev) for g in range(Gc)])
+        Wd=[torch.as_tensor(Wp[g], dtype=torch.float64, device=dev) for g in range(Gc)])
 
 
 def _vol_device(plan: S4Plan) -> torch.Tensor:
@@ -453,7 +466,9 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
     # ---- 1. RFF features (K13) and 2. vol scales -----------------------------------------
     range_push("pfml_inputs.rff")
     Wdev = plan.Wd if plan.Wd is not None else [
-        torch.as_tensor(plan.W[g], dtype=torch.float64, device=dev) for g in range(Gc)]
+        torch.nn.functional.pad(torch.as_tensor(plan.W[g], dtype=torch.float64, device=dev),
+                                (0, 0, 0, plan.feats.shape[1] - plan.W[g].shape[0]))
+        for g in range(Gc)]
     # the gathered addend's feature table: every g block side by side, [R + 1, Gc * Pp], each
     # block written in place by its RFF launch (no concatenation pass)
     Fcat = torch.empty((plan.feats.shape[0] + 1, Gc * Pp), dtype=torch.float64, device=dev)
