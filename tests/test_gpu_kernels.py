@@ -96,8 +96,9 @@ def test_gemm_fused_matches_torch(gpu, ta, tb, cfg, shape):
 @pytest.mark.parametrize("cfg", [3, 6, 8])
 def test_gemm_gathered_addend(gpu, cfg):
     """The gathered addend of the Horner steps (standardised signals formed in the epilogue):
-    out = rs * (A B) + es_i * (F[rows_i] - shift) * scale on the first e_cols columns, vs the
-    torch oracle, with rows repeated and out of order."""
+    out = os_i (rs * (A B) + es_i * (F[rows_i] - shift) * scale on the first e_cols columns
+    + the diagonal), vs the torch oracle, with rows repeated and out of order and a strided
+    output row scale."""
     from pfml.ops.gemm import gemm_fused
     b, M, N, K, E = 3, 130, 202, 96, 150
     A, B = _rand(b, M, K, seed=1), _rand(b, K, N, seed=2)
@@ -106,7 +107,8 @@ def test_gemm_gathered_addend(gpu, cfg):
     kw = dict(row_scale=_rand(b, M, seed=5), addend=F, addend_cols=E, addend_rows=rows[:, 7],
               addend_col_shift=_rand(b, 2, E, seed=6)[:, 0],
               addend_col_scale=_rand(b, 2, E, seed=6)[:, 1],
-              addend_row_scale=_rand(b, 4, M, seed=7)[:, 2], diag_col0=E, diag_value=1.0)
+              addend_row_scale=_rand(b, 4, M, seed=7)[:, 2], diag_col0=E, diag_value=1.0,
+              out_row_scale=_rand(b, 3, M, seed=8)[:, 1])    # (the next step's k-scale)
     ref = gemm_fused(A, B, torch.empty(b, M, N, dtype=torch.float64), **kw)
     kd = {k: (v.to(gpu) if isinstance(v, torch.Tensor) else v) for k, v in kw.items()}
     out = gemm_fused(A.to(gpu), B.to(gpu), torch.empty(b, M, N, dtype=torch.float64, device=gpu),

@@ -147,6 +147,11 @@ def test_rff_and_standardize(gpu):
     P = F.shape[1]
     Fw = rff_features(X.to(gpu), W.to(gpu), width=P + 1, pad_rows=1)
     assert torch.equal(Fw[:300, :P].cpu(), Fd) and not Fw[300:].any() and not Fw[:, P:].any()
+    # written in place into a column block of a wider table (S4's gathered-addend table)
+    tab = torch.full((301, 3 * (P + 1)), 7.0, dtype=torch.float64, device=gpu)
+    rff_features(X.to(gpu), W.to(gpu), width=P + 1, pad_rows=1, out=tab[:, P + 1:2 * P + 2])
+    assert torch.equal(tab[:, P + 1:2 * P + 2], Fw)
+    assert bool((tab[:, :P + 1] == 7.0).all()) and bool((tab[:, 2 * P + 2:] == 7.0).all())
     stack = torch.full((2, 13, 40, 2 * (P + 1)), 7.0, dtype=torch.float64, device=gpu)
     standardize_signals(Fw, idx.to(gpu), mask.to(gpu), vol.to(gpu), P=P,
                         out=stack[..., P + 1:])
