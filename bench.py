@@ -24,9 +24,11 @@ The same JSON line also carries the FULL grid-search wall-clock including the S4
 construction (``s4_s5_s6_wall_ms``: every PFML month's Barra Sigma, m_func, (24) Horner
 chains and (25) summands for 2 distinct g on a synthetic 500-stock universe, then S5 + S6),
 timed the same way (barrier + synchronize on both sides, max over ranks).  Multi-GPU: each
-rank builds the S4 summands of its own hp-year blocks plus the one-block validation halo
-(``search.local_month_rows``) - no per-month matrix crosses ranks.  ``--no-inputs`` skips
-it; ``--with-inputs`` makes that full pipeline the timed step itself.
+rank builds the S4 summands of the months it owns (``search.s4_compute_rows``: its burn-in
+pieces and hp-year blocks) and receives the one-block validation halo of its last year from
+the next rank by one all-gather (``search.complete_local_reals``) - every month's S4 runs
+once.  ``--no-inputs`` skips it; ``--with-inputs`` makes that full pipeline the timed step
+itself.
 """
 from __future__ import annotations
 
@@ -53,7 +55,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 import pfml  # noqa: E402
 from pfml.config import Config  # noqa: E402
-from pfml.models.search import PfmlReals, grid_search, validation_scores_all  # noqa: E402
+from pfml.models.search import (PfmlReals, complete_local_reals, grid_search,  # noqa: E402
+                                validation_scores_all)
 from pfml.ops.gemm import gemm  # noqa: E402
 from pfml.ops.ridge import _HostClock  # noqa: E402
 from pfml.parallel import collectives as coll  # noqa: E402
@@ -100,8 +103,9 @@ def one_step(reals: PfmlReals, cfg: Config, engine=None):
         s4 = run_plan(plan, cfg, defer_checks=True)
         LAST_S4.update(plan=plan, cfg=cfg, out=s4)
         out = s4.reals
-        reals = PfmlReals(months=out.months, r_tilde=out.r_tilde, denom=out.denom,
-                          all_months=all_months)
+        # this rank computed only the months it owns; the validation halo of its last hp year
+        # (the next rank's first block) arrives by one all-gather instead of a second S4
+        reals = complete_local_reals(out.r_tilde, out.denom, all_months, cfg.hp_years)
     res = grid_search(reals, cfg)
     th = _HostClock()
     out = validation_scores_all(res.obj, cfg.run.compat_mode)     # every frame, 2 launches
@@ -122,7 +126,7 @@ def engine_setup(cfg: Config, env, n_stocks: int, precision: str = "fp64"):
     layout and device copies only - the arithmetic is all in the timed step)."""
     from pfml.data.synthetic import engine_inputs
     from pfml.models.pfml_inputs import make_s4_plan
-    from pfml.models.search import local_month_rows
+    from pfml.models.search import s4_compute_rows
     from pfml.utils.dates import pfml_date_grids
     cfg.run.compat_mode = False          # distinct RFF draw per g: no Q1 duplication
     cfg.run.precision = precision
@@ -131,7 +135,7 @@ def engine_setup(cfg: Config, env, n_stocks: int, precision: str = "fp64"):
                         int(cfg.settings["pf"]["dates"]["start_year"]),
                         int(cfg.settings["pf"]["dates"]["split_years"]))
     months = g["m2"]
-    rows = local_month_rows(months, cfg.hp_years, env.world_size, env.rank)
+    rows = s4_compute_rows(months, cfg.hp_years, env.world_size, env.rank)
     plan = make_s4_plan(cfg, chars, barra, wealth, rf, env.device, months[rows])
     return (plan, months), (chars, barra, wealth, rf)
 
@@ -433,7 +437,8 @@ def main():
         finish_s4()
         full = {"s4_ms": round(ms_s4, 1), "s4_s5_s6_wall_ms": round(ms_full, 1),
                 "s4_hip_graph": repf is not None,
-                "s4_months": int(len(eng[1])), "s4_setup_s": round(setup_full, 2),
+                "s4_months": int(len(eng[1])), "s4_months_rank": int(len(eng[0].months)),
+                "s4_setup_s": round(setup_full, 2),
                 "s4_outputs_finite": bool(torch.isfinite(fbox["res"].obj).all().item())}
     prec_err = None
     if args.with_inputs and args.precision != "fp64":

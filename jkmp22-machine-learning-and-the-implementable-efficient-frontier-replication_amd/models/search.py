@@ -179,9 +179,99 @@ def owned_month_rows(all_months: np.ndarray, years: np.ndarray, world: int,
     return np.unique(np.concatenate(rows)).astype(np.int64) if rows else np.zeros(0, np.int64)
 
 
+def s4_compute_rows(all_months: np.ndarray, years: np.ndarray, world: int,
+                    rank: int) -> np.ndarray:
+    """Global rows whose S4 summands ``rank`` computes: its local rows (``local_month_rows``)
+    that it also owns.  The rest of its local rows - the validation halo of its last hp year,
+    which is the next rank's first block - arrive from their owners (``complete_local_reals``)
+    instead of being built twice: every month's S4 runs on exactly one rank."""
+    return np.intersect1d(local_month_rows(all_months, years, world, rank),
+                          owned_month_rows(all_months, years, world, rank)).astype(np.int64)
+
+
 def s4_month_counts(all_months: np.ndarray, years: np.ndarray, world: int) -> list:
     """S4 months per rank (load balance report)."""
-    return [len(local_month_rows(all_months, years, world, r)) for r in range(world)]
+    return [len(s4_compute_rows(all_months, years, world, r)) for r in range(world)]
+
+
+_HALO: dict = {}
+
+
+def _halo_layout(all_months: np.ndarray, years: np.ndarray, world: int, rank: int,
+                 dev) -> dict:
+    """Index layout of the S4 halo exchange, cached per shape (and device: the index tensors
+    are uploaded once, outside any graph capture).  Each rank sends the rows of its computed
+    months that another rank holds as halo (``send``, sorted); the sends are concatenated in
+    rank order by ONE known-size all-gather, and rank ``rank`` takes its halo rows from it
+    (``gidx``)."""
+    key = (np.asarray(all_months).tobytes(), np.asarray(years).tobytes(), world, rank, str(dev))
+    hit = _HALO.get(key)
+    if hit is not None:
+        return hit
+    loc = [local_month_rows(all_months, years, world, r) for r in range(world)]
+    comp = [s4_compute_rows(all_months, years, world, r) for r in range(world)]
+    halo = [np.setdiff1d(loc[r], comp[r]) for r in range(world)]
+    need = np.unique(np.concatenate(halo)) if world > 1 else np.zeros(0, np.int64)
+    send = [np.intersect1d(comp[r], need) for r in range(world)]
+    off = np.concatenate([[0], np.cumsum([len(s) for s in send])]).astype(np.int64)
+    gidx = []
+    for h in halo[rank]:
+        src = [s for s in range(world) if s != rank and h in set(send[s].tolist())]
+        if len(src) != 1:
+            raise ValueError(f"rank {rank}: halo month row {h} has {len(src)} senders")
+        s = src[0]
+        gidx.append(off[s] + int(np.searchsorted(send[s], h)))
+    L = loc[rank]
+
+    def tens(a):
+        return torch.as_tensor(np.asarray(a, np.int64), device=dev)
+
+    out = dict(T=len(L), counts=[len(s) for s in send],
+               pos_comp=tens(np.searchsorted(L, comp[rank])),
+               pos_halo=tens(np.searchsorted(L, halo[rank])),
+               send_in_comp=tens(np.searchsorted(comp[rank], send[rank])),
+               gidx=tens(gidx), n_halo=len(halo[rank]))
+    if len(_HALO) > 16:
+        _HALO.clear()
+    _HALO[key] = out
+    return out
+
+
+def complete_local_reals(r_c: torch.Tensor, d_c: torch.Tensor, all_months: np.ndarray,
+                         years) -> "PfmlReals":
+    """This rank's local PFML summands (``local_month_rows``: its chunks plus the validation
+    halo) from the ones it computed (``s4_compute_rows``: r_c [G, Tc, P], d_c [G, Tc, P, P]):
+    the halo months come from their owners by one known-size all-gather of the rows other
+    ranks need (~12 months x G x P x P doubles per rank over xGMI, ~50 MB at P = 513) instead
+    of a second S4 of them.  In a one-process rehearsal of a W-rank run (tools/bench_shard.py:
+    collectives are no-ops) the halo rows are zeros: the shapes are real, only the timing is
+    meaningful."""
+    all_months = np.asarray(all_months, np.int64)
+    years = np.asarray(years)
+    env = dist_env()
+    W, r = env.world_size, env.rank
+    rows_l = local_month_rows(all_months, years, W, r)
+    if W == 1:
+        return PfmlReals(months=all_months[rows_l], r_tilde=r_c, denom=d_c,
+                         all_months=all_months)
+    lay = _halo_layout(all_months, years, W, r, d_c.device)
+    G, _, P = r_c.shape
+    R = torch.empty((G, lay["T"], P), dtype=r_c.dtype, device=r_c.device)
+    D = torch.empty((G, lay["T"], P, P), dtype=d_c.dtype, device=d_c.device)
+    R.index_copy_(1, lay["pos_comp"], r_c)
+    D.index_copy_(1, lay["pos_comp"], d_c)
+    if env.is_dist:
+        sD = d_c.index_select(1, lay["send_in_comp"]).transpose(0, 1).contiguous()
+        sR = r_c.index_select(1, lay["send_in_comp"]).transpose(0, 1).contiguous()
+        gD = coll.all_gather_known(sD, lay["counts"])          # [sum sends, G, P, P]
+        gR = coll.all_gather_known(sR, lay["counts"])
+        if lay["n_halo"]:
+            D.index_copy_(1, lay["pos_halo"], gD.index_select(0, lay["gidx"]).transpose(0, 1))
+            R.index_copy_(1, lay["pos_halo"], gR.index_select(0, lay["gidx"]).transpose(0, 1))
+    elif lay["n_halo"]:
+        D.index_fill_(1, lay["pos_halo"], 0.0)
+        R.index_fill_(1, lay["pos_halo"], 0.0)
+    return PfmlReals(months=all_months[rows_l], r_tilde=R, denom=D, all_months=all_months)
 
 
 @dataclass

@@ -21,14 +21,15 @@ whose inputs changed.
 Multi-GPU (torchrun, one rank per GPU, RCCL):
   * pfml-input / pfml-search-coef: the months are cut into canonical chunks (burn-in pieces
     and groups of hp years, search.win_layout) that ranks own whole; each rank builds the S4
-    summands of ITS chunks plus the one-block validation halo (search.local_month_rows) - no
-    per-month matrix crosses ranks, the S4 months balance, and the expanding windows need one
+    summands of ITS chunks (search.s4_compute_rows) and receives the one-block validation halo
+    of its last year from the next rank by one all-gather (search.complete_local_reals) -
+    every month's S4 runs once, the S4 months balance, and the expanding windows need one
     all-gather of P x P chunk totals (bitwise the 1-rank sums), the utilities one.  Both stages
     keep per-rank artifacts and per-rank done markers: a resumed run recomputes only the
     shards whose marker is missing or stale.
-  * pfml-aim: each rank forms the aim portfolios of the OOS months whose coefficients and
-    signals it holds (year Y's validation block is Y's OOS block); the aims (N doubles per
-    month) are all-gathered.
+  * pfml-aim: each rank forms the aim portfolios of the OOS months whose signals its S4
+    built, with the coefficients of every hp year (one all-gather of the betas); the aims
+    (N doubles per month) are all-gathered.
   * pfml-best-hps: m_t of the OOS months sharded over ranks, the recursion chained across
     ranks by one N-vector hand-off (portfolio.pfml_weights); CSVs written by rank 0.
 """
@@ -169,8 +170,10 @@ class Pipeline:
         self._load_common()
         st = self.state
         m2 = st["grids"]["m2"]
-        months = m2[search.local_month_rows(m2, self.cfg.hp_years, self.env.world_size,
-                                            self.env.rank)]
+        # the months this rank's S4 computes (it owns them); its validation halo comes from
+        # the next rank below (search.complete_local_reals)
+        months = m2[search.s4_compute_rows(m2, self.cfg.hp_years, self.env.world_size,
+                                           self.env.rank)]
         if self.checkpoint and self.store.is_done("pfml-input", self._rank_key("pfml-input"),
                                                   rank=self.env.rank):
             log.info(f"[pfml-input] rank {self.env.rank}: shard up to date (resume)")
@@ -184,13 +187,14 @@ class Pipeline:
                                st["risk_free"], self.device, months=months, keep_m=keep)
         self._guard_inputs(res, months)
         st["m_oos"] = res.m_keep
-        R = res.reals
-        R = search.PfmlReals(months=months, r_tilde=R.r_tilde, denom=R.denom, all_months=m2)
+        R = search.complete_local_reals(res.reals.r_tilde, res.reals.denom, m2,
+                                        self.cfg.hp_years)
         st["reals"] = R
         st["signal_t"], st["signal_ids"], st["signal_months"] = res.signal_t, res.ids, months
         st["rff_w"] = res.rff_w
         if self.checkpoint:
-            payload = {"months": torch.as_tensor(months), "all_months": torch.as_tensor(m2),
+            payload = {"months": torch.as_tensor(R.months), "all_months": torch.as_tensor(m2),
+                       "signal_months": torch.as_tensor(months),
                        "r_tilde": R.r_tilde, "denom": R.denom,
                        "rff_w": torch.as_tensor(res.rff_w),
                        "counts": torch.as_tensor([len(x) for x in res.ids]),
@@ -258,7 +262,8 @@ class Pipeline:
             st["signal_t"] = [[t[f"sig{g}"][offs[i]:offs[i + 1]] for i in range(len(counts))]
                               for g in range(G)]
             st["signal_ids"] = [ids[offs[i]:offs[i + 1]] for i in range(len(counts))]
-            st["signal_months"] = st["reals"].months
+            st["signal_months"] = (t["signal_months"].numpy() if "signal_months" in t
+                                   else st["reals"].months)
             st["rff_w"] = t["rff_w"].numpy()
 
     def _guard_grid(self, grid) -> None:
@@ -343,13 +348,16 @@ class Pipeline:
             self._ensure_reals()
         if "beta" not in st:
             self._pfml_hp_reals_load()
-        # the OOS months whose coefficients (year oos_year, quirk Q13) live on this rank; their
-        # signals are in this rank's validation halo
+        # the OOS months whose signals this rank's S4 built (the months it owns), with the
+        # coefficients of their year (oos_year, quirk Q13) from any rank: one all-gather of the
+        # per-year betas (the signals of a month stay where S4 computed them)
+        years_b, beta_b = search.gather_beta(st["grid"])
         oos = st["grids"]["oos"]
         oos_year = month_end(oos + 1).year.to_numpy()
-        mine = oos[np.isin(oos_year, np.asarray(st["beta_years"]))]
-        local = portfolio.aim_portfolios(self.cfg, self._validation(), st["beta_years"],
-                                         st["beta"], st["signal_months"], st["signal_t"],
+        mine = oos[np.isin(oos_year, np.asarray(years_b)) &
+                   np.isin(oos, np.asarray(st["signal_months"]))]
+        local = portfolio.aim_portfolios(self.cfg, self._validation(), years_b, beta_b,
+                                         st["signal_months"], st["signal_t"],
                                          st["signal_ids"], mine)
         st["aims"] = portfolio.gather_aims(local, self.cfg, self.device)
         if self.checkpoint and self.env.is_main:

@@ -60,6 +60,21 @@ def _worker(rank, world, port, out_dir, task):
                             "vy": torch.as_tensor(res.val_year),
                             "beta": beta, "years": torch.as_tensor(years)},
                            os.path.join(out_dir, "grid.pt"))
+        elif task == "halo":
+            # S4 of the owned months only, the validation halo by the all-gather: every
+            # rank's local summands are BITWISE the rows of the one-process arrays
+            from pfml.models.search import (complete_local_reals, local_month_rows,
+                                            s4_compute_rows)
+            cfg, reals = _small_reals()
+            comp = s4_compute_rows(reals.months, cfg.hp_years, world, rank)
+            loc = local_month_rows(reals.months, cfg.hp_years, world, rank)
+            got = complete_local_reals(reals.r_tilde[:, comp].clone(),
+                                       reals.denom[:, comp].clone(), reals.months, cfg.hp_years)
+            ok = (np.array_equal(got.months, reals.months[loc])
+                  and torch.equal(got.denom, reals.denom[:, loc])
+                  and torch.equal(got.r_tilde, reals.r_tilde[:, loc]))
+            torch.save({"ok": ok, "n_comp": len(comp), "n_loc": len(loc)},
+                       os.path.join(out_dir, f"halo{rank}.pt"))
         elif task == "pipeline":
             from pfml.pipeline import Pipeline
             cfg = _PIPE_CFG[0].override([f"run.data_dir={out_dir}",
@@ -127,6 +142,37 @@ def test_local_month_rows_cover_once_plus_halo():
     m2 = np.arange(mi_from_ym(1963, 1), mi_from_ym(2023, 11) + 1)     # 731 PFML months
     cnt = np.asarray(s4_month_counts(m2, np.asarray(prod.hp_years), 8))
     assert cnt.max() / cnt.mean() <= 1.15, cnt
+
+
+def test_s4_compute_rows_partition_the_months():
+    """Every local month is computed by exactly one rank (s4_compute_rows partition the union
+    of the local rows), and a rank's halo months are computed by other ranks."""
+    from pfml.models.search import local_month_rows, s4_compute_rows
+    cfg, reals = _small_reals()
+    years = np.asarray(cfg.hp_years)
+    for world in (2, 3, 5, 8):
+        loc = [local_month_rows(reals.months, years, world, r) for r in range(world)]
+        comp = [s4_compute_rows(reals.months, years, world, r) for r in range(world)]
+        allc = np.concatenate(comp)
+        assert len(allc) == len(np.unique(allc))
+        assert set(allc.tolist()) == set(np.concatenate(loc).tolist())
+        for r in range(world):
+            halo = np.setdiff1d(loc[r], comp[r])
+            assert len(halo) <= 12
+            others = set(np.concatenate([comp[s] for s in range(world) if s != r]).tolist())
+            assert set(halo.tolist()) <= others
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_exchange_matches_local_rows(world, tmp_path):
+    _run(world, "halo", tmp_path)
+    short = 0
+    for r in range(world):
+        d = torch.load(os.path.join(tmp_path, f"halo{r}.pt"), weights_only=True)
+        assert d["ok"], (r, d)
+        assert d["n_comp"] <= d["n_loc"]
+        short += d["n_comp"] < d["n_loc"]
+    assert short >= 1                              # some rank did receive a halo
 
 
 def test_collectives_gloo(tmp_path):

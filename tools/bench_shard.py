@@ -24,12 +24,13 @@ from pfml.parallel import dist as pdist  # noqa: E402
 
 
 def with_inputs(worlds, steps: int) -> dict:
-    """Per-rank S4 (this rank's PFML months: local_month_rows, burn-in pieces + hp-year
-    blocks + a one-block halo) and its S4 + S5 + S6 step, every rank of each W in turn on
-    this one GPU (PFML_Input_Data.py:318-491 sharded by month blocks; collectives no-ops)."""
+    """Per-rank S4 (the PFML months this rank computes: s4_compute_rows, its burn-in pieces
+    and hp-year blocks; the validation halo of its last year arrives from the next rank by an
+    all-gather, zeros here) and its S4 + S5 + S6 step, every rank of each W in turn on this
+    one GPU (PFML_Input_Data.py:318-491 sharded by month blocks; collectives no-ops)."""
     from pfml.data.synthetic import engine_inputs
     from pfml.models.pfml_inputs import make_s4_plan, run_plan
-    from pfml.models.search import local_month_rows
+    from pfml.models.search import s4_compute_rows
     from pfml.utils.dates import pfml_date_grids
     dev = torch.device("cuda", 0)
     cfg = Config.default()
@@ -47,7 +48,7 @@ def with_inputs(worlds, steps: int) -> dict:
         for r in range(W):
             env = pdist.DistEnv(rank=r, world_size=W, device=dev)
             pdist.set_env(env)
-            rows = local_month_rows(months, cfg.hp_years, W, r)
+            rows = s4_compute_rows(months, cfg.hp_years, W, r)
             plan = make_s4_plan(cfg, chars, barra, wealth, rf, dev, months[rows])
             eng = (plan, months)
             # both timed forms replay as captured HIP graphs (S4's checks deferred: no host
