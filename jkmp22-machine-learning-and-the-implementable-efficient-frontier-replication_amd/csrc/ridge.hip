@@ -461,7 +461,8 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
                                              int L, double* work, double* beta_out, int64_t ldo,
                                              long long* tim, int* lu_list, int* lu_count,
                                              int lu_cap, const int* wgmap, int nwg,
-                                             unsigned* syncw, hipStream_t st);
+                                             unsigned* syncw, const int* n_host,
+                                             hipStream_t st);
 
 // Workspace per cell: enough for whichever path the launcher picks (band path: ridge_band.hip).
 extern "C" int64_t pfml_ridge_work_doubles(int n, int L) {
@@ -485,14 +486,14 @@ extern "C" hipError_t pfml_ridge_grid(const double* SD, int64_t ldS, const doubl
                                       const double* lvec, int L, double* work, double* beta_out,
                                       int64_t ldo, int* lu_list, int* lu_count, int lu_cap,
                                       const int* wgmap, int nwg, unsigned* syncw,
-                                      hipStream_t st) {
+                                      const int* n_host, hipStream_t st) {
   if (ncells <= 0) return hipSuccess;
   if (L > 128 || nmax > NMAX) return hipErrorInvalidValue;
   const CellDesc* cd = static_cast<const CellDesc*>(cells);
   if (nmax <= pfml_ridge_band_nmax())
     return pfml_ridge_band_launch(SD, ldS, Sr, cells, ncells, lvec, L, work, beta_out, ldo,
                                   g_ridge_timing, lu_list, lu_count, lu_cap, wgmap, nwg, syncw,
-                                  st);
+                                  n_host, st);
   hipLaunchKernelGGL(ridge_tridiag_blocked_kernel, dim3(ncells), dim3(NT), 0, st, SD, ldS, Sr,
                      cd, L, work);
   const int64_t nth = (int64_t)ncells * L;

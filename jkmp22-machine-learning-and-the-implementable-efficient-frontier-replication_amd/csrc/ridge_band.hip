@@ -1460,18 +1460,23 @@ __global__ __launch_bounds__(64) void ridge_band_lu_kernel(
 // re-reads its V blocks transposed through a wave-private LDS image (no barrier) and updates
 // Y_b -= V_b M.
 // ---------------------------------------------------------------------------------------
+// Row-block capacity per wave of the production shape (n <= BNMAX, 8 waves).  Cells of small n
+// take narrower instances (NWT waves x NBT blocks, ridge_band_bt_launch): their LDS (the
+// wave-private V images and the partial-P ping-pong) shrinks with the instance, so two or three
+// workgroups share a CU instead of one, and fewer waves idle (n = 65 has 5 row blocks).
 constexpr int NBW = (BNMAX / 16 + NWB - 1) / NWB;   // row blocks per wave
 
-__global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
-    const RidgeCellDesc* __restrict__ cells, int ncells, int L, double* __restrict__ work,
+template <int NWT, int NBT>
+__global__ __launch_bounds__(NWT * 64) void ridge_band_backtransform_kernel(
+    const RidgeCellDesc* __restrict__ cells, int cell0, int ncells, int L, double* __restrict__ work,
     double* __restrict__ beta_out, int64_t ldo, const unsigned* __restrict__ syncw) {
-  __shared__ double red[2][NWB][BB * BB];
-  __shared__ double Vw[NWB][NBW][BB][LS];         // wave-private V_b images (transpose)
+  __shared__ double red[2][NWT][BB * BB];
+  __shared__ double Vw[NWT][NBT][BB][LS];         // wave-private V_b images (transpose)
   // (the chunks of a cell are adjacent in dispatch order, so they run together and share
   // the cell's V panels through the caches; an XCD-grouped order measured slower)
   const int nch = (L + LC - 1) / LC;
   if ((int)blockIdx.x >= ncells * nch) return;
-  const int cell = blockIdx.x / nch, ch = blockIdx.x % nch;
+  const int cell = cell0 + (int)blockIdx.x / nch, ch = blockIdx.x % nch;
   const RidgeCellDesc cd = cells[cell];
   const int n = cd.n;
   const int lane = threadIdx.x & 63;
@@ -1486,22 +1491,22 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
   {   // padding columns [n, ldo) of this chunk's lambda rows are zero (no fill by the caller)
     const int lc = min(LC, L - l0), pad = (int)(ldo - n);
     double* __restrict__ o = beta_out + cd.out + (int64_t)l0 * ldo + n;
-    for (int e = threadIdx.x; e < lc * pad; e += NTB) o[(int64_t)(e / pad) * ldo + e % pad] = 0.0;
+    for (int e = threadIdx.x; e < lc * pad; e += NWT * 64) o[(int64_t)(e / pad) * ldo + e % pad] = 0.0;
   }
   // a cell whose cooperative reduction timed out (its error word, CoopSync) gets NaN betas:
   // the grid search's non-finite-cell recovery then recomputes it (never silent garbage)
   const bool failed = syncw != nullptr && syncw[(int64_t)cell * COOP_SYNC + 1] != 0u;
-  double4_t Y[NBW];
+  double4_t Y[NBT];
 #pragma unroll
-  for (int q = 0; q < NBW; ++q)
+  for (int q = 0; q < NBT; ++q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int i = 16 * (wid + NWB * q) + g4 + 4 * r;
+      const int i = 16 * (wid + NWT * q) + g4 + 4 * r;
       Y[q][r] = (lok && i < n) ? (failed ? __builtin_nan("") : yc[i]) : 0.0;
     }
   // va[q][r] = V_p[16 b - r0 + 4 r + g4][c16] for the live blocks b = wid + 8 q of panel p
   const int lda = band_npad(n);                   // A's leading dimension (padded)
-  double vn[NBW][4], tn[4];
+  double vn[NBT][4], tn[4];
   // Branch-free loads (the row clamped into the panel: dead blocks and rows past m read a
   // valid, cached element) and the unit-lower-triangular mask applied where the panel is
   // used: with the loads under conditions and the mask right after them, the compiler waited
@@ -1510,8 +1515,8 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
     const int k0 = p * BB, r0 = k0 + BB, m = n - r0;
     const double* Ap = A + (int64_t)r0 * lda + k0; // &V_p[0][0] (wave-uniform)
 #pragma unroll
-    for (int q = 0; q < NBW; ++q) {
-      const int b = wid + NWB * q;
+    for (int q = 0; q < NBT; ++q) {
+      const int b = wid + NWT * q;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = 16 * b - r0 + 4 * r + g4;
@@ -1527,12 +1532,12 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
   if (np > 0) fetch(np - 1);
   for (int p = np - 1; p >= 0; --p) {
     double (*rp)[BB * BB] = red[p & 1];
-    double va[NBW][4], tv[4];
+    double va[NBT][4], tv[4];
     {
       const int m = n - (p * BB + BB);
 #pragma unroll
-      for (int q = 0; q < NBW; ++q) {
-        const int b = wid + NWB * q;
+      for (int q = 0; q < NBT; ++q) {
+        const int b = wid + NWT * q;
         const bool live = b > p && b < nb;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1547,8 +1552,8 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
     // P_w = sum over live blocks of V_b^T Y_b; V_b also to the wave's LDS image
     double4_t Pp[2] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};   // two MFMA chains
 #pragma unroll
-    for (int q = 0; q < NBW; ++q) {
-      const int b = wid + NWB * q;
+    for (int q = 0; q < NBT; ++q) {
+      const int b = wid + NWT * q;
       if (b > p && b < nb) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -1566,13 +1571,13 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
     for (int r = 0; r < 4; ++r) {
       double pv = 0.0;
 #pragma unroll
-      for (int w = 0; w < NWB; ++w) pv += rp[w][(4 * r + g4) * BB + c16];
+      for (int w = 0; w < NWT; ++w) pv += rp[w][(4 * r + g4) * BB + c16];
       Mm = mfma_f64_16x16x4(tv[r], pv, Mm);
     }
     // Y_b -= V_b M   (A operand V_b[c16][4 r + g4] from the wave's own image)
 #pragma unroll
-    for (int q = 0; q < NBW; ++q) {
-      const int b = wid + NWB * q;
+    for (int q = 0; q < NBT; ++q) {
+      const int b = wid + NWT * q;
       if (b > p && b < nb) {
         double4_t acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -1584,10 +1589,10 @@ __global__ __launch_bounds__(NTB) void ridge_band_backtransform_kernel(
   if (lok) {
     double* __restrict__ out = beta_out + cd.out + (int64_t)(l0 + c16) * ldo;
 #pragma unroll
-    for (int q = 0; q < NBW; ++q)
+    for (int q = 0; q < NBT; ++q)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int i = 16 * (wid + NWB * q) + g4 + 4 * r;
+        const int i = 16 * (wid + NWT * q) + g4 + 4 * r;
         if (i < n) out[i] = Y[q][r];
       }
   }
@@ -1668,12 +1673,51 @@ extern "C" hipError_t pfml_band_qr_bench(const double* P, int m, int nblocks, in
 // Poll bound of the cooperative reduction's hand-off waits for later launches (0: default).
 extern "C" void pfml_coop_set_spin_max(unsigned n) { g_coop_spin_max = n ? n : COOP_SPIN_MAX; }
 
+namespace {
+// kernel 3 instances by cell size: (waves, row blocks per wave) with 16 NWT NBT >= n
+template <int NWT, int NBT>
+void bt_one(const RidgeCellDesc* cd, int c0, int nc, int L, double* work, double* beta_out,
+            int64_t ldo, const unsigned* syncw, hipStream_t st) {
+  const int nch = (L + LC - 1) / LC;
+  hipLaunchKernelGGL((ridge_band_backtransform_kernel<NWT, NBT>), dim3(nc * nch), dim3(NWT * 64),
+                     0, st, cd, c0, nc, L, work, beta_out, ldo, syncw);
+}
+
+int bt_class(int n) { return n <= 96 ? 0 : (n <= 192 ? 1 : (n <= 320 ? 2 : 3)); }
+
+// kernel 3 over a launch's cells: one launch per run of consecutive cells of one instance
+// class (the plan orders cells by size, ops/ridge.py ridge_plan, so a grid has one run per
+// size class).  n_host: the cells' n in plan order (host copy); nullptr = the 8-wave form for all.
+void ridge_band_bt_launch(const RidgeCellDesc* cd, const int* n_host, int ncells, int L,
+                          double* work, double* beta_out, int64_t ldo, const unsigned* syncw,
+                          hipStream_t st) {
+  if (n_host == nullptr) {
+    bt_one<NWB, NBW>(cd, 0, ncells, L, work, beta_out, ldo, syncw, st);
+    return;
+  }
+  int c0 = 0;
+  while (c0 < ncells) {
+    const int k = bt_class(n_host[c0]);
+    int c1 = c0 + 1;
+    while (c1 < ncells && bt_class(n_host[c1]) == k) ++c1;
+    switch (k) {
+      case 0: bt_one<2, 3>(cd, c0, c1 - c0, L, work, beta_out, ldo, syncw, st); break;
+      case 1: bt_one<4, 3>(cd, c0, c1 - c0, L, work, beta_out, ldo, syncw, st); break;
+      case 2: bt_one<4, 5>(cd, c0, c1 - c0, L, work, beta_out, ldo, syncw, st); break;
+      default: bt_one<NWB, NBW>(cd, c0, c1 - c0, L, work, beta_out, ldo, syncw, st); break;
+    }
+    c0 = c1;
+  }
+}
+}  // namespace
+
 extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, const double* Sr,
                                              const void* cells, int ncells, const double* lvec,
                                              int L, double* work, double* beta_out, int64_t ldo,
                                              long long* tim, int* lu_list, int* lu_count,
                                              int lu_cap, const int* wgmap, int nwg,
-                                             unsigned* syncw, hipStream_t st) {
+                                             unsigned* syncw, const int* n_host,
+                                             hipStream_t st) {
   const RidgeCellDesc* cd = static_cast<const RidgeCellDesc*>(cells);
   // the cooperative reduction: nwg workgroups (wgmap: cell << 8 | w << 4 | K - 1), the cells'
   // sync words zeroed on the stream first (a memset node under graph capture)
@@ -1699,7 +1743,6 @@ extern "C" hipError_t pfml_ridge_band_launch(const double* SD, int64_t ldS, cons
                        lu_list, lu_count, lu_cap);
   }
   const int nch = (L + LC - 1) / LC;
-  hipLaunchKernelGGL(ridge_band_backtransform_kernel, dim3(ncells * nch), dim3(NTB), 0, st, cd,
-                     ncells, L, work, beta_out, ldo, syncw);
+  ridge_band_bt_launch(cd, n_host, ncells, L, work, beta_out, ldo, syncw, st);
   return hipGetLastError();
 }

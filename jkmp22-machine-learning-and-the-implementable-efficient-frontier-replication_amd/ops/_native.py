@@ -28,7 +28,7 @@ def _declare_hip(lib):
     P, I, L, D = C.c_void_p, C.c_int, C.c_int64, C.c_double
     lib.pfml_dgemm.argtypes = [I, I, I, I, I, I, D, P, L, L, P, L, L, D, P, L, L, P, L, P, L, P]
     lib.pfml_dgemm.restype = I
-    lib.pfml_ridge_grid.argtypes = [P, L, P, P, I, I, P, I, P, P, L, P, P, I, P, I, P, P]
+    lib.pfml_ridge_grid.argtypes = [P, L, P, P, I, I, P, I, P, P, L, P, P, I, P, I, P, P, P]
     lib.pfml_ridge_grid.restype = I
     lib.pfml_ridge_work_doubles.argtypes = [I, I]
     lib.pfml_ridge_work_doubles.restype = L

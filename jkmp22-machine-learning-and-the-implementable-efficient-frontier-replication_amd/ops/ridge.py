@@ -376,8 +376,10 @@ def ridge_plan(P: int, L: int, cell_src, cell_n, cell_scale, ncu: int = 256) -> 
     wsz = wsz[order]
     desc["work"] = np.concatenate([[0], np.cumsum(wsz)[:-1]])
     wgmap = coop_wgmap(coop_k(desc["n"], ncu))
+    # host copy of n in plan order: the back-transform's instance per size class
+    n_host = np.ascontiguousarray(desc["n"], dtype=np.int32)
     return {"desc": desc, "work": int(wsz.sum()), "nmax": int(cell_n.max()), "nc": nc,
-            "wgmap": wgmap}
+            "wgmap": wgmap, "n_host": n_host}
 
 
 nat.register_hip("pfml_ridge_repair", [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int,
@@ -425,6 +427,14 @@ def repairs_done() -> int:
     return int(sum(int(c.item()) for c in LAST_REPAIRS))
 
 
+def _n_host_ptr(plan: dict):
+    """Host pointer to the plan's per-cell n (read during the launch call only);
+    PFML_BT_CLASSES=0: None, every cell on the 8-wave back-transform."""
+    if os.environ.get("PFML_BT_CLASSES", "1") == "0" or "n_host" not in plan:
+        return None
+    return plan["n_host"].ctypes.data
+
+
 def band_path(plan: dict) -> bool:
     """True when the launch takes the band path (ridge_band.hip, n <= 528), whose non-SPD
     lambdas are repaired in the band domain inside the launch; the tridiagonal path
@@ -465,7 +475,7 @@ def ridge_launch(plan: dict, d_desc: torch.Tensor, SD: torch.Tensor, Sr: torch.T
                                             d_wgmap.data_ptr() if band else None,
                                             len(plan["wgmap"]) if band else 0,
                                             sync.data_ptr() if band else None,
-                                            nat.stream_of(SD)),
+                                            _n_host_ptr(plan), nat.stream_of(SD)),
               "pfml_ridge_grid")
     return count
 
