@@ -780,9 +780,36 @@ def quad_plan(P: int, L: int, Pb: int, job_cell, job_month, job_n, job_out=None)
     order = np.lexsort((gg, rt))
     gg, rt = gg[order], rt[order]
     jobs_t = gj[gg]                                      # [ntiles, mm]
+    if len(jobs_t) and os.environ.get("PFML_QUAD_XCD", "1") != "0":
+        jobs_t, rt = _xcd_affine(jobs_t, rt, jc[jobs_t[:, 0]])
     tile_job = np.where(jobs_t >= 0, (jobs_t << 5) | rt[:, None], -1).astype(np.int32).reshape(-1)
     return {"desc": desc, "tile_job": tile_job, "nj": nj, "ntiles": len(gg),
             "nslots": int(ntile.sum()), "mm": mm}
+
+
+NXCD = 8   # MI355X: workgroup b of a launch is dispatched to XCD b mod 8
+
+
+def _xcd_affine(jobs_t: np.ndarray, rt: np.ndarray, cell: np.ndarray):
+    """Reorder a utilities launch's tiles (kept in their longest-first order per XCD) so that
+    every tile of one cell runs on XCD ``cell mod 8``: slot s of the launch goes to XCD s mod 8
+    and takes the next tile of that XCD's queue (cells numbered densely within the launch).  A cell's beta block (L x n, ~0.4 MB at
+    n = 513) is then read by its 12 months x row tiles through ONE L2 instead of all eight -
+    in launch order every XCD saw every cell, and the L2s kept re-fetching beta from HBM.
+    Queues that run dry hand their slots to the longest remaining one (the tail loses the
+    affinity, not the order)."""
+    _, x = np.unique(np.asarray(cell, np.int64), return_inverse=True)   # dense cell ranks
+    x = x.reshape(-1) % NXCD
+    queues = [list(np.nonzero(x == k)[0]) for k in range(NXCD)]
+    heads = [0] * NXCD
+    order = np.empty(len(x), dtype=np.int64)
+    for s in range(len(x)):
+        k = s % NXCD
+        if heads[k] >= len(queues[k]):
+            k = int(np.argmax([len(q) - h for q, h in zip(queues, heads)]))
+        order[s] = queues[k][heads[k]]
+        heads[k] += 1
+    return jobs_t[order], rt[order]
 
 
 def quad_launch(plan: dict, d_desc: torch.Tensor, d_tj: torch.Tensor, D: torch.Tensor,
