@@ -322,28 +322,31 @@ __device__ __forceinline__ void band_panel_hh(double* __restrict__ A, int n, int
       tk[3] += tc2 - tc1;
       tk[5] = tc2;
     }
-    double xn2 = 0.0, dc = 0.0;
+    // the wave partials summed as a depth-3 tree (not an 8-deep chain), and the column's
+    // scalars below without a branch, so the dc sum overlaps the rsq / rcp chain instead of
+    // following it (the compiler kept every instruction after a data-dependent branch behind it)
+    static_assert(NWR == 8, "tree sum of 8 wave partials");
+    double xs[NWR], ds[NWR];
 #pragma unroll
     for (int w = 0; w < NWR; ++w) {
-      xn2 += redf[par * 256 + w * 16 + j];
-      dc += redf[par * 256 + w * 16 + cq];
+      xs[w] = redf[par * 256 + w * 16 + j];
+      ds[w] = redf[par * 256 + w * 16 + cq];
     }
+    const double xn2 = ((xs[0] + xs[1]) + (xs[2] + xs[3])) + ((xs[4] + xs[5]) + (xs[6] + xs[7]));
+    const double dc = ((ds[0] + ds[1]) + (ds[2] + ds[3])) + ((ds[4] + ds[5]) + (ds[6] + ds[7]));
     const double alpha = redf[512 + par * 16 + j];
     const double vjc = redf[512 + par * 16 + cq];
-    double tau, beta, scal;
-    if (xn2 == 0.0) {
-      tau = 0.0; beta = alpha; scal = 0.0;
-    } else {
-      // beta = -sign(alpha) ||x||, tau = 1 + |alpha| / ||x||, 1 / (alpha - beta) =
-      // sign(alpha) / (|alpha| + ||x||): one rsq and one rcp chain (Newton-refined) instead
-      // of the IEEE sqrt and two divide sequences on the per-column critical path
-      const double nrm2 = fma(alpha, alpha, xn2);
-      const double rn = rsqrt_f64(nrm2);
-      const double nrm = nrm2 * rn;
-      beta = -copysign(nrm, alpha);
-      tau = fma(fabs(alpha), rn, 1.0);
-      scal = copysign(rcp_f64(fabs(alpha) + nrm), alpha);
-    }
+    // beta = -sign(alpha) ||x||, tau = 1 + |alpha| / ||x||, 1 / (alpha - beta) =
+    // sign(alpha) / (|alpha| + ||x||): one rsq and one rcp chain (Newton-refined) instead of
+    // the IEEE sqrt and two divide sequences on the per-column critical path.  xn2 = 0 (nothing
+    // below the diagonal): tau = 0, beta = alpha, scal = 0 (the chains run on a dummy 1).
+    const bool zc = xn2 == 0.0;
+    const double nrm2 = zc ? 1.0 : fma(alpha, alpha, xn2);
+    const double rn = rsqrt_f64(nrm2);
+    const double nrm = nrm2 * rn;
+    const double beta = zc ? alpha : -copysign(nrm, alpha);
+    const double tau = zc ? 0.0 : fma(fabs(alpha), rn, 1.0);
+    const double scal = zc ? 0.0 : copysign(rcp_f64(fabs(alpha) + nrm), alpha);
     // v_j' a_cq = a_cq[j] + scal sum_{i > j} x_j[i] a_cq[i] = vjc + scal dc: for cq > j the
     // update coefficient wc = tau (...), for a finished column cq < j (unscaled u_cq, factor
     // myscal) the dlarft dot G[cq][j] = v_cq' v_j = myscal (...): G = V'V comes free
