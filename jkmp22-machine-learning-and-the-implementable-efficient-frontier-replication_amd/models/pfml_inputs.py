@@ -477,10 +477,12 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
     vol = _vol_device(plan)
     range_pop()
 
-    r_out = torch.zeros((G, T, P), dtype=torch.float64, device=dev)
-    d_out = torch.zeros((G, T, P, P), dtype=torch.float64, device=dev)
-    risk_out = torch.zeros_like(d_out) if keep_risk_tc else None
-    tc_out = torch.zeros_like(d_out) if keep_risk_tc else None
+    # every (g, month) block is written by exactly one batch below (the batches partition the
+    # plan's months): no zero fill of the 3 GB denom stack in front of the batches
+    r_out = torch.empty((G, T, P), dtype=torch.float64, device=dev)
+    d_out = torch.empty((G, T, P, P), dtype=torch.float64, device=dev)
+    risk_out = torch.empty_like(d_out) if keep_risk_tc else None
+    tc_out = torch.empty_like(d_out) if keep_risk_tc else None
     signal_t = [[None] * T for _ in range(G)]
     # singular const flags (batch) and the running count (on device), one of each per stream
     nst = max(1, len(_s4_streams(dev, len(plan.batches)) or []))

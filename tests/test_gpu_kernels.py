@@ -517,6 +517,31 @@ def test_ridge_utilities_stream_groups(gpu, streams, monkeypatch):
     assert torch.allclose(go.cpu(), ro, rtol=1e-8, atol=1e-12 * ro.abs().max().item())
 
 
+def test_backtransform_size_classes(gpu, monkeypatch):
+    """The back-transform's size-class instances (2 / 4 / 4 / 8 waves for n <= 96 / 192 / 320
+    / 528, csrc/ridge_band.hip ridge_band_bt_launch) against the single 8-wave form
+    (PFML_BT_CLASSES=0) on a launch mixing all four classes: the same betas to rounding (the
+    partial sums of V'Y run over a different wave split), and both against the CPU oracle."""
+    from pfml.ops import ridge as rg
+    P = 513
+    SD = _spd_stack(2, P, n_obs=700, seed=95)
+    Sr = _rand(2, P, seed=96)
+    lv = torch.tensor([1e-4] + list(np.exp(np.linspace(-6, 6, 40))), dtype=torch.float64)
+    src = np.array([0, 1, 0, 1, 0, 1, 1])
+    nn = np.array([513, 257, 129, 65, 300, 96, 17])
+    sc = np.full(len(src), 1.5e-3)
+    out = {}
+    for v in ("0", "1"):
+        monkeypatch.setenv("PFML_BT_CLASSES", v)
+        out[v] = rg.ridge_grid(SD.to(gpu), Sr.to(gpu), src, nn, sc, lv.to(gpu)).cpu()
+    ref = rg.ridge_grid(SD, Sr, src, nn, sc, lv)
+    for v in ("0", "1"):
+        rel = ((out[v] - ref).norm(dim=-1) / ref.norm(dim=-1).clamp(min=1e-300)).max().item()
+        assert rel < 1e-9, (v, rel)
+    rel = ((out["1"] - out["0"]).norm(dim=-1) / out["0"].norm(dim=-1).clamp(min=1e-300)).max().item()
+    assert rel < 1e-12, rel
+
+
 @pytest.mark.parametrize("fmt", ["bf16", "fp8"])
 @pytest.mark.parametrize("ta,tb", [(False, False), (True, False), (False, True)])
 def test_gemm_lowp(gpu, fmt, ta, tb):
