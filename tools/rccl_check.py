@@ -49,6 +49,29 @@ def run_checks() -> dict:
     got = coll.recv_prev(z)
     ok["send_recv"] = bool(r == 0 or torch.equal(got, torch.arange(6, dtype=torch.float64,
                                                                    device=dev) + r - 1))
+    if dev.type == "cuda":
+        # a segment-wise captured step with collectives inside (parallel/graphs.py, the
+        # multi-rank bench path): replays equal the eager step, and the process group's
+        # watchdog survives the captures (no collective event on a capturing stream)
+        from pfml.parallel.graphs import SegmentedGraph
+        a = torch.randn(64, 64, dtype=torch.float64, device=dev, generator=torch.Generator(
+            device=dev).manual_seed(7))
+        res = {}
+
+        def step():
+            u = a @ a + float(r)
+            v = coll.all_gather_known(u[: counts[r]], counts)
+            res["out"] = (v @ a[:, :8]).sum(0) + coll.all_gather_known(u[:1, :3], [1] * W).sum()
+
+        step()
+        eager = res["out"].clone()
+        rep = SegmentedGraph(dev).capture(step)
+        outs = []
+        for _ in range(3):
+            rep()
+            outs.append(res["out"].clone())
+        torch.cuda.synchronize()
+        ok["segmented_capture"] = all(bool(torch.equal(o, eager)) for o in outs)
     pdist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
