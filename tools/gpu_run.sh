@@ -154,6 +154,13 @@ for step in ${MODE//,/ }; do
       # per-rank S4 + S5 + S6 of W = 1, 2, 4, 8 rank shards on this GPU (whole-node projection)
       timeout -k 10 900 python tools/bench_shard.py --with-inputs 1,2,4,8 2 > $OUT/shard_s4.json 2> $OUT/shard_s4.err
       rc=$?; cat $OUT/shard_s4.json; if [ $rc -ne 0 ]; then tail -5 $OUT/shard_s4.err; exit $rc; fi ;;
+    segtl)
+      # kernel timeline of the segmented (multi-rank form) grid step: RCCL at a forced world of
+      # one, the process group from the env (no launcher under the profiler)
+      (cd /tmp && export TMPDIR=/tmp PFML_DIST_FORCE=1 WORLD_SIZE=1 RANK=0 LOCAL_RANK=0 LOCAL_WORLD_SIZE=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29571 && timeout -k 10 300 rocprofv3 --kernel-trace -d $OUT/profseg -o run -- python3 $ROOT/bench.py --steps 3 --warmup 1 --no-inputs > $OUT/profseg.log 2>&1)
+      rc=$?; grep '^{' $OUT/profseg.log | cut -c1-200; if [ $rc -ne 0 ]; then tail -3 $OUT/profseg.log; exit $rc; fi
+      python tools/rocprof_timeline.py $(find $OUT/profseg -name "*.db" | head -1) --last 80 > $OUT/timeline_seg.txt 2>&1
+      tail -45 $OUT/timeline_seg.txt ;;
     shard)
       PFML_SHARD_GRAPH=1 timeout -k 10 300 python tools/bench_shard.py 1,2,4,8 > $OUT/shard.json 2> $OUT/shard.err
       rc=$?; cat $OUT/shard.json; if [ $rc -ne 0 ]; then tail -3 $OUT/shard.err; exit $rc; fi ;;
