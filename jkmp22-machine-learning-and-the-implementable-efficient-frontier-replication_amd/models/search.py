@@ -418,9 +418,12 @@ def window_sums(reals: "PfmlReals", su: dict) -> tuple[torch.Tensor, torch.Tenso
     totD, totR, scratch = chunk_totals(X, R, su)
     env = dist_env()
     if env.is_dist:
-        # [nlc, G, ...] chunk-major: one known-size all-gather of every rank's chunk totals
-        totD = coll.all_gather_known(totD, [c for c in su["counts"]])
-        totR = coll.all_gather_known(totR, [c for c in su["counts"]])
+        # chunk-major rows [slot][matrix totals | vector totals]: ONE known-size all-gather of
+        # every rank's chunk totals (matrices and vectors together)
+        G, P = totD.shape[1], totD.shape[-1]
+        tot = coll.all_gather_known(scratch["tot"], [c for c in su["counts"]])
+        totD = tot[:, :G * P * P].view(-1, G, P, P)
+        totR = tot[:, G * P * P:].view(-1, G, P)
     elif env.world_size > 1:
         # one-process rehearsal of a rank of a W-rank run (tools/bench_shard.py: collectives
         # are no-ops): the gathered layout with this rank's totals in its own slots and zeros

@@ -144,8 +144,13 @@ def chunk_totals(X: torch.Tensor, R: torch.Tensor, su: dict):
     Returns (totD, totR, bufs); ``bufs`` carries the segment sums to ``chunk_windows``."""
     G, T, P, _ = X.shape
     nlc, nseg, skip, nYl = su["nlc"], su["nseg"], su["skip"], su["nYl"]
-    totD = torch.empty((nlc, G, P, P), dtype=X.dtype, device=X.device)
-    totR = torch.empty((nlc, G, P), dtype=X.dtype, device=X.device)
+    # matrix and vector totals of a chunk side by side in ONE row of one buffer (``bufs["tot"]``,
+    # [nlc, G P P + G P]): the multi-rank path all-gathers them as one collective; totD / totR
+    # are row-strided views and the kernels take that row stride
+    GPP = G * P * P
+    tot = torch.empty((nlc, GPP + G * P), dtype=X.dtype, device=X.device)
+    totD = tot[:, :GPP].view(nlc, G, P, P)
+    totR = tot[:, GPP:].view(nlc, G, P)
     out = torch.empty((G, nYl, P, P), dtype=X.dtype, device=X.device)
     if nat.is_device(X):
         if X.dtype != torch.float64 or not X.is_contiguous():
@@ -158,12 +163,12 @@ def chunk_totals(X: torch.Tensor, R: torch.Tensor, su: dict):
         nat.check(lib.pfml_wsum_chunk_totals(
             X.data_ptr(), P, T, G, st.data_ptr(), sp.data_ptr(), nseg, skip, out.data_ptr(),
             scratch.data_ptr() if scratch is not None else None, nlc, idx.data_ptr(),
-            totD.data_ptr(), G * P * P, s), "pfml_wsum_chunk_totals")
+            totD.data_ptr(), totD.stride(0), s), "pfml_wsum_chunk_totals")
         nat.check(lib.pfml_wvec_chunk(
             R.data_ptr(), P, T, G, st.data_ptr(), sp.data_ptr(), nseg, skip, 0, nlc,
-            idx.data_ptr(), su["layout"].C, cidx.data_ptr(), su["clast"], totR.data_ptr(), G * P,
-            None, s), "pfml_wvec_chunk")
-        return totD, totR, {"out": out, "scratch": scratch}
+            idx.data_ptr(), su["layout"].C, cidx.data_ptr(), su["clast"], totR.data_ptr(),
+            totR.stride(0), None, s), "pfml_wvec_chunk")
+        return totD, totR, {"out": out, "scratch": scratch, "tot": tot}
     segD = [_fold_months(X, a, b) for a, b in zip(su["st"], su["sp"])]
     segR = [_fold_months(R, a, b) for a, b in zip(su["st"], su["sp"])]
     for lc in range(nlc):
@@ -172,7 +177,7 @@ def chunk_totals(X: torch.Tensor, R: torch.Tensor, su: dict):
             accD = accD + segD[s]
             accR = accR + segR[s]
         totD[lc], totR[lc] = accD, accR
-    return totD, totR, {"out": out, "segD": segD, "segR": segR}
+    return totD, totR, {"out": out, "segD": segD, "segR": segR, "tot": tot}
 
 
 def chunk_windows(X: torch.Tensor, R: torch.Tensor, su: dict, totD: torch.Tensor,
@@ -196,13 +201,17 @@ def chunk_windows(X: torch.Tensor, R: torch.Tensor, su: dict, totD: torch.Tensor
         lib = nat.hip_lib()
         s = nat.stream_of(X)
         scratch = bufs["scratch"]
+        # (row-strided totals: each slot's G blocks contiguous, the slots totD.stride(0) apart)
+        if totD.stride()[1:] != (P * P, P, 1) or totR.stride()[1:] != (P, 1):
+            raise ValueError("chunk_windows: chunk totals must be row-strided [slot][g] blocks")
         nat.check(lib.pfml_wsum_chunk_prefix(
             P, G, nseg, skip, out.data_ptr(), scratch.data_ptr() if scratch is not None else None,
-            C, cidx.data_ptr(), totD.data_ptr(), G * P * P, clast, s), "pfml_wsum_chunk_prefix")
+            C, cidx.data_ptr(), totD.data_ptr(), totD.stride(0), clast, s),
+            "pfml_wsum_chunk_prefix")
         nat.check(lib.pfml_wvec_chunk(
             R.data_ptr(), P, T, G, st.data_ptr(), sp.data_ptr(), nseg, skip, 1, 0,
-            idx.data_ptr(), C, cidx.data_ptr(), clast, totR.data_ptr(), G * P, Sr.data_ptr(), s),
-            "pfml_wvec_chunk")
+            idx.data_ptr(), C, cidx.data_ptr(), clast, totR.data_ptr(), totR.stride(0),
+            Sr.data_ptr(), s), "pfml_wvec_chunk")
         return out, Sr
     segD, segR = bufs["segD"], bufs["segR"]
     pD, pR = torch.zeros_like(X[:, 0]), torch.zeros_like(R[:, 0])

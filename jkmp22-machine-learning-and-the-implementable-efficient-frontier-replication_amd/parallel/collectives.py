@@ -90,6 +90,14 @@ def _all_gather_known_into(out: torch.Tensor | None, x: torch.Tensor, counts) ->
     m = max(counts)
     if m == 0:
         return x
+    if min(counts) == m and not _staged(x):
+        # equal shares (e.g. the chunk totals when the chunks split evenly over the ranks):
+        # the rank-order concatenation IS the all-gather output - gathered straight into the
+        # (static) destination, no padding, no concatenation, no copy
+        if out is None:
+            out = torch.empty((e.world_size * m, *x.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, x.contiguous())
+        return out
     pad = x.contiguous()
     if x.shape[0] < m:
         pad = torch.zeros((m, *x.shape[1:]), dtype=x.dtype, device=x.device)
