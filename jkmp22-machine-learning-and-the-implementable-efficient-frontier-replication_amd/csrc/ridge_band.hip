@@ -580,6 +580,37 @@ __device__ __forceinline__ void coop_x_accum(const double* __restrict__ A, int l
   for (; k < m; k += 32) chunk(k, std::integral_constant<int, 4>{});
 }
 
+// Trailing-update rows of each wave at K = 1, per number of live row blocks nI: row I holds
+// the tiles J = 1..I (row 0: the diagonal band tile), i.e. max(1, ceil(I / TBR)) chunks of TBR
+// tiles, and the rows go to the waves longest-first, each to the least-loaded wave (LPT).  The
+// fixed snake (w, 15 - w, 16 + w, 31 - w) balanced only nI = 32: as the panels advance, the
+// rows >= nI it drops are the long ones of the low waves, and the K = 1 update waited up to 2x
+// on its slowest wave (wave 0 idle ~14 % of a cell's cycles at the barrier after the update).
+// Which wave updates a tile does not change its arithmetic: the same bits.
+constexpr int UPD_RMAX = 8;
+constexpr int UPD_NI = BNMAX / BB + 2;
+struct UpdRows {
+  signed char r[UPD_NI][NWR][UPD_RMAX];
+};
+constexpr UpdRows make_upd_rows() {
+  UpdRows t{};
+  for (int nI = 0; nI < UPD_NI; ++nI) {
+    int load[NWR] = {}, cnt[NWR] = {};
+    for (int w = 0; w < NWR; ++w)
+      for (int k = 0; k < UPD_RMAX; ++k) t.r[nI][w][k] = -1;
+    for (int I = nI - 1; I >= 0; --I) {
+      const int c = I == 0 ? 1 : (I + TBR - 1) / TBR;
+      int best = -1;
+      for (int w = 0; w < NWR; ++w)
+        if (cnt[w] < UPD_RMAX && (best < 0 || load[w] < load[best])) best = w;
+      t.r[nI][best][cnt[best]++] = (signed char)I;
+      load[best] += c;
+    }
+  }
+  return t;
+}
+__constant__ UpdRows kUpdRows = make_upd_rows();
+
 template <bool TIMED>
 __global__ __launch_bounds__(NTR) void band_coop_kernel(
     const double* __restrict__ SD, int64_t ldS, const double* __restrict__ Sr,
@@ -856,7 +887,14 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
       // TBR tiles per chunk, next chunk's tiles loaded before this chunk's MFMAs (the
       // one-workgroup kernel's trailing loop; stores through the buffer descriptor)
       const int first_u = ((wu - (p + 1)) % Ku + Ku) % Ku;
+      // K = 1: the LPT table (kUpdRows); K > 1: the snake over the waves of this workgroup's
+      // rows first_u + pos Ku.  A row >= nI ends the wave's list.
+      const int RR = (K == 1) ? UPD_RMAX : 4;
       auto row_of = [&](int rr) {
+        if (K == 1) {
+          const int r = (rr < UPD_RMAX) ? (int)kUpdRows.r[nI][wid][rr] : -1;
+          return r < 0 ? nI : r;
+        }
         const int pos = 2 * NWR * (rr >> 1) + ((rr & 1) ? (2 * NWR - 1 - wid) : wid);
         return first_u + pos * Ku;
       };
@@ -873,15 +911,15 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
         }
       };
       int rr = 0, I = row_of(0);
-      while (rr < 4 && I >= nI) I = row_of(++rr);
-      if (rr >= 4) I = nI;
+      while (rr < RR && I >= nI) I = row_of(++rr);
+      if (rr >= RR) I = nI;
       int J0 = (I == 0) ? 0 : 1;
       auto advance = [&]() {
         J0 += TBR;
         if (J0 > I) {
           do I = row_of(++rr);
-          while (rr < 4 && I >= nI);
-          if (rr >= 4) I = nI;
+          while (rr < RR && I >= nI);
+          if (rr >= RR) I = nI;
           J0 = (I == 0) ? 0 : 1;
         }
       };
@@ -1015,6 +1053,7 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
       update();
       COOP_TMARK(5)
       __syncthreads();
+      COOP_TMARK(3)                                  // (timing: wave 0 waiting for the update)
       if (p + 1 < npan) lookahead();
       COOP_TMARK(6)
     } else if (qwg) {
