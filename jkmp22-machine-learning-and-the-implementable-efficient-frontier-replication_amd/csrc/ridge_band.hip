@@ -887,16 +887,14 @@ __global__ __launch_bounds__(NTR) void band_coop_kernel(
       // TBR tiles per chunk, next chunk's tiles loaded before this chunk's MFMAs (the
       // one-workgroup kernel's trailing loop; stores through the buffer descriptor)
       const int first_u = ((wu - (p + 1)) % Ku + Ku) % Ku;
-      // K = 1: the LPT table (kUpdRows); K > 1: the snake over the waves of this workgroup's
-      // rows first_u + pos Ku.  A row >= nI ends the wave's list.
-      const int RR = (K == 1) ? UPD_RMAX : 4;
+      // this workgroup's rows first_u + u Ku (u < nu) go to its waves by the LPT table of nu
+      // rows (kUpdRows: K = 1 exactly; K > 1 the costs ceil((first_u + u Ku) / TBR) grow
+      // linearly in u as the table's do).  A row >= nI ends the wave's list.
+      constexpr int RR = UPD_RMAX;
+      const int nu = (first_u < nI) ? (nI - first_u + Ku - 1) / Ku : 0;
       auto row_of = [&](int rr) {
-        if (K == 1) {
-          const int r = (rr < UPD_RMAX) ? (int)kUpdRows.r[nI][wid][rr] : -1;
-          return r < 0 ? nI : r;
-        }
-        const int pos = 2 * NWR * (rr >> 1) + ((rr & 1) ? (2 * NWR - 1 - wid) : wid);
-        return first_u + pos * Ku;
+        const int r = (rr < UPD_RMAX) ? (int)kUpdRows.r[nu][wid][rr] : -1;
+        return r < 0 ? nI : first_u + r * Ku;
       };
       double4_t nxt[TBR];
       auto fetch = [&](int I, int J0) {
