@@ -14,6 +14,8 @@
 #   stressprof kernel stats of the stress    prec bf16 / fp8 S4 GEMMs (BASELINE config 5)  pmc     PMC counters of one grid step
 #   shards4    per-rank S4 + grid step of W = 1 / 2 / 4 / 8 rank shards on this GPU
 #   multiproc  2, 4 and 8 ranks sharing the GPU (gloo), utilities bitwise vs 1 rank
+#   rccl1      RCCL collectives + segmented-capture check and the distributed bench at a forced world of one
+#   segtl      kernel timeline of the segmented (multi-rank form) grid step under RCCL at world one
 set -o pipefail
 TAG=${1:-r03}
 MODE=${2:-suite}
