@@ -35,13 +35,46 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import logging
 
-import numpy as np
-import torch
+def _rank_launch() -> None:
+    """``--gpus N`` is authoritative.  Run without a launcher (no WORLD_SIZE) and N > 1, this
+    process starts N ranks itself - ``torch.distributed.run`` as a CHILD process, before any
+    GPU call and before the engine is imported - and exits with its code (rank 0 prints the
+    one JSON line).  Under a launcher whose WORLD_SIZE differs from N it refuses to run: a
+    1-rank measurement can never be reported as an N-GPU point, nor the other way round."""
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    n = ap.parse_known_args()[0].gpus
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != n:
+            sys.stderr.write(f"bench.py: --gpus {n} but the launcher started WORLD_SIZE={ws} "
+                             f"ranks; run with matching --gpus (or without a launcher)\n")
+            sys.exit(2)
+        return
+    if n <= 1:
+        return
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+           str(n), "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__), *sys.argv[1:]]
+    sys.exit(subprocess.call(cmd))
+
+
+if __name__ == "__main__":
+    _rank_launch()
+
+import logging  # noqa: E402
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 # the engine's stage logs go to stderr here: stdout carries the one JSON result line only
 if not logging.getLogger("pfml").handlers:
@@ -70,7 +103,11 @@ METRIC = "PFML hp×window solves/sec (whole node); full grid-search wall-clock, 
 
 
 def synthetic_reals(cfg: Config, device, n_months: int = 710, n_stocks: int = 500,
-                    seed: int = 0) -> PfmlReals:
+                    seed: int = 0, collinear: int = 0) -> PfmlReals:
+    """``collinear = R > 0``: X_t = Z_t B_g' with a fixed per-g basis B_g (P x R), so EVERY
+    expanding window sum has rank <= R: the cells with p + 1 > R are exactly singular at
+    lambda = 0 - the reference's np.linalg.solve on collinear RFF summands
+    (PFML_Search_Coef.py:131-133, General_functions.py:81) - and go through the device repair."""
     G = len(cfg.g_vec)
     P = cfg.p_max + 1
     last = mi_from_ym(int(cfg.hp_years.max()), 11)
@@ -81,9 +118,18 @@ def synthetic_reals(cfg: Config, device, n_months: int = 710, n_stocks: int = 50
     chunk = 32
     for g in range(G):
         gen.manual_seed(seed * 1000 + g)
+        Bg = None
+        if collinear:
+            Bg = torch.randn((P, collinear), generator=gen, dtype=torch.float64,
+                             device=device) / collinear ** 0.5
         for a in range(0, n_months, chunk):
             b = min(n_months, a + chunk)
-            X = torch.randn((b - a, n_stocks, P), generator=gen, dtype=torch.float64, device=device)
+            if Bg is None:
+                X = torch.randn((b - a, n_stocks, P), generator=gen, dtype=torch.float64,
+                                device=device)
+            else:
+                X = torch.randn((b - a, n_stocks, collinear), generator=gen,
+                                dtype=torch.float64, device=device) @ Bg.T
             gemm(X, X, trans_a=True, alpha=1.0 / n_stocks, out=denom[g, a:b], backend="own")
             del X
         r[g] = 0.05 * torch.randn((n_months, P), generator=gen, dtype=torch.float64, device=device)
@@ -319,6 +365,10 @@ def main():
                     help="synthetic denom_t of rank <= NT per month (X_t: NT x P, so early "
                          "expanding windows are singular at lambda = 0 and exercise the device "
                          "LU repair of the band path); reports the repair count")
+    ap.add_argument("--collinear", type=int, default=0, metavar="R",
+                    help="synthetic summands whose every expanding window has rank <= R (a "
+                         "fixed per-g basis): the cells with p + 1 > R are singular at lambda "
+                         "= 0 and are repaired on the device (reported as 'repairs')")
     ap.add_argument("--dump", default="",
                     help="rank 0 saves the gathered utilities of the last step here (tests)")
     ap.add_argument("--no-inputs", action="store_true",
@@ -358,7 +408,8 @@ def main():
         reals = None
     else:
         reals = synthetic_reals(cfg, dev, n_months=args.months,
-                                n_stocks=args.rank_deficient or args.stocks)
+                                n_stocks=args.rank_deficient or args.stocks,
+                                collinear=args.collinear)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t_setup = time.perf_counter() - t_setup
@@ -386,13 +437,12 @@ def main():
     value = n_solves / (ms / 1000.0)
     # sanity: finite outputs; device repairs (non-SPD ridge systems) of the last step
     finite = bool(torch.isfinite(res.obj).all().item())
-    from pfml.ops.ridge import repairs_done
+    from pfml.ops.ridge import coop_errors, repairs_done
     from pfml.utils.log import COUNTERS
     repairs = repairs_done() if dev.type == "cuda" else 0
     if dev.type == "cuda":
         # cooperative hand-off timeouts of the last step (NaN betas: a production run's S5
         # guard recomputes those cells, pipeline._guard_grid); counted, never silent
-        from pfml.ops.ridge import coop_errors
         nto = coop_errors()
         if nto:
             COUNTERS.add("ridge.coop_timeouts", nto)
@@ -418,9 +468,13 @@ def main():
             sbox["out"] = run_plan(eng[0], cfg_full, defer_checks=True)
 
         # S4 alone and S4 + S5 + S6, each replayed as a HIP graph (segments between the
-        # collectives on several ranks) unless --no-graph; one graph alive at a time
+        # collectives on several ranks) unless --no-graph; one graph alive at a time; each
+        # the median of >= 3 individually timed replays (min / max reported too)
+        n_rep = 1 if args.tiny else 3
         rep4 = graphed(s4_step, dev) if (args.graph and dev.type == "cuda") else None
-        ms_s4 = timed(rep4 or s4_step, 1, 1, dev)
+        fn4 = rep4 or s4_step
+        fn4()
+        t_s4 = [timed(fn4, 1, 0, dev) for _ in range(n_rep)]
         finish_inputs(eng[0], cfg_full, sbox["out"])
         del rep4, sbox
         if dev.type == "cuda":
@@ -433,9 +487,30 @@ def main():
         repf = None
         if args.graph and dev.type == "cuda":
             repf = segmented(full_step, dev) if env.is_dist else graphed(full_step, dev)
-        ms_full = timed(repf or full_step, max(1, min(args.steps, 2)), 1, dev)
+        fnf = repf or full_step
+        fnf()
+        t_full = [timed(fnf, 1, 0, dev) for _ in range(n_rep)]
+        ms_full = float(np.median(t_full))
+        # repairs / fallbacks of the S4-FED grid (the only grid built from real PFML
+        # summands): ridge band-LU repairs of its last step, m_func repairs and singular
+        # consts of its S4 (counted by finish_inputs), cooperative timeouts
+        c0 = dict(COUNTERS.as_dict())
+        s4_rep = repairs_done() if dev.type == "cuda" else 0
         finish_s4()
-        full = {"s4_ms": round(ms_s4, 1), "s4_s5_s6_wall_ms": round(ms_full, 1),
+        if dev.type == "cuda":
+            nto = coop_errors()
+            if nto:
+                COUNTERS.add("ridge.coop_timeouts", nto)
+        c1 = COUNTERS.as_dict()
+        s4_fb = {k: v - c0.get(k, 0) for k, v in c1.items() if v != c0.get(k, 0)}
+        full = {"s4_ms": round(float(np.median(t_s4)), 1),
+                "s4_ms_min": round(min(t_s4), 1), "s4_ms_median": round(float(np.median(t_s4)), 1),
+                "s4_ms_max": round(max(t_s4), 1),
+                "s4_s5_s6_wall_ms": round(ms_full, 1),
+                "s4_s5_s6_wall_ms_min": round(min(t_full), 1),
+                "s4_s5_s6_wall_ms_max": round(max(t_full), 1),
+                "s4_replays": n_rep,
+                "s4_repairs": int(s4_rep), "s4_fallbacks": s4_fb,
                 "s4_hip_graph": repf is not None,
                 "s4_months": int(len(eng[1])), "s4_months_rank": int(len(eng[0].months)),
                 "s4_setup_s": round(setup_full, 2),
@@ -455,6 +530,9 @@ def main():
             "value": round(value, 1),
             "unit": "solves/s",
             "n_gpus": env.world_size,
+            "world_size": (torch.distributed.get_world_size() if env.is_dist else 1),
+            "nccl_ranks": (torch.distributed.get_world_size()
+                           if env.is_dist and env.backend == "nccl" else 0),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
@@ -480,6 +558,7 @@ def main():
                 "ridge_solve_dtype": "fp64 (lambda = 0 / rank-deficient systems: bf16 cannot "
                                      "carry them, SURVEY 7.4)",
                 "rank_deficient_nt": args.rank_deficient or None,
+                "collinear_rank": args.collinear or None,
                 "hip_graph": use_graph,
             },
             "repairs": repairs,
@@ -489,6 +568,11 @@ def main():
             rec["data"] = (f"synthetic rank-deficient summands: denom_t = X_t'X_t/NT with X_t "
                            f"~ N(0,1) of shape {args.rank_deficient} x 513 (rank <= "
                            f"{args.rank_deficient} per month), {args.months} months")
+        if args.collinear:
+            rec["data"] = (f"synthetic collinear summands: X_t = Z_t B_g' with a fixed P x "
+                           f"{args.collinear} basis per g (every window rank <= "
+                           f"{args.collinear}: cells with p + 1 > {args.collinear} singular at "
+                           f"lambda = 0), {args.months} months")
         if full is not None:
             rec.update(full)
             rec["full_vs_baseline"] = round(BASELINE_FULL_S / (full["s4_s5_s6_wall_ms"] / 1000.0), 1)

@@ -668,12 +668,54 @@ extern "C" int pfml_gemm_epi_size() { return (int)sizeof(PfmlGemmEpi); }
 #define PFML_SYM_CFG 7
 #endif
 
+static hipError_t dgemm_chunk(int ta, int tb, int M, int N, int K, int batch,
+                              const double* A, int64_t lda, int64_t sA,
+                              const double* B, int64_t ldb, int64_t sB,
+                              double* C, int64_t ldc, int64_t sC,
+                              const PfmlGemmEpi* h, hipStream_t st);
+
+// 2 GB buffer-store limit per C batch entry (store_tile): larger outputs are split into row
+// chunks on the host - every row-indexed operand (A's rows, the row / output / addend scales,
+// the diagonal vector, the addend or its gathered row index, Ct's columns) is offset by the
+// chunk's first row, the diagonal's column origin moves with it.  Not splittable: the
+// symmetric mode (mirror stores cross chunks) and a transposed output that is itself >= 2 GB.
 extern "C" hipError_t pfml_dgemm_ex(int ta, int tb, int M, int N, int K, int batch,
                                     const double* A, int64_t lda, int64_t sA,
                                     const double* B, int64_t ldb, int64_t sB,
                                     double* C, int64_t ldc, int64_t sC,
                                     const PfmlGemmEpi* h, hipStream_t st) {
   if (M <= 0 || N <= 0 || batch <= 0) return hipSuccess;
+  const int64_t lim = (int64_t)1 << 31;
+  if (((int64_t)(M - 1) * ldc + N) * 8 < lim)
+    return dgemm_chunk(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, h, st);
+  if (h->sym || ldc <= 0) return hipErrorInvalidValue;
+  // rows per chunk: a multiple of 128 (tile height; keeps A's and the vectors' 16-B alignment)
+  int64_t rows = ((lim / 8 - N) / ldc) / 128 * 128;
+  if (rows < 128) return hipErrorInvalidValue;
+  for (int64_t m0 = 0; m0 < M; m0 += rows) {
+    const int mc = (int)std::min<int64_t>(rows, M - m0);
+    PfmlGemmEpi e = *h;
+    if (e.rs) e.rs += m0;
+    if (e.es) e.es += m0;
+    if (e.dv) e.dv += m0;
+    if (e.os) e.os += m0;
+    if (e.erow) e.erow += m0;
+    else if (e.E) e.E += m0 * e.lde;
+    if (e.Ct) e.Ct += m0;
+    e.diag_col0 += (int)m0;
+    const double* Ac = ta ? A + m0 : A + m0 * lda;
+    const hipError_t err = dgemm_chunk(ta, tb, mc, N, K, batch, Ac, lda, sA, B, ldb, sB,
+                                       C + m0 * ldc, ldc, sC, &e, st);
+    if (err != hipSuccess) return err;
+  }
+  return hipSuccess;
+}
+
+static hipError_t dgemm_chunk(int ta, int tb, int M, int N, int K, int batch,
+                              const double* A, int64_t lda, int64_t sA,
+                              const double* B, int64_t ldb, int64_t sB,
+                              double* C, int64_t ldc, int64_t sC,
+                              const PfmlGemmEpi* h, hipStream_t st) {
   Epi ep{h->alpha, h->beta, h->rs, h->srs, h->cs, h->scs, h->ks, h->sks, h->E, h->lde, h->sE,
          h->e_cols, h->diag_col0, h->dval, h->dv, h->sdv, h->has_diag, h->es, h->ses,
          h->sincos, h->sym, h->Ct, h->ldct, h->sCt, h->erow, h->serow, h->ecm, h->ecs,
@@ -701,7 +743,7 @@ extern "C" hipError_t pfml_dgemm_ex(int ta, int tb, int M, int N, int K, int bat
     const bool ok = !h->sincos && M >= 2 && N >= 2 && K >= 2 && a_cont % 2 == 0 &&
                     b_cont % 2 == 0 && lda % 2 == 0 && ldb % 2 == 0 && sA % 2 == 0 &&
                     sB % 2 == 0 && aligned16(A) && aligned16(B) &&
-                    (!ep.ks || (aligned16(ep.ks) && ep.sks % 2 == 0));
+                    (!ep.ks || (aligned16(ep.ks) && ep.sks % 2 == 0 && K % 2 == 0));
     if (ok) {
       if (cfg == 6)
         return launch_glds<128, 128>(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC,

@@ -709,6 +709,7 @@ def finish_inputs(plan: S4Plan, cfg: Config, out: PfmlInputs) -> PfmlInputs:
     if pend["mstat"] is not None:
         bad = torch.nonzero(pend["mstat"]).flatten().cpu().numpy()
         if len(bad):
+            COUNTERS.add("pfml_inputs.mfunc_repaired_months", len(bad))
             keep = None
             if out.m_keep is not None:
                 keep = np.intersect1d(out.m_keep["months"], plan.months[bad])

@@ -79,7 +79,9 @@ def _ledger(ta, tb, M, N, K, batch, A3, B3, C3, ks=None, sks=0, sincos=False, cf
            and sa % 2 == 0 and sb % 2 == 0 and A3.data_ptr() % 16 == 0
            and B3.data_ptr() % 16 == 0
            and (ks is None or (ks.data_ptr() % 16 == 0 and sks % 2 == 0)))
-    if cfg in (6, 7, 8, 9, 10, 11) and not (vec and not sincos and min(M, N, K) >= 2):
+    # the LDS-DMA forms load the k-scale in 16-byte pairs: they also need an even K
+    if cfg in (6, 7, 8, 9, 10, 11) and not (vec and not sincos and min(M, N, K) >= 2 and
+                                            (ks is None or K % 2 == 0)):
         cfg = 3
     bm, bn = {1: (128, 128), 2: (128, 64), 6: (128, 128), 8: (128, 64), 9: (128, 128),
               10: (128, 64), 11: (128, 128)}.get(cfg, (64, 64))

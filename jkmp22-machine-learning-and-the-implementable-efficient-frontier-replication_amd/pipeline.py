@@ -76,6 +76,8 @@ _DEPS = {
 }
 # stages whose artifacts are per rank (resume per shard)
 _SHARDED = ("pfml-input", "pfml-search-coef")
+# per-rank artifact payload versions (part of the done-marker key)
+_FORMAT = {"pfml-input": 2}
 
 
 class Pipeline:
@@ -122,7 +124,9 @@ class Pipeline:
         return self.state
 
     def _rank_key(self, st: str) -> str:
-        return f"{self._keys[st]}|w{self.env.world_size}"
+        # payload format versions: a shard written by an older layout (pfml-input before
+        # "signal_months" was stored) is stale and recomputed, never reinterpreted
+        return f"{self._keys[st]}|w{self.env.world_size}|v{_FORMAT.get(st, 1)}"
 
     def _all_done(self, st: str) -> bool:
         """Resume decision, identical on every rank (stages contain collectives)."""
@@ -178,6 +182,15 @@ class Pipeline:
                                                   rank=self.env.rank):
             log.info(f"[pfml-input] rank {self.env.rank}: shard up to date (resume)")
             self._ensure_reals()
+            if self.env.world_size > 1:
+                # another rank's shard is being recomputed (else the stage would have been
+                # skipped): its halo exchange is a collective, so this rank joins it with the
+                # rows it computed, taken from its loaded local rows
+                R = st["reals"]
+                pos = torch.as_tensor(np.searchsorted(R.months, months), device=R.denom.device)
+                st["reals"] = search.complete_local_reals(
+                    R.r_tilde.index_select(1, pos), R.denom.index_select(1, pos), m2,
+                    self.cfg.hp_years)
             return
         # S9 reuses S4's m_tilde of the OOS months this rank owns (PFML_best_hps.py:185-190
         # recomputes exactly these m_t)

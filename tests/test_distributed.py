@@ -214,6 +214,51 @@ def test_bench_contract_two_ranks_gloo(tmp_path):
     assert rec["value"] > 0 and rec["config"]["outputs_finite"]
 
 
+def test_bench_gpus_flag_spawns_ranks(tmp_path):
+    """``bench.py --gpus 2`` WITHOUT a launcher starts the two ranks itself: the
+    record says n_gpus 2 / dp2 / world_size 2, and the gathered utilities are bitwise those of
+    the one-rank run."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="1", PYTHONPATH=root)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    common = [sys.executable, os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "0",
+              "--tiny", "--device", "cpu", "--no-inputs"]
+    recs = {}
+    for n in (1, 2):
+        r = subprocess.run([*common, "--gpus", str(n), "--dump", str(tmp_path / f"w{n}.pt")],
+                           capture_output=True, text=True, timeout=600, env=env,
+                           cwd=str(tmp_path))
+        assert r.returncode == 0, r.stderr[-3000:]
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        assert len(lines) == 1, r.stdout
+        recs[n] = json.loads(lines[0])
+    assert recs[2]["n_gpus"] == 2 and recs[2]["world_size"] == 2
+    assert recs[2]["config"]["parallelism"] == "dp2"
+    assert recs[1]["n_gpus"] == 1 and recs[1]["config"]["parallelism"] == "dp1"
+    a = torch.load(tmp_path / "w1.pt", weights_only=True)
+    b = torch.load(tmp_path / "w2.pt", weights_only=True)
+    assert torch.equal(a["val_months"], b["val_months"])
+    assert torch.equal(a["obj"], b["obj"])                      # bitwise
+
+
+def test_bench_gpus_mismatch_fails():
+    """A launcher whose WORLD_SIZE differs from --gpus is refused (non-zero exit, a message),
+    before any work is done."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "1",
+                        "--tiny", "--device", "cpu"], capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=2" in r.stderr, (r.returncode, r.stderr[-2000:])
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
 def test_bench_with_inputs_two_ranks_equals_one(tmp_path):
     """bench.py --with-inputs: each rank builds the S4 summands of its own hp-year blocks +
     validation halo only; the gathered utilities equal the single-process run."""
@@ -278,6 +323,37 @@ def test_pipeline_sharded_matches_single(world, start, small_data, tmp_path):
     for st in ("pfml-input", "pfml-search-coef"):
         for r in range(world):
             assert os.path.exists(os.path.join(d2, "art", st, f"_DONE.rank{r}.json"))
+
+
+@pytest.mark.timeout(600)
+def test_pipeline_partial_resume_two_ranks(small_data, tmp_path):
+    """Resume of a 2-rank run where ONE rank's pfml-input marker is gone: the rank
+    whose shard is up to date still joins the halo all-gather of the rank that recomputes (no
+    deadlock) and the resumed run writes the CSVs of the uninterrupted one, bitwise."""
+    from pfml.parallel import dist as pdist
+    base = small_data.override(["pf.dates.start_year=1999", "pf.dates.end_yr=2012",
+                                "pf.dates.split_years=3"])
+    d = str(tmp_path / "wn")
+    _copy_inputs(small_data.run.data_dir, d)
+    pdist.set_env(None)
+    _PIPE_CFG[:] = [base]
+    _run(2, "pipeline", d)
+    first = {}
+    for name in ("validation.csv", "weights.csv", "pf.csv", "pf_summary.csv"):
+        with open(os.path.join(d, name)) as f:
+            first[name] = f.read()
+        os.remove(os.path.join(d, name))
+    # rank 1's S4 shard is stale; every later stage's marker too (they re-run on the resume)
+    os.remove(os.path.join(d, "art", "pfml-input", "_DONE.rank1.json"))
+    for st in _PIPE_STAGES[1:]:
+        art = os.path.join(d, "art", st)
+        for n in (os.listdir(art) if os.path.isdir(art) else []):
+            if n.startswith("_DONE"):
+                os.remove(os.path.join(art, n))
+    _run(2, "pipeline", d)
+    for name, txt in first.items():
+        with open(os.path.join(d, name)) as f:
+            assert f.read() == txt, name
 
 
 @pytest.mark.parametrize("fault", ["pfml-search-coef", "pfml-best-hps"])

@@ -64,7 +64,8 @@ def test_gemm_epi_struct_matches():
 
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 @pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
-@pytest.mark.parametrize("shape", [(2, 37, 53, 29), (3, 130, 258, 100), (2, 96, 224, 96)])
+@pytest.mark.parametrize("shape", [(2, 37, 53, 29), (3, 130, 258, 100), (2, 96, 224, 96),
+                                   (3, 130, 258, 99)])
 def test_gemm_fused_matches_torch(gpu, ta, tb, cfg, shape):
     """Every fusion of csrc/gemm_f64.hip (k-scale prologue, row/col scale, beta, addend block,
     diagonal vector) vs the fp64 torch oracle, for odd (scalar staging) and even (16-byte
@@ -91,6 +92,50 @@ def test_gemm_fused_matches_torch(gpu, ta, tb, cfg, shape):
                      addend=E.to(gpu), addend_cols=8, diag_col0=8, diag_value=1.0,
                      tile_cfg=cfg).cpu()
     assert (out - ref).abs().max().item() / ref.abs().max().item() < 1e-13
+
+
+def test_gemm_output_above_2gb_row_split(gpu):
+    """A C batch entry of 2 GB or more (the epilogue's buffer stores use 32-bit offsets) is
+    split into row chunks on the host: row scale, diagonal vector, addend and the
+    transposed second output are offset per chunk; vs the torch product on the device."""
+    from pfml.ops.gemm import gemm_fused
+    M, N, K = 16640, 16400, 8          # C: 2.18 GB
+    g = torch.Generator(device=gpu).manual_seed(3)
+    A = torch.randn(1, M, K, generator=g, dtype=torch.float64, device=gpu)
+    B = torch.randn(1, K, N, generator=g, dtype=torch.float64, device=gpu)
+    rs = torch.randn(1, M, generator=g, dtype=torch.float64, device=gpu)
+    dv = torch.randn(1, M, generator=g, dtype=torch.float64, device=gpu)
+    E = torch.randn(1, M, 8, generator=g, dtype=torch.float64, device=gpu)
+    C = torch.empty(1, M, N, dtype=torch.float64, device=gpu)
+    gemm_fused(A, B, C, row_scale=rs, addend=E, addend_cols=8, diag_col0=5, diag_vec=dv)
+    ref = torch.bmm(A, B) * rs[..., None]
+    ref[..., :8] += E
+    i = torch.arange(min(M, N - 5), device=gpu)
+    ref[0, i, i + 5] += dv[0, i]
+    err = ((C - ref).abs().max() / ref.abs().max()).item()
+    assert err < 1e-13, err
+    del C, ref
+    torch.cuda.empty_cache()
+    # transposed second output (X21 = X12') across the split
+    M2, N2 = 17000, 2048
+    A2 = torch.randn(1, M2, K, generator=g, dtype=torch.float64, device=gpu)
+    B2 = torch.randn(1, K, 16000, generator=g, dtype=torch.float64, device=gpu)
+    C2 = torch.empty(1, M2, 16000, dtype=torch.float64, device=gpu)
+    Ct = torch.empty(1, 16000, M2, dtype=torch.float64, device=gpu)
+    # Ct is itself >= 2 GB: not splittable -> the launch must fail loudly, not write garbage
+    with pytest.raises(RuntimeError):
+        gemm_fused(A2, B2, C2, mirror_out=Ct)
+    del C2, Ct
+    torch.cuda.empty_cache()
+    C3 = torch.empty(1, M2, 16000, dtype=torch.float64, device=gpu)
+    Ct3 = torch.empty(1, N2, M2, dtype=torch.float64, device=gpu)
+    B3 = B2[..., :N2].contiguous()
+    C3v = C3[..., :N2]
+    # a strided output view of 2.2 GB extent (ldc = 16000) with a 0.28 GB transposed copy
+    gemm_fused(A2, B3, C3v, mirror_out=Ct3)
+    ref3 = torch.bmm(A2, B3)
+    assert ((C3v - ref3).abs().max() / ref3.abs().max()).item() < 1e-13
+    assert torch.equal(Ct3, C3v.transpose(1, 2))
 
 
 @pytest.mark.parametrize("cfg", [3, 6, 8])

@@ -90,6 +90,13 @@ for step in ${MODE//,/ }; do
     bench)
       timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err
       rc=$?; grep '^{' $OUT/bench.json | cut -c1-400; if [ $rc -ne 0 ]; then tail -5 $OUT/bench.err; exit $rc; fi ;;
+    repair)
+      # lambda = 0 repair load on the production grid: collinear summands (every window rank
+      # <= 200) vs the clean step on the same box
+      timeout -k 10 300 python bench.py --no-inputs --steps 20 --warmup 5 > $OUT/bench_clean.json 2> $OUT/bench_clean.err
+      rc=$?; grep '^{' $OUT/bench_clean.json | cut -c1-300; if [ $rc -ne 0 ]; then tail -5 $OUT/bench_clean.err; exit $rc; fi
+      timeout -k 10 300 python bench.py --no-inputs --steps 20 --warmup 5 --collinear 200 > $OUT/bench_collinear.json 2> $OUT/bench_collinear.err
+      rc=$?; grep '^{' $OUT/bench_collinear.json | cut -c1-300; if [ $rc -ne 0 ]; then tail -5 $OUT/bench_collinear.err; exit $rc; fi ;;
     qr)
       # panel QR in isolation (band_panel_factor): cycles per panel, Householder vs CholeskyQR2
       timeout -k 10 200 python tools/bench_qr.py 497 241 > $OUT/qr_bench.jsonl 2> $OUT/qr_bench.err
