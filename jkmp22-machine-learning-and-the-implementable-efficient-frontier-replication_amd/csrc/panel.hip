@@ -57,7 +57,9 @@ __global__ __launch_bounds__(256) void standardize_kernel(const double* __restri
                                                           double* __restrict__ out, int64_t ldo,
                                                           int64_t so, int Pw,
                                                           double* __restrict__ stats,
-                                                          int64_t lds, int write_out) {
+                                                          int64_t lds, int write_out,
+                                                          const double* __restrict__ rsc,
+                                                          int64_t srsc) {
   __shared__ double red[4][64], red2[4][64];
   __shared__ double colmean[64], colscale[64];
   const int bt = diag_tile(blockIdx.y, B, TH);   // (b, theta)
@@ -131,7 +133,11 @@ __global__ __launch_bounds__(256) void standardize_kernel(const double* __restri
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int i = i0 + 4 * u;
-        if (i < N) o[(int64_t)i * ldo + c] = (i < n && c < P) ? (x[u] - mu) * sc / vv[u] : 0.0;
+        if (i < N) {
+          double v = (i < n && c < P) ? (x[u] - mu) * sc / vv[u] : 0.0;
+          if (rsc != nullptr) v *= rsc[(int64_t)b * srsc + i];
+          o[(int64_t)i * ldo + c] = v;
+        }
       }
     }
   }
@@ -146,7 +152,7 @@ __global__ __launch_bounds__(1024) void standardize_reg_kernel(
     const double* __restrict__ F, int P, int64_t ldf, const int64_t* __restrict__ rows,
     const int* __restrict__ n_real, int B, int TH, int N, const double* __restrict__ vol,
     double* __restrict__ out, int64_t ldo, int64_t so, int Pw, double* __restrict__ stats,
-    int64_t lds, int write_out) {
+    int64_t lds, int write_out, const double* __restrict__ rsc, int64_t srsc) {
   constexpr int NP = 16;
   __shared__ double red[NP][64], red2[NP][64];
   __shared__ double colmean[64], colscale[64];
@@ -207,8 +213,11 @@ __global__ __launch_bounds__(1024) void standardize_reg_kernel(
 #pragma unroll
   for (int u = 0; u < RPT; ++u) {
     const int i = part + NP * u;
-    if (i < N)
-      o[(int64_t)i * ldo + c] = (i < n && c < P) ? (x[u] - mu) * sc / vol[rw[2 * i]] : 0.0;
+    if (i < N) {
+      double v = (i < n && c < P) ? (x[u] - mu) * sc / vol[rw[2 * i]] : 0.0;
+      if (rsc != nullptr) v *= rsc[(int64_t)b * srsc + i];     // (a separate rounding step)
+      o[(int64_t)i * ldo + c] = v;
+    }
   }
 }
 
@@ -227,12 +236,14 @@ extern "C" hipError_t pfml_rff_sincos(const double* Z, int64_t R, int half, doub
 // stats (nullable): the column means and scales of every (b, theta) tile, [B*TH][2][lds]
 // (mean row, then scale row; columns P..Pw-1 zero); write_out = 0: the stats only (the
 // standardised values are then formed where they are consumed: the Horner GEMM's gathered
-// addend, csrc/gemm_f64.hip)
+// addend, csrc/gemm_f64.hip).  rsc (nullable): an output row scale rsc[b * srsc + i] applied
+// after the standardisation (the k-scale of the Horner step that reads the block: T_11's
+// signal block is written in place, scaled, with no separate pass)
 extern "C" hipError_t pfml_standardize(const double* F, int P, int64_t ldf, const int64_t* rows,
                                        const int* n_real, int B, int TH, int N,
                                        const double* vol, double* out, int64_t ldo, int64_t so,
                                        int Pw, double* stats, int64_t lds, int write_out,
-                                       hipStream_t st) {
+                                       const double* rsc, int64_t srsc, hipStream_t st) {
   if (B <= 0 || N <= 0) return hipSuccess;
   if (Pw < P || ldf < P || (write_out && ldo < Pw) || (stats && lds < Pw) ||
       (!write_out && !stats))
@@ -240,9 +251,10 @@ extern "C" hipError_t pfml_standardize(const double* F, int P, int64_t ldf, cons
   dim3 grid((Pw + 63) / 64, (B + TH - 1) * TH);     // diagonal order (diag_tile)
   if (N <= 16 * 32)
     hipLaunchKernelGGL(standardize_reg_kernel<32>, grid, dim3(1024), 0, st, F, P, ldf, rows,
-                       n_real, B, TH, N, vol, out, ldo, so, Pw, stats, lds, write_out);
+                       n_real, B, TH, N, vol, out, ldo, so, Pw, stats, lds, write_out, rsc,
+                       srsc);
   else
     hipLaunchKernelGGL(standardize_kernel, grid, dim3(256), 0, st, F, P, ldf, rows, n_real, B, TH,
-                       N, vol, out, ldo, so, Pw, stats, lds, write_out);
+                       N, vol, out, ldo, so, Pw, stats, lds, write_out, rsc, srsc);
   return hipGetLastError();
 }

@@ -271,3 +271,66 @@ extern "C" hipError_t pfml_db_mu(const double* M, const double* Minv, int B, int
   hipLaunchKernelGGL(db_mu_final_kernel, dim3((B + 63) / 64), dim3(64), 0, st, work, B, 0, mu);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------
+// Horner chain set-up of (24) (models/pfml_inputs.py run_plan), one pass each instead of a
+// chain of torch ops (diag_embed, temporaries, strided multiplies):
+//
+//   horner_init   T_11's identity and Q blocks from m_tilde:
+//                   I block  T[i, j]     = (i == j) ? k10_i : 0
+//                   Q block  T[i, N + j] = ((mt_ij * ks12_j) * a_i) * k10_i
+//                 (R_11 = diag(a) m_tilde diag(D_11 / a), pre-scaled by the next step's k-scale,
+//                 in the rounding order of the former elementwise form)
+//   block_add     out = X + Y on N x N blocks of strided rows (U_0's identity block Q + T_1)
+// Grid (column chunks, rows, batch); every store coalesced along the row.
+// ---------------------------------------------------------------------------------------
+namespace {
+
+__global__ __launch_bounds__(256) void horner_init_kernel(
+    double* __restrict__ T, int64_t ldt, int64_t sT, const double* __restrict__ mt, int64_t ldm,
+    int64_t sm, const double* __restrict__ k10, const double* __restrict__ ks12, int64_t sk,
+    const double* __restrict__ a, int64_t sa, int N) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int i = blockIdx.y, b = blockIdx.z;
+  if (j >= N) return;
+  double* Tr = T + (int64_t)b * sT + (int64_t)i * ldt;
+  const double ki = k10[(int64_t)b * sk + i];
+  const double q = mt[(int64_t)b * sm + (int64_t)i * ldm + j] * ks12[(int64_t)b * sk + j];
+  Tr[j] = (i == j) ? ki : 0.0;
+  Tr[N + j] = (q * a[(int64_t)b * sa + i]) * ki;
+}
+
+__global__ __launch_bounds__(256) void block_add_kernel(double* __restrict__ out, int64_t ldo,
+                                                        int64_t so, const double* __restrict__ X,
+                                                        int64_t ldx, int64_t sx,
+                                                        const double* __restrict__ Y,
+                                                        int64_t ldy, int64_t sy, int M, int N) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int i = blockIdx.y, b = blockIdx.z;
+  if (j >= N || i >= M) return;
+  out[(int64_t)b * so + (int64_t)i * ldo + j] =
+      X[(int64_t)b * sx + (int64_t)i * ldx + j] + Y[(int64_t)b * sy + (int64_t)i * ldy + j];
+}
+
+}  // namespace
+
+extern "C" hipError_t pfml_horner_init(double* T, int64_t ldt, int64_t sT, const double* mt,
+                                       int64_t ldm, int64_t sm, const double* k10,
+                                       const double* ks12, int64_t sk, const double* a,
+                                       int64_t sa, int N, int B, hipStream_t st) {
+  if (N <= 0 || B <= 0) return hipSuccess;
+  if (N > 65535 || B > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(horner_init_kernel, dim3((N + 255) / 256, N, B), dim3(256), 0, st, T, ldt,
+                     sT, mt, ldm, sm, k10, ks12, sk, a, sa, N);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pfml_block_add(double* out, int64_t ldo, int64_t so, const double* X,
+                                     int64_t ldx, int64_t sx, const double* Y, int64_t ldy,
+                                     int64_t sy, int M, int N, int B, hipStream_t st) {
+  if (M <= 0 || N <= 0 || B <= 0) return hipSuccess;
+  if (M > 65535 || B > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(block_add_kernel, dim3((N + 255) / 256, M, B), dim3(256), 0, st, out, ldo, so,
+                     X, ldx, sx, Y, ldy, sy, M, N);
+  return hipGetLastError();
+}

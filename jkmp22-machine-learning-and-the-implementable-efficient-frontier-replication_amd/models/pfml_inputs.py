@@ -362,9 +362,11 @@ def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
             rf=tt([rfmap[int(d)] for d in bm])))
     # even inner dimensions (a zero factor / a zero feature column - exact zeros in every sum):
     # the GEMMs on them (X F, X' omega, the RFF product) then take the 16-byte-load kernels
+    # (+ two spare zero columns: run_plan puts the month's returns into the first, so that the
+    # X' omega GEMM of the risk term also yields r_tilde = omega' r as its extra row)
     K = barra.X.shape[1]
     Kp = _even(K)
-    bX = np.zeros((barra.X.shape[0] + 1, Kp))
+    bX = np.zeros((barra.X.shape[0] + 1, Kp + 2))
     bX[:-1, :K] = barra.X
     bF = np.zeros((barra.F.shape[0], Kp, Kp))
     bF[:, :K, :K] = barra.F
@@ -420,8 +422,8 @@ def _vol_device(plan: S4Plan) -> torch.Tensor:
         br = plan.vol_brow
         ok = br >= 0
         brc = torch.where(ok, br, torch.zeros_like(br))
-        Xr = plan.bX[brc]                                         # [Mv, nv, K]
         Fm = plan.bF[plan.vol_fpos]                               # one F per vol month
+        Xr = plan.bX[brc][..., :Fm.shape[-1]]                     # [Mv, nv, K]
         d = (gemm(Xr, Fm, backend="own") * Xr).sum(-1) + plan.biv[brc]
         v = torch.where(ok, d.sqrt(), torch.full_like(d, float("nan")))
         real = plan.vol_real if plan.vol_real is not None else plan.vol_rows < plan.R
@@ -524,11 +526,18 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
             # GEMM operand) into [B, 3, N, Gc*Pp]; lags 1..10 only as per-column means and scales -
             # the Horner steps form (F[row] - mean) * scale / vol in their epilogue (gathered
             # addend), so 10 of the 13 [N, Gc*Pp] signal blocks per month are never stored
-            S = torch.empty((B, 3, N, GP), dtype=torch.float64, device=dev)
-            idx3 = torch.cat([bt.idx[:, :1], bt.idx[:, lb:lb + 2]], 1)     # (no host index list)
+            # (lag 0: signal_t and T_0's addend; lag 12: U_0's GEMM operand; lag 11 is written
+            # below straight into T_11, pre-scaled by the next step's k-scale)
+            S0 = torch.empty((B, 1, N, GP), dtype=torch.float64, device=dev)
+            S12 = torch.empty((B, 1, N, GP), dtype=torch.float64, device=dev)
+            idx0 = bt.idx[:, :1].contiguous()
+            idx12 = bt.idx[:, lb + 1:lb + 2].contiguous()
             for g in range(Gc):
-                standardize_signals(rffs[g], idx3, bt.mask, vol, P=P,
-                                    out=S[..., g * Pp:(g + 1) * Pp], n_real=bt.n_real)
+                gs = slice(g * Pp, (g + 1) * Pp)
+                standardize_signals(rffs[g], idx0, bt.mask, vol, P=P, out=S0[..., gs],
+                                    n_real=bt.n_real)
+                standardize_signals(rffs[g], idx12, bt.mask, vol, P=P, out=S12[..., gs],
+                                    n_real=bt.n_real)
             stats = torch.empty((B, lb - 1, 2, GP), dtype=torch.float64, device=dev)
             for g in range(Gc):
                 signal_stats(rffs[g], bt.idx[:, 1:lb], bt.mask, P,
@@ -537,8 +546,10 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
             ivol = torch.where(bt.mask.unsqueeze(1) > 0, 1.0 / vol[bt.idx[:, 1:lb]],
                                torch.zeros((), dtype=torch.float64, device=dev))
             # Barra Sigma = X F X' + diag(ivol) (K1; pad rows: X = 0, ivol = 1 -> identity block)
-            Xl = plan.bX[bt.brow]                                       # [B, N, K]
+            Xr = plan.bX[bt.brow]                                       # [B, N, K + 2]
             Fb = plan.bF[bt.fpos]                                       # [B, K, K]
+            Kf = Fb.shape[-1]
+            Xl = Xr[..., :Kf]                                           # [B, N, K]
             iv = plan.biv[bt.brow]                                      # [B, N]
             XF = gemm(Xl, Fb, backend="own")                             # in-house fp64 MFMA GEMM
             Sigma = torch.empty((B, N, N), dtype=torch.float64, device=dev)
@@ -546,8 +557,11 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
                 # symmetric mode: the lower triangle mirrored, an exactly symmetric Sigma
                 gemm_fused(XF, Xl, Sigma, trans_b=True, diag_col0=0, diag_vec=iv, sym=True)
             else:
-                gemm_prec(XF, Xl, prec, trans_b=True, out=Sigma)
+                gemm_prec(XF, Xl.contiguous(), prec, trans_b=True, out=Sigma)
                 Sigma.diagonal(dim1=1, dim2=2).add_(iv)
+            # the returns ride in the first spare column (after Sigma's GEMM, which reads only
+            # the K factor columns): X' omega below then carries r_tilde = omega' r as row K
+            Xr[..., Kf] = bt.r
             # m = diag(a) m_tilde diag(1/a) (Lemma 1); a and 1/a are folded into the Horner GEMMs
             mt, a = la.m_tilde(Sigma, bt.lam, bt.w, bt.rf, mu, gamma, cfg.run.iterations,
                                mask=bt.mask, status=None if mstat is None else mstat[b0:b0 + B],
@@ -578,13 +592,17 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
             ks = Dg * ainv.unsqueeze(1)                                 # [B, 13, N]
             Wr = Wd + N
             Tb = [torch.empty((B, N, Wr), dtype=torch.float64, device=dev) for _ in range(2)]
-            k10 = ks[:, lb - 1].unsqueeze(-1)
-            torch.mul(S[:, 1], k10, out=Tb[0][:, :, :GP])
-            Tb[0][:, :, GP:Wd] = torch.diag_embed(ks[:, lb - 1])
-            # R_11 = diag(a) m_tilde diag(D_11 / a): elementwise, in the rounding order the fused
+            # T_11 = [S_11 | I | R_11], every row pre-scaled by ks_10: the signal block by the
+            # standardisation itself (output row scale), the identity block diag(ks_10), and
+            # R_11 = diag(a) m_tilde diag(D_11 / a) elementwise, in the rounding order the fused
             # GEMM against the identity produced ((m_tilde * k-scale) * row scale), then ks_10
-            torch.mul(mt * ks[:, lb].unsqueeze(-2), a.unsqueeze(-1), out=Tb[0][:, :, Wd:])
-            Tb[0][:, :, Wd:].mul_(k10)
+            idx11 = bt.idx[:, lb:lb + 1].contiguous()
+            T11 = Tb[0].unsqueeze(1)
+            for g in range(Gc):
+                standardize_signals(rffs[g], idx11, bt.mask, vol, P=P,
+                                    out=T11[..., g * Pp:(g + 1) * Pp], n_real=bt.n_real,
+                                    row_scale=ks[:, lb - 1])
+            la.horner_init(Tb[0][:, :, GP:], mt, ks[:, lb - 1], ks[:, lb], a)
             cur = 0
             for th in range(lb - 1, 0, -1):
                 gemm_fused(mt, Tb[cur], Tb[cur ^ 1], row_scale=a,
@@ -601,14 +619,14 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
             T0f, U0f = TU0[0], TU0[1]
             T0, U0 = T0f[:, :, :Wd], U0f[:, :, :Wd]
             gemm_fused(mt, T1[:, :, :Wd], T0, row_scale=a, k_scale=ks[:, 0].contiguous(),
-                       addend=S[:, 0], addend_cols=GP, diag_col0=GP, diag_value=1.0)
+                       addend=S0[:, 0], addend_cols=GP, diag_col0=GP, diag_value=1.0)
             # U_0 = T_1 + Q [S_12 | I]: the S_12 block on the GEMM, the identity block as Q + T_1
-            gemm_fused(T1[:, :, Wd:], S[:, 2], U0[:, :, :GP], addend=T1[:, :, :GP],
+            gemm_fused(T1[:, :, Wd:], S12[:, 0], U0[:, :, :GP], addend=T1[:, :, :GP],
                        addend_cols=GP)
-            torch.add(T1[:, :, Wd:], T1[:, :, GP:Wd], out=U0[:, :, GP:])
+            la.block_add(U0[:, :, GP:], T1[:, :, Wd:], T1[:, :, GP:Wd])
             del Tb, T1
-            sig0 = S[:, 0].clone()                                      # signal_t blocks
-            del S, stats, ivol
+            sig0 = S0[:, 0]                                             # signal_t blocks
+            del S12, stats, ivol
             # omega = const^-1 Omega, solved in place on the augmented [Omega | const] rows (K7)
             om2 = la.solve_augmented(TU0.view(2 * B, N, Wz), N, GP, a0=GP, b0=0,
                                      status=sing[:2 * B], z0=Wd)                  # [2B, N, GP]
@@ -620,11 +638,12 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
             # X (F (X' omega)) + ivol o omega), tc = w omega_chg' Lambda omega_chg, denom
             # (omega stays a row-strided view of the solve buffer: every consumer takes the
             # row stride; omega_chg is a fresh tensor)
-            rt_ = gemm(omega, bt.r.unsqueeze(-1).contiguous(), trans_a=True,
-                       backend="own").squeeze(-1)                                # [B, GP]
-            XtO = torch.empty((B, Xl.shape[2], GP), dtype=torch.float64, device=dev)
-            gemm_fused(Xl, omega, XtO, trans_a=True)
-            FXO = gemm(Fb, XtO, backend="own")
+            # [X | r | 0]' omega: X' omega for the risk term and r_tilde = omega' r (row K) in
+            # one GEMM
+            XtO = torch.empty((B, Kf + 2, GP), dtype=torch.float64, device=dev)
+            gemm_fused(Xr, omega, XtO, trans_a=True)
+            rt_ = XtO[:, Kf]                                                     # [B, GP]
+            FXO = gemm(Fb, XtO[:, :Kf], backend="own")
             SO = torch.empty_like(omega)
             gemm_fused(Xl, FXO, SO, addend=omega, addend_row_scale=iv)
             lw = (bt.lam * bt.w.view(B, 1)).contiguous()

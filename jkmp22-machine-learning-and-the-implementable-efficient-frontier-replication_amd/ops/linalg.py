@@ -473,6 +473,52 @@ def mf_sym(mode: int, X: torch.Tensor, Y: torch.Tensor | None, out: torch.Tensor
     return out
 
 
+nat.register_hip("pfml_horner_init", [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
+                                      C.c_int64, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
+                                      C.c_int64, C.c_int, C.c_int, C.c_void_p])
+nat.register_hip("pfml_block_add", [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
+                                    C.c_int64, C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int,
+                                    C.c_int, C.c_void_p])
+
+
+def horner_init(T: torch.Tensor, mt: torch.Tensor, k10: torch.Tensor, ks12: torch.Tensor,
+                a: torch.Tensor) -> torch.Tensor:
+    """T_11's identity and Q blocks of the (24) Horner chain (models/pfml_inputs.py) in one pass
+    (csrc/s4.hip horner_init): T [B, N, 2N] (a column block of the Horner buffer) gets
+    [diag(k10) | ((mt * ks12_j) * a_i) * k10_i].  k10 / ks12 [B, N] share a batch stride."""
+    B, N, _ = mt.shape
+    if nat.is_device(T):
+        if (T.stride(-1) != 1 or mt.stride(-1) != 1 or k10.stride(-1) != 1 or
+                ks12.stride(-1) != 1 or a.stride(-1) != 1 or k10.stride(0) != ks12.stride(0) or
+                T.shape[-1] < 2 * N):
+            raise ValueError("horner_init: unsupported layout")
+        _work.add("horner_init_kernel", 3.0 * B * N * N, 24.0 * B * N * N)
+        nat.check(nat.hip_lib().pfml_horner_init(
+            T.data_ptr(), T.stride(1), T.stride(0), mt.data_ptr(), mt.stride(1), mt.stride(0),
+            k10.data_ptr(), ks12.data_ptr(), k10.stride(0), a.data_ptr(), a.stride(0), N, B,
+            nat.stream_of(T)), "pfml_horner_init")
+        return T
+    T[:, :, :N] = torch.diag_embed(k10)
+    torch.mul(mt * ks12.unsqueeze(-2), a.unsqueeze(-1), out=T[:, :, N:2 * N])
+    T[:, :, N:2 * N].mul_(k10.unsqueeze(-1))
+    return T
+
+
+def block_add(out: torch.Tensor, X: torch.Tensor, Y: torch.Tensor) -> torch.Tensor:
+    """out = X + Y on [B, M, N] blocks of strided rows (unit inner stride), one pass."""
+    B, M, N = out.shape
+    if nat.is_device(out):
+        for t in (out, X, Y):
+            if t.stride(-1) != 1 or tuple(t.shape) != (B, M, N):
+                raise ValueError("block_add: unsupported layout")
+        nat.check(nat.hip_lib().pfml_block_add(
+            out.data_ptr(), out.stride(1), out.stride(0), X.data_ptr(), X.stride(1), X.stride(0),
+            Y.data_ptr(), Y.stride(1), Y.stride(0), M, N, B, nat.stream_of(out)),
+            "pfml_block_add")
+        return out
+    return torch.add(X, Y, out=out)
+
+
 def _db_mu(M: torch.Tensor, Minv: torch.Tensor, unscaled: bool, out: torch.Tensor) -> None:
     B, N, _ = M.shape
     if nat.is_device(M):

@@ -19,7 +19,7 @@ nat.register_hip("pfml_rff_sincos", [C.c_void_p, C.c_int64, C.c_int, C.c_void_p,
 nat.register_hip("pfml_standardize", [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
                                       C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                       C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_int64,
-                                      C.c_int, C.c_void_p])
+                                      C.c_int, C.c_void_p, C.c_int64, C.c_void_p])
 
 
 def rff_features(X: torch.Tensor, W: torch.Tensor, precision: str = "fp64",
@@ -74,13 +74,17 @@ def rff_features(X: torch.Tensor, W: torch.Tensor, precision: str = "fp64",
 
 def standardize_signals(F: torch.Tensor, idx: torch.Tensor, mask: torch.Tensor,
                         vol: torch.Tensor, P: int | None = None, out: torch.Tensor | None = None,
-                        n_real: torch.Tensor | None = None) -> torch.Tensor:
+                        n_real: torch.Tensor | None = None,
+                        row_scale: torch.Tensor | None = None) -> torch.Tensor:
     """Gather + standardise the signal windows.
 
     F: [R+1, >= P] panel features (last row all zero, used for padding; P real columns),
     idx: [B, TH, N] rows, mask: [B, N] 1 for real stocks (real rows first), vol: [R+1].
     Returns [B, TH, N, Pw]: ``out`` may be a column block view of a wider buffer (e.g. one g's
-    block of the [B, TH, N, G*Pw] S4 signal stack), columns P..Pw-1 come out zero."""
+    block of the [B, TH, N, G*Pw] S4 signal stack), columns P..Pw-1 come out zero.
+    ``row_scale`` [B, N] (unit inner stride): every output row i of month b is multiplied by
+    row_scale[b, i] afterwards (a separate rounding step: bitwise the standardised block times
+    the scale) - the k-scale of the Horner step that reads the block."""
     B, TH, N = idx.shape
     P = P or F.shape[1]
     if out is None:
@@ -94,9 +98,12 @@ def standardize_signals(F: torch.Tensor, idx: torch.Tensor, mask: torch.Tensor,
         n_real = n_real.to(torch.int32).contiguous()
         rows = idx.to(torch.int64).contiguous()
         _work.add("standardize", 6.0 * B * TH * N * P, 8.0 * B * TH * N * (P + Pw))
+        if row_scale is not None and row_scale.stride(-1) != 1:
+            raise ValueError("standardize_signals: row_scale needs unit inner stride")
         nat.check(nat.hip_lib().pfml_standardize(
             F.data_ptr(), P, F.stride(0), rows.data_ptr(), n_real.data_ptr(), B, TH, N,
             vol.data_ptr(), out.data_ptr(), out.stride(2), out.stride(1), Pw, None, 0, 1,
+            nat.ptr(row_scale), 0 if row_scale is None else row_scale.stride(0),
             nat.stream_of(F)), "pfml_standardize")
         return out
     F = F[:, :P]
@@ -111,6 +118,8 @@ def standardize_signals(F: torch.Tensor, idx: torch.Tensor, mask: torch.Tensor,
     v = vol[idx].unsqueeze(-1)
     out.zero_()
     out[..., :P] = S / v
+    if row_scale is not None:
+        out.mul_(row_scale.view(B, 1, N, 1))
     return out
 
 
@@ -133,7 +142,7 @@ def signal_stats(F: torch.Tensor, idx: torch.Tensor, mask: torch.Tensor, P: int,
         _work.add("standardize", 4.0 * B * TH * N * P, 8.0 * B * TH * N * P)
         nat.check(nat.hip_lib().pfml_standardize(
             F.data_ptr(), P, F.stride(0), rows.data_ptr(), n_real.data_ptr(), B, TH, N,
-            F.data_ptr(), None, 0, 0, Pw, out.data_ptr(), out.stride(-2), 0,
+            F.data_ptr(), None, 0, 0, Pw, out.data_ptr(), out.stride(-2), 0, None, 0,
             nat.stream_of(F)), "pfml_standardize")
         return out
     S = F[:, :P][idx]                                           # [B, TH, N, P]
