@@ -55,6 +55,9 @@ struct Epi {
   const double* ecm; const double* ecs; int64_t secm;
   const double* os; int64_t sos;      // output row scale, applied last (null: 1): the next
                                       // Horner step's k-scale folded into this step's output
+  int ms, ns;                         // store clip (0: M / N): only C[:ms, :ns] is read (beta)
+                                      // and written - e.g. the P x P denom of a product
+                                      // computed at the padded (even) width Pp, stored in place
 };
 
 // Output tile of workgroup wg: batch entry b, first row bm / column bn.  Grouped order:
@@ -376,7 +379,8 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(
         }
     return;
   }
-  store_tile<TM, TN>(acc, ep, b, bm + wm * (BM / 2), bn + wn * (BN / 2), lane, M, N, C, ldc);
+  store_tile<TM, TN>(acc, ep, b, bm + wm * (BM / 2), bn + wn * (BN / 2), lane,
+                     ep.ms ? min(M, ep.ms) : M, ep.ns ? min(N, ep.ns) : N, C, ldc);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -560,7 +564,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void dgemm_glds_kernel(
       __syncthreads();
     }
   }
-  store_tile<TM, TN>(acc, ep, b, bm + wm * (BM / WM), bn + wn * (BN / WN), lane, M, N, C, ldc);
+  store_tile<TM, TN>(acc, ep, b, bm + wm * (BM / WM), bn + wn * (BN / WN), lane,
+                     ep.ms ? min(M, ep.ms) : M, ep.ns ? min(N, ep.ns) : N, C, ldc);
 }
 
 template <int BM, int BN, int WM = 2, int WN = 2, int NS = 2>
@@ -660,6 +665,7 @@ struct PfmlGemmEpi {
   int tile_cfg;      // 0 auto, 1: 128x128, 2: 128x64, 3: 64x64 (BK 16, two LDS buffers);
                      // 4: 64x64 BK 32 one buffer, 5: 64x64 BK 32 two buffers (a 128x128
                      // BK 32 form spills: 144 B per lane)
+  int ms, ns;        // store clip (Epi)
 };
 
 extern "C" int pfml_gemm_epi_size() { return (int)sizeof(PfmlGemmEpi); }
@@ -688,7 +694,7 @@ extern "C" hipError_t pfml_dgemm_ex(int ta, int tb, int M, int N, int K, int bat
   const int64_t lim = (int64_t)1 << 31;
   if (((int64_t)(M - 1) * ldc + N) * 8 < lim)
     return dgemm_chunk(ta, tb, M, N, K, batch, A, lda, sA, B, ldb, sB, C, ldc, sC, h, st);
-  if (h->sym || ldc <= 0) return hipErrorInvalidValue;
+  if (h->sym || h->ms || h->ns || ldc <= 0) return hipErrorInvalidValue;
   // rows per chunk: a multiple of 128 (tile height; keeps A's and the vectors' 16-B alignment)
   int64_t rows = ((lim / 8 - N) / ldc) / 128 * 128;
   if (rows < 128) return hipErrorInvalidValue;
@@ -719,7 +725,7 @@ static hipError_t dgemm_chunk(int ta, int tb, int M, int N, int K, int batch,
   Epi ep{h->alpha, h->beta, h->rs, h->srs, h->cs, h->scs, h->ks, h->sks, h->E, h->lde, h->sE,
          h->e_cols, h->diag_col0, h->dval, h->dv, h->sdv, h->has_diag, h->es, h->ses,
          h->sincos, h->sym, h->Ct, h->ldct, h->sCt, h->erow, h->serow, h->ecm, h->ecs,
-         h->secm, h->os, h->sos};
+         h->secm, h->os, h->sos, h->ms, h->ns};
   // symmetric mode: square C, square tiles, no sincos
   if (h->sym && (M != N || h->sincos)) return hipErrorInvalidValue;
   // the epilogue's buffer stores address a batch entry of C / Ct with 32-bit byte offsets

@@ -664,6 +664,17 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
                 og, cg, sg = omega[:, :, cs], omega_chg[:, :, cs], SO[:, :, cs]
                 # risk = gamma omega' (Sigma omega) and tc = w omega_chg' Lambda omega_chg are
                 # symmetric: the GEMM's symmetric mode computes the lower tiles and mirrors them
+                if prec == "fp64" and not keep_risk_tc:
+                    # computed at the even width Pp, the P x P block stored straight into the
+                    # denom stack (store clip; same arithmetic as the padded temporary)
+                    dd = d_out[g, sl]
+                    gemm_fused(og, sg, dd, trans_a=True, alpha=gamma, sym=True, clip=True)
+                    gemm_fused(cg, cg, dd, trans_a=True, k_scale=lw, beta=1.0, sym=True,
+                               clip=True)
+                    r_out[g, sl] = rt_[:, g * Pp:g * Pp + P]
+                    for bi in range(B):
+                        signal_t[g][b0 + bi] = sig0[bi, : int(bt.ns[bi]), g * Pp:g * Pp + P]
+                    continue
                 if prec == "fp64":
                     gemm_fused(og, sg, Dt, trans_a=True, alpha=gamma, sym=True)
                 else:

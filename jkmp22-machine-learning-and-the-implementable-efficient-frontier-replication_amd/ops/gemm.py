@@ -28,7 +28,7 @@ class _Epi(C.Structure):
                 ("diag_col0", _I), ("dval", _D), ("dv", _P), ("sdv", _L), ("has_diag", _I),
                 ("es", _P), ("ses", _L), ("sincos", _I), ("sym", _I), ("Ct", _P), ("ldct", _L),
                 ("sCt", _L), ("erow", _P), ("serow", _L), ("ecm", _P), ("ecs", _P),
-                ("secm", _L), ("os", _P), ("sos", _L), ("tile_cfg", _I)]
+                ("secm", _L), ("os", _P), ("sos", _L), ("tile_cfg", _I), ("ms", _I), ("ns", _I)]
 
 
 nat.register_hip("pfml_dgemm_ex", [_I, _I, _I, _I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _L,
@@ -288,7 +288,8 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
                addend_rows: torch.Tensor | None = None,
                addend_col_shift: torch.Tensor | None = None,
                addend_col_scale: torch.Tensor | None = None,
-               out_row_scale: torch.Tensor | None = None) -> torch.Tensor:
+               out_row_scale: torch.Tensor | None = None,
+               clip: bool = False) -> torch.Tensor:
     """out = diag(os) (alpha diag(rs) op(A) diag(ks) op(B) diag(cs) + beta out
              + diag(es) addend[:, :, :addend_cols]  (on out's first addend_cols columns)
              + diag(diag_vec or diag_value) placed at out[:, i, diag_col0 + i]).
@@ -311,16 +312,23 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
     (batch stride 0 = broadcast); scale vectors are [n] or [B, n].
 
     ``sincos=True`` (K13): v = alpha op(A) op(B) never stored - out (width >= 2 N + 1) gets
-    the row [1, cos v_1, sin v_1, cos v_2, sin v_2, ...] (columns past 2 N + 1 untouched)."""
+    the row [1, cos v_1, sin v_1, cos v_2, sin v_2, ...] (columns past 2 N + 1 untouched).
+
+    ``clip=True``: out is [.., Ms, Ns] with Ms <= M, Ns <= N - the product is computed at the
+    operands' full (e.g. even-padded) size and only its leading Ms x Ns block is read (beta)
+    and stored, straight into the final buffer (no padded temporary + copy)."""
     A3, B3, C3 = _as3(A), _as3(B), _as3(out)
     batch = C3.shape[0]
     M = A3.shape[2] if trans_a else A3.shape[1]
     K = A3.shape[1] if trans_a else A3.shape[2]
     N = B3.shape[1] if trans_b else B3.shape[2]
+    Ms, Ns = (C3.shape[1], C3.shape[2]) if clip else (M, N)
+    if clip and (sincos or Ms > M or Ns > N or mirror_out is not None or Ms < 1 or Ns < 1):
+        raise ValueError("gemm_fused(clip): out [.., <= M, <= N], no sincos / mirror_out")
     if sincos:
         if C3.shape[1] != M or C3.shape[2] < 2 * N + 1:
             raise ValueError("gemm_fused(sincos): out must be [.., M, >= 2N + 1]")
-    elif (B3.shape[2] if trans_b else B3.shape[1]) != K or tuple(C3.shape[1:]) != (M, N):
+    elif (B3.shape[2] if trans_b else B3.shape[1]) != K or tuple(C3.shape[1:]) != (Ms, Ns):
         raise ValueError(f"gemm_fused: shapes {tuple(A3.shape)} {tuple(B3.shape)} -> {tuple(C3.shape)}")
     if addend is not None and addend_cols is None:
         addend_cols = N
@@ -364,7 +372,8 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
                   int(diag_col0 is not None), nat.ptr(es), ses, int(sincos), int(sym),
                   nat.ptr(T3), 0 if T3 is None else T3.stride(1),
                   0 if T3 is None else T3.stride(0), nat.ptr(er), ser, nat.ptr(ecm),
-                  nat.ptr(ecs), secm, nat.ptr(osc), sos, int(tile_cfg or _TILE_DEFAULT))
+                  nat.ptr(ecs), secm, nat.ptr(osc), sos, int(tile_cfg or _TILE_DEFAULT),
+                  int(Ms) if clip else 0, int(Ns) if clip else 0)
         if _work.on():
             _ledger(trans_a, trans_b, M, N, K, batch, A3, B3, C3, ks=ks, sks=sks,
                     sincos=sincos, cfg=tile_cfg, sym=sym,
@@ -397,7 +406,12 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
         C3[:, :, 2:2 * N + 1:2] = torch.sin(r)
         return out
     if beta != 0.0:
-        r = r + beta * C3
+        if clip:
+            Cf = torch.zeros((batch, M, N), dtype=C3.dtype, device=C3.device)
+            Cf[:, :Ms, :Ns] = C3
+            r = r + beta * Cf
+        else:
+            r = r + beta * C3
     r = r.expand(batch, M, N).clone()
     if E3 is not None and addend_cols:
         if gathered:
@@ -425,7 +439,7 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
         r = r * osv.unsqueeze(-1)
     if sym:                                     # the lower triangle, mirrored (device form)
         r = torch.tril(r) + torch.tril(r, -1).transpose(-1, -2)
-    C3.copy_(r)
+    C3.copy_(r[:, :Ms, :Ns] if clip else r)
     if T3 is not None:
         T3.copy_(r.transpose(-1, -2))
     return out

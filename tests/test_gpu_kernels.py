@@ -94,6 +94,30 @@ def test_gemm_fused_matches_torch(gpu, ta, tb, cfg, shape):
     assert (out - ref).abs().max().item() / ref.abs().max().item() < 1e-13
 
 
+@pytest.mark.parametrize("sym", [False, True])
+def test_gemm_store_clip(gpu, sym):
+    """Store clip (S4's denom written in place): the product of the even-padded operands, only
+    the leading Ms x Ns block read for beta and stored into a [B, Ms, Ns] buffer - equal to the
+    padded product's block (bitwise: same kernel, same arithmetic) and to the fp64 oracle."""
+    from pfml.ops.gemm import gemm_fused
+    b, K, P = 3, 130, 513
+    Pp = P + 1
+    A, B = _rand(b, K, Pp, seed=1).to(gpu), _rand(b, K, Pp, seed=2).to(gpu)
+    if sym:
+        B = A
+    ks = _rand(b, K, seed=3).to(gpu)
+    C0 = _rand(b, Pp, Pp, seed=4).to(gpu)
+    C0 = 0.5 * (C0 + C0.transpose(1, 2))
+    full = C0.clone()
+    gemm_fused(A, B, full, trans_a=True, k_scale=ks, beta=1.0, alpha=0.7, sym=sym)
+    dd = C0[:, :P, :P].contiguous()
+    gemm_fused(A, B, dd, trans_a=True, k_scale=ks, beta=1.0, alpha=0.7, sym=sym, clip=True)
+    assert torch.equal(dd, full[:, :P, :P])
+    ref = gemm_fused(A.cpu(), B.cpu(), C0.cpu()[:, :P, :P].contiguous(), trans_a=True,
+                     k_scale=ks.cpu(), beta=1.0, alpha=0.7, sym=sym, clip=True)
+    assert ((dd.cpu() - ref).abs().max() / ref.abs().max()).item() < 1e-13
+
+
 def test_gemm_output_above_2gb_row_split(gpu):
     """A C batch entry of 2 GB or more (the epilogue's buffer stores use 32-bit offsets) is
     split into row chunks on the host: row scale, diagonal vector, addend and the
