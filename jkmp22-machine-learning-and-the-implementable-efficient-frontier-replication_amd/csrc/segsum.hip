@@ -370,6 +370,18 @@ __global__ __launch_bounds__(256) void wsum_chunk_prefix_kernel(
   const int64_t PP = (int64_t)P * P;
   const int t = threadIdx.x, c = t & 31, r0 = t >> 5;
   const double* tg = tot + (int64_t)g * PP;     // slot k at tg + k * tstride
+  // the first segment's tile is in flight during the prefix, each next one while the current
+  // is added and written (clamped loads, masked on use; the same adds in the same order)
+  double nx[4];
+  auto fetch = [&](int s) {
+    const double* o = seg_slot(out, scratch, g, s, nseg, skip, PP);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int i = min(I * 32 + r0 + 8 * q, P - 1), j = min(J * 32 + c, P - 1);
+      nx[q] = o[(int64_t)i * P + j];
+    }
+  };
+  fetch(s0);
   // the C + ch prefix tiles, loaded together, then added in the canonical order
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   const int nk = C + ch;
@@ -397,11 +409,14 @@ __global__ __launch_bounds__(256) void wsum_chunk_prefix_kernel(
     }
   }
   for (int s = s0; s < s1; ++s) {
-    const double* o = seg_slot(out, scratch, g, s, nseg, skip, PP);
+    double cur[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cur[q] = nx[q];
+    if (s + 1 < s1) fetch(s + 1);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = r0 + 8 * q, i = I * 32 + r, j = J * 32 + c;
-      const double v = tile_upper(I, J, i, j, r, c, P) ? o[(int64_t)i * P + j] : 0.0;
+      const double v = tile_upper(I, J, i, j, r, c, P) ? cur[q] : 0.0;
       acc[q] += v;
       Ts[r][c] = acc[q];
     }
