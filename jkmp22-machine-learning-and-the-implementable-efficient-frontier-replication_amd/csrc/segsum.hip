@@ -7,7 +7,6 @@
 // denom stack this reads 2.1 MB per month exactly once; rows of even length that are 16-byte
 // aligned take the double2 (16 B per lane) path.
 #include "common.h"
-#include <cstdlib>
 
 namespace {
 
@@ -96,64 +95,6 @@ __global__ __launch_bounds__(256) void wsum_upper_kernel(const double* __restric
   }
 }
 
-// Balanced form of the pass above (the production launch): workgroup x < ceil(P / 2) sums the
-// STRICTLY upper parts of rows i = x and k = P - 1 - x, (P - 1 - i) + i = P - 1 elements, so
-// every workgroup has the same count (512 at P = 513: two per thread, no idle tail); the
-// middle row of an odd P is alone; workgroup x = ceil(P / 2) sums the diagonal.  Every element
-// keeps the four-chain month order of wsum_upper_kernel (bitwise the same sums); two elements
-// per thread put eight month loads in flight per lane.  (The row-per-workgroup form left
-// rows i > P - 256 with fewer live lanes than a wave slot: 4.6 TB/s, 325 us per grid step.)
-__global__ __launch_bounds__(256) void wsum_upper_pair_kernel(
-    const double* __restrict__ X, int P, int T, const int* __restrict__ seg_start,
-    const int* __restrict__ seg_stop, int nseg, int skip, double* __restrict__ out,
-    double* __restrict__ scratch) {
-  const int x = blockIdx.x, s = blockIdx.y, g = blockIdx.z;
-  const int nh = (P + 1) / 2;
-  const int a = seg_start[s], b = seg_stop[s];
-  const int64_t PP = (int64_t)P * P;
-  const double* src = X + (int64_t)g * T * PP;
-  double* dst = seg_slot(out, scratch, g, s, nseg, skip, PP);
-  const int i = x, k = P - 1 - x;
-  const int Li = P - 1 - i;                              // strictly upper part of row i
-  const int cnt = x == nh ? P : (k == i ? Li : P - 1);
-  for (int e0 = threadIdx.x; e0 < cnt; e0 += 512) {
-    int64_t off[2];
-    bool ok[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int e = e0 + 256 * q;
-      ok[q] = e < cnt;
-      const int ee = min(e, cnt - 1);
-      off[q] = x == nh ? (int64_t)ee * (P + 1)
-                       : (ee < Li ? (int64_t)i * P + i + 1 + ee
-                                  : (int64_t)k * P + k + 1 + (ee - Li));
-    }
-    double acc[2][4] = {{0.0, 0.0, 0.0, 0.0}, {0.0, 0.0, 0.0, 0.0}};
-    int tm = a;
-    for (; tm + 4 <= b; tm += 4) {
-      double v[2][4];
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[q][u] = src[(int64_t)(tm + u) * PP + off[q]];
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc[q][u] += v[q][u];
-    }
-    for (; tm < b; ++tm) {
-      double v[2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) v[q] = src[(int64_t)tm * PP + off[q]];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) acc[q][0] += v[q];
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-      if (ok[q]) dst[off[q]] = (acc[q][0] + acc[q][1]) + (acc[q][2] + acc[q][3]);
-  }
-}
-
 // pass 2 on 32 x 32 tiles (I <= J) of the upper triangle: running sum over segments in
 // registers, tile (I, J) and its transpose (J, I) both written row-contiguous via LDS.  The
 // next segment's tile is loaded while the current one is written (loads clamped into the
@@ -216,8 +157,8 @@ extern "C" hipError_t pfml_window_prefix_sym(const double* X, int P, int T, int 
                                              hipStream_t st) {
   if (nseg <= 0 || P <= 0 || G <= 0) return hipSuccess;
   if (skip < 0 || skip > nseg || (skip > 0 && scratch == nullptr)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(wsum_upper_pair_kernel, dim3((P + 1) / 2 + 1, nseg, G), dim3(256), 0, st, X,
-                     P, T, seg_start, seg_stop, nseg, skip, out, scratch);
+  hipLaunchKernelGGL(wsum_upper_kernel, dim3(P, nseg, G), dim3(256), 0, st, X, P, T, seg_start,
+                     seg_stop, nseg, skip, out, scratch);
   const int nt = (P + 31) / 32;
   hipLaunchKernelGGL(wsum_prefix_mirror_kernel, dim3(nt * (nt + 1) / 2, G), dim3(256), 0, st, P,
                      nseg, skip, out, scratch);
@@ -497,12 +438,8 @@ extern "C" hipError_t pfml_wsum_chunk_totals(const double* X, int P, int T, int 
                                              hipStream_t st) {
   if (nseg <= 0 || P <= 0 || G <= 0) return hipSuccess;
   if (skip < 0 || skip > nseg || (skip > 0 && scratch == nullptr)) return hipErrorInvalidValue;
-  if (std::getenv("PFML_WSUM_ROWS") != nullptr)         // A/B: the row-per-workgroup form
-    hipLaunchKernelGGL(wsum_upper_kernel, dim3(P, nseg, G), dim3(256), 0, st, X, P, T, seg_start,
-                       seg_stop, nseg, skip, out, scratch);
-  else
-    hipLaunchKernelGGL(wsum_upper_pair_kernel, dim3((P + 1) / 2 + 1, nseg, G), dim3(256), 0, st,
-                       X, P, T, seg_start, seg_stop, nseg, skip, out, scratch);
+  hipLaunchKernelGGL(wsum_upper_kernel, dim3(P, nseg, G), dim3(256), 0, st, X, P, T, seg_start,
+                     seg_stop, nseg, skip, out, scratch);
   if (nlc > 0) {
     const int nt = (P + 31) / 32;
     hipLaunchKernelGGL(wsum_chunk_totals_kernel, dim3(nt * (nt + 1) / 2, G, nlc), dim3(256), 0, st, P,

@@ -853,27 +853,6 @@ def test_chunked_window_sums_world_bitwise(gpu):
             assert torch.equal(got[y][1], ref[y][1]), (W, y)
 
 
-@pytest.mark.parametrize("P", [37, 64, 513])
-def test_window_sums_paired_rows_bitwise(gpu, monkeypatch, P):
-    """The balanced segment-sum pass (row pairs + a diagonal workgroup, two elements per lane)
-    gives BITWISE the windows of the row-per-workgroup form, odd and even P."""
-    from pfml.utils.dates import mi_from_ym
-    G = 2
-    months = np.arange(mi_from_ym(2000, 0), mi_from_ym(2012, 11) + 1, dtype=np.int64)
-    years = np.arange(2004, 2012)
-    T = len(months)
-    X = _rand(G, T, P, P, seed=93)
-    X = X + X.transpose(-1, -2)
-    R = _rand(G, T, P, seed=94)
-    monkeypatch.delenv("PFML_WSUM_ROWS", raising=False)
-    pair = _chunked_windows_all_ranks(X, R, months, years, 1, gpu)
-    monkeypatch.setenv("PFML_WSUM_ROWS", "1")
-    rows = _chunked_windows_all_ranks(X, R, months, years, 1, gpu)
-    assert sorted(pair) == sorted(rows)
-    for y in pair:
-        assert torch.equal(pair[y][0], rows[y][0]), y
-
-
 def test_quadform_two_months_bitwise(gpu, monkeypatch):
     """Two validation months per workgroup (shared beta tiles) give BITWISE the utilities of
     one month per workgroup (same per-month MFMA order), incl. an odd job out and n < 64."""
