@@ -419,7 +419,7 @@ nat.register_hip("pfml_mfunc_sym", [C.POINTER(_MfArgs), C.c_void_p])
 nat.register_hip("pfml_mf_args_size", [])
 nat.register_hip("pfml_db_mu", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_int64,
                                 C.c_int, C.c_void_p, C.c_void_p, C.c_void_p])
-nat.register_hip("pfml_db_mu_work_doubles", [C.c_int])
+nat.register_hip("pfml_db_mu_work_doubles2", [C.c_int, C.c_int], C.c_int64)
 
 
 def _sym(x: torch.Tensor) -> torch.Tensor:
@@ -525,7 +525,8 @@ def _db_mu(M: torch.Tensor, Minv: torch.Tensor, unscaled: bool, out: torch.Tenso
         lib = nat.hip_lib()
         if not unscaled:                         # (unscaled steps launch no norm pass)
             _work.add("db_norm_partial_kernel", 4.0 * B * N * N, 16.0 * B * N * N)
-        wbuf = torch.empty(lib.pfml_db_mu_work_doubles(B), dtype=torch.float64, device=M.device)
+        wbuf = torch.empty(lib.pfml_db_mu_work_doubles2(B, N), dtype=torch.float64,
+                           device=M.device)
         nat.check(lib.pfml_db_mu(M.data_ptr(), Minv.data_ptr(), B, N, N, N * N, int(unscaled),
                                  out.data_ptr(), wbuf.data_ptr(), nat.stream_of(M)), "pfml_db_mu")
         return
