@@ -170,10 +170,6 @@ def auto_month_batch(n_stocks: int, gp: int, device, cap: int = 1024) -> int:
 # S4+S5+S6 on one MI355X (A/B on one box): 1 stream 357.6, 2: 345.5, 3: 341.4, 4: 340.8 ms
 # (profiles/r05_s4_streams_ab.json; 4 hardware queues per process).  1: one stream.
 S4_STREAMS = int(os.environ.get("PFML_S4_STREAMS", "3"))
-# PFML_S4_STAGGER=1: batch k's m_func phase (standardise, Sigma, m_tilde) starts only after
-# batch k-1's has ended, so the streams run out of phase - one batch's latency-bound m_func
-# under another's Horner GEMMs instead of all of them in the same phase (A/B switch)
-S4_STAGGER = os.environ.get("PFML_S4_STAGGER", "0") == "1"
 _STREAMS: dict = {}
 
 
@@ -518,15 +514,12 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
     if streams:                     # side streams fork from (and below join) the caller's
         for st_ in streams:
             st_.wait_stream(torch.cuda.current_stream(dev))
-    ev_a = None
     for kb, bt in enumerate(plan.batches):
         B = len(bt.months)
         sing = sing_all[kb % len(sing_all)]
         nsing_t = nsing_all[kb % len(nsing_all)]
         ctx = torch.cuda.stream(streams[kb % len(streams)]) if streams else contextlib.nullcontext()
         with ctx:
-            if streams and S4_STAGGER and ev_a is not None:
-                torch.cuda.current_stream(dev).wait_event(ev_a)
             range_push("pfml_inputs.batch")
             # signals of every distinct g, written into one [B, 13, N, Gc*Pp] stack
             # signals (K11/K12): lags 0, 11 and 12 materialised (signal_t, T_11's S block, U_0's
@@ -573,9 +566,6 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
             mt, a = la.m_tilde(Sigma, bt.lam, bt.w, bt.rf, mu, gamma, cfg.run.iterations,
                                mask=bt.mask, status=None if mstat is None else mstat[b0:b0 + B],
                                sigma_exact_sym=prec == "fp64")
-            if streams and S4_STAGGER:
-                ev_a = torch.cuda.Event()
-                ev_a.record()
             if m_keep is not None:
                 sel = [(bi, kpos[int(d)]) for bi, d in enumerate(bt.months) if int(d) in kpos]
                 if sel:
