@@ -62,6 +62,12 @@ for step in ${MODE//,/ }; do
       rc=$?; tail -1 $OUT/prof_s4r.log | cut -c1-300; if [ $rc -ne 0 ]; then tail -5 $OUT/prof_s4r.log; exit $rc; fi
       python tools/roofline_s4.py $(find $OUT/prof_s4r -name "*.db" | head -1) $OUT/work_ledger.json > $OUT/roofline_s4.md 2>&1
       rc=$?; cat $OUT/roofline_s4.md | head -30; python tools/rocprof_summary.py $(find $OUT/prof_s4r -name "*.db" | head -1) --top 40 > $OUT/kernels_s4r.txt 2>&1; rm -rf $OUT/prof_s4r; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    stressroof)
+      # roofline of the 3000-stock stress: one eager S4 of 16 months on one stream
+      (cd /tmp && export TMPDIR=/tmp PFML_S4_STREAMS=1 PFML_WORK_LEDGER=$OUT/work_ledger_stress.json && timeout -k 10 600 rocprofv3 --kernel-trace -d $OUT/prof_sr -o run -- python3 $ROOT/bench.py --s4-stress 16 --stocks 3000 --warmup 0 > $OUT/prof_sr.log 2>&1)
+      rc=$?; tail -1 $OUT/prof_sr.log | cut -c1-300; if [ $rc -ne 0 ]; then tail -5 $OUT/prof_sr.log; exit $rc; fi
+      python tools/roofline_s4.py $(find $OUT/prof_sr -name "*.db" | head -1) $OUT/work_ledger_stress.json > $OUT/roofline_stress.md 2>&1
+      rc=$?; head -40 $OUT/roofline_stress.md; python tools/rocprof_summary.py $(find $OUT/prof_sr -name "*.db" | head -1) --top 40 > $OUT/kernels_sr.txt 2>&1; rm -rf $OUT/prof_sr; if [ $rc -ne 0 ]; then exit $rc; fi ;;
     dgemmpmc)
       # in-house DGEMM on the Horner shape / large squares: TF/s, then one PMC pass
       timeout -k 10 200 python tools/micro/dgemm_shapes.py 5 > $OUT/dgemm_shapes.log 2>&1
