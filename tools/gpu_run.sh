@@ -169,6 +169,10 @@ for step in ${MODE//,/ }; do
       # per-rank S4 + S5 + S6 of W = 1, 2, 4, 8 rank shards on this GPU (whole-node projection)
       timeout -k 10 900 python tools/bench_shard.py --with-inputs 1,2,4,8 2 > $OUT/shard_s4.json 2> $OUT/shard_s4.err
       rc=$?; cat $OUT/shard_s4.json; if [ $rc -ne 0 ]; then tail -5 $OUT/shard_s4.err; exit $rc; fi ;;
+    shard8)
+      # per-rank S4 + step of the W = 8 shards only (PFML_* A/B switches from the caller)
+      timeout -k 10 600 python tools/bench_shard.py --with-inputs 8 2 > $OUT/shard8_s4.json 2> $OUT/shard8_s4.err
+      rc=$?; cat $OUT/shard8_s4.json; if [ $rc -ne 0 ]; then tail -5 $OUT/shard8_s4.err; exit $rc; fi ;;
     segtl)
       # kernel timeline of the segmented (multi-rank form) grid step: RCCL at a forced world of
       # one, the process group from the env (no launcher under the profiler)
