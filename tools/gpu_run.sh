@@ -173,6 +173,11 @@ for step in ${MODE//,/ }; do
       # per-rank S4 + step of the W = 8 shards only (PFML_* A/B switches from the caller)
       timeout -k 10 600 python tools/bench_shard.py --with-inputs 8 2 > $OUT/shard8_s4.json 2> $OUT/shard8_s4.err
       rc=$?; cat $OUT/shard8_s4.json; if [ $rc -ne 0 ]; then tail -5 $OUT/shard8_s4.err; exit $rc; fi ;;
+    shard8prof)
+      # kernel stats of rank 0's S4 + step at W = 8 on one stream (serial: the latency floor)
+      (cd /tmp && export TMPDIR=/tmp PFML_S4_STREAMS=1 && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_sh8 -o run -- python3 $ROOT/tools/bench_shard.py --with-inputs 8 1 0 > $OUT/prof_sh8.log 2>&1)
+      rc=$?; tail -2 $OUT/prof_sh8.log | cut -c1-300; if [ $rc -ne 0 ]; then exit $rc; fi
+      python tools/rocprof_summary.py $(find $OUT/prof_sh8 -name "*.db" | head -1) --top 45 > $OUT/kernels_sh8.txt 2>&1; rm -rf $OUT/prof_sh8; cat $OUT/kernels_sh8.txt ;;
     segtl)
       # kernel timeline of the segmented (multi-rank form) grid step: RCCL at a forced world of
       # one, the process group from the env (no launcher under the profiler)
