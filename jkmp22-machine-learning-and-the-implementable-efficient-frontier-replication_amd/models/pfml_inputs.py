@@ -641,7 +641,7 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
             # [X | r | 0]' omega: X' omega for the risk term and r_tilde = omega' r (row K) in
             # one GEMM
             XtO = torch.empty((B, Kf + 2, GP), dtype=torch.float64, device=dev)
-            gemm_fused(Xr, omega, XtO, trans_a=True)
+            gemm_fused(Xr, omega, XtO, trans_a=True, tile_cfg=7)     # (K + 2 rows: 64-row tiles)
             rt_ = XtO[:, Kf]                                                     # [B, GP]
             FXO = gemm(Fb, XtO[:, :Kf], backend="own")
             SO = torch.empty_like(omega)
