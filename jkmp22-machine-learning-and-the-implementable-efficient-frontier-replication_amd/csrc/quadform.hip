@@ -22,6 +22,7 @@
 // float atomics).
 #include "common.h"
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -225,6 +226,152 @@ __global__ __launch_bounds__(NT, MM == 1 ? 3 : 2) void quadform_kernel(
   }
 }
 
+// Direct-A form.  A wave's D rows are private to it (16 rows per wave, the tile's four waves
+// disjoint), so D needs no LDS staging at all: every lane loads its own MFMA A fragments
+// straight from global memory into registers, two K steps ahead (a ring of three 4-double
+// fragment sets), and only the beta K-tile - shared by the four waves - goes through LDS.
+// That takes the D tile's ds_writes, its masking pass and its place in the per-step vmcnt
+// wait out of every step; the D stream (from HBM) has two steps to land.
+//   k assignment within a 16-deep step: MFMA slice s takes k = k0 + 4c + s for lane group
+//   c = lane >> 4, so lane (r, c) reads D[row r][k0 + 4c .. k0 + 4c + 3] - four consecutive
+//   doubles of its row per step - and beta's LDS image is read at the same k.
+//   beta image: row l (16 doubles = 32 banks), element k at l * 16 + (k ^ g(l)),
+//   g(l) = (m & 3) | ((m & 4) << 1), m = (l >> 1) & 7: the fragment reads (16 rows x 2 lane
+//   groups per half-wave) hit all 64 banks, the staging writes 2-way at most.
+// Same tile grid, partial slots and epilogue as quadform_kernel<1>; the k summation order
+// differs (bits differ from that form, same on every rank count).
+__device__ __forceinline__ int qd_swz(int l) {
+  const int m = (l >> 1) & 7;
+  return (m & 3) | ((m & 4) << 1);
+}
+
+__global__ __launch_bounds__(NT, 3) void quadform_direct_kernel(
+    const double* __restrict__ D, int64_t ldD, const double* __restrict__ R,
+    const double* __restrict__ Bt, int64_t ldB, const JobDesc* __restrict__ jobs,
+    const int* __restrict__ tile_job, int L, double* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) double Bs[2][NCOL * BK];
+  static_assert(NW * NCOL <= 2 * NCOL * BK, "cross-wave sums must fit in the beta buffers");
+  double (*red)[NCOL] = reinterpret_cast<double (*)[NCOL]>(&Bs[0][0]);
+
+  const int tile = blockIdx.x;
+  const int tj = tile_job[tile];
+  const int jm = tj >> 5, rt = tj & 31;
+  const JobDesc jd = jobs[jm];
+  const int i0 = rt * BM;
+  const int nfull = jd.n;
+  const int n = quad_main(nfull);
+  const bool tail = n != nfull;
+  const double* Dm = D + jd.d_off;
+  const double* rm = R + jd.r_off;
+  const double* bt = Bt + jd.b_off;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int r = lane & 15, c = lane >> 4;
+  const int swz = qd_swz(r);                      // g(16 q + r) = g(r)
+
+  double4_t acc[NTILE];
+#pragma unroll
+  for (int q = 0; q < NTILE; ++q) acc[q] = double4_t{0.0, 0.0, 0.0, 0.0};
+
+  // this lane's D row (clamped: rows past n feed accumulator rows the epilogue drops)
+  const double* drow = Dm + (int64_t)min(i0 + w * 16 + r, n - 1) * ldD;
+  double da[3][4];                                 // A fragments of steps s, s + 1, s + 2
+  auto dload = [&](int slot, int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) da[slot][u] = drow[min(k0 + 4 * c + u, n - 1)];
+  };
+  constexpr int BQ = (NCOL * BK) / NT;             // 7 beta elements per thread per step
+  double rb[BQ];
+  auto bload = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) {
+      const int e = t + q * NT, l = e / BK, k = e % BK;
+      rb[q] = bt[(int64_t)min(l, L - 1) * ldB + min(k0 + k, n - 1)];
+    }
+  };
+  auto bstore = [&](int buf, int k0) {
+#pragma unroll
+    for (int q = 0; q < BQ; ++q) {
+      const int e = t + q * NT, l = e / BK, k = e % BK;
+      Bs[buf][l * BK + (k ^ qd_swz(l))] = (l < L && k0 + k < n) ? rb[q] : 0.0;
+    }
+  };
+
+  const int nst = (n - i0 + BK - 1) / BK;          // K steps of this row tile
+  bload(i0);
+  dload(0, i0);
+  if (nst > 1) dload(1, i0 + BK);
+  bstore(0, i0);
+  __syncthreads();
+  // one K step; SLOT = st % 3 as a compile-time constant (the fragment ring stays in
+  // registers: the step loop below is unrolled by three)
+  auto step = [&](auto slot_c, int st) -> bool {
+    constexpr int cur = decltype(slot_c)::value;
+    const int k0 = i0 + st * BK;
+    const int buf = st & 1;
+    const bool more = st + 1 < nst;
+    // beta of the next step first, then D two steps ahead: the end-of-step wait for beta
+    // leaves the D loads in flight (vmcnt counts in issue order)
+    if (more) bload(k0 + BK);
+    if (st + 2 < nst) dload((cur + 2) % 3, k0 + 2 * BK);
+    // the diagonal block (k < i0 + 64) weighted 1/2: acc = U / 2 (see quadform_kernel)
+    const double wd = (k0 < i0 + BM) ? 0.5 : 1.0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int k = k0 + 4 * c + s;
+      const double a = (k < n) ? wd * da[cur][s] : 0.0;
+#pragma unroll
+      for (int q = 0; q < NTILE; ++q) {
+        const double b = Bs[buf][(q * 16 + r) * BK + ((4 * c + s) ^ swz)];
+        acc[q] = mfma_f64_16x16x4(a, b, acc[q]);
+      }
+    }
+    if (!more) return false;
+    bstore(buf ^ 1, k0 + BK);
+    __syncthreads();
+    return true;
+  };
+  for (int st = 0;; st += 3) {
+    if (!step(std::integral_constant<int, 0>{}, st)) break;
+    if (!step(std::integral_constant<int, 1>{}, st + 1)) break;
+    if (!step(std::integral_constant<int, 2>{}, st + 2)) break;
+  }
+  __syncthreads();                                 // red reuses Bs
+
+  if (tail) {
+#pragma unroll
+    for (int q = 0; q < NTILE; ++q) {
+      const int l = min(q * 16 + (lane & 15), L - 1);
+      const double bt_l = bt[(int64_t)l * ldB + n];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int gi = min(i0 + w * 16 + PFML_F64_CROW(lane, rr), n - 1);
+        acc[q][rr] = fma(Dm[(int64_t)gi * ldD + n], bt_l, acc[q][rr]);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NTILE; ++q) {
+    const int l = q * 16 + (lane & 15);
+    double s = 0.0;
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int gi = i0 + w * 16 + PFML_F64_CROW(lane, rr);
+      if (gi < n && l < L) s += bt[(int64_t)l * ldB + gi] * (rm[gi] - acc[q][rr]);
+    }
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    if (lane < 16) red[w][l] = s;
+  }
+  __syncthreads();
+  if (t < L) {
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) s += red[q][t];
+    partial[(int64_t)(jd.ptile0 + rt) * L + t] = s;
+  }
+}
+
 __global__ void quadform_reduce_kernel(const double* __restrict__ partial,
                                        const JobDesc* __restrict__ jobs, int njobs, int L,
                                        const double* __restrict__ D, int64_t ldD,
@@ -252,15 +399,19 @@ extern "C" int pfml_quadform_job_desc_size() { return (int)sizeof(JobDesc); }
 extern "C" int pfml_quadform_rows_per_tile() { return BM; }
 extern "C" int pfml_quadform_row_tiles(int n) { return (quad_main(n) + BM - 1) / BM; }
 
-// tile_job: mm (1 or 2) int32 entries per tile (see quadform_kernel).
+// tile_job: mm (1 or 2; 1 for the direct form, mm = 3) int32 entries per tile.
 extern "C" hipError_t pfml_quadform(const double* D, int64_t ldD, const double* R,
                                     const double* Bt, int64_t ldB, const void* jobs, int njobs,
                                     const int* tile_job, int ntiles, int mm, int L,
                                     double* partial, double* obj, hipStream_t st) {
   if (njobs <= 0) return hipSuccess;
-  if (L > NCOL || (mm != 1 && mm != 2)) return hipErrorInvalidValue;
+  // mm: months per tile (1 / 2); 3 = the direct-A form on the one-month tile list
+  if (L > NCOL || mm < 1 || mm > 3) return hipErrorInvalidValue;
   const JobDesc* jd = static_cast<const JobDesc*>(jobs);
-  if (mm == 2)
+  if (mm == 3)
+    hipLaunchKernelGGL(quadform_direct_kernel, dim3(ntiles), dim3(NT), 0, st, D, ldD, R, Bt, ldB,
+                       jd, tile_job, L, partial);
+  else if (mm == 2)
     hipLaunchKernelGGL(quadform_kernel<2>, dim3(ntiles), dim3(NT), 0, st, D, ldD, R, Bt, ldB, jd,
                        tile_job, L, partial);
   else

@@ -829,9 +829,15 @@ def quad_launch(plan: dict, d_desc: torch.Tensor, d_tj: torch.Tensor, D: torch.T
     L, Pb = beta.shape[1], beta.shape[2]
     nt = plan["ntiles"]
     partial = torch.empty((plan["nslots"], L), dtype=torch.float64, device=D.device)
+    # one-month tiles take the direct-A form (csrc/quadform.hip quadform_direct_kernel: D
+    # fragments straight to registers two steps ahead, only beta through LDS) unless
+    # PFML_QUAD_DIRECT=0
+    mm = plan["mm"]
+    if mm == 1 and os.environ.get("PFML_QUAD_DIRECT", "1") != "0":
+        mm = 3
     nat.check(nat.hip_lib().pfml_quadform(D.data_ptr(), P, R.data_ptr(), beta.data_ptr(), Pb,
                                           d_desc.data_ptr(), plan["nj"], d_tj.data_ptr(), nt,
-                                          plan["mm"], L,
+                                          mm, L,
                                           partial.data_ptr(), obj.data_ptr(),
                                           nat.stream_of(D)), "pfml_quadform")
 

@@ -865,6 +865,7 @@ def test_quadform_two_months_bitwise(gpu, monkeypatch):
     jm = np.array([0, 1, 2, 3, 4, 5, 6, 0, 1])
     jn = np.array([130, 130, 130, 65, 65, 33, 33, 33, 33])
     args = (D.to(gpu), R.to(gpu), beta.to(gpu), jc, jm, jn)
+    monkeypatch.setenv("PFML_QUAD_DIRECT", "0")
     monkeypatch.setenv("PFML_QUAD_MM", "1")
     one = quadform_utilities(*args).cpu()
     monkeypatch.setenv("PFML_QUAD_MM", "2")
@@ -872,3 +873,27 @@ def test_quadform_two_months_bitwise(gpu, monkeypatch):
     assert torch.equal(one, two)
     ref = quadform_utilities(D, R, beta, jc, jm, jn)
     assert torch.allclose(two, ref, rtol=1e-11, atol=1e-11)
+    # the direct-A form (default for one-month tiles): its own k order, same oracle
+    monkeypatch.setenv("PFML_QUAD_MM", "1")
+    monkeypatch.setenv("PFML_QUAD_DIRECT", "1")
+    direct = quadform_utilities(*args).cpu()
+    assert torch.allclose(direct, ref, rtol=1e-11, atol=1e-11)
+
+
+@pytest.mark.parametrize("direct", ["0", "1"])
+def test_quadform_production_shape(gpu, monkeypatch, direct):
+    """Both utilities forms at the production cell size (n = 513: nine row tiles, tail index
+    split off) and a mixed launch (n = 257 / 129 / 65 cells), against the CPU oracle."""
+    from pfml.ops.ridge import quadform_utilities
+    monkeypatch.setenv("PFML_QUAD_DIRECT", direct)
+    P, L = 513, 101
+    D = _spd_stack(4, P, n_obs=600, seed=98) / 600
+    R = _rand(4, P, seed=99)
+    beta = 0.1 * _rand(4, L, P, seed=100)
+    jc = np.array([0, 0, 1, 2, 3, 0])
+    jm = np.array([0, 1, 2, 3, 0, 3])
+    jn = np.array([513, 513, 257, 129, 65, 513])
+    out = quadform_utilities(D.to(gpu), R.to(gpu), beta.to(gpu), jc, jm, jn).cpu()
+    ref = quadform_utilities(D, R, beta, jc, jm, jn)
+    rel = ((out - ref).abs() / ref.abs().clamp_min(1e-9)).max().item()
+    assert rel < 1e-10, rel
