@@ -305,6 +305,39 @@ extern "C" hipError_t pfml_db_mu(const double* M, const double* Minv, int B, int
 }
 
 // ---------------------------------------------------------------------------------------
+// Denman-Beavers convergence check before the Newton-Schulz tail step (ops/linalg.py
+// _db_sqrt): the last step replaces M^-1 by its first-order Neumann form 2I - M, whose error
+// is O(|M - I|^2); a matrix with any |M_ij - delta_ij| > tol (or a non-finite entry) sets its
+// status flag, and the month is recomputed by the convergence-checked reference form.  Grid
+// (row slabs, batch): every workgroup that sees a violation stores 1 (no reduction needed).
+// ---------------------------------------------------------------------------------------
+namespace {
+constexpr int CK_ROWS = 16;
+__global__ __launch_bounds__(256) void db_check_kernel(const double* __restrict__ M, int N,
+                                                       int64_t ld, int64_t sX, double tol,
+                                                       int* __restrict__ status) {
+  const int b = blockIdx.y;
+  const int r0 = blockIdx.x * CK_ROWS, r1 = min(N, r0 + CK_ROWS);
+  const double* A = M + (int64_t)b * sX;
+  bool bad = false;
+  for (int i = r0; i < r1; ++i)
+    for (int j = threadIdx.x; j < N; j += 256) {
+      const double d = fabs(A[(int64_t)i * ld + j] - (i == j ? 1.0 : 0.0));
+      bad |= !(d <= tol);                       // NaN counts as not converged
+    }
+  if (__syncthreads_or(bad) && threadIdx.x == 0) status[b] = 1;
+}
+}  // namespace
+
+extern "C" hipError_t pfml_db_check(const double* M, int B, int N, int64_t ld, int64_t sX,
+                                    double tol, int* status, hipStream_t st) {
+  if (B <= 0 || N <= 0) return hipSuccess;
+  hipLaunchKernelGGL(db_check_kernel, dim3((N + CK_ROWS - 1) / CK_ROWS, B), dim3(256), 0, st, M,
+                     N, ld, sX, tol, status);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
 // Horner chain set-up of (24) (models/pfml_inputs.py run_plan), one pass each instead of a
 // chain of torch ops (diag_embed, temporaries, strided multiplies):
 //

@@ -543,16 +543,27 @@ def _db_mu(M: torch.Tensor, Minv: torch.Tensor, unscaled: bool, out: torch.Tenso
 
 
 def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tensor | None,
-             ws: list, exact_sym: bool = False) -> torch.Tensor:
+             ws: list, exact_sym: bool = False, ns_tail: bool | None = None) -> torch.Tensor:
     """sqrtm(S) by ``iters`` scaled product-form Denman-Beavers steps with NO host sync:
     norm scaling mu (computed on the device) for the first ``scaled_iters`` steps, then
     quadratically convergent unscaled steps.  ws: 4 [B, N, N] work buffers; ``exact_sym``: S is
-    exactly symmetric (bit for bit)."""
+    exactly symmetric (bit for bit).
+
+    ``ns_tail`` (default ``DB_NS_TAIL``): the last (unscaled) step takes M^-1 as its
+    first-order Neumann form 2I - M - a Newton-Schulz step Y <- (3Y - Y M) / 2, one product
+    and NO inverse, whose error against the exact step is O(|M - I|^2).  By then M is the
+    identity to 1e-16 .. 1e-10 on production spectra (cond(x^2 + 4x) up to 7e14,
+    profiles/r06_db_tail.json: the exact step changed nothing but the cost of an inverse); a
+    matrix with any |M_ij - delta_ij| > DB_TAIL_TOL (1e-7: tail error < 1e-14) sets ``status``
+    and is recomputed by the convergence-checked reference form, like a failed pivot."""
     B, N, _ = S.shape
     M, Y, Mi, Yn = ws
     M.copy_(S)
     Y.copy_(S)
     mu = torch.empty(B, dtype=S.dtype, device=S.device)
+    if ns_tail is None:
+        ns_tail = DB_NS_TAIL
+    ns_tail = ns_tail and iters > scaled_iters
     # S, M, M^-1 and Y are symmetric (M, Y are polynomials in S; in exact arithmetic Y and M^-1
     # commute, so Y M^-1 is symmetric too).  sym_inv: M^-1 by the one-triangle inverse;
     # sym_prod: Y M^-1 on its lower tiles, mirrored.  With both (and S exactly symmetric, as
@@ -562,6 +573,14 @@ def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tenso
     dev_sym = nat.is_device(M) and N >= _BLOCKED_MIN_N
     sym_inv, sym_prod = DB_SYM and dev_sym, DB_SYMPROD and dev_sym
     for it in range(iters):
+        if ns_tail and it == iters - 1:
+            # Newton-Schulz tail: Y' = 1.5 Y - 0.5 Y M (Y M symmetric, as Y M^-1 is)
+            _db_check(M, DB_TAIL_TOL, status)
+            rs = torch.full((B, N), -0.5, dtype=S.dtype, device=S.device)
+            es = torch.full((B, N), 1.5, dtype=S.dtype, device=S.device)
+            gemm_fused(Y, M, Yn, row_scale=rs, addend=Y, addend_row_scale=es, sym=sym_prod)
+            Y, Yn = Yn, Y
+            break
         if sym_inv:
             spd_inverse_sym(Mi, status, src=M)
         else:
@@ -579,11 +598,26 @@ def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tenso
     return Y
 
 
-# Denman-Beavers steps: 8 reach 1e-14 parity with the reference's scipy sqrtm m_func on
-# production spectra (cond(x^2 + 4x) ~ 1e5-1e7, TC on and off; tests/test_gpu_pipeline.py,
-# tests/test_golden.py); one more for margin.  Norm scaling in the first 6.
-DB_ITERS = 9
+# Denman-Beavers steps: 7 exact steps leave M within 1e-10 of I on production spectra
+# (cond(x^2 + 4x) ~ 1e5 - 7e14, TC on and off; profiles/r06_db_tail.json), the 8th is the
+# Newton-Schulz tail (above; PFML_DB_NS_TAIL=0: an exact 8th step).  The former 9th exact step
+# moved nothing (|M - I| ~ 1e-20 .. 1e-32 at its start).  Norm scaling in the first 6.
+DB_ITERS = 8
 DB_SCALED_ITERS = 6
+DB_NS_TAIL = os.environ.get("PFML_DB_NS_TAIL", "1") != "0"
+DB_TAIL_TOL = 1e-7
+nat.register_hip("pfml_db_check", [C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_int64,
+                                   C.c_double, C.c_void_p, C.c_void_p])
+
+
+def _db_check(M: torch.Tensor, tol: float, status: torch.Tensor | None) -> None:
+    """Flag (status = 1) the matrices of M [B, N, N] with any |M_ij - delta_ij| > tol or a
+    non-finite entry (csrc/s4.hip db_check_kernel); the CPU path has no status to set."""
+    if status is None or not nat.is_device(M):
+        return
+    B, N, _ = M.shape
+    nat.check(nat.hip_lib().pfml_db_check(M.data_ptr(), B, N, M.stride(1), M.stride(0), tol,
+                                          status.data_ptr(), nat.stream_of(M)), "pfml_db_check")
 
 
 def m_tilde(sigma: torch.Tensor, lam: torch.Tensor, w: torch.Tensor, rf: torch.Tensor,

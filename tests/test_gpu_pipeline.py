@@ -100,6 +100,30 @@ def test_db_sqrt_device_matches_eigh(gpu):
     assert (got - ref).abs().max().item() / ref.abs().max().item() < 1e-11
 
 
+def test_db_newton_schulz_tail(gpu):
+    """The Denman-Beavers Newton-Schulz tail (last step with M^-1 = 2I - M): equal to the
+    all-exact steps to rounding, and a matrix whose M is still far from I at the tail
+    (too few steps) is flagged for the reference-form repair instead of returned."""
+    from pfml.ops.linalg import DB_ITERS, DB_SCALED_ITERS, _db_sqrt
+    B, N = 3, 160
+    X = _rand(B, N + 40, N, seed=17)
+    S = X.transpose(1, 2) @ X / N
+    S = S @ S + 1e-3 * torch.eye(N, dtype=torch.float64)
+    Sd = S.to(gpu)
+
+    def run(iters, tail, scaled=DB_SCALED_ITERS):
+        st = torch.zeros(B, dtype=torch.int32, device=gpu)
+        ws = [torch.empty_like(Sd) for _ in range(4)]
+        return _db_sqrt(Sd, iters, scaled, st, ws, ns_tail=tail).cpu(), st.cpu()
+
+    tail, st = run(DB_ITERS, True)
+    exact, st0 = run(DB_ITERS + 1, False)
+    assert int(st.sum()) == 0 and int(st0.sum()) == 0
+    assert (tail - exact).abs().max().item() / exact.abs().max().item() < 1e-13
+    _, st_short = run(3, True, scaled=2)            # tail after two steps: far from I
+    assert st_short.tolist() == [1] * B
+
+
 @pytest.mark.parametrize("tc", [True, False])
 def test_m_tilde_production_shape(gpu, tc):
     """m at N = 496 (padded S&P 500 width) on the device vs the reference-form torch m_func
