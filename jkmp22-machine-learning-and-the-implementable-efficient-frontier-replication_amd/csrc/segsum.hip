@@ -82,40 +82,6 @@ __global__ __launch_bounds__(256) void wsum_upper_kernel(const double* __restric
   const int64_t PP = (int64_t)P * P;
   const double* src = X + (int64_t)g * T * PP + (int64_t)i * P;
   double* dst = seg_slot(out, scratch, g, s, nseg, skip, PP) + (int64_t)i * P;
-  if (b - a == 12) {
-    // an hp-year segment (every segment but the burn-in pieces): all twelve month loads of
-    // both of a lane's columns in flight at once, then the adds in the order of the loop
-    // below (chain u takes months u, u + 4, u + 8), so the sums are bitwise that loop's
-    const int j0 = i + threadIdx.x, j1 = j0 + 256;
-    const int c0 = min(j0, P - 1), c1 = min(j1, P - 1);
-    double x0[12], x1[12];
-#pragma unroll
-    for (int u = 0; u < 12; ++u) x0[u] = src[(int64_t)(a + u) * PP + c0];
-    if (j1 < P) {
-#pragma unroll
-      for (int u = 0; u < 12; ++u) x1[u] = src[(int64_t)(a + u) * PP + c1];
-    }
-    if (j0 < P) {
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int u = 0; u < 12; ++u) acc[u & 3] += x0[u];
-      dst[j0] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    }
-    if (j1 < P) {
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int u = 0; u < 12; ++u) acc[u & 3] += x1[u];
-      dst[j1] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    }
-    if (j1 + 256 >= P) return;                    // P <= i + 512: both columns were all
-    for (int j = j1 + 256; j < P; j += 256) {
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int u = 0; u < 12; ++u) acc[u & 3] += src[(int64_t)(a + u) * PP + j];
-      dst[j] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    }
-    return;
-  }
   for (int j = i + threadIdx.x; j < P; j += 256) {
     // four independent chains: four month loads in flight per lane
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
