@@ -13,6 +13,8 @@
 //             from Sigma on the fly (no sigma_gr / x / base matrices are stored)
 //   MF_DB     M'   = I/2 + (mu^2 sym(M) + mu^-2 sym(Minv))/4    (Denman-Beavers update)
 //   MF_SHAT   out  = sym(X) + d I                                (sigma_hat = x + 2I, root + sigma_hat)
+//   MF_M0     out  = (sym(X) + d I - sym(Y)) / 2                 (m_tilde_0 = (sigma_hat - root) / 2,
+//             the reference's own form, General_functions.py:955)
 //
 // Per-batch scalars (s = gamma / w, c = 1 + rf + mu, mu_DB) and per-row vectors (a = lambda^-1/2,
 // mask) are read from device memory: nothing here needs the host.
@@ -24,7 +26,7 @@ typedef double double2_t __attribute__((ext_vector_type(2)));
 
 constexpr int TS = 32;
 
-enum Mode { MF_X = 0, MF_FIX = 1, MF_DB = 2, MF_SHAT = 3 };
+enum Mode { MF_X = 0, MF_FIX = 1, MF_DB = 2, MF_SHAT = 3, MF_M0 = 4 };
 
 struct MfArgs {
   int mode, B, N;
@@ -86,6 +88,8 @@ __global__ __launch_bounds__(256) void mfunc_sym_kernel(MfArgs p) {
       const double mu2 = s * s;
       v = 0.25 * (mu2 * xs + ys / mu2);
       if (i == j) v += 0.5;
+    } else if (p.mode == MF_M0) {
+      v = 0.5 * ((i == j ? xs + p.d : xs) - ys);
     } else {
       v = xs + ys;
       if (i == j) v += p.d;
@@ -117,6 +121,8 @@ __device__ __forceinline__ double mf_value(const MfArgs& p, int i, int j, double
     const double mu2 = s * s;
     v = 0.25 * (mu2 * xs + ys / mu2);
     if (i == j) v += 0.5;
+  } else if (p.mode == MF_M0) {
+    v = 0.5 * ((i == j ? xs + p.d : xs) - ys);
   } else {
     v = xs + ys;
     if (i == j) v += p.d;

@@ -405,7 +405,7 @@ def sqrtm_spd(S: torch.Tensor, max_iter: int = 40, tol: float = 1e-13) -> torch.
 # ---------------------------------------------------------------------------------------
 # Fused symmetric passes (csrc/s4.hip) and the device m_func
 # ---------------------------------------------------------------------------------------
-MF_X, MF_FIX, MF_DB, MF_SHAT = 0, 1, 2, 3
+MF_X, MF_FIX, MF_DB, MF_SHAT, MF_M0 = 0, 1, 2, 3, 4
 
 
 class _MfArgs(C.Structure):
@@ -467,6 +467,8 @@ def mf_sym(mode: int, X: torch.Tensor, Y: torch.Tensor | None, out: torch.Tensor
     elif mode == MF_DB:
         mu2 = (svec * svec).view(B, 1, 1)
         r = 0.25 * (mu2 * xs + ys / mu2) + 0.5 * eye
+    elif mode == MF_M0:
+        r = 0.5 * ((xs + d * eye) - ys)
     else:
         r = xs + (ys if ys is not None else 0.0) + d * eye
     out.copy_(r)
@@ -606,6 +608,8 @@ DB_ITERS = 8
 DB_SCALED_ITERS = 6
 DB_NS_TAIL = os.environ.get("PFML_DB_NS_TAIL", "1") != "0"
 DB_TAIL_TOL = 1e-7
+# m_tilde_0 by the reference's (sigma_hat - root) / 2 (one pass) instead of the inverse form
+M0_CANCEL = os.environ.get("PFML_M0_CANCEL", "1") != "0"
 nat.register_hip("pfml_db_check", [C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_int64,
                                    C.c_double, C.c_void_p, C.c_void_p])
 
@@ -655,16 +659,25 @@ def m_tilde(sigma: torch.Tensor, lam: torch.Tensor, w: torch.Tensor, rf: torch.T
     gemm_fused(x, x, S, addend=x, addend_row_scale=four, sym=True)
     ws = [torch.empty_like(sigma) for _ in range(4)]
     root = _db_sqrt(S, db_iters, DB_SCALED_ITERS, status, ws, exact_sym=True)
-    # m_tilde_0 = (sigma_hat - root)/2 = 2 (sigma_hat + root)^-1   (cancellation-free form)
+    # m_tilde_0 = (sigma_hat - root) / 2, the reference's form (General_functions.py:955), in
+    # one pass.  Its cancellation costs accuracy only along the large eigenvalues l of x (error
+    # ~ eps l there), and the first fixed-point step maps an error along such a direction to
+    # ~eps / l (the step's derivative there is ~(x + 2I)^-2): m after the ten steps equals the
+    # cancellation-free 2 (sigma_hat + root)^-1 start's to rounding, also with eig(x) up to 6e7
+    # (TC off) and down to 3e-7 (profiles/r06_m0_form.json) - one SPD inverse per month fewer.
     mt = ws[2]
     # (x is exactly symmetric - MF_X symmetrises - and so is root when its last product was
     # the one-triangle one)
-    mf_sym(MF_SHAT, x, root, mt, d=2.0, flat=DB_SYMPROD and db_iters > 0
-           and nat.is_device(x) and N >= _BLOCKED_MIN_N)
-    # (the 11 inverses below are of exactly symmetric arguments and only used symmetrically:
+    flat_root = DB_SYMPROD and db_iters > 0 and nat.is_device(x) and N >= _BLOCKED_MIN_N
+    if M0_CANCEL:
+        mf_sym(MF_M0, x, root, mt, d=2.0, flat=flat_root)
+    else:                      # 2 (sigma_hat + root)^-1 (PFML_M0_CANCEL=0: the former form)
+        mf_sym(MF_SHAT, x, root, mt, d=2.0, flat=flat_root)
+        # (an exactly symmetric argument, used symmetrically: the one-triangle form)
+        spd_inverse_sym(mt, status)
+        mt.mul_(2.0)
+    # (the 10 inverses below are of exactly symmetric arguments and only used symmetrically:
     # the one-triangle form)
-    spd_inverse_sym(mt, status)
-    mt.mul_(2.0)
     Aq = ws[3]
     for _ in range(iterations):
         mf_sym(MF_FIX, sigma, mt, Aq, svec=s, cvec=c, a=a, mask=mask, flat=flat)
