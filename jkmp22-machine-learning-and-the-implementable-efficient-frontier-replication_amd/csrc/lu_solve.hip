@@ -548,8 +548,13 @@ hipError_t lu_solve_2level(double* M, int n, int m, int64_t ldm, int64_t sM, int
       int* pv = piv + (int64_t)((k0 - K0) / NB) * batch * NB;
       hipError_t e = lu_pivot_launch<NB, PMAX>(M, n, ldm, sM, a0, k0, nb, pv, status, batch, st);
       if (e != hipSuccess) return e;
-      // live set of the inner step: A columns k0 .. aend (swap) / right of the block, and Z
-      const int nswap = (aend - k0) + kb;
+      // live set of the inner step: A columns k0 .. aend (swap) / right of the block, and the
+      // Z columns populated so far - the unit columns of the earlier inner blocks (swap) plus
+      // this block's (update).  Z's later columns are still zero: a swap or a rank-NB update
+      // of them is an exact no-op (x - C 0 = x), so they are not touched (the update streams
+      // 128 + 128 instead of 224 / 192 / 160 / 128 columns per inner block)
+      const int zlive = k0 - K0;
+      const int nswap = (aend - k0) + zlive;
       hipLaunchKernelGGL((lu_swap_kernel<NB>), dim3((nswap + 255) / 256, batch), dim3(256), 0, st,
                          M, ldm, sM, nswap, a0 + k0, aend - k0, z0, k0, nb, pv);
       hipLaunchKernelGGL(lu_zunit_kernel, dim3(batch), dim3(64), 0, st, M, ldm, sM, k0,
@@ -557,7 +562,7 @@ hipError_t lu_solve_2level(double* M, int n, int m, int64_t ldm, int64_t sM, int
       hipLaunchKernelGGL((lu_blockinv_kernel<NB>), dim3(batch), dim3(256), 0, st, M, ldm, sM, a0,
                          k0, nb, Pbuf);
       const int nA = aend - (k0 + nb);
-      const int nlive = nA + kb;
+      const int nlive = nA + zlive + nb;
       hipLaunchKernelGGL((lu_rowpanel_kernel<NB>), dim3((nlive + 255) / 256, batch), dim3(256), 0,
                          st, M, ldm, sM, nlive, a0 + k0 + nb, nA, z0, k0, nb, Pbuf, Rbuf);
       hipLaunchKernelGGL((lu_snapshot_kernel<NB>), dim3((n + 255) / 256, batch), dim3(256), 0, st,

@@ -280,7 +280,7 @@ def _lu_ledger(M, n, m, ldm, sM, a0, b0, z0, batch) -> None:
         aend = K0 + kb
         for k0 in range(K0, aend, nb):
             b = min(nb, aend - k0)
-            nlive = aend - (k0 + b) + kb
+            nlive = aend - (k0 + b) + (k0 - K0) + b      # (only Z's populated columns)
             _work.add(upd, 2.0 * batch * n * nlive * b, 8.0 * batch * 2 * n * nlive)
             _work.add(piv, 2.0 * batch * (n - k0) * b * b, 8.0 * batch * (n - k0) * b)
         nAr = n - aend
