@@ -83,6 +83,7 @@ class SearchPlan:
     count: np.ndarray                  # [nY] months in the expanding window of year Y
     val_start: np.ndarray              # [nY] validation month rows [(Y-1)-12, Y-11]
     val_stop: np.ndarray
+    n_months: int = 0                  # months in the list the plan was made for
 
 
 def make_plan(months: np.ndarray, years: np.ndarray) -> SearchPlan:
@@ -98,7 +99,8 @@ def make_plan(months: np.ndarray, years: np.ndarray) -> SearchPlan:
     val_start = np.searchsorted(months, [mi_from_ym(y - 1, 12) for y in years], side="left")
     val_stop = np.searchsorted(months, [mi_from_ym(y, 11) for y in years], side="right")
     return SearchPlan(np.asarray(years), seg_start.astype(np.int64), seg_stop.astype(np.int64),
-                      burn_stop, count, val_start.astype(np.int64), val_stop.astype(np.int64))
+                      burn_stop, count, val_start.astype(np.int64), val_stop.astype(np.int64),
+                      len(months))
 
 
 NCHUNK = 8            # canonical chunks per kind (covers world 1, 2, 4, 8 bitwise alike)
@@ -107,19 +109,54 @@ NCHUNK = 8            # canonical chunks per kind (covers world 1, 2, 4, 8 bitwi
 @dataclass
 class WinLayout:
     """World-size independent cut of the month axis for the window sums: C burn-in pieces
-    (global month rows [a, b), near-equal, possibly empty) and C groups of consecutive hp
-    years.  Chunk c of either kind belongs to rank c * world // C."""
+    (global month rows [a, b), possibly empty, sized to balance the per-rank S4 months) and C
+    groups of consecutive hp years.  Chunk c of either kind belongs to rank c * world // C."""
     C: int
     burn: list
     ychunks: list
 
 
 def win_layout(plan: "SearchPlan", nY: int, world: int) -> WinLayout:
+    """The year chunks are near-equal in years; the burn-in months are cut so that burn piece
+    c plus year chunk c (its months, and for the last chunk the months after the last block,
+    which its owner also builds) are near-equal in MONTHS - the per-rank S4 load, since rank r
+    of a W-rank run owns pieces and chunks c with c * W // C == r.  (Equal burn pieces left a
+    W = 8 run 95 / 82 months on its busiest / lightest ranks.)  The cut depends on C only,
+    never on the world size, so the window sums stay bitwise the same on every world size."""
     C = max(NCHUNK, int(world))
     nb = int(plan.burn_stop)
-    burn = [(r.start, r.stop) for r in (coll.contiguous_split(nb, C, k) for k in range(C))]
     ych = [coll.contiguous_split(nY, C, c) for c in range(C)]
+    ym = np.zeros(C, np.int64)
+    for c, ys in enumerate(ych):
+        if len(ys):
+            ym[c] = int(plan.seg_stop[ys[-1]]) - int(plan.seg_start[ys[0]])
+    if nY and len(ych[-1]):
+        ym[-1] += int(plan.n_months) - int(plan.seg_stop[-1])
+    sizes = _water_fill(nb, ym)
+    off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    burn = [(int(off[k]), int(off[k + 1])) for k in range(C)]
     return WinLayout(C, burn, ych)
+
+
+def _water_fill(total: int, base: np.ndarray) -> np.ndarray:
+    """Non-negative integers s (sum = total) making base + s as level as possible: s_c =
+    max(0, level - base_c) for the level that spends ``total``, the remainder dealt one by one
+    to the lowest base + s (ties: the lower index) - deterministic."""
+    base = np.asarray(base, np.int64)
+    s = np.zeros(len(base), np.int64)
+    if total <= 0 or len(base) == 0:
+        return s
+    lo, hi = int(base.min()), int(base.max()) + total
+    while lo < hi:                       # largest level whose fill does not exceed total
+        mid = (lo + hi + 1) // 2
+        if int(np.maximum(0, mid - base).sum()) <= total:
+            lo = mid
+        else:
+            hi = mid - 1
+    s = np.maximum(0, lo - base)
+    for _ in range(int(total - s.sum())):
+        s[int(np.argmin(base + s))] += 1
+    return s
 
 
 def chunk_owner(c: int, C: int, world: int) -> int:
