@@ -221,7 +221,147 @@ __global__ __launch_bounds__(1024) void standardize_reg_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Signal statistics of lags 1..10 by differences (models/pfml_inputs.py run_plan).  Lag theta
+// of month b standardises the rows of b's universe at date d = b - theta; the ten months that
+// read date d have nearly the same universe (a few names enter or leave per month), so the
+// column sums over U(d) = the union of those universes' rows at d are formed ONCE per date
+// (date_sums_kernel) and each (b, theta) subtracts the few rows of U(d) outside its own
+// universe (excl_stats_kernel) - instead of re-reading ~N gathered rows per (b, theta).
+//   dsum[d] = [S1 = sum (x - K), S2 = sum (x - K)^2, K] over U(d), K = x of U(d)'s first row
+//   (t1, t2) = (S1, S2) - the same sums over the excluded rows, then the standardize kernels'
+//   mean / scale formulas (shifted moments: no cancellation of raw ones).
+// U(d) is built from the GLOBAL month grid and every sum runs in a fixed order, so a month's
+// statistics are bitwise the same however the months are sharded or batched.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void date_sums_kernel(const double* __restrict__ F, int P,
+                                                         int64_t ldf,
+                                                         const int64_t* __restrict__ urows,
+                                                         const int* __restrict__ un, int umax,
+                                                         int Pw, double* __restrict__ dsum) {
+  constexpr int NP = 16;
+  __shared__ double red[NP][64], red2[NP][64];
+  const int d = blockIdx.y;
+  const int t = threadIdx.x, lane = t & 63;
+  const int part = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int c = blockIdx.x * 64 + lane;
+  const int cc = min(c, P - 1);
+  const int n = un[d];
+  const int64_t* rw = urows + (int64_t)d * umax;
+  const double K = (n > 0) ? F[rw[0] * ldf + cc] : 0.0;
+  double s1 = 0.0, s2 = 0.0;
+  for (int i0 = part; i0 < n; i0 += 8 * NP) {
+    double x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + NP * u;
+      x[u] = (i < n) ? F[rw[i] * ldf + cc] - K : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      s1 += x[u];
+      s2 += x[u] * x[u];
+    }
+  }
+  red[part][lane] = s1;
+  red2[part][lane] = s2;
+  __syncthreads();
+  if (part == 0 && c < Pw) {
+    double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+      t1 += red[q][lane];
+      t2 += red2[q][lane];
+    }
+    double* o = dsum + (int64_t)d * 3 * Pw;
+    o[c] = t1;
+    o[Pw + c] = t2;
+    o[2 * Pw + c] = K;
+  }
+}
+
+__global__ __launch_bounds__(256) void excl_stats_kernel(
+    const double* __restrict__ F, int P, int64_t ldf, const int64_t* __restrict__ erows,
+    const int* __restrict__ en, int emax, const int* __restrict__ dpos,
+    const double* __restrict__ dsum, const int* __restrict__ n_real, int TH, int Pw,
+    double* __restrict__ stats, int64_t lds) {
+  constexpr int NP = 4;
+  __shared__ double red[NP][64], red2[NP][64];
+  const int bt = blockIdx.y, b = bt / TH;
+  const int t = threadIdx.x, lane = t & 63;
+  const int part = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int c = blockIdx.x * 64 + lane;
+  const int cc = min(c, P - 1);
+  const int ne = en[bt];
+  const int64_t* rw = erows + (int64_t)bt * emax;
+  const double* ds = dsum + (int64_t)dpos[bt] * 3 * Pw;
+  const int cw = min(c, Pw - 1);
+  const double K = ds[2 * Pw + cw];
+  double e1 = 0.0, e2 = 0.0;
+  for (int i0 = part; i0 < ne; i0 += 4 * NP) {
+    double x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + NP * u;
+      x[u] = (i < ne) ? F[rw[i] * ldf + cc] - K : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      e1 += x[u];
+      e2 += x[u] * x[u];
+    }
+  }
+  red[part][lane] = e1;
+  red2[part][lane] = e2;
+  __syncthreads();
+  if (part != 0 || c >= Pw) return;
+  double u1 = 0.0, u2 = 0.0;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    u1 += red[q][lane];
+    u2 += red2[q][lane];
+  }
+  const double t1 = ds[c] - u1, t2 = ds[Pw + c] - u2;
+  const double n = (double)n_real[b];
+  double mu, sc;
+  if (c == 0) {                                          // constant column: not demeaned
+    mu = 0.0;
+    const double tk = t1 + n * K;
+    sc = sqrt(1.0 / (t2 + 2.0 * K * tk - n * K * K));
+  } else {
+    mu = K + t1 / n;
+    sc = sqrt(1.0 / (t2 - t1 * t1 / n));
+  }
+  stats[(int64_t)bt * 2 * lds + c] = c < P ? mu : 0.0;
+  stats[(int64_t)bt * 2 * lds + lds + c] = c < P ? sc : 0.0;
+}
+
 }  // namespace
+
+// per-date shifted column sums over U(d): urows [nd, umax] panel rows (first un[d] real),
+// dsum [nd, 3, Pw] (S1, S2, K rows)
+extern "C" hipError_t pfml_date_sums(const double* F, int P, int64_t ldf, const int64_t* urows,
+                                     const int* un, int umax, int nd, int Pw, double* dsum,
+                                     hipStream_t st) {
+  if (nd <= 0) return hipSuccess;
+  if (Pw < P || ldf < P) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(date_sums_kernel, dim3((Pw + 63) / 64, nd), dim3(1024), 0, st, F, P, ldf,
+                     urows, un, umax, Pw, dsum);
+  return hipGetLastError();
+}
+
+// statistics of the B x TH tiles (b, theta) from their date's sums minus their excluded rows:
+// erows [B * TH, emax] (first en[.] real), dpos [B * TH] date slot, stats as pfml_standardize
+extern "C" hipError_t pfml_excl_stats(const double* F, int P, int64_t ldf, const int64_t* erows,
+                                      const int* en, int emax, const int* dpos,
+                                      const double* dsum, const int* n_real, int B, int TH,
+                                      int Pw, double* stats, int64_t lds, hipStream_t st) {
+  if (B <= 0 || TH <= 0) return hipSuccess;
+  if (Pw < P || ldf < P || lds < Pw) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(excl_stats_kernel, dim3((Pw + 63) / 64, B * TH), dim3(256), 0, st, F, P, ldf,
+                     erows, en, emax, dpos, dsum, n_real, TH, Pw, stats, lds);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t pfml_rff_sincos(const double* Z, int64_t R, int half, double* out,
                                       int64_t ldo, hipStream_t st) {

@@ -48,7 +48,8 @@ from ..config import Config, get_features, interleaved_order
 from ..data import io
 from ..ops import linalg as la
 from ..ops.gemm import gemm, gemm_fused, gemm_prec
-from ..ops.panel import rff_features, signal_stats, standardize_signals
+from ..ops.panel import (date_sums, excl_stats, rff_features, signal_stats,
+                         standardize_signals)
 from ..utils.dates import month_index, pfml_date_grids
 from ..utils.log import COUNTERS, get_logger
 from ..utils.trace import range_pop, range_push
@@ -184,6 +185,44 @@ def _s4_streams(dev, n_batches: int):
     return _STREAMS[key]
 
 
+# statistics of lags 1..10 (the Horner steps' gathered addend) from per-date union sums minus
+# each month's few excluded rows (csrc/panel.hip date_sums / excl_stats) instead of a gathered
+# pass over every (month, lag) tile; PFML_S4_DSTAT=0 takes the direct pass
+DSTAT = os.environ.get("PFML_S4_DSTAT", "1") != "0"
+
+
+def _lag_date_layout(panel: "Panel", grid_months: np.ndarray, months: np.ndarray,
+                     idx_raw: list, ns: list, lb: int, R: int):
+    """Host layout of the lag 1..10 statistics by differences.  For every date d that a month
+    of this plan reads at a lag 1..lb-1: U(d) = the sorted rows at d of the union of the
+    universes of the GLOBAL grid months b with 1 <= b - d <= lb - 1 (so a month's statistics
+    do not depend on how the months are sharded), and per (month, lag) tile the sorted rows of
+    U(d) outside its own universe.  idx_raw: per batch the raw [B, lb + 2, N] panel rows."""
+    gm = np.asarray(grid_months, np.int64)
+    dates = np.unique(np.concatenate([np.asarray(m, np.int64)[:, None] - np.arange(1, lb)[None, :]
+                                      for m in months]).ravel()) if len(months) else \
+        np.zeros(0, np.int64)
+    slot = {int(d): k for k, d in enumerate(dates)}
+    urows = []
+    for d in dates:
+        bs = gm[(gm - d >= 1) & (gm - d <= lb - 1)]
+        ids = np.unique(np.concatenate([panel.ids[panel.valid_rows(int(b))] for b in bs]))
+        r = panel.rows(int(d), ids)
+        urows.append(np.unique(r[r >= 0]))
+    ex = []
+    for bm, idx, nb in zip(months, idx_raw, ns):
+        rows_b, n_b, pos_b = [], [], []
+        for bi, b in enumerate(bm):
+            for th in range(1, lb):
+                u = urows[slot[int(b) - th]]
+                e = np.setdiff1d(u, idx[bi, th, :int(nb[bi])], assume_unique=False)
+                rows_b.append(e)
+                n_b.append(len(e))
+                pos_b.append(slot[int(b) - th])
+        ex.append((rows_b, n_b, pos_b))
+    return dates, urows, ex
+
+
 def _even(n: int) -> int:
     return n + (n & 1)
 
@@ -201,6 +240,11 @@ class _Batch:
     r: torch.Tensor             # [B, N] ret_ld1 (pad 0)
     w: torch.Tensor             # [B] wealth
     rf: torch.Tensor            # [B]
+    # lag 1..10 statistics by differences (``DSTAT``): per (month, lag) tile the rows of its
+    # date's union universe outside the month's universe, and the date's slot
+    ex_rows: torch.Tensor | None = None    # [B * (lb - 1), emax] (first ex_n real)
+    ex_n: torch.Tensor | None = None       # [B * (lb - 1)] int32
+    ex_dpos: torch.Tensor | None = None    # [B * (lb - 1)] int32
 
 
 @dataclass
@@ -234,6 +278,8 @@ class S4Plan:
     vol_real: torch.Tensor | None = None   # [Mv, nv] slot holds a real panel row (the vol
                                 # month's median runs over all of them, whether this plan
                                 # keeps a row or not)
+    du_rows: torch.Tensor | None = None    # [nd, umax] union-universe rows of each lag date
+    du_n: torch.Tensor | None = None       # [nd] int32
 
 
 def universe_npad(chars: pd.DataFrame, months: np.ndarray) -> int:
@@ -320,7 +366,7 @@ def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         if torch.device(dev).type == "cuda" and S4_STREAMS > 1 and T > 1:
             bsz = min(bsz, -(-T // S4_STREAMS))              # one batch per stream at least
         log.info(f"PFML inputs: {bsz} months per batch (N <= {nmax})")
-    batches, sig_rows, sig_ids = [], [], []
+    batches, sig_rows, sig_ids, idx_raw = [], [], [], []
     for b0 in range(0, T, bsz):
         bm = months[b0: b0 + bsz]
         B = len(bm)
@@ -354,6 +400,7 @@ def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
             sig_rows.append(rows_d)
             sig_ids.append(ids)
         mask = (np.arange(Npad)[None, :] < ns[:, None]).astype(np.float64)
+        idx_raw.append(idx)
         tt = lambda x, dt=torch.float64: torch.as_tensor(x, dtype=dt, device=dev)  # noqa: E731
         batches.append(_Batch(
             months=bm, ns=ns, idx=tt(idx, torch.int64), mask=tt(mask),
@@ -380,7 +427,12 @@ def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
     # an RFF feature row, a vol slot and a growth factor - a rank's S4 then scales with its own
     # months instead of paying the RFF GEMM of the whole panel (per-row arithmetic: the same
     # bits); vol months still take their medians over every row of the month
+    dl = None
+    if DSTAT and dev.type == "cuda" and lb > 1:
+        dl = _lag_date_layout(panel, grids["m2"], [b.months for b in batches], idx_raw,
+                              [b.ns for b in batches], lb, R)
     used = np.unique(np.concatenate([b.idx.cpu().numpy().ravel() for b in batches]
+                                    + ([np.concatenate(dl[1])] if dl and len(dl[1]) else [])
                                     + [np.zeros(0, np.int64)]))
     used = used[used < R]
     Rc = len(used)
@@ -393,6 +445,23 @@ def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
 
     for b in batches:
         b.idx = torch.as_tensor(remap(b.idx.cpu().numpy()), dtype=torch.int64, device=dev)
+    du_rows = du_n = None
+    if dl is not None:
+        dates, urows, ex = dl
+        umax = max([len(u) for u in urows] + [1])
+        ua = np.full((len(urows), umax), Rc, np.int64)
+        for k, u in enumerate(urows):
+            ua[k, :len(u)] = remap(u)
+        du_rows = torch.as_tensor(ua, device=dev)
+        du_n = torch.as_tensor(np.asarray([len(u) for u in urows], np.int32), device=dev)
+        for b, (rows_b, n_b, pos_b) in zip(batches, ex):
+            emax = max(n_b + [1])
+            ea = np.full((len(rows_b), emax), Rc, np.int64)
+            for k, e in enumerate(rows_b):
+                ea[k, :len(e)] = remap(e)
+            b.ex_rows = torch.as_tensor(ea, device=dev)
+            b.ex_n = torch.as_tensor(np.asarray(n_b, np.int32), device=dev)
+            b.ex_dpos = torch.as_tensor(np.asarray(pos_b, np.int32), device=dev)
     vol_real = vol_rows < R
     vol_rows = remap(vol_rows)
     feats_p = np.zeros((Rc, kfp))
@@ -409,7 +478,8 @@ def make_s4_plan(cfg: Config, chars: pd.DataFrame, barra: BarraCov, wealth: pd.D
         biv=torch.as_tensor(biv, dtype=torch.float64, device=dev),
         bF=torch.as_tensor(bF, dtype=torch.float64, device=dev),
         batches=batches, sig_rows=sig_rows, sig_ids=sig_ids, R=Rc,
-        Wd=[torch.as_tensor(Wp[g], dtype=torch.float64, device=dev) for g in range(Gc)])
+        Wd=[torch.as_tensor(Wp[g], dtype=torch.float64, device=dev) for g in range(Gc)],
+        du_rows=du_rows, du_n=du_n)
 
 
 def _vol_device(plan: S4Plan) -> torch.Tensor:
@@ -477,6 +547,10 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
     rffs = [rff_features(plan.feats, Wdev[g], prec, width=Pp, pad_rows=1,
                          out=Fcat[:, g * Pp:(g + 1) * Pp]) for g in range(Gc)]
     vol = _vol_device(plan)
+    # lag 1..10 statistics by differences: every lag date's union sums, once (per g block)
+    dsums = None
+    if plan.du_rows is not None:
+        dsums = [date_sums(rffs[g], plan.du_rows, plan.du_n, P, Pp) for g in range(Gc)]
     range_pop()
 
     # every (g, month) block is written by exactly one batch below (the batches partition the
@@ -540,8 +614,12 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
                                     n_real=bt.n_real)
             stats = torch.empty((B, lb - 1, 2, GP), dtype=torch.float64, device=dev)
             for g in range(Gc):
-                signal_stats(rffs[g], bt.idx[:, 1:lb], bt.mask, P,
-                             out=stats[..., g * Pp:(g + 1) * Pp], n_real=bt.n_real)
+                if dsums is not None and bt.ex_rows is not None:
+                    excl_stats(rffs[g], bt.ex_rows, bt.ex_n, bt.ex_dpos, dsums[g], bt.n_real,
+                               P, out=stats[..., g * Pp:(g + 1) * Pp])
+                else:
+                    signal_stats(rffs[g], bt.idx[:, 1:lb], bt.mask, P,
+                                 out=stats[..., g * Pp:(g + 1) * Pp], n_real=bt.n_real)
             # 1 / vol of each lag's rows (0 on padding rows: their standardised signal is 0)
             ivol = torch.where(bt.mask.unsqueeze(1) > 0, 1.0 / vol[bt.idx[:, 1:lb]],
                                torch.zeros((), dtype=torch.float64, device=dev))
@@ -723,6 +801,21 @@ def _sub_plan(plan: S4Plan, pos: np.ndarray) -> S4Plan:
                  ns=np.concatenate([bt.ns[sel] for bt, sel in parts]),
                  **{f: cat(f) for f in ("idx", "mask", "n_real", "brow", "fpos", "lam", "r",
                                          "w", "rf")})
+    if all(bt.ex_rows is not None for bt, _ in parts):
+        # the lag-statistics tiles of the selected months (TH per month), padded to one width
+        # (padding slots are never read: ex_n counts the real ones) - the re-run's statistics
+        # are then the same sums as the full run's
+        th = parts[0][0].ex_rows.shape[0] // len(parts[0][0].months)
+        emax = max(bt.ex_rows.shape[1] for bt, _ in parts)
+        rows, ns_, dps = [], [], []
+        for bt, sel in parts:
+            t = (torch.as_tensor(sel, device=bt.idx.device).unsqueeze(1) * th
+                 + torch.arange(th, device=bt.idx.device)).reshape(-1)
+            rows.append(torch.nn.functional.pad(bt.ex_rows[t], (0, emax - bt.ex_rows.shape[1]),
+                                                value=plan.R))
+            ns_.append(bt.ex_n[t])
+            dps.append(bt.ex_dpos[t])
+        sub.ex_rows, sub.ex_n, sub.ex_dpos = torch.cat(rows), torch.cat(ns_), torch.cat(dps)
     return dataclasses.replace(plan, months=plan.months[pos], batches=[sub],
                                sig_rows=[plan.sig_rows[i] for i in pos],
                                sig_ids=[plan.sig_ids[i] for i in pos])

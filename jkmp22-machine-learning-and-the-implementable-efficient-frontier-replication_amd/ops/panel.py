@@ -20,6 +20,11 @@ nat.register_hip("pfml_standardize", [C.c_void_p, C.c_int, C.c_int64, C.c_void_p
                                       C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                       C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_int64,
                                       C.c_int, C.c_void_p, C.c_int64, C.c_void_p])
+nat.register_hip("pfml_date_sums", [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
+                                    C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p])
+nat.register_hip("pfml_excl_stats", [C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
+                                     C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                     C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p])
 
 
 def rff_features(X: torch.Tensor, W: torch.Tensor, precision: str = "fp64",
@@ -155,4 +160,44 @@ def signal_stats(F: torch.Tensor, idx: torch.Tensor, mask: torch.Tensor, P: int,
     out.zero_()
     out[:, :, 0, :P] = mean[:, :, 0]
     out[:, :, 1, :P] = norm[:, :, 0]
+    return out
+
+
+def date_sums(F: torch.Tensor, urows: torch.Tensor, un: torch.Tensor, P: int, Pw: int,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """Per-date shifted column sums over the date's union universe U(d) (csrc/panel.hip
+    date_sums_kernel): urows [nd, umax] panel rows (the first un[d] real), returns dsum
+    [nd, 3, Pw] = (sum (x - K), sum (x - K)^2, K) with K the value of U(d)'s first row; the
+    statistics of every (month, lag) reading date d follow by ``excl_stats``.  Device only."""
+    nd, umax = urows.shape
+    if out is None:
+        out = torch.empty((nd, 3, Pw), dtype=F.dtype, device=F.device)
+    if F.stride(-1) != 1 or not urows.is_contiguous() or not un.is_contiguous():
+        raise ValueError("date_sums: unsupported layout")
+    _work.add("date_sums", 3.0 * int(un.numel()) * umax * P, 8.0 * nd * umax * P)
+    nat.check(nat.hip_lib().pfml_date_sums(F.data_ptr(), P, F.stride(0), urows.data_ptr(),
+                                           un.data_ptr(), umax, nd, Pw, out.data_ptr(),
+                                           nat.stream_of(F)), "pfml_date_sums")
+    return out
+
+
+def excl_stats(F: torch.Tensor, erows: torch.Tensor, en: torch.Tensor, dpos: torch.Tensor,
+               dsum: torch.Tensor, n_real: torch.Tensor, P: int, out: torch.Tensor
+               ) -> torch.Tensor:
+    """``signal_stats`` of the [B, TH] (month, lag) tiles from their dates' union sums
+    (``date_sums``) minus the rows of U(d) outside the month's universe: erows [B * TH, emax]
+    (the first en[.] real), dpos [B * TH] date slot of each tile.  out as ``signal_stats``
+    ([B, TH, 2, >= Pw] view).  Device only."""
+    B, TH = out.shape[0], out.shape[1]
+    Pw = dsum.shape[-1]
+    emax = erows.shape[-1]
+    if (out.stride(-1) != 1 or out.stride(-2) != out.stride(1) // 2 or
+            out.stride(1) * TH != out.stride(0) or F.stride(-1) != 1):
+        raise ValueError("excl_stats: unsupported output layout")
+    _work.add("excl_stats", 3.0 * B * TH * emax * P, 8.0 * B * TH * emax * P)
+    nat.check(nat.hip_lib().pfml_excl_stats(F.data_ptr(), P, F.stride(0), erows.data_ptr(),
+                                            en.data_ptr(), emax, dpos.data_ptr(),
+                                            dsum.data_ptr(), n_real.data_ptr(), B, TH, Pw,
+                                            out.data_ptr(), out.stride(-2), nat.stream_of(F)),
+              "pfml_excl_stats")
     return out

@@ -220,6 +220,38 @@ def test_pfml_inputs_gpu_matches_cpu(gpu, small_data):
                                   atol=1e-13)
 
 
+def test_s4_lag_stats_by_difference(gpu, small_data, monkeypatch):
+    """Lag 1..10 statistics from per-date union sums minus each month's excluded rows
+    (csrc/panel.hip date_sums / excl_stats) vs the direct gathered pass: the same summands to
+    rounding, and bitwise the same whether the months run as one plan or as a sub-range (the
+    union universes come from the global month grid)."""
+    from pfml.config import get_features
+    from pfml.data import io
+    from pfml.models import pfml_inputs as PI
+    from pfml.models.risk import BarraCov
+    from pfml.utils.dates import pfml_date_grids
+    cfg = small_data
+    d = cfg.run.data_dir
+    chars = io.read_processed_chars(d, get_features())
+    barra = BarraCov.load(os.path.join(d, "Barra_Cov.npz"))
+    wealth = pd.read_csv(os.path.join(d, "wealth_processed.csv"), parse_dates=["eom"])
+    rf = io.read_risk_free(d)
+    g = pfml_date_grids(int(barra.months.min()), 11, cfg.settings["split"]["test_end"], 1971, 10)
+    months = g["m2"][:30]
+    monkeypatch.setattr(PI, "DSTAT", True)
+    plan = PI.make_s4_plan(cfg, chars, barra, wealth, rf, gpu, months=months, batch=12)
+    assert plan.du_rows is not None and int(plan.batches[0].ex_n.max()) > 0
+    dif = PI.run_plan(plan, cfg)
+    sub = PI.run_plan(PI.make_s4_plan(cfg, chars, barra, wealth, rf, gpu, months=months[10:],
+                                      batch=7), cfg)
+    assert torch.equal(sub.reals.denom, dif.reals.denom[:, 10:])
+    monkeypatch.setattr(PI, "DSTAT", False)
+    direct = PI.run_plan(PI.make_s4_plan(cfg, chars, barra, wealth, rf, gpu, months=months,
+                                         batch=12), cfg)
+    for a, b in [(dif.reals.r_tilde, direct.reals.r_tilde), (dif.reals.denom, direct.reals.denom)]:
+        assert ((a - b).abs().max() / b.abs().max()).item() < 1e-12
+
+
 def test_s4_two_streams_bitwise(gpu, small_data, monkeypatch):
     """S4 month batches on two streams (PFML_S4_STREAMS=2: each batch's latency-bound kernels
     overlap the other's GEMMs) give bitwise the one-stream summands, eager and as a replayed

@@ -196,7 +196,7 @@ for step in ${MODE//,/ }; do
       # targeted GPU tests: PFML_KTEST = pytest -k expression
       timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "${PFML_KTEST}" > $OUT/pytest_k.log 2>&1
       rc=$?; tail -3 $OUT/pytest_k.log
-      if [ $rc -ne 0 ]; then grep -E "^E |FAILED" $OUT/pytest_k.log | head -20; exit $rc; fi ;;
+      if [ $rc -ne 0 ]; then grep -E "^E |FAILED" $OUT/pytest_k.log | cut -c1-300 | head -20; exit $rc; fi ;;
     e2e)
       # production-shape end-to-end run of `main` (SURVEY §7 north star): synthetic raw data of
       # the production shape (500 stocks, 1952-2023), the two S0 stages, then the 8 stages of
