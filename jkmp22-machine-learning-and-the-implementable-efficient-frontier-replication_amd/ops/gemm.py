@@ -274,6 +274,8 @@ def _vec3(v, batch):
 # A/B switch for the auto tile choice (0 auto, 1: 128x128, 2: 128x64, 3: 64x64; 4, 5: BK = 32
 # variants, csrc/gemm_f64.hip PfmlGemmEpi), read once
 _TILE_DEFAULT = int(os.environ.get("PFML_GEMM_TILE", "0"))
+# the same for symmetric-mode products only (square tiles: 3 / 7 64 x 64, 1 / 6 128 x 128)
+_SYM_TILE = int(os.environ.get("PFML_SYM_TILE", "0"))
 
 
 def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: bool = False,
@@ -372,7 +374,7 @@ def gemm_fused(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor, *, trans_a: 
                   int(diag_col0 is not None), nat.ptr(es), ses, int(sincos), int(sym),
                   nat.ptr(T3), 0 if T3 is None else T3.stride(1),
                   0 if T3 is None else T3.stride(0), nat.ptr(er), ser, nat.ptr(ecm),
-                  nat.ptr(ecs), secm, nat.ptr(osc), sos, int(tile_cfg or _TILE_DEFAULT),
+                  nat.ptr(ecs), secm, nat.ptr(osc), sos, int(tile_cfg or (_SYM_TILE if sym else 0) or _TILE_DEFAULT),
                   int(Ms) if clip else 0, int(Ns) if clip else 0)
         if _work.on():
             _ledger(trans_a, trans_b, M, N, K, batch, A3, B3, C3, ks=ks, sks=sks,
