@@ -352,7 +352,8 @@ extern "C" hipError_t pfml_db_check(const double* M, int B, int N, int64_t ld, i
 //                   Q block  T[i, N + j] = ((mt_ij * ks12_j) * a_i) * k10_i
 //                 (R_11 = diag(a) m_tilde diag(D_11 / a), pre-scaled by the next step's k-scale,
 //                 in the rounding order of the former elementwise form)
-//   block_add     out = X + Y on N x N blocks of strided rows (U_0's identity block Q + T_1)
+//   block_add     out = X + Y (or X + diag(s) Y, one fma) on blocks of strided rows (U_0's
+//                 identity block Q + T_1; omega_chg = omega - diag(D_0) omega_l1)
 // Grid (column chunks, rows, batch); every store coalesced along the row.
 // ---------------------------------------------------------------------------------------
 namespace {
@@ -375,12 +376,16 @@ __global__ __launch_bounds__(256) void block_add_kernel(double* __restrict__ out
                                                         int64_t so, const double* __restrict__ X,
                                                         int64_t ldx, int64_t sx,
                                                         const double* __restrict__ Y,
-                                                        int64_t ldy, int64_t sy, int M, int N) {
+                                                        int64_t ldy, int64_t sy,
+                                                        const double* __restrict__ ys,
+                                                        int64_t sys, int M, int N) {
   const int j = blockIdx.x * 256 + threadIdx.x;
   const int i = blockIdx.y, b = blockIdx.z;
   if (j >= N || i >= M) return;
+  const double x = X[(int64_t)b * sx + (int64_t)i * ldx + j];
+  const double y = Y[(int64_t)b * sy + (int64_t)i * ldy + j];
   out[(int64_t)b * so + (int64_t)i * ldo + j] =
-      X[(int64_t)b * sx + (int64_t)i * ldx + j] + Y[(int64_t)b * sy + (int64_t)i * ldy + j];
+      ys ? __builtin_fma(ys[(int64_t)b * sys + i], y, x) : x + y;
 }
 
 }  // namespace
@@ -398,10 +403,11 @@ extern "C" hipError_t pfml_horner_init(double* T, int64_t ldt, int64_t sT, const
 
 extern "C" hipError_t pfml_block_add(double* out, int64_t ldo, int64_t so, const double* X,
                                      int64_t ldx, int64_t sx, const double* Y, int64_t ldy,
-                                     int64_t sy, int M, int N, int B, hipStream_t st) {
+                                     int64_t sy, const double* ys, int64_t sys, int M, int N,
+                                     int B, hipStream_t st) {
   if (M <= 0 || N <= 0 || B <= 0) return hipSuccess;
   if (M > 65535 || B > 65535) return hipErrorInvalidValue;
   hipLaunchKernelGGL(block_add_kernel, dim3((N + 255) / 256, M, B), dim3(256), 0, st, out, ldo, so,
-                     X, ldx, sx, Y, ldy, sy, M, N);
+                     X, ldx, sx, Y, ldy, sy, ys, sys, M, N);
   return hipGetLastError();
 }

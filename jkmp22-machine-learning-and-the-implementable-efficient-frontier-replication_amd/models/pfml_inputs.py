@@ -198,7 +198,9 @@ def _lag_date_layout(panel: "Panel", grid_months: np.ndarray, months: np.ndarray
     universes of the GLOBAL grid months b with 1 <= b - d <= lb - 1 (so a month's statistics
     do not depend on how the months are sharded), and per (month, lag) tile the sorted rows of
     U(d) outside its own universe.  idx_raw: per batch the raw [B, lb + 2, N] panel rows."""
-    gm = np.asarray(grid_months, np.int64)
+    # (the plan's own months join the grid: a month outside it must still find its rows in U(d))
+    own_months = [np.asarray(m, np.int64) for m in months] + [np.zeros(0, np.int64)]
+    gm = np.union1d(np.asarray(grid_months, np.int64), np.concatenate(own_months))
     dates = np.unique(np.concatenate([np.asarray(m, np.int64)[:, None] - np.arange(1, lb)[None, :]
                                       for m in months]).ravel()) if len(months) else \
         np.zeros(0, np.int64)
@@ -215,7 +217,10 @@ def _lag_date_layout(panel: "Panel", grid_months: np.ndarray, months: np.ndarray
         for bi, b in enumerate(bm):
             for th in range(1, lb):
                 u = urows[slot[int(b) - th]]
-                e = np.setdiff1d(u, idx[bi, th, :int(nb[bi])], assume_unique=False)
+                own = idx[bi, th, :int(nb[bi])]
+                if len(np.setdiff1d(own, u)):
+                    raise AssertionError(f"month {b} lag {th}: rows outside the union universe")
+                e = np.setdiff1d(u, own, assume_unique=False)
                 rows_b.append(e)
                 n_b.append(len(e))
                 pos_b.append(slot[int(b) - th])
@@ -709,7 +714,9 @@ def run_plan(plan: S4Plan, cfg: Config, keep_risk_tc: bool = False,
             om2 = la.solve_augmented(TU0.view(2 * B, N, Wz), N, GP, a0=GP, b0=0,
                                      status=sing[:2 * B], z0=Wd)                  # [2B, N, GP]
             omega, omega_l1 = om2[:B], om2[B:]
-            omega_chg = torch.addcmul(omega, Dg[:, 0].unsqueeze(-1), omega_l1, value=-1.0)
+            # omega_chg = omega - diag(D_0) omega_l1: one strided pass over the solve buffer
+            omega_chg = la.block_add(torch.empty((B, N, GP), dtype=torch.float64, device=dev),
+                                     omega, omega_l1, y_row_scale=-Dg[:, 0])
             nsing_t += torch.maximum(sing[:B], sing[B:2 * B]).sum()
             sing.zero_()
             # (25): r_tilde = omega' r, risk = gamma omega' Sigma omega (Sigma in low-rank form:

@@ -479,8 +479,8 @@ nat.register_hip("pfml_horner_init", [C.c_void_p, C.c_int64, C.c_int64, C.c_void
                                       C.c_int64, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p,
                                       C.c_int64, C.c_int, C.c_int, C.c_void_p])
 nat.register_hip("pfml_block_add", [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_int64,
-                                    C.c_int64, C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_int,
-                                    C.c_int, C.c_void_p])
+                                    C.c_int64, C.c_void_p, C.c_int64, C.c_int64, C.c_void_p,
+                                    C.c_int64, C.c_int, C.c_int, C.c_int, C.c_void_p])
 
 
 def horner_init(T: torch.Tensor, mt: torch.Tensor, k10: torch.Tensor, ks12: torch.Tensor,
@@ -506,18 +506,26 @@ def horner_init(T: torch.Tensor, mt: torch.Tensor, k10: torch.Tensor, ks12: torc
     return T
 
 
-def block_add(out: torch.Tensor, X: torch.Tensor, Y: torch.Tensor) -> torch.Tensor:
-    """out = X + Y on [B, M, N] blocks of strided rows (unit inner stride), one pass."""
+def block_add(out: torch.Tensor, X: torch.Tensor, Y: torch.Tensor,
+              y_row_scale: torch.Tensor | None = None) -> torch.Tensor:
+    """out = X + Y on [B, M, N] blocks of strided rows (unit inner stride), one pass;
+    ``y_row_scale`` [B, M] (unit inner stride): out = X + diag(s) Y, one fma per element."""
     B, M, N = out.shape
     if nat.is_device(out):
         for t in (out, X, Y):
             if t.stride(-1) != 1 or tuple(t.shape) != (B, M, N):
                 raise ValueError("block_add: unsupported layout")
+        if y_row_scale is not None and (y_row_scale.stride(-1) != 1 or
+                                        tuple(y_row_scale.shape) != (B, M)):
+            raise ValueError("block_add: y_row_scale must be [B, M] with unit inner stride")
         nat.check(nat.hip_lib().pfml_block_add(
             out.data_ptr(), out.stride(1), out.stride(0), X.data_ptr(), X.stride(1), X.stride(0),
-            Y.data_ptr(), Y.stride(1), Y.stride(0), M, N, B, nat.stream_of(out)),
+            Y.data_ptr(), Y.stride(1), Y.stride(0), nat.ptr(y_row_scale),
+            0 if y_row_scale is None else y_row_scale.stride(0), M, N, B, nat.stream_of(out)),
             "pfml_block_add")
         return out
+    if y_row_scale is not None:
+        return torch.addcmul(X, y_row_scale.unsqueeze(-1), Y, out=out)
     return torch.add(X, Y, out=out)
 
 
@@ -560,12 +568,18 @@ def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tenso
     and is recomputed by the convergence-checked reference form, like a failed pivot."""
     B, N, _ = S.shape
     M, Y, Mi, Yn = ws
-    M.copy_(S)
-    Y.copy_(S)
     mu = torch.empty(B, dtype=S.dtype, device=S.device)
     if ns_tail is None:
         ns_tail = DB_NS_TAIL
     ns_tail = ns_tail and iters > scaled_iters
+    # the first (exact) step reads S itself as both M and Y - no copies; its M update goes to
+    # the unused buffer ``spare`` (S is only read)
+    spare = None
+    if iters >= 2:
+        spare, M, Y = M, S, S
+    else:
+        M.copy_(S)
+        Y.copy_(S)
     # S, M, M^-1 and Y are symmetric (M, Y are polynomials in S; in exact arithmetic Y and M^-1
     # commute, so Y M^-1 is symmetric too).  sym_inv: M^-1 by the one-triangle inverse;
     # sym_prod: Y M^-1 on its lower tiles, mirrored.  With both (and S exactly symmetric, as
@@ -593,6 +607,11 @@ def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tenso
         es = (0.5 * mu).view(B, 1).expand(B, N).contiguous()
         gemm_fused(Y, Mi, Yn, row_scale=rs, addend=Y, addend_row_scale=es, sym=sym_prod)
         Y, Yn = Yn, Y
+        if it == 0 and spare is not None:
+            # (Yn is S now: the new M goes to the spare buffer; S retires, ws[1] is free)
+            mf_sym(MF_DB, M, Mi, spare, svec=mu, flat=sym_inv and exact_sym)
+            M, Yn = spare, ws[1]
+            continue
         mf_sym(MF_DB, M, Mi, Yn, svec=mu, flat=sym_inv and (exact_sym or it > 0))
         # (Yn was free: the new M went into it)
         M, Yn = Yn, M

@@ -74,6 +74,17 @@ for step in ${MODE//,/ }; do
       rc=$?; tail -1 $OUT/dgemm_shapes.log; if [ $rc -ne 0 ]; then tail -5 $OUT/dgemm_shapes.log; exit $rc; fi
       (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/dgemm_pmc -o run -- python3 $ROOT/tools/micro/dgemm_shapes.py 2 > $OUT/dgemm_pmc.log 2>&1)
       rc=$?; python tools/pmc_summary.py $OUT/dgemm_pmc --top 8 > $OUT/dgemm_pmc.txt 2>&1; cat $OUT/dgemm_pmc.txt; if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    invab)
+      # SPD-inverse kernels: bitwise A/B against a saved build (lib_ab/old.so) + node latency
+      PFML_HIP_LIB=$ROOT/lib_ab/old.so timeout -k 10 200 python tools/micro/inverse_ab.py save $OUT/inv_old.sha > $OUT/inv_old.json 2>&1
+      rc=$?; tail -1 $OUT/inv_old.json | cut -c1-600; if [ $rc -ne 0 ]; then exit $rc; fi
+      timeout -k 10 200 python tools/micro/inverse_ab.py save $OUT/inv_new.sha > $OUT/inv_new.json 2>&1
+      rc=$?; tail -1 $OUT/inv_new.json | cut -c1-600; if [ $rc -ne 0 ]; then exit $rc; fi
+      python tools/micro/inverse_ab.py cmp $OUT/inv_old.sha $OUT/inv_new.sha | tee $OUT/inv_cmp.json
+      PFML_HIP_LIB=$ROOT/lib_ab/old.so timeout -k 10 200 python tools/micro/node_timing.py 36 715 > $OUT/node_timing_old.jsonl 2>&1
+      rc=$?; grep '^{' $OUT/node_timing_old.jsonl | cut -c1-300; if [ $rc -ne 0 ]; then tail -3 $OUT/node_timing_old.jsonl; exit $rc; fi
+      timeout -k 10 200 python tools/micro/node_timing.py 36 715 > $OUT/node_timing.jsonl 2>&1
+      rc=$?; grep '^{' $OUT/node_timing.jsonl | cut -c1-300; if [ $rc -ne 0 ]; then tail -3 $OUT/node_timing.jsonl; exit $rc; fi ;;
     gemmtest)
       # GEMM / SPD-inverse kernel tests only (fast numerics check of a kernel change)
       timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -k "gemm or spd_inverse or mfma" -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gemm.log 2>&1
