@@ -140,8 +140,33 @@ def test_local_month_rows_cover_once_plus_halo():
         assert extra <= 12 * (world - 1)                # halos only
     prod = Config.default()
     m2 = np.arange(mi_from_ym(1963, 1), mi_from_ym(2023, 11) + 1)     # 731 PFML months
-    cnt = np.asarray(s4_month_counts(m2, np.asarray(prod.hp_years), 8))
-    assert cnt.max() / cnt.mean() <= 1.15, cnt
+    for world in (2, 4, 8):
+        cnt = np.asarray(s4_month_counts(m2, np.asarray(prod.hp_years), world))
+        assert cnt.sum() == len(m2)
+        # water-filled burn-in pieces: the ranks' S4 months within 1 % (W = 8: 92 / 92 / 92 /
+        # 91 / 91 / 91 / 91 / 91; W = 2: 367 / 364 - the cut is the C = 8 one of every W)
+        assert cnt.max() / cnt.mean() <= 1.01, (world, cnt)
+
+
+def test_water_fill_levels_the_loads():
+    """search._water_fill: non-negative integers summing to ``total`` that level base + s
+    (the burn-in months that balance the per-rank S4 load), deterministic."""
+    from pfml.models.search import _water_fill
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        base = rng.integers(0, 60, size=int(rng.integers(1, 10)))
+        total = int(rng.integers(0, 400))
+        s = _water_fill(total, base)
+        assert s.min() >= 0 and int(s.sum()) == total
+        lv = base + s
+        # every filled slot sits at the top level (within one of the remainder deal)
+        if total:
+            top = lv[s > 0]
+            assert top.max() - top.min() <= 1
+            assert lv.min() >= top.min() - 1 or (s == 0).all()
+        assert (s == _water_fill(total, base)).all()
+    assert list(_water_fill(5, np.array([3, 0, 0]))) == [0, 3, 2]
+    assert list(_water_fill(0, np.array([1, 2]))) == [0, 0]
 
 
 def test_s4_compute_rows_partition_the_months():
