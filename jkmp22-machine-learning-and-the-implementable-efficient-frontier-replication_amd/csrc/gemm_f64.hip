@@ -25,6 +25,7 @@
 //  * 1-D grid over (matrix, tile) with the bijective XCD remap (common.h): the tiles of one
 //    matrix run on one XCD and share its L2 (A row panels / B column panels).
 #include "common.h"
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -680,6 +681,16 @@ static hipError_t dgemm_chunk(int ta, int tb, int M, int N, int K, int batch,
                               double* C, int64_t ldc, int64_t sC,
                               const PfmlGemmEpi* h, hipStream_t st);
 
+// PFML_GEMM_SMALL_TILES: below this many 128 x 64 tiles an auto launch takes 64 x 64 tiles
+// (0: never); default one workgroup per CU
+static int64_t small_launch_tiles() {
+  static const int64_t v = [] {
+    const char* e = getenv("PFML_GEMM_SMALL_TILES");
+    return e ? (int64_t)atoll(e) : (int64_t)256;
+  }();
+  return v;
+}
+
 // 2 GB buffer-store limit per C batch entry (store_tile): larger outputs are split into row
 // chunks on the host - every row-indexed operand (A's rows, the row / output / addend scales,
 // the diagonal vector, the addend or its gathered row index, Ct's columns) is offset by the
@@ -739,6 +750,14 @@ static hipError_t dgemm_chunk(int ta, int tb, int M, int N, int K, int batch,
     // register-staged 64 x 64), 128 x 128 for large matrices; square 64 x 64 tiles in the
     // symmetric mode (profiles/r05_dgemm_shapes.json)
     cfg = (M >= 1024 && N >= 1024) ? 6 : (h->sym ? PFML_SYM_CFG : 8);
+    // A launch of fewer 128 x 64 tiles than CUs (the SPD-inverse products of the per-rank
+    // S4 of a many-GPU run, ~30 months per batch) takes 64 x 64 tiles: twice the workgroups
+    // and half of each one's MFMA chain (PFML_GEMM_SMALL_TILES; at 768 = three per CU the
+    // one-GPU S4 got 0.5 ms slower, profiles/r06_experiments.md).  Every output element sees the same k steps in the same order in both forms, so
+    // the bits do not depend on the choice (tests/test_gpu_kernels.py
+    // test_gemm_tile_forms_bitwise) - nor, therefore, on the batch size.
+    if (cfg == 8 && (int64_t)((M + 127) / 128) * ((N + 63) / 64) * batch < small_launch_tiles())
+      cfg = 7;
   }
   if (cfg == 1 && h->sincos) cfg = 3;    // the 128 x 128 kernel has no sincos epilogue
   if (h->sym && (cfg == 2 || cfg == 8 || cfg == 10)) cfg = cfg == 2 ? 3 : 7;   // square tiles

@@ -67,7 +67,7 @@ def _ledger(ta, tb, M, N, K, batch, A3, B3, C3, ks=None, sks=0, sincos=False, cf
     launch counts the flops of the tiles it runs (on and below the diagonal)."""
     cfg = 0 if cfg < 0 else (cfg or _TILE_DEFAULT)          # -1: pfml_dgemm (always auto)
     if cfg == 0:
-        cfg = _auto_cfg(M, N, K, sym)
+        cfg = _auto_cfg(M, N, K, sym, batch)
     if cfg == 1 and sincos:
         cfg = 3
     if sym and cfg in (2, 8, 10):
@@ -104,10 +104,17 @@ def _ledger(ta, tb, M, N, K, batch, A3, B3, C3, ks=None, sks=0, sincos=False, cf
               8.0 * (na + nb + batch * M * N) * frac + extra_bytes)
 
 
-def _auto_cfg(M: int, N: int, K: int, sym: bool = False) -> int:
+_SMALL_TILES = int(os.environ.get("PFML_GEMM_SMALL_TILES", "256"))
+
+
+def _auto_cfg(M: int, N: int, K: int, sym: bool = False, batch: int = 1) -> int:
     """Host mirror of the auto tile choice of pfml_dgemm_ex (tile_cfg 0; the LDS-DMA forms
-    fall back to 3 where their 16-byte chunking does not apply, mirrored in _ledger)."""
-    return 6 if (M >= 1024 and N >= 1024) else (7 if sym else 8)
+    fall back to 3 where their 16-byte chunking does not apply, mirrored in _ledger): a launch
+    of fewer than PFML_GEMM_SMALL_TILES 128 x 64 tiles takes 64 x 64 tiles (same bits)."""
+    cfg = 6 if (M >= 1024 and N >= 1024) else (7 if sym else 8)
+    if cfg == 8 and -(-M // 128) * -(-N // 64) * batch < _SMALL_TILES:
+        cfg = 7
+    return cfg
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, *, trans_a: bool = False, trans_b: bool = False,

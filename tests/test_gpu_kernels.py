@@ -94,6 +94,40 @@ def test_gemm_fused_matches_torch(gpu, ta, tb, cfg, shape):
     assert (out - ref).abs().max().item() / ref.abs().max().item() < 1e-13
 
 
+def test_gemm_tile_forms_bitwise(gpu):
+    """The 64 x 64 and 128 x 64 LDS-DMA tiles (tile_cfg 7 / 8) give BITWISE the same result
+    for the S4 GEMM forms - the Horner step (row scale, gathered standardised addend, identity
+    diagonal, output row scale), the k-scaled T_0 step, X' omega (trans_a) and a plain product:
+    every element sees the same k steps in the same order.  The auto choice may therefore take
+    the 64 x 64 form for launches too small to fill the chip (batch-dependent) without the bits
+    depending on the batch size or the rank count."""
+    from pfml.ops.gemm import gemm_fused
+    b, M, K, GP, R = 3, 250, 250, 130, 400
+    mt = _rand(b, M, K, seed=1).to(gpu)
+    T = _rand(b, K, GP + M, seed=2).to(gpu)
+    a = _rand(b, M, seed=3).to(gpu)
+    feats = _rand(R, GP, seed=4).to(gpu)
+    rows = torch.randint(0, R, (b, M), generator=torch.Generator().manual_seed(5)).to(gpu)
+    shift, scale = _rand(b, GP, seed=6).to(gpu), _rand(b, GP, seed=7).to(gpu)
+    ivol, ks = _rand(b, M, seed=8).to(gpu), _rand(b, K, seed=9).to(gpu)
+    outs = {}
+    for cfg in (7, 8):
+        o1 = torch.empty(b, M, GP + M, dtype=torch.float64, device=gpu)
+        gemm_fused(mt, T, o1, row_scale=a, addend=feats, addend_cols=GP, addend_rows=rows,
+                   addend_col_shift=shift, addend_col_scale=scale, addend_row_scale=ivol,
+                   diag_col0=GP, diag_value=1.0, out_row_scale=ks, tile_cfg=cfg)
+        o2 = torch.empty_like(o1)
+        gemm_fused(mt, T, o2, row_scale=a, k_scale=ks, addend=o1[:, :, :GP], addend_cols=GP,
+                   diag_col0=GP, diag_value=1.0, tile_cfg=cfg)
+        o3 = torch.empty(b, K, GP, dtype=torch.float64, device=gpu)
+        gemm_fused(mt, T[:, :M, :GP].contiguous(), o3, trans_a=True, tile_cfg=cfg)
+        o4 = torch.empty(b, M, GP + M, dtype=torch.float64, device=gpu)
+        gemm_fused(mt, T, o4, tile_cfg=cfg)
+        outs[cfg] = (o1, o2, o3, o4)
+    for x, y in zip(outs[7], outs[8]):
+        assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("sym", [False, True])
 def test_gemm_store_clip(gpu, sym):
     """Store clip (S4's denom written in place): the product of the even-padded operands, only
