@@ -23,6 +23,19 @@ from pfml.config import Config  # noqa: E402
 from pfml.parallel import dist as pdist  # noqa: E402
 
 
+def _median_ms(fn, reps: int) -> float:
+    """Median wall time of ``reps`` synchronised calls (one slow replay - another process on
+    the box, a clock dip - must not become a rank's number)."""
+    ts = []
+    for _ in range(max(1, reps)):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append(1e3 * (time.perf_counter() - t))
+    return float(sorted(ts)[len(ts) // 2])
+
+
 def with_inputs(worlds, steps: int) -> dict:
     """Per-rank S4 (the PFML months this rank computes: s4_compute_rows, its burn-in pieces
     and hp-year blocks; the validation halo of its last year arrives from the next rank by an
@@ -58,12 +71,7 @@ def with_inputs(worlds, steps: int) -> dict:
             hip_graph &= rep is not None
             rep = rep or f_s4
             rep()                                                 # warm-up
-            torch.cuda.synchronize()
-            t = time.perf_counter()
-            for _ in range(steps):
-                rep()
-            torch.cuda.synchronize()
-            t_s4 = 1e3 * (time.perf_counter() - t) / steps
+            t_s4 = _median_ms(rep, steps)
             del rep
             torch.cuda.empty_cache()
             f_all = lambda: bench.one_step(None, cfg, eng)                 # noqa: E731
@@ -71,12 +79,7 @@ def with_inputs(worlds, steps: int) -> dict:
             hip_graph &= rep is not None
             rep = rep or f_all
             rep()                                                 # warm-up (plans, caches)
-            torch.cuda.synchronize()
-            t = time.perf_counter()
-            for _ in range(steps):
-                rep()
-            torch.cuda.synchronize()
-            t_all = 1e3 * (time.perf_counter() - t) / steps
+            t_all = _median_ms(rep, steps)
             del rep
             bench.LAST_S4.clear()
             s4.append(round(t_s4, 1))

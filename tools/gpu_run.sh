@@ -178,7 +178,7 @@ for step in ${MODE//,/ }; do
       tail -32 $OUT/timeline1.txt ;;
     shards4)
       # per-rank S4 + S5 + S6 of W = 1, 2, 4, 8 rank shards on this GPU (whole-node projection)
-      timeout -k 10 900 python tools/bench_shard.py --with-inputs 1,2,4,8 2 > $OUT/shard_s4.json 2> $OUT/shard_s4.err
+      timeout -k 10 900 python tools/bench_shard.py --with-inputs 1,2,4,8 5 > $OUT/shard_s4.json 2> $OUT/shard_s4.err
       rc=$?; cat $OUT/shard_s4.json; if [ $rc -ne 0 ]; then tail -5 $OUT/shard_s4.err; exit $rc; fi ;;
     shard8)
       # per-rank S4 + step of the W = 8 shards only (PFML_* A/B switches from the caller)
