@@ -322,6 +322,77 @@ __global__ __launch_bounds__(256) void lu_blockinv_kernel(const double* __restri
   }
 }
 
+// The same inverse for NB = 32 with the block in registers (thread (ti, tj) of 256 holds rows
+// 2 ti.., columns 2 tj..): the owners post pivot row / column p to a double-buffered LDS line,
+// ONE barrier per pivot instead of four (the LDS form re-read and re-wrote the whole block
+// around each pivot: ~33 us per call, latency, at the ~60-matrix batches of a many-GPU run's
+// per-rank S4).  Every element takes the same operations on the same values in the same
+// order: bitwise the LDS form.
+template <int NB>
+__global__ __launch_bounds__(256) void lu_blockinv_reg_kernel(const double* __restrict__ M,
+                                                              int64_t ldm, int64_t sM, int a0,
+                                                              int k0, int nb,
+                                                              double* __restrict__ Pbuf) {
+  static_assert(NB == 32, "2 x 2 elements per thread of 256");
+  __shared__ double rowp[2][NB], colp[2][NB];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int ti = t >> 4, tj = t & 15;
+  const double* Mb = M + (int64_t)b * sM;
+  double x[2][2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int i = 2 * ti + u, j = 2 * tj + v;
+      x[u][v] = (i < nb && j < nb) ? Mb[(int64_t)(k0 + i) * ldm + a0 + k0 + j] : 0.0;
+    }
+  for (int p = 0; p < nb; ++p) {
+    const int buf = p & 1, h = p & 1;
+    if (ti == (p >> 1)) {
+      rowp[buf][2 * tj] = x[h][0];
+      rowp[buf][2 * tj + 1] = x[h][1];
+    }
+    if (tj == (p >> 1)) {
+      colp[buf][2 * ti] = x[0][h];
+      colp[buf][2 * ti + 1] = x[1][h];
+    }
+    __syncthreads();
+    const double inv = 1.0 / rowp[buf][p];
+    const double rp[2] = {rowp[buf][2 * tj], rowp[buf][2 * tj + 1]};
+    const double cp[2] = {colp[buf][2 * ti], colp[buf][2 * ti + 1]};
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int v = 0; v < 2; ++v) {
+        const int i = 2 * ti + u, j = 2 * tj + v;
+        if (i < nb && j < nb) {
+          if (i != p && j != p) x[u][v] -= cp[u] * rp[v] * inv;
+          else if (i == p && j != p) x[u][v] *= inv;
+          else if (i != p) x[u][v] *= -inv;
+          else x[u][v] = inv;
+        }
+      }
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int i = 2 * ti + u, j = 2 * tj + v;
+      Pbuf[(int64_t)b * NB * NB + i * NB + j] = (i < nb && j < nb) ? x[u][v] : 0.0;
+    }
+}
+
+template <int NB>
+void lu_blockinv_launch(const double* M, int64_t ldm, int64_t sM, int a0, int k0, int nb,
+                        double* Pbuf, int batch, hipStream_t st) {
+  if constexpr (NB == 32)
+    hipLaunchKernelGGL((lu_blockinv_reg_kernel<NB>), dim3(batch), dim3(256), 0, st, M, ldm, sM,
+                       a0, k0, nb, Pbuf);
+  else
+    hipLaunchKernelGGL((lu_blockinv_kernel<NB>), dim3(batch), dim3(256), 0, st, M, ldm, sM, a0,
+                       k0, nb, Pbuf);
+}
+
 // R = P M_k over live columns (excluding block k's own A columns) -> Rbuf [NB][nlive]
 template <int NB>
 __global__ __launch_bounds__(256) void lu_rowpanel_kernel(const double* __restrict__ M, int64_t ldm,
@@ -463,8 +534,7 @@ hipError_t lu_solve_nb(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
     const int nswap = (n - k0) + m;           // A cols >= k0 and all B cols
     hipLaunchKernelGGL((lu_swap_kernel<NB>), dim3((nswap + 255) / 256, batch), dim3(256), 0, st,
                        M, ldm, sM, nswap, a0 + k0, n - k0, b0, k0, nb, piv);
-    hipLaunchKernelGGL((lu_blockinv_kernel<NB>), dim3(batch), dim3(256), 0, st, M, ldm, sM, a0,
-                       k0, nb, Pbuf);
+    lu_blockinv_launch<NB>(M, ldm, sM, a0, k0, nb, Pbuf, batch, st);
     const int nA = n - (k0 + nb);            // live A columns right of the block
     const int nlive = nA + m;
     if (nlive > 0) {
@@ -559,8 +629,7 @@ hipError_t lu_solve_2level(double* M, int n, int m, int64_t ldm, int64_t sM, int
                          M, ldm, sM, nswap, a0 + k0, aend - k0, z0, k0, nb, pv);
       hipLaunchKernelGGL(lu_zunit_kernel, dim3(batch), dim3(64), 0, st, M, ldm, sM, k0,
                          z0 + (k0 - K0), nb);
-      hipLaunchKernelGGL((lu_blockinv_kernel<NB>), dim3(batch), dim3(256), 0, st, M, ldm, sM, a0,
-                         k0, nb, Pbuf);
+      lu_blockinv_launch<NB>(M, ldm, sM, a0, k0, nb, Pbuf, batch, st);
       const int nA = aend - (k0 + nb);
       const int nlive = nA + zlive + nb;
       hipLaunchKernelGGL((lu_rowpanel_kernel<NB>), dim3((nlive + 255) / 256, batch), dim3(256), 0,

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Bitwise A/B of two builds of the SPD-inverse kernels (csrc/spd_inverse.hip: the 64-leaf
-Gauss-Jordan, the one-launch 65..128-row node, the one-triangle recursive inverse).
+Gauss-Jordan, the one-launch 65..128-row node, the one-triangle recursive inverse) and of the
+pivoted LU solve (csrc/lu_solve.hip).
 
     PFML_HIP_LIB=<lib A> python tools/micro/inverse_ab.py save A.json
     PFML_HIP_LIB=<lib B> python tools/micro/inverse_ab.py save B.json
@@ -52,6 +53,31 @@ def save(path):
         out[f"{B}x{n}"] = hashlib.sha256(X.cpu().numpy().tobytes()).hexdigest()
         times[f"{B}x{n}"] = {"ms": round(e0.elapsed_time(e1) / reps, 4), "max_abs_XA_minus_I": err,
                              "status": int(st.sum())}
+    # the pivoted LU solve of augmented [B | A] rows (csrc/lu_solve.hip, the S4 const^-1 Omega
+    # form: one- and two-level), general A (partial pivoting active)
+    for k, (B, n, m, two) in enumerate([(64, 490, 258, True), (64, 490, 258, False),
+                                        (24, 137, 66, True)]):
+        g = torch.Generator(device=dev).manual_seed(100 + k)
+        Wz = m + n + (la.LU_PANEL_COLS if two else 0)
+        M0 = torch.randn(B, n, Wz, generator=g, dtype=torch.float64, device=dev)
+        M = M0.clone()
+        st = torch.zeros(B, dtype=torch.int32, device=dev)
+        z0 = m + n if two else None
+        la.solve_augmented(M, n, m, a0=m, b0=0, status=st, z0=z0)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            M.copy_(M0)
+            la.solve_augmented(M, n, m, a0=m, b0=0, status=st, z0=z0)
+        e1.record()
+        torch.cuda.synchronize()
+        X = M[:, :, :m]
+        res = float((torch.bmm(M0[:, :, m:m + n], X) - M0[:, :, :m]).abs().max())
+        key = f"lu{'2' if two else '1'}_{B}x{n}x{m}"
+        out[key] = hashlib.sha256(X.contiguous().cpu().numpy().tobytes()).hexdigest()
+        times[key] = {"ms_incl_copy": round(e0.elapsed_time(e1) / 10, 4), "max_abs_residual": res,
+                      "status": int(st.sum())}
     with open(path, "w") as f:
         json.dump(out, f)
     print(json.dumps({"lib": os.environ.get("PFML_HIP_LIB", "in-tree"), "cases": times}))
