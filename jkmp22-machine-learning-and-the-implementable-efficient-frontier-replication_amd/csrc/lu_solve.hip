@@ -10,7 +10,7 @@
 //      (LAPACK-style sequential swap list);
 //   2. the swaps are applied to every live column (A cols >= k0 and all B cols);
 //   3. P = A_kk^-1 (Gauss-Jordan in LDS, pivots non-zero by construction);
-//   4. row panel R = P M_k (live columns), column panel snapshot C = M[:, k-block];
+//   4. row panel R = P M_k (live columns); the column panel C = M[:, k-block] is read in place;
 //   5. all other rows: M_i -= C_i R  (rank-NB update on fp64 MFMA); block rows: M_k = R.
 // Columns of A left of the current block are never touched again (they would hold the
 // identity), so the work is n^3 + 2 n^2 m flops like an LU solve.
@@ -422,36 +422,21 @@ __global__ __launch_bounds__(256) void lu_rowpanel_kernel(const double* __restri
   }
 }
 
-template <int NB>
-__global__ __launch_bounds__(256) void lu_snapshot_kernel(const double* __restrict__ M, int n,
-                                                          int64_t ldm, int64_t sM, int a0, int k0,
-                                                          int nb, double* __restrict__ Cbuf) {
-  const int b = blockIdx.y;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const double* src = M + (int64_t)b * sM + (int64_t)i * ldm + a0 + k0;
-  double* dst = Cbuf + ((int64_t)b * n + i) * NB;
-  double v[NB];
-#pragma unroll
-  for (int q = 0; q < NB; ++q) v[q] = src[min(q, nb - 1)];     // all loads in flight
-#pragma unroll
-  for (int q = 0; q < NB; ++q) dst[q] = (q < nb) ? v[q] : 0.0;
-}
-
-// rows outside block k: M_i -= C_i R ; block rows: M_k = R   (live columns only)
+// rows outside block k: M_i -= C_i R ; block rows: M_k = R   (live columns only).  C = block
+// k's own A columns (from column c0 = a0 + k0), read in place: they are not live, so no tile
+// of this launch writes them (a snapshot copy of them per step cost a pass of its own).
 template <int NB>
 __global__ __launch_bounds__(256) void lu_update_kernel(double* __restrict__ M, int n, int64_t ldm,
                                                         int64_t sM, int nlive, int a_first, int nA,
                                                         int b0, int k0, int nb,
-                                                        const double* __restrict__ Rbuf,
-                                                        const double* __restrict__ Cbuf) {
+                                                        const double* __restrict__ Rbuf, int c0) {
   constexpr int BT = 64;
   __shared__ double Cs[NB][BT + 16];
   __shared__ double Rs[NB][BT + 16];
   const int b = blockIdx.y;
   double* Mb = M + (int64_t)b * sM;
   const double* Rb = Rbuf + (int64_t)b * NB * nlive;
-  const double* Cb = Cbuf + (int64_t)b * n * NB;
+  const double* Cb = Mb + c0;
   const int tc = (nlive + BT - 1) / BT;
   const int I0 = (blockIdx.x / tc) * BT, V0 = (blockIdx.x % tc) * BT;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -462,14 +447,14 @@ __global__ __launch_bounds__(256) void lu_update_kernel(double* __restrict__ M, 
 #pragma unroll
   for (int u = 0; u < QS; ++u) {
     const int e = t + u * 256;
-    cv[u] = Cb[(int64_t)min(I0 + e / NB, n - 1) * NB + e % NB];
+    cv[u] = Cb[(int64_t)min(I0 + e / NB, n - 1) * ldm + min(e % NB, nb - 1)];
     rv[u] = Rb[(int64_t)min(e / BT, nb - 1) * nlive + min(V0 + e % BT, nlive - 1)];
   }
 #pragma unroll
   for (int u = 0; u < QS; ++u) {
     const int e = t + u * 256;
     const int i = e / NB, q = e % NB;
-    Cs[q][i] = (I0 + i < n) ? cv[u] : 0.0;
+    Cs[q][i] = (I0 + i < n && q < nb) ? cv[u] : 0.0;
     const int q2 = e / BT, j = e % BT;
     Rs[q2][j] = (V0 + j < nlive && q2 < nb) ? rv[u] : 0.0;
   }
@@ -525,8 +510,7 @@ hipError_t lu_solve_nb(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
                        int batch, double* work, int* status, hipStream_t st) {
   double* Pbuf = work;
   double* Rbuf = Pbuf + (int64_t)batch * NB * NB;
-  double* Cbuf = Rbuf + (int64_t)batch * NB * (n + m);
-  int* piv = reinterpret_cast<int*>(Cbuf + (int64_t)batch * n * NB);
+  int* piv = reinterpret_cast<int*>(Rbuf + (int64_t)batch * NB * (n + m));
   for (int k0 = 0; k0 < n; k0 += NB) {
     const int nb = (n - k0 < NB) ? (n - k0) : NB;
     hipError_t e = lu_pivot_launch<NB, PMAX>(M, n, ldm, sM, a0, k0, nb, piv, status, batch, st);
@@ -540,11 +524,9 @@ hipError_t lu_solve_nb(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
     if (nlive > 0) {
       hipLaunchKernelGGL((lu_rowpanel_kernel<NB>), dim3((nlive + 255) / 256, batch), dim3(256), 0,
                          st, M, ldm, sM, nlive, a0 + k0 + nb, nA, b0, k0, nb, Pbuf, Rbuf);
-      hipLaunchKernelGGL((lu_snapshot_kernel<NB>), dim3((n + 255) / 256, batch), dim3(256), 0, st,
-                         M, n, ldm, sM, a0, k0, nb, Cbuf);
       const int tiles = ((n + 63) / 64) * ((nlive + 63) / 64);
       hipLaunchKernelGGL((lu_update_kernel<NB>), dim3(tiles, batch), dim3(256), 0, st, M, n, ldm,
-                         sM, nlive, a0 + k0 + nb, nA, b0, k0, nb, Rbuf, Cbuf);
+                         sM, nlive, a0 + k0 + nb, nA, b0, k0, nb, Rbuf, a0 + k0);
     }
   }
   return hipGetLastError();
@@ -605,8 +587,7 @@ hipError_t lu_solve_2level(double* M, int n, int m, int64_t ldm, int64_t sM, int
                            int z0, int batch, double* work, int* status, hipStream_t st) {
   double* Pbuf = work;
   double* Rbuf = Pbuf + (int64_t)batch * NB * NB;
-  double* Cbuf = Rbuf + (int64_t)batch * NB * (2 * LU_KB);
-  double* RK = Cbuf + (int64_t)batch * n * NB;
+  double* RK = Rbuf + (int64_t)batch * NB * (2 * LU_KB);
   int* piv = reinterpret_cast<int*>(RK + (int64_t)batch * LU_KB * (n + m));
   for (int K0 = 0; K0 < n; K0 += LU_KB) {
     const int kb = (n - K0 < LU_KB) ? (n - K0) : LU_KB;
@@ -634,11 +615,9 @@ hipError_t lu_solve_2level(double* M, int n, int m, int64_t ldm, int64_t sM, int
       const int nlive = nA + zlive + nb;
       hipLaunchKernelGGL((lu_rowpanel_kernel<NB>), dim3((nlive + 255) / 256, batch), dim3(256), 0,
                          st, M, ldm, sM, nlive, a0 + k0 + nb, nA, z0, k0, nb, Pbuf, Rbuf);
-      hipLaunchKernelGGL((lu_snapshot_kernel<NB>), dim3((n + 255) / 256, batch), dim3(256), 0, st,
-                         M, n, ldm, sM, a0, k0, nb, Cbuf);
       const int tiles = ((n + 63) / 64) * ((nlive + 63) / 64);
       hipLaunchKernelGGL((lu_update_kernel<NB>), dim3(tiles, batch), dim3(256), 0, st, M, n, ldm,
-                         sM, nlive, a0 + k0 + nb, nA, z0, k0, nb, Rbuf, Cbuf);
+                         sM, nlive, a0 + k0 + nb, nA, z0, k0, nb, Rbuf, a0 + k0);
     }
     // the rest: swaps in sequence order, then R_K <- Z_K R_K, R_other += Z_other R_K
     const int nAr = n - aend;
@@ -683,8 +662,7 @@ extern "C" int pfml_lu_panel_cols() { return LU_KB; }
 
 extern "C" int64_t pfml_lu_solve_work_doubles(int n, int m, int batch) {
   const int64_t NB = 32;                     // the larger block: enough for every variant
-  return (int64_t)batch * (NB * NB + NB * (n + m + 2 * LU_KB) + (int64_t)n * NB +
-                           (int64_t)LU_KB * (n + m)) +
+  return (int64_t)batch * (NB * NB + NB * (n + m + 2 * LU_KB) + (int64_t)LU_KB * (n + m)) +
          (int64_t)batch * LU_KB;             // pivots (ints, 4 inner blocks of NB)
 }
 
