@@ -370,3 +370,31 @@ def test_exposureless_factor_keeps_finite_cov_in_compat():
     assert (Fm[0, 1, :] == 0).all() and (Fm[0, :, 1] == 0).all()
     assert np.isnan(Fm[0, 3, 0]) and np.isnan(Fm[1, 3, 0])
     assert np.isfinite(Fm[1, 1, [0, 2, 4]]).all()           # exposed in window 2
+
+
+def test_dgemm_auto_tile_rule():
+    """Host mirror of the DGEMM's auto tile choice (ops/gemm.py _auto_cfg, csrc/gemm_f64.hip
+    dgemm_chunk): 128 x 64 LDS-DMA tiles on the S4 shapes, 64 x 64 when a launch would have
+    fewer 128 x 64 tiles than CUs (the per-rank inverse products of a many-GPU run), 128 x 128
+    for large matrices, square 64 x 64 in the symmetric mode."""
+    from pfml.ops.gemm import _SMALL_TILES, _auto_cfg
+    assert _SMALL_TILES == 256
+    assert _auto_cfg(490, 2006, 490, batch=92) == 8           # Horner step, 92-month rank
+    assert _auto_cfg(245, 245, 245, batch=244) == 8           # inverse top level, one GPU
+    assert _auto_cfg(245, 245, 245, batch=31) == 7            # the same at 31 months / batch
+    assert _auto_cfg(490, 490, 490, sym=True, batch=1) == 7
+    assert _auto_cfg(2048, 2048, 512, batch=1) == 6
+
+
+def test_block_add_row_scale_cpu():
+    """la.block_add on strided [B, M, N] views: X + Y, and X + diag(s) Y (omega_chg = omega -
+    diag(D_0) omega_l1) exactly as torch's addcmul."""
+    from pfml.ops import linalg as la
+    g = torch.Generator().manual_seed(7)
+    big = torch.randn(2, 3, 9, 40, generator=g, dtype=torch.float64)
+    X, Y = big[0, :, :, :25], big[1, :, :, 5:30]
+    s = torch.randn(3, 9, generator=g, dtype=torch.float64)
+    out = torch.empty(3, 9, 25, dtype=torch.float64)
+    assert torch.equal(la.block_add(out, X, Y), X + Y)
+    assert torch.equal(la.block_add(out, X, Y, y_row_scale=-s),
+                       torch.addcmul(X, -s.unsqueeze(-1), Y))
