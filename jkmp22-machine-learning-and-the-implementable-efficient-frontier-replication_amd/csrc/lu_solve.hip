@@ -393,13 +393,15 @@ void lu_blockinv_launch(const double* M, int64_t ldm, int64_t sM, int a0, int k0
                        k0, nb, Pbuf);
 }
 
-// R = P M_k over live columns (excluding block k's own A columns) -> Rbuf [NB][nlive]
+// R = P M_k over live columns (excluding block k's own A columns) -> Rbuf [NB][nlive].  Live
+// columns v >= vz are virtual: the two-level form's Z columns of the current inner block, whose
+// rows k0.. hold the unit vectors e_(v - vz) (not stored: no zero-fill or unit pass of Z)
 template <int NB>
 __global__ __launch_bounds__(256) void lu_rowpanel_kernel(const double* __restrict__ M, int64_t ldm,
                                                           int64_t sM, int nlive, int a_first,
                                                           int nA, int b0, int k0, int nb,
                                                           const double* __restrict__ Pbuf,
-                                                          double* __restrict__ Rbuf) {
+                                                          double* __restrict__ Rbuf, int vz) {
   __shared__ double P[NB][NB + 1];
   const int b = blockIdx.y;
   const int t = threadIdx.x;
@@ -411,7 +413,9 @@ __global__ __launch_bounds__(256) void lu_rowpanel_kernel(const double* __restri
   const double* Mb = M + (int64_t)b * sM;
   double col[NB];
 #pragma unroll
-  for (int q = 0; q < NB; ++q) col[q] = (q < nb) ? Mb[(int64_t)(k0 + q) * ldm + c] : 0.0;
+  for (int q = 0; q < NB; ++q)
+    col[q] = (v >= vz) ? (q == v - vz ? 1.0 : 0.0)
+                       : ((q < nb) ? Mb[(int64_t)(k0 + q) * ldm + c] : 0.0);
   double* Rb = Rbuf + (int64_t)b * NB * nlive;
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
@@ -422,14 +426,16 @@ __global__ __launch_bounds__(256) void lu_rowpanel_kernel(const double* __restri
   }
 }
 
-// rows outside block k: M_i -= C_i R ; block rows: M_k = R   (live columns only).  C = block
+// rows outside block k: M_i -= C_i R ; block rows: M_k = R   (live columns only; virtual
+// columns v >= vz, see lu_rowpanel_kernel, read as 0).  C = block
 // k's own A columns (from column c0 = a0 + k0), read in place: they are not live, so no tile
 // of this launch writes them (a snapshot copy of them per step cost a pass of its own).
 template <int NB>
 __global__ __launch_bounds__(256) void lu_update_kernel(double* __restrict__ M, int n, int64_t ldm,
                                                         int64_t sM, int nlive, int a_first, int nA,
                                                         int b0, int k0, int nb,
-                                                        const double* __restrict__ Rbuf, int c0) {
+                                                        const double* __restrict__ Rbuf, int c0,
+                                                        int vz) {
   constexpr int BT = 64;
   __shared__ double Cs[NB][BT + 16];
   __shared__ double Rs[NB][BT + 16];
@@ -487,7 +493,8 @@ __global__ __launch_bounds__(256) void lu_update_kernel(double* __restrict__ M, 
       for (int r = 0; r < 4; ++r) {
         const int i = min(I0 + wm * 32 + x * 16 + PFML_F64_CROW(lane, r), n - 1);
         const int v = min(V0 + wn * 32 + y * 16 + (lane & 15), nlive - 1);
-        old[x][y][r] = Mb[(int64_t)i * ldm + live_col(v, nA, a_first, b0)];
+        // (virtual live columns v >= vz: zero outside the block rows, which take R)
+        old[x][y][r] = v >= vz ? 0.0 : Mb[(int64_t)i * ldm + live_col(v, nA, a_first, b0)];
         nrow[x][y][r] = Rb[(int64_t)min(max(i - k0, 0), nb - 1) * nlive + v];
       }
 #pragma unroll
@@ -523,10 +530,10 @@ hipError_t lu_solve_nb(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
     const int nlive = nA + m;
     if (nlive > 0) {
       hipLaunchKernelGGL((lu_rowpanel_kernel<NB>), dim3((nlive + 255) / 256, batch), dim3(256), 0,
-                         st, M, ldm, sM, nlive, a0 + k0 + nb, nA, b0, k0, nb, Pbuf, Rbuf);
+                         st, M, ldm, sM, nlive, a0 + k0 + nb, nA, b0, k0, nb, Pbuf, Rbuf, nlive);
       const int tiles = ((n + 63) / 64) * ((nlive + 63) / 64);
       hipLaunchKernelGGL((lu_update_kernel<NB>), dim3(tiles, batch), dim3(256), 0, st, M, n, ldm,
-                         sM, nlive, a0 + k0 + nb, nA, b0, k0, nb, Rbuf, a0 + k0);
+                         sM, nlive, a0 + k0 + nb, nA, b0, k0, nb, Rbuf, a0 + k0, nlive);
     }
   }
   return hipGetLastError();
@@ -536,28 +543,15 @@ hipError_t lu_solve_nb(double* M, int n, int m, int64_t ldm, int64_t sM, int a0,
 // Two-level form (n <= 3072): 128-wide outer panels.  The 32-wide (n > 512: 16-wide) inner steps above run on the
 // panel's own A columns plus a 128-column block Z of M (the inner update touches <= 256
 // columns instead of all n + m), and Z accumulates the panel's Gauss-Jordan transform:
-// the unit vector of each pivot row is placed in Z when its inner block is reached (after
-// that block's row swaps), so at the end Z = T E_K with T the panel's transform after all of
-// its swaps.  The rest of M (A columns right of the panel and the B columns) then takes the
+// the unit vector of each pivot row enters Z when its inner block is reached (after that
+// block's row swaps), so at the end Z = T E_K with T the panel's transform after all of its
+// swaps.  Z is never zero-filled or seeded: a block's Z columns are VIRTUAL in its own step
+// (the row panel reads them as the unit vectors, the update as zeros outside the block rows)
+// and that step's update writes every row of them.  The rest of M (A columns right of the panel and the B columns) then takes the
 // swaps and T in one go:  R <- Perm R,  R_K <- Z_K R_K,  R_other <- R_other + Z_other R_K,
 // i.e. three K = 128 fp64 MFMA GEMMs per column range (csrc/gemm_f64.hip) in place of four
 // bandwidth-bound rank-32 passes over every live column.
 constexpr int LU_KB = 128;
-
-__global__ __launch_bounds__(256) void lu_zinit_kernel(double* __restrict__ M, int n, int64_t ldm,
-                                                       int64_t sM, int z0) {
-  const int b = blockIdx.y;
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= (int64_t)n * LU_KB) return;
-  M[(int64_t)b * sM + (e / LU_KB) * ldm + z0 + e % LU_KB] = 0.0;
-}
-
-// unit entries of the current inner block's pivot rows: M[k0 + j][zc + j] = 1
-__global__ __launch_bounds__(64) void lu_zunit_kernel(double* __restrict__ M, int64_t ldm,
-                                                      int64_t sM, int k0, int zc, int nb) {
-  const int j = threadIdx.x;
-  if (j < nb) M[(int64_t)blockIdx.x * sM + (int64_t)(k0 + j) * ldm + zc + j] = 1.0;
-}
 
 // RK[b][r][v] = M[K0 + r][live column v]   (rest columns: A right of the panel, then B)
 __global__ __launch_bounds__(256) void lu_rk_kernel(const double* __restrict__ M, int64_t ldm,
@@ -592,8 +586,6 @@ hipError_t lu_solve_2level(double* M, int n, int m, int64_t ldm, int64_t sM, int
   for (int K0 = 0; K0 < n; K0 += LU_KB) {
     const int kb = (n - K0 < LU_KB) ? (n - K0) : LU_KB;
     const int aend = K0 + kb;
-    hipLaunchKernelGGL(lu_zinit_kernel, dim3((n * LU_KB + 255) / 256, batch), dim3(256), 0, st, M,
-                       n, ldm, sM, z0);
     for (int k0 = K0; k0 < aend; k0 += NB) {
       const int nb = (aend - k0 < NB) ? (aend - k0) : NB;
       int* pv = piv + (int64_t)((k0 - K0) / NB) * batch * NB;
@@ -608,16 +600,15 @@ hipError_t lu_solve_2level(double* M, int n, int m, int64_t ldm, int64_t sM, int
       const int nswap = (aend - k0) + zlive;
       hipLaunchKernelGGL((lu_swap_kernel<NB>), dim3((nswap + 255) / 256, batch), dim3(256), 0, st,
                          M, ldm, sM, nswap, a0 + k0, aend - k0, z0, k0, nb, pv);
-      hipLaunchKernelGGL(lu_zunit_kernel, dim3(batch), dim3(64), 0, st, M, ldm, sM, k0,
-                         z0 + (k0 - K0), nb);
       lu_blockinv_launch<NB>(M, ldm, sM, a0, k0, nb, Pbuf, batch, st);
       const int nA = aend - (k0 + nb);
       const int nlive = nA + zlive + nb;
       hipLaunchKernelGGL((lu_rowpanel_kernel<NB>), dim3((nlive + 255) / 256, batch), dim3(256), 0,
-                         st, M, ldm, sM, nlive, a0 + k0 + nb, nA, z0, k0, nb, Pbuf, Rbuf);
+                         st, M, ldm, sM, nlive, a0 + k0 + nb, nA, z0, k0, nb, Pbuf, Rbuf,
+                         nA + zlive);
       const int tiles = ((n + 63) / 64) * ((nlive + 63) / 64);
       hipLaunchKernelGGL((lu_update_kernel<NB>), dim3(tiles, batch), dim3(256), 0, st, M, n, ldm,
-                         sM, nlive, a0 + k0 + nb, nA, z0, k0, nb, Rbuf, a0 + k0);
+                         sM, nlive, a0 + k0 + nb, nA, z0, k0, nb, Rbuf, a0 + k0, nA + zlive);
     }
     // the rest: swaps in sequence order, then R_K <- Z_K R_K, R_other += Z_other R_K
     const int nAr = n - aend;
