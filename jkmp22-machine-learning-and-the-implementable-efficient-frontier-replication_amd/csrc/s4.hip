@@ -153,28 +153,41 @@ __global__ __launch_bounds__(256) void mfunc_flat_kernel(MfArgs p) {
     aj[k] = av ? reinterpret_cast<const double2_t*>(av)[q] : double2_t{0.0, 0.0};
     mj[k] = mv ? reinterpret_cast<const double2_t*>(mv)[q] : double2_t{0.0, 0.0};
   }
-  for (int i = blockIdx.x * FLAT_ROWS + w; i < r1; i += 4) {
-    const double ai = av ? av[i] : 0.0, mi = mv ? mv[i] : 0.0;
-    const double2_t* xr = reinterpret_cast<const double2_t*>(X + (int64_t)i * p.ld);
-    const double2_t* yr = Y ? reinterpret_cast<const double2_t*>(Y + (int64_t)i * p.ld) : nullptr;
-    double2_t* orow = reinterpret_cast<double2_t*>(O + (int64_t)i * p.ld);
-    // every load of the row first (clamped addresses), then the values and the stores
-    double2_t xv[FLAT_QM], yv[FLAT_QM];
+  // two rows per wave per iteration, every load of both issued before the first store (the
+  // output may alias an input - in-place passes - so the compiler keeps each row's loads behind
+  // the previous row's stores; a row of one wave, ~8 KB, was all it had in flight)
+  for (int i0 = blockIdx.x * FLAT_ROWS + w; i0 < r1; i0 += 8) {
+    double2_t xv[2][FLAT_QM], yv[2][FLAT_QM];
 #pragma unroll
-    for (int k = 0; k < FLAT_QM; ++k) {
-      const int q = min(lane + 64 * k, np - 1);
-      xv[k] = xr[q];
-      yv[k] = yr ? yr[q] : double2_t{0.0, 0.0};
+    for (int h = 0; h < 2; ++h) {
+      const int i = min(i0 + 4 * h, r1 - 1);
+      const double2_t* xr = reinterpret_cast<const double2_t*>(X + (int64_t)i * p.ld);
+      const double2_t* yr =
+          Y ? reinterpret_cast<const double2_t*>(Y + (int64_t)i * p.ld) : nullptr;
+#pragma unroll
+      for (int k = 0; k < FLAT_QM; ++k) {
+        const int q = min(lane + 64 * k, np - 1);
+        xv[h][k] = xr[q];
+        yv[h][k] = yr ? yr[q] : double2_t{0.0, 0.0};
+      }
     }
 #pragma unroll
-    for (int k = 0; k < FLAT_QM; ++k) {
-      const int q = lane + 64 * k;
-      if (q < np) {
-        const int j = 2 * q;
-        const double v0 = mf_value(p, i, j, xv[k].x, yv[k].x, s, c, ai, aj[k].x, mi, mj[k].x);
-        const double v1 = mf_value(p, i, j + 1, xv[k].y, yv[k].y, s, c, ai, aj[k].y, mi,
-                                   mj[k].y);
-        orow[q] = double2_t{v0, v1};
+    for (int h = 0; h < 2; ++h) {
+      const int i = i0 + 4 * h;
+      if (i >= r1) break;
+      const double ai = av ? av[i] : 0.0, mi = mv ? mv[i] : 0.0;
+      double2_t* orow = reinterpret_cast<double2_t*>(O + (int64_t)i * p.ld);
+#pragma unroll
+      for (int k = 0; k < FLAT_QM; ++k) {
+        const int q = lane + 64 * k;
+        if (q < np) {
+          const int j = 2 * q;
+          const double v0 = mf_value(p, i, j, xv[h][k].x, yv[h][k].x, s, c, ai, aj[k].x, mi,
+                                     mj[k].x);
+          const double v1 = mf_value(p, i, j + 1, xv[h][k].y, yv[h][k].y, s, c, ai, aj[k].y, mi,
+                                     mj[k].y);
+          orow[q] = double2_t{v0, v1};
+        }
       }
     }
   }
