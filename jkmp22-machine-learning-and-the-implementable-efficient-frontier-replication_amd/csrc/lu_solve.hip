@@ -427,9 +427,9 @@ __global__ __launch_bounds__(256) void lu_rowpanel_kernel(const double* __restri
 }
 
 // rows outside block k: M_i -= C_i R ; block rows: M_k = R   (live columns only; virtual
-// columns v >= vz, see lu_rowpanel_kernel, read as 0).  C = block
-// k's own A columns (from column c0 = a0 + k0), read in place: they are not live, so no tile
-// of this launch writes them (a snapshot copy of them per step cost a pass of its own).
+// columns v >= vz, see lu_rowpanel_kernel, read as 0).  C = block k's own A columns (from
+// column c0 = a0 + k0), read in place: they are not live, so no tile of this launch writes
+// them (a snapshot copy of them per step cost a pass of its own).
 template <int NB>
 __global__ __launch_bounds__(256) void lu_update_kernel(double* __restrict__ M, int n, int64_t ldm,
                                                         int64_t sM, int nlive, int a_first, int nA,
