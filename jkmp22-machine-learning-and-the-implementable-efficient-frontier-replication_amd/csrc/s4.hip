@@ -257,6 +257,35 @@ __global__ __launch_bounds__(64) void db_mu_final_kernel(const double* __restric
   mu[b] = unscaled ? 1.0 : sqrt(sqrt(sqrt(tb) / fmax(sqrt(ta), 1e-300)));
 }
 
+// The same mu (one thread, the same fixed-order sums) plus the Denman-Beavers product's row
+// scales as [B, N] rows: rs = 0.5 / mu (torch's 0.5 / mu is reciprocal(mu) * 0.5, bitwise
+// the same since the halving is exact) and es = 0.5 mu - in place of a reciprocal, two
+// multiplies and two broadcast copies per iteration (ops/linalg.py _db_sqrt).
+__global__ __launch_bounds__(256) void db_mu_rows_kernel(const double* __restrict__ part, int ns,
+                                                         int unscaled, double* __restrict__ mu,
+                                                         int N, double* __restrict__ rs,
+                                                         double* __restrict__ es) {
+  __shared__ double smu;
+  const int b = blockIdx.x;
+  if (threadIdx.x == 0) {
+    double ta = 0.0, tb = 0.0;
+    for (int q = 0; q < ns; ++q) {
+      ta += part[((int64_t)b * ns + q) * 2];
+      tb += part[((int64_t)b * ns + q) * 2 + 1];
+    }
+    const double m = unscaled ? 1.0 : sqrt(sqrt(sqrt(tb) / fmax(sqrt(ta), 1e-300)));
+    mu[b] = m;
+    smu = m;
+  }
+  __syncthreads();
+  const double m = smu;
+  const double r = (1.0 / m) * 0.5, e = 0.5 * m;
+  for (int i = threadIdx.x; i < N; i += 256) {
+    rs[(int64_t)b * N + i] = r;
+    es[(int64_t)b * N + i] = e;
+  }
+}
+
 }  // namespace
 
 struct PfmlMfArgs {
@@ -320,6 +349,27 @@ extern "C" hipError_t pfml_db_mu(const double* M, const double* Minv, int B, int
     hipLaunchKernelGGL(db_norm_partial_kernel<1>, dim3(ns, B), dim3(256), 0, st, M, Minv, N, ld,
                        sX, work);
   hipLaunchKernelGGL(db_mu_final_kernel, dim3((B + 63) / 64), dim3(64), 0, st, work, B, ns, 0, mu);
+  return hipGetLastError();
+}
+
+// pfml_db_mu plus the row scales rs / es ([B, N], contiguous) of the Y update (db_mu_rows_kernel)
+extern "C" hipError_t pfml_db_mu_rows(const double* M, const double* Minv, int B, int N, int64_t ld,
+                                      int64_t sX, int unscaled, double* mu, double* work,
+                                      double* rs, double* es, hipStream_t st) {
+  if (B <= 0 || N <= 0) return hipSuccess;
+  const int ns = mu_split(N);
+  if (!unscaled) {
+    const bool vec = N % 2 == 0 && ld % 2 == 0 && sX % 2 == 0 &&
+                     ((uintptr_t)M & 15) == 0 && ((uintptr_t)Minv & 15) == 0;
+    if (vec)
+      hipLaunchKernelGGL(db_norm_partial_kernel<2>, dim3(ns, B), dim3(256), 0, st, M, Minv, N,
+                         ld, sX, work);
+    else
+      hipLaunchKernelGGL(db_norm_partial_kernel<1>, dim3(ns, B), dim3(256), 0, st, M, Minv, N,
+                         ld, sX, work);
+  }
+  hipLaunchKernelGGL(db_mu_rows_kernel, dim3(B), dim3(256), 0, st, work, ns, unscaled, mu, N, rs,
+                     es);
   return hipGetLastError();
 }
 

@@ -417,6 +417,9 @@ class _MfArgs(C.Structure):
 
 nat.register_hip("pfml_mfunc_sym", [C.POINTER(_MfArgs), C.c_void_p])
 nat.register_hip("pfml_mf_args_size", [])
+nat.register_hip("pfml_db_mu_rows", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int64,
+                                     C.c_int64, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p])
 nat.register_hip("pfml_db_mu", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_int64,
                                 C.c_int, C.c_void_p, C.c_void_p, C.c_void_p])
 nat.register_hip("pfml_db_mu_work_doubles2", [C.c_int, C.c_int], C.c_int64)
@@ -529,6 +532,27 @@ def block_add(out: torch.Tensor, X: torch.Tensor, Y: torch.Tensor,
     return torch.add(X, Y, out=out)
 
 
+def _db_mu_rows(M: torch.Tensor, Minv: torch.Tensor, unscaled: bool, mu: torch.Tensor,
+                rs: torch.Tensor, es: torch.Tensor) -> None:
+    """``_db_mu`` plus the Y update's row scales rs = 0.5 / mu, es = 0.5 mu as [B, N] rows (one
+    device kernel with the mu reduction: csrc/s4.hip db_mu_rows_kernel)."""
+    B, N, _ = M.shape
+    if nat.is_device(M):
+        lib = nat.hip_lib()
+        if not unscaled:
+            _work.add("db_norm_partial_kernel", 4.0 * B * N * N, 16.0 * B * N * N)
+        wbuf = torch.empty(lib.pfml_db_mu_work_doubles2(B, N), dtype=torch.float64,
+                           device=M.device)
+        nat.check(lib.pfml_db_mu_rows(M.data_ptr(), Minv.data_ptr(), B, N, N, N * N,
+                                      int(unscaled), mu.data_ptr(), wbuf.data_ptr(),
+                                      rs.data_ptr(), es.data_ptr(), nat.stream_of(M)),
+                  "pfml_db_mu_rows")
+        return
+    _db_mu(M, Minv, unscaled, mu)
+    rs.copy_((0.5 / mu).view(B, 1).expand(B, N))
+    es.copy_((0.5 * mu).view(B, 1).expand(B, N))
+
+
 def _db_mu(M: torch.Tensor, Minv: torch.Tensor, unscaled: bool, out: torch.Tensor) -> None:
     B, N, _ = M.shape
     if nat.is_device(M):
@@ -569,6 +593,8 @@ def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tenso
     B, N, _ = S.shape
     M, Y, Mi, Yn = ws
     mu = torch.empty(B, dtype=S.dtype, device=S.device)
+    rs = torch.empty((B, N), dtype=S.dtype, device=S.device)     # Y update row scales
+    es = torch.empty((B, N), dtype=S.dtype, device=S.device)
     if ns_tail is None:
         ns_tail = DB_NS_TAIL
     ns_tail = ns_tail and iters > scaled_iters
@@ -592,8 +618,8 @@ def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tenso
         if ns_tail and it == iters - 1:
             # Newton-Schulz tail: Y' = 1.5 Y - 0.5 Y M (Y M symmetric, as Y M^-1 is)
             _db_check(M, DB_TAIL_TOL, status)
-            rs = torch.full((B, N), -0.5, dtype=S.dtype, device=S.device)
-            es = torch.full((B, N), 1.5, dtype=S.dtype, device=S.device)
+            rs.fill_(-0.5)
+            es.fill_(1.5)
             gemm_fused(Y, M, Yn, row_scale=rs, addend=Y, addend_row_scale=es, sym=sym_prod)
             Y, Yn = Yn, Y
             break
@@ -601,10 +627,8 @@ def _db_sqrt(S: torch.Tensor, iters: int, scaled_iters: int, status: torch.Tenso
             spd_inverse_sym(Mi, status, src=M)
         else:
             spd_inverse_into(M, Mi, status)
-        _db_mu(M, Mi, it >= scaled_iters, mu)
         # Y' = (mu/2) Y + (1/(2 mu)) Y M^-1 ;  M' = I/2 + (mu^2 M + mu^-2 M^-1)/4
-        rs = (0.5 / mu).view(B, 1).expand(B, N).contiguous()
-        es = (0.5 * mu).view(B, 1).expand(B, N).contiguous()
+        _db_mu_rows(M, Mi, it >= scaled_iters, mu, rs, es)
         gemm_fused(Y, Mi, Yn, row_scale=rs, addend=Y, addend_row_scale=es, sym=sym_prod)
         Y, Yn = Yn, Y
         if it == 0 and spare is not None:

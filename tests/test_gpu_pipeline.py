@@ -124,6 +124,36 @@ def test_db_newton_schulz_tail(gpu):
     assert st_short.tolist() == [1] * B
 
 
+def test_db_mu_rows_bitwise(gpu, monkeypatch):
+    """The Denman-Beavers scaling mu and the Y update's row scales from ONE device kernel
+    (csrc/s4.hip db_mu_rows_kernel) give bitwise the square root of the torch form (mu kernel,
+    then 0.5 / mu and 0.5 mu broadcast by torch), and the starting copies of S are not needed
+    (S is only read)."""
+    from pfml.ops import linalg as la
+    B, N = 3, 160
+    X = _rand(B, N + 40, N, seed=23)
+    S = X.transpose(1, 2) @ X / N
+    S = (S @ S + 1e-3 * torch.eye(N, dtype=torch.float64)).to(gpu)
+    S = 0.5 * (S + S.transpose(1, 2))
+    S0 = S.clone()
+
+    def run():
+        st = torch.zeros(B, dtype=torch.int32, device=gpu)
+        ws = [torch.empty_like(S) for _ in range(4)]
+        return la._db_sqrt(S, la.DB_ITERS, la.DB_SCALED_ITERS, st, ws, exact_sym=True).clone()
+
+    fused = run()
+    assert torch.equal(S, S0)
+
+    def torch_rows(M, Mi, unscaled, mu, rs, es):
+        la._db_mu(M, Mi, unscaled, mu)
+        rs.copy_((0.5 / mu).view(B, 1).expand(B, N))
+        es.copy_((0.5 * mu).view(B, 1).expand(B, N))
+
+    monkeypatch.setattr(la, "_db_mu_rows", torch_rows)
+    assert torch.equal(run(), fused)
+
+
 @pytest.mark.parametrize("tc", [True, False])
 def test_m_tilde_production_shape(gpu, tc):
     """m at N = 496 (padded S&P 500 width) on the device vs the reference-form torch m_func
